@@ -1,0 +1,87 @@
+// rt_internal.h — shared declarations of the gfx950 path-trace backend.
+//
+// Device layout of a scene (built once per rt_upload_scene from the
+// reference's 48-B node / 48-B vertex / 16-B material records):
+//
+//   nodes : 2 x float4 per node (32 B), in the reference's preorder
+//           [0] = (bbox_min.xyz, skip)   skip = first node after this subtree
+//           [1] = (bbox_max.xyz, leaf)   leaf = flattened triangle index, or -1
+//           The left child of an internal node i is i+1 (BVHFlattener.java:51-75:
+//           myIndex = currentNodeIndex++ and the left subtree is flattened
+//           first), so the reference's stack DFS (compute_dynamic_ray.comp:185-210:
+//           push right, push left) visits nodes in preorder, skipping the
+//           subtree of every node whose box test fails.  "next = hit ? i+1 :
+//           skip" replays exactly that visit sequence with no stack at all.
+//   tris  : 3 x float4 per flattened triangle (48 B)
+//           [0] = (v0.xyz, n.x) [1] = (e1.xyz, n.y) [2] = (e2.xyz, n.z)
+//           e1 = v1-v0, e2 = v2-v0 and n = normalize(cross(e1,e2)) are the
+//           values hit_triangle computes (compute_dynamic_ray.comp:106-107,124)
+//           evaluated once on the host in IEEE binary32: the same bits.
+//   mats  : 1 x float4 per flattened triangle (albedo.rgb, type)
+#pragma once
+#include <cstdint>
+#include <cstddef>
+#include <hip/hip_runtime.h>
+
+#include "../../include/rtamd.h"
+
+namespace rtamd {
+
+struct DevScene {
+    int      n_nodes = 0;     // nodes in the compact array
+    int      end     = 0;     // traversal ends when the node index reaches this (= skip of root)
+    int      n_tris  = 0;
+    float4*  nodes   = nullptr;
+    float4*  tris    = nullptr;
+    float4*  mats    = nullptr;
+};
+
+struct Counters {               // device-side work counters (see rt_stats)
+    unsigned long long segments;
+    unsigned long long node_visits;
+    unsigned long long tri_tests;
+    unsigned long long mat_reads;
+};
+
+struct CamF {                   // the four vec3 of the CameraUBO
+    float ox, oy, oz;
+    float lx, ly, lz;
+    float hx, hy, hz;
+    float vx, vy, vz;
+};
+
+struct TraceArgs {
+    DevScene scene;
+    CamF     cam;
+    int      width, height;     // full frame
+    int      max_bounces;
+    int      x0, y0, tw, th;    // columns [x0, x0+tw); th local rows
+    // Local row ly is frame row y0 + ((ly / band_h) * band_stride + band_off) * band_h + ly % band_h:
+    // a plain tile is band_h = th, band_stride = 1, band_off = 0; rank r of N
+    // interleaved 16-row bands is band_h = 16, band_stride = N, band_off = r.
+    int      band_h, band_stride, band_off;
+    uchar4*  out_rgba;          // tw*th, nullable
+    float*   out_rad;           // tw*th*3, nullable
+    Counters* counters;         // nullable
+};
+
+// Host-side compact-scene build from the reference records; validates the
+// buffers.  Returns RT_OK or RT_ERR_BAD_SCENE with a message in *err.
+struct HostScene {
+    int n_nodes = 0, end = 0, n_tris = 0, max_depth = 0;
+    float4* nodes = nullptr;    // 2*n_nodes
+    float4* tris  = nullptr;    // 3*n_tris
+    float4* mats  = nullptr;    // n_tris
+};
+int build_host_scene(const void* vertices, size_t vertex_bytes,
+                     const void* materials, size_t material_bytes,
+                     const void* bvh_nodes, size_t bvh_bytes,
+                     HostScene* out, const char** err);
+void free_host_scene(HostScene* s);
+
+// Kernel launcher (rt_trace.hip).
+hipError_t launch_trace(const TraceArgs& a, hipStream_t stream);
+
+void set_error(const char* fmt, ...);
+
+}  // namespace rtamd

@@ -1,0 +1,542 @@
+// rt_runtime.hip — the C ABI of include/rtamd.h: context, scene upload and
+// frame render.  Replaces the render-side role of VulkanEngine
+// (VulkanEngine.java:318-431); the Vulkan plumbing (instance, descriptor sets,
+// barriers, staging image) has no counterpart: device buffers + one HIP
+// stream per device.
+#include "rt_internal.h"
+
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstdlib>
+#include <algorithm>
+#include <cstring>
+#include <new>
+#include <string>
+#include <vector>
+
+namespace rtamd {
+
+static thread_local char g_err[1024] = "";
+
+void set_error(const char* fmt, ...) {
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(g_err, sizeof g_err, fmt, ap);
+    va_end(ap);
+}
+
+#define RT_HIP_CHECK(expr)                                                        \
+    do {                                                                          \
+        hipError_t e_ = (expr);                                                   \
+        if (e_ != hipSuccess) {                                                   \
+            set_error("%s failed: %s (%s:%d)", #expr, hipGetErrorString(e_),      \
+                      __FILE__, __LINE__);                                        \
+            return RT_ERR_HIP;                                                    \
+        }                                                                         \
+    } while (0)
+
+// ------------------------------------------------------------ scene build --
+
+static inline float f32_at(const unsigned char* p, size_t off) {
+    float f;
+    std::memcpy(&f, p + off, 4);
+    return f;
+}
+static inline int32_t i32_at(const unsigned char* p, size_t off) {
+    int32_t v;
+    std::memcpy(&v, p + off, 4);
+    return v;
+}
+
+void free_host_scene(HostScene* s) {
+    std::free(s->nodes);
+    std::free(s->tris);
+    std::free(s->mats);
+    *s = HostScene{};
+}
+
+int build_host_scene(const void* vertices, size_t vertex_bytes,
+                     const void* materials, size_t material_bytes,
+                     const void* bvh_nodes, size_t bvh_bytes,
+                     HostScene* out, const char** err) {
+    static thread_local std::string msg;
+    *out = HostScene{};
+    const size_t n_nodes = bvh_bytes < RT_NODE_RECORD_BYTES ? 0 : bvh_bytes / RT_NODE_RECORD_BYTES;
+    const size_t n_tris  = vertex_bytes < RT_VERTEX_RECORD_BYTES ? 0 : vertex_bytes / RT_VERTEX_RECORD_BYTES;
+    const size_t n_mats  = material_bytes < RT_MATERIAL_RECORD_BYTES ? 0 : material_bytes / RT_MATERIAL_RECORD_BYTES;
+    auto fail = [&](const std::string& m) {
+        msg = m;
+        *err = msg.c_str();
+        free_host_scene(out);
+        return RT_ERR_BAD_SCENE;
+    };
+    if (n_nodes && bvh_bytes % RT_NODE_RECORD_BYTES)
+        return fail("bvh_bytes is not a multiple of 48");
+    if (n_tris && vertex_bytes % RT_VERTEX_RECORD_BYTES)
+        return fail("vertex_bytes is not a multiple of 48");
+    if (n_mats && material_bytes % RT_MATERIAL_RECORD_BYTES)
+        return fail("material_bytes is not a multiple of 16");
+    if (n_nodes > (size_t)INT32_MAX / 2 || n_tris > (size_t)INT32_MAX / 3)
+        return fail("scene too large for 32-bit node/triangle indices");
+    if (n_nodes && (!bvh_nodes)) return fail("null bvh buffer");
+    if (n_tris && (!vertices)) return fail("null vertex buffer");
+    if (n_mats && (!materials)) return fail("null material buffer");
+
+    out->n_nodes = (int)n_nodes;
+    out->n_tris  = (int)n_tris;
+    if (n_nodes == 0) {
+        out->end = 0;   // empty scene: every ray misses (reference: undefined read of node 0)
+        return RT_OK;
+    }
+    const unsigned char* nb = static_cast<const unsigned char*>(bvh_nodes);
+    std::vector<int32_t> skip(n_nodes), depth(n_nodes, 0);
+    out->nodes = static_cast<float4*>(std::malloc(sizeof(float4) * 2 * n_nodes));
+    if (!out->nodes) return fail("out of host memory");
+
+    // Pass 1 (reverse): leaf skip = i+1, internal skip = skip(right).  The
+    // layout must be the reference flattener's preorder: left == i+1 and the
+    // left subtree ends exactly where the right child starts.
+    for (size_t k = n_nodes; k-- > 0;) {
+        const unsigned char* r = nb + k * RT_NODE_RECORD_BYTES;
+        const int32_t data = i32_at(r, 32), count = i32_at(r, 36);
+        if (count < 0) {                                   // leaf (compute_dynamic_ray.comp:194-195)
+            const int64_t tri = -((int64_t)data + 1);
+            if (tri < 0 || (size_t)tri >= n_tris || (size_t)tri >= n_mats)
+                return fail("leaf node " + std::to_string(k) + " references triangle " +
+                            std::to_string(tri) + " outside the vertex/material buffers");
+            skip[k] = (int32_t)(k + 1);
+        } else {
+            if ((size_t)data != k + 1 || count <= data || (size_t)count >= n_nodes)
+                return fail("node " + std::to_string(k) +
+                            " is not in the reference's preorder layout (left must be i+1, right > left)");
+            if (skip[data] != count)
+                return fail("node " + std::to_string(k) + ": left subtree does not end at the right child");
+            skip[k] = skip[count];
+        }
+    }
+    out->end = skip[0];
+    int max_depth = 0;
+    for (size_t k = 0; k < (size_t)out->end; ++k) {
+        const unsigned char* r = nb + k * RT_NODE_RECORD_BYTES;
+        const int32_t data = i32_at(r, 32), count = i32_at(r, 36);
+        if (count >= 0) {
+            depth[data] = depth[k] + 1;
+            depth[count] = depth[k] + 1;
+        }
+        if (depth[k] > max_depth) max_depth = depth[k];
+        float4 A, B;
+        A.x = f32_at(r, 0);  A.y = f32_at(r, 4);  A.z = f32_at(r, 8);
+        B.x = f32_at(r, 16); B.y = f32_at(r, 20); B.z = f32_at(r, 24);
+        int32_t sk = skip[k], leaf = count < 0 ? -(data + 1) : -1;
+        std::memcpy(&A.w, &sk, 4);
+        std::memcpy(&B.w, &leaf, 4);
+        out->nodes[2 * k] = A;
+        out->nodes[2 * k + 1] = B;
+    }
+    out->max_depth = max_depth;
+
+    out->tris = static_cast<float4*>(std::malloc(sizeof(float4) * 3 * (n_tris ? n_tris : 1)));
+    out->mats = static_cast<float4*>(std::malloc(sizeof(float4) * (n_tris ? n_tris : 1)));
+    if (!out->tris || !out->mats) return fail("out of host memory");
+    const unsigned char* vb = static_cast<const unsigned char*>(vertices);
+    const unsigned char* mb = static_cast<const unsigned char*>(materials);
+    for (size_t t = 0; t < n_tris; ++t) {
+        const unsigned char* r = vb + t * RT_VERTEX_RECORD_BYTES;
+        const float v0x = f32_at(r, 0),  v0y = f32_at(r, 4),  v0z = f32_at(r, 8);
+        const float v1x = f32_at(r, 16), v1y = f32_at(r, 20), v1z = f32_at(r, 24);
+        const float v2x = f32_at(r, 32), v2y = f32_at(r, 36), v2z = f32_at(r, 40);
+        // edge1/edge2 and normalize(cross(edge1, edge2)) exactly as
+        // hit_triangle computes them (compute_dynamic_ray.comp:106-107,124).
+        const float e1x = v1x - v0x, e1y = v1y - v0y, e1z = v1z - v0z;
+        const float e2x = v2x - v0x, e2y = v2y - v0y, e2z = v2z - v0z;
+        const float cx = e1y * e2z - e1z * e2y;
+        const float cy = e1z * e2x - e1x * e2z;
+        const float cz = e1x * e2y - e1y * e2x;
+        const float l = std::sqrt((cx * cx + cy * cy) + cz * cz);
+        const float nx = cx / l, ny = cy / l, nz = cz / l;
+        out->tris[3 * t + 0] = make_float4(v0x, v0y, v0z, nx);
+        out->tris[3 * t + 1] = make_float4(e1x, e1y, e1z, ny);
+        out->tris[3 * t + 2] = make_float4(e2x, e2y, e2z, nz);
+        if (t < n_mats) {
+            const unsigned char* m = mb + t * RT_MATERIAL_RECORD_BYTES;
+            out->mats[t] = make_float4(f32_at(m, 0), f32_at(m, 4), f32_at(m, 8), f32_at(m, 12));
+        } else {
+            out->mats[t] = make_float4(0.f, 0.f, 0.f, -1.f);   // never referenced (validated above)
+        }
+    }
+    return RT_OK;
+}
+
+}  // namespace rtamd
+
+// ------------------------------------------------------------------ context --
+
+using namespace rtamd;
+
+struct PerDevice {
+    int          device = 0;
+    hipStream_t  stream = nullptr;
+    hipEvent_t   ev0 = nullptr, ev1 = nullptr;
+    DevScene     scene;
+    Counters*    d_counters = nullptr;
+    uchar4*      d_rgba = nullptr;
+    float*       d_rad = nullptr;
+    size_t       out_cap = 0;      // pixels
+};
+
+struct rt_ctx {
+    std::vector<PerDevice> dev;
+    bool has_scene = false;
+    int  n_nodes = 0, n_tris = 0, max_depth = 0;
+};
+
+static void free_scene(PerDevice& p) {
+    if (p.scene.nodes) (void)hipFree(p.scene.nodes);
+    if (p.scene.tris) (void)hipFree(p.scene.tris);
+    if (p.scene.mats) (void)hipFree(p.scene.mats);
+    p.scene = DevScene{};
+}
+
+static CamF cam_from_ubo(const rt_camera_ubo* c) {
+    CamF f;
+    f.ox = c->origin[0];     f.oy = c->origin[1];     f.oz = c->origin[2];
+    f.lx = c->lower_left[0]; f.ly = c->lower_left[1]; f.lz = c->lower_left[2];
+    f.hx = c->horizontal[0]; f.hy = c->horizontal[1]; f.hz = c->horizontal[2];
+    f.vx = c->vertical[0];   f.vy = c->vertical[1];   f.vz = c->vertical[2];
+    return f;
+}
+
+extern "C" {
+
+const char* rt_last_error(void) { return g_err; }
+
+int rt_create(const int* device_ids, int n_devices, rt_ctx** out) {
+    if (!out || n_devices < 1 || !device_ids) {
+        set_error("rt_create: need out != NULL and n_devices >= 1 (there is no CPU backend)");
+        return RT_ERR_INVALID_ARG;
+    }
+    *out = nullptr;
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || count == 0) {
+        set_error("rt_create: no HIP device visible");
+        return RT_ERR_NO_DEVICE;
+    }
+    rt_ctx* ctx = new (std::nothrow) rt_ctx;
+    if (!ctx) { set_error("rt_create: out of memory"); return RT_ERR_OOM; }
+    for (int k = 0; k < n_devices; ++k) {
+        const int d = device_ids[k];
+        if (d < 0 || d >= count) {
+            set_error("rt_create: device id %d out of range (0..%d)", d, count - 1);
+            rt_destroy(ctx);
+            return RT_ERR_NO_DEVICE;
+        }
+        hipDeviceProp_t prop;
+        if (hipGetDeviceProperties(&prop, d) != hipSuccess || std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) {
+            set_error("rt_create: device %d is not gfx950 (%s)", d, prop.gcnArchName);
+            rt_destroy(ctx);
+            return RT_ERR_NO_DEVICE;
+        }
+        PerDevice p;
+        p.device = d;
+        hipError_t e = hipSetDevice(d);
+        if (e == hipSuccess) e = hipStreamCreateWithFlags(&p.stream, hipStreamNonBlocking);
+        if (e == hipSuccess) e = hipEventCreate(&p.ev0);
+        if (e == hipSuccess) e = hipEventCreate(&p.ev1);
+        if (e == hipSuccess) e = hipMalloc(&p.d_counters, sizeof(Counters));
+        ctx->dev.push_back(p);
+        if (e != hipSuccess) {
+            set_error("rt_create: HIP setup on device %d failed: %s", d, hipGetErrorString(e));
+            rt_destroy(ctx);
+            return RT_ERR_HIP;
+        }
+    }
+    *out = ctx;
+    return RT_OK;
+}
+
+int rt_destroy(rt_ctx* ctx) {
+    if (!ctx) return RT_OK;
+    for (PerDevice& p : ctx->dev) {
+        (void)hipSetDevice(p.device);
+        if (p.stream) (void)hipStreamSynchronize(p.stream);
+        free_scene(p);
+        if (p.d_counters) (void)hipFree(p.d_counters);
+        if (p.d_rgba) (void)hipFree(p.d_rgba);
+        if (p.d_rad) (void)hipFree(p.d_rad);
+        if (p.ev0) (void)hipEventDestroy(p.ev0);
+        if (p.ev1) (void)hipEventDestroy(p.ev1);
+        if (p.stream) (void)hipStreamDestroy(p.stream);
+    }
+    delete ctx;
+    return RT_OK;
+}
+
+int rt_upload_scene(rt_ctx* ctx, const void* vertices, size_t vertex_bytes,
+                    const void* materials, size_t material_bytes,
+                    const void* bvh_nodes, size_t bvh_bytes) {
+    if (!ctx) { set_error("rt_upload_scene: null context"); return RT_ERR_INVALID_ARG; }
+    HostScene hs;
+    const char* err = nullptr;
+    int rc = build_host_scene(vertices, vertex_bytes, materials, material_bytes,
+                              bvh_nodes, bvh_bytes, &hs, &err);
+    if (rc != RT_OK) { set_error("rt_upload_scene: %s", err); return rc; }
+    ctx->has_scene = false;
+    for (PerDevice& p : ctx->dev) {
+        RT_HIP_CHECK(hipSetDevice(p.device));
+        RT_HIP_CHECK(hipStreamSynchronize(p.stream));   // like vkDeviceWaitIdle, VulkanEngine.java:321
+        free_scene(p);
+        DevScene s;
+        s.n_nodes = hs.n_nodes;
+        s.end = hs.end;
+        s.n_tris = hs.n_tris;
+        const size_t nb = sizeof(float4) * 2 * (size_t)(hs.n_nodes ? hs.n_nodes : 1);
+        const size_t tb = sizeof(float4) * 3 * (size_t)(hs.n_tris ? hs.n_tris : 1);
+        const size_t mb = sizeof(float4) * (size_t)(hs.n_tris ? hs.n_tris : 1);
+        hipError_t e = hipMalloc(&s.nodes, nb);
+        if (e == hipSuccess) e = hipMalloc(&s.tris, tb);
+        if (e == hipSuccess) e = hipMalloc(&s.mats, mb);
+        if (e == hipSuccess && hs.n_nodes) e = hipMemcpy(s.nodes, hs.nodes, nb, hipMemcpyHostToDevice);
+        if (e == hipSuccess && hs.n_tris) e = hipMemcpy(s.tris, hs.tris, tb, hipMemcpyHostToDevice);
+        if (e == hipSuccess && hs.n_tris) e = hipMemcpy(s.mats, hs.mats, mb, hipMemcpyHostToDevice);
+        p.scene = s;
+        if (e != hipSuccess) {
+            set_error("rt_upload_scene: device %d: %s", p.device, hipGetErrorString(e));
+            free_scene(p);
+            free_host_scene(&hs);
+            return e == hipErrorOutOfMemory ? RT_ERR_OOM : RT_ERR_HIP;
+        }
+    }
+    ctx->n_nodes = hs.n_nodes;
+    ctx->n_tris = hs.n_tris;
+    ctx->max_depth = hs.max_depth;
+    ctx->has_scene = true;
+    free_host_scene(&hs);
+    return RT_OK;
+}
+
+int rt_scene_info(rt_ctx* ctx, size_t* n_nodes, size_t* n_tris, int* max_depth) {
+    if (!ctx) { set_error("rt_scene_info: null context"); return RT_ERR_INVALID_ARG; }
+    if (!ctx->has_scene) { set_error("rt_scene_info: no scene uploaded"); return RT_ERR_NO_SCENE; }
+    if (n_nodes) *n_nodes = (size_t)ctx->n_nodes;
+    if (n_tris) *n_tris = (size_t)ctx->n_tris;
+    if (max_depth) *max_depth = ctx->max_depth;
+    return RT_OK;
+}
+
+static int check_render_args(rt_ctx* ctx, const rt_camera_ubo* cam, int width, int height,
+                             int max_bounces, const char* fn) {
+    if (!ctx || !cam) { set_error("%s: null context or camera", fn); return RT_ERR_INVALID_ARG; }
+    if (width < 1 || height < 1 || (int64_t)width * (int64_t)height > (int64_t)1 << 31) {
+        set_error("%s: bad frame size %dx%d", fn, width, height);
+        return RT_ERR_INVALID_ARG;
+    }
+    if (max_bounces < 1 || max_bounces > 1024) {
+        set_error("%s: max_bounces must be in [1, 1024], got %d", fn, max_bounces);
+        return RT_ERR_INVALID_ARG;
+    }
+    if (!ctx->has_scene) { set_error("%s: no scene uploaded", fn); return RT_ERR_NO_SCENE; }
+    return RT_OK;
+}
+
+static int ensure_out(PerDevice& p, size_t pixels, bool rad) {
+    if (pixels > p.out_cap || (rad && !p.d_rad)) {
+        if (p.d_rgba) (void)hipFree(p.d_rgba);
+        if (p.d_rad) (void)hipFree(p.d_rad);
+        p.d_rgba = nullptr;
+        p.d_rad = nullptr;
+        p.out_cap = 0;
+        RT_HIP_CHECK(hipMalloc(&p.d_rgba, pixels * 4));
+        if (rad) RT_HIP_CHECK(hipMalloc(&p.d_rad, pixels * 12));
+        p.out_cap = pixels;
+    }
+    return RT_OK;
+}
+
+int rt_render_tile_device(rt_ctx* ctx, const rt_camera_ubo* cam, int width, int height,
+                          int max_bounces, int x0, int y0, int tile_w, int tile_h,
+                          void* d_out_rgba, void* d_out_radiance, void* stream, rt_stats* stats) {
+    int rc = check_render_args(ctx, cam, width, height, max_bounces, "rt_render_tile_device");
+    if (rc) return rc;
+    if (tile_w < 1 || tile_h < 1 || x0 < 0 || y0 < 0 || x0 + tile_w > width || y0 + tile_h > height) {
+        set_error("rt_render_tile_device: tile (%d,%d %dx%d) outside the %dx%d frame",
+                  x0, y0, tile_w, tile_h, width, height);
+        return RT_ERR_INVALID_ARG;
+    }
+    PerDevice& p = ctx->dev[0];
+    RT_HIP_CHECK(hipSetDevice(p.device));
+    hipStream_t s = stream ? static_cast<hipStream_t>(stream) : p.stream;
+    TraceArgs a;
+    a.scene = p.scene;
+    a.cam = cam_from_ubo(cam);
+    a.width = width; a.height = height; a.max_bounces = max_bounces;
+    a.x0 = x0; a.y0 = y0; a.tw = tile_w; a.th = tile_h;
+    a.band_h = tile_h; a.band_stride = 1; a.band_off = 0;
+    a.out_rgba = static_cast<uchar4*>(d_out_rgba);
+    a.out_rad = static_cast<float*>(d_out_radiance);
+    a.counters = nullptr;
+    if (stats) {
+        a.counters = p.d_counters;
+        RT_HIP_CHECK(hipMemsetAsync(p.d_counters, 0, sizeof(Counters), s));
+    }
+    if (stats) RT_HIP_CHECK(hipEventRecord(p.ev0, s));
+    RT_HIP_CHECK(launch_trace(a, s));
+    if (stats) {
+        RT_HIP_CHECK(hipEventRecord(p.ev1, s));
+        RT_HIP_CHECK(hipEventSynchronize(p.ev1));
+        Counters c;
+        RT_HIP_CHECK(hipMemcpy(&c, p.d_counters, sizeof c, hipMemcpyDeviceToHost));
+        float ms = 0.f;
+        RT_HIP_CHECK(hipEventElapsedTime(&ms, p.ev0, p.ev1));
+        stats->pixels = (uint64_t)tile_w * (uint64_t)tile_h;
+        stats->segments = c.segments;
+        stats->node_visits = c.node_visits;
+        stats->tri_tests = c.tri_tests;
+        stats->mat_reads = c.mat_reads;
+        stats->ms = ms;
+    }
+    return RT_OK;
+}
+
+int rt_band_rows(int height, int band_h, int band_stride, int band_off) {
+    if (height < 1 || band_h < 1 || band_stride < 1 || band_off < 0 || band_off >= band_stride) return -1;
+    // rows of frame [0, height) whose band index b = row / band_h has b % band_stride == band_off
+    const int n_bands = (height + band_h - 1) / band_h;
+    int rows = 0;
+    for (int b = band_off; b < n_bands; b += band_stride)
+        rows += std::min(band_h, height - b * band_h);
+    return rows;
+}
+
+static int render_bands_on(PerDevice& p, const rt_camera_ubo* cam, int width, int height, int max_bounces,
+                           int band_h, int band_stride, int band_off, int rows,
+                           uchar4* d_rgba, float* d_rad, hipStream_t s, bool count) {
+    TraceArgs a;
+    a.scene = p.scene;
+    a.cam = cam_from_ubo(cam);
+    a.width = width; a.height = height; a.max_bounces = max_bounces;
+    a.x0 = 0; a.y0 = 0; a.tw = width; a.th = rows;
+    a.band_h = band_h; a.band_stride = band_stride; a.band_off = band_off;
+    a.out_rgba = d_rgba;
+    a.out_rad = d_rad;
+    a.counters = count ? p.d_counters : nullptr;
+    if (count) RT_HIP_CHECK(hipMemsetAsync(p.d_counters, 0, sizeof(Counters), s));
+    RT_HIP_CHECK(hipEventRecord(p.ev0, s));
+    RT_HIP_CHECK(launch_trace(a, s));
+    RT_HIP_CHECK(hipEventRecord(p.ev1, s));
+    return RT_OK;
+}
+
+static int collect_stats(PerDevice& p, uint64_t pixels, rt_stats* stats, bool accumulate) {
+    Counters c;
+    RT_HIP_CHECK(hipMemcpy(&c, p.d_counters, sizeof c, hipMemcpyDeviceToHost));
+    float ms = 0.f;
+    RT_HIP_CHECK(hipEventElapsedTime(&ms, p.ev0, p.ev1));
+    if (!accumulate) std::memset(stats, 0, sizeof *stats);
+    stats->pixels += pixels;
+    stats->segments += c.segments;
+    stats->node_visits += c.node_visits;
+    stats->tri_tests += c.tri_tests;
+    stats->mat_reads += c.mat_reads;
+    if (ms > stats->ms) stats->ms = ms;
+    return RT_OK;
+}
+
+int rt_render_bands_device(rt_ctx* ctx, const rt_camera_ubo* cam, int width, int height, int max_bounces,
+                           int band_h, int band_stride, int band_off,
+                           void* d_out_rgba, void* d_out_radiance, void* stream, rt_stats* stats) {
+    int rc = check_render_args(ctx, cam, width, height, max_bounces, "rt_render_bands_device");
+    if (rc) return rc;
+    const int rows = rt_band_rows(height, band_h, band_stride, band_off);
+    if (rows < 0) {
+        set_error("rt_render_bands_device: bad bands (band_h %d, stride %d, offset %d)", band_h, band_stride, band_off);
+        return RT_ERR_INVALID_ARG;
+    }
+    if (rows == 0) {
+        if (stats) std::memset(stats, 0, sizeof *stats);
+        return RT_OK;
+    }
+    PerDevice& p = ctx->dev[0];
+    RT_HIP_CHECK(hipSetDevice(p.device));
+    hipStream_t s = stream ? static_cast<hipStream_t>(stream) : p.stream;
+    rc = render_bands_on(p, cam, width, height, max_bounces, band_h, band_stride, band_off, rows,
+                         static_cast<uchar4*>(d_out_rgba), static_cast<float*>(d_out_radiance), s, stats != nullptr);
+    if (rc) return rc;
+    if (stats) {
+        RT_HIP_CHECK(hipEventSynchronize(p.ev1));
+        return collect_stats(p, (uint64_t)rows * width, stats, false);
+    }
+    return RT_OK;
+}
+
+int rt_render(rt_ctx* ctx, const rt_camera_ubo* cam, int width, int height, int max_bounces,
+              uint8_t* out_rgba, float* out_radiance, rt_stats* stats) {
+    int rc = check_render_args(ctx, cam, width, height, max_bounces, "rt_render");
+    if (rc) return rc;
+    if (!out_rgba) { set_error("rt_render: out_rgba is required"); return RT_ERR_INVALID_ARG; }
+    const int nd = (int)ctx->dev.size();
+    // Device k renders the interleaved 16-row bands k, k+nd, ... (sky rows and
+    // geometry rows spread evenly), into a packed buffer that is read back and
+    // scattered to the bands' rows.
+    const int bh = nd == 1 ? height : 16;
+    std::vector<int> rows(nd);
+    for (int k = 0; k < nd; ++k) rows[k] = rt_band_rows(height, bh, nd, k);
+    for (int k = 0; k < nd; ++k) {
+        if (rows[k] == 0) continue;
+        PerDevice& p = ctx->dev[k];
+        RT_HIP_CHECK(hipSetDevice(p.device));
+        rc = ensure_out(p, (size_t)width * rows[k], out_radiance != nullptr);
+        if (rc) return rc;
+        rc = render_bands_on(p, cam, width, height, max_bounces, bh, nd, k, rows[k], p.d_rgba,
+                             out_radiance ? p.d_rad : nullptr, p.stream, stats != nullptr);
+        if (rc) return rc;
+    }
+    if (stats) std::memset(stats, 0, sizeof *stats);
+    std::vector<uint8_t> stage_rgba;
+    std::vector<float> stage_rad;
+    for (int k = 0; k < nd; ++k) {
+        if (rows[k] == 0) continue;
+        PerDevice& p = ctx->dev[k];
+        RT_HIP_CHECK(hipSetDevice(p.device));
+        const size_t px = (size_t)width * rows[k];
+        uint8_t* dst_rgba = out_rgba;
+        float* dst_rad = out_radiance;
+        if (nd > 1) {
+            stage_rgba.resize(px * 4);
+            dst_rgba = stage_rgba.data();
+            if (out_radiance) { stage_rad.resize(px * 3); dst_rad = stage_rad.data(); }
+        }
+        RT_HIP_CHECK(hipMemcpyAsync(dst_rgba, p.d_rgba, px * 4, hipMemcpyDeviceToHost, p.stream));
+        if (out_radiance)
+            RT_HIP_CHECK(hipMemcpyAsync(dst_rad, p.d_rad, px * 12, hipMemcpyDeviceToHost, p.stream));
+        RT_HIP_CHECK(hipStreamSynchronize(p.stream));
+        if (nd > 1) {
+            for (int ly = 0; ly < rows[k]; ++ly) {
+                const int y = ((ly / bh) * nd + k) * bh + ly % bh;
+                std::memcpy(out_rgba + (size_t)y * width * 4, dst_rgba + (size_t)ly * width * 4, (size_t)width * 4);
+                if (out_radiance)
+                    std::memcpy(out_radiance + (size_t)y * width * 3, dst_rad + (size_t)ly * width * 3,
+                                (size_t)width * 12);
+            }
+        }
+        if (stats) {
+            rc = collect_stats(p, px, stats, true);
+            if (rc) return rc;
+        }
+    }
+    return RT_OK;
+}
+
+int rt_scene_validate(const void* vertices, size_t vertex_bytes, const void* materials, size_t material_bytes,
+                      const void* bvh_nodes, size_t bvh_bytes, size_t* n_nodes, int* max_depth) {
+    HostScene hs;
+    const char* err = nullptr;
+    int rc = build_host_scene(vertices, vertex_bytes, materials, material_bytes, bvh_nodes, bvh_bytes, &hs, &err);
+    if (rc != RT_OK) { set_error("rt_scene_validate: %s", err); return rc; }
+    if (n_nodes) *n_nodes = (size_t)hs.end;
+    if (max_depth) *max_depth = hs.max_depth;
+    free_host_scene(&hs);
+    return RT_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,120 @@
+"""ctypes binding of the C ABI (include/rtamd.h) — the Python stand-in for the
+JNI shim a Java host would use.
+
+The library is the in-tree lib/librtamd.so built by __graft_entry__.build()
+(or `make -C 3d-ray-tracer-vulkan_amd`).  There is no fallback: if it is
+missing or fails to load, every call raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import threading
+
+PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.path.join(PKG_ROOT, "lib", "librtamd.so")
+
+RT_OK = 0
+RT_ERR = {
+    -1: "RT_ERR_INVALID_ARG",
+    -2: "RT_ERR_NO_DEVICE",
+    -3: "RT_ERR_HIP",
+    -4: "RT_ERR_BAD_SCENE",
+    -5: "RT_ERR_NO_SCENE",
+    -6: "RT_ERR_OOM",
+    -7: "RT_ERR_IO",
+}
+
+# Every symbol include/rtamd.h declares (checked by tests/test_abi.py).
+EXPORTED = (
+    "rt_create", "rt_upload_scene", "rt_render", "rt_render_tile_device", "rt_destroy",
+    "rt_last_error", "rt_scene_info", "rt_bvh_layout_size", "rt_build_scene",
+    "rt_camera_from_lookat", "rt_mesh_load_obj", "rt_mesh_tri_count", "rt_mesh_transform",
+    "rt_mesh_free", "rt_mesh_procedural", "rt_render_bands_device", "rt_band_rows",
+    "rt_scene_validate",
+)
+
+
+class RtError(RuntimeError):
+    """A non-zero status from the C ABI (the JNI shim throws RuntimeException)."""
+
+    def __init__(self, code: int, message: str):
+        super().__init__(f"{RT_ERR.get(code, code)}: {message}")
+        self.code = code
+
+
+class CameraUBO(C.Structure):
+    _fields_ = [
+        ("origin", C.c_float * 4),
+        ("lower_left", C.c_float * 4),
+        ("horizontal", C.c_float * 4),
+        ("vertical", C.c_float * 4),
+        ("frame_count", C.c_int32),
+        ("sky_enabled", C.c_int32),
+        ("pad", C.c_int32 * 2),
+    ]
+
+
+class Stats(C.Structure):
+    _fields_ = [
+        ("pixels", C.c_uint64),
+        ("segments", C.c_uint64),
+        ("node_visits", C.c_uint64),
+        ("tri_tests", C.c_uint64),
+        ("mat_reads", C.c_uint64),
+        ("ms", C.c_double),
+    ]
+
+    def as_dict(self) -> dict:
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+assert C.sizeof(CameraUBO) == 80
+
+_lock = threading.Lock()
+_lib = None
+
+
+def lib() -> C.CDLL:
+    global _lib
+    with _lock:
+        if _lib is None:
+            if not os.path.exists(LIB_PATH):
+                raise RtError(-3, f"{LIB_PATH} is missing: run __graft_entry__.build() "
+                                  "(there is no non-HIP fallback)")
+            L = C.CDLL(LIB_PATH)
+            vp, sz, i32, u64, dp, fp = C.c_void_p, C.c_size_t, C.c_int, C.c_uint64, C.POINTER(C.c_double), C.POINTER(C.c_float)
+            sig = {
+                "rt_create": (i32, [C.POINTER(C.c_int), i32, C.POINTER(vp)]),
+                "rt_upload_scene": (i32, [vp, vp, sz, vp, sz, vp, sz]),
+                "rt_render": (i32, [vp, C.POINTER(CameraUBO), i32, i32, i32, vp, vp, C.POINTER(Stats)]),
+                "rt_render_tile_device": (i32, [vp, C.POINTER(CameraUBO), i32, i32, i32, i32, i32, i32, i32,
+                                                vp, vp, vp, C.POINTER(Stats)]),
+                "rt_destroy": (i32, [vp]),
+                "rt_last_error": (C.c_char_p, []),
+                "rt_scene_info": (i32, [vp, C.POINTER(sz), C.POINTER(sz), C.POINTER(i32)]),
+                "rt_bvh_layout_size": (i32, [sz, C.POINTER(sz), C.POINTER(sz)]),
+                "rt_build_scene": (i32, [dp, fp, sz, u64, i32, fp, fp, vp]),
+                "rt_camera_from_lookat": (i32, [dp, dp, dp, C.c_double, C.c_double, C.POINTER(CameraUBO)]),
+                "rt_mesh_load_obj": (i32, [C.c_char_p, C.POINTER(vp)]),
+                "rt_mesh_tri_count": (sz, [vp]),
+                "rt_mesh_transform": (i32, [vp, dp, dp, dp]),
+                "rt_mesh_free": (i32, [vp]),
+                "rt_mesh_procedural": (i32, [sz, u64, dp, dp, dp]),
+                "rt_render_bands_device": (i32, [vp, C.POINTER(CameraUBO), i32, i32, i32, i32, i32, i32,
+                                                 vp, vp, vp, C.POINTER(Stats)]),
+                "rt_band_rows": (i32, [i32, i32, i32, i32]),
+                "rt_scene_validate": (i32, [vp, sz, vp, sz, vp, sz, C.POINTER(sz), C.POINTER(i32)]),
+            }
+            for name, (res, args) in sig.items():
+                f = getattr(L, name)
+                f.restype = res
+                f.argtypes = args
+            _lib = L
+        return _lib
+
+
+def check(rc: int) -> None:
+    if rc != RT_OK:
+        msg = lib().rt_last_error()
+        raise RtError(rc, msg.decode() if msg else "")

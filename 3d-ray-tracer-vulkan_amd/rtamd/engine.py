@@ -1,0 +1,211 @@
+"""Render side of the host API.
+
+Renderer   — a synchronous wrapper of one rt_ctx (the C ABI).
+HipEngine  — a mirror of the reference's VulkanEngine public API
+             (src/dev/demir/vulkan/engine/VulkanEngine.java:120-185): a render
+             thread fed through queues that are drained to their latest value
+             (handleCommands :277-313), rendering frames as long as a scene and
+             a camera are present (mainLoop :244-271) and publishing each one to
+             an AtomicReference-like slot (:264).
+FrameData  — FrameData.java:9-16 (+ the render statistics its TODO asks for).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import queue
+import threading
+import time
+from dataclasses import dataclass
+from typing import Optional, Sequence, Tuple, Union
+
+import numpy as np
+
+from ._lib import CameraUBO, RtError, Stats, check, lib
+from .scene import BuiltCpuData, Camera
+
+REFERENCE_WIDTH = 1280          # VulkanEngine.java:45
+REFERENCE_HEIGHT = 720          # VulkanEngine.java:46
+REFERENCE_MAX_BOUNCES = 10      # compute_dynamic_ray.comp:44
+
+
+def _ubo(cam: Union[Camera, CameraUBO, bytes]) -> CameraUBO:
+    if isinstance(cam, Camera):
+        return cam.ubo
+    if isinstance(cam, CameraUBO):
+        return cam
+    if isinstance(cam, (bytes, bytearray)) and len(cam) == 80:
+        return CameraUBO.from_buffer_copy(cam)
+    raise TypeError("camera must be a Camera, a CameraUBO or 80 UBO bytes")
+
+
+class Renderer:
+    """One context on one or more HIP devices (rt_create / rt_destroy)."""
+
+    def __init__(self, device_ids: Sequence[int] = (0,)):
+        ids = (C.c_int * len(device_ids))(*device_ids)
+        self._ctx = C.c_void_p()
+        check(lib().rt_create(ids, len(device_ids), C.byref(self._ctx)))
+        self.device_ids = tuple(device_ids)
+
+    def close(self) -> None:
+        if self._ctx:
+            lib().rt_destroy(self._ctx)
+            self._ctx = C.c_void_p()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def upload_scene(self, data: BuiltCpuData) -> None:
+        """internalSwapScene (VulkanEngine.java:318-373); deep copy."""
+        v = np.ascontiguousarray(data.model_vertex_data, dtype=np.float32)
+        m = np.ascontiguousarray(data.model_material_data, dtype=np.float32)
+        b = np.ascontiguousarray(data.flat_bvh_data, dtype=np.uint8)
+        check(lib().rt_upload_scene(self._ctx, v.ctypes.data, v.nbytes, m.ctypes.data, m.nbytes,
+                                    b.ctypes.data, b.nbytes))
+
+    def upload_raw(self, vertices: bytes, materials: bytes, nodes: bytes) -> None:
+        check(lib().rt_upload_scene(self._ctx, vertices, len(vertices), materials, len(materials),
+                                    nodes, len(nodes)))
+
+    def scene_info(self) -> dict:
+        nn, nt, d = C.c_size_t(), C.c_size_t(), C.c_int()
+        check(lib().rt_scene_info(self._ctx, C.byref(nn), C.byref(nt), C.byref(d)))
+        return {"n_nodes": nn.value, "n_tris": nt.value, "max_depth": d.value}
+
+    def render(self, camera, width: int, height: int, max_bounces: int = REFERENCE_MAX_BOUNCES,
+               radiance: bool = False, stats: bool = False):
+        """renderFrame (VulkanEngine.java:401-431).  Returns (rgba[H,W,4] uint8,
+        radiance[H,W,3] float32 or None, stats dict or None)."""
+        rgba = np.empty((height, width, 4), dtype=np.uint8)
+        rad = np.empty((height, width, 3), dtype=np.float32) if radiance else None
+        st = Stats() if stats else None
+        check(lib().rt_render(self._ctx, C.byref(_ubo(camera)), width, height, max_bounces,
+                              rgba.ctypes.data, rad.ctypes.data if rad is not None else None,
+                              C.byref(st) if st is not None else None))
+        return rgba, rad, (st.as_dict() if st is not None else None)
+
+    def render_tile_device(self, camera, width: int, height: int, max_bounces: int,
+                           x0: int, y0: int, tile_w: int, tile_h: int,
+                           d_rgba: Optional[int], d_radiance: Optional[int] = None,
+                           stream: Optional[int] = None, stats: bool = False):
+        """Enqueue one tile into device buffers (raw device pointers, e.g.
+        torch tensor data_ptr()) on a HIP stream handle."""
+        st = Stats() if stats else None
+        check(lib().rt_render_tile_device(self._ctx, C.byref(_ubo(camera)), width, height, max_bounces,
+                                          x0, y0, tile_w, tile_h, d_rgba, d_radiance, stream,
+                                          C.byref(st) if st is not None else None))
+        return st.as_dict() if st is not None else None
+
+
+@dataclass
+class FrameData:
+    """FrameData.java: RGBA8 pixels of one frame, row 0 = top."""
+    pixel_data: np.ndarray
+    stats: Optional[dict] = None
+
+
+class AtomicReference:
+    """The java.util.concurrent.atomic.AtomicReference the UI shares with the engine."""
+
+    def __init__(self, value=None):
+        self._v = value
+        self._lock = threading.Lock()
+
+    def set(self, v) -> None:
+        with self._lock:
+            self._v = v
+
+    def get(self):
+        with self._lock:
+            return self._v
+
+    def get_and_set(self, v):
+        with self._lock:
+            old, self._v = self._v, v
+            return old
+
+
+class HipEngine:
+    """Drop-in for VulkanEngine: same public methods, a render thread that owns
+    the rt_ctx (single-thread affinity, VulkanEngine.java:194-206)."""
+
+    def __init__(self, frame_queue: AtomicReference, width: int = REFERENCE_WIDTH,
+                 height: int = REFERENCE_HEIGHT, max_bounces: int = REFERENCE_MAX_BOUNCES,
+                 device_ids: Sequence[int] = (0,), collect_stats: bool = False):
+        self.frame_queue = frame_queue
+        self.width, self.height, self.max_bounces = width, height, max_bounces
+        self.device_ids = tuple(device_ids)
+        self.collect_stats = collect_stats
+        self._scene_q: "queue.Queue[BuiltCpuData]" = queue.Queue()
+        self._camera_q: "queue.Queue[Camera]" = queue.Queue()
+        self._sky_q: "queue.Queue[bool]" = queue.Queue()
+        self._running = False
+        self._thread = threading.Thread(target=self._run, name="HIP-Engine-Thread", daemon=True)
+        self.is_sky_enabled = 1
+        self.frames_rendered = 0
+        self.error: Optional[BaseException] = None
+
+    # --- public API (UI thread) ---
+    def start(self) -> None:
+        self._running = True
+        self._thread.start()
+
+    def stop(self) -> None:
+        self._running = False
+        self._thread.join(5.0)          # 5 s graceful window, VulkanEngine.java:145
+
+    def submit_scene(self, scene_data: BuiltCpuData) -> None:
+        self._scene_q.put(scene_data)
+
+    def submit_camera_update(self, camera: Camera) -> None:
+        self._camera_q.put(camera)
+
+    def submit_sky_toggle(self, is_sky_on: bool) -> None:
+        self._sky_q.put(bool(is_sky_on))
+
+    # --- render thread ---
+    def _run(self) -> None:
+        renderer = None
+        try:
+            renderer = Renderer(self.device_ids)
+            have_scene, camera = False, None
+            while self._running:
+                try:                                        # one scene per pass (:281-285)
+                    renderer.upload_scene(self._scene_q.get_nowait())
+                    have_scene = True
+                except queue.Empty:
+                    pass
+                while True:                                 # drain to the latest camera (:288-298)
+                    try:
+                        camera = self._camera_q.get_nowait()
+                    except queue.Empty:
+                        break
+                while True:                                 # latest sky state (:300-312)
+                    try:
+                        self.is_sky_enabled = 1 if self._sky_q.get_nowait() else 0
+                    except queue.Empty:
+                        break
+                if not have_scene or camera is None:
+                    time.sleep(0.016)
+                    continue
+                ubo = CameraUBO.from_buffer_copy(bytes(camera.ubo))
+                ubo.sky_enabled = self.is_sky_enabled        # written, ignored by the shader
+                rgba, _, st = renderer.render(ubo, self.width, self.height, self.max_bounces,
+                                              stats=self.collect_stats)
+                self.frame_queue.set(FrameData(rgba, st))
+                self.frames_rendered += 1
+        except BaseException as e:                          # FATAL (VRT) path, :197-201
+            self.error = e
+            self._running = False
+        finally:
+            if renderer is not None:
+                renderer.close()

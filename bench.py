@@ -1,0 +1,230 @@
+#!/usr/bin/env python3
+"""Benchmark: Mrays/s (ray segments per second) of the path-trace path.
+
+Workload (N = 1): BASELINE config 3 — the 50k-triangle synthetic scene at
+1920x1080, 4 bounces, default camera.  One step = one whole
+frame traced on the GPU(s): every pixel's full path, RGBA8 written to HBM.
+With N > 1 ranks (one process per GPU, torch.distributed over RCCL), the
+same frame is split into interleaved 16-row bands, rank r tracing bands
+r, r+N, ..., and the RGBA8 bands are gathered to rank 0 over xGMI
+(dist.gather) inside the timed step: strong scaling of one frame.
+
+value = segments of the frame x steps / wall time of the timed steps (max over
+ranks), in millions.  A segment is one executed bounce-loop iteration
+(compute_dynamic_ray.comp:179-232); its count per frame is deterministic and is
+taken from a counting pass outside the timed region.
+
+roofline: algorithmic bytes of one trace launch (32 B per BVH node visit +
+36 B per triangle test + 16 B per material read + 4 B per pixel; DESIGN.md
+§Roofline) / the launch's average device time from HIP events recorded on the
+launch stream, against 8 TB/s HBM.
+cpu_baseline: the CPU oracle (oracle/rt_oracle.c, OpenMP) on a bounded row
+sample of the same frame, rank 0 at N = 1 only.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "3d-ray-tracer-vulkan_amd"))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0      # MI355X HBM3E, MI355X_MICROARCH.md chip table
+BASELINE = json.load(open(os.path.join(ROOT, "BASELINE.json")))
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--config", type=int, default=3, help="BASELINE config index (3 = headline)")
+    ap.add_argument("--band", type=int, default=16, help="band height for N > 1")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU baseline sample time")
+    ap.add_argument("--traffic-json", default=None,
+                    help="PMC-derived HBM bytes per launch (profiles/*.json) to report as roofline.traffic")
+    args = ap.parse_args()
+
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    import rtamd
+    from rtamd import configs
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        log(f"note: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE")
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    cfg = configs.get(args.config)
+    t0 = time.time()
+    built = cfg.build()
+    cam = cfg.camera()
+    log(f"[rank {rank}] built {cfg.name}: {built.triangle_count} flat tris, {built.n_nodes} nodes "
+        f"in {time.time() - t0:.2f}s")
+    W, H, B = cfg.width, cfg.height, cfg.max_bounces
+
+    renderer = rtamd.Renderer((local_rank,))
+    renderer.upload_scene(built)
+    L = rtamd.lib()
+    band_h = H if world == 1 else args.band
+    rows = L.rt_band_rows(H, band_h, world, rank)
+    max_rows = max(L.rt_band_rows(H, band_h, world, r) for r in range(world))
+    d_rgba = torch.empty((max_rows, W, 4), dtype=torch.uint8, device=dev)
+    stream = torch.cuda.current_stream(dev)
+
+    import ctypes as C
+    from rtamd._lib import Stats, check
+
+    def trace(stats: bool = False):
+        s = Stats()
+        check(L.rt_render_bands_device(renderer._ctx, C.byref(cam.ubo), W, H, B, band_h, world, rank,
+                                       d_rgba.data_ptr(), None, stream.cuda_stream,
+                                       C.byref(s) if stats else None))
+        return s.as_dict() if stats else None
+
+    gather_list = [torch.empty_like(d_rgba) for _ in range(world)] if (world > 1 and rank == 0) else None
+
+    def step(ev=None):
+        if ev is not None:
+            ev[0].record(stream)
+        trace()
+        if ev is not None:
+            ev[1].record(stream)
+        if world > 1:
+            dist.gather(d_rgba, gather_list, dst=0)
+
+    # Counting pass (untimed): this rank's work, then the frame totals.
+    st = trace(stats=True)
+    counts = torch.tensor([st["pixels"], st["segments"], st["node_visits"], st["tri_tests"], st["mat_reads"]],
+                          dtype=torch.float64, device=dev)
+    local = counts.clone()
+    if world > 1:
+        dist.all_reduce(counts)
+    pixels, segments, node_visits, tri_tests, mat_reads = [float(x) for x in counts.tolist()]
+    l_pix, l_seg, l_nodes, l_tris, l_mats = [float(x) for x in local.tolist()]
+    log(f"[rank {rank}] frame: {segments:.0f} segments ({segments / pixels:.3f}/px), "
+        f"{node_visits / segments:.2f} node visits/seg, {tri_tests / segments:.3f} tri tests/seg")
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    t_start = time.perf_counter()
+    for k in range(args.steps):
+        step(evs[k])
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t_start
+    kernel_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
+
+    t = torch.tensor([elapsed, kernel_ms], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed, kernel_ms_max = float(t[0]), float(t[1])
+
+    value = segments * args.steps / elapsed / 1e6
+    alg_bytes = 32.0 * l_nodes + 36.0 * l_tris + 16.0 * l_mats + 4.0 * l_pix
+    ref_layout_bytes = 48.0 * l_nodes + 48.0 * l_tris + 16.0 * l_mats + 4.0 * l_pix
+    achieved = alg_bytes / (kernel_ms * 1e-3) / 1e9
+    traffic = None
+    if args.traffic_json and os.path.exists(args.traffic_json):
+        traffic = json.load(open(args.traffic_json)).get("hbm_bytes_per_launch")
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(built, cam, W, H, B, segments, args.cpu_seconds)
+
+    if rank == 0:
+        out = {
+            "metric": BASELINE["metric"],
+            "value": round(value, 2),
+            "unit": "Mrays/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (seeded procedural 50k-triangle shell + ground plane + type-3 cube; default camera)",
+            "config": {
+                "workload": cfg.name,
+                "width": W, "height": H, "max_bounces": B,
+                "triangles_flat": built.triangle_count, "bvh_nodes": built.n_nodes,
+                "segments_per_frame": int(segments),
+                "node_visits_per_segment": round(node_visits / segments, 3),
+                "tri_tests_per_segment": round(tri_tests / segments, 4),
+                "partition": "single frame" if world == 1 else f"interleaved {band_h}-row bands, dist.gather to rank 0",
+                "parallelism": f"tile{world}",
+            },
+            "roofline": {
+                "bound": "hbm",
+                "achieved": round(achieved, 1),
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4),
+                "traffic": traffic,
+                "kernel": "trace_kernel",
+                "kernel_ms": round(kernel_ms, 4),
+                "alg_bytes_per_launch": int(alg_bytes),
+                "alg_bytes_per_segment": round(alg_bytes / l_seg, 1),
+                "reference_layout_frac": round(ref_layout_bytes / (kernel_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+            },
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out), flush=True)
+    renderer.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(built, cam, W, H, B, frame_segments, target_s):
+    """The oracle on every k-th row of the same frame, all host threads we may use."""
+    from oracle import oracle_lib
+    threads = max(1, min(16, int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)))
+    args = (built.model_vertex_data, built.model_material_data, built.flat_bvh_data, cam.ubo_bytes(), W, H, B)
+    # probe on every 64th row, then size the sample to ~target_s
+    t0 = time.perf_counter()
+    _, _, c = oracle_lib.render(*args, row_step=64, radiance=False, n_threads=threads)
+    probe = time.perf_counter() - t0
+    rate = c["segments"] / max(probe, 1e-6)
+    step = 64
+    for s in (32, 16, 8, 4, 2, 1):
+        if frame_segments / s / rate <= target_s:
+            step = s
+    t0 = time.perf_counter()
+    _, _, c = oracle_lib.render(*args, row_step=step, radiance=False, n_threads=threads)
+    dt = time.perf_counter() - t0
+    return {
+        "value": round(c["segments"] / dt / 1e6, 3),
+        "unit": "Mrays/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": f"every {step}th row of the same frame ({c['pixels']} px, {c['segments']} segments, {dt:.2f} s)",
+    }
+
+
+if __name__ == "__main__":
+    main()

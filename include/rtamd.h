@@ -1,0 +1,201 @@
+/*
+ * rtamd.h — C ABI of the MI355X (gfx950) path-trace backend.
+ *
+ * This is the drop-in boundary for the reference's per-pixel render path
+ * (this-Demir/3D-Ray-Tracer-Vulkan).  A Java host binds these symbols through a
+ * thin JNI shim; Python binds them through ctypes
+ * (3d-ray-tracer-vulkan_amd/rtamd/_lib.py).  Plain C types only: pointers,
+ * sizes, and POD structs whose bytes equal the reference's Vulkan buffers.
+ *
+ * Status convention: every int-returning call returns RT_OK (0) on success and
+ * a negative RT_ERR_* code on failure; rt_last_error() then returns a
+ * thread-local, human-readable message.  No C++ exception crosses this ABI.
+ *
+ * Threading: an rt_ctx is single-thread-affine, like the reference's VRT
+ * thread (VulkanEngine.java:194-206).  Different contexts may be used from
+ * different threads.
+ */
+#ifndef RTAMD_H
+#define RTAMD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RT_OK               0
+#define RT_ERR_INVALID_ARG -1  /* null pointer, bad size, bad dimension        */
+#define RT_ERR_NO_DEVICE   -2  /* no gfx950 device / bad device id             */
+#define RT_ERR_HIP         -3  /* a HIP runtime call failed                    */
+#define RT_ERR_BAD_SCENE   -4  /* node/triangle buffers are malformed          */
+#define RT_ERR_NO_SCENE    -5  /* rt_render before rt_upload_scene             */
+#define RT_ERR_OOM         -6  /* host or device allocation failed             */
+#define RT_ERR_IO          -7  /* file could not be read / parsed              */
+
+/* Byte sizes of the reference's std430/std140 records. */
+#define RT_VERTEX_RECORD_BYTES   48  /* one flattened triangle: 3 x (vec3 pos, float pad)  SceneBuilder.java:95-99 */
+#define RT_MATERIAL_RECORD_BYTES 16  /* (vec3 albedo, float type)                          SceneBuilder.java:103   */
+#define RT_NODE_RECORD_BYTES     48  /* LinearBVHNode, std430                              BVHFlattener.java:19    */
+#define RT_CAMERA_UBO_BYTES      80  /* CameraUBO + frameCount + isSkyEnabled              VulkanEngine.java:378-396 */
+#define RT_REFERENCE_MAX_BOUNCES 10  /* compute_dynamic_ray.comp:44 */
+
+typedef struct rt_ctx rt_ctx;
+
+/* Same 80 bytes the reference writes into its camera UBO
+ * (VulkanEngine.java:387-395; std140 vec3 at offsets 0/16/32/48; ints at 64/68).
+ * frame_count and sky_enabled are accepted and ignored, as in the shader
+ * (compute_dynamic_ray.comp:26-34 declares neither). */
+typedef struct rt_camera_ubo {
+    float   origin[4];
+    float   lower_left[4];
+    float   horizontal[4];
+    float   vertical[4];
+    int32_t frame_count;
+    int32_t sky_enabled;
+    int32_t pad[2];
+} rt_camera_ubo;
+
+/* Work counters of one render call.  segments = executed iterations of the
+ * bounce loop (compute_dynamic_ray.comp:179-232); node_visits = hit_aabb calls
+ * (:193); tri_tests = hit_triangle calls (:201); mat_reads = scatter calls (:217).
+ * They are counted in the reference's visit order, so they are the same for
+ * every implementation of the path. */
+typedef struct rt_stats {
+    uint64_t pixels;
+    uint64_t segments;
+    uint64_t node_visits;
+    uint64_t tri_tests;
+    uint64_t mat_reads;
+    double   ms;          /* device time of the trace kernel(s), HIP events */
+} rt_stats;
+
+/* ---------------------------------------------------------------- engine -- */
+
+/* Replaces VulkanEngine.initVulkan (VulkanEngine.java:211-238).
+ * device_ids: HIP ordinals to render on (n_devices >= 1).  With several
+ * devices a frame is split into interleaved row bands, one per device, and
+ * read back per band.  There is no CPU backend: no gfx950 device is an error. */
+int rt_create(const int* device_ids, int n_devices, rt_ctx** out);
+
+/* Replaces VulkanEngine.internalSwapScene (VulkanEngine.java:318-373).
+ * vertices : 48 B per flattened triangle (SceneBuilder.java:92-99)
+ * materials: 16 B per flattened triangle (SceneBuilder.java:103)
+ * bvh_nodes: 48 B per node, preorder, little-endian (BVHFlattener.java:51-97)
+ * Deep-copies; the caller may free the buffers on return (the Java host frees
+ * them right after upload, VulkanEngine.java:343,351).  Sizes below one record
+ * (the reference's 1-float / 1-byte dummies for an empty scene,
+ * SceneBuilder.java:61-70) upload an empty scene, which renders sky only. */
+int rt_upload_scene(rt_ctx* ctx,
+                    const void* vertices,  size_t vertex_bytes,
+                    const void* materials, size_t material_bytes,
+                    const void* bvh_nodes, size_t bvh_bytes);
+
+/* Replaces VulkanEngine.renderFrame (VulkanEngine.java:401-431): renders one
+ * width x height frame synchronously and copies it to host memory.
+ * out_rgba    : width*height*4 bytes, RGBA8 UNORM, row 0 = top (required)
+ * out_radiance: width*height*3 floats, the sqrt'd colour before quantisation
+ *               (nullable)
+ * stats       : nullable.
+ * max_bounces : the shader's MAX_BOUNCES; 10 reproduces the reference. */
+int rt_render(rt_ctx* ctx, const rt_camera_ubo* cam,
+              int width, int height, int max_bounces,
+              uint8_t* out_rgba, float* out_radiance, rt_stats* stats);
+
+/* Device-resident form for multi-GPU tiling and benchmarking: renders the
+ * rectangle [x0, x0+tile_w) x [y0, y0+tile_h) of a width x height frame of
+ * device 0 of ctx into DEVICE buffers d_out_rgba (tile_w*tile_h*4 B, may be
+ * null) and d_out_radiance (tile_w*tile_h*3 floats, may be null), enqueued on
+ * `stream` (a hipStream_t; null = the context's own stream).  Asynchronous
+ * unless stats is non-null, in which case it waits and fills stats. */
+int rt_render_tile_device(rt_ctx* ctx, const rt_camera_ubo* cam,
+                          int width, int height, int max_bounces,
+                          int x0, int y0, int tile_w, int tile_h,
+                          void* d_out_rgba, void* d_out_radiance,
+                          void* stream, rt_stats* stats);
+
+/* Interleaved row bands, for splitting a frame over GPUs with balanced work:
+ * renders every frame row y whose band index y / band_h is congruent to
+ * band_off modulo band_stride, packed in increasing y into DEVICE buffers of
+ * rt_band_rows(height, band_h, band_stride, band_off) rows of width pixels.
+ * Same stream / stats semantics as rt_render_tile_device. */
+int rt_render_bands_device(rt_ctx* ctx, const rt_camera_ubo* cam,
+                           int width, int height, int max_bounces,
+                           int band_h, int band_stride, int band_off,
+                           void* d_out_rgba, void* d_out_radiance,
+                           void* stream, rt_stats* stats);
+
+/* Row count of such a band set (-1 for bad arguments).  Pure host code. */
+int rt_band_rows(int height, int band_h, int band_stride, int band_off);
+
+/* Replaces VulkanEngine.cleanup. Null is accepted. */
+int rt_destroy(rt_ctx* ctx);
+
+/* Thread-local message for the last failing call on this thread. */
+const char* rt_last_error(void);
+
+/* Node / triangle counts and tree depth of the uploaded scene. */
+int rt_scene_info(rt_ctx* ctx, size_t* n_nodes, size_t* n_tris, int* max_depth);
+
+/* The validation rt_upload_scene performs, without a device (pure host code):
+ * RT_OK, or RT_ERR_BAD_SCENE with the reason in rt_last_error().  The node
+ * array must be the reference flattener's preorder layout (left child i+1,
+ * BVHFlattener.java:51-75) with every leaf's triangle inside the vertex and
+ * material buffers.  n_nodes receives the nodes reachable from the root. */
+int rt_scene_validate(const void* vertices, size_t vertex_bytes,
+                      const void* materials, size_t material_bytes,
+                      const void* bvh_nodes, size_t bvh_bytes,
+                      size_t* n_nodes, int* max_depth);
+
+/* ----------------------------------------------------------- scene build -- */
+/* Host-side producers of the three buffers, replacing the Java SceneBuilder
+ * (SceneBuilder.java:38-118), BVHBuilder (BVHBuilder.java:48-108), BVHFlattener
+ * (BVHFlattener.java:30-97) and Camera (Camera.java:44-68).  Pure CPU code. */
+
+/* Node / flattened-triangle counts the reference builder produces for n input
+ * triangles (they depend on n only: a range of 1 or 2 triangles becomes one
+ * node with two leaves, BVHBuilder.java:60-71). */
+int rt_bvh_layout_size(size_t n_tris, size_t* n_nodes, size_t* n_flat_tris);
+
+/* Builds the median-split BVH and writes the three reference buffers.
+ * tri_verts : n_tris*9 doubles, post-transform vertices v0,v1,v2 (Triangle.java:35-51)
+ * tri_mats  : n_tris*4 floats, (r,g,b,type) per triangle
+ * axis_seed : seeds the per-node split axis (the reference's is unseeded,
+ *             BVHBuilder.java:53; pixels do not depend on it)
+ * out_vertices : n_flat*12 floats; out_materials: n_flat*4 floats;
+ * out_nodes    : n_nodes*48 bytes. Sizes from rt_bvh_layout_size.
+ * n_threads    : 0 = all hardware threads.  Output does not depend on it. */
+int rt_build_scene(const double* tri_verts, const float* tri_mats, size_t n_tris,
+                   uint64_t axis_seed, int n_threads,
+                   float* out_vertices, float* out_materials, void* out_nodes);
+
+/* Camera.recalculateViewport (Camera.java:44-68) in double, cast to float as
+ * Vec3.store does (Vec3.java:132-136). */
+int rt_camera_from_lookat(const double origin[3], const double lookat[3],
+                          const double vup[3], double vfov_deg, double aspect,
+                          rt_camera_ubo* out);
+
+/* OBJ mesh (SceneBuilder.loadModel, SceneBuilder.java:129-191).  Faces with
+ * more than 3 vertices are fan-triangulated from vertex 0 (the convex case of
+ * Assimp's aiProcess_Triangulate; parity vs Assimp unpinned). */
+typedef struct rt_mesh rt_mesh;
+int    rt_mesh_load_obj(const char* path, rt_mesh** out);
+size_t rt_mesh_tri_count(const rt_mesh* mesh);
+/* Writes tri_count*9 doubles: float(obj) * scale + position, in double
+ * (SceneBuilder.java:172-174). */
+int    rt_mesh_transform(const rt_mesh* mesh, const double scale[3],
+                         const double position[3], double* out_tri_verts);
+int    rt_mesh_free(rt_mesh* mesh);
+
+/* Seeded procedural closed mesh (a displaced ellipsoid shell) with exactly
+ * n_tris triangles (n_tris even, >= 8) filling the box [bmin, bmax]; used for
+ * the synthetic 50k / 1M triangle configurations. */
+int rt_mesh_procedural(size_t n_tris, uint64_t seed,
+                       const double bmin[3], const double bmax[3],
+                       double* out_tri_verts);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RTAMD_H */

@@ -1,0 +1,73 @@
+"""ctypes wrapper of oracle/liboracle.so (rt_oracle.c).  TEST INFRASTRUCTURE ONLY."""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(HERE, "liboracle.so")
+
+
+class Counts(C.Structure):
+    _fields_ = [("pixels", C.c_uint64), ("segments", C.c_uint64), ("node_visits", C.c_uint64),
+                ("tri_tests", C.c_uint64), ("mat_reads", C.c_uint64)]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+_lib = None
+
+
+def build() -> None:
+    subprocess.run(["make", "-s", "-C", HERE], check=True)
+
+
+def lib() -> C.CDLL:
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB):
+            build()
+        L = C.CDLL(LIB)
+        f3 = C.POINTER(C.c_float)
+        L.orc_pcg.restype = C.c_uint32
+        L.orc_pcg.argtypes = [C.c_uint32]
+        L.orc_random_float.restype = C.c_float
+        L.orc_random_float.argtypes = [C.POINTER(C.c_uint32)]
+        L.orc_random_in_unit_sphere.argtypes = [C.POINTER(C.c_uint32), f3]
+        L.orc_hit_aabb.argtypes = [f3, f3, f3, f3, C.c_float, C.c_float]
+        L.orc_hit_triangle.argtypes = [f3, f3, f3, f3, f3, f3, f3]
+        L.orc_scatter.argtypes = [f3, C.POINTER(C.c_uint32), f3, f3, f3, f3, f3]
+        L.orc_render.argtypes = [C.c_void_p, C.c_size_t, C.c_void_p, C.c_size_t, C.c_void_p, C.c_size_t,
+                                 C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
+                                 C.c_int, C.c_void_p, C.c_void_p, C.POINTER(Counts), C.c_int]
+        _lib = L
+    return _lib
+
+
+def _buf(x):
+    a = np.ascontiguousarray(np.frombuffer(x, dtype=np.uint8) if isinstance(x, (bytes, bytearray)) else x)
+    return a, a.ctypes.data, a.nbytes
+
+
+def render(vertices, materials, nodes, camera_ubo: bytes, width: int, height: int, max_bounces: int,
+           tile=None, row_step: int = 1, radiance: bool = True, n_threads: int = 0):
+    """Returns (rgba[rows, w, 4], radiance[rows, w, 3] or None, counts dict)."""
+    x0, y0, tw, th = tile if tile is not None else (0, 0, width, height)
+    rows = (th + row_step - 1) // row_step
+    v, vp, vn = _buf(vertices)
+    m, mp, mn = _buf(materials)
+    b, bp, bn = _buf(nodes)
+    cam = np.frombuffer(bytes(camera_ubo), dtype=np.uint8).copy()
+    rgba = np.empty((rows, tw, 4), dtype=np.uint8)
+    rad = np.empty((rows, tw, 3), dtype=np.float32) if radiance else None
+    c = Counts()
+    rc = lib().orc_render(vp, vn, mp, mn, bp, bn, cam.ctypes.data, width, height, max_bounces,
+                          x0, y0, tw, th, row_step, rgba.ctypes.data,
+                          rad.ctypes.data if rad is not None else None, C.byref(c), n_threads)
+    if rc != 0:
+        raise RuntimeError(f"orc_render failed ({rc})")
+    return rgba, rad, c.as_dict()

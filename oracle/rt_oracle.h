@@ -1,0 +1,38 @@
+/*
+ * rt_oracle.h — CPU oracle of the path-trace path.  TEST INFRASTRUCTURE ONLY
+ * (see rt_oracle.c for the rules of use and the parity status).
+ */
+#ifndef RT_ORACLE_H
+#define RT_ORACLE_H
+#include <stddef.h>
+#include <stdint.h>
+
+typedef struct {                      /* the 80-B CameraUBO (VulkanEngine.java:387-395) */
+    float origin[4], lower_left[4], horizontal[4], vertical[4];
+    int32_t frame_count, sky_enabled, pad[2];
+} orc_camera;
+
+typedef struct {
+    uint64_t pixels, segments, node_visits, tri_tests, mat_reads;
+} orc_counts;
+
+uint32_t orc_pcg(uint32_t v);
+float    orc_random_float(uint32_t* seed);
+void     orc_random_in_unit_sphere(uint32_t* seed, float out[3]);
+int      orc_hit_aabb(const float origin[3], const float dir[3], const float bmin[3],
+                      const float bmax[3], float t_min, float t_max);
+int      orc_hit_triangle(const float origin[3], const float dir[3], const float v0[3],
+                          const float v1[3], const float v2[3], float* closest_t, float normal[3]);
+int      orc_scatter(const float material[4], uint32_t* seed, const float dir_in[3],
+                     const float hit_pos[3], const float normal[3], float att[3], float dir_out[3]);
+
+/* Renders rows y0, y0+row_step, ... of the tile [x0,x0+tile_w) x [y0,y0+tile_h)
+ * of a width x height frame.  Output rows are packed (row r of the output =
+ * frame row y0 + r*row_step).  n_threads: 0 = OpenMP default. */
+int orc_render(const void* vertices, size_t vertex_bytes,
+               const void* materials, size_t material_bytes,
+               const void* bvh_nodes, size_t bvh_bytes,
+               const orc_camera* cam, int width, int height, int max_bounces,
+               int x0, int y0, int tile_w, int tile_h, int row_step,
+               uint8_t* out_rgba, float* out_radiance, orc_counts* counts, int n_threads);
+#endif
