@@ -365,7 +365,7 @@ int rt_render_tile_device(rt_ctx* ctx, const rt_camera_ubo* cam, int width, int 
     }
     PerDevice& p = ctx->dev[0];
     RT_HIP_CHECK(hipSetDevice(p.device));
-    hipStream_t s = stream ? static_cast<hipStream_t>(stream) : p.stream;
+    hipStream_t s = static_cast<hipStream_t>(stream);   // NULL = the null stream
     TraceArgs a;
     a.scene = p.scene;
     a.cam = cam_from_ubo(cam);
@@ -458,7 +458,7 @@ int rt_render_bands_device(rt_ctx* ctx, const rt_camera_ubo* cam, int width, int
     }
     PerDevice& p = ctx->dev[0];
     RT_HIP_CHECK(hipSetDevice(p.device));
-    hipStream_t s = stream ? static_cast<hipStream_t>(stream) : p.stream;
+    hipStream_t s = static_cast<hipStream_t>(stream);   // NULL = the null stream
     rc = render_bands_on(p, cam, width, height, max_bounces, band_h, band_stride, band_off, rows,
                          static_cast<uchar4*>(d_out_rgba), static_cast<float*>(d_out_radiance), s, stats != nullptr);
     if (rc) return rc;

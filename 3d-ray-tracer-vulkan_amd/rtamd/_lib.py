@@ -82,6 +82,14 @@ def lib() -> C.CDLL:
             if not os.path.exists(LIB_PATH):
                 raise RtError(-3, f"{LIB_PATH} is missing: run __graft_entry__.build() "
                                   "(there is no non-HIP fallback)")
+            # torch bundles its own libamdhip64.so.7 (same soname as ROCm's).  The
+            # first one loaded serves the whole process, and torch only works
+            # with its own; load it first so torch tensors and this library
+            # share one HIP runtime.
+            try:
+                import torch  # noqa: F401
+            except ImportError:
+                pass
             L = C.CDLL(LIB_PATH)
             vp, sz, i32, u64, dp, fp = C.c_void_p, C.c_size_t, C.c_int, C.c_uint64, C.POINTER(C.c_double), C.POINTER(C.c_float)
             sig = {

@@ -107,8 +107,10 @@ int rt_render(rt_ctx* ctx, const rt_camera_ubo* cam,
  * rectangle [x0, x0+tile_w) x [y0, y0+tile_h) of a width x height frame of
  * device 0 of ctx into DEVICE buffers d_out_rgba (tile_w*tile_h*4 B, may be
  * null) and d_out_radiance (tile_w*tile_h*3 floats, may be null), enqueued on
- * `stream` (a hipStream_t; null = the context's own stream).  Asynchronous
- * unless stats is non-null, in which case it waits and fills stats. */
+ * `stream` (a hipStream_t of the same HIP runtime; NULL = the null stream).
+ * Asynchronous unless stats is non-null, in which case it waits and fills
+ * stats.  A process that also uses PyTorch must load torch's HIP runtime
+ * first (rtamd/_lib.py does), so that one runtime owns the device pointers. */
 int rt_render_tile_device(rt_ctx* ctx, const rt_camera_ubo* cam,
                           int width, int height, int max_bounces,
                           int x0, int y0, int tile_w, int tile_h,

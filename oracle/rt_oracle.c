@@ -197,7 +197,7 @@ static unsigned char unorm8(float c) {
 /* One invocation of main() (:158-237).  Returns 0, or -1 on stack overflow or
  * an out-of-range index (where the reference reads out of bounds). */
 static int shade_pixel(const scene* s, const orc_camera* cam, int W, int H, int max_bounces,
-                       int px, int py, float out_rgb[3], orc_counts* cnt) {
+                       int px, int py, float out_rgb[3], orc_counts* cnt, uint32_t* prof) {
     uint32_t seed = (uint32_t)(py * W + px);                                   /* :164 */
     float u = ((float)px + orc_random_float(&seed)) / (float)W;                /* :167 */
     float v = ((float)(H - 1 - py) + orc_random_float(&seed)) / (float)H;      /* :168 */
@@ -213,6 +213,7 @@ static int shade_pixel(const scene* s, const orc_camera* cam, int W, int H, int 
     vec3 attenuation = v3(1.0f, 1.0f, 1.0f);
     for (int b = 0; b < max_bounces; ++b) {                                    /* :179 */
         cnt->segments++;
+        const uint64_t nv0 = cnt->node_visits, tt0 = cnt->tri_tests;
         float closest_t = T_MAX;
         int hit_triangle_index = -1;
         vec3 hit_normal = v3(0.0f, 0.0f, 0.0f);
@@ -247,6 +248,7 @@ static int shade_pixel(const scene* s, const orc_camera* cam, int W, int H, int 
                 }
             }
         }
+        if (prof) prof[b] = (uint32_t)(cnt->node_visits - nv0) | ((uint32_t)(cnt->tri_tests - tt0) << 20);
         if (hit_triangle_index != -1) {                                        /* :212 */
             vec3 hit_pos = ray_at(r, closest_t);
             vec3 mat_att;
@@ -277,6 +279,18 @@ int orc_render(const void* vertices, size_t vertex_bytes,
                const orc_camera* cam, int width, int height, int max_bounces,
                int x0, int y0, int tile_w, int tile_h, int row_step,
                uint8_t* out_rgba, float* out_radiance, orc_counts* counts, int n_threads) {
+    return orc_render_profile(vertices, vertex_bytes, materials, material_bytes, bvh_nodes, bvh_bytes, cam,
+                              width, height, max_bounces, x0, y0, tile_w, tile_h, row_step, out_rgba,
+                              out_radiance, counts, n_threads, NULL);
+}
+
+int orc_render_profile(const void* vertices, size_t vertex_bytes,
+               const void* materials, size_t material_bytes,
+               const void* bvh_nodes, size_t bvh_bytes,
+               const orc_camera* cam, int width, int height, int max_bounces,
+               int x0, int y0, int tile_w, int tile_h, int row_step,
+               uint8_t* out_rgba, float* out_radiance, orc_counts* counts, int n_threads,
+               uint32_t* profile) {
     if (!cam || width < 1 || height < 1 || max_bounces < 1 || tile_w < 1 || tile_h < 1 ||
         x0 < 0 || y0 < 0 || x0 + tile_w > width || y0 + tile_h > height || row_step < 1)
         return -2;
@@ -299,7 +313,9 @@ int orc_render(const void* vertices, size_t vertex_bytes,
         orc_counts c = {0, 0, 0, 0, 0};
         for (int lx = 0; lx < tile_w; ++lx) {
             float rgb[3];
-            if (shade_pixel(&s, cam, width, height, max_bounces, x0 + lx, y0 + ly, rgb, &c)) {
+            uint32_t* prof = profile ? profile + ((size_t)rr * (size_t)tile_w + (size_t)lx) * (size_t)max_bounces : NULL;
+            if (prof) memset(prof, 0, sizeof(uint32_t) * (size_t)max_bounces);
+            if (shade_pixel(&s, cam, width, height, max_bounces, x0 + lx, y0 + ly, rgb, &c, prof)) {
                 err |= 1;
                 rgb[0] = rgb[1] = rgb[2] = 0.0f;
             }

@@ -35,4 +35,14 @@ int orc_render(const void* vertices, size_t vertex_bytes,
                const orc_camera* cam, int width, int height, int max_bounces,
                int x0, int y0, int tile_w, int tile_h, int row_step,
                uint8_t* out_rgba, float* out_radiance, orc_counts* counts, int n_threads);
+/* Same, plus profile[pixel * max_bounces + b] = node visits (low 20 bits) |
+ * triangle tests << 20 of bounce b (0 where the path ended earlier).
+ * An analysis aid for kernel design (tools/simd_model.py). */
+int orc_render_profile(const void* vertices, size_t vertex_bytes,
+                       const void* materials, size_t material_bytes,
+                       const void* bvh_nodes, size_t bvh_bytes,
+                       const orc_camera* cam, int width, int height, int max_bounces,
+                       int x0, int y0, int tile_w, int tile_h, int row_step,
+                       uint8_t* out_rgba, float* out_radiance, orc_counts* counts, int n_threads,
+                       uint32_t* profile);
 #endif

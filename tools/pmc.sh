@@ -1,0 +1,30 @@
+#!/bin/bash
+# PMC passes over a short bench run (one rocprofv3 process per counter set;
+# --pmc is never combined with other tracing).  Usage: tools/pmc.sh TAG
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+TAG=${1:-pmc}
+OUT=gpurun_out/$TAG
+mkdir -p "$OUT"
+rocprofv3 -L > "$OUT/counters_list.txt" 2>&1 || true
+pass() {  # pass NAME COUNTERS...
+  local name=$1; shift
+  echo "$(date +%T) pass $name: $*" >> "$OUT/status.txt"
+  timeout -k 10 300 rocprofv3 --pmc "$@" --kernel-include-regex trace_kernel --output-format csv \
+      -d "$OUT/$name" -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline > "$OUT/$name.log" 2>&1
+  local rc=$?
+  echo "$(date +%T) pass $name rc=$rc" >> "$OUT/status.txt"
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
+}
+PASSES=${PMC_PASSES:-"A B C D E"}
+for p in $PASSES; do
+  case $p in
+    A) pass A SQ_WAVES SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU ;;
+    B) pass B TCP_TOTAL_CACHE_ACCESSES_sum TCP_TCC_READ_REQ_sum TCC_HIT_sum TCC_MISS_sum ;;
+    C) pass C FETCH_SIZE ;;
+    D) pass D SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_LDS GRBM_GUI_ACTIVE TA_BUSY_avr ;;
+    E) pass E TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum TCC_REQ_sum ;;
+  esac
+done
+echo "$(date +%T) pmc done" >> "$OUT/status.txt"
