@@ -50,6 +50,9 @@ struct CamF {                   // the four vec3 of the CameraUBO
     float vx, vy, vz;
 };
 
+constexpr int kKernelSimple = 0;       // one lane per pixel, 8x8 pixels per wave
+constexpr int kKernelPersistent = 1;   // persistent waves + tile queue + deferred shading
+
 struct TraceArgs {
     DevScene scene;
     CamF     cam;
@@ -63,6 +66,10 @@ struct TraceArgs {
     uchar4*  out_rgba;          // tw*th, nullable
     float*   out_rad;           // tw*th*3, nullable
     Counters* counters;         // nullable
+    int      kernel;            // kKernelSimple / kKernelPersistent
+    unsigned* queue;            // persistent: zeroed work counter for this launch
+    int      shade_min;         // persistent: shade once this many lanes of a wave are ready
+    int      grid_blocks;       // persistent: blocks of 256 threads
 };
 
 // Host-side compact-scene build from the reference records; validates the
@@ -81,6 +88,7 @@ void free_host_scene(HostScene* s);
 
 // Kernel launcher (rt_trace.hip).
 hipError_t launch_trace(const TraceArgs& a, hipStream_t stream);
+int persistent_blocks_per_cu();   // occupancy of trace_persistent (current device), capped at 8
 
 void set_error(const char* fmt, ...);
 

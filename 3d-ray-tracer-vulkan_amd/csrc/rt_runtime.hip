@@ -183,10 +183,19 @@ struct PerDevice {
     uchar4*      d_rgba = nullptr;
     float*       d_rad = nullptr;
     size_t       out_cap = 0;      // pixels
+    unsigned*    d_queue = nullptr; // ring of kQueueSlots work counters (persistent kernel)
+    unsigned     queue_slot = 0;
+    int          n_cu = 0;
+    int          blocks_per_cu = 1;
 };
+
+static constexpr unsigned kQueueSlots = 64;
 
 struct rt_ctx {
     std::vector<PerDevice> dev;
+    int  kernel = kKernelPersistent;
+    int  shade_min = 16;
+    int  blocks_per_cu = 0;        // 0 = from the occupancy query
     bool has_scene = false;
     int  n_nodes = 0, n_tris = 0, max_depth = 0;
 };
@@ -196,6 +205,17 @@ static void free_scene(PerDevice& p) {
     if (p.scene.tris) (void)hipFree(p.scene.tris);
     if (p.scene.mats) (void)hipFree(p.scene.mats);
     p.scene = DevScene{};
+}
+
+static void set_schedule(const rt_ctx* ctx, PerDevice& p, TraceArgs& a) {
+    a.kernel = ctx->kernel;
+    a.shade_min = ctx->shade_min;
+    a.queue = p.d_queue + (p.queue_slot++ % kQueueSlots);
+    const int bpc = ctx->blocks_per_cu > 0 ? ctx->blocks_per_cu : p.blocks_per_cu;
+    a.grid_blocks = std::max(1, p.n_cu * bpc);
+    // never more waves than 8x8 pixel tiles
+    const int tiles = ((a.tw + 7) / 8) * ((a.th + 7) / 8);
+    a.grid_blocks = std::min(a.grid_blocks, std::max(1, (tiles + 3) / 4));
 }
 
 static CamF cam_from_ubo(const rt_camera_ubo* c) {
@@ -224,6 +244,9 @@ int rt_create(const int* device_ids, int n_devices, rt_ctx** out) {
     }
     rt_ctx* ctx = new (std::nothrow) rt_ctx;
     if (!ctx) { set_error("rt_create: out of memory"); return RT_ERR_OOM; }
+    if (const char* k = std::getenv("RTAMD_KERNEL")) ctx->kernel = std::strcmp(k, "simple") == 0 ? kKernelSimple : kKernelPersistent;
+    if (const char* v = std::getenv("RTAMD_SHADE_MIN")) ctx->shade_min = std::max(1, std::min(64, std::atoi(v)));
+    if (const char* v = std::getenv("RTAMD_BLOCKS_PER_CU")) ctx->blocks_per_cu = std::max(0, std::min(32, std::atoi(v)));
     for (int k = 0; k < n_devices; ++k) {
         const int d = device_ids[k];
         if (d < 0 || d >= count) {
@@ -244,6 +267,9 @@ int rt_create(const int* device_ids, int n_devices, rt_ctx** out) {
         if (e == hipSuccess) e = hipEventCreate(&p.ev0);
         if (e == hipSuccess) e = hipEventCreate(&p.ev1);
         if (e == hipSuccess) e = hipMalloc(&p.d_counters, sizeof(Counters));
+        if (e == hipSuccess) e = hipMalloc(&p.d_queue, sizeof(unsigned) * kQueueSlots);
+        p.n_cu = prop.multiProcessorCount;
+        p.blocks_per_cu = persistent_blocks_per_cu();
         ctx->dev.push_back(p);
         if (e != hipSuccess) {
             set_error("rt_create: HIP setup on device %d failed: %s", d, hipGetErrorString(e));
@@ -262,6 +288,7 @@ int rt_destroy(rt_ctx* ctx) {
         if (p.stream) (void)hipStreamSynchronize(p.stream);
         free_scene(p);
         if (p.d_counters) (void)hipFree(p.d_counters);
+        if (p.d_queue) (void)hipFree(p.d_queue);
         if (p.d_rgba) (void)hipFree(p.d_rgba);
         if (p.d_rad) (void)hipFree(p.d_rad);
         if (p.ev0) (void)hipEventDestroy(p.ev0);
@@ -375,6 +402,7 @@ int rt_render_tile_device(rt_ctx* ctx, const rt_camera_ubo* cam, int width, int 
     a.out_rgba = static_cast<uchar4*>(d_out_rgba);
     a.out_rad = static_cast<float*>(d_out_radiance);
     a.counters = nullptr;
+    set_schedule(ctx, p, a);
     if (stats) {
         a.counters = p.d_counters;
         RT_HIP_CHECK(hipMemsetAsync(p.d_counters, 0, sizeof(Counters), s));
@@ -408,7 +436,7 @@ int rt_band_rows(int height, int band_h, int band_stride, int band_off) {
     return rows;
 }
 
-static int render_bands_on(PerDevice& p, const rt_camera_ubo* cam, int width, int height, int max_bounces,
+static int render_bands_on(const rt_ctx* ctx, PerDevice& p, const rt_camera_ubo* cam, int width, int height, int max_bounces,
                            int band_h, int band_stride, int band_off, int rows,
                            uchar4* d_rgba, float* d_rad, hipStream_t s, bool count) {
     TraceArgs a;
@@ -420,6 +448,7 @@ static int render_bands_on(PerDevice& p, const rt_camera_ubo* cam, int width, in
     a.out_rgba = d_rgba;
     a.out_rad = d_rad;
     a.counters = count ? p.d_counters : nullptr;
+    set_schedule(ctx, p, a);
     if (count) RT_HIP_CHECK(hipMemsetAsync(p.d_counters, 0, sizeof(Counters), s));
     RT_HIP_CHECK(hipEventRecord(p.ev0, s));
     RT_HIP_CHECK(launch_trace(a, s));
@@ -459,7 +488,7 @@ int rt_render_bands_device(rt_ctx* ctx, const rt_camera_ubo* cam, int width, int
     PerDevice& p = ctx->dev[0];
     RT_HIP_CHECK(hipSetDevice(p.device));
     hipStream_t s = static_cast<hipStream_t>(stream);   // NULL = the null stream
-    rc = render_bands_on(p, cam, width, height, max_bounces, band_h, band_stride, band_off, rows,
+    rc = render_bands_on(ctx, p, cam, width, height, max_bounces, band_h, band_stride, band_off, rows,
                          static_cast<uchar4*>(d_out_rgba), static_cast<float*>(d_out_radiance), s, stats != nullptr);
     if (rc) return rc;
     if (stats) {
@@ -487,7 +516,7 @@ int rt_render(rt_ctx* ctx, const rt_camera_ubo* cam, int width, int height, int 
         RT_HIP_CHECK(hipSetDevice(p.device));
         rc = ensure_out(p, (size_t)width * rows[k], out_radiance != nullptr);
         if (rc) return rc;
-        rc = render_bands_on(p, cam, width, height, max_bounces, bh, nd, k, rows[k], p.d_rgba,
+        rc = render_bands_on(ctx, p, cam, width, height, max_bounces, bh, nd, k, rows[k], p.d_rgba,
                              out_radiance ? p.d_rad : nullptr, p.stream, stats != nullptr);
         if (rc) return rc;
     }
@@ -524,6 +553,31 @@ int rt_render(rt_ctx* ctx, const rt_camera_ubo* cam, int width, int height, int 
             if (rc) return rc;
         }
     }
+    return RT_OK;
+}
+
+int rt_set_option(rt_ctx* ctx, const char* name, int64_t value) {
+    if (!ctx || !name) { set_error("rt_set_option: null argument"); return RT_ERR_INVALID_ARG; }
+    if (std::strcmp(name, "kernel") == 0 && (value == kKernelSimple || value == kKernelPersistent)) {
+        ctx->kernel = (int)value;
+    } else if (std::strcmp(name, "shade_min") == 0 && value >= 1 && value <= 64) {
+        ctx->shade_min = (int)value;
+    } else if (std::strcmp(name, "blocks_per_cu") == 0 && value >= 0 && value <= 32) {
+        ctx->blocks_per_cu = (int)value;
+    } else {
+        set_error("rt_set_option: unknown option or bad value: %s = %lld", name, (long long)value);
+        return RT_ERR_INVALID_ARG;
+    }
+    return RT_OK;
+}
+
+int rt_get_option(rt_ctx* ctx, const char* name, int64_t* value) {
+    if (!ctx || !name || !value) { set_error("rt_get_option: null argument"); return RT_ERR_INVALID_ARG; }
+    if (std::strcmp(name, "kernel") == 0) *value = ctx->kernel;
+    else if (std::strcmp(name, "shade_min") == 0) *value = ctx->shade_min;
+    else if (std::strcmp(name, "blocks_per_cu") == 0)
+        *value = ctx->blocks_per_cu > 0 ? ctx->blocks_per_cu : (ctx->dev.empty() ? 0 : ctx->dev[0].blocks_per_cu);
+    else { set_error("rt_get_option: unknown option %s", name); return RT_ERR_INVALID_ARG; }
     return RT_OK;
 }
 

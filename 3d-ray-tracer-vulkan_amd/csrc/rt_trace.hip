@@ -1,4 +1,4 @@
-// rt_trace.hip — gfx950 path-trace kernel for the reference's per-pixel
+// rt_trace.hip — gfx950 path-trace kernels for the reference's per-pixel
 // render path (shaders/compute_dynamic_ray.comp, dispatched by
 // VulkanEngine.recordComputeCommands, VulkanEngine.java:437-515).
 //
@@ -10,7 +10,18 @@
 //
 // Traversal: stackless preorder walk over the compact 32-B nodes
 // (rt_internal.h), which replays the reference's stack DFS
-// (compute_dynamic_ray.comp:185-210) node for node.
+// (compute_dynamic_ray.comp:185-210) node for node: next = hit ? i+1 : skip(i).
+//
+// Two schedules of the same per-pixel work:
+//   trace_simple      one lane = one pixel for its whole path (the
+//                     reference's dispatch shape, 8x8 pixels per wave).
+//   trace_persistent  persistent waves; a lane whose path ends pulls the next
+//                     pixel from a global queue of 8x8 tiles, and the shading
+//                     block (scatter / sky / pixel write) runs only once enough
+//                     lanes of the wave have finished a segment, so traversal
+//                     steps run with most lanes busy.  Results are identical:
+//                     every pixel's path is independent (its RNG seed is its
+//                     pixel index, :164) and is computed with the same ops.
 #include "rt_internal.h"
 
 namespace rtamd {
@@ -66,173 +77,321 @@ __device__ __forceinline__ uint8_t unorm8(float c) {
     return c > 0.0f ? (c < 1.0f ? (uint8_t)__builtin_rintf(c * 255.0f) : (uint8_t)255) : (uint8_t)0;
 }
 
+// Frame row of local row ly (rt_internal.h, TraceArgs band mapping).
+__device__ __forceinline__ int frame_row(const TraceArgs& a, int ly) {
+    return a.y0 + ((ly / a.band_h) * a.band_stride + a.band_off) * a.band_h + ly % a.band_h;
+}
+
+// Seed, AA jitter and primary ray (:164-173).
+__device__ __forceinline__ void primary_ray(const TraceArgs& a, int x, int y, uint32_t& seed, V3& o, V3& d) {
+    seed = (uint32_t)(y * a.width + x);
+    const float u = ((float)x + rnd(seed)) / (float)a.width;
+    const float v = ((float)(a.height - 1 - y) + rnd(seed)) / (float)a.height;
+    const V3 cam_o = {a.cam.ox, a.cam.oy, a.cam.oz};
+    const V3 cam_l = {a.cam.lx, a.cam.ly, a.cam.lz};
+    const V3 cam_h = {a.cam.hx, a.cam.hy, a.cam.hz};
+    const V3 cam_v = {a.cam.vx, a.cam.vy, a.cam.vz};
+    o = cam_o;
+    d = vnormalize(vsub(vadd(vadd(cam_l, vscale(cam_h, u)), vscale(cam_v, v)), cam_o));
+}
+
+// One node of the walk: hit_aabb (:88-103) and, at a leaf whose box is hit,
+// hit_triangle (:105-129).  Returns the next node index.
 template <bool COUNT>
-__global__ __launch_bounds__(256) void trace_kernel(TraceArgs a) {
+__device__ __forceinline__ int node_step(const float4* __restrict__ nodes, const float4* __restrict__ tris,
+                                         int i, V3 o, V3 d, V3 inv, float& closest, int& hit,
+                                         unsigned long long& c_node, unsigned long long& c_tri) {
+    const float4 A = nodes[2 * i];
+    const float4 B = nodes[2 * i + 1];
+    if (COUNT) ++c_node;
+    const float t0x = (A.x - o.x) * inv.x, t1x = (B.x - o.x) * inv.x;
+    const float t0y = (A.y - o.y) * inv.y, t1y = (B.y - o.y) * inv.y;
+    const float t0z = (A.z - o.z) * inv.z, t1z = (B.z - o.z) * inv.z;
+    const float te = fmaxf(fmaxf(fminf(t0x, t1x), fminf(t0y, t1y)), fminf(t0z, t1z));
+    const float tx = fminf(fminf(fmaxf(t0x, t1x), fmaxf(t0y, t1y)), fmaxf(t0z, t1z));
+    const bool hb = tx > te && tx > kTMin && te < closest;
+    const int leaf = __float_as_int(B.w);
+    if (hb && leaf >= 0) {
+        if (COUNT) ++c_tri;
+        const float4 P0 = tris[3 * leaf + 0];
+        const float4 P1 = tris[3 * leaf + 1];
+        const float4 P2 = tris[3 * leaf + 2];
+        const V3 v0 = {P0.x, P0.y, P0.z};
+        const V3 e1 = {P1.x, P1.y, P1.z};
+        const V3 e2 = {P2.x, P2.y, P2.z};
+        const V3 pv = vcross(d, e2);
+        const float det = vdot(e1, pv);
+        if (!(det > -0.00001f && det < 0.00001f)) {
+            const float inv_det = 1.0f / det;
+            const V3 s = vsub(o, v0);
+            const float uu = inv_det * vdot(s, pv);
+            if (!(uu < 0.0f || uu > 1.0f)) {
+                const V3 q = vcross(s, e1);
+                const float vv = inv_det * vdot(d, q);
+                if (!(vv < 0.0f || (uu + vv) > 1.0f)) {
+                    const float t = inv_det * vdot(e2, q);
+                    if (t > kTMin && t < closest) {
+                        closest = t;
+                        hit = leaf;
+                    }
+                }
+            }
+        }
+    }
+    return hb ? i + 1 : __float_as_int(A.w);
+}
+
+// The hit normal of :124-125: normalize(cross(e1,e2)) (precomputed per
+// triangle, rt_internal.h), flipped to face against d.
+__device__ __forceinline__ V3 hit_normal(const float4* __restrict__ tris, int hit, V3 d) {
+    V3 n = {tris[3 * hit + 0].w, tris[3 * hit + 1].w, tris[3 * hit + 2].w};
+    if (vdot(d, n) > 0.0f) n = {-n.x, -n.y, -n.z};
+    return n;
+}
+
+// scatter (:132-154).  Returns true and the new direction / albedo on scatter.
+__device__ __forceinline__ bool scatter(float4 M, V3 d, V3 n, uint32_t& seed, V3& nd) {
+    if (M.w == 0.0f) {                                                    // Lambertian :137-143
+        const V3 ru = vnormalize(rnd_in_sphere(seed));
+        V3 sd = vadd(n, ru);
+        if (sqrtf(vdot(sd, sd)) < 0.0001f) sd = n;
+        nd = vnormalize(sd);
+        return true;
+    }
+    if (M.w == 1.0f || M.w == 2.0f) {                                     // metal :145-151
+        const float fuzz = (M.w == 2.0f) ? 0.3f : 0.0f;
+        const V3 di = vnormalize(d);
+        const float k = 2.0f * vdot(n, di);
+        const V3 refl = vsub(di, vscale(n, k));                           // reflect()
+        const V3 p = rnd_in_sphere(seed);
+        nd = vnormalize(vadd(refl, vscale(p, fuzz)));
+        return vdot(nd, n) > 0.0f;
+    }
+    nd = d;
+    return false;                                                         // :153
+}
+
+__device__ __forceinline__ V3 sky_color(V3 d) {                          // getSkyColor :81-85
+    const V3 ud = vnormalize(d);
+    const float t = 0.5f * (ud.y + 1.0f);
+    const float omt = 1.0f - t;
+    return {omt * 1.0f + t * 0.5f, omt * 1.0f + t * 0.7f, omt * 1.0f + t * 1.0f};
+}
+
+__device__ __forceinline__ void write_pixel(const TraceArgs& a, int lx, int ly, V3 fin) {
+    const V3 g = {sqrtf(fin.x), sqrtf(fin.y), sqrtf(fin.z)};              // :235
+    const size_t p = (size_t)ly * (size_t)a.tw + (size_t)lx;
+    if (a.out_rgba) a.out_rgba[p] = make_uchar4(unorm8(g.x), unorm8(g.y), unorm8(g.z), 255);
+    if (a.out_rad) {
+        a.out_rad[3 * p + 0] = g.x;
+        a.out_rad[3 * p + 1] = g.y;
+        a.out_rad[3 * p + 2] = g.z;
+    }
+}
+
+__device__ __forceinline__ void flush_counters(Counters* c, unsigned long long s, unsigned long long n,
+                                               unsigned long long t, unsigned long long m) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        s += __shfl_xor(s, off);
+        n += __shfl_xor(n, off);
+        t += __shfl_xor(t, off);
+        m += __shfl_xor(m, off);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        atomicAdd(&c->segments, s);
+        atomicAdd(&c->node_visits, n);
+        atomicAdd(&c->tri_tests, t);
+        atomicAdd(&c->mat_reads, m);
+    }
+}
+
+// ------------------------------------------------------------ simple kernel --
+
+template <bool COUNT>
+__global__ __launch_bounds__(256) void trace_simple(TraceArgs a) {
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
     // One wave = one 8x8 pixel tile (the reference's local_size 8x8x1,
     // compute_dynamic_ray.comp:157); a 256-thread block = 16x16 pixels.
     const int lx = blockIdx.x * 16 + (wave & 1) * 8 + (lane & 7);
     const int ly = blockIdx.y * 16 + (wave >> 1) * 8 + (lane >> 3);
-    const bool active = lx < a.tw && ly < a.th;
-
     unsigned long long c_seg = 0, c_node = 0, c_tri = 0, c_mat = 0;
 
-    if (active) {
+    if (lx < a.tw && ly < a.th) {
         const int x = a.x0 + lx;
-        const int y = a.y0 + ((ly / a.band_h) * a.band_stride + a.band_off) * a.band_h + ly % a.band_h;
-        const float4* __restrict__ nodes = a.scene.nodes;
-        const float4* __restrict__ tris  = a.scene.tris;
-        const float4* __restrict__ mats  = a.scene.mats;
-        const int end = a.scene.end;
-
-        uint32_t seed = (uint32_t)(y * a.width + x);                                 // :164
-        const float u = ((float)x + rnd(seed)) / (float)a.width;                     // :167
-        const float v = ((float)(a.height - 1 - y) + rnd(seed)) / (float)a.height;   // :168
-
-        const V3 cam_o = {a.cam.ox, a.cam.oy, a.cam.oz};
-        const V3 cam_l = {a.cam.lx, a.cam.ly, a.cam.lz};
-        const V3 cam_h = {a.cam.hx, a.cam.hy, a.cam.hz};
-        const V3 cam_v = {a.cam.vx, a.cam.vy, a.cam.vz};
-        V3 o = cam_o;
-        V3 d = vnormalize(vsub(vadd(vadd(cam_l, vscale(cam_h, u)), vscale(cam_v, v)), cam_o));  // :173
-
+        const int y = frame_row(a, ly);
+        uint32_t seed;
+        V3 o, d;
+        primary_ray(a, x, y, seed, o, d);
         V3 fin = {0.0f, 0.0f, 0.0f};
         V3 att = {1.0f, 1.0f, 1.0f};
-
-        for (int b = 0; b < a.max_bounces; ++b) {                                     // :179
+        for (int b = 0; b < a.max_bounces; ++b) {                         // :179
             if (COUNT) ++c_seg;
             float closest = kTMax;
-            int   hit = -1;
-            V3    n = {0.0f, 0.0f, 0.0f};
-            const V3 inv = {1.0f / d.x, 1.0f / d.y, 1.0f / d.z};                     // :89
-
+            int hit = -1;
+            const V3 inv = {1.0f / d.x, 1.0f / d.y, 1.0f / d.z};          // :89
             int i = 0;
-            while (i < end) {
-                const float4 A = nodes[2 * i];
-                const float4 B = nodes[2 * i + 1];
-                if (COUNT) ++c_node;
-                // hit_aabb (:88-103)
-                const float t0x = (A.x - o.x) * inv.x, t1x = (B.x - o.x) * inv.x;
-                const float t0y = (A.y - o.y) * inv.y, t1y = (B.y - o.y) * inv.y;
-                const float t0z = (A.z - o.z) * inv.z, t1z = (B.z - o.z) * inv.z;
-                const float te = fmaxf(fmaxf(fminf(t0x, t1x), fminf(t0y, t1y)), fminf(t0z, t1z));
-                const float tx = fminf(fminf(fmaxf(t0x, t1x), fmaxf(t0y, t1y)), fmaxf(t0z, t1z));
-                const bool hb = tx > te && tx > kTMin && te < closest;
-                const int leaf = __float_as_int(B.w);
-                if (hb && leaf >= 0) {
-                    if (COUNT) ++c_tri;
-                    // hit_triangle (:105-129)
-                    const float4 P0 = tris[3 * leaf + 0];
-                    const float4 P1 = tris[3 * leaf + 1];
-                    const float4 P2 = tris[3 * leaf + 2];
-                    const V3 v0 = {P0.x, P0.y, P0.z};
-                    const V3 e1 = {P1.x, P1.y, P1.z};
-                    const V3 e2 = {P2.x, P2.y, P2.z};
-                    const V3 pv = vcross(d, e2);
-                    const float det = vdot(e1, pv);
-                    if (!(det > -0.00001f && det < 0.00001f)) {
-                        const float inv_det = 1.0f / det;
-                        const V3 s = vsub(o, v0);
-                        const float uu = inv_det * vdot(s, pv);
-                        if (!(uu < 0.0f || uu > 1.0f)) {
-                            const V3 q = vcross(s, e1);
-                            const float vv = inv_det * vdot(d, q);
-                            if (!(vv < 0.0f || (uu + vv) > 1.0f)) {
-                                const float t = inv_det * vdot(e2, q);
-                                if (t > kTMin && t < closest) {
-                                    closest = t;
-                                    hit = leaf;
-                                    n = {P0.w, P1.w, P2.w};
-                                    if (vdot(d, n) > 0.0f) n = {-n.x, -n.y, -n.z};
-                                }
-                            }
-                        }
-                    }
-                }
-                i = hb ? i + 1 : __float_as_int(A.w);
-            }
-
-            if (hit >= 0) {                                                          // :212
+            while (i < a.scene.end)
+                i = node_step<COUNT>(a.scene.nodes, a.scene.tris, i, o, d, inv, closest, hit, c_node, c_tri);
+            if (hit >= 0) {                                               // :212
                 if (COUNT) ++c_mat;
-                const V3 hp = vadd(o, vscale(d, closest));                             // ray_at :77-79
-                const float4 M = mats[hit];
-                bool scattered;
+                const V3 n = hit_normal(a.scene.tris, hit, d);
+                const V3 hp = vadd(o, vscale(d, closest));                  // ray_at :77-79
+                const float4 M = a.scene.mats[hit];
                 V3 nd;
-                if (M.w == 0.0f) {                                                   // Lambertian :137-143
-                    const V3 ru = vnormalize(rnd_in_sphere(seed));
-                    V3 sd = vadd(n, ru);
-                    if (sqrtf(vdot(sd, sd)) < 0.0001f) sd = n;
-                    nd = vnormalize(sd);
-                    scattered = true;
-                } else if (M.w == 1.0f || M.w == 2.0f) {                             // metal :145-151
-                    const float fuzz = (M.w == 2.0f) ? 0.3f : 0.0f;
-                    const V3 di = vnormalize(d);
-                    const float k = 2.0f * vdot(n, di);
-                    const V3 refl = vsub(di, vscale(n, k));                          // reflect()
-                    const V3 p = rnd_in_sphere(seed);
-                    nd = vnormalize(vadd(refl, vscale(p, fuzz)));
-                    scattered = vdot(nd, n) > 0.0f;
-                } else {
-                    scattered = false;                                               // :153
-                    nd = d;
+                if (!scatter(M, d, n, seed, nd)) break;                   // attenuation = 0: black
+                att = vmul(att, V3{M.x, M.y, M.z});
+                o = hp;
+                d = nd;
+            } else {
+                fin = vmul(att, sky_color(d));
+                break;
+            }
+            if (b == a.max_bounces - 1) fin = {0.0f, 0.0f, 0.0f};        // :229-231
+        }
+        write_pixel(a, lx, ly, fin);
+    }
+    if (COUNT) flush_counters(a.counters, c_seg, c_node, c_tri, c_mat);
+}
+
+// -------------------------------------------------------- persistent kernel --
+
+constexpr int kIdle = 0, kTrace = 1, kReady = 2;
+
+__device__ __forceinline__ int lanes_below(uint64_t mask) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
+}
+
+template <bool COUNT>
+__global__ __launch_bounds__(256) void trace_persistent(TraceArgs a) {
+    const int lane = threadIdx.x & 63;
+    const int tiles_x = (a.tw + 7) >> 3;
+    const int n_slots = tiles_x * ((a.th + 7) >> 3) * 64;   // pixel slots, 8x8 tiles in row-major tile order
+    const float4* __restrict__ nodes = a.scene.nodes;
+    const float4* __restrict__ tris = a.scene.tris;
+    const int end = a.scene.end;
+    const int shade_min = a.shade_min;
+
+    unsigned long long c_seg = 0, c_node = 0, c_tri = 0, c_mat = 0;
+    int pool_next = 0, pool_end = 0;     // wave-uniform: this wave's unclaimed slots
+    bool exhausted = false;              // wave-uniform: the global queue is empty
+
+    int mode = kIdle;
+    int lx = 0, ly = 0, b = 0, node = 0, hit = -1;
+    uint32_t seed = 0;
+    float closest = kTMax;
+    V3 o = {0.f, 0.f, 0.f}, d = {0.f, 0.f, 1.f}, inv = {0.f, 0.f, 1.f}, att = {1.f, 1.f, 1.f};
+
+    for (;;) {
+        // ---- refill idle lanes with new pixels (consecutive slots = one 8x8 tile)
+        uint64_t idle = __ballot(mode == kIdle);
+        while (idle != 0 && !exhausted) {
+            if (pool_next >= pool_end) {
+                int base = 0;
+                if (lane == 0) base = (int)atomicAdd(a.queue, 64u);
+                base = __shfl(base, 0);
+                if (base >= n_slots) { exhausted = true; break; }
+                pool_next = base;
+                pool_end = base + 64;
+            }
+            const int avail = pool_end - pool_next;
+            const int rank = lanes_below(idle);
+            if (mode == kIdle && rank < avail) {
+                const int slot = pool_next + rank;
+                const int tile = slot >> 6, w = slot & 63;
+                lx = (tile % tiles_x) * 8 + (w & 7);
+                ly = (tile / tiles_x) * 8 + (w >> 3);
+                if (lx < a.tw && ly < a.th) {
+                    const int x = a.x0 + lx, y = frame_row(a, ly);
+                    primary_ray(a, x, y, seed, o, d);
+                    att = {1.0f, 1.0f, 1.0f};
+                    b = 0;
+                    inv = {1.0f / d.x, 1.0f / d.y, 1.0f / d.z};
+                    closest = kTMax;
+                    hit = -1;
+                    node = 0;
+                    mode = kTrace;
+                    if (COUNT) ++c_seg;
                 }
-                if (scattered) {
+            }
+            pool_next += min(__popcll(idle), avail);
+            idle = __ballot(mode == kIdle);
+        }
+
+        // ---- traversal: step until enough lanes wait to be shaded
+        for (;;) {
+            if (mode == kTrace) {
+                node = node_step<COUNT>(nodes, tris, node, o, d, inv, closest, hit, c_node, c_tri);
+                if (node >= end) mode = kReady;
+            }
+            const uint64_t trace = __ballot(mode == kTrace);
+            if (trace == 0 || __popcll(__ballot(mode == kReady)) >= shade_min) break;
+        }
+
+        // ---- shading: scatter or sky; next segment, or finish the pixel
+        if (mode == kReady) {
+            bool finish = true;
+            V3 fin = {0.0f, 0.0f, 0.0f};
+            if (hit >= 0) {
+                if (COUNT) ++c_mat;
+                const V3 n = hit_normal(tris, hit, d);
+                const V3 hp = vadd(o, vscale(d, closest));
+                const float4 M = a.scene.mats[hit];
+                V3 nd;
+                if (scatter(M, d, n, seed, nd) && b < a.max_bounces - 1) {
                     att = vmul(att, V3{M.x, M.y, M.z});
                     o = hp;
                     d = nd;
-                } else {
-                    att = {0.0f, 0.0f, 0.0f};
-                    break;
+                    ++b;
+                    inv = {1.0f / d.x, 1.0f / d.y, 1.0f / d.z};
+                    closest = kTMax;
+                    hit = -1;
+                    node = 0;
+                    mode = kTrace;
+                    finish = false;
+                    if (COUNT) ++c_seg;
                 }
+                // absorbed (:220-222) or scattered on the last bounce (:229-231): black
             } else {
-                // getSkyColor (:81-85)
-                const V3 ud = vnormalize(d);
-                const float t = 0.5f * (ud.y + 1.0f);
-                const float omt = 1.0f - t;
-                const V3 sky = {omt * 1.0f + t * 0.5f, omt * 1.0f + t * 0.7f, omt * 1.0f + t * 1.0f};
-                fin = vmul(att, sky);
-                break;
+                fin = vmul(att, sky_color(d));
             }
-            if (b == a.max_bounces - 1) fin = {0.0f, 0.0f, 0.0f};                   // :229-231
+            if (finish) {
+                write_pixel(a, lx, ly, fin);
+                mode = kIdle;
+            }
         }
-
-        const V3 g = {sqrtf(fin.x), sqrtf(fin.y), sqrtf(fin.z)};                    // :235
-        const size_t p = (size_t)ly * (size_t)a.tw + (size_t)lx;
-        if (a.out_rgba) a.out_rgba[p] = make_uchar4(unorm8(g.x), unorm8(g.y), unorm8(g.z), 255);
-        if (a.out_rad) {
-            a.out_rad[3 * p + 0] = g.x;
-            a.out_rad[3 * p + 1] = g.y;
-            a.out_rad[3 * p + 2] = g.z;
-        }
+        if (exhausted && __ballot(mode != kIdle) == 0) break;
     }
-
-    if (COUNT) {
-#pragma unroll
-        for (int off = 32; off > 0; off >>= 1) {
-            c_seg  += __shfl_xor(c_seg, off);
-            c_node += __shfl_xor(c_node, off);
-            c_tri  += __shfl_xor(c_tri, off);
-            c_mat  += __shfl_xor(c_mat, off);
-        }
-        if (lane == 0) {
-            atomicAdd(&a.counters->segments, c_seg);
-            atomicAdd(&a.counters->node_visits, c_node);
-            atomicAdd(&a.counters->tri_tests, c_tri);
-            atomicAdd(&a.counters->mat_reads, c_mat);
-        }
-    }
+    if (COUNT) flush_counters(a.counters, c_seg, c_node, c_tri, c_mat);
 }
 
 }  // namespace
 
+int persistent_blocks_per_cu() {
+    int n = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, trace_persistent<false>, 256, 0) != hipSuccess || n < 1)
+        n = 1;
+    return n > 8 ? 8 : n;
+}
+
 hipError_t launch_trace(const TraceArgs& a, hipStream_t stream) {
     const dim3 block(256);
-    const dim3 grid((a.tw + 15) / 16, (a.th + 15) / 16);
-    if (a.counters)
-        hipLaunchKernelGGL(trace_kernel<true>, grid, block, 0, stream, a);
-    else
-        hipLaunchKernelGGL(trace_kernel<false>, grid, block, 0, stream, a);
+    if (a.kernel == kKernelPersistent) {
+        const dim3 grid(a.grid_blocks);
+        hipError_t e = hipMemsetAsync(a.queue, 0, sizeof(unsigned), stream);
+        if (e != hipSuccess) return e;
+        if (a.counters)
+            hipLaunchKernelGGL(trace_persistent<true>, grid, block, 0, stream, a);
+        else
+            hipLaunchKernelGGL(trace_persistent<false>, grid, block, 0, stream, a);
+    } else {
+        const dim3 grid((a.tw + 15) / 16, (a.th + 15) / 16);
+        if (a.counters)
+            hipLaunchKernelGGL(trace_simple<true>, grid, block, 0, stream, a);
+        else
+            hipLaunchKernelGGL(trace_simple<false>, grid, block, 0, stream, a);
+    }
     return hipGetLastError();
 }
 

@@ -64,6 +64,16 @@ class Renderer:
         except Exception:
             pass
 
+    def set_option(self, name: str, value: int) -> None:
+        """Schedule options (rt_set_option): "kernel" (0 simple, 1 persistent),
+        "shade_min", "blocks_per_cu".  Results do not depend on them."""
+        check(lib().rt_set_option(self._ctx, name.encode(), int(value)))
+
+    def get_option(self, name: str) -> int:
+        v = C.c_int64()
+        check(lib().rt_get_option(self._ctx, name.encode(), C.byref(v)))
+        return v.value
+
     def upload_scene(self, data: BuiltCpuData) -> None:
         """internalSwapScene (VulkanEngine.java:318-373); deep copy."""
         v = np.ascontiguousarray(data.model_vertex_data, dtype=np.float32)

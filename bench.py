@@ -179,6 +179,7 @@ def main() -> None:
                 "tri_tests_per_segment": round(tri_tests / segments, 4),
                 "partition": "single frame" if world == 1 else f"interleaved {band_h}-row bands, dist.gather to rank 0",
                 "parallelism": f"tile{world}",
+                "schedule": {k: renderer.get_option(k) for k in ("kernel", "shade_min", "blocks_per_cu")},
             },
             "roofline": {
                 "bound": "hbm",

@@ -131,6 +131,19 @@ int rt_render_bands_device(rt_ctx* ctx, const rt_camera_ubo* cam,
 /* Row count of such a band set (-1 for bad arguments).  Pure host code. */
 int rt_band_rows(int height, int band_h, int band_stride, int band_off);
 
+/* Schedule options (no effect on results, which are identical for every
+ * setting):
+ *   "kernel"        0 = one lane per pixel (the reference's dispatch shape),
+ *                   1 = persistent waves with a tile queue (default)
+ *   "shade_min"     persistent: shade once this many lanes of a wave are
+ *                   ready (1..64, default 16)
+ *   "blocks_per_cu" persistent: resident 256-thread blocks per CU (0 = from
+ *                   the occupancy query)
+ * Defaults can also be set with the RTAMD_KERNEL=simple|persistent,
+ * RTAMD_SHADE_MIN and RTAMD_BLOCKS_PER_CU environment variables. */
+int rt_set_option(rt_ctx* ctx, const char* name, int64_t value);
+int rt_get_option(rt_ctx* ctx, const char* name, int64_t* value);
+
 /* Replaces VulkanEngine.cleanup. Null is accepted. */
 int rt_destroy(rt_ctx* ctx);
 

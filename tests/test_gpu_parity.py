@@ -106,6 +106,37 @@ def test_config5_1m_row_subset(renderer):
     _assert_same(rgba, rad, st, *ref)
 
 
+@pytest.mark.parametrize("opts", [
+    {"kernel": 0},
+    {"kernel": 1, "shade_min": 1},
+    {"kernel": 1, "shade_min": 16},
+    {"kernel": 1, "shade_min": 64},
+    {"kernel": 1, "shade_min": 24, "blocks_per_cu": 1},
+])
+def test_schedules_identical(renderer, opts):
+    """Every schedule gives the oracle's frame and counters (config 2 at the
+    reference's 10 bounces, and every 6th row of config 3)."""
+    from rtamd import configs
+    try:
+        for k, v in opts.items():
+            renderer.set_option(k, v)
+        cfg = configs.config2()
+        built, cam, b, rgba, rad, st = _full_frame(renderer, cfg, max_bounces=10)
+        _assert_same(rgba, rad, st, *_oracle(built, cam.ubo_bytes(), cfg.width, cfg.height, 10))
+        cfg = configs.config3()
+        built = cfg.build()
+        cam = cfg.camera()
+        renderer.upload_scene(built)
+        rgba, rad, st = _bands_device(renderer, cam, cfg.width, cfg.height, cfg.max_bounces, 1, 6, 1)
+        ref = _oracle(built, cam.ubo_bytes(), cfg.width, cfg.height, cfg.max_bounces,
+                      tile=(0, 1, cfg.width, cfg.height - 1), row_step=6)
+        _assert_same(rgba, rad, st, *ref)
+    finally:
+        renderer.set_option("kernel", 1)
+        renderer.set_option("shade_min", 16)
+        renderer.set_option("blocks_per_cu", 0)
+
+
 def test_tiles_compose_to_frame(renderer):
     """Tiles and interleaved bands reassemble into the full frame bit for bit
     (the seed depends on global pixel coordinates only, :164)."""

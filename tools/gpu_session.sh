@@ -10,7 +10,7 @@ TAG=${1:-r01}; shift || true
 STEPS=${*:-test smoke bench prof}
 OUT=gpurun_out/$TAG
 mkdir -p "$OUT"
-status() { echo "$(date +%T) $*" | tee -a "$OUT/status.txt"; }
+status() { echo "$(date +%T) $*" >> "$OUT/status.txt"; }
 run() {  # run NAME SECONDS CMD...
   local name=$1 secs=$2; shift 2
   status "start $name"
