@@ -70,6 +70,7 @@ struct TraceArgs {
     unsigned* queue;            // persistent: zeroed work counter for this launch
     int      shade_min;         // persistent: shade once this many lanes of a wave are ready
     int      grid_blocks;       // persistent: blocks of 256 threads
+    int      wave_tile;         // simple: wave tile (8<<s) x (8>>s), s in 0..3
 };
 
 // Host-side compact-scene build from the reference records; validates the

@@ -196,6 +196,7 @@ struct rt_ctx {
     int  kernel = kKernelPersistent;
     int  shade_min = 16;
     int  blocks_per_cu = 0;        // 0 = from the occupancy query
+    int  wave_tile = 0;            // simple kernel: 8x8 / 16x4 / 32x2 / 64x1
     bool has_scene = false;
     int  n_nodes = 0, n_tris = 0, max_depth = 0;
 };
@@ -210,6 +211,7 @@ static void free_scene(PerDevice& p) {
 static void set_schedule(const rt_ctx* ctx, PerDevice& p, TraceArgs& a) {
     a.kernel = ctx->kernel;
     a.shade_min = ctx->shade_min;
+    a.wave_tile = ctx->wave_tile;
     a.queue = p.d_queue + (p.queue_slot++ % kQueueSlots);
     const int bpc = ctx->blocks_per_cu > 0 ? ctx->blocks_per_cu : p.blocks_per_cu;
     a.grid_blocks = std::max(1, p.n_cu * bpc);
@@ -564,6 +566,8 @@ int rt_set_option(rt_ctx* ctx, const char* name, int64_t value) {
         ctx->shade_min = (int)value;
     } else if (std::strcmp(name, "blocks_per_cu") == 0 && value >= 0 && value <= 32) {
         ctx->blocks_per_cu = (int)value;
+    } else if (std::strcmp(name, "wave_tile") == 0 && value >= 0 && value <= 3) {
+        ctx->wave_tile = (int)value;
     } else {
         set_error("rt_set_option: unknown option or bad value: %s = %lld", name, (long long)value);
         return RT_ERR_INVALID_ARG;
@@ -575,6 +579,7 @@ int rt_get_option(rt_ctx* ctx, const char* name, int64_t* value) {
     if (!ctx || !name || !value) { set_error("rt_get_option: null argument"); return RT_ERR_INVALID_ARG; }
     if (std::strcmp(name, "kernel") == 0) *value = ctx->kernel;
     else if (std::strcmp(name, "shade_min") == 0) *value = ctx->shade_min;
+    else if (std::strcmp(name, "wave_tile") == 0) *value = ctx->wave_tile;
     else if (std::strcmp(name, "blocks_per_cu") == 0)
         *value = ctx->blocks_per_cu > 0 ? ctx->blocks_per_cu : (ctx->dev.empty() ? 0 : ctx->dev[0].blocks_per_cu);
     else { set_error("rt_get_option: unknown option %s", name); return RT_ERR_INVALID_ARG; }

@@ -212,10 +212,13 @@ template <bool COUNT>
 __global__ __launch_bounds__(256) void trace_simple(TraceArgs a) {
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
-    // One wave = one 8x8 pixel tile (the reference's local_size 8x8x1,
-    // compute_dynamic_ray.comp:157); a 256-thread block = 16x16 pixels.
-    const int lx = blockIdx.x * 16 + (wave & 1) * 8 + (lane & 7);
-    const int ly = blockIdx.y * 16 + (wave >> 1) * 8 + (lane >> 3);
+    // One wave = one tile of 64 pixels, (8 << s) x (8 >> s) with s = a.wave_tile
+    // (s = 0: 8x8, the reference's local_size 8x8x1, compute_dynamic_ray.comp:157);
+    // a 256-thread block = 4 such tiles side by side.
+    const int s = a.wave_tile;
+    const int tw_w = 8 << s, th_w = 8 >> s;
+    const int lx = (blockIdx.x * 4 + wave) * tw_w + (lane & (tw_w - 1));
+    const int ly = blockIdx.y * th_w + (lane >> (3 + s));
     unsigned long long c_seg = 0, c_node = 0, c_tri = 0, c_mat = 0;
 
     if (lx < a.tw && ly < a.th) {
@@ -311,7 +314,7 @@ __global__ __launch_bounds__(256) void trace_persistent(TraceArgs a) {
                     closest = kTMax;
                     hit = -1;
                     node = 0;
-                    mode = kTrace;
+                    mode = end > 0 ? kTrace : kReady;
                     if (COUNT) ++c_seg;
                 }
             }
@@ -348,7 +351,7 @@ __global__ __launch_bounds__(256) void trace_persistent(TraceArgs a) {
                     closest = kTMax;
                     hit = -1;
                     node = 0;
-                    mode = kTrace;
+                    mode = end > 0 ? kTrace : kReady;
                     finish = false;
                     if (COUNT) ++c_seg;
                 }
@@ -386,7 +389,8 @@ hipError_t launch_trace(const TraceArgs& a, hipStream_t stream) {
         else
             hipLaunchKernelGGL(trace_persistent<false>, grid, block, 0, stream, a);
     } else {
-        const dim3 grid((a.tw + 15) / 16, (a.th + 15) / 16);
+        const int tw_w = 8 << a.wave_tile, th_w = 8 >> a.wave_tile;
+        const dim3 grid((a.tw + 4 * tw_w - 1) / (4 * tw_w), (a.th + th_w - 1) / th_w);
         if (a.counters)
             hipLaunchKernelGGL(trace_simple<true>, grid, block, 0, stream, a);
         else

@@ -139,6 +139,7 @@ int rt_band_rows(int height, int band_h, int band_stride, int band_off);
  *                   ready (1..64, default 16)
  *   "blocks_per_cu" persistent: resident 256-thread blocks per CU (0 = from
  *                   the occupancy query)
+ *   "wave_tile"     kernel 0: pixels per wave (8<<s) x (8>>s), s = 0..3
  * Defaults can also be set with the RTAMD_KERNEL=simple|persistent,
  * RTAMD_SHADE_MIN and RTAMD_BLOCKS_PER_CU environment variables. */
 int rt_set_option(rt_ctx* ctx, const char* name, int64_t value);

@@ -23,6 +23,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=7)
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--variant", action="append", default=[])
+    ap.add_argument("--bounces", type=int, default=0, help="override the config's max_bounces")
     args = ap.parse_args()
     variants = args.variant or ["kernel=0", "kernel=1,shade_min=8", "kernel=1,shade_min=16",
                                 "kernel=1,shade_min=32"]
@@ -34,7 +35,7 @@ def main():
     cfg = configs.get(args.config)
     built = cfg.build()
     cam = cfg.camera()
-    W, H, B = cfg.width, cfg.height, cfg.max_bounces
+    W, H, B = cfg.width, cfg.height, (args.bounces or cfg.max_bounces)
     r = rtamd.Renderer((0,))
     r.upload_scene(built)
     L = rtamd.lib()
@@ -68,11 +69,11 @@ def main():
             e1.record(stream)
             e1.synchronize()
             times[v].append(e0.elapsed_time(e1) / args.iters)
-        apply("kernel=1,shade_min=16,blocks_per_cu=0")
+        apply("kernel=1,shade_min=16,blocks_per_cu=0,wave_tile=0")
     for v in variants:
         med = statistics.median(times[v])
         print(json.dumps({"variant": v, "config": cfg.name, "median_ms": round(med, 4),
-                          "min_ms": round(min(times[v]), 4), "mrays_s": round(segs / med / 1e3, 1)}))
+                          "min_ms": round(min(times[v]), 4), "bounces": B, "mrays_s": round(segs / med / 1e3, 1)}))
     r.close()
 
 
