@@ -52,6 +52,17 @@ struct CamF {                   // the four vec3 of the CameraUBO
 
 constexpr int kKernelSimple = 0;       // one lane per pixel, 8x8 pixels per wave
 constexpr int kKernelPersistent = 1;   // persistent waves + tile queue + deferred shading
+constexpr int kKernelSplit = 2;        // simple for the first seg_limit segments, then the
+                                       // surviving paths are spilled to a compacted queue and
+                                       // finished by the persistent kernel
+
+// A path suspended between two segments (48 B): everything the bounce loop
+// (compute_dynamic_ray.comp:179-232) carries from one iteration to the next.
+struct PathState {
+    float4 q0;   // origin.xyz, attenuation.x
+    float4 q1;   // direction.xyz, attenuation.y
+    float4 q2;   // attenuation.z, seed (bits), bounce index b (bits), lx | ly << 16 (bits)
+};
 
 struct TraceArgs {
     DevScene scene;
@@ -71,6 +82,10 @@ struct TraceArgs {
     int      shade_min;         // persistent: shade once this many lanes of a wave are ready
     int      grid_blocks;       // persistent: blocks of 256 threads
     int      wave_tile;         // simple: wave tile (8<<s) x (8>>s), s in 0..3
+    int      seg_limit;         // simple: segments before a live path is spilled (>= max_bounces: never)
+    PathState* spill;           // split: spilled paths (capacity tw*th)
+    unsigned* spill_count;      // split: number of spilled paths (zeroed before the simple pass)
+    int      resume;            // persistent: take paths from spill[] instead of pixel tiles
 };
 
 // Host-side compact-scene build from the reference records; validates the

@@ -183,8 +183,10 @@ struct PerDevice {
     uchar4*      d_rgba = nullptr;
     float*       d_rad = nullptr;
     size_t       out_cap = 0;      // pixels
-    unsigned*    d_queue = nullptr; // ring of kQueueSlots work counters (persistent kernel)
+    unsigned*    d_queue = nullptr; // ring of kQueueSlots work counters + kQueueSlots spill counters
     unsigned     queue_slot = 0;
+    PathState*   d_spill = nullptr; // split schedule: suspended paths
+    size_t       spill_cap = 0;
     int          n_cu = 0;
     int          blocks_per_cu = 1;
 };
@@ -197,6 +199,7 @@ struct rt_ctx {
     int  shade_min = 16;
     int  blocks_per_cu = 0;        // 0 = from the occupancy query
     int  wave_tile = 0;            // simple kernel: 8x8 / 16x4 / 32x2 / 64x1
+    int  seg_limit = 2;            // split: segments traced in the lockstep pass
     bool has_scene = false;
     int  n_nodes = 0, n_tris = 0, max_depth = 0;
 };
@@ -208,16 +211,35 @@ static void free_scene(PerDevice& p) {
     p.scene = DevScene{};
 }
 
-static void set_schedule(const rt_ctx* ctx, PerDevice& p, TraceArgs& a) {
+static int set_schedule(const rt_ctx* ctx, PerDevice& p, TraceArgs& a) {
     a.kernel = ctx->kernel;
     a.shade_min = ctx->shade_min;
     a.wave_tile = ctx->wave_tile;
-    a.queue = p.d_queue + (p.queue_slot++ % kQueueSlots);
+    a.seg_limit = ctx->kernel == kKernelSplit ? ctx->seg_limit : (1 << 30);
+    a.resume = 0;
+    const unsigned slot = p.queue_slot++ % kQueueSlots;
+    a.queue = p.d_queue + slot;
+    a.spill_count = p.d_queue + kQueueSlots + slot;
     const int bpc = ctx->blocks_per_cu > 0 ? ctx->blocks_per_cu : p.blocks_per_cu;
     a.grid_blocks = std::max(1, p.n_cu * bpc);
-    // never more waves than 8x8 pixel tiles
-    const int tiles = ((a.tw + 7) / 8) * ((a.th + 7) / 8);
-    a.grid_blocks = std::min(a.grid_blocks, std::max(1, (tiles + 3) / 4));
+    if (a.kernel == kKernelPersistent) {
+        // never more waves than 8x8 pixel tiles
+        const int tiles = ((a.tw + 7) / 8) * ((a.th + 7) / 8);
+        a.grid_blocks = std::min(a.grid_blocks, std::max(1, (tiles + 3) / 4));
+    }
+    a.spill = nullptr;
+    if (a.kernel == kKernelSplit) {
+        const size_t need = (size_t)a.tw * (size_t)a.th;
+        if (need > p.spill_cap) {
+            if (p.d_spill) (void)hipFree(p.d_spill);
+            p.d_spill = nullptr;
+            p.spill_cap = 0;
+            RT_HIP_CHECK(hipMalloc(&p.d_spill, need * sizeof(PathState)));
+            p.spill_cap = need;
+        }
+        a.spill = p.d_spill;
+    }
+    return RT_OK;
 }
 
 static CamF cam_from_ubo(const rt_camera_ubo* c) {
@@ -246,7 +268,10 @@ int rt_create(const int* device_ids, int n_devices, rt_ctx** out) {
     }
     rt_ctx* ctx = new (std::nothrow) rt_ctx;
     if (!ctx) { set_error("rt_create: out of memory"); return RT_ERR_OOM; }
-    if (const char* k = std::getenv("RTAMD_KERNEL")) ctx->kernel = std::strcmp(k, "simple") == 0 ? kKernelSimple : kKernelPersistent;
+    if (const char* k = std::getenv("RTAMD_KERNEL"))
+        ctx->kernel = std::strcmp(k, "simple") == 0 ? kKernelSimple
+                    : std::strcmp(k, "persistent") == 0 ? kKernelPersistent : kKernelSplit;
+    if (const char* v = std::getenv("RTAMD_SEG_LIMIT")) ctx->seg_limit = std::max(1, std::min(1024, std::atoi(v)));
     if (const char* v = std::getenv("RTAMD_SHADE_MIN")) ctx->shade_min = std::max(1, std::min(64, std::atoi(v)));
     if (const char* v = std::getenv("RTAMD_BLOCKS_PER_CU")) ctx->blocks_per_cu = std::max(0, std::min(32, std::atoi(v)));
     for (int k = 0; k < n_devices; ++k) {
@@ -269,7 +294,7 @@ int rt_create(const int* device_ids, int n_devices, rt_ctx** out) {
         if (e == hipSuccess) e = hipEventCreate(&p.ev0);
         if (e == hipSuccess) e = hipEventCreate(&p.ev1);
         if (e == hipSuccess) e = hipMalloc(&p.d_counters, sizeof(Counters));
-        if (e == hipSuccess) e = hipMalloc(&p.d_queue, sizeof(unsigned) * kQueueSlots);
+        if (e == hipSuccess) e = hipMalloc(&p.d_queue, sizeof(unsigned) * 2 * kQueueSlots);
         p.n_cu = prop.multiProcessorCount;
         p.blocks_per_cu = persistent_blocks_per_cu();
         ctx->dev.push_back(p);
@@ -291,6 +316,7 @@ int rt_destroy(rt_ctx* ctx) {
         free_scene(p);
         if (p.d_counters) (void)hipFree(p.d_counters);
         if (p.d_queue) (void)hipFree(p.d_queue);
+        if (p.d_spill) (void)hipFree(p.d_spill);
         if (p.d_rgba) (void)hipFree(p.d_rgba);
         if (p.d_rad) (void)hipFree(p.d_rad);
         if (p.ev0) (void)hipEventDestroy(p.ev0);
@@ -404,7 +430,7 @@ int rt_render_tile_device(rt_ctx* ctx, const rt_camera_ubo* cam, int width, int 
     a.out_rgba = static_cast<uchar4*>(d_out_rgba);
     a.out_rad = static_cast<float*>(d_out_radiance);
     a.counters = nullptr;
-    set_schedule(ctx, p, a);
+    if (int rs = set_schedule(ctx, p, a)) return rs;
     if (stats) {
         a.counters = p.d_counters;
         RT_HIP_CHECK(hipMemsetAsync(p.d_counters, 0, sizeof(Counters), s));
@@ -450,7 +476,7 @@ static int render_bands_on(const rt_ctx* ctx, PerDevice& p, const rt_camera_ubo*
     a.out_rgba = d_rgba;
     a.out_rad = d_rad;
     a.counters = count ? p.d_counters : nullptr;
-    set_schedule(ctx, p, a);
+    if (int rs = set_schedule(ctx, p, a)) return rs;
     if (count) RT_HIP_CHECK(hipMemsetAsync(p.d_counters, 0, sizeof(Counters), s));
     RT_HIP_CHECK(hipEventRecord(p.ev0, s));
     RT_HIP_CHECK(launch_trace(a, s));
@@ -560,12 +586,14 @@ int rt_render(rt_ctx* ctx, const rt_camera_ubo* cam, int width, int height, int 
 
 int rt_set_option(rt_ctx* ctx, const char* name, int64_t value) {
     if (!ctx || !name) { set_error("rt_set_option: null argument"); return RT_ERR_INVALID_ARG; }
-    if (std::strcmp(name, "kernel") == 0 && (value == kKernelSimple || value == kKernelPersistent)) {
+    if (std::strcmp(name, "kernel") == 0 && value >= kKernelSimple && value <= kKernelSplit) {
         ctx->kernel = (int)value;
     } else if (std::strcmp(name, "shade_min") == 0 && value >= 1 && value <= 64) {
         ctx->shade_min = (int)value;
     } else if (std::strcmp(name, "blocks_per_cu") == 0 && value >= 0 && value <= 32) {
         ctx->blocks_per_cu = (int)value;
+    } else if (std::strcmp(name, "seg_limit") == 0 && value >= 1 && value <= 1024) {
+        ctx->seg_limit = (int)value;
     } else if (std::strcmp(name, "wave_tile") == 0 && value >= 0 && value <= 3) {
         ctx->wave_tile = (int)value;
     } else {
@@ -580,6 +608,7 @@ int rt_get_option(rt_ctx* ctx, const char* name, int64_t* value) {
     if (std::strcmp(name, "kernel") == 0) *value = ctx->kernel;
     else if (std::strcmp(name, "shade_min") == 0) *value = ctx->shade_min;
     else if (std::strcmp(name, "wave_tile") == 0) *value = ctx->wave_tile;
+    else if (std::strcmp(name, "seg_limit") == 0) *value = ctx->seg_limit;
     else if (std::strcmp(name, "blocks_per_cu") == 0)
         *value = ctx->blocks_per_cu > 0 ? ctx->blocks_per_cu : (ctx->dev.empty() ? 0 : ctx->dev[0].blocks_per_cu);
     else { set_error("rt_get_option: unknown option %s", name); return RT_ERR_INVALID_ARG; }

@@ -206,6 +206,10 @@ __device__ __forceinline__ void flush_counters(Counters* c, unsigned long long s
     }
 }
 
+__device__ __forceinline__ int lanes_below(uint64_t mask) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
+}
+
 // ------------------------------------------------------------ simple kernel --
 
 template <bool COUNT>
@@ -220,6 +224,8 @@ __global__ __launch_bounds__(256) void trace_simple(TraceArgs a) {
     const int lx = (blockIdx.x * 4 + wave) * tw_w + (lane & (tw_w - 1));
     const int ly = blockIdx.y * th_w + (lane >> (3 + s));
     unsigned long long c_seg = 0, c_node = 0, c_tri = 0, c_mat = 0;
+    bool spill = false;
+    PathState st;
 
     if (lx < a.tw && ly < a.th) {
         const int x = a.x0 + lx;
@@ -230,6 +236,14 @@ __global__ __launch_bounds__(256) void trace_simple(TraceArgs a) {
         V3 fin = {0.0f, 0.0f, 0.0f};
         V3 att = {1.0f, 1.0f, 1.0f};
         for (int b = 0; b < a.max_bounces; ++b) {                         // :179
+            if (b == a.seg_limit) {                                       // hand the path on
+                spill = true;
+                st.q0 = make_float4(o.x, o.y, o.z, att.x);
+                st.q1 = make_float4(d.x, d.y, d.z, att.y);
+                st.q2 = make_float4(att.z, __uint_as_float(seed), __int_as_float(b),
+                                    __int_as_float(lx | (ly << 16)));
+                break;
+            }
             if (COUNT) ++c_seg;
             float closest = kTMax;
             int hit = -1;
@@ -253,7 +267,16 @@ __global__ __launch_bounds__(256) void trace_simple(TraceArgs a) {
             }
             if (b == a.max_bounces - 1) fin = {0.0f, 0.0f, 0.0f};        // :229-231
         }
-        write_pixel(a, lx, ly, fin);
+        if (!spill) write_pixel(a, lx, ly, fin);
+    }
+    // Append this wave's live paths to the spill queue (one atomic per wave);
+    // lanes keep their tile order, so neighbouring paths stay neighbours.
+    const uint64_t sm = __ballot(spill);
+    if (sm != 0) {
+        unsigned base = 0;
+        if (lane == 0) base = atomicAdd(a.spill_count, (unsigned)__popcll(sm));
+        base = __shfl(base, 0);
+        if (spill) a.spill[base + lanes_below(sm)] = st;
     }
     if (COUNT) flush_counters(a.counters, c_seg, c_node, c_tri, c_mat);
 }
@@ -262,15 +285,13 @@ __global__ __launch_bounds__(256) void trace_simple(TraceArgs a) {
 
 constexpr int kIdle = 0, kTrace = 1, kReady = 2;
 
-__device__ __forceinline__ int lanes_below(uint64_t mask) {
-    return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
-}
-
 template <bool COUNT>
 __global__ __launch_bounds__(256) void trace_persistent(TraceArgs a) {
     const int lane = threadIdx.x & 63;
     const int tiles_x = (a.tw + 7) >> 3;
-    const int n_slots = tiles_x * ((a.th + 7) >> 3) * 64;   // pixel slots, 8x8 tiles in row-major tile order
+    // Work slots: 8x8 pixel tiles in row-major tile order, or (resume) the
+    // paths the simple pass spilled, in spill order.
+    const int n_slots = a.resume ? (int)*a.spill_count : tiles_x * ((a.th + 7) >> 3) * 64;
     const float4* __restrict__ nodes = a.scene.nodes;
     const float4* __restrict__ tris = a.scene.tris;
     const int end = a.scene.end;
@@ -300,7 +321,25 @@ __global__ __launch_bounds__(256) void trace_persistent(TraceArgs a) {
             }
             const int avail = pool_end - pool_next;
             const int rank = lanes_below(idle);
-            if (mode == kIdle && rank < avail) {
+            if (a.resume) {
+                if (mode == kIdle && rank < avail && pool_next + rank < n_slots) {
+                    const PathState p = a.spill[pool_next + rank];
+                    o = {p.q0.x, p.q0.y, p.q0.z};
+                    d = {p.q1.x, p.q1.y, p.q1.z};
+                    att = {p.q0.w, p.q1.w, p.q2.x};
+                    seed = __float_as_uint(p.q2.y);
+                    b = __float_as_int(p.q2.z);
+                    const int pix = __float_as_int(p.q2.w);
+                    lx = pix & 0xFFFF;
+                    ly = pix >> 16;
+                    inv = {1.0f / d.x, 1.0f / d.y, 1.0f / d.z};
+                    closest = kTMax;
+                    hit = -1;
+                    node = 0;
+                    mode = end > 0 ? kTrace : kReady;
+                    if (COUNT) ++c_seg;
+                }
+            } else if (mode == kIdle && rank < avail) {
                 const int slot = pool_next + rank;
                 const int tile = slot >> 6, w = slot & 63;
                 lx = (tile % tiles_x) * 8 + (w & 7);
@@ -380,6 +419,22 @@ int persistent_blocks_per_cu() {
 
 hipError_t launch_trace(const TraceArgs& a, hipStream_t stream) {
     const dim3 block(256);
+    if (a.kernel == kKernelSplit) {
+        // pass 1: coherent 8x8 lockstep tiles for the first seg_limit segments
+        TraceArgs s = a;
+        s.kernel = kKernelSimple;
+        s.resume = 0;
+        hipError_t e = hipMemsetAsync(a.spill_count, 0, sizeof(unsigned), stream);
+        if (e != hipSuccess) return e;
+        e = launch_trace(s, stream);
+        if (e != hipSuccess) return e;
+        // pass 2: the surviving paths, compacted, on persistent waves
+        TraceArgs p = a;
+        p.kernel = kKernelPersistent;
+        p.resume = 1;
+        p.seg_limit = 1 << 30;
+        return launch_trace(p, stream);
+    }
     if (a.kernel == kKernelPersistent) {
         const dim3 grid(a.grid_blocks);
         hipError_t e = hipMemsetAsync(a.queue, 0, sizeof(unsigned), stream);

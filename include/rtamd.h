@@ -134,13 +134,18 @@ int rt_band_rows(int height, int band_h, int band_stride, int band_off);
 /* Schedule options (no effect on results, which are identical for every
  * setting):
  *   "kernel"        0 = one lane per pixel (the reference's dispatch shape),
- *                   1 = persistent waves with a tile queue (default)
+ *                   1 = persistent waves with a tile queue,
+ *                   2 = split: kernel 0 for the first seg_limit segments of
+ *                       every path, then the surviving paths, compacted, on
+ *                       persistent waves
+ *   "seg_limit"     split: segments traced in the first pass (default 2)
  *   "shade_min"     persistent: shade once this many lanes of a wave are
  *                   ready (1..64, default 16)
  *   "blocks_per_cu" persistent: resident 256-thread blocks per CU (0 = from
  *                   the occupancy query)
  *   "wave_tile"     kernel 0: pixels per wave (8<<s) x (8>>s), s = 0..3
- * Defaults can also be set with the RTAMD_KERNEL=simple|persistent,
+ * Defaults can also be set with the RTAMD_KERNEL=simple|persistent|split,
+ * RTAMD_SEG_LIMIT,
  * RTAMD_SHADE_MIN and RTAMD_BLOCKS_PER_CU environment variables. */
 int rt_set_option(rt_ctx* ctx, const char* name, int64_t value);
 int rt_get_option(rt_ctx* ctx, const char* name, int64_t* value);

@@ -13,6 +13,7 @@ from conftest import has_gpu
 pytestmark = pytest.mark.gpu
 
 COUNTERS = ("segments", "node_visits", "tri_tests", "mat_reads")
+DEFAULT_OPTS = {"kernel": 1, "shade_min": 16, "blocks_per_cu": 0, "wave_tile": 0, "seg_limit": 2}
 
 
 def _oracle(built, cam_bytes, w, h, b, **kw):
@@ -112,6 +113,10 @@ def test_config5_1m_row_subset(renderer):
     {"kernel": 1, "shade_min": 16},
     {"kernel": 1, "shade_min": 64},
     {"kernel": 1, "shade_min": 24, "blocks_per_cu": 1},
+    {"kernel": 0, "wave_tile": 3},
+    {"kernel": 2, "seg_limit": 1},
+    {"kernel": 2, "seg_limit": 2},
+    {"kernel": 2, "seg_limit": 3, "shade_min": 1},
 ])
 def test_schedules_identical(renderer, opts):
     """Every schedule gives the oracle's frame and counters (config 2 at the
@@ -132,9 +137,8 @@ def test_schedules_identical(renderer, opts):
                       tile=(0, 1, cfg.width, cfg.height - 1), row_step=6)
         _assert_same(rgba, rad, st, *ref)
     finally:
-        renderer.set_option("kernel", 1)
-        renderer.set_option("shade_min", 16)
-        renderer.set_option("blocks_per_cu", 0)
+        for k, v in DEFAULT_OPTS.items():
+            renderer.set_option(k, v)
 
 
 def test_tiles_compose_to_frame(renderer):
