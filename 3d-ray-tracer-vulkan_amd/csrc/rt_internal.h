@@ -86,6 +86,7 @@ struct TraceArgs {
     PathState* spill;           // split: spilled paths (capacity tw*th)
     unsigned* spill_count;      // split: number of spilled paths (zeroed before the simple pass)
     int      resume;            // persistent: take paths from spill[] instead of pixel tiles
+    unsigned long long* diag;   // simple kernel diagnostics: 4 words per wave, or null
 };
 
 // Host-side compact-scene build from the reference records; validates the

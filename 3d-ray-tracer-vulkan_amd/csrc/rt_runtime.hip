@@ -187,6 +187,8 @@ struct PerDevice {
     unsigned     queue_slot = 0;
     PathState*   d_spill = nullptr; // split schedule: suspended paths
     size_t       spill_cap = 0;
+    unsigned long long* d_diag = nullptr;   // diagnostics (option "diag")
+    size_t       diag_cap = 0, diag_used = 0;
     int          n_cu = 0;
     int          blocks_per_cu = 1;
 };
@@ -200,6 +202,7 @@ struct rt_ctx {
     int  blocks_per_cu = 0;        // 0 = from the occupancy query
     int  wave_tile = 0;            // simple kernel: 8x8 / 16x4 / 32x2 / 64x1
     int  seg_limit = 2;            // split: segments traced in the lockstep pass
+    int  diag = 0;                 // record per-wave timestamps (kernel 0 only)
     bool has_scene = false;
     int  n_nodes = 0, n_tris = 0, max_depth = 0;
 };
@@ -226,6 +229,20 @@ static int set_schedule(const rt_ctx* ctx, PerDevice& p, TraceArgs& a) {
         // never more waves than 8x8 pixel tiles
         const int tiles = ((a.tw + 7) / 8) * ((a.th + 7) / 8);
         a.grid_blocks = std::min(a.grid_blocks, std::max(1, (tiles + 3) / 4));
+    }
+    a.diag = nullptr;
+    if (ctx->diag && a.kernel == kKernelSimple) {
+        const int tw_w = 8 << a.wave_tile, th_w = 8 >> a.wave_tile;
+        const size_t waves = (size_t)((a.tw + 4 * tw_w - 1) / (4 * tw_w)) * ((a.th + th_w - 1) / th_w) * 4;
+        if (waves * 4 > p.diag_cap) {
+            if (p.d_diag) (void)hipFree(p.d_diag);
+            p.d_diag = nullptr;
+            p.diag_cap = 0;
+            RT_HIP_CHECK(hipMalloc(&p.d_diag, waves * 4 * sizeof(unsigned long long)));
+            p.diag_cap = waves * 4;
+        }
+        p.diag_used = waves * 4;
+        a.diag = p.d_diag;
     }
     a.spill = nullptr;
     if (a.kernel == kKernelSplit) {
@@ -594,6 +611,8 @@ int rt_set_option(rt_ctx* ctx, const char* name, int64_t value) {
         ctx->blocks_per_cu = (int)value;
     } else if (std::strcmp(name, "seg_limit") == 0 && value >= 1 && value <= 1024) {
         ctx->seg_limit = (int)value;
+    } else if (std::strcmp(name, "diag") == 0 && (value == 0 || value == 1)) {
+        ctx->diag = (int)value;
     } else if (std::strcmp(name, "wave_tile") == 0 && value >= 0 && value <= 3) {
         ctx->wave_tile = (int)value;
     } else {
@@ -612,6 +631,18 @@ int rt_get_option(rt_ctx* ctx, const char* name, int64_t* value) {
     else if (std::strcmp(name, "blocks_per_cu") == 0)
         *value = ctx->blocks_per_cu > 0 ? ctx->blocks_per_cu : (ctx->dev.empty() ? 0 : ctx->dev[0].blocks_per_cu);
     else { set_error("rt_get_option: unknown option %s", name); return RT_ERR_INVALID_ARG; }
+    return RT_OK;
+}
+
+int rt_diag_copy(rt_ctx* ctx, void* dst, size_t cap_words, size_t* n_words) {
+    if (!ctx || !n_words) { set_error("rt_diag_copy: null argument"); return RT_ERR_INVALID_ARG; }
+    PerDevice& p = ctx->dev[0];
+    *n_words = p.diag_used;
+    if (dst && p.d_diag && p.diag_used) {
+        RT_HIP_CHECK(hipSetDevice(p.device));
+        RT_HIP_CHECK(hipDeviceSynchronize());
+        RT_HIP_CHECK(hipMemcpy(dst, p.d_diag, std::min(cap_words, p.diag_used) * 8, hipMemcpyDeviceToHost));
+    }
     return RT_OK;
 }
 

@@ -212,10 +212,32 @@ __device__ __forceinline__ int lanes_below(uint64_t mask) {
 
 // ------------------------------------------------------------ simple kernel --
 
-template <bool COUNT>
+// Diagnostic stamp (diag builds only): global realtime clock (100 MHz) and
+// the wave's hardware placement.
+__device__ __forceinline__ void diag_stamp(unsigned long long* rec, int which) {
+    unsigned long long t;
+    asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t) :: "memory");
+    if ((threadIdx.x & 63) == 0) {
+        rec[which] = t;
+        if (which == 0) {
+            unsigned hw, xcc;
+            asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+            asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+            rec[2] = ((unsigned long long)xcc << 32) | hw;
+            rec[3] = ((unsigned long long)(blockIdx.y * gridDim.x + blockIdx.x) << 8) | (threadIdx.x >> 6);
+        }
+    }
+}
+
+template <bool COUNT, bool DIAG = false>
 __global__ __launch_bounds__(256) void trace_simple(TraceArgs a) {
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
+    unsigned long long* drec = nullptr;
+    if (DIAG) {
+        drec = a.diag + 4 * (size_t)((blockIdx.y * gridDim.x + blockIdx.x) * 4 + wave);
+        diag_stamp(drec, 0);
+    }
     // One wave = one tile of 64 pixels, (8 << s) x (8 >> s) with s = a.wave_tile
     // (s = 0: 8x8, the reference's local_size 8x8x1, compute_dynamic_ray.comp:157);
     // a 256-thread block = 4 such tiles side by side.
@@ -279,6 +301,7 @@ __global__ __launch_bounds__(256) void trace_simple(TraceArgs a) {
         if (spill) a.spill[base + lanes_below(sm)] = st;
     }
     if (COUNT) flush_counters(a.counters, c_seg, c_node, c_tri, c_mat);
+    if (DIAG) diag_stamp(drec, 1);
 }
 
 // -------------------------------------------------------- persistent kernel --
@@ -446,7 +469,9 @@ hipError_t launch_trace(const TraceArgs& a, hipStream_t stream) {
     } else {
         const int tw_w = 8 << a.wave_tile, th_w = 8 >> a.wave_tile;
         const dim3 grid((a.tw + 4 * tw_w - 1) / (4 * tw_w), (a.th + th_w - 1) / th_w);
-        if (a.counters)
+        if (a.diag)
+            hipLaunchKernelGGL((trace_simple<false, true>), grid, block, 0, stream, a);
+        else if (a.counters)
             hipLaunchKernelGGL(trace_simple<true>, grid, block, 0, stream, a);
         else
             hipLaunchKernelGGL(trace_simple<false>, grid, block, 0, stream, a);

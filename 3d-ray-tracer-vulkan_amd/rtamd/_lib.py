@@ -31,7 +31,7 @@ EXPORTED = (
     "rt_last_error", "rt_scene_info", "rt_bvh_layout_size", "rt_build_scene",
     "rt_camera_from_lookat", "rt_mesh_load_obj", "rt_mesh_tri_count", "rt_mesh_transform",
     "rt_mesh_free", "rt_mesh_procedural", "rt_render_bands_device", "rt_band_rows",
-    "rt_scene_validate", "rt_set_option", "rt_get_option",
+    "rt_scene_validate", "rt_set_option", "rt_get_option", "rt_diag_copy",
 )
 
 
@@ -115,6 +115,7 @@ def lib() -> C.CDLL:
                 "rt_scene_validate": (i32, [vp, sz, vp, sz, vp, sz, C.POINTER(sz), C.POINTER(i32)]),
                 "rt_set_option": (i32, [vp, C.c_char_p, C.c_int64]),
                 "rt_get_option": (i32, [vp, C.c_char_p, C.POINTER(C.c_int64)]),
+                "rt_diag_copy": (i32, [vp, vp, sz, C.POINTER(sz)]),
             }
             for name, (res, args) in sig.items():
                 f = getattr(L, name)

@@ -148,6 +148,11 @@ int rt_band_rows(int height, int band_h, int band_stride, int band_off);
  * RTAMD_SEG_LIMIT,
  * RTAMD_SHADE_MIN and RTAMD_BLOCKS_PER_CU environment variables. */
 int rt_set_option(rt_ctx* ctx, const char* name, int64_t value);
+/* Diagnostics: with option "diag" = 1, kernel 0 records per wave
+ * {start, end} (s_memrealtime, 100 MHz), {XCC id << 32 | HW_ID}, {block << 8 |
+ * wave} into a device buffer; rt_diag_copy copies up to cap_words 64-bit words
+ * of the last launch (n_words = words recorded).  Not for timing runs. */
+int rt_diag_copy(rt_ctx* ctx, void* dst, size_t cap_words, size_t* n_words);
 int rt_get_option(rt_ctx* ctx, const char* name, int64_t* value);
 
 /* Replaces VulkanEngine.cleanup. Null is accepted. */
