@@ -87,6 +87,7 @@ struct TraceArgs {
     unsigned* spill_count;      // split: number of spilled paths (zeroed before the simple pass)
     int      resume;            // persistent: take paths from spill[] instead of pixel tiles
     unsigned long long* diag;   // simple kernel diagnostics: 4 words per wave, or null
+    int      prio_after;        // simple: raise wave priority after this many node steps (0 = never)
 };
 
 // Host-side compact-scene build from the reference records; validates the

@@ -203,6 +203,7 @@ struct rt_ctx {
     int  wave_tile = 0;            // simple kernel: 8x8 / 16x4 / 32x2 / 64x1
     int  seg_limit = 2;            // split: segments traced in the lockstep pass
     int  diag = 0;                 // record per-wave timestamps (kernel 0 only)
+    int  prio_after = 0;           // kernel 0: s_setprio(3) after this many node steps
     bool has_scene = false;
     int  n_nodes = 0, n_tris = 0, max_depth = 0;
 };
@@ -218,6 +219,7 @@ static int set_schedule(const rt_ctx* ctx, PerDevice& p, TraceArgs& a) {
     a.kernel = ctx->kernel;
     a.shade_min = ctx->shade_min;
     a.wave_tile = ctx->wave_tile;
+    a.prio_after = ctx->prio_after > 0 ? ctx->prio_after : -1;
     a.seg_limit = ctx->kernel == kKernelSplit ? ctx->seg_limit : (1 << 30);
     a.resume = 0;
     const unsigned slot = p.queue_slot++ % kQueueSlots;
@@ -611,6 +613,8 @@ int rt_set_option(rt_ctx* ctx, const char* name, int64_t value) {
         ctx->blocks_per_cu = (int)value;
     } else if (std::strcmp(name, "seg_limit") == 0 && value >= 1 && value <= 1024) {
         ctx->seg_limit = (int)value;
+    } else if (std::strcmp(name, "prio_after") == 0 && value >= 0 && value <= (1 << 30)) {
+        ctx->prio_after = (int)value;
     } else if (std::strcmp(name, "diag") == 0 && (value == 0 || value == 1)) {
         ctx->diag = (int)value;
     } else if (std::strcmp(name, "wave_tile") == 0 && value >= 0 && value <= 3) {
@@ -628,6 +632,7 @@ int rt_get_option(rt_ctx* ctx, const char* name, int64_t* value) {
     else if (std::strcmp(name, "shade_min") == 0) *value = ctx->shade_min;
     else if (std::strcmp(name, "wave_tile") == 0) *value = ctx->wave_tile;
     else if (std::strcmp(name, "seg_limit") == 0) *value = ctx->seg_limit;
+    else if (std::strcmp(name, "prio_after") == 0) *value = ctx->prio_after;
     else if (std::strcmp(name, "blocks_per_cu") == 0)
         *value = ctx->blocks_per_cu > 0 ? ctx->blocks_per_cu : (ctx->dev.empty() ? 0 : ctx->dev[0].blocks_per_cu);
     else { set_error("rt_get_option: unknown option %s", name); return RT_ERR_INVALID_ARG; }

@@ -248,6 +248,7 @@ __global__ __launch_bounds__(256) void trace_simple(TraceArgs a) {
     unsigned long long c_seg = 0, c_node = 0, c_tri = 0, c_mat = 0;
     bool spill = false;
     PathState st;
+    int steps = 0;
 
     if (lx < a.tw && ly < a.th) {
         const int x = a.x0 + lx;
@@ -271,8 +272,12 @@ __global__ __launch_bounds__(256) void trace_simple(TraceArgs a) {
             int hit = -1;
             const V3 inv = {1.0f / d.x, 1.0f / d.y, 1.0f / d.z};          // :89
             int i = 0;
-            while (i < a.scene.end)
+            while (i < a.scene.end) {
                 i = node_step<COUNT>(a.scene.nodes, a.scene.tris, i, o, d, inv, closest, hit, c_node, c_tri);
+                // A wave still walking after prio_after steps holds the frame's
+                // critical path: let it win instruction arbitration.
+                if (++steps == a.prio_after) __builtin_amdgcn_s_setprio(3);
+            }
             if (hit >= 0) {                                               // :212
                 if (COUNT) ++c_mat;
                 const V3 n = hit_normal(a.scene.tris, hit, d);
