@@ -64,6 +64,16 @@ struct PathState {
     float4 q2;   // attenuation.z, seed (bits), bounce index b (bits), lx | ly << 16 (bits)
 };
 
+constexpr int kKernelTiered = 3;       // simple with a per-path visit budget; paths over budget
+                                       // are suspended mid-walk and finished by trace_coop (one
+                                       // wave per ray, 64-node windows, exact scalar replay)
+
+// A path suspended inside a segment (64 B): PathState + the walk's position.
+struct HeavyRay {
+    PathState p;
+    float4    q3;   // closest_t, next node (bits), hit triangle (bits), unused
+};
+
 struct TraceArgs {
     DevScene scene;
     CamF     cam;
@@ -88,6 +98,10 @@ struct TraceArgs {
     int      resume;            // persistent: take paths from spill[] instead of pixel tiles
     unsigned long long* diag;   // simple kernel diagnostics: 4 words per wave, or null
     int      prio_after;        // simple: raise wave priority after this many node steps (0 = never)
+    int      heavy_budget;      // simple: node visits per path before it is handed to the
+                                //   cooperative pass (<= 0: never)
+    HeavyRay* heavy;            // tiered: suspended heavy paths (capacity tw*th)
+    unsigned* heavy_count;      // tiered: number of heavy paths (zeroed before the simple pass)
 };
 
 // Host-side compact-scene build from the reference records; validates the

@@ -189,6 +189,8 @@ struct PerDevice {
     size_t       spill_cap = 0;
     unsigned long long* d_diag = nullptr;   // diagnostics (option "diag")
     size_t       diag_cap = 0, diag_used = 0;
+    HeavyRay*    d_heavy = nullptr; // tiered schedule: paths suspended over budget
+    size_t       heavy_cap = 0;
     int          n_cu = 0;
     int          blocks_per_cu = 1;
 };
@@ -204,6 +206,7 @@ struct rt_ctx {
     int  seg_limit = 2;            // split: segments traced in the lockstep pass
     int  diag = 0;                 // record per-wave timestamps (kernel 0 only)
     int  prio_after = 0;           // kernel 0: s_setprio(3) after this many node steps
+    int  heavy_budget = 256;       // tiered: node visits per path in tier 1
     bool has_scene = false;
     int  n_nodes = 0, n_tris = 0, max_depth = 0;
 };
@@ -258,6 +261,21 @@ static int set_schedule(const rt_ctx* ctx, PerDevice& p, TraceArgs& a) {
         }
         a.spill = p.d_spill;
     }
+    a.heavy_budget = 1 << 30;
+    a.heavy = nullptr;
+    a.heavy_count = p.d_queue + 2 * kQueueSlots + slot;
+    if (a.kernel == kKernelTiered) {
+        a.heavy_budget = ctx->heavy_budget;
+        const size_t need = (size_t)a.tw * (size_t)a.th;
+        if (need > p.heavy_cap) {
+            if (p.d_heavy) (void)hipFree(p.d_heavy);
+            p.d_heavy = nullptr;
+            p.heavy_cap = 0;
+            RT_HIP_CHECK(hipMalloc(&p.d_heavy, need * sizeof(HeavyRay)));
+            p.heavy_cap = need;
+        }
+        a.heavy = p.d_heavy;
+    }
     return RT_OK;
 }
 
@@ -289,7 +307,8 @@ int rt_create(const int* device_ids, int n_devices, rt_ctx** out) {
     if (!ctx) { set_error("rt_create: out of memory"); return RT_ERR_OOM; }
     if (const char* k = std::getenv("RTAMD_KERNEL"))
         ctx->kernel = std::strcmp(k, "simple") == 0 ? kKernelSimple
-                    : std::strcmp(k, "persistent") == 0 ? kKernelPersistent : kKernelSplit;
+                    : std::strcmp(k, "persistent") == 0 ? kKernelPersistent
+                    : std::strcmp(k, "split") == 0 ? kKernelSplit : kKernelTiered;
     if (const char* v = std::getenv("RTAMD_SEG_LIMIT")) ctx->seg_limit = std::max(1, std::min(1024, std::atoi(v)));
     if (const char* v = std::getenv("RTAMD_SHADE_MIN")) ctx->shade_min = std::max(1, std::min(64, std::atoi(v)));
     if (const char* v = std::getenv("RTAMD_BLOCKS_PER_CU")) ctx->blocks_per_cu = std::max(0, std::min(32, std::atoi(v)));
@@ -313,7 +332,7 @@ int rt_create(const int* device_ids, int n_devices, rt_ctx** out) {
         if (e == hipSuccess) e = hipEventCreate(&p.ev0);
         if (e == hipSuccess) e = hipEventCreate(&p.ev1);
         if (e == hipSuccess) e = hipMalloc(&p.d_counters, sizeof(Counters));
-        if (e == hipSuccess) e = hipMalloc(&p.d_queue, sizeof(unsigned) * 2 * kQueueSlots);
+        if (e == hipSuccess) e = hipMalloc(&p.d_queue, sizeof(unsigned) * 3 * kQueueSlots);
         p.n_cu = prop.multiProcessorCount;
         p.blocks_per_cu = persistent_blocks_per_cu();
         ctx->dev.push_back(p);
@@ -336,6 +355,8 @@ int rt_destroy(rt_ctx* ctx) {
         if (p.d_counters) (void)hipFree(p.d_counters);
         if (p.d_queue) (void)hipFree(p.d_queue);
         if (p.d_spill) (void)hipFree(p.d_spill);
+        if (p.d_heavy) (void)hipFree(p.d_heavy);
+        if (p.d_diag) (void)hipFree(p.d_diag);
         if (p.d_rgba) (void)hipFree(p.d_rgba);
         if (p.d_rad) (void)hipFree(p.d_rad);
         if (p.ev0) (void)hipEventDestroy(p.ev0);
@@ -605,7 +626,7 @@ int rt_render(rt_ctx* ctx, const rt_camera_ubo* cam, int width, int height, int 
 
 int rt_set_option(rt_ctx* ctx, const char* name, int64_t value) {
     if (!ctx || !name) { set_error("rt_set_option: null argument"); return RT_ERR_INVALID_ARG; }
-    if (std::strcmp(name, "kernel") == 0 && value >= kKernelSimple && value <= kKernelSplit) {
+    if (std::strcmp(name, "kernel") == 0 && value >= kKernelSimple && value <= kKernelTiered) {
         ctx->kernel = (int)value;
     } else if (std::strcmp(name, "shade_min") == 0 && value >= 1 && value <= 64) {
         ctx->shade_min = (int)value;
@@ -613,6 +634,8 @@ int rt_set_option(rt_ctx* ctx, const char* name, int64_t value) {
         ctx->blocks_per_cu = (int)value;
     } else if (std::strcmp(name, "seg_limit") == 0 && value >= 1 && value <= 1024) {
         ctx->seg_limit = (int)value;
+    } else if (std::strcmp(name, "heavy_budget") == 0 && value >= 1 && value <= (1 << 30)) {
+        ctx->heavy_budget = (int)value;
     } else if (std::strcmp(name, "prio_after") == 0 && value >= 0 && value <= (1 << 30)) {
         ctx->prio_after = (int)value;
     } else if (std::strcmp(name, "diag") == 0 && (value == 0 || value == 1)) {
@@ -633,6 +656,7 @@ int rt_get_option(rt_ctx* ctx, const char* name, int64_t* value) {
     else if (std::strcmp(name, "wave_tile") == 0) *value = ctx->wave_tile;
     else if (std::strcmp(name, "seg_limit") == 0) *value = ctx->seg_limit;
     else if (std::strcmp(name, "prio_after") == 0) *value = ctx->prio_after;
+    else if (std::strcmp(name, "heavy_budget") == 0) *value = ctx->heavy_budget;
     else if (std::strcmp(name, "blocks_per_cu") == 0)
         *value = ctx->blocks_per_cu > 0 ? ctx->blocks_per_cu : (ctx->dev.empty() ? 0 : ctx->dev[0].blocks_per_cu);
     else { set_error("rt_get_option: unknown option %s", name); return RT_ERR_INVALID_ARG; }

@@ -246,8 +246,7 @@ __global__ __launch_bounds__(256) void trace_simple(TraceArgs a) {
     const int lx = (blockIdx.x * 4 + wave) * tw_w + (lane & (tw_w - 1));
     const int ly = blockIdx.y * th_w + (lane >> (3 + s));
     unsigned long long c_seg = 0, c_node = 0, c_tri = 0, c_mat = 0;
-    bool spill = false;
-    PathState st;
+    bool spill = false, heavy = false;
     int steps = 0;
 
     if (lx < a.tw && ly < a.th) {
@@ -261,10 +260,11 @@ __global__ __launch_bounds__(256) void trace_simple(TraceArgs a) {
         for (int b = 0; b < a.max_bounces; ++b) {                         // :179
             if (b == a.seg_limit) {                                       // hand the path on
                 spill = true;
-                st.q0 = make_float4(o.x, o.y, o.z, att.x);
-                st.q1 = make_float4(d.x, d.y, d.z, att.y);
-                st.q2 = make_float4(att.z, __uint_as_float(seed), __int_as_float(b),
-                                    __int_as_float(lx | (ly << 16)));
+                PathState* st = a.spill + atomicAdd(a.spill_count, 1u);
+                st->q0 = make_float4(o.x, o.y, o.z, att.x);
+                st->q1 = make_float4(d.x, d.y, d.z, att.y);
+                st->q2 = make_float4(att.z, __uint_as_float(seed), __int_as_float(b),
+                                     __int_as_float(lx | (ly << 16)));
                 break;
             }
             if (COUNT) ++c_seg;
@@ -277,7 +277,18 @@ __global__ __launch_bounds__(256) void trace_simple(TraceArgs a) {
                 // A wave still walking after prio_after steps holds the frame's
                 // critical path: let it win instruction arbitration.
                 if (++steps == a.prio_after) __builtin_amdgcn_s_setprio(3);
+                if (steps >= a.heavy_budget && i < a.scene.end) {         // hand the walk on
+                    heavy = true;
+                    HeavyRay* hv = a.heavy + atomicAdd(a.heavy_count, 1u);
+                    hv->p.q0 = make_float4(o.x, o.y, o.z, att.x);
+                    hv->p.q1 = make_float4(d.x, d.y, d.z, att.y);
+                    hv->p.q2 = make_float4(att.z, __uint_as_float(seed), __int_as_float(b),
+                                           __int_as_float(lx | (ly << 16)));
+                    hv->q3 = make_float4(closest, __int_as_float(i), __int_as_float(hit), 0.0f);
+                    break;
+                }
             }
+            if (heavy) break;
             if (hit >= 0) {                                               // :212
                 if (COUNT) ++c_mat;
                 const V3 n = hit_normal(a.scene.tris, hit, d);
@@ -294,16 +305,7 @@ __global__ __launch_bounds__(256) void trace_simple(TraceArgs a) {
             }
             if (b == a.max_bounces - 1) fin = {0.0f, 0.0f, 0.0f};        // :229-231
         }
-        if (!spill) write_pixel(a, lx, ly, fin);
-    }
-    // Append this wave's live paths to the spill queue (one atomic per wave);
-    // lanes keep their tile order, so neighbouring paths stay neighbours.
-    const uint64_t sm = __ballot(spill);
-    if (sm != 0) {
-        unsigned base = 0;
-        if (lane == 0) base = atomicAdd(a.spill_count, (unsigned)__popcll(sm));
-        base = __shfl(base, 0);
-        if (spill) a.spill[base + lanes_below(sm)] = st;
+        if (!spill && !heavy) write_pixel(a, lx, ly, fin);
     }
     if (COUNT) flush_counters(a.counters, c_seg, c_node, c_tri, c_mat);
     if (DIAG) diag_stamp(drec, 1);
@@ -436,6 +438,153 @@ __global__ __launch_bounds__(256) void trace_persistent(TraceArgs a) {
     if (COUNT) flush_counters(a.counters, c_seg, c_node, c_tri, c_mat);
 }
 
+// ------------------------------------------------------- cooperative kernel --
+//
+// One wave walks ONE ray.  The walk is the reference's preorder visit sequence
+// (compute_dynamic_ray.comp:185-210), replayed exactly:
+//   1. lane k loads node n+k of the window [n, n+64) (2 KB, coalesced) and
+//      computes its slab test; leaves whose box is hit at the current
+//      closest_t also run the triangle test up to (but not including) the
+//      "t < closest_t" compare (:105-122);
+//   2. ballots turn "box hit at closest_t" (H), "triangle hit that improves
+//      closest_t" (T) and "is a leaf" (Lf) into 64-bit masks;
+//   3. the scalar unit replays the walk through the window: node k is hit iff
+//      bit k of H; next = k+1 on a hit, skip(k) on a miss; a triangle hit
+//      updates closest_t / hit and re-ballots H and T (closest_t only shrinks,
+//      so a leaf not pre-tested at the old closest_t cannot hit at the new one).
+// Box and triangle tests are the same float operations as node_step, so
+// closest_t, the hit and the visit / test counts equal the per-lane walk's.
+
+__device__ __forceinline__ int lane_i(int v, int k) { return __builtin_amdgcn_readlane(v, k); }
+__device__ __forceinline__ float lane_f(float v, int k) {
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), k));
+}
+
+template <bool COUNT>
+__device__ __forceinline__ void coop_walk(const float4* __restrict__ nodes, const float4* __restrict__ tris,
+                                          int end, int n, V3 o, V3 d, V3 inv, float& closest, int& hit,
+                                          unsigned long long& c_node, unsigned long long& c_tri) {
+    const int lane = threadIdx.x & 63;
+    while (n < end) {
+        const int j = n + lane;
+        float te = 0.0f, tt = 0.0f;
+        int sk = 0, lf = -1;
+        bool ind = false, tv = false;
+        if (j < end) {
+            const float4 A = nodes[2 * j];
+            const float4 B = nodes[2 * j + 1];
+            const float t0x = (A.x - o.x) * inv.x, t1x = (B.x - o.x) * inv.x;
+            const float t0y = (A.y - o.y) * inv.y, t1y = (B.y - o.y) * inv.y;
+            const float t0z = (A.z - o.z) * inv.z, t1z = (B.z - o.z) * inv.z;
+            te = fmaxf(fmaxf(fminf(t0x, t1x), fminf(t0y, t1y)), fminf(t0z, t1z));
+            const float tx = fminf(fminf(fmaxf(t0x, t1x), fmaxf(t0y, t1y)), fmaxf(t0z, t1z));
+            ind = tx > te && tx > kTMin;
+            sk = __float_as_int(A.w);
+            lf = __float_as_int(B.w);
+            if (ind && lf >= 0 && te < closest) {
+                const float4 P0 = tris[3 * lf + 0];
+                const float4 P1 = tris[3 * lf + 1];
+                const float4 P2 = tris[3 * lf + 2];
+                const V3 v0 = {P0.x, P0.y, P0.z};
+                const V3 e1 = {P1.x, P1.y, P1.z};
+                const V3 e2 = {P2.x, P2.y, P2.z};
+                const V3 pv = vcross(d, e2);
+                const float det = vdot(e1, pv);
+                if (!(det > -0.00001f && det < 0.00001f)) {
+                    const float inv_det = 1.0f / det;
+                    const V3 s = vsub(o, v0);
+                    const float uu = inv_det * vdot(s, pv);
+                    if (!(uu < 0.0f || uu > 1.0f)) {
+                        const V3 q = vcross(s, e1);
+                        const float vv = inv_det * vdot(d, q);
+                        if (!(vv < 0.0f || (uu + vv) > 1.0f)) {
+                            tt = inv_det * vdot(e2, q);
+                            tv = tt > kTMin;
+                        }
+                    }
+                }
+            }
+        }
+        uint64_t H = __ballot(ind && te < closest);
+        uint64_t T = __ballot(tv && tt < closest);
+        const uint64_t Lf = __ballot(lf >= 0);
+        const int lim = min(64, end - n);
+        int k = 0;
+        while (k < lim) {
+            if (COUNT) ++c_node;
+            if ((H >> k) & 1ull) {
+                if ((Lf >> k) & 1ull) {
+                    if (COUNT) ++c_tri;
+                    if ((T >> k) & 1ull) {
+                        closest = lane_f(tt, k);
+                        hit = lane_i(lf, k);
+                        H = __ballot(ind && te < closest);
+                        T = __ballot(tv && tt < closest);
+                    }
+                }
+                ++k;
+            } else {
+                k = lane_i(sk, k) - n;
+            }
+        }
+        n += k;
+    }
+}
+
+template <bool COUNT>
+__global__ __launch_bounds__(256) void trace_coop(TraceArgs a) {
+    const int lane = threadIdx.x & 63;
+    const int end = a.scene.end;
+    const int n_rays = (int)*a.heavy_count;
+    unsigned long long c_seg = 0, c_node = 0, c_tri = 0, c_mat = 0;   // wave-uniform
+    for (;;) {
+        int r = 0;
+        if (lane == 0) r = (int)atomicAdd(a.queue, 1u);
+        r = __builtin_amdgcn_readfirstlane(r);
+        if (r >= n_rays) break;
+        const HeavyRay hv = a.heavy[r];
+        V3 o = {hv.p.q0.x, hv.p.q0.y, hv.p.q0.z};
+        V3 d = {hv.p.q1.x, hv.p.q1.y, hv.p.q1.z};
+        V3 att = {hv.p.q0.w, hv.p.q1.w, hv.p.q2.x};
+        uint32_t seed = __float_as_uint(hv.p.q2.y);
+        int b = __float_as_int(hv.p.q2.z);
+        const int pix = __float_as_int(hv.p.q2.w);
+        float closest = hv.q3.x;
+        int node = __float_as_int(hv.q3.y);
+        int hit = __float_as_int(hv.q3.z);
+        V3 fin = {0.0f, 0.0f, 0.0f};
+        for (;;) {
+            const V3 inv = {1.0f / d.x, 1.0f / d.y, 1.0f / d.z};
+            coop_walk<COUNT>(a.scene.nodes, a.scene.tris, end, node, o, d, inv, closest, hit, c_node, c_tri);
+            if (hit < 0) {
+                fin = vmul(att, sky_color(d));
+                break;
+            }
+            if (COUNT) ++c_mat;
+            const V3 n = hit_normal(a.scene.tris, hit, d);
+            const V3 hp = vadd(o, vscale(d, closest));
+            const float4 M = a.scene.mats[hit];
+            V3 nd;
+            if (!scatter(M, d, n, seed, nd) || b == a.max_bounces - 1) break;   // black
+            att = vmul(att, V3{M.x, M.y, M.z});
+            o = hp;
+            d = nd;
+            ++b;
+            closest = kTMax;
+            hit = -1;
+            node = 0;
+            if (COUNT) ++c_seg;
+        }
+        if (lane == 0) write_pixel(a, pix & 0xFFFF, pix >> 16, fin);
+    }
+    if (COUNT && lane == 0) {
+        atomicAdd(&a.counters->segments, c_seg);
+        atomicAdd(&a.counters->node_visits, c_node);
+        atomicAdd(&a.counters->tri_tests, c_tri);
+        atomicAdd(&a.counters->mat_reads, c_mat);
+    }
+}
+
 }  // namespace
 
 int persistent_blocks_per_cu() {
@@ -447,6 +596,23 @@ int persistent_blocks_per_cu() {
 
 hipError_t launch_trace(const TraceArgs& a, hipStream_t stream) {
     const dim3 block(256);
+    if (a.kernel == kKernelTiered) {
+        // tier 1: lockstep tiles; paths over the visit budget are suspended
+        TraceArgs s = a;
+        s.kernel = kKernelSimple;
+        hipError_t e = hipMemsetAsync(a.heavy_count, 0, sizeof(unsigned), stream);
+        if (e != hipSuccess) return e;
+        e = launch_trace(s, stream);
+        if (e != hipSuccess) return e;
+        // tier 2: one wave per suspended path
+        e = hipMemsetAsync(a.queue, 0, sizeof(unsigned), stream);
+        if (e != hipSuccess) return e;
+        if (a.counters)
+            hipLaunchKernelGGL(trace_coop<true>, dim3(a.grid_blocks), block, 0, stream, a);
+        else
+            hipLaunchKernelGGL(trace_coop<false>, dim3(a.grid_blocks), block, 0, stream, a);
+        return hipGetLastError();
+    }
     if (a.kernel == kKernelSplit) {
         // pass 1: coherent 8x8 lockstep tiles for the first seg_limit segments
         TraceArgs s = a;

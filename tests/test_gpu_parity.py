@@ -13,7 +13,8 @@ from conftest import has_gpu
 pytestmark = pytest.mark.gpu
 
 COUNTERS = ("segments", "node_visits", "tri_tests", "mat_reads")
-DEFAULT_OPTS = {"kernel": 1, "shade_min": 16, "blocks_per_cu": 0, "wave_tile": 0, "seg_limit": 2}
+DEFAULT_OPTS = {"kernel": 3, "shade_min": 16, "blocks_per_cu": 0, "wave_tile": 0, "seg_limit": 2,
+                "heavy_budget": 256}
 
 
 def _oracle(built, cam_bytes, w, h, b, **kw):
@@ -117,6 +118,9 @@ def test_config5_1m_row_subset(renderer):
     {"kernel": 2, "seg_limit": 1},
     {"kernel": 2, "seg_limit": 2},
     {"kernel": 2, "seg_limit": 3, "shade_min": 1},
+    {"kernel": 3, "heavy_budget": 1},
+    {"kernel": 3, "heavy_budget": 40},
+    {"kernel": 3, "heavy_budget": 256},
 ])
 def test_schedules_identical(renderer, opts):
     """Every schedule gives the oracle's frame and counters (config 2 at the
