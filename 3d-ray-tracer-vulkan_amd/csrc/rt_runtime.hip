@@ -185,6 +185,7 @@ struct PerDevice {
     size_t       out_cap = 0;      // pixels
     unsigned*    d_queue = nullptr; // ring of kQueueSlots work counters + kQueueSlots spill counters
     unsigned     queue_slot = 0;
+    unsigned     last_slot = 0;
     PathState*   d_spill = nullptr; // split schedule: suspended paths
     size_t       spill_cap = 0;
     unsigned long long* d_diag = nullptr;   // diagnostics (option "diag")
@@ -226,6 +227,7 @@ static int set_schedule(const rt_ctx* ctx, PerDevice& p, TraceArgs& a) {
     a.seg_limit = ctx->kernel == kKernelSplit ? ctx->seg_limit : (1 << 30);
     a.resume = 0;
     const unsigned slot = p.queue_slot++ % kQueueSlots;
+    p.last_slot = slot;
     a.queue = p.d_queue + slot;
     a.spill_count = p.d_queue + kQueueSlots + slot;
     const int bpc = ctx->blocks_per_cu > 0 ? ctx->blocks_per_cu : p.blocks_per_cu;
@@ -448,6 +450,8 @@ static int ensure_out(PerDevice& p, size_t pixels, bool rad) {
     return RT_OK;
 }
 
+static int collect_stats(const rt_ctx* ctx, PerDevice& p, uint64_t pixels, rt_stats* stats, bool accumulate);
+
 int rt_render_tile_device(rt_ctx* ctx, const rt_camera_ubo* cam, int width, int height,
                           int max_bounces, int x0, int y0, int tile_w, int tile_h,
                           void* d_out_rgba, void* d_out_radiance, void* stream, rt_stats* stats) {
@@ -480,16 +484,7 @@ int rt_render_tile_device(rt_ctx* ctx, const rt_camera_ubo* cam, int width, int 
     if (stats) {
         RT_HIP_CHECK(hipEventRecord(p.ev1, s));
         RT_HIP_CHECK(hipEventSynchronize(p.ev1));
-        Counters c;
-        RT_HIP_CHECK(hipMemcpy(&c, p.d_counters, sizeof c, hipMemcpyDeviceToHost));
-        float ms = 0.f;
-        RT_HIP_CHECK(hipEventElapsedTime(&ms, p.ev0, p.ev1));
-        stats->pixels = (uint64_t)tile_w * (uint64_t)tile_h;
-        stats->segments = c.segments;
-        stats->node_visits = c.node_visits;
-        stats->tri_tests = c.tri_tests;
-        stats->mat_reads = c.mat_reads;
-        stats->ms = ms;
+        return collect_stats(ctx, p, (uint64_t)tile_w * (uint64_t)tile_h, stats, false);
     }
     return RT_OK;
 }
@@ -524,9 +519,14 @@ static int render_bands_on(const rt_ctx* ctx, PerDevice& p, const rt_camera_ubo*
     return RT_OK;
 }
 
-static int collect_stats(PerDevice& p, uint64_t pixels, rt_stats* stats, bool accumulate) {
+static int collect_stats(const rt_ctx* ctx, PerDevice& p, uint64_t pixels, rt_stats* stats, bool accumulate) {
     Counters c;
     RT_HIP_CHECK(hipMemcpy(&c, p.d_counters, sizeof c, hipMemcpyDeviceToHost));
+    unsigned handoffs = 0;
+    if (ctx->kernel == kKernelSplit || ctx->kernel == kKernelTiered) {
+        const unsigned* src = p.d_queue + (ctx->kernel == kKernelSplit ? 1 : 2) * kQueueSlots + p.last_slot;
+        RT_HIP_CHECK(hipMemcpy(&handoffs, src, sizeof handoffs, hipMemcpyDeviceToHost));
+    }
     float ms = 0.f;
     RT_HIP_CHECK(hipEventElapsedTime(&ms, p.ev0, p.ev1));
     if (!accumulate) std::memset(stats, 0, sizeof *stats);
@@ -535,6 +535,7 @@ static int collect_stats(PerDevice& p, uint64_t pixels, rt_stats* stats, bool ac
     stats->node_visits += c.node_visits;
     stats->tri_tests += c.tri_tests;
     stats->mat_reads += c.mat_reads;
+    stats->handoffs += handoffs;
     if (ms > stats->ms) stats->ms = ms;
     return RT_OK;
 }
@@ -561,7 +562,7 @@ int rt_render_bands_device(rt_ctx* ctx, const rt_camera_ubo* cam, int width, int
     if (rc) return rc;
     if (stats) {
         RT_HIP_CHECK(hipEventSynchronize(p.ev1));
-        return collect_stats(p, (uint64_t)rows * width, stats, false);
+        return collect_stats(ctx, p, (uint64_t)rows * width, stats, false);
     }
     return RT_OK;
 }
@@ -617,7 +618,7 @@ int rt_render(rt_ctx* ctx, const rt_camera_ubo* cam, int width, int height, int 
             }
         }
         if (stats) {
-            rc = collect_stats(p, px, stats, true);
+            rc = collect_stats(ctx, p, px, stats, true);
             if (rc) return rc;
         }
     }

@@ -63,6 +63,7 @@ class Stats(C.Structure):
         ("tri_tests", C.c_uint64),
         ("mat_reads", C.c_uint64),
         ("ms", C.c_double),
+        ("handoffs", C.c_uint64),
     ]
 
     def as_dict(self) -> dict:

@@ -69,6 +69,7 @@ typedef struct rt_stats {
     uint64_t tri_tests;
     uint64_t mat_reads;
     double   ms;          /* device time of the trace kernel(s), HIP events */
+    uint64_t handoffs;    /* paths handed to a second pass (split / tiered schedules) */
 } rt_stats;
 
 /* ---------------------------------------------------------------- engine -- */

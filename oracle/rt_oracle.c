@@ -46,6 +46,11 @@
 #define MAX_REJECT_TRIPLES 65536
 #define STACK_SIZE 64                /* :185 */
 
+/* visit tracing (orc_trace_pixel; analysis aid, single-threaded use only) */
+static int32_t* g_trace = NULL;
+static int g_trace_cap = 0, g_trace_n = 0;
+static void trace_rec(int32_t v) { if (g_trace && g_trace_n < g_trace_cap) g_trace[g_trace_n++] = v; }
+
 typedef struct { float x, y, z; } vec3;
 
 static vec3 v3(float x, float y, float z) { vec3 r = {x, y, z}; return r; }
@@ -213,6 +218,7 @@ static int shade_pixel(const scene* s, const orc_camera* cam, int W, int H, int 
     vec3 attenuation = v3(1.0f, 1.0f, 1.0f);
     for (int b = 0; b < max_bounces; ++b) {                                    /* :179 */
         cnt->segments++;
+        trace_rec(-(b + 1));
         const uint64_t nv0 = cnt->node_visits, tt0 = cnt->tri_tests;
         float closest_t = T_MAX;
         int hit_triangle_index = -1;
@@ -228,6 +234,7 @@ static int shade_pixel(const scene* s, const orc_camera* cam, int W, int H, int 
             vec3 bmax = v3(f32_at(nd, 16), f32_at(nd, 20), f32_at(nd, 24));
             int32_t data = i32_at(nd, 32), count = i32_at(nd, 36);
             cnt->node_visits++;
+            trace_rec(node_index);
             if (hit_aabb(r, bmin, bmax, T_MIN, closest_t)) {
                 if (count < 0) {
                     int tri = -(data + 1);
@@ -382,4 +389,27 @@ int orc_scatter(const float material[4], uint32_t* seed, const float dir_in[3],
     att[0] = a.x; att[1] = a.y; att[2] = a.z;
     dir_out[0] = sc.dir.x; dir_out[1] = sc.dir.y; dir_out[2] = sc.dir.z;
     return ok;
+}
+
+/* Analysis aid: the node visit sequence of one pixel's path (segment k's
+ * visits follow a -(k+1) marker).  Returns the number of entries written, or
+ * -1.  Single-threaded; same arithmetic as orc_render. */
+int orc_trace_pixel(const void* vertices, size_t vertex_bytes, const void* materials, size_t material_bytes,
+                    const void* bvh_nodes, size_t bvh_bytes, const orc_camera* cam, int width, int height,
+                    int max_bounces, int px, int py, int32_t* out, int cap) {
+    scene s;
+    s.verts = (const unsigned char*)vertices;
+    s.mats = (const unsigned char*)materials;
+    s.nodes = (const unsigned char*)bvh_nodes;
+    s.n_nodes = bvh_bytes / 48;
+    s.n_tris = vertex_bytes / 48;
+    s.n_mats = material_bytes / 16;
+    g_trace = out;
+    g_trace_cap = cap;
+    g_trace_n = 0;
+    orc_counts c = {0, 0, 0, 0, 0};
+    float rgb[3];
+    int rc = shade_pixel(&s, cam, width, height, max_bounces, px, py, rgb, &c, NULL);
+    g_trace = NULL;
+    return rc ? -1 : g_trace_n;
 }

@@ -36,7 +36,7 @@ def main():
         t0 = time.time()
         st = r.render_tile_device(cam, W, H, B, 0, 0, W, H, out.data_ptr(), None, None, stats=True)
         print(f"{args.variant} launch {i}: {1e3 * (time.time() - t0):.2f} ms wall, {st['ms']:.3f} ms events, "
-              f"segments {st['segments']} visits {st['node_visits']}", flush=True)
+              f"segments {st['segments']} visits {st['node_visits']} handoffs {st['handoffs']}", flush=True)
     r.close()
 
 
