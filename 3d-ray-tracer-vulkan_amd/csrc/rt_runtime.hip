@@ -200,10 +200,10 @@ static constexpr unsigned kQueueSlots = 64;
 
 struct rt_ctx {
     std::vector<PerDevice> dev;
-    int  kernel = kKernelPersistent;
+    int  kernel = kKernelSimple;   // fastest measured on config 3
     int  shade_min = 16;
     int  blocks_per_cu = 0;        // 0 = from the occupancy query
-    int  wave_tile = 0;            // simple kernel: 8x8 / 16x4 / 32x2 / 64x1
+    int  wave_tile = 2;            // simple kernel: 8x8 / 16x4 / 32x2 (default) / 64x1
     int  seg_limit = 2;            // split: segments traced in the lockstep pass
     int  diag = 0;                 // record per-wave timestamps (kernel 0 only)
     int  prio_after = 0;           // kernel 0: s_setprio(3) after this many node steps

@@ -1,0 +1,87 @@
+"""Multi-GPU frame tiling: one process per GPU (torch.distributed; backend
+"nccl" = RCCL over xGMI on MI355X, "gloo" for CPU tests).
+
+The frame is split into interleaved row bands: rank r of N traces the
+band_h-row bands r, r+N, r+2N, ... (so sky rows and geometry rows spread
+evenly over the ranks).  The scene is replicated on every rank (uploaded once
+per rank); pixels are independent and seeded by their global (x, y)
+(compute_dynamic_ray.comp:164), so the assembled frame equals the one-GPU
+frame bit for bit.  The one exchange is a gather of each rank's packed band
+rows to rank 0, which scatters them into the frame.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import Callable, Optional
+
+import numpy as np
+
+from ._lib import check, lib
+
+
+def band_row_count(height: int, band_h: int, world: int, rank: int) -> int:
+    n = lib().rt_band_rows(height, band_h, world, rank)
+    if n < 0:
+        raise ValueError("bad band partition")
+    return n
+
+
+def band_rows(height: int, band_h: int, world: int, rank: int) -> np.ndarray:
+    """Frame rows of rank's bands, in the packed order the kernels write them."""
+    y = np.arange(height)
+    return y[(y // band_h) % world == rank]
+
+
+def gather_frame(local, height: int, band_h: int, group=None):
+    """Gather every rank's packed band rows (torch tensor [rows_r, W, C]) to
+    rank 0 and assemble the [height, W, C] frame there (None elsewhere)."""
+    import torch
+    import torch.distributed as dist
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    counts = [band_row_count(height, band_h, world, r) for r in range(world)]
+    max_rows = max(counts)
+    if local.shape[0] < max_rows:
+        pad = torch.zeros((max_rows - local.shape[0],) + tuple(local.shape[1:]), dtype=local.dtype,
+                          device=local.device)
+        local = torch.cat([local, pad])
+    gl = [torch.empty_like(local) for _ in range(world)] if rank == 0 else None
+    dist.gather(local, gl, dst=0, group=group)
+    if rank != 0:
+        return None
+    out = torch.empty((height,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
+    for r in range(world):
+        rows = torch.as_tensor(band_rows(height, band_h, world, r), device=local.device)
+        out[rows] = gl[r][: counts[r]]
+    return out
+
+
+class DistRenderer:
+    """Renders frames over all ranks: each rank traces its bands on its GPU
+    with rt_render_bands_device, then gather_frame assembles rank 0's copy."""
+
+    def __init__(self, renderer, band_h: int = 16, group=None):
+        import torch
+        import torch.distributed as dist
+        self.r = renderer
+        self.band_h = band_h
+        self.group = group
+        self.world = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
+        self.device = torch.device("cuda", torch.cuda.current_device())
+
+    def trace_local(self, camera, width: int, height: int, max_bounces: int, out=None, stream=None):
+        import torch
+        from .engine import _ubo
+        rows = band_row_count(height, self.band_h, self.world, self.rank)
+        if out is None:
+            out = torch.empty((rows, width, 4), dtype=torch.uint8, device=self.device)
+        s = stream if stream is not None else torch.cuda.current_stream(self.device)
+        check(lib().rt_render_bands_device(self.r._ctx, C.byref(_ubo(camera)), width, height, max_bounces,
+                                           self.band_h, self.world, self.rank, out.data_ptr(), None,
+                                           s.cuda_stream, None))
+        return out
+
+    def render(self, camera, width: int, height: int, max_bounces: int):
+        local = self.trace_local(camera, width, height, max_bounces)
+        return gather_frame(local, height, self.band_h, self.group)

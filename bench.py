@@ -98,7 +98,7 @@ def main() -> None:
                                        C.byref(s) if stats else None))
         return s.as_dict() if stats else None
 
-    gather_list = [torch.empty_like(d_rgba) for _ in range(world)] if (world > 1 and rank == 0) else None
+    from rtamd.dist import gather_frame
 
     def step(ev=None):
         if ev is not None:
@@ -107,7 +107,7 @@ def main() -> None:
         if ev is not None:
             ev[1].record(stream)
         if world > 1:
-            dist.gather(d_rgba, gather_list, dst=0)
+            gather_frame(d_rgba[:rows], H, band_h)     # RCCL gather + rank-0 assembly of the frame
 
     # Counting pass (untimed): this rank's work, then the frame totals.
     st = trace(stats=True)
@@ -177,7 +177,8 @@ def main() -> None:
                 "segments_per_frame": int(segments),
                 "node_visits_per_segment": round(node_visits / segments, 3),
                 "tri_tests_per_segment": round(tri_tests / segments, 4),
-                "partition": "single frame" if world == 1 else f"interleaved {band_h}-row bands, dist.gather to rank 0",
+                "partition": "single frame" if world == 1 else
+                             f"interleaved {band_h}-row bands, RCCL gather + assembly on rank 0",
                 "parallelism": f"tile{world}",
                 "schedule": {k: renderer.get_option(k) for k in ("kernel", "shade_min", "blocks_per_cu")},
             },

@@ -1,0 +1,114 @@
+"""The C ABI library (no GPU needed): it loads, exports every symbol
+include/rtamd.h declares, validates scenes and reports errors."""
+import ctypes as C
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+from conftest import has_gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "rtamd.h")
+
+
+def header_symbols():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return set(re.findall(r"\b(rt_[a-z_0-9]+)\s*\(", src))
+
+
+def test_library_exports_every_header_symbol():
+    from rtamd import LIB_PATH, lib
+    lib()
+    out = subprocess.run(["nm", "-D", "--defined-only", LIB_PATH], capture_output=True, text=True, check=True).stdout
+    exported = set(re.findall(r"\bT (rt_[a-z_0-9]+)$", out, flags=re.M))
+    syms = header_symbols()
+    assert len(syms) >= 20
+    assert syms <= exported, syms - exported
+    from rtamd._lib import EXPORTED
+    assert set(EXPORTED) == syms
+
+
+def test_library_is_gfx950_code_object():
+    from rtamd import LIB_PATH
+    data = open(LIB_PATH, "rb").read()
+    assert b"gfx950" in data and b"trace_simple" in data and b"trace_coop" in data
+
+
+def test_structs_match_reference_bytes():
+    from rtamd import CameraUBO, Stats
+    assert C.sizeof(CameraUBO) == 80              # VulkanEngine.java createCameraUbo: 80 bytes
+    assert CameraUBO.vertical.offset == 48 and CameraUBO.frame_count.offset == 64
+    assert CameraUBO.sky_enabled.offset == 68
+    assert Stats.ms.offset == 40
+
+
+@pytest.mark.skipif(has_gpu(), reason="only meaningful without a GPU")
+def test_no_cpu_fallback():
+    from rtamd import Renderer, RtError
+    with pytest.raises(RtError, match="NO_DEVICE|HIP"):
+        Renderer((0,))
+    with pytest.raises(RtError, match="INVALID_ARG"):
+        Renderer(())
+
+
+def _validate(v, m, n):
+    from rtamd import lib
+    from rtamd._lib import check
+    nn, d = C.c_size_t(), C.c_int()
+    v, m, n = (np.ascontiguousarray(x) for x in (v, m, n))
+    check(lib().rt_scene_validate(v.ctypes.data, v.nbytes, m.ctypes.data, m.nbytes, n.ctypes.data, n.nbytes,
+                                  C.byref(nn), C.byref(d)))
+    return nn.value, d.value
+
+
+def test_scene_validation():
+    from rtamd import RtError, configs
+    b = configs.config2().build()
+    v, m, n = b.model_vertex_data, b.model_material_data, b.flat_bvh_data
+    assert _validate(v, m, n) == (31, 4)
+    # the reference's empty-scene dummies (SceneBuilder.java:61-70) are an empty scene
+    assert _validate(np.zeros(1, np.float32), np.zeros(1, np.float32), np.zeros(1, np.uint8))[0] == 0
+    bad = n.copy().view(np.int32).reshape(-1, 12)
+    bad[0, 8] = 3                                  # left child must be i+1
+    with pytest.raises(RtError, match="BAD_SCENE.*preorder"):
+        _validate(v, m, bad)
+    bad = n.copy().view(np.int32).reshape(-1, 12)
+    leaf = np.nonzero(bad[:, 9] < 0)[0][0]
+    bad[leaf, 8] = -(1000 + 1)                     # triangle 1000 does not exist
+    with pytest.raises(RtError, match="BAD_SCENE.*triangle 1000"):
+        _validate(v, m, bad)
+    with pytest.raises(RtError, match="BAD_SCENE.*material|BAD_SCENE.*outside"):
+        _validate(v, m[:4], n)                     # materials shorter than the triangles used
+    with pytest.raises(RtError, match="multiple of 48"):
+        _validate(v, m, n[:-8])
+
+
+def test_band_rows():
+    from rtamd import lib
+    from rtamd.dist import band_rows
+    for h in (1, 7, 16, 720, 1080, 2160):
+        for bh in (1, 16, 64):
+            for world in (1, 2, 3, 4, 8):
+                rows = [lib().rt_band_rows(h, bh, world, r) for r in range(world)]
+                assert sum(rows) == h
+                for r in range(world):
+                    assert len(band_rows(h, bh, world, r)) == rows[r]
+    assert lib().rt_band_rows(10, 0, 1, 0) == -1
+    assert lib().rt_band_rows(10, 4, 2, 2) == -1
+
+
+def test_error_message_is_thread_local():
+    import threading
+    from rtamd import lib
+    L = lib()
+    L.rt_set_option(None, b"kernel", 0)
+    msg = L.rt_last_error()
+    seen = []
+    t = threading.Thread(target=lambda: seen.append(L.rt_last_error()))
+    t.start()
+    t.join()
+    assert b"null" in msg and seen == [b""]

@@ -13,7 +13,7 @@ from conftest import has_gpu
 pytestmark = pytest.mark.gpu
 
 COUNTERS = ("segments", "node_visits", "tri_tests", "mat_reads")
-DEFAULT_OPTS = {"kernel": 3, "shade_min": 16, "blocks_per_cu": 0, "wave_tile": 0, "seg_limit": 2,
+DEFAULT_OPTS = {"kernel": 0, "shade_min": 16, "blocks_per_cu": 0, "wave_tile": 2, "seg_limit": 2,
                 "heavy_budget": 256}
 
 
@@ -264,3 +264,20 @@ def test_hip_engine_publishes_frames():
     assert frame is not None and frame.pixel_data.shape == (180, 320, 4)
     ref = _oracle(built, cam.ubo_bytes(), 320, 180, 3)[0]
     assert np.array_equal(frame.pixel_data, ref)
+
+
+def test_golden_frames_on_gpu(renderer):
+    """The GPU reproduces the committed golden frames (tests/golden/golden.json)."""
+    import hashlib
+    import json
+    import os
+    from rtamd import configs
+    g_all = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "golden.json")))["frames"]
+    for name, g in g_all.items():
+        renderer.upload_scene(configs.get(g["config"]).build())
+        cam = configs.Camera.default(g["width"], g["height"])
+        rgba, rad, st = renderer.render(cam, g["width"], g["height"], g["max_bounces"], radiance=True, stats=True)
+        assert hashlib.sha256(rgba.tobytes()).hexdigest() == g["rgba_sha256"], name
+        assert hashlib.sha256(rad.tobytes()).hexdigest() == g["radiance_sha256"], name
+        for k in COUNTERS:
+            assert st[k] == g["counts"][k], (name, k)

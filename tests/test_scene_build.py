@@ -1,0 +1,196 @@
+"""Host scene pipeline (CPU): the product's C++ builder vs the Python
+restatement of the Java code (oracle/scene_oracle.py), byte for byte."""
+import json
+import os
+import random
+
+import numpy as np
+import pytest
+
+from conftest import reference_path
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+GOLDEN = json.load(open(os.path.join(HERE, "golden", "golden.json")))
+
+
+def _oracle_build(verts, mats, seed):
+    from oracle import scene_oracle
+    tris = [(tuple(v[0:3]), tuple(v[3:6]), tuple(v[6:9]), tuple(m)) for v, m in zip(verts.tolist(), mats.tolist())]
+    return scene_oracle.build_scene(tris, seed)
+
+
+def _same(built, ref):
+    vb, mb, bb, nf = ref
+    assert built.triangle_count == nf
+    assert built.model_vertex_data.tobytes() == vb
+    assert built.model_material_data.tobytes() == mb
+    assert built.flat_bvh_data.tobytes() == bb
+
+
+def test_layout_sizes():
+    from oracle import scene_oracle
+    import ctypes as C
+    from rtamd import lib
+    for n in list(range(0, 300)) + [1000, 4097, 50_000, 1_000_000]:
+        nn, nf = C.c_size_t(), C.c_size_t()
+        assert lib().rt_bvh_layout_size(n, C.byref(nn), C.byref(nf)) == 0
+        assert (nn.value, nf.value) == scene_oracle.layout_size(n)
+        if n:
+            assert nn.value == 2 * nf.value - 1          # full binary tree
+
+
+@pytest.mark.parametrize("k", [1, 2])
+def test_config_scenes_match_restatement(k):
+    from rtamd import configs, build_buffers, triangles_of
+    cfg = configs.get(k)
+    verts, mats = triangles_of(cfg.scene)
+    for seed in (1, 2, 12345):
+        _same(build_buffers(verts, mats, seed), _oracle_build(verts, mats, seed))
+
+
+def _random_tris(n, rng, grid=False):
+    if grid:   # many exactly tied centroids, flat (axis-aligned) triangles, negative zeros
+        pts = rng.integers(-3, 4, size=(n, 3, 3)).astype(np.float64)
+        pts[rng.random((n, 3, 3)) < 0.1] = -0.0
+        pts[rng.random(n) < 0.3, :, 1] = 0.0
+    else:
+        pts = rng.normal(size=(n, 3, 3)) * rng.uniform(0.1, 10, size=(n, 1, 1))
+    mats = rng.random((n, 4)).astype(np.float32)
+    mats[:, 3] = rng.integers(0, 4, n)
+    return pts.reshape(n, 9), mats
+
+
+@pytest.mark.parametrize("n", [1, 2, 3, 4, 5, 7, 16, 17, 100, 257, 1500])
+@pytest.mark.parametrize("grid", [False, True])
+def test_random_scenes_match_restatement(n, grid):
+    from rtamd import build_buffers
+    rng = np.random.default_rng(n * 7 + grid)
+    verts, mats = _random_tris(n, rng, grid)
+    seed = int(rng.integers(0, 1 << 62))
+    _same(build_buffers(verts, mats, seed), _oracle_build(verts, mats, seed))
+
+
+def test_thread_count_does_not_change_output():
+    from rtamd import build_buffers
+    rng = np.random.default_rng(5)
+    verts, mats = _random_tris(120_000, rng)
+    a = build_buffers(verts, mats, 3, n_threads=1)
+    b = build_buffers(verts, mats, 3, n_threads=8)
+    for x, y in ((a.model_vertex_data, b.model_vertex_data), (a.model_material_data, b.model_material_data),
+                 (a.flat_bvh_data, b.flat_bvh_data)):
+        assert np.array_equal(x, y)
+
+
+def test_built_buffers_validate_and_are_preorder():
+    import ctypes as C
+    from rtamd import lib, configs
+    for k in (1, 2, 3):
+        b = configs.get(k).build()
+        nn, depth = C.c_size_t(), C.c_int()
+        assert lib().rt_scene_validate(b.model_vertex_data.ctypes.data, b.model_vertex_data.nbytes,
+                                       b.model_material_data.ctypes.data, b.model_material_data.nbytes,
+                                       b.flat_bvh_data.ctypes.data, b.flat_bvh_data.nbytes,
+                                       C.byref(nn), C.byref(depth)) == 0
+        assert nn.value == b.n_nodes
+
+
+@pytest.mark.parametrize("name", list(GOLDEN["scenes"]))
+def test_config_buffers_golden(name):
+    import hashlib
+    from rtamd import configs
+    k = int(name[3])
+    cfg = configs.get(k)
+    b = cfg.build()
+    g = GOLDEN["scenes"][name]
+    sha = lambda a: hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+    assert (b.triangle_count, b.n_nodes) == (g["flat_triangles"], g["nodes"])
+    assert sha(b.model_vertex_data) == g["vertices_sha256"]
+    assert sha(b.model_material_data) == g["materials_sha256"]
+    assert sha(b.flat_bvh_data) == g["nodes_sha256"]
+    assert cfg.camera().ubo_bytes().hex() == g["camera_ubo_hex"]
+
+
+def test_camera_matches_restatement():
+    from oracle import scene_oracle
+    from rtamd import Camera
+    rng = random.Random(3)
+    cams = [((-25, 30, 140), (0, 0, 0), (0, 1, 0), 20.0, 1280 / 720)]
+    for _ in range(50):
+        o = tuple(rng.uniform(-200, 200) for _ in range(3))
+        la = tuple(rng.uniform(-20, 20) for _ in range(3))
+        cams.append((o, la, (0.0, 1.0, 0.0), rng.uniform(5, 120), rng.uniform(0.3, 4.0)))
+    for o, la, up, fov, asp in cams:
+        c = Camera(o, la, up, fov, asp)
+        assert c.ubo_bytes() == scene_oracle.camera_ubo(tuple(map(float, o)), tuple(map(float, la)),
+                                                        up, fov, asp)
+
+
+def test_camera_move_recomputes_viewport():
+    from rtamd import Camera
+    c = Camera.default(1280, 720)
+    before = c.ubo_bytes()
+    c.set_origin((-25 + 5.5, 30, 140))          # VulkanApp 'D' key, VulkanApp.java:765
+    assert c.ubo_bytes() != before and c.get_origin() == (-19.5, 30.0, 140.0)
+
+
+def test_procedural_mesh():
+    from rtamd import Mesh
+    from rtamd.configs import FINAL_BASE_MESH_BMAX, FINAL_BASE_MESH_BMIN
+    for n in (8, 1000, 50_000, 200_002):
+        m = Mesh.procedural(n, 0x5EED, FINAL_BASE_MESH_BMIN, FINAL_BASE_MESH_BMAX)
+        assert len(m) == n
+        assert (m.tris.min(axis=(0, 1)) >= np.float32(FINAL_BASE_MESH_BMIN) - 1e-3).all()
+        assert (m.tris.max(axis=(0, 1)) <= np.float32(FINAL_BASE_MESH_BMAX) + 1e-3).all()
+    # closed: every undirected edge is shared by exactly two triangles
+    m = Mesh.procedural(1000, 1, (-1, -1, -1), (1, 1, 1))
+    v = m.tris.reshape(-1, 3)
+    _, idx = np.unique(v, axis=0, return_inverse=True)
+    t = idx.reshape(-1, 3)
+    edges = np.sort(np.concatenate([t[:, [0, 1]], t[:, [1, 2]], t[:, [2, 0]]]), axis=1)
+    _, cnt = np.unique(edges, axis=0, return_counts=True)
+    assert (cnt == 2).all()
+    a = Mesh.procedural(5000, 9, (-1, -1, -1), (1, 1, 1)).tris
+    b = Mesh.procedural(5000, 9, (-1, -1, -1), (1, 1, 1)).tris
+    assert np.array_equal(a, b)
+
+
+def test_obj_loader_on_reference_assets():
+    """SceneBuilder.loadModel inputs: the reference's own OBJ files (read when
+    the reference checkout is present; the configs embed the same triangles)."""
+    from rtamd import Mesh
+    from rtamd.configs import cube_mesh, plane_mesh
+    assert np.array_equal(Mesh.load_obj(reference_path("objects", "cube.obj")).tris, cube_mesh().tris)
+    assert np.array_equal(Mesh.load_obj(reference_path("objects", "ground_plane.obj")).tris, plane_mesh().tris)
+    fbm = Mesh.load_obj(reference_path("objects", "FinalBaseMesh.obj"))
+    assert len(fbm) == 48_918                   # 24,459 quads -> 2 triangles each
+    lo, hi = fbm.tris.min(axis=(0, 1)), fbm.tris.max(axis=(0, 1))
+    assert np.allclose(lo, [-5.8425, -0.0566, -1.8531]) and np.allclose(hi, [5.8425, 20.6841, 1.9170])
+
+
+def test_obj_loader_formats(tmp_path):
+    from rtamd import Mesh, RtError
+    p = tmp_path / "m.obj"
+    p.write_text("# c\nv 0 0 0\nv 1 0 0\nv 1 1 0\nv 0 1 0\nvn 0 0 1\n"
+                 "f 1/1/1 2/2/1 3/3/1 4/4/1\nf -4 -2 -1\nl 1 2\n")
+    m = Mesh.load_obj(str(p))
+    assert len(m) == 3                          # quad -> 2, triangle with relative indices -> 1
+    assert m.tris[2].tolist() == [[0, 0, 0], [1, 1, 0], [0, 1, 0]]
+    bad = tmp_path / "bad.obj"
+    bad.write_text("v 0 0 0\nf 1 2 3\n")
+    with pytest.raises(RtError, match="IO"):
+        Mesh.load_obj(str(bad))
+    with pytest.raises(RtError, match="IO"):
+        Mesh.load_obj(str(tmp_path / "missing.obj"))
+
+
+def test_scene_builder_skips_unloadable_models(tmp_path):
+    """SceneBuilder.java:55-58: a model that fails to load is skipped."""
+    from rtamd import ModelInstance, Scene, SceneBuilder
+    from rtamd.configs import ground_plane_instance
+    s = Scene()
+    s.add_instance(ModelInstance(str(tmp_path / "nope.obj"), "missing"))
+    s.add_instance(ground_plane_instance())
+    b = SceneBuilder().build_scene(s)
+    assert b.triangle_count == 2                # 2 plane triangles -> one node with 2 leaves
+    empty = SceneBuilder().build_scene(Scene())
+    assert empty.triangle_count == 0 and empty.flat_bvh_data.size == 1   # the 1-byte dummy
