@@ -229,7 +229,13 @@ __device__ __forceinline__ void diag_stamp(unsigned long long* rec, int which) {
     }
 }
 
-template <bool COUNT, bool DIAG = false>
+// Optional features of trace_simple, compiled in only where a schedule needs
+// them so the default inner loop carries no extra compares.
+constexpr int kFeatSpill = 1;   // split schedule: hand paths on after seg_limit segments
+constexpr int kFeatHeavy = 2;   // tiered schedule: hand walks on after heavy_budget visits
+constexpr int kFeatPrio = 4;    // raise wave priority after prio_after visits
+
+template <bool COUNT, bool DIAG = false, int FEAT = 0>
 __global__ __launch_bounds__(256) void trace_simple(TraceArgs a) {
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
@@ -258,7 +264,7 @@ __global__ __launch_bounds__(256) void trace_simple(TraceArgs a) {
         V3 fin = {0.0f, 0.0f, 0.0f};
         V3 att = {1.0f, 1.0f, 1.0f};
         for (int b = 0; b < a.max_bounces; ++b) {                         // :179
-            if (b == a.seg_limit) {                                       // hand the path on
+            if ((FEAT & kFeatSpill) && b == a.seg_limit) {               // hand the path on
                 spill = true;
                 PathState* st = a.spill + atomicAdd(a.spill_count, 1u);
                 st->q0 = make_float4(o.x, o.y, o.z, att.x);
@@ -276,8 +282,9 @@ __global__ __launch_bounds__(256) void trace_simple(TraceArgs a) {
                 i = node_step<COUNT>(a.scene.nodes, a.scene.tris, i, o, d, inv, closest, hit, c_node, c_tri);
                 // A wave still walking after prio_after steps holds the frame's
                 // critical path: let it win instruction arbitration.
-                if (++steps == a.prio_after) __builtin_amdgcn_s_setprio(3);
-                if (steps >= a.heavy_budget && i < a.scene.end) {         // hand the walk on
+                if (FEAT & (kFeatPrio | kFeatHeavy)) ++steps;
+                if ((FEAT & kFeatPrio) && steps == a.prio_after) __builtin_amdgcn_s_setprio(3);
+                if ((FEAT & kFeatHeavy) && steps >= a.heavy_budget && i < a.scene.end) {   // hand the walk on
                     heavy = true;
                     HeavyRay* hv = a.heavy + atomicAdd(a.heavy_count, 1u);
                     hv->p.q0 = make_float4(o.x, o.y, o.z, att.x);
@@ -640,12 +647,20 @@ hipError_t launch_trace(const TraceArgs& a, hipStream_t stream) {
     } else {
         const int tw_w = 8 << a.wave_tile, th_w = 8 >> a.wave_tile;
         const dim3 grid((a.tw + 4 * tw_w - 1) / (4 * tw_w), (a.th + th_w - 1) / th_w);
-        if (a.diag)
-            hipLaunchKernelGGL((trace_simple<false, true>), grid, block, 0, stream, a);
-        else if (a.counters)
-            hipLaunchKernelGGL(trace_simple<true>, grid, block, 0, stream, a);
-        else
-            hipLaunchKernelGGL(trace_simple<false>, grid, block, 0, stream, a);
+        const int feat = (a.seg_limit < (1 << 30) ? kFeatSpill : 0) |
+                         (a.heavy_budget < (1 << 30) ? kFeatHeavy : 0) | (a.prio_after > 0 ? kFeatPrio : 0);
+#define RT_SIMPLE(F)                                                                              \
+        if (a.diag) hipLaunchKernelGGL((trace_simple<false, true, F>), grid, block, 0, stream, a); \
+        else if (a.counters) hipLaunchKernelGGL((trace_simple<true, false, F>), grid, block, 0, stream, a); \
+        else hipLaunchKernelGGL((trace_simple<false, false, F>), grid, block, 0, stream, a);
+        switch (feat) {
+            case 0: RT_SIMPLE(0) break;
+            case kFeatSpill: RT_SIMPLE(kFeatSpill) break;
+            case kFeatHeavy: RT_SIMPLE(kFeatHeavy) break;
+            case kFeatPrio: RT_SIMPLE(kFeatPrio) break;
+            default: RT_SIMPLE(kFeatSpill | kFeatHeavy | kFeatPrio) break;
+        }
+#undef RT_SIMPLE
     }
     return hipGetLastError();
 }
