@@ -43,6 +43,9 @@ def main():
     stream = torch.cuda.Stream()
     torch.cuda.set_stream(stream)
 
+    def log(*x):
+        print(*x, file=sys.stderr, flush=True)
+
     def launch(stats=False):
         s = Stats()
         check(L.rt_render_bands_device(r._ctx, C.byref(cam.ubo), W, H, B, H, 1, 0, out.data_ptr(), None,
@@ -54,11 +57,13 @@ def main():
             k, val = kv.split("=")
             r.set_option(k, int(val))
 
-    apply("kernel=1")
+    log("counting pass")
     segs = launch(stats=True).segments
+    log("segments", segs)
     times = {v: [] for v in variants}
     for _ in range(args.rounds):
         for v in variants:
+            log("variant", v)
             apply(v)
             for _ in range(2):
                 launch()
@@ -69,7 +74,7 @@ def main():
             e1.record(stream)
             e1.synchronize()
             times[v].append(e0.elapsed_time(e1) / args.iters)
-        apply("kernel=1,shade_min=16,blocks_per_cu=0,wave_tile=0")
+        apply("kernel=0,shade_min=16,blocks_per_cu=0,wave_tile=2,heavy_budget=256")
     for v in variants:
         med = statistics.median(times[v])
         print(json.dumps({"variant": v, "config": cfg.name, "median_ms": round(med, 4),
