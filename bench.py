@@ -189,7 +189,7 @@ def main() -> None:
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": traffic,
-                "kernel": "trace_kernel",
+                "kernel": "trace_simple" if renderer.get_option("kernel") == 0 else "trace_*",
                 "kernel_ms": round(kernel_ms, 4),
                 "alg_bytes_per_launch": int(alg_bytes),
                 "alg_bytes_per_segment": round(alg_bytes / l_seg, 1),

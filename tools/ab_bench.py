@@ -24,6 +24,7 @@ def main():
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--variant", action="append", default=[])
     ap.add_argument("--bounces", type=int, default=0, help="override the config's max_bounces")
+    ap.add_argument("--first", default="", help="options applied before the counting pass")
     args = ap.parse_args()
     variants = args.variant or ["kernel=0", "kernel=1,shade_min=8", "kernel=1,shade_min=16",
                                 "kernel=1,shade_min=32"]
@@ -57,6 +58,8 @@ def main():
             k, val = kv.split("=")
             r.set_option(k, int(val))
 
+    if args.first:
+        apply(args.first)
     log("counting pass")
     segs = launch(stats=True).segments
     log("segments", segs)

@@ -11,7 +11,7 @@ rocprofv3 -L > "$OUT/counters_list.txt" 2>&1 || true
 pass() {  # pass NAME COUNTERS...
   local name=$1; shift
   echo "$(date +%T) pass $name: $*" >> "$OUT/status.txt"
-  timeout -k 10 300 rocprofv3 --pmc "$@" --kernel-include-regex trace_kernel --output-format csv \
+  timeout -k 10 300 rocprofv3 --pmc "$@" --kernel-include-regex "trace_(simple|persistent|coop)" --output-format csv \
       -d "$OUT/$name" -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline > "$OUT/$name.log" 2>&1
   local rc=$?
   echo "$(date +%T) pass $name rc=$rc" >> "$OUT/status.txt"
