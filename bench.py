@@ -50,7 +50,7 @@ def main() -> None:
     ap.add_argument("--band", type=int, default=16, help="band height for N > 1")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU baseline sample time")
-    ap.add_argument("--traffic-json", default=None,
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "latest_pmc_traffic.json"),
                     help="PMC-derived HBM bytes per launch (profiles/*.json) to report as roofline.traffic")
     args = ap.parse_args()
 
@@ -148,9 +148,11 @@ def main() -> None:
     alg_bytes = 32.0 * l_nodes + 36.0 * l_tris + 16.0 * l_mats + 4.0 * l_pix
     ref_layout_bytes = 48.0 * l_nodes + 48.0 * l_tris + 16.0 * l_mats + 4.0 * l_pix
     achieved = alg_bytes / (kernel_ms * 1e-3) / 1e9
-    traffic = None
+    traffic, traffic_src = None, None
     if args.traffic_json and os.path.exists(args.traffic_json):
-        traffic = json.load(open(args.traffic_json)).get("hbm_bytes_per_launch")
+        tj = json.load(open(args.traffic_json))
+        if tj.get("config") == cfg.name and world == 1:   # PMC bytes of the same kernel on this workload
+            traffic, traffic_src = tj.get("hbm_bytes_per_launch"), tj.get("source")
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -189,6 +191,7 @@ def main() -> None:
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": traffic,
+                "traffic_source": traffic_src,
                 "kernel": "trace_simple" if renderer.get_option("kernel") == 0 else "trace_*",
                 "kernel_ms": round(kernel_ms, 4),
                 "alg_bytes_per_launch": int(alg_bytes),
