@@ -4,19 +4,36 @@
 // reference's 48-B node / 48-B vertex / 16-B material records):
 //
 //   nodes : 2 x float4 per node (32 B), in the reference's preorder
-//           [0] = (bbox_min.xyz, skip)   skip = first node after this subtree
-//           [1] = (bbox_max.xyz, leaf)   leaf = flattened triangle index, or -1
+//           [0] = (bbox_min.xyz, skip | L(skip) << 31)
+//           [1] = (bbox_max.xyz, L(i+1) | L(i) << 1)
+//           skip = first node after this subtree; L(j) = "node j is a leaf".
 //           The left child of an internal node i is i+1 (BVHFlattener.java:51-75:
 //           myIndex = currentNodeIndex++ and the left subtree is flattened
 //           first), so the reference's stack DFS (compute_dynamic_ray.comp:185-210:
 //           push right, push left) visits nodes in preorder, skipping the
 //           subtree of every node whose box test fails.  "next = hit ? i+1 :
-//           skip" replays exactly that visit sequence with no stack at all.
-//   tris  : 3 x float4 per flattened triangle (48 B)
-//           [0] = (v0.xyz, n.x) [1] = (e1.xyz, n.y) [2] = (e2.xyz, n.z)
-//           e1 = v1-v0, e2 = v2-v0 and n = normalize(cross(e1,e2)) are the
-//           values hit_triangle computes (compute_dynamic_ray.comp:106-107,124)
-//           evaluated once on the host in IEEE binary32: the same bits.
+//           skip" replays exactly that visit sequence with no stack at all, and
+//           the L bits tell a walker whether the node it moves to is a leaf, so
+//           it fetches that leaf's triangle together with the node (one memory
+//           round trip per visit).
+//   leafs : 3 x float4 per NODE index (48 B; meaningful at leaves only)
+//           [0] = (v0.xyz, triangle index) [1] = (e1.xyz, 0) [2] = (e2.xyz, 0)
+//           e1 = v1-v0, e2 = v2-v0 are the values hit_triangle computes
+//           (compute_dynamic_ray.comp:106-107), evaluated once on the host in
+//           IEEE binary32: the same bits.
+//   pairs : 4 x float4 per NODE index (64 B; meaningful at internal nodes only):
+//           the boxes of both children of node i and where they are
+//           [0] = (L.min.xyz, R.min.x) [1] = (L.max.xyz, R.min.y)
+//           [2] = (R.max.xyz, R.min.z) [3] = (R | L(R) << 31, L(i+1), skip(i), 0)
+//           with L = i+1 and R = the right child.  The default walk
+//           (trace_simple, "walk" 1) loads this one record when node i is hit
+//           and runs both children's slab tests at once.  A slab test does
+//           not depend on closest_t; only the final "t_enter < closest_t"
+//           does, so the right child's t_enter is kept on a short per-lane
+//           stack and compared when the reference would pop it — the same
+//           float bits, compared at the same point in the visit sequence.
+//   norms : 1 x float4 per flattened triangle: normalize(cross(e1,e2)) (:124),
+//           likewise precomputed; read once per hit when shading.
 //   mats  : 1 x float4 per flattened triangle (albedo.rgb, type)
 #pragma once
 #include <cstdint>
@@ -31,8 +48,12 @@ struct DevScene {
     int      n_nodes = 0;     // nodes in the compact array
     int      end     = 0;     // traversal ends when the node index reaches this (= skip of root)
     int      n_tris  = 0;
+    int      root_leaf = 0;   // L(0)
+    float    root_box[6] = {0, 0, 0, 0, 0, 0};   // node 0's min.xyz, max.xyz (kernel argument)
     float4*  nodes   = nullptr;
-    float4*  tris    = nullptr;
+    float4*  leafs   = nullptr;
+    float4*  pairs   = nullptr;
+    float4*  norms   = nullptr;
     float4*  mats    = nullptr;
 };
 
@@ -102,14 +123,21 @@ struct TraceArgs {
                                 //   cooperative pass (<= 0: never)
     HeavyRay* heavy;            // tiered: suspended heavy paths (capacity tw*th)
     unsigned* heavy_count;      // tiered: number of heavy paths (zeroed before the simple pass)
+    int      coop_lanes;        // simple: finish a wave's walks cooperatively once at most
+                                //   this many lanes are still walking (0 = never)
+    int      walk;              // simple: 0 = one node per step (nodes/leafs),
+                                //   1 = child pairs + per-lane stack of t_enter (pairs)
 };
 
 // Host-side compact-scene build from the reference records; validates the
 // buffers.  Returns RT_OK or RT_ERR_BAD_SCENE with a message in *err.
 struct HostScene {
-    int n_nodes = 0, end = 0, n_tris = 0, max_depth = 0;
+    int n_nodes = 0, end = 0, n_tris = 0, max_depth = 0, root_leaf = 0;
+    float root_box[6] = {0, 0, 0, 0, 0, 0};
     float4* nodes = nullptr;    // 2*n_nodes
-    float4* tris  = nullptr;    // 3*n_tris
+    float4* leafs = nullptr;    // 3*n_nodes
+    float4* pairs = nullptr;    // 4*n_nodes
+    float4* norms = nullptr;    // n_tris
     float4* mats  = nullptr;    // n_tris
 };
 int build_host_scene(const void* vertices, size_t vertex_bytes,

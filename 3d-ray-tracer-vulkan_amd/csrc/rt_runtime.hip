@@ -51,7 +51,9 @@ static inline int32_t i32_at(const unsigned char* p, size_t off) {
 
 void free_host_scene(HostScene* s) {
     std::free(s->nodes);
-    std::free(s->tris);
+    std::free(s->leafs);
+    std::free(s->pairs);
+    std::free(s->norms);
     std::free(s->mats);
     *s = HostScene{};
 }
@@ -116,6 +118,13 @@ int build_host_scene(const void* vertices, size_t vertex_bytes,
         }
     }
     out->end = skip[0];
+    std::vector<uint8_t> is_leaf(n_nodes + 1, 0);
+    for (size_t k = 0; k < n_nodes; ++k) is_leaf[k] = i32_at(nb + k * RT_NODE_RECORD_BYTES, 36) < 0;
+    out->root_leaf = is_leaf[0];
+    out->leafs = static_cast<float4*>(std::calloc(3 * n_nodes, sizeof(float4)));
+    out->pairs = static_cast<float4*>(std::calloc(4 * n_nodes, sizeof(float4)));
+    if (!out->leafs || !out->pairs) return fail("out of host memory");
+    const unsigned char* vb = static_cast<const unsigned char*>(vertices);
     int max_depth = 0;
     for (size_t k = 0; k < (size_t)out->end; ++k) {
         const unsigned char* r = nb + k * RT_NODE_RECORD_BYTES;
@@ -128,36 +137,65 @@ int build_host_scene(const void* vertices, size_t vertex_bytes,
         float4 A, B;
         A.x = f32_at(r, 0);  A.y = f32_at(r, 4);  A.z = f32_at(r, 8);
         B.x = f32_at(r, 16); B.y = f32_at(r, 20); B.z = f32_at(r, 24);
-        int32_t sk = skip[k], leaf = count < 0 ? -(data + 1) : -1;
-        std::memcpy(&A.w, &sk, 4);
-        std::memcpy(&B.w, &leaf, 4);
+        const uint32_t sk = (uint32_t)skip[k];
+        const uint32_t aw = sk | ((sk < (uint32_t)out->end && is_leaf[sk]) ? 0x80000000u : 0u);
+        const uint32_t bw = ((k + 1 < (size_t)out->end && is_leaf[k + 1]) ? 1u : 0u) | (is_leaf[k] ? 2u : 0u);
+        std::memcpy(&A.w, &aw, 4);
+        std::memcpy(&B.w, &bw, 4);
         out->nodes[2 * k] = A;
         out->nodes[2 * k + 1] = B;
+        if (k == 0) {
+            out->root_box[0] = A.x; out->root_box[1] = A.y; out->root_box[2] = A.z;
+            out->root_box[3] = B.x; out->root_box[4] = B.y; out->root_box[5] = B.z;
+        }
+        if (count >= 0) {
+            const unsigned char* l = nb + (size_t)data * RT_NODE_RECORD_BYTES;
+            const unsigned char* rr = nb + (size_t)count * RT_NODE_RECORD_BYTES;
+            const uint32_t rw = (uint32_t)count | (is_leaf[count] ? 0x80000000u : 0u);
+            const uint32_t lw = is_leaf[data] ? 1u : 0u;
+            const uint32_t sw = (uint32_t)skip[k];
+            float rwf, lwf, swf;
+            std::memcpy(&rwf, &rw, 4);
+            std::memcpy(&lwf, &lw, 4);
+            std::memcpy(&swf, &sw, 4);
+            out->pairs[4 * k + 0] = make_float4(f32_at(l, 0), f32_at(l, 4), f32_at(l, 8), f32_at(rr, 0));
+            out->pairs[4 * k + 1] = make_float4(f32_at(l, 16), f32_at(l, 20), f32_at(l, 24), f32_at(rr, 4));
+            out->pairs[4 * k + 2] = make_float4(f32_at(rr, 16), f32_at(rr, 20), f32_at(rr, 24), f32_at(rr, 8));
+            out->pairs[4 * k + 3] = make_float4(rwf, lwf, swf, 0.f);
+        }
+        if (count < 0) {
+            // edge1 / edge2 exactly as hit_triangle computes them (compute_dynamic_ray.comp:106-107)
+            const int32_t tri = -(data + 1);
+            const unsigned char* v = vb + (size_t)tri * RT_VERTEX_RECORD_BYTES;
+            const float v0x = f32_at(v, 0),  v0y = f32_at(v, 4),  v0z = f32_at(v, 8);
+            const float v1x = f32_at(v, 16), v1y = f32_at(v, 20), v1z = f32_at(v, 24);
+            const float v2x = f32_at(v, 32), v2y = f32_at(v, 36), v2z = f32_at(v, 40);
+            float tw;
+            std::memcpy(&tw, &tri, 4);
+            out->leafs[3 * k + 0] = make_float4(v0x, v0y, v0z, tw);
+            out->leafs[3 * k + 1] = make_float4(v1x - v0x, v1y - v0y, v1z - v0z, 0.f);
+            out->leafs[3 * k + 2] = make_float4(v2x - v0x, v2y - v0y, v2z - v0z, 0.f);
+        }
     }
     out->max_depth = max_depth;
 
-    out->tris = static_cast<float4*>(std::malloc(sizeof(float4) * 3 * (n_tris ? n_tris : 1)));
+    out->norms = static_cast<float4*>(std::malloc(sizeof(float4) * (n_tris ? n_tris : 1)));
     out->mats = static_cast<float4*>(std::malloc(sizeof(float4) * (n_tris ? n_tris : 1)));
-    if (!out->tris || !out->mats) return fail("out of host memory");
-    const unsigned char* vb = static_cast<const unsigned char*>(vertices);
+    if (!out->norms || !out->mats) return fail("out of host memory");
     const unsigned char* mb = static_cast<const unsigned char*>(materials);
     for (size_t t = 0; t < n_tris; ++t) {
         const unsigned char* r = vb + t * RT_VERTEX_RECORD_BYTES;
         const float v0x = f32_at(r, 0),  v0y = f32_at(r, 4),  v0z = f32_at(r, 8);
         const float v1x = f32_at(r, 16), v1y = f32_at(r, 20), v1z = f32_at(r, 24);
         const float v2x = f32_at(r, 32), v2y = f32_at(r, 36), v2z = f32_at(r, 40);
-        // edge1/edge2 and normalize(cross(edge1, edge2)) exactly as
-        // hit_triangle computes them (compute_dynamic_ray.comp:106-107,124).
+        // normalize(cross(edge1, edge2)) exactly as hit_triangle computes it (:124)
         const float e1x = v1x - v0x, e1y = v1y - v0y, e1z = v1z - v0z;
         const float e2x = v2x - v0x, e2y = v2y - v0y, e2z = v2z - v0z;
         const float cx = e1y * e2z - e1z * e2y;
         const float cy = e1z * e2x - e1x * e2z;
         const float cz = e1x * e2y - e1y * e2x;
         const float l = std::sqrt((cx * cx + cy * cy) + cz * cz);
-        const float nx = cx / l, ny = cy / l, nz = cz / l;
-        out->tris[3 * t + 0] = make_float4(v0x, v0y, v0z, nx);
-        out->tris[3 * t + 1] = make_float4(e1x, e1y, e1z, ny);
-        out->tris[3 * t + 2] = make_float4(e2x, e2y, e2z, nz);
+        out->norms[t] = make_float4(cx / l, cy / l, cz / l, 0.f);
         if (t < n_mats) {
             const unsigned char* m = mb + t * RT_MATERIAL_RECORD_BYTES;
             out->mats[t] = make_float4(f32_at(m, 0), f32_at(m, 4), f32_at(m, 8), f32_at(m, 12));
@@ -208,13 +246,17 @@ struct rt_ctx {
     int  diag = 0;                 // record per-wave timestamps (kernel 0 only)
     int  prio_after = 0;           // kernel 0: s_setprio(3) after this many node steps
     int  heavy_budget = 256;       // tiered: node visits per path in tier 1
+    int  coop_lanes = 2;           // kernel 0: cooperative tail once <= this many lanes walk (0 = off)
+    int  walk = 0;                 // kernel 0: 0 = node per step (fastest measured), 1 = child pairs + t_enter stack
     bool has_scene = false;
     int  n_nodes = 0, n_tris = 0, max_depth = 0;
 };
 
 static void free_scene(PerDevice& p) {
     if (p.scene.nodes) (void)hipFree(p.scene.nodes);
-    if (p.scene.tris) (void)hipFree(p.scene.tris);
+    if (p.scene.leafs) (void)hipFree(p.scene.leafs);
+    if (p.scene.pairs) (void)hipFree(p.scene.pairs);
+    if (p.scene.norms) (void)hipFree(p.scene.norms);
     if (p.scene.mats) (void)hipFree(p.scene.mats);
     p.scene = DevScene{};
 }
@@ -224,6 +266,8 @@ static int set_schedule(const rt_ctx* ctx, PerDevice& p, TraceArgs& a) {
     a.shade_min = ctx->shade_min;
     a.wave_tile = ctx->wave_tile;
     a.prio_after = ctx->prio_after > 0 ? ctx->prio_after : -1;
+    a.coop_lanes = ctx->coop_lanes;
+    a.walk = ctx->walk;
     a.seg_limit = ctx->kernel == kKernelSplit ? ctx->seg_limit : (1 << 30);
     a.resume = 0;
     const unsigned slot = p.queue_slot++ % kQueueSlots;
@@ -310,7 +354,10 @@ int rt_create(const int* device_ids, int n_devices, rt_ctx** out) {
     if (const char* k = std::getenv("RTAMD_KERNEL"))
         ctx->kernel = std::strcmp(k, "simple") == 0 ? kKernelSimple
                     : std::strcmp(k, "persistent") == 0 ? kKernelPersistent
-                    : std::strcmp(k, "split") == 0 ? kKernelSplit : kKernelTiered;
+                    : std::strcmp(k, "split") == 0 ? kKernelSplit
+                    : std::strcmp(k, "tiered") == 0 ? kKernelTiered : ctx->kernel;
+    if (const char* v = std::getenv("RTAMD_WALK")) ctx->walk = std::atoi(v) ? 1 : 0;
+    if (const char* v = std::getenv("RTAMD_COOP_LANES")) ctx->coop_lanes = std::max(0, std::min(64, std::atoi(v)));
     if (const char* v = std::getenv("RTAMD_SEG_LIMIT")) ctx->seg_limit = std::max(1, std::min(1024, std::atoi(v)));
     if (const char* v = std::getenv("RTAMD_SHADE_MIN")) ctx->shade_min = std::max(1, std::min(64, std::atoi(v)));
     if (const char* v = std::getenv("RTAMD_BLOCKS_PER_CU")) ctx->blocks_per_cu = std::max(0, std::min(32, std::atoi(v)));
@@ -387,14 +434,26 @@ int rt_upload_scene(rt_ctx* ctx, const void* vertices, size_t vertex_bytes,
         s.n_nodes = hs.n_nodes;
         s.end = hs.end;
         s.n_tris = hs.n_tris;
-        const size_t nb = sizeof(float4) * 2 * (size_t)(hs.n_nodes ? hs.n_nodes : 1);
-        const size_t tb = sizeof(float4) * 3 * (size_t)(hs.n_tris ? hs.n_tris : 1);
+        s.root_leaf = hs.root_leaf;
+        std::memcpy(s.root_box, hs.root_box, sizeof s.root_box);
+        // nodes and leafs are padded so that a walker may always read four
+        // float4 from any record start (rt_trace.hip, walk 1).
+        const size_t nn = (size_t)hs.n_nodes;
+        const size_t nb = sizeof(float4) * (2 * nn + 2);
+        const size_t lb = sizeof(float4) * (3 * nn + 1);
+        const size_t pb = sizeof(float4) * 4 * (size_t)(hs.n_nodes ? hs.n_nodes : 1);
         const size_t mb = sizeof(float4) * (size_t)(hs.n_tris ? hs.n_tris : 1);
         hipError_t e = hipMalloc(&s.nodes, nb);
-        if (e == hipSuccess) e = hipMalloc(&s.tris, tb);
+        if (e == hipSuccess) e = hipMalloc(&s.leafs, lb);
+        if (e == hipSuccess) e = hipMalloc(&s.pairs, pb);
+        if (e == hipSuccess) e = hipMemset(s.nodes + 2 * nn, 0, 2 * sizeof(float4));
+        if (e == hipSuccess) e = hipMemset(s.leafs + 3 * nn, 0, sizeof(float4));
+        if (e == hipSuccess) e = hipMalloc(&s.norms, mb);
         if (e == hipSuccess) e = hipMalloc(&s.mats, mb);
-        if (e == hipSuccess && hs.n_nodes) e = hipMemcpy(s.nodes, hs.nodes, nb, hipMemcpyHostToDevice);
-        if (e == hipSuccess && hs.n_tris) e = hipMemcpy(s.tris, hs.tris, tb, hipMemcpyHostToDevice);
+        if (e == hipSuccess && hs.n_nodes) e = hipMemcpy(s.nodes, hs.nodes, nb - 2 * sizeof(float4), hipMemcpyHostToDevice);
+        if (e == hipSuccess && hs.n_nodes) e = hipMemcpy(s.leafs, hs.leafs, lb - sizeof(float4), hipMemcpyHostToDevice);
+        if (e == hipSuccess && hs.n_nodes) e = hipMemcpy(s.pairs, hs.pairs, pb, hipMemcpyHostToDevice);
+        if (e == hipSuccess && hs.n_tris) e = hipMemcpy(s.norms, hs.norms, mb, hipMemcpyHostToDevice);
         if (e == hipSuccess && hs.n_tris) e = hipMemcpy(s.mats, hs.mats, mb, hipMemcpyHostToDevice);
         p.scene = s;
         if (e != hipSuccess) {
@@ -639,6 +698,10 @@ int rt_set_option(rt_ctx* ctx, const char* name, int64_t value) {
         ctx->heavy_budget = (int)value;
     } else if (std::strcmp(name, "prio_after") == 0 && value >= 0 && value <= (1 << 30)) {
         ctx->prio_after = (int)value;
+    } else if (std::strcmp(name, "coop_lanes") == 0 && value >= 0 && value <= 64) {
+        ctx->coop_lanes = (int)value;
+    } else if (std::strcmp(name, "walk") == 0 && (value == 0 || value == 1)) {
+        ctx->walk = (int)value;
     } else if (std::strcmp(name, "diag") == 0 && (value == 0 || value == 1)) {
         ctx->diag = (int)value;
     } else if (std::strcmp(name, "wave_tile") == 0 && value >= 0 && value <= 3) {
@@ -658,6 +721,8 @@ int rt_get_option(rt_ctx* ctx, const char* name, int64_t* value) {
     else if (std::strcmp(name, "seg_limit") == 0) *value = ctx->seg_limit;
     else if (std::strcmp(name, "prio_after") == 0) *value = ctx->prio_after;
     else if (std::strcmp(name, "heavy_budget") == 0) *value = ctx->heavy_budget;
+    else if (std::strcmp(name, "coop_lanes") == 0) *value = ctx->coop_lanes;
+    else if (std::strcmp(name, "walk") == 0) *value = ctx->walk;
     else if (std::strcmp(name, "blocks_per_cu") == 0)
         *value = ctx->blocks_per_cu > 0 ? ctx->blocks_per_cu : (ctx->dev.empty() ? 0 : ctx->dev[0].blocks_per_cu);
     else { set_error("rt_get_option: unknown option %s", name); return RT_ERR_INVALID_ARG; }

@@ -6,22 +6,26 @@
 // in IEEE binary32, in the shader's evaluation order, with no contraction
 // (built with -ffp-contract=off) and hipcc's correctly rounded f32 division
 // and sqrt.  The CPU oracle (oracle/rt_oracle.c) states the same contract, so
-// the two agree bit for bit; see DESIGN.md §Parity.
+// the two agree bit for bit; see DESIGN.md §2.
 //
-// Traversal: stackless preorder walk over the compact 32-B nodes
-// (rt_internal.h), which replays the reference's stack DFS
-// (compute_dynamic_ray.comp:185-210) node for node: next = hit ? i+1 : skip(i).
+// Traversal: stackless preorder walk over the compact nodes (rt_internal.h),
+// which replays the reference's stack DFS (compute_dynamic_ray.comp:185-210)
+// node for node: next = hit ? i+1 : skip(i).  Every schedule below visits the
+// same nodes, runs the same triangle tests in the same order and sees the same
+// closest_t at each test, so frames and work counters are identical.
 //
-// Two schedules of the same per-pixel work:
-//   trace_simple      one lane = one pixel for its whole path (the
-//                     reference's dispatch shape, 8x8 pixels per wave).
-//   trace_persistent  persistent waves; a lane whose path ends pulls the next
-//                     pixel from a global queue of 8x8 tiles, and the shading
-//                     block (scatter / sky / pixel write) runs only once enough
-//                     lanes of the wave have finished a segment, so traversal
-//                     steps run with most lanes busy.  Results are identical:
-//                     every pixel's path is independent (its RNG seed is its
-//                     pixel index, :164) and is computed with the same ops.
+// Schedules of the same per-pixel work:
+//   trace_simple      one lane = one pixel for its whole path; a wave is a
+//                     tile of 64 pixels (the reference's 8x8 dispatch shape, or
+//                     16x4 / 32x2 / 64x1).  With the cooperative tail, once at
+//                     most coop_lanes lanes of a wave are still walking, the
+//                     whole wave finishes their walks one ray at a time with
+//                     coop_walk.
+//   trace_persistent  persistent waves pulling 8x8 tiles from a queue; lanes
+//                     refill when their path ends; shading is deferred until
+//                     shade_min lanes are ready.
+//   split / tiered    trace_simple for the first part of every path, then the
+//                     rest on trace_persistent (resume) or trace_coop.
 #include "rt_internal.h"
 
 namespace rtamd {
@@ -95,61 +99,87 @@ __device__ __forceinline__ void primary_ray(const TraceArgs& a, int x, int y, ui
     d = vnormalize(vsub(vadd(vadd(cam_l, vscale(cam_h, u)), vscale(cam_v, v)), cam_o));
 }
 
-// One node of the walk: hit_aabb (:88-103) and, at a leaf whose box is hit,
-// hit_triangle (:105-129).  Returns the next node index.
-template <bool COUNT>
-__device__ __forceinline__ int node_step(const float4* __restrict__ nodes, const float4* __restrict__ tris,
-                                         int i, V3 o, V3 d, V3 inv, float& closest, int& hit,
-                                         unsigned long long& c_node, unsigned long long& c_tri) {
-    const float4 A = nodes[2 * i];
-    const float4 B = nodes[2 * i + 1];
-    if (COUNT) ++c_node;
+// Slab test of hit_aabb (:88-103), split into the part that does not depend
+// on closest_t (ind) and t_enter; the box is hit iff ind && te < closest_t.
+__device__ __forceinline__ void slab(float4 A, float4 B, V3 o, V3 inv, float& te, bool& ind) {
     const float t0x = (A.x - o.x) * inv.x, t1x = (B.x - o.x) * inv.x;
     const float t0y = (A.y - o.y) * inv.y, t1y = (B.y - o.y) * inv.y;
     const float t0z = (A.z - o.z) * inv.z, t1z = (B.z - o.z) * inv.z;
-    const float te = fmaxf(fmaxf(fminf(t0x, t1x), fminf(t0y, t1y)), fminf(t0z, t1z));
+    te = fmaxf(fmaxf(fminf(t0x, t1x), fminf(t0y, t1y)), fminf(t0z, t1z));
     const float tx = fminf(fminf(fmaxf(t0x, t1x), fmaxf(t0y, t1y)), fmaxf(t0z, t1z));
-    const bool hb = tx > te && tx > kTMin && te < closest;
-    const int leaf = __float_as_int(B.w);
-    if (hb && leaf >= 0) {
+    ind = tx > te && tx > kTMin;
+}
+
+// hit_triangle (:105-129) up to its final "t < closest_t" compare: returns
+// true and t when det, u, v and t > T_MIN all pass.
+__device__ __forceinline__ bool tri_test(float4 P0, float4 P1, float4 P2, V3 o, V3 d, float& t) {
+    const V3 v0 = {P0.x, P0.y, P0.z};
+    const V3 e1 = {P1.x, P1.y, P1.z};
+    const V3 e2 = {P2.x, P2.y, P2.z};
+    const V3 pv = vcross(d, e2);
+    const float det = vdot(e1, pv);
+    if (det > -0.00001f && det < 0.00001f) return false;
+    const float inv_det = 1.0f / det;
+    const V3 s = vsub(o, v0);
+    const float uu = inv_det * vdot(s, pv);
+    if (uu < 0.0f || uu > 1.0f) return false;
+    const V3 q = vcross(s, e1);
+    const float vv = inv_det * vdot(d, q);
+    if (vv < 0.0f || (uu + vv) > 1.0f) return false;
+    t = inv_det * vdot(e2, q);
+    return t > kTMin;
+}
+
+// One node of the walk.  `leaf` says whether node i is a leaf (from its
+// predecessor's L bits), so the leaf's triangle is fetched in the same round
+// trip as the node.  Returns the next node index and updates `leaf`.
+//
+// Visit counting, in every walk: the reference's DFS pushes the root once and
+// both children of every internal node whose box is hit, and pops (= visits)
+// every node it pushes, so a segment visits exactly 1 + 2 x (hit internal
+// nodes) nodes.  Walks count the root when the segment starts and 2 per hit
+// internal node, which lets a walk skip children it can prove are missed
+// without visiting them.
+template <bool COUNT>
+__device__ __forceinline__ int node_step(const float4* __restrict__ nodes, const float4* __restrict__ leafs,
+                                         int i, bool& leaf, V3 o, V3 d, V3 inv, float& closest, int& hit,
+                                         unsigned long long& c_node, unsigned long long& c_tri) {
+    const float4 A = nodes[2 * i];
+    const float4 B = nodes[2 * i + 1];
+    float4 P0 = make_float4(0.f, 0.f, 0.f, 0.f), P1 = P0, P2 = P0;
+    if (leaf) {
+        P0 = leafs[3 * i + 0];
+        P1 = leafs[3 * i + 1];
+        P2 = leafs[3 * i + 2];
+    }
+    float te;
+    bool ind;
+    slab(A, B, o, inv, te, ind);
+    const bool hb = ind && te < closest;
+    if (COUNT && hb && !leaf) c_node += 2;
+    if (hb && leaf) {
         if (COUNT) ++c_tri;
-        const float4 P0 = tris[3 * leaf + 0];
-        const float4 P1 = tris[3 * leaf + 1];
-        const float4 P2 = tris[3 * leaf + 2];
-        const V3 v0 = {P0.x, P0.y, P0.z};
-        const V3 e1 = {P1.x, P1.y, P1.z};
-        const V3 e2 = {P2.x, P2.y, P2.z};
-        const V3 pv = vcross(d, e2);
-        const float det = vdot(e1, pv);
-        if (!(det > -0.00001f && det < 0.00001f)) {
-            const float inv_det = 1.0f / det;
-            const V3 s = vsub(o, v0);
-            const float uu = inv_det * vdot(s, pv);
-            if (!(uu < 0.0f || uu > 1.0f)) {
-                const V3 q = vcross(s, e1);
-                const float vv = inv_det * vdot(d, q);
-                if (!(vv < 0.0f || (uu + vv) > 1.0f)) {
-                    const float t = inv_det * vdot(e2, q);
-                    if (t > kTMin && t < closest) {
-                        closest = t;
-                        hit = leaf;
-                    }
-                }
-            }
+        float t;
+        if (tri_test(P0, P1, P2, o, d, t) && t < closest) {
+            closest = t;
+            hit = __float_as_int(P0.w);
         }
     }
-    return hb ? i + 1 : __float_as_int(A.w);
+    const uint32_t aw = __float_as_uint(A.w), bw = __float_as_uint(B.w);
+    leaf = hb ? (bw & 1u) : (aw >> 31);
+    return hb ? i + 1 : (int)(aw & 0x7FFFFFFFu);
 }
 
 // The hit normal of :124-125: normalize(cross(e1,e2)) (precomputed per
 // triangle, rt_internal.h), flipped to face against d.
-__device__ __forceinline__ V3 hit_normal(const float4* __restrict__ tris, int hit, V3 d) {
-    V3 n = {tris[3 * hit + 0].w, tris[3 * hit + 1].w, tris[3 * hit + 2].w};
+__device__ __forceinline__ V3 hit_normal(const float4* __restrict__ norms, int hit, V3 d) {
+    const float4 N = norms[hit];
+    V3 n = {N.x, N.y, N.z};
     if (vdot(d, n) > 0.0f) n = {-n.x, -n.y, -n.z};
     return n;
 }
 
-// scatter (:132-154).  Returns true and the new direction / albedo on scatter.
+// scatter (:132-154).  Returns true and the new direction on scatter.
 __device__ __forceinline__ bool scatter(float4 M, V3 d, V3 n, uint32_t& seed, V3& nd) {
     if (M.w == 0.0f) {                                                    // Lambertian :137-143
         const V3 ru = vnormalize(rnd_in_sphere(seed));
@@ -210,6 +240,81 @@ __device__ __forceinline__ int lanes_below(uint64_t mask) {
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
 }
 
+// Keep loaded values where they are: an empty asm that "modifies" them stops
+// the compiler from sinking a load into the branch that uses it (which would
+// turn one memory round trip into two dependent ones).
+__device__ __forceinline__ void pin(float4& q) { asm volatile("" : "+v"(q.x), "+v"(q.y), "+v"(q.z), "+v"(q.w)); }
+__device__ __forceinline__ void pin(uint2& q) { asm volatile("" : "+v"(q.x), "+v"(q.y)); }
+
+__device__ __forceinline__ int lane_i(int v, int k) { return __builtin_amdgcn_readlane(v, k); }
+__device__ __forceinline__ float lane_f(float v, int k) {
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), k));
+}
+
+// ------------------------------------------------------------ cooperative walk --
+//
+// The whole wave walks ONE ray (arguments wave-uniform), replaying the
+// reference's visit sequence exactly:
+//   1. lane k loads node n+k of the window [n, n+64) and, in the same round
+//      trip, the leaf record indexed by that node (2 + 3 coalesced 16-B
+//      loads per lane); it runs the slab test and, for a leaf whose box is hit
+//      at the current closest_t, the triangle test up to "t < closest_t";
+//   2. ballots make 64-bit masks: box hit at closest_t (H), triangle hit that
+//      improves closest_t (T), is a leaf (Lf);
+//   3. the scalar unit replays the walk through the window: node k is hit iff
+//      bit k of H; next = k+1 on a hit, skip(k) on a miss; a triangle hit
+//      updates closest_t / hit and re-ballots H and T (closest_t only shrinks,
+//      so a leaf not pre-tested at the old closest_t cannot hit at the new one).
+// The float operations are node_step's, so closest_t, the hit and the visit /
+// triangle-test counts equal the per-lane walk's.
+template <bool COUNT>
+__device__ __forceinline__ void coop_walk(const float4* __restrict__ nodes, const float4* __restrict__ leafs,
+                                          int end, int n, V3 o, V3 d, V3 inv, float& closest, int& hit,
+                                          unsigned long long& c_node, unsigned long long& c_tri) {
+    const int lane = threadIdx.x & 63;
+    while (n < end) {
+        const int j = n + lane;
+        float te = 0.0f, tt = 0.0f;
+        int sk = 0, tri = -1;
+        bool ind = false, tv = false, lf = false;
+        if (j < end) {
+            const float4 A = nodes[2 * j];
+            const float4 B = nodes[2 * j + 1];
+            const float4 P0 = leafs[3 * j + 0];
+            const float4 P1 = leafs[3 * j + 1];
+            const float4 P2 = leafs[3 * j + 2];
+            slab(A, B, o, inv, te, ind);
+            sk = (int)(__float_as_uint(A.w) & 0x7FFFFFFFu);
+            lf = (__float_as_uint(B.w) & 2u) != 0;
+            tri = __float_as_int(P0.w);
+            if (lf && ind && te < closest) tv = tri_test(P0, P1, P2, o, d, tt);
+        }
+        uint64_t H = __ballot(ind && te < closest);
+        uint64_t T = __ballot(tv && tt < closest);
+        const uint64_t Lf = __ballot(lf);
+        const int lim = min(64, end - n);
+        int k = 0;
+        while (k < lim) {
+            if ((H >> k) & 1ull) {
+                if (COUNT && !((Lf >> k) & 1ull)) c_node += 2;
+                if ((Lf >> k) & 1ull) {
+                    if (COUNT) ++c_tri;
+                    if ((T >> k) & 1ull) {
+                        closest = lane_f(tt, k);
+                        hit = lane_i(tri, k);
+                        H = __ballot(ind && te < closest);
+                        T = __ballot(tv && tt < closest);
+                    }
+                }
+                ++k;
+            } else {
+                k = lane_i(sk, k) - n;
+            }
+        }
+        n += k;
+    }
+}
+
 // ------------------------------------------------------------ simple kernel --
 
 // Diagnostic stamp (diag builds only): global realtime clock (100 MHz) and
@@ -230,12 +335,17 @@ __device__ __forceinline__ void diag_stamp(unsigned long long* rec, int which) {
 }
 
 // Optional features of trace_simple, compiled in only where a schedule needs
-// them so the default inner loop carries no extra compares.
-constexpr int kFeatSpill = 1;   // split schedule: hand paths on after seg_limit segments
-constexpr int kFeatHeavy = 2;   // tiered schedule: hand walks on after heavy_budget visits
-constexpr int kFeatPrio = 4;    // raise wave priority after prio_after visits
+// them so the default inner loop carries no extra work.
+constexpr int kFeatSpill = 1;     // split schedule: hand paths on after seg_limit segments
+constexpr int kFeatHeavy = 2;     // tiered schedule: hand walks on after heavy_budget visits
+constexpr int kFeatPrio = 4;      // raise wave priority after prio_after visits
+constexpr int kFeatCoopTail = 8;  // finish the last coop_lanes walks of a wave cooperatively
 
-template <bool COUNT, bool DIAG = false, int FEAT = 0>
+constexpr int kStack = 8;                    // per-lane t_enter stack entries in LDS (walk 1)
+constexpr uint32_t kIdx = 0x7FFFFFFFu;
+constexpr int kPair = 0, kLeaf = 1, kNode = 2, kSkip = 3;   // walk 1: record kinds
+
+template <bool COUNT, bool DIAG = false, int FEAT = 0, int WALK = 1>
 __global__ __launch_bounds__(256) void trace_simple(TraceArgs a) {
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
@@ -244,6 +354,9 @@ __global__ __launch_bounds__(256) void trace_simple(TraceArgs a) {
         drec = a.diag + 4 * (size_t)((blockIdx.y * gridDim.x + blockIdx.x) * 4 + wave);
         diag_stamp(drec, 0);
     }
+    // walk 1: the right siblings still to visit, as (t_enter or +inf, R | L(R) << 31),
+    // newest kStack per lane; older ones are dropped and found again by skip pointers.
+    __shared__ uint2 stk[WALK == 1 ? kStack : 1][256];
     // One wave = one tile of 64 pixels, (8 << s) x (8 >> s) with s = a.wave_tile
     // (s = 0: 8x8, the reference's local_size 8x8x1, compute_dynamic_ray.comp:157);
     // a 256-thread block = 4 such tiles side by side.
@@ -251,69 +364,257 @@ __global__ __launch_bounds__(256) void trace_simple(TraceArgs a) {
     const int tw_w = 8 << s, th_w = 8 >> s;
     const int lx = (blockIdx.x * 4 + wave) * tw_w + (lane & (tw_w - 1));
     const int ly = blockIdx.y * th_w + (lane >> (3 + s));
+    const bool pixel = lx < a.tw && ly < a.th;
+    const float4* __restrict__ nodes = a.scene.nodes;
+    const float4* __restrict__ leafs = a.scene.leafs;
+    const float4* __restrict__ pairs = a.scene.pairs;
+    const int end = a.scene.end;
+    const V3 rlo = {a.scene.root_box[0], a.scene.root_box[1], a.scene.root_box[2]};
+    const V3 rhi = {a.scene.root_box[3], a.scene.root_box[4], a.scene.root_box[5]};
     unsigned long long c_seg = 0, c_node = 0, c_tri = 0, c_mat = 0;
-    bool spill = false, heavy = false;
     int steps = 0;
 
-    if (lx < a.tw && ly < a.th) {
-        const int x = a.x0 + lx;
-        const int y = frame_row(a, ly);
-        uint32_t seed;
-        V3 o, d;
-        primary_ray(a, x, y, seed, o, d);
-        V3 fin = {0.0f, 0.0f, 0.0f};
-        V3 att = {1.0f, 1.0f, 1.0f};
-        for (int b = 0; b < a.max_bounces; ++b) {                         // :179
-            if ((FEAT & kFeatSpill) && b == a.seg_limit) {               // hand the path on
-                spill = true;
-                PathState* st = a.spill + atomicAdd(a.spill_count, 1u);
-                st->q0 = make_float4(o.x, o.y, o.z, att.x);
-                st->q1 = make_float4(d.x, d.y, d.z, att.y);
-                st->q2 = make_float4(att.z, __uint_as_float(seed), __int_as_float(b),
-                                     __int_as_float(lx | (ly << 16)));
-                break;
+    uint32_t seed = 0;
+    V3 o = {0.f, 0.f, 0.f}, d = {0.f, 0.f, 1.f};
+    if (pixel) primary_ray(a, a.x0 + lx, frame_row(a, ly), seed, o, d);
+    V3 fin = {0.0f, 0.0f, 0.0f};
+    V3 att = {1.0f, 1.0f, 1.0f};
+    bool alive = pixel, handed_on = false;
+
+    // The bounce loop (:179) is wave-uniform: a lane whose path has ended
+    // stays in it with alive = false, so the cooperative tail below can use
+    // every lane of the wave.
+    for (int b = 0; b < a.max_bounces; ++b) {
+        if (__ballot(alive) == 0) break;
+        if ((FEAT & kFeatSpill) && alive && b == a.seg_limit) {           // hand the path on
+            PathState* st = a.spill + atomicAdd(a.spill_count, 1u);
+            st->q0 = make_float4(o.x, o.y, o.z, att.x);
+            st->q1 = make_float4(d.x, d.y, d.z, att.y);
+            st->q2 = make_float4(att.z, __uint_as_float(seed), __int_as_float(b), __int_as_float(lx | (ly << 16)));
+            alive = false;
+            handed_on = true;
+        }
+        float closest = kTMax;
+        int hit = -1;
+        const V3 inv = {1.0f / d.x, 1.0f / d.y, 1.0f / d.z};              // :89
+        // The walk's position: n = the next node the reference would visit.
+        int n = 0;
+        bool nleaf = a.scene.root_leaf != 0;
+        bool walking = alive && end > 0;
+        // walk 1 state: n's t_enter (+inf: its slab test failed) unless nload
+        // (n's own box still to be read); done_n: n is finished; skip(n) if known
+        // (else -1); the stack depth and its lowest entry still held; the kind
+        // of record the next load fetches.
+        float nte = __builtin_inff();
+        int nskip = end, sp = 0, lo = 0, kind = kPair;
+        bool lost = false, nload = false, done_n = false;
+        if (WALK == 1 && walking) {
+            float te;
+            bool ind;
+            slab(make_float4(rlo.x, rlo.y, rlo.z, 0.f), make_float4(rhi.x, rhi.y, rhi.z, 0.f), o, inv, te, ind);
+            nte = ind ? te : __builtin_inff();
+        }
+        if (COUNT && alive) {
+            ++c_seg;
+            if (end > 0) ++c_node;                                       // the root visit
+        }
+        if (WALK == 0 && !(FEAT & (kFeatPrio | kFeatHeavy))) {
+            // The per-node walk: one dependent load per visit, lanes in lockstep.
+            while (walking) {
+                n = node_step<COUNT>(nodes, leafs, n, nleaf, o, d, inv, closest, hit, c_node, c_tri);
+                walking = n < end;
+                if ((FEAT & kFeatCoopTail) && __popcll(__ballot(walking)) <= a.coop_lanes) break;
             }
-            if (COUNT) ++c_seg;
-            float closest = kTMax;
-            int hit = -1;
-            const V3 inv = {1.0f / d.x, 1.0f / d.y, 1.0f / d.z};          // :89
-            int i = 0;
-            while (i < a.scene.end) {
-                i = node_step<COUNT>(a.scene.nodes, a.scene.tris, i, o, d, inv, closest, hit, c_node, c_tri);
-                // A wave still walking after prio_after steps holds the frame's
-                // critical path: let it win instruction arbitration.
-                if (FEAT & (kFeatPrio | kFeatHeavy)) ++steps;
-                if ((FEAT & kFeatPrio) && steps == a.prio_after) __builtin_amdgcn_s_setprio(3);
-                if ((FEAT & kFeatHeavy) && steps >= a.heavy_budget && i < a.scene.end) {   // hand the walk on
-                    heavy = true;
-                    HeavyRay* hv = a.heavy + atomicAdd(a.heavy_count, 1u);
-                    hv->p.q0 = make_float4(o.x, o.y, o.z, att.x);
-                    hv->p.q1 = make_float4(d.x, d.y, d.z, att.y);
-                    hv->p.q2 = make_float4(att.z, __uint_as_float(seed), __int_as_float(b),
-                                           __int_as_float(lx | (ly << 16)));
-                    hv->q3 = make_float4(closest, __int_as_float(i), __int_as_float(hit), 0.0f);
+        } else for (;;) {
+            if (WALK == 1 && walking) {
+                // Advance, without memory traffic, to the next visit that
+                // needs a record: misses are counted and popped here.
+                for (;;) {
+                    if (!done_n) {
+                        if (nload) {
+                            if (n >= end) walking = false;
+                            kind = kNode;
+                            break;
+                        }
+                        if (nte < closest) {
+                            kind = nleaf ? kLeaf : kPair;
+                            break;
+                        }
+                        // n's box is missed: its subtree is finished
+                    }
+                    done_n = false;
+                    if (sp > lo) {                                // the reference's next pop
+                        --sp;
+                        uint2 e = stk[sp & (kStack - 1)][threadIdx.x];
+                        pin(e);
+                        nte = __uint_as_float(e.x);
+                        n = (int)(e.y & kIdx);
+                        nleaf = (e.y >> 31) != 0u;
+                        nskip = -1;
+                        continue;
+                    }
+                    if (!lost) {
+                        walking = false;
+                        break;
+                    }
+                    // Entries were dropped: the next node is skip(n) in preorder.
+                    if (nskip >= 0) {
+                        n = nskip;
+                        nload = true;
+                        continue;
+                    }
+                    kind = kSkip;                                 // skip(n) is in n's own record
                     break;
                 }
             }
-            if (heavy) break;
+            const uint64_t wm = __ballot(walking);
+            if (wm == 0) break;
+            if ((FEAT & kFeatCoopTail) && __popcll(wm) <= a.coop_lanes) break;
+            if (!walking) continue;
+            if (FEAT & (kFeatPrio | kFeatHeavy)) ++steps;
+            // A wave still walking after prio_after steps holds the frame's
+            // critical path: let it win instruction arbitration.
+            if ((FEAT & kFeatPrio) && steps == a.prio_after) __builtin_amdgcn_s_setprio(3);
+            if ((FEAT & kFeatHeavy) && steps >= a.heavy_budget) {      // hand the walk on
+                const int start = (WALK == 1 && kind == kSkip) ? (int)(__float_as_uint(nodes[2 * n].w) & kIdx) : n;
+                HeavyRay* hv = a.heavy + atomicAdd(a.heavy_count, 1u);
+                hv->p.q0 = make_float4(o.x, o.y, o.z, att.x);
+                hv->p.q1 = make_float4(d.x, d.y, d.z, att.y);
+                hv->p.q2 = make_float4(att.z, __uint_as_float(seed), __int_as_float(b),
+                                       __int_as_float(lx | (ly << 16)));
+                hv->q3 = make_float4(closest, __int_as_float(start), __int_as_float(hit), 0.f);
+                alive = false;
+                handed_on = true;
+                walking = false;
+                continue;
+            }
+            if (WALK == 0) {
+                n = node_step<COUNT>(nodes, leafs, n, nleaf, o, d, inv, closest, hit, c_node, c_tri);
+                walking = n < end;
+                continue;
+            }
+            // One record per lane per step, whatever its kind (arrays padded
+            // so that four float4 are always readable).
+            const float4* rp = kind == kPair ? pairs + 4 * n : kind == kLeaf ? leafs + 3 * n : nodes + 2 * n;
+            float4 Q0 = rp[0];
+            float4 Q1 = rp[1];
+            float4 Q2 = rp[2];
+            float4 Q3 = rp[3];
+            pin(Q0);
+            pin(Q1);
+            pin(Q2);
+            pin(Q3);
+            if (kind == kPair) {
+                // n is a hit internal node: its two children are visited
+                // (counted here).  Both slab tests at once; a child whose box
+                // already misses at this closest_t misses at every later one,
+                // so only live children are walked or stacked.
+                if (COUNT) c_node += 2;
+                float teL, teR;
+                bool indL, indR;
+                slab(Q0, Q1, o, inv, teL, indL);
+                slab(make_float4(Q0.w, Q1.w, Q2.w, 0.f), Q2, o, inv, teR, indR);
+                const uint32_t rw = __float_as_uint(Q3.x);
+                const int skp = (int)__float_as_uint(Q3.z);
+                const float tL = indL ? teL : __builtin_inff();
+                const float tR = indR ? teR : __builtin_inff();
+                const bool hL = tL < closest, hR = tR < closest;
+                if (hL) {
+                    if (hR) {                                     // R waits on the stack
+                        stk[sp & (kStack - 1)][threadIdx.x] = make_uint2(__float_as_uint(tR), rw);
+                        ++sp;
+                        if (sp - lo > kStack) {
+                            lo = sp - kStack;
+                            lost = true;
+                        }
+                    }
+                    n = n + 1;
+                    nte = tL;
+                    nleaf = __float_as_uint(Q3.y) != 0u;
+                    nskip = hR ? (int)(rw & kIdx) : skp;
+                } else if (hR) {
+                    n = (int)(rw & kIdx);
+                    nte = tR;
+                    nleaf = (rw >> 31) != 0u;
+                    nskip = skp;
+                } else {
+                    done_n = true;
+                    nskip = skp;
+                }
+            } else if (kind == kLeaf) {
+                // n is a hit leaf: the triangle test (:196-200).
+                if (COUNT) ++c_tri;
+                float t;
+                if (tri_test(Q0, Q1, Q2, o, d, t) && t < closest) {
+                    closest = t;
+                    hit = __float_as_int(Q0.w);
+                }
+                done_n = true;
+                nskip = n + 1;
+            } else if (kind == kNode) {
+                float te;
+                bool ind;
+                slab(Q0, Q1, o, inv, te, ind);
+                nte = ind ? te : __builtin_inff();
+                nleaf = (__float_as_uint(Q1.w) & 2u) != 0u;
+                nskip = (int)(__float_as_uint(Q0.w) & kIdx);
+                nload = false;
+            } else {
+                n = (int)(__float_as_uint(Q0.w) & kIdx);
+                nload = true;
+            }
+        }
+        if (FEAT & kFeatCoopTail) {
+            // Every lane is here.  Finish the remaining walks one ray at a
+            // time with the whole wave, each from its next node n.
+            uint64_t rem = __ballot(walking);
+            while (rem != 0) {
+                const int L = __ffsll((long long)rem) - 1;
+                rem &= rem - 1;
+                const V3 bo = {lane_f(o.x, L), lane_f(o.y, L), lane_f(o.z, L)};
+                const V3 bd = {lane_f(d.x, L), lane_f(d.y, L), lane_f(d.z, L)};
+                const V3 bi = {lane_f(inv.x, L), lane_f(inv.y, L), lane_f(inv.z, L)};
+                float bc = lane_f(closest, L);
+                int bh = lane_i(hit, L);
+                unsigned long long cn = 0, ct = 0;   // wave-uniform: counted once, by lane L
+                int start = n;
+                if (WALK == 1 && kind == kSkip && lane == L) start = (int)(__float_as_uint(nodes[2 * n].w) & kIdx);
+                coop_walk<COUNT>(nodes, leafs, end, lane_i(start, L), bo, bd, bi, bc, bh, cn, ct);
+                if (lane == L) {
+                    closest = bc;
+                    hit = bh;
+                    if (COUNT) {
+                        c_node += cn;
+                        c_tri += ct;
+                    }
+                }
+            }
+        }
+        if (alive) {
             if (hit >= 0) {                                               // :212
                 if (COUNT) ++c_mat;
-                const V3 n = hit_normal(a.scene.tris, hit, d);
+                const V3 nrm = hit_normal(a.scene.norms, hit, d);
                 const V3 hp = vadd(o, vscale(d, closest));                  // ray_at :77-79
                 const float4 M = a.scene.mats[hit];
                 V3 nd;
-                if (!scatter(M, d, n, seed, nd)) break;                   // attenuation = 0: black
-                att = vmul(att, V3{M.x, M.y, M.z});
-                o = hp;
-                d = nd;
+                if (!scatter(M, d, nrm, seed, nd)) {
+                    alive = false;                                        // attenuation = 0: black
+                } else {
+                    att = vmul(att, V3{M.x, M.y, M.z});
+                    o = hp;
+                    d = nd;
+                    if (b == a.max_bounces - 1) {                         // :229-231
+                        fin = {0.0f, 0.0f, 0.0f};
+                        alive = false;
+                    }
+                }
             } else {
                 fin = vmul(att, sky_color(d));
-                break;
+                alive = false;
             }
-            if (b == a.max_bounces - 1) fin = {0.0f, 0.0f, 0.0f};        // :229-231
         }
-        if (!spill && !heavy) write_pixel(a, lx, ly, fin);
     }
+    if (pixel && !handed_on) write_pixel(a, lx, ly, fin);
     if (COUNT) flush_counters(a.counters, c_seg, c_node, c_tri, c_mat);
     if (DIAG) diag_stamp(drec, 1);
 }
@@ -330,9 +631,10 @@ __global__ __launch_bounds__(256) void trace_persistent(TraceArgs a) {
     // paths the simple pass spilled, in spill order.
     const int n_slots = a.resume ? (int)*a.spill_count : tiles_x * ((a.th + 7) >> 3) * 64;
     const float4* __restrict__ nodes = a.scene.nodes;
-    const float4* __restrict__ tris = a.scene.tris;
+    const float4* __restrict__ leafs = a.scene.leafs;
     const int end = a.scene.end;
     const int shade_min = a.shade_min;
+    const bool root_leaf = a.scene.root_leaf != 0;
 
     unsigned long long c_seg = 0, c_node = 0, c_tri = 0, c_mat = 0;
     int pool_next = 0, pool_end = 0;     // wave-uniform: this wave's unclaimed slots
@@ -340,12 +642,13 @@ __global__ __launch_bounds__(256) void trace_persistent(TraceArgs a) {
 
     int mode = kIdle;
     int lx = 0, ly = 0, b = 0, node = 0, hit = -1;
+    bool leaf = root_leaf;
     uint32_t seed = 0;
     float closest = kTMax;
     V3 o = {0.f, 0.f, 0.f}, d = {0.f, 0.f, 1.f}, inv = {0.f, 0.f, 1.f}, att = {1.f, 1.f, 1.f};
 
     for (;;) {
-        // ---- refill idle lanes with new pixels (consecutive slots = one 8x8 tile)
+        // ---- refill idle lanes (consecutive slots = one 8x8 tile / spill order)
         uint64_t idle = __ballot(mode == kIdle);
         while (idle != 0 && !exhausted) {
             if (pool_next >= pool_end) {
@@ -358,40 +661,44 @@ __global__ __launch_bounds__(256) void trace_persistent(TraceArgs a) {
             }
             const int avail = pool_end - pool_next;
             const int rank = lanes_below(idle);
-            if (a.resume) {
-                if (mode == kIdle && rank < avail && pool_next + rank < n_slots) {
-                    const PathState p = a.spill[pool_next + rank];
-                    o = {p.q0.x, p.q0.y, p.q0.z};
-                    d = {p.q1.x, p.q1.y, p.q1.z};
-                    att = {p.q0.w, p.q1.w, p.q2.x};
-                    seed = __float_as_uint(p.q2.y);
-                    b = __float_as_int(p.q2.z);
-                    const int pix = __float_as_int(p.q2.w);
-                    lx = pix & 0xFFFF;
-                    ly = pix >> 16;
-                    inv = {1.0f / d.x, 1.0f / d.y, 1.0f / d.z};
-                    closest = kTMax;
-                    hit = -1;
-                    node = 0;
-                    mode = end > 0 ? kTrace : kReady;
-                    if (COUNT) ++c_seg;
-                }
-            } else if (mode == kIdle && rank < avail) {
+            if (mode == kIdle && rank < avail) {
                 const int slot = pool_next + rank;
-                const int tile = slot >> 6, w = slot & 63;
-                lx = (tile % tiles_x) * 8 + (w & 7);
-                ly = (tile / tiles_x) * 8 + (w >> 3);
-                if (lx < a.tw && ly < a.th) {
-                    const int x = a.x0 + lx, y = frame_row(a, ly);
-                    primary_ray(a, x, y, seed, o, d);
-                    att = {1.0f, 1.0f, 1.0f};
-                    b = 0;
+                bool start = false;
+                if (a.resume) {
+                    if (slot < n_slots) {
+                        const PathState p = a.spill[slot];
+                        o = {p.q0.x, p.q0.y, p.q0.z};
+                        d = {p.q1.x, p.q1.y, p.q1.z};
+                        att = {p.q0.w, p.q1.w, p.q2.x};
+                        seed = __float_as_uint(p.q2.y);
+                        b = __float_as_int(p.q2.z);
+                        const int pix = __float_as_int(p.q2.w);
+                        lx = pix & 0xFFFF;
+                        ly = pix >> 16;
+                        start = true;
+                    }
+                } else {
+                    const int tile = slot >> 6, w = slot & 63;
+                    lx = (tile % tiles_x) * 8 + (w & 7);
+                    ly = (tile / tiles_x) * 8 + (w >> 3);
+                    if (lx < a.tw && ly < a.th) {
+                        primary_ray(a, a.x0 + lx, frame_row(a, ly), seed, o, d);
+                        att = {1.0f, 1.0f, 1.0f};
+                        b = 0;
+                        start = true;
+                    }
+                }
+                if (start) {
                     inv = {1.0f / d.x, 1.0f / d.y, 1.0f / d.z};
                     closest = kTMax;
                     hit = -1;
                     node = 0;
+                    leaf = root_leaf;
                     mode = end > 0 ? kTrace : kReady;
-                    if (COUNT) ++c_seg;
+                    if (COUNT) {
+                        ++c_seg;
+                        if (end > 0) ++c_node;              // the root visit
+                    }
                 }
             }
             pool_next += min(__popcll(idle), avail);
@@ -401,7 +708,7 @@ __global__ __launch_bounds__(256) void trace_persistent(TraceArgs a) {
         // ---- traversal: step until enough lanes wait to be shaded
         for (;;) {
             if (mode == kTrace) {
-                node = node_step<COUNT>(nodes, tris, node, o, d, inv, closest, hit, c_node, c_tri);
+                node = node_step<COUNT>(nodes, leafs, node, leaf, o, d, inv, closest, hit, c_node, c_tri);
                 if (node >= end) mode = kReady;
             }
             const uint64_t trace = __ballot(mode == kTrace);
@@ -414,7 +721,7 @@ __global__ __launch_bounds__(256) void trace_persistent(TraceArgs a) {
             V3 fin = {0.0f, 0.0f, 0.0f};
             if (hit >= 0) {
                 if (COUNT) ++c_mat;
-                const V3 n = hit_normal(tris, hit, d);
+                const V3 n = hit_normal(a.scene.norms, hit, d);
                 const V3 hp = vadd(o, vscale(d, closest));
                 const float4 M = a.scene.mats[hit];
                 V3 nd;
@@ -427,9 +734,13 @@ __global__ __launch_bounds__(256) void trace_persistent(TraceArgs a) {
                     closest = kTMax;
                     hit = -1;
                     node = 0;
+                    leaf = root_leaf;
                     mode = end > 0 ? kTrace : kReady;
                     finish = false;
-                    if (COUNT) ++c_seg;
+                    if (COUNT) {
+                        ++c_seg;
+                        if (end > 0) ++c_node;              // the root visit
+                    }
                 }
                 // absorbed (:220-222) or scattered on the last bounce (:229-231): black
             } else {
@@ -446,98 +757,8 @@ __global__ __launch_bounds__(256) void trace_persistent(TraceArgs a) {
 }
 
 // ------------------------------------------------------- cooperative kernel --
-//
-// One wave walks ONE ray.  The walk is the reference's preorder visit sequence
-// (compute_dynamic_ray.comp:185-210), replayed exactly:
-//   1. lane k loads node n+k of the window [n, n+64) (2 KB, coalesced) and
-//      computes its slab test; leaves whose box is hit at the current
-//      closest_t also run the triangle test up to (but not including) the
-//      "t < closest_t" compare (:105-122);
-//   2. ballots turn "box hit at closest_t" (H), "triangle hit that improves
-//      closest_t" (T) and "is a leaf" (Lf) into 64-bit masks;
-//   3. the scalar unit replays the walk through the window: node k is hit iff
-//      bit k of H; next = k+1 on a hit, skip(k) on a miss; a triangle hit
-//      updates closest_t / hit and re-ballots H and T (closest_t only shrinks,
-//      so a leaf not pre-tested at the old closest_t cannot hit at the new one).
-// Box and triangle tests are the same float operations as node_step, so
-// closest_t, the hit and the visit / test counts equal the per-lane walk's.
-
-__device__ __forceinline__ int lane_i(int v, int k) { return __builtin_amdgcn_readlane(v, k); }
-__device__ __forceinline__ float lane_f(float v, int k) {
-    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), k));
-}
-
-template <bool COUNT>
-__device__ __forceinline__ void coop_walk(const float4* __restrict__ nodes, const float4* __restrict__ tris,
-                                          int end, int n, V3 o, V3 d, V3 inv, float& closest, int& hit,
-                                          unsigned long long& c_node, unsigned long long& c_tri) {
-    const int lane = threadIdx.x & 63;
-    while (n < end) {
-        const int j = n + lane;
-        float te = 0.0f, tt = 0.0f;
-        int sk = 0, lf = -1;
-        bool ind = false, tv = false;
-        if (j < end) {
-            const float4 A = nodes[2 * j];
-            const float4 B = nodes[2 * j + 1];
-            const float t0x = (A.x - o.x) * inv.x, t1x = (B.x - o.x) * inv.x;
-            const float t0y = (A.y - o.y) * inv.y, t1y = (B.y - o.y) * inv.y;
-            const float t0z = (A.z - o.z) * inv.z, t1z = (B.z - o.z) * inv.z;
-            te = fmaxf(fmaxf(fminf(t0x, t1x), fminf(t0y, t1y)), fminf(t0z, t1z));
-            const float tx = fminf(fminf(fmaxf(t0x, t1x), fmaxf(t0y, t1y)), fmaxf(t0z, t1z));
-            ind = tx > te && tx > kTMin;
-            sk = __float_as_int(A.w);
-            lf = __float_as_int(B.w);
-            if (ind && lf >= 0 && te < closest) {
-                const float4 P0 = tris[3 * lf + 0];
-                const float4 P1 = tris[3 * lf + 1];
-                const float4 P2 = tris[3 * lf + 2];
-                const V3 v0 = {P0.x, P0.y, P0.z};
-                const V3 e1 = {P1.x, P1.y, P1.z};
-                const V3 e2 = {P2.x, P2.y, P2.z};
-                const V3 pv = vcross(d, e2);
-                const float det = vdot(e1, pv);
-                if (!(det > -0.00001f && det < 0.00001f)) {
-                    const float inv_det = 1.0f / det;
-                    const V3 s = vsub(o, v0);
-                    const float uu = inv_det * vdot(s, pv);
-                    if (!(uu < 0.0f || uu > 1.0f)) {
-                        const V3 q = vcross(s, e1);
-                        const float vv = inv_det * vdot(d, q);
-                        if (!(vv < 0.0f || (uu + vv) > 1.0f)) {
-                            tt = inv_det * vdot(e2, q);
-                            tv = tt > kTMin;
-                        }
-                    }
-                }
-            }
-        }
-        uint64_t H = __ballot(ind && te < closest);
-        uint64_t T = __ballot(tv && tt < closest);
-        const uint64_t Lf = __ballot(lf >= 0);
-        const int lim = min(64, end - n);
-        int k = 0;
-        while (k < lim) {
-            if (COUNT) ++c_node;
-            if ((H >> k) & 1ull) {
-                if ((Lf >> k) & 1ull) {
-                    if (COUNT) ++c_tri;
-                    if ((T >> k) & 1ull) {
-                        closest = lane_f(tt, k);
-                        hit = lane_i(lf, k);
-                        H = __ballot(ind && te < closest);
-                        T = __ballot(tv && tt < closest);
-                    }
-                }
-                ++k;
-            } else {
-                k = lane_i(sk, k) - n;
-            }
-        }
-        n += k;
-    }
-}
-
+// Tier 2 of the tiered schedule: one wave per suspended path, coop_walk for
+// the rest of its current segment and all later ones.
 template <bool COUNT>
 __global__ __launch_bounds__(256) void trace_coop(TraceArgs a) {
     const int lane = threadIdx.x & 63;
@@ -562,13 +783,13 @@ __global__ __launch_bounds__(256) void trace_coop(TraceArgs a) {
         V3 fin = {0.0f, 0.0f, 0.0f};
         for (;;) {
             const V3 inv = {1.0f / d.x, 1.0f / d.y, 1.0f / d.z};
-            coop_walk<COUNT>(a.scene.nodes, a.scene.tris, end, node, o, d, inv, closest, hit, c_node, c_tri);
+            coop_walk<COUNT>(a.scene.nodes, a.scene.leafs, end, node, o, d, inv, closest, hit, c_node, c_tri);
             if (hit < 0) {
                 fin = vmul(att, sky_color(d));
                 break;
             }
             if (COUNT) ++c_mat;
-            const V3 n = hit_normal(a.scene.tris, hit, d);
+            const V3 n = hit_normal(a.scene.norms, hit, d);
             const V3 hp = vadd(o, vscale(d, closest));
             const float4 M = a.scene.mats[hit];
             V3 nd;
@@ -580,7 +801,10 @@ __global__ __launch_bounds__(256) void trace_coop(TraceArgs a) {
             closest = kTMax;
             hit = -1;
             node = 0;
-            if (COUNT) ++c_seg;
+            if (COUNT) {
+                ++c_seg;
+                if (end > 0) ++c_node;              // the root visit
+            }
         }
         if (lane == 0) write_pixel(a, pix & 0xFFFF, pix >> 16, fin);
     }
@@ -621,7 +845,7 @@ hipError_t launch_trace(const TraceArgs& a, hipStream_t stream) {
         return hipGetLastError();
     }
     if (a.kernel == kKernelSplit) {
-        // pass 1: coherent 8x8 lockstep tiles for the first seg_limit segments
+        // pass 1: lockstep tiles for the first seg_limit segments
         TraceArgs s = a;
         s.kernel = kKernelSimple;
         s.resume = 0;
@@ -648,17 +872,26 @@ hipError_t launch_trace(const TraceArgs& a, hipStream_t stream) {
         const int tw_w = 8 << a.wave_tile, th_w = 8 >> a.wave_tile;
         const dim3 grid((a.tw + 4 * tw_w - 1) / (4 * tw_w), (a.th + th_w - 1) / th_w);
         const int feat = (a.seg_limit < (1 << 30) ? kFeatSpill : 0) |
-                         (a.heavy_budget < (1 << 30) ? kFeatHeavy : 0) | (a.prio_after > 0 ? kFeatPrio : 0);
-#define RT_SIMPLE(F)                                                                              \
-        if (a.diag) hipLaunchKernelGGL((trace_simple<false, true, F>), grid, block, 0, stream, a); \
-        else if (a.counters) hipLaunchKernelGGL((trace_simple<true, false, F>), grid, block, 0, stream, a); \
-        else hipLaunchKernelGGL((trace_simple<false, false, F>), grid, block, 0, stream, a);
-        switch (feat) {
-            case 0: RT_SIMPLE(0) break;
-            case kFeatSpill: RT_SIMPLE(kFeatSpill) break;
-            case kFeatHeavy: RT_SIMPLE(kFeatHeavy) break;
-            case kFeatPrio: RT_SIMPLE(kFeatPrio) break;
-            default: RT_SIMPLE(kFeatSpill | kFeatHeavy | kFeatPrio) break;
+                         (a.heavy_budget < (1 << 30) ? kFeatHeavy : 0) | (a.prio_after > 0 ? kFeatPrio : 0) |
+                         (a.coop_lanes > 0 ? kFeatCoopTail : 0);
+#define RT_SIMPLE(F, W)                                                                                        \
+        if (a.diag) hipLaunchKernelGGL((trace_simple<false, true, F, W>), grid, block, 0, stream, a);           \
+        else if (a.counters) hipLaunchKernelGGL((trace_simple<true, false, F, W>), grid, block, 0, stream, a); \
+        else hipLaunchKernelGGL((trace_simple<false, false, F, W>), grid, block, 0, stream, a);
+        if (a.walk == 0) {
+            switch (feat) {
+                case 0: RT_SIMPLE(0, 0) break;
+                case kFeatCoopTail: RT_SIMPLE(kFeatCoopTail, 0) break;
+                default: RT_SIMPLE(kFeatSpill | kFeatHeavy | kFeatPrio | kFeatCoopTail, 0) break;
+            }
+        } else {
+            switch (feat) {
+                case 0: RT_SIMPLE(0, 1) break;
+                case kFeatCoopTail: RT_SIMPLE(kFeatCoopTail, 1) break;
+                case kFeatSpill: RT_SIMPLE(kFeatSpill, 1) break;
+                case kFeatHeavy: RT_SIMPLE(kFeatHeavy, 1) break;
+                default: RT_SIMPLE(kFeatSpill | kFeatHeavy | kFeatPrio | kFeatCoopTail, 1) break;
+            }
         }
 #undef RT_SIMPLE
     }

@@ -182,7 +182,7 @@ def main() -> None:
                 "partition": "single frame" if world == 1 else
                              f"interleaved {band_h}-row bands, RCCL gather + assembly on rank 0",
                 "parallelism": f"tile{world}",
-                "schedule": {k: renderer.get_option(k) for k in ("kernel", "shade_min", "blocks_per_cu")},
+                "schedule": {k: renderer.get_option(k) for k in ("kernel", "walk", "wave_tile", "coop_lanes")},
             },
             "roofline": {
                 "bound": "hbm",
@@ -198,6 +198,7 @@ def main() -> None:
                 "alg_bytes_per_segment": round(alg_bytes / l_seg, 1),
                 "reference_layout_frac": round(ref_layout_bytes / (kernel_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
             },
+            "primary_mrays_s": round(pixels * args.steps / elapsed / 1e6, 2),
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)

@@ -134,20 +134,32 @@ int rt_band_rows(int height, int band_h, int band_stride, int band_off);
 
 /* Schedule options (no effect on results, which are identical for every
  * setting):
- *   "kernel"        0 = one lane per pixel (the reference's dispatch shape),
+ *   "kernel"        0 = one lane per pixel (the reference's dispatch shape;
+ *                       default),
  *                   1 = persistent waves with a tile queue,
  *                   2 = split: kernel 0 for the first seg_limit segments of
  *                       every path, then the surviving paths, compacted, on
- *                       persistent waves
+ *                       persistent waves,
+ *                   3 = tiered: kernel 0 with a per-path visit budget; walks
+ *                       over budget finish one wave per ray (64-node windows)
+ *   "walk"          kernel 0: 0 = one node per step (default), 1 = child-pair
+ *                   records + per-lane stack of right-child entry distances
+ *   "coop_lanes"    kernel 0: once at most this many lanes of a wave are still
+ *                   walking, the whole wave finishes their walks one ray at a
+ *                   time (0..64, default 2; 0 = off)
+ *   "wave_tile"     kernel 0: pixels per wave (8<<s) x (8>>s), s = 0..3
+ *                   (default 2: 32x2)
+ *   "prio_after"    kernel 0: raise a wave's priority after this many walk
+ *                   steps (0 = never, default)
  *   "seg_limit"     split: segments traced in the first pass (default 2)
+ *   "heavy_budget"  tiered: walk steps per path in the first pass (default 256)
  *   "shade_min"     persistent: shade once this many lanes of a wave are
  *                   ready (1..64, default 16)
  *   "blocks_per_cu" persistent: resident 256-thread blocks per CU (0 = from
  *                   the occupancy query)
- *   "wave_tile"     kernel 0: pixels per wave (8<<s) x (8>>s), s = 0..3
- * Defaults can also be set with the RTAMD_KERNEL=simple|persistent|split,
- * RTAMD_SEG_LIMIT,
- * RTAMD_SHADE_MIN and RTAMD_BLOCKS_PER_CU environment variables. */
+ * Defaults can also be set with the environment variables
+ * RTAMD_KERNEL=simple|persistent|split|tiered, RTAMD_WALK, RTAMD_COOP_LANES,
+ * RTAMD_SEG_LIMIT, RTAMD_SHADE_MIN and RTAMD_BLOCKS_PER_CU. */
 int rt_set_option(rt_ctx* ctx, const char* name, int64_t value);
 /* Diagnostics: with option "diag" = 1, kernel 0 records per wave
  * {start, end} (s_memrealtime, 100 MHz), {XCC id << 32 | HW_ID}, {block << 8 |

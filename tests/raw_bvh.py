@@ -1,0 +1,61 @@
+"""Hand-built BVHs in the reference's flat layout (BVHFlattener.java:51-90 record format),
+for shapes the reference's own builder never makes."""
+import struct
+from types import SimpleNamespace
+
+import numpy as np
+
+
+def raw_bvh_scene(n, shape, seed):
+    """Triangles in front of the default camera under a hand-built BVH of the
+    given shape: "left" = left-deep chain (right children are leaves), "right"
+    = right-deep chain, "random" = random split points.  Any tree in the
+    reference's preorder layout is a valid upload (VulkanEngine takes the
+    buffer as is); deep chains overflow the walk's 8-entry t_enter stack."""
+    rng = np.random.default_rng(seed)
+    c = rng.uniform(-14, 14, (n, 1, 3))
+    tv = (c + rng.uniform(-4, 4, (n, 3, 3))).astype(np.float32)
+    mats = np.concatenate([rng.uniform(0.2, 0.9, (n, 3)), rng.integers(0, 3, (n, 1))], 1).astype(np.float32)
+    lo, hi = tv.min(1), tv.max(1)
+
+    def build(ids):
+        if len(ids) == 1:
+            return ids[0]
+        if shape == "left":
+            k = len(ids) - 1
+        elif shape == "right":
+            k = 1
+        else:
+            k = int(rng.integers(1, len(ids)))
+        return (build(ids[:k]), build(ids[k:]))
+
+    recs, order = [], []
+
+    def rec(node):
+        my = len(recs)
+        recs.append(None)
+        if isinstance(node, tuple):
+            ids = []
+
+            def leaves(x):
+                if isinstance(x, tuple):
+                    leaves(x[0]), leaves(x[1])
+                else:
+                    ids.append(x)
+            leaves(node)
+            bmin, bmax = lo[ids].min(0), hi[ids].max(0)
+            li = rec(node[0])
+            ri = rec(node[1])
+            tail = struct.pack("<ii", li, ri)
+        else:
+            bmin, bmax = lo[node], hi[node]
+            tail = struct.pack("<ii", -(len(order) + 1), -1)
+            order.append(node)
+        recs[my] = struct.pack("<4f4f", *bmin, 0.0, *bmax, 0.0) + tail + b"\0" * 8
+        return my
+
+    rec(build(list(range(n))))
+    verts = np.zeros((n, 3, 4), np.float32)
+    verts[:, :, :3] = tv[order]
+    return SimpleNamespace(model_vertex_data=verts.reshape(-1), model_material_data=mats[order].reshape(-1),
+                           flat_bvh_data=np.frombuffer(b"".join(recs), np.uint8).copy(), triangle_count=n)

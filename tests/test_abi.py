@@ -112,3 +112,14 @@ def test_error_message_is_thread_local():
     t.start()
     t.join()
     assert b"null" in msg and seen == [b""]
+
+
+def test_unbalanced_bvh_validates():
+    """Left-/right-deep chains and random splits are valid preorder uploads."""
+    from raw_bvh import raw_bvh_scene
+    for shape, n, depth in (("left", 50, 49), ("right", 200, 199), ("random", 300, None)):
+        b = raw_bvh_scene(n, shape, seed=n)
+        nn, md = _validate(b.model_vertex_data, b.model_material_data, b.flat_bvh_data)
+        assert nn == 2 * n - 1
+        if depth is not None:
+            assert md == depth

@@ -9,12 +9,13 @@ import numpy as np
 import pytest
 
 from conftest import has_gpu
+from raw_bvh import raw_bvh_scene
 
 pytestmark = pytest.mark.gpu
 
 COUNTERS = ("segments", "node_visits", "tri_tests", "mat_reads")
 DEFAULT_OPTS = {"kernel": 0, "shade_min": 16, "blocks_per_cu": 0, "wave_tile": 2, "seg_limit": 2,
-                "heavy_budget": 256}
+                "heavy_budget": 256, "prio_after": 0, "coop_lanes": 2, "walk": 0}
 
 
 def _oracle(built, cam_bytes, w, h, b, **kw):
@@ -110,6 +111,10 @@ def test_config5_1m_row_subset(renderer):
 
 @pytest.mark.parametrize("opts", [
     {"kernel": 0},
+    {"kernel": 0, "coop_lanes": 0},
+    {"kernel": 0, "walk": 1},
+    {"kernel": 0, "walk": 1, "coop_lanes": 0},
+    {"kernel": 3, "walk": 1, "heavy_budget": 40},
     {"kernel": 1, "shade_min": 1},
     {"kernel": 1, "shade_min": 16},
     {"kernel": 1, "shade_min": 64},
@@ -121,6 +126,10 @@ def test_config5_1m_row_subset(renderer):
     {"kernel": 3, "heavy_budget": 1},
     {"kernel": 3, "heavy_budget": 40},
     {"kernel": 3, "heavy_budget": 256},
+    {"kernel": 0, "coop_lanes": 1},
+    {"kernel": 0, "coop_lanes": 8},
+    {"kernel": 0, "coop_lanes": 64},
+    {"kernel": 0, "coop_lanes": 4, "wave_tile": 0, "prio_after": 64},
 ])
 def test_schedules_identical(renderer, opts):
     """Every schedule gives the oracle's frame and counters (config 2 at the
@@ -281,3 +290,24 @@ def test_golden_frames_on_gpu(renderer):
         assert hashlib.sha256(rad.tobytes()).hexdigest() == g["radiance_sha256"], name
         for k in COUNTERS:
             assert st[k] == g["counts"][k], (name, k)
+
+
+
+@pytest.mark.parametrize("shape,n", [("left", 50), ("right", 200), ("random", 300)])
+@pytest.mark.parametrize("walk", [0, 1])
+def test_unbalanced_bvh(renderer, shape, n, walk):
+    from rtamd import configs
+    built = raw_bvh_scene(n, shape, seed=n)
+    renderer.upload_raw(built.model_vertex_data.tobytes(), built.model_material_data.tobytes(),
+                        built.flat_bvh_data.tobytes())
+    if shape == "random":
+        assert renderer.scene_info()["max_depth"] < 60     # the oracle's reference stack is 64 deep
+    try:
+        renderer.set_option("walk", walk)
+        for (w, h, b) in [(160, 96, 6), (33, 17, 10)]:
+            cam = configs.Camera.default(w, h)
+            rgba, rad, st = renderer.render(cam, w, h, b, radiance=True, stats=True)
+            _assert_same(rgba, rad, st, *_oracle(built, cam.ubo_bytes(), w, h, b))
+            assert st["tri_tests"] > 0
+    finally:
+        renderer.set_option("walk", 0)

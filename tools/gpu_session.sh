@@ -2,7 +2,8 @@
 # One GPU session on the gpurun box: parity tests, smoke, bench, rocprof.
 # Each GPU step has its own time limit; a fault / abort / timeout ends the
 # session (no further GPU step runs).  Usage: tools/gpu_session.sh TAG [steps...]
-# steps: test smoke bench prof pmc   (default: test smoke bench prof)
+# steps: test smoke bench prof pmc ab   (default: test smoke bench prof)
+# ab: tools/ab_bench.py with the arguments in $AB_ARGS
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
@@ -28,8 +29,9 @@ for s in $STEPS; do
     bench) run bench 600 python bench.py --steps 20 --warmup 5 > "$OUT/bench.json" 2> "$OUT/bench.err" ;;
     prof)  run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- \
                python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline > "$OUT/prof.log" 2>&1 ;;
-    pmc)   run pmc 600 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex trace_kernel --output-format csv \
+    pmc)   run pmc 600 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "trace_(simple|persistent|coop)" --output-format csv \
                -d "$OUT/pmc" -o run -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline > "$OUT/pmc.log" 2>&1 ;;
+    ab)    run ab 900 python tools/ab_bench.py ${AB_ARGS:-} > "$OUT/ab.jsonl" 2> "$OUT/ab.err" ;;
   esac
 done
 status "session done"
