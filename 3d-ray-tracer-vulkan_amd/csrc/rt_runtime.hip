@@ -232,6 +232,11 @@ struct PerDevice {
     size_t       heavy_cap = 0;
     int          n_cu = 0;
     int          blocks_per_cu = 1;
+    // rt_render_async: two frame slots, a copy stream, per-slot events
+    hipStream_t  copy_stream = nullptr;
+    uchar4*      d_ring[2] = {nullptr, nullptr};
+    size_t       ring_cap = 0;     // pixels per slot
+    hipEvent_t   traced[2] = {nullptr, nullptr}, copied[2] = {nullptr, nullptr};
 };
 
 static constexpr unsigned kQueueSlots = 64;
@@ -250,6 +255,7 @@ struct rt_ctx {
     int  walk = 0;                 // kernel 0: 0 = node per step (fastest measured), 1 = child pairs + t_enter stack
     bool has_scene = false;
     int  n_nodes = 0, n_tris = 0, max_depth = 0;
+    uint64_t issued = 0;           // rt_render_async tickets handed out
 };
 
 static void free_scene(PerDevice& p) {
@@ -382,6 +388,11 @@ int rt_create(const int* device_ids, int n_devices, rt_ctx** out) {
         if (e == hipSuccess) e = hipEventCreate(&p.ev1);
         if (e == hipSuccess) e = hipMalloc(&p.d_counters, sizeof(Counters));
         if (e == hipSuccess) e = hipMalloc(&p.d_queue, sizeof(unsigned) * 3 * kQueueSlots);
+        if (e == hipSuccess) e = hipStreamCreateWithFlags(&p.copy_stream, hipStreamNonBlocking);
+        for (int k2 = 0; k2 < 2 && e == hipSuccess; ++k2) {
+            e = hipEventCreateWithFlags(&p.traced[k2], hipEventDisableTiming);
+            if (e == hipSuccess) e = hipEventCreateWithFlags(&p.copied[k2], hipEventDisableTiming);
+        }
         p.n_cu = prop.multiProcessorCount;
         p.blocks_per_cu = persistent_blocks_per_cu();
         ctx->dev.push_back(p);
@@ -400,7 +411,14 @@ int rt_destroy(rt_ctx* ctx) {
     for (PerDevice& p : ctx->dev) {
         (void)hipSetDevice(p.device);
         if (p.stream) (void)hipStreamSynchronize(p.stream);
+        if (p.copy_stream) (void)hipStreamSynchronize(p.copy_stream);
         free_scene(p);
+        for (int k2 = 0; k2 < 2; ++k2) {
+            if (p.d_ring[k2]) (void)hipFree(p.d_ring[k2]);
+            if (p.traced[k2]) (void)hipEventDestroy(p.traced[k2]);
+            if (p.copied[k2]) (void)hipEventDestroy(p.copied[k2]);
+        }
+        if (p.copy_stream) (void)hipStreamDestroy(p.copy_stream);
         if (p.d_counters) (void)hipFree(p.d_counters);
         if (p.d_queue) (void)hipFree(p.d_queue);
         if (p.d_spill) (void)hipFree(p.d_spill);
@@ -680,6 +698,95 @@ int rt_render(rt_ctx* ctx, const rt_camera_ubo* cam, int width, int height, int 
             rc = collect_stats(ctx, p, px, stats, true);
             if (rc) return rc;
         }
+    }
+    return RT_OK;
+}
+
+void* rt_host_alloc(size_t bytes) {
+    void* p = nullptr;
+    if (bytes == 0 || hipHostMalloc(&p, bytes, hipHostMallocPortable) != hipSuccess) {
+        set_error("rt_host_alloc: could not pin %zu bytes", bytes);
+        return nullptr;
+    }
+    return p;
+}
+
+void rt_host_free(void* p) {
+    if (p) (void)hipHostFree(p);
+}
+
+int rt_render_async(rt_ctx* ctx, const rt_camera_ubo* cam, int width, int height, int max_bounces,
+                    uint8_t* out_rgba, uint64_t* ticket) {
+    int rc = check_render_args(ctx, cam, width, height, max_bounces, "rt_render_async");
+    if (rc) return rc;
+    if (!out_rgba || !ticket) { set_error("rt_render_async: out_rgba and ticket are required"); return RT_ERR_INVALID_ARG; }
+    const int nd = (int)ctx->dev.size();
+    const int bh = nd == 1 ? height : 16;
+    const int n_bands = (height + bh - 1) / bh;
+    const size_t band_bytes = (size_t)bh * (size_t)width * 4;
+    const uint64_t t = ctx->issued + 1;
+    const int slot = (int)(t & 1);
+    for (int k = 0; k < nd; ++k) {
+        const int rows = rt_band_rows(height, bh, nd, k);
+        if (rows == 0) continue;
+        PerDevice& p = ctx->dev[k];
+        RT_HIP_CHECK(hipSetDevice(p.device));
+        const size_t px = (size_t)width * rows;
+        if (px > p.ring_cap) {                      // grow both slots once nothing is in flight
+            RT_HIP_CHECK(hipStreamSynchronize(p.stream));
+            RT_HIP_CHECK(hipStreamSynchronize(p.copy_stream));
+            for (int k2 = 0; k2 < 2; ++k2) {
+                if (p.d_ring[k2]) (void)hipFree(p.d_ring[k2]);
+                p.d_ring[k2] = nullptr;
+            }
+            p.ring_cap = 0;
+            for (int k2 = 0; k2 < 2; ++k2) RT_HIP_CHECK(hipMalloc(&p.d_ring[k2], px * 4));
+            p.ring_cap = px;
+        }
+        // The slot's previous frame (ticket t-2) must be read back before it is overwritten.
+        RT_HIP_CHECK(hipStreamWaitEvent(p.stream, p.copied[slot], 0));
+        rc = render_bands_on(ctx, p, cam, width, height, max_bounces, bh, nd, k, rows, p.d_ring[slot], nullptr,
+                             p.stream, false);
+        if (rc) return rc;
+        RT_HIP_CHECK(hipEventRecord(p.traced[slot], p.stream));
+        RT_HIP_CHECK(hipStreamWaitEvent(p.copy_stream, p.traced[slot], 0));
+        if (nd == 1) {
+            RT_HIP_CHECK(hipMemcpyAsync(out_rgba, p.d_ring[slot], px * 4, hipMemcpyDeviceToHost, p.copy_stream));
+        } else {
+            // bands k, k+nd, ...: every full band in one strided copy, a partial last band on its own
+            const int n_k = (n_bands - k + nd - 1) / nd;
+            const int last = k + (n_k - 1) * nd;
+            const bool partial = (last + 1) * bh > height;
+            const int full = partial ? n_k - 1 : n_k;
+            if (full > 0)
+                RT_HIP_CHECK(hipMemcpy2DAsync(out_rgba + (size_t)k * band_bytes, (size_t)nd * band_bytes,
+                                              p.d_ring[slot], band_bytes, band_bytes, (size_t)full,
+                                              hipMemcpyDeviceToHost, p.copy_stream));
+            if (partial)
+                RT_HIP_CHECK(hipMemcpyAsync(out_rgba + (size_t)last * band_bytes,
+                                            reinterpret_cast<uint8_t*>(p.d_ring[slot]) + (size_t)full * band_bytes,
+                                            (size_t)(height - last * bh) * width * 4, hipMemcpyDeviceToHost,
+                                            p.copy_stream));
+        }
+        RT_HIP_CHECK(hipEventRecord(p.copied[slot], p.copy_stream));
+    }
+    ctx->issued = t;
+    *ticket = t;
+    return RT_OK;
+}
+
+int rt_render_wait(rt_ctx* ctx, uint64_t ticket) {
+    if (!ctx) { set_error("rt_render_wait: null context"); return RT_ERR_INVALID_ARG; }
+    if (ticket == 0 || ticket > ctx->issued) {
+        set_error("rt_render_wait: ticket %llu was not issued (last %llu)", (unsigned long long)ticket,
+                  (unsigned long long)ctx->issued);
+        return RT_ERR_INVALID_ARG;
+    }
+    // A slot's event may since have been re-recorded by a newer frame; copies
+    // complete in issue order, so waiting for the newer one covers this one.
+    for (PerDevice& p : ctx->dev) {
+        RT_HIP_CHECK(hipSetDevice(p.device));
+        RT_HIP_CHECK(hipEventSynchronize(p.copied[ticket & 1]));
     }
     return RT_OK;
 }

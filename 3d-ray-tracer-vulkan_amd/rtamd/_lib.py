@@ -32,6 +32,7 @@ EXPORTED = (
     "rt_camera_from_lookat", "rt_mesh_load_obj", "rt_mesh_tri_count", "rt_mesh_transform",
     "rt_mesh_free", "rt_mesh_procedural", "rt_render_bands_device", "rt_band_rows",
     "rt_scene_validate", "rt_set_option", "rt_get_option", "rt_diag_copy",
+    "rt_host_alloc", "rt_host_free", "rt_render_async", "rt_render_wait",
 )
 
 
@@ -117,6 +118,10 @@ def lib() -> C.CDLL:
                 "rt_set_option": (i32, [vp, C.c_char_p, C.c_int64]),
                 "rt_get_option": (i32, [vp, C.c_char_p, C.POINTER(C.c_int64)]),
                 "rt_diag_copy": (i32, [vp, vp, sz, C.POINTER(sz)]),
+                "rt_host_alloc": (vp, [sz]),
+                "rt_host_free": (None, [vp]),
+                "rt_render_async": (i32, [vp, C.POINTER(CameraUBO), i32, i32, i32, vp, C.POINTER(u64)]),
+                "rt_render_wait": (i32, [vp, u64]),
             }
             for name, (res, args) in sig.items():
                 f = getattr(L, name)

@@ -103,6 +103,19 @@ class Renderer:
                               C.byref(st) if st is not None else None))
         return rgba, rad, (st.as_dict() if st is not None else None)
 
+    def render_async(self, camera, width: int, height: int, max_bounces: int, out: "PinnedFrame") -> int:
+        """Enqueue a whole frame into a pinned host frame and return its ticket
+        (rt_render_async); the frame is complete after wait(ticket)."""
+        if out.shape != (height, width, 4):
+            raise ValueError(f"frame buffer is {out.shape}, need {(height, width, 4)}")
+        t = C.c_uint64()
+        check(lib().rt_render_async(self._ctx, C.byref(_ubo(camera)), width, height, max_bounces,
+                                    out.ptr, C.byref(t)))
+        return t.value
+
+    def wait(self, ticket: int) -> None:
+        check(lib().rt_render_wait(self._ctx, ticket))
+
     def render_tile_device(self, camera, width: int, height: int, max_bounces: int,
                            x0: int, y0: int, tile_w: int, tile_h: int,
                            d_rgba: Optional[int], d_radiance: Optional[int] = None,
@@ -114,6 +127,27 @@ class Renderer:
                                           x0, y0, tile_w, tile_h, d_rgba, d_radiance, stream,
                                           C.byref(st) if st is not None else None))
         return st.as_dict() if st is not None else None
+
+
+class PinnedFrame:
+    """An RGBA8 frame in pinned host memory (rt_host_alloc), as a numpy view."""
+
+    def __init__(self, height: int, width: int):
+        n = height * width * 4
+        self.ptr = lib().rt_host_alloc(n)
+        if not self.ptr:
+            raise RtError(-6, lib().rt_last_error().decode())   # RT_ERR_OOM
+        self.array = np.ctypeslib.as_array((C.c_uint8 * n).from_address(self.ptr)).reshape(height, width, 4)
+        self.shape = self.array.shape
+
+    def close(self) -> None:
+        if self.ptr:
+            self.array = None
+            lib().rt_host_free(self.ptr)
+            self.ptr = None
+
+    def __del__(self):
+        self.close()
 
 
 @dataclass
@@ -150,8 +184,12 @@ class HipEngine:
 
     def __init__(self, frame_queue: AtomicReference, width: int = REFERENCE_WIDTH,
                  height: int = REFERENCE_HEIGHT, max_bounces: int = REFERENCE_MAX_BOUNCES,
-                 device_ids: Sequence[int] = (0,), collect_stats: bool = False):
+                 device_ids: Sequence[int] = (0,), collect_stats: bool = False, pipelined: bool = True):
         self.frame_queue = frame_queue
+        # pipelined: two frames in flight (rt_render_async), so frame k's readback
+        # overlaps frame k+1's trace; the reference waits for each frame
+        # (VulkanEngine.java:410-429).  Stats need the synchronous path.
+        self.pipelined = pipelined and not collect_stats
         self.width, self.height, self.max_bounces = width, height, max_bounces
         self.device_ids = tuple(device_ids)
         self.collect_stats = collect_stats
@@ -162,6 +200,7 @@ class HipEngine:
         self._thread = threading.Thread(target=self._run, name="HIP-Engine-Thread", daemon=True)
         self.is_sky_enabled = 1
         self.frames_rendered = 0
+        self.frames_submitted = 0
         self.error: Optional[BaseException] = None
 
     # --- public API (UI thread) ---
@@ -185,12 +224,16 @@ class HipEngine:
     # --- render thread ---
     def _run(self) -> None:
         renderer = None
+        slots, pending = None, []
         try:
             renderer = Renderer(self.device_ids)
             have_scene, camera = False, None
             while self._running:
                 try:                                        # one scene per pass (:281-285)
-                    renderer.upload_scene(self._scene_q.get_nowait())
+                    scene = self._scene_q.get_nowait()
+                    while pending:                          # frames of the old scene first
+                        self._finish(renderer, slots, pending.pop(0))
+                    renderer.upload_scene(scene)
                     have_scene = True
                 except queue.Empty:
                     pass
@@ -209,13 +252,35 @@ class HipEngine:
                     continue
                 ubo = CameraUBO.from_buffer_copy(bytes(camera.ubo))
                 ubo.sky_enabled = self.is_sky_enabled        # written, ignored by the shader
-                rgba, _, st = renderer.render(ubo, self.width, self.height, self.max_bounces,
-                                              stats=self.collect_stats)
-                self.frame_queue.set(FrameData(rgba, st))
-                self.frames_rendered += 1
+                if not self.pipelined:
+                    rgba, _, st = renderer.render(ubo, self.width, self.height, self.max_bounces,
+                                                  stats=self.collect_stats)
+                    self._publish(FrameData(rgba, st))
+                    continue
+                if slots is None:
+                    slots = [PinnedFrame(self.height, self.width) for _ in range(2)]
+                k = self.frames_submitted % 2
+                pending.append((renderer.render_async(ubo, self.width, self.height, self.max_bounces, slots[k]), k))
+                self.frames_submitted += 1
+                if len(pending) == 2:
+                    self._finish(renderer, slots, pending.pop(0))
+            while pending:                                  # drain on stop
+                self._finish(renderer, slots, pending.pop(0))
         except BaseException as e:                          # FATAL (VRT) path, :197-201
             self.error = e
             self._running = False
         finally:
             if renderer is not None:
                 renderer.close()
+            for f in slots or ():
+                f.close()
+
+    def _finish(self, renderer, slots, item) -> None:
+        ticket, k = item
+        renderer.wait(ticket)
+        # a fresh buffer per frame, as the reference publishes (:416-429)
+        self._publish(FrameData(slots[k].array.copy()))
+
+    def _publish(self, frame: "FrameData") -> None:
+        self.frame_queue.set(frame)
+        self.frames_rendered += 1

@@ -132,6 +132,24 @@ int rt_render_bands_device(rt_ctx* ctx, const rt_camera_ubo* cam,
 /* Row count of such a band set (-1 for bad arguments).  Pure host code. */
 int rt_band_rows(int height, int band_h, int band_stride, int band_off);
 
+/* Pipelined frames (overlap the readback with the next
+ * frame; the reference waits on a fence after every frame,
+ * VulkanEngine.java:410-429).
+ *
+ * rt_render_async enqueues one whole frame (trace + RGBA8 readback into
+ * out_rgba) and returns at once with a ticket; rt_render_wait blocks until that
+ * frame is complete in out_rgba.  Two frame slots rotate per device, so with two
+ * frames in flight the readback of frame k overlaps the trace of frame k+1.
+ * out_rgba must stay valid until its ticket completes; it should come from
+ * rt_host_alloc (pinned, portable), since a copy into pageable memory cannot run
+ * asynchronously.  A Java host wraps rt_host_alloc memory with JNI
+ * NewDirectByteBuffer.  Frames are identical to rt_render's. */
+void* rt_host_alloc(size_t bytes);
+void  rt_host_free(void* p);
+int rt_render_async(rt_ctx* ctx, const rt_camera_ubo* cam, int width, int height, int max_bounces,
+                    uint8_t* out_rgba, uint64_t* ticket);
+int rt_render_wait(rt_ctx* ctx, uint64_t ticket);
+
 /* Schedule options (no effect on results, which are identical for every
  * setting):
  *   "kernel"        0 = one lane per pixel (the reference's dispatch shape;

@@ -248,6 +248,43 @@ def test_multi_device_context_interleaves(renderer):
         assert st[k] == ref_st[k]
 
 
+@pytest.mark.parametrize("devices", [(0,), (0, 0)])
+def test_render_async_matches_sync(devices):
+    """rt_render_async (two slots, copy stream, strided band readback) gives
+    rt_render's frames, in order, with frames in flight and a new camera per frame."""
+    if not has_gpu():
+        pytest.skip("no GPU")
+    import rtamd
+    from rtamd import configs
+    from rtamd.engine import PinnedFrame
+    cfg = configs.config2()
+    built = cfg.build()
+    w, h, b = 333, 201, 3            # 201 rows: a partial last 16-row band
+    r = rtamd.Renderer(devices)
+    frames = [PinnedFrame(h, w) for _ in range(2)]
+    try:
+        r.upload_scene(built)
+        cams = [rtamd.Camera((-25.0 + 7 * k, 30.0, 140.0 - 9 * k), (0.0, 0.0, 0.0), (0.0, 1.0, 0.0), 20.0, w / h)
+                for k in range(5)]
+        refs = [r.render(c, w, h, b)[0] for c in cams]
+        pending = []
+        for k, c in enumerate(cams):
+            pending.append((r.render_async(c, w, h, b, frames[k % 2]), k))
+            if len(pending) == 2:
+                t, j = pending.pop(0)
+                r.wait(t)
+                assert np.array_equal(frames[j % 2].array, refs[j]), f"frame {j}"
+        t, j = pending.pop(0)
+        r.wait(t)
+        assert np.array_equal(frames[j % 2].array, refs[j])
+        with pytest.raises(rtamd.RtError, match="INVALID_ARG"):
+            r.wait(t + 1)
+    finally:
+        r.close()
+        for f in frames:
+            f.close()
+
+
 def test_hip_engine_publishes_frames():
     """HipEngine mirrors VulkanEngine: submit scene + camera, frames appear in the slot."""
     if not has_gpu():
@@ -259,6 +296,7 @@ def test_hip_engine_publishes_frames():
     built = cfg.build()
     slot = rtamd.AtomicReference()
     eng = rtamd.HipEngine(slot, width=320, height=180, max_bounces=3)
+    assert eng.pipelined
     eng.start()
     eng.submit_scene(built)
     eng.submit_sky_toggle(True)

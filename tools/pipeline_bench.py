@@ -1,0 +1,70 @@
+#!/usr/bin/env python3
+"""PCIe-inclusive frame rate: synchronous rt_render vs pipelined rt_render_async
+(two frames in flight, pinned host frames), whole frames of a config.
+
+Usage: python tools/pipeline_bench.py [--config 3] [--frames 60]
+Prints one JSON line per mode: frames/s, ms/frame, Mrays/s including the
+device->host copy of every frame.  (bench.py's `value` never includes PCIe.)
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(ROOT, "3d-ray-tracer-vulkan_amd"), ROOT]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", type=int, default=3)
+    ap.add_argument("--frames", type=int, default=60)
+    args = ap.parse_args()
+    import numpy as np
+    import torch  # noqa: F401  (load torch's HIP runtime first, as rtamd does)
+    import rtamd
+    from rtamd import configs
+    from rtamd.engine import PinnedFrame
+
+    cfg = configs.get(args.config)
+    built = cfg.build()
+    cam = cfg.camera()
+    W, H, B = cfg.width, cfg.height, cfg.max_bounces
+    r = rtamd.Renderer((0,))
+    r.upload_scene(built)
+    segs = r.render(cam, W, H, B, stats=True)[2]["segments"]
+    pageable = np.empty((H, W, 4), np.uint8)
+    frames = [PinnedFrame(H, W) for _ in range(2)]
+
+    def sync_run(n):
+        for _ in range(n):
+            r.render(cam, W, H, B)
+
+    def async_run(n):
+        pending = []
+        for k in range(n):
+            pending.append(r.render_async(cam, W, H, B, frames[k % 2]))
+            if len(pending) == 2:
+                r.wait(pending.pop(0))
+        for t in pending:
+            r.wait(t)
+
+    for name, fn in (("sync rt_render (pageable copy, fence per frame)", sync_run),
+                     ("rt_render_async, 2 in flight, pinned", async_run)):
+        fn(5)
+        t0 = time.perf_counter()
+        fn(args.frames)
+        dt = time.perf_counter() - t0
+        print(json.dumps({"mode": name, "config": cfg.name, "frames": args.frames,
+                          "fps": round(args.frames / dt, 1), "ms_per_frame": round(dt / args.frames * 1e3, 3),
+                          "mrays_s_incl_pcie": round(segs * args.frames / dt / 1e6, 1)}), flush=True)
+    assert np.array_equal(frames[(args.frames - 1) % 2].array, r.render(cam, W, H, B)[0])
+    del pageable
+    r.close()
+    for f in frames:
+        f.close()
+
+
+if __name__ == "__main__":
+    main()
