@@ -77,6 +77,13 @@ constexpr int kKernelSplit = 2;        // simple for the first seg_limit segment
                                        // surviving paths are spilled to a compacted queue and
                                        // finished by the persistent kernel
 
+// Non-reference extensions (option "extensions", off by
+// default, kernel 0 only).  The reference has none of them (SURVEY.md §0 facts
+// 3-4); oracle/rt_oracle.h ORC_EXT_* states the same semantics.
+constexpr int kExtSkyToggle = 1;    // a miss is black when sky_enabled == 0
+constexpr int kExtEmissive = 2;     // a type-3 hit ends the path with attenuation * albedo
+constexpr int kExtAccumulate = 4;   // seed += frame_count*W*H; output sqrt(mean of linear colour)
+
 // A path suspended between two segments (48 B): everything the bounce loop
 // (compute_dynamic_ray.comp:179-232) carries from one iteration to the next.
 struct PathState {
@@ -125,6 +132,10 @@ struct TraceArgs {
     unsigned* heavy_count;      // tiered: number of heavy paths (zeroed before the simple pass)
     int      coop_lanes;        // simple: finish a wave's walks cooperatively once at most
                                 //   this many lanes are still walking (0 = never)
+    int      ext;               // simple: non-reference extensions, kExt* bits (0 = the reference)
+    int      sky_enabled;       // CameraUBO.sky_enabled (@68), read only with kExtSkyToggle
+    int      frame_count;       // CameraUBO.frame_count (@64), read only with kExtAccumulate
+    float*   accum;             // kExtAccumulate: running linear-colour sums, 3 floats per pixel (tw*th)
     int      walk;              // simple: 0 = one node per step (nodes/leafs),
                                 //   1 = child pairs + per-lane stack of t_enter (pairs)
 };

@@ -237,6 +237,8 @@ struct PerDevice {
     uchar4*      d_ring[2] = {nullptr, nullptr};
     size_t       ring_cap = 0;     // pixels per slot
     hipEvent_t   traced[2] = {nullptr, nullptr}, copied[2] = {nullptr, nullptr};
+    float*       d_accum = nullptr;  // extension kExtAccumulate: running sums
+    size_t       accum_n = 0;        // floats
 };
 
 static constexpr unsigned kQueueSlots = 64;
@@ -252,6 +254,7 @@ struct rt_ctx {
     int  prio_after = 0;           // kernel 0: s_setprio(3) after this many node steps
     int  heavy_budget = 256;       // tiered: node visits per path in tier 1
     int  coop_lanes = 2;           // kernel 0: cooperative tail once <= this many lanes walk (0 = off)
+    int  ext = 0;                  // non-reference extensions (kExt* bits), off by default
     int  walk = 0;                 // kernel 0: 0 = node per step (fastest measured), 1 = child pairs + t_enter stack
     bool has_scene = false;
     int  n_nodes = 0, n_tris = 0, max_depth = 0;
@@ -267,14 +270,33 @@ static void free_scene(PerDevice& p) {
     p.scene = DevScene{};
 }
 
-static int set_schedule(const rt_ctx* ctx, PerDevice& p, TraceArgs& a) {
-    a.kernel = ctx->kernel;
+// The extensions exist in kernel 0 only; with any of them on, kernel 0 runs.
+static int effective_kernel(const rt_ctx* ctx) { return ctx->ext ? kKernelSimple : ctx->kernel; }
+
+static int set_schedule(const rt_ctx* ctx, PerDevice& p, TraceArgs& a, const rt_camera_ubo* cam) {
+    a.kernel = effective_kernel(ctx);
     a.shade_min = ctx->shade_min;
     a.wave_tile = ctx->wave_tile;
     a.prio_after = ctx->prio_after > 0 ? ctx->prio_after : -1;
     a.coop_lanes = ctx->coop_lanes;
     a.walk = ctx->walk;
-    a.seg_limit = ctx->kernel == kKernelSplit ? ctx->seg_limit : (1 << 30);
+    a.seg_limit = a.kernel == kKernelSplit ? ctx->seg_limit : (1 << 30);
+    a.ext = ctx->ext;
+    a.sky_enabled = cam->sky_enabled;
+    a.frame_count = cam->frame_count;
+    a.accum = nullptr;
+    if (a.ext & kExtAccumulate) {
+        const size_t need = (size_t)a.tw * (size_t)a.th * 3;
+        if (need != p.accum_n) {                 // a new frame partition starts from zero sums
+            if (p.d_accum) (void)hipFree(p.d_accum);
+            p.d_accum = nullptr;
+            p.accum_n = 0;
+            RT_HIP_CHECK(hipMalloc(&p.d_accum, need * sizeof(float)));
+            RT_HIP_CHECK(hipMemset(p.d_accum, 0, need * sizeof(float)));
+            p.accum_n = need;
+        }
+        a.accum = p.d_accum;
+    }
     a.resume = 0;
     const unsigned slot = p.queue_slot++ % kQueueSlots;
     p.last_slot = slot;
@@ -424,6 +446,7 @@ int rt_destroy(rt_ctx* ctx) {
         if (p.d_spill) (void)hipFree(p.d_spill);
         if (p.d_heavy) (void)hipFree(p.d_heavy);
         if (p.d_diag) (void)hipFree(p.d_diag);
+        if (p.d_accum) (void)hipFree(p.d_accum);
         if (p.d_rgba) (void)hipFree(p.d_rgba);
         if (p.d_rad) (void)hipFree(p.d_rad);
         if (p.ev0) (void)hipEventDestroy(p.ev0);
@@ -551,7 +574,7 @@ int rt_render_tile_device(rt_ctx* ctx, const rt_camera_ubo* cam, int width, int 
     a.out_rgba = static_cast<uchar4*>(d_out_rgba);
     a.out_rad = static_cast<float*>(d_out_radiance);
     a.counters = nullptr;
-    if (int rs = set_schedule(ctx, p, a)) return rs;
+    if (int rs = set_schedule(ctx, p, a, cam)) return rs;
     if (stats) {
         a.counters = p.d_counters;
         RT_HIP_CHECK(hipMemsetAsync(p.d_counters, 0, sizeof(Counters), s));
@@ -588,7 +611,7 @@ static int render_bands_on(const rt_ctx* ctx, PerDevice& p, const rt_camera_ubo*
     a.out_rgba = d_rgba;
     a.out_rad = d_rad;
     a.counters = count ? p.d_counters : nullptr;
-    if (int rs = set_schedule(ctx, p, a)) return rs;
+    if (int rs = set_schedule(ctx, p, a, cam)) return rs;
     if (count) RT_HIP_CHECK(hipMemsetAsync(p.d_counters, 0, sizeof(Counters), s));
     RT_HIP_CHECK(hipEventRecord(p.ev0, s));
     RT_HIP_CHECK(launch_trace(a, s));
@@ -600,8 +623,9 @@ static int collect_stats(const rt_ctx* ctx, PerDevice& p, uint64_t pixels, rt_st
     Counters c;
     RT_HIP_CHECK(hipMemcpy(&c, p.d_counters, sizeof c, hipMemcpyDeviceToHost));
     unsigned handoffs = 0;
-    if (ctx->kernel == kKernelSplit || ctx->kernel == kKernelTiered) {
-        const unsigned* src = p.d_queue + (ctx->kernel == kKernelSplit ? 1 : 2) * kQueueSlots + p.last_slot;
+    const int kernel = effective_kernel(ctx);
+    if (kernel == kKernelSplit || kernel == kKernelTiered) {
+        const unsigned* src = p.d_queue + (kernel == kKernelSplit ? 1 : 2) * kQueueSlots + p.last_slot;
         RT_HIP_CHECK(hipMemcpy(&handoffs, src, sizeof handoffs, hipMemcpyDeviceToHost));
     }
     float ms = 0.f;
@@ -807,6 +831,8 @@ int rt_set_option(rt_ctx* ctx, const char* name, int64_t value) {
         ctx->prio_after = (int)value;
     } else if (std::strcmp(name, "coop_lanes") == 0 && value >= 0 && value <= 64) {
         ctx->coop_lanes = (int)value;
+    } else if (std::strcmp(name, "extensions") == 0 && value >= 0 && value <= 7) {
+        ctx->ext = (int)value;
     } else if (std::strcmp(name, "walk") == 0 && (value == 0 || value == 1)) {
         ctx->walk = (int)value;
     } else if (std::strcmp(name, "diag") == 0 && (value == 0 || value == 1)) {
@@ -830,6 +856,7 @@ int rt_get_option(rt_ctx* ctx, const char* name, int64_t* value) {
     else if (std::strcmp(name, "heavy_budget") == 0) *value = ctx->heavy_budget;
     else if (std::strcmp(name, "coop_lanes") == 0) *value = ctx->coop_lanes;
     else if (std::strcmp(name, "walk") == 0) *value = ctx->walk;
+    else if (std::strcmp(name, "extensions") == 0) *value = ctx->ext;
     else if (std::strcmp(name, "blocks_per_cu") == 0)
         *value = ctx->blocks_per_cu > 0 ? ctx->blocks_per_cu : (ctx->dev.empty() ? 0 : ctx->dev[0].blocks_per_cu);
     else { set_error("rt_get_option: unknown option %s", name); return RT_ERR_INVALID_ARG; }

@@ -87,8 +87,14 @@ __device__ __forceinline__ int frame_row(const TraceArgs& a, int ly) {
 }
 
 // Seed, AA jitter and primary ray (:164-173).
+__device__ __forceinline__ void primary_ray_seeded(const TraceArgs& a, int x, int y, uint32_t& seed, V3& o, V3& d);
 __device__ __forceinline__ void primary_ray(const TraceArgs& a, int x, int y, uint32_t& seed, V3& o, V3& d) {
     seed = (uint32_t)(y * a.width + x);
+    primary_ray_seeded(a, x, y, seed, o, d);
+}
+
+// primary_ray with a caller-chosen initial seed (the accumulation extension).
+__device__ __forceinline__ void primary_ray_seeded(const TraceArgs& a, int x, int y, uint32_t& seed, V3& o, V3& d) {
     const float u = ((float)x + rnd(seed)) / (float)a.width;
     const float v = ((float)(a.height - 1 - y) + rnd(seed)) / (float)a.height;
     const V3 cam_o = {a.cam.ox, a.cam.oy, a.cam.oz};
@@ -340,6 +346,7 @@ constexpr int kFeatSpill = 1;     // split schedule: hand paths on after seg_lim
 constexpr int kFeatHeavy = 2;     // tiered schedule: hand walks on after heavy_budget visits
 constexpr int kFeatPrio = 4;      // raise wave priority after prio_after visits
 constexpr int kFeatCoopTail = 8;  // finish the last coop_lanes walks of a wave cooperatively
+constexpr int kFeatExt = 16;      // non-reference extensions (option "extensions", kExt*)
 
 constexpr int kStack = 8;                    // per-lane t_enter stack entries in LDS (walk 1)
 constexpr uint32_t kIdx = 0x7FFFFFFFu;
@@ -376,7 +383,16 @@ __global__ __launch_bounds__(256) void trace_simple(TraceArgs a) {
 
     uint32_t seed = 0;
     V3 o = {0.f, 0.f, 0.f}, d = {0.f, 0.f, 1.f};
-    if (pixel) primary_ray(a, a.x0 + lx, frame_row(a, ly), seed, o, d);
+    if (pixel) {
+        const int x = a.x0 + lx, y = frame_row(a, ly);
+        if ((FEAT & kFeatExt) && (a.ext & kExtAccumulate)) {
+            // extension: a new sample per frame; frame 0 is the reference's seed (:164)
+            seed = (uint32_t)(y * a.width + x) + (uint32_t)a.frame_count * (uint32_t)(a.width * a.height);
+            primary_ray_seeded(a, x, y, seed, o, d);
+        } else {
+            primary_ray(a, x, y, seed, o, d);
+        }
+    }
     V3 fin = {0.0f, 0.0f, 0.0f};
     V3 att = {1.0f, 1.0f, 1.0f};
     bool alive = pixel, handed_on = false;
@@ -597,7 +613,10 @@ __global__ __launch_bounds__(256) void trace_simple(TraceArgs a) {
                 const V3 hp = vadd(o, vscale(d, closest));                  // ray_at :77-79
                 const float4 M = a.scene.mats[hit];
                 V3 nd;
-                if (!scatter(M, d, nrm, seed, nd)) {
+                if ((FEAT & kFeatExt) && (a.ext & kExtEmissive) && M.w == 3.0f) {
+                    fin = vmul(att, V3{M.x, M.y, M.z});                   // extension: type 3 emits
+                    alive = false;
+                } else if (!scatter(M, d, nrm, seed, nd)) {
                     alive = false;                                        // attenuation = 0: black
                 } else {
                     att = vmul(att, V3{M.x, M.y, M.z});
@@ -609,10 +628,23 @@ __global__ __launch_bounds__(256) void trace_simple(TraceArgs a) {
                     }
                 }
             } else {
-                fin = vmul(att, sky_color(d));
+                if ((FEAT & kFeatExt) && (a.ext & kExtSkyToggle) && a.sky_enabled == 0)
+                    fin = {0.0f, 0.0f, 0.0f};                             // extension: sky off
+                else
+                    fin = vmul(att, sky_color(d));
                 alive = false;
             }
         }
+    }
+    if ((FEAT & kFeatExt) && (a.ext & kExtAccumulate) && pixel && !handed_on) {
+        // extension: running sum of the linear colour, shown as sqrt(mean)
+        float* acc = a.accum + 3 * ((size_t)ly * (size_t)a.tw + (size_t)lx);
+        const float nf = (float)(a.frame_count + 1);
+        const V3 sum = a.frame_count == 0 ? fin : V3{acc[0] + fin.x, acc[1] + fin.y, acc[2] + fin.z};
+        acc[0] = sum.x;
+        acc[1] = sum.y;
+        acc[2] = sum.z;
+        fin = {sum.x / nf, sum.y / nf, sum.z / nf};
     }
     if (pixel && !handed_on) write_pixel(a, lx, ly, fin);
     if (COUNT) flush_counters(a.counters, c_seg, c_node, c_tri, c_mat);
@@ -873,7 +905,7 @@ hipError_t launch_trace(const TraceArgs& a, hipStream_t stream) {
         const dim3 grid((a.tw + 4 * tw_w - 1) / (4 * tw_w), (a.th + th_w - 1) / th_w);
         const int feat = (a.seg_limit < (1 << 30) ? kFeatSpill : 0) |
                          (a.heavy_budget < (1 << 30) ? kFeatHeavy : 0) | (a.prio_after > 0 ? kFeatPrio : 0) |
-                         (a.coop_lanes > 0 ? kFeatCoopTail : 0);
+                         (a.coop_lanes > 0 ? kFeatCoopTail : 0) | (a.ext != 0 ? kFeatExt : 0);
 #define RT_SIMPLE(F, W)                                                                                        \
         if (a.diag) hipLaunchKernelGGL((trace_simple<false, true, F, W>), grid, block, 0, stream, a);           \
         else if (a.counters) hipLaunchKernelGGL((trace_simple<true, false, F, W>), grid, block, 0, stream, a); \
@@ -882,7 +914,8 @@ hipError_t launch_trace(const TraceArgs& a, hipStream_t stream) {
             switch (feat) {
                 case 0: RT_SIMPLE(0, 0) break;
                 case kFeatCoopTail: RT_SIMPLE(kFeatCoopTail, 0) break;
-                default: RT_SIMPLE(kFeatSpill | kFeatHeavy | kFeatPrio | kFeatCoopTail, 0) break;
+                case kFeatCoopTail | kFeatExt: RT_SIMPLE(kFeatCoopTail | kFeatExt, 0) break;
+                default: RT_SIMPLE(kFeatSpill | kFeatHeavy | kFeatPrio | kFeatCoopTail | kFeatExt, 0) break;
             }
         } else {
             switch (feat) {
@@ -890,7 +923,7 @@ hipError_t launch_trace(const TraceArgs& a, hipStream_t stream) {
                 case kFeatCoopTail: RT_SIMPLE(kFeatCoopTail, 1) break;
                 case kFeatSpill: RT_SIMPLE(kFeatSpill, 1) break;
                 case kFeatHeavy: RT_SIMPLE(kFeatHeavy, 1) break;
-                default: RT_SIMPLE(kFeatSpill | kFeatHeavy | kFeatPrio | kFeatCoopTail, 1) break;
+                default: RT_SIMPLE(kFeatSpill | kFeatHeavy | kFeatPrio | kFeatCoopTail | kFeatExt, 1) break;
             }
         }
 #undef RT_SIMPLE

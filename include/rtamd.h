@@ -167,6 +167,17 @@ int rt_render_wait(rt_ctx* ctx, uint64_t ticket);
  *                   time (0..64, default 2; 0 = off)
  *   "wave_tile"     kernel 0: pixels per wave (8<<s) x (8>>s), s = 0..3
  *                   (default 2: 32x2)
+ *   "extensions"    NON-REFERENCE features, bits (default 0 = the reference's
+ *                   shader exactly).  Any bit set
+ *                   runs kernel 0:
+ *                   1 = honour sky_enabled (@68): a miss is black when it is 0
+ *                   2 = a type-3 ("Emissive (Light)") hit ends the path with
+ *                       attenuation * albedo (the reference renders it black)
+ *                   4 = progressive accumulation: seed += frame_count*W*H
+ *                       (frame 0 is the reference's frame), a per-device buffer
+ *                       keeps the running sum of the linear colour (frame_count
+ *                       0 overwrites it; a new frame partition starts from
+ *                       zero) and the output is sqrt(sum / (frame_count+1))
  *   "prio_after"    kernel 0: raise a wave's priority after this many walk
  *                   steps (0 = never, default)
  *   "seg_limit"     split: segments traced in the first pass (default 2)

@@ -44,6 +44,7 @@ def lib() -> C.CDLL:
         L.orc_render.argtypes = [C.c_void_p, C.c_size_t, C.c_void_p, C.c_size_t, C.c_void_p, C.c_size_t,
                                  C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
                                  C.c_int, C.c_void_p, C.c_void_p, C.POINTER(Counts), C.c_int]
+        L.orc_render_ext.argtypes = L.orc_render.argtypes + [C.c_int, C.c_void_p]
         _lib = L
     return _lib
 
@@ -53,9 +54,15 @@ def _buf(x):
     return a, a.ctypes.data, a.nbytes
 
 
+EXT_SKY_TOGGLE, EXT_EMISSIVE, EXT_ACCUMULATE = 1, 2, 4   # rt_oracle.h ORC_EXT_*
+
+
 def render(vertices, materials, nodes, camera_ubo: bytes, width: int, height: int, max_bounces: int,
-           tile=None, row_step: int = 1, radiance: bool = True, n_threads: int = 0):
-    """Returns (rgba[rows, w, 4], radiance[rows, w, 3] or None, counts dict)."""
+           tile=None, row_step: int = 1, radiance: bool = True, n_threads: int = 0, ext: int = 0,
+           accum: "np.ndarray | None" = None):
+    """Returns (rgba[rows, w, 4], radiance[rows, w, 3] or None, counts dict).
+    ext: ORC_EXT_* bits (non-reference extensions); accum: float32[rows, w, 3],
+    updated in place, required with EXT_ACCUMULATE."""
     x0, y0, tw, th = tile if tile is not None else (0, 0, width, height)
     rows = (th + row_step - 1) // row_step
     v, vp, vn = _buf(vertices)
@@ -65,9 +72,12 @@ def render(vertices, materials, nodes, camera_ubo: bytes, width: int, height: in
     rgba = np.empty((rows, tw, 4), dtype=np.uint8)
     rad = np.empty((rows, tw, 3), dtype=np.float32) if radiance else None
     c = Counts()
-    rc = lib().orc_render(vp, vn, mp, mn, bp, bn, cam.ctypes.data, width, height, max_bounces,
-                          x0, y0, tw, th, row_step, rgba.ctypes.data,
-                          rad.ctypes.data if rad is not None else None, C.byref(c), n_threads)
+    if accum is not None:
+        assert accum.dtype == np.float32 and accum.shape == (rows, tw, 3) and accum.flags.c_contiguous
+    rc = lib().orc_render_ext(vp, vn, mp, mn, bp, bn, cam.ctypes.data, width, height, max_bounces,
+                              x0, y0, tw, th, row_step, rgba.ctypes.data,
+                              rad.ctypes.data if rad is not None else None, C.byref(c), n_threads,
+                              ext, accum.ctypes.data if accum is not None else None)
     if rc != 0:
         raise RuntimeError(f"orc_render failed ({rc})")
     return rgba, rad, c.as_dict()

@@ -202,8 +202,11 @@ static unsigned char unorm8(float c) {
 /* One invocation of main() (:158-237).  Returns 0, or -1 on stack overflow or
  * an out-of-range index (where the reference reads out of bounds). */
 static int shade_pixel(const scene* s, const orc_camera* cam, int W, int H, int max_bounces,
-                       int px, int py, float out_rgb[3], orc_counts* cnt, uint32_t* prof) {
+                       int px, int py, float out_rgb[3], orc_counts* cnt, uint32_t* prof, int ext,
+                       float lin[3]) {
     uint32_t seed = (uint32_t)(py * W + px);                                   /* :164 */
+    if (ext & ORC_EXT_ACCUMULATE)              /* extension: a new sample per frame (frame 0 = :164) */
+        seed += (uint32_t)cam->frame_count * (uint32_t)(W * H);
     float u = ((float)px + orc_random_float(&seed)) / (float)W;                /* :167 */
     float v = ((float)(H - 1 - py) + orc_random_float(&seed)) / (float)H;      /* :168 */
     vec3 o = v3(cam->origin[0], cam->origin[1], cam->origin[2]);
@@ -261,6 +264,12 @@ static int shade_pixel(const scene* s, const orc_camera* cam, int W, int H, int 
             vec3 mat_att;
             ray scattered;
             cnt->mat_reads++;
+            if ((ext & ORC_EXT_EMISSIVE) && f32_at(s->mats, (size_t)hit_triangle_index * 16 + 12) == 3.0f) {
+                /* extension: a type-3 material emits its albedo (the reference renders it black) */
+                const unsigned char* m = s->mats + (size_t)hit_triangle_index * 16;
+                final_color = mul3(attenuation, v3(f32_at(m, 0), f32_at(m, 4), f32_at(m, 8)));
+                break;
+            }
             if (scatter(s, &seed, r, hit_triangle_index, hit_pos, hit_normal, &mat_att, &scattered)) {
                 attenuation = mul3(attenuation, mat_att);
                 r = scattered;
@@ -269,10 +278,18 @@ static int shade_pixel(const scene* s, const orc_camera* cam, int W, int H, int 
                 break;
             }
         } else {
-            final_color = mul3(attenuation, sky_color(r));
+            if ((ext & ORC_EXT_SKY_TOGGLE) && cam->sky_enabled == 0)
+                final_color = v3(0.0f, 0.0f, 0.0f);   /* extension: sky off, a miss is black */
+            else
+                final_color = mul3(attenuation, sky_color(r));
             break;
         }
         if (b == max_bounces - 1) final_color = v3(0.0f, 0.0f, 0.0f);         /* :229-231 */
+    }
+    if (lin) {                                 /* extension: accumulation wants the linear colour */
+        lin[0] = final_color.x;
+        lin[1] = final_color.y;
+        lin[2] = final_color.z;
     }
     out_rgb[0] = sqrtf(final_color.x);                                         /* :235 */
     out_rgb[1] = sqrtf(final_color.y);
@@ -291,6 +308,14 @@ int orc_render(const void* vertices, size_t vertex_bytes,
                               out_radiance, counts, n_threads, NULL);
 }
 
+static int render_core(const void* vertices, size_t vertex_bytes,
+               const void* materials, size_t material_bytes,
+               const void* bvh_nodes, size_t bvh_bytes,
+               const orc_camera* cam, int width, int height, int max_bounces,
+               int x0, int y0, int tile_w, int tile_h, int row_step,
+               uint8_t* out_rgba, float* out_radiance, orc_counts* counts, int n_threads,
+               uint32_t* profile, int ext, float* accum);
+
 int orc_render_profile(const void* vertices, size_t vertex_bytes,
                const void* materials, size_t material_bytes,
                const void* bvh_nodes, size_t bvh_bytes,
@@ -298,6 +323,31 @@ int orc_render_profile(const void* vertices, size_t vertex_bytes,
                int x0, int y0, int tile_w, int tile_h, int row_step,
                uint8_t* out_rgba, float* out_radiance, orc_counts* counts, int n_threads,
                uint32_t* profile) {
+    return render_core(vertices, vertex_bytes, materials, material_bytes, bvh_nodes, bvh_bytes, cam, width,
+                       height, max_bounces, x0, y0, tile_w, tile_h, row_step, out_rgba, out_radiance, counts,
+                       n_threads, profile, 0, NULL);
+}
+
+int orc_render_ext(const void* vertices, size_t vertex_bytes,
+                   const void* materials, size_t material_bytes,
+                   const void* bvh_nodes, size_t bvh_bytes,
+                   const orc_camera* cam, int width, int height, int max_bounces,
+                   int x0, int y0, int tile_w, int tile_h, int row_step,
+                   uint8_t* out_rgba, float* out_radiance, orc_counts* counts, int n_threads,
+                   int ext, float* accum) {
+    if ((ext & ORC_EXT_ACCUMULATE) && !accum) return -2;
+    return render_core(vertices, vertex_bytes, materials, material_bytes, bvh_nodes, bvh_bytes, cam, width,
+                       height, max_bounces, x0, y0, tile_w, tile_h, row_step, out_rgba, out_radiance, counts,
+                       n_threads, NULL, ext, accum);
+}
+
+static int render_core(const void* vertices, size_t vertex_bytes,
+               const void* materials, size_t material_bytes,
+               const void* bvh_nodes, size_t bvh_bytes,
+               const orc_camera* cam, int width, int height, int max_bounces,
+               int x0, int y0, int tile_w, int tile_h, int row_step,
+               uint8_t* out_rgba, float* out_radiance, orc_counts* counts, int n_threads,
+               uint32_t* profile, int ext, float* accum) {
     if (!cam || width < 1 || height < 1 || max_bounces < 1 || tile_w < 1 || tile_h < 1 ||
         x0 < 0 || y0 < 0 || x0 + tile_w > width || y0 + tile_h > height || row_step < 1)
         return -2;
@@ -322,11 +372,22 @@ int orc_render_profile(const void* vertices, size_t vertex_bytes,
             float rgb[3];
             uint32_t* prof = profile ? profile + ((size_t)rr * (size_t)tile_w + (size_t)lx) * (size_t)max_bounces : NULL;
             if (prof) memset(prof, 0, sizeof(uint32_t) * (size_t)max_bounces);
-            if (shade_pixel(&s, cam, width, height, max_bounces, x0 + lx, y0 + ly, rgb, &c, prof)) {
+            float lin[3];
+            if (shade_pixel(&s, cam, width, height, max_bounces, x0 + lx, y0 + ly, rgb, &c, prof, ext, lin)) {
                 err |= 1;
                 rgb[0] = rgb[1] = rgb[2] = 0.0f;
+                lin[0] = lin[1] = lin[2] = 0.0f;
             }
             const size_t p = (size_t)rr * (size_t)tile_w + (size_t)lx;
+            if (ext & ORC_EXT_ACCUMULATE) {
+                /* extension: running sum of the linear colour; shown as sqrt(mean) */
+                float* acc = accum + 3 * p;
+                const float n = (float)(cam->frame_count + 1);
+                for (int k = 0; k < 3; ++k) {
+                    acc[k] = cam->frame_count == 0 ? lin[k] : acc[k] + lin[k];
+                    rgb[k] = sqrtf(acc[k] / n);
+                }
+            }
             if (out_rgba) {
                 out_rgba[4 * p + 0] = unorm8(rgb[0]);
                 out_rgba[4 * p + 1] = unorm8(rgb[1]);
@@ -409,7 +470,7 @@ int orc_trace_pixel(const void* vertices, size_t vertex_bytes, const void* mater
     g_trace_n = 0;
     orc_counts c = {0, 0, 0, 0, 0};
     float rgb[3];
-    int rc = shade_pixel(&s, cam, width, height, max_bounces, px, py, rgb, &c, NULL);
+    int rc = shade_pixel(&s, cam, width, height, max_bounces, px, py, rgb, &c, NULL, 0, NULL);
     g_trace = NULL;
     return rc ? -1 : g_trace_n;
 }

@@ -45,4 +45,23 @@ int orc_render_profile(const void* vertices, size_t vertex_bytes,
                        int x0, int y0, int tile_w, int tile_h, int row_step,
                        uint8_t* out_rgba, float* out_radiance, orc_counts* counts, int n_threads,
                        uint32_t* profile);
+/* Non-reference extensions, the semantics the GPU path's
+ * option "extensions" implements; bit-exact against it, unpinned against any
+ * reference (the reference has none of them):
+ *   ORC_EXT_SKY_TOGGLE  a miss is black when cam->sky_enabled == 0
+ *   ORC_EXT_EMISSIVE    a type-3 hit ends the path with attenuation * albedo
+ *   ORC_EXT_ACCUMULATE  seed += frame_count * W * H; accum (3 floats per output
+ *                       pixel, packed like out_rgba) holds the running sum of the
+ *                       linear colour (frame_count 0 overwrites it); the output is
+ *                       sqrt(sum / (frame_count + 1)) */
+#define ORC_EXT_SKY_TOGGLE 1
+#define ORC_EXT_EMISSIVE   2
+#define ORC_EXT_ACCUMULATE 4
+int orc_render_ext(const void* vertices, size_t vertex_bytes,
+                   const void* materials, size_t material_bytes,
+                   const void* bvh_nodes, size_t bvh_bytes,
+                   const orc_camera* cam, int width, int height, int max_bounces,
+                   int x0, int y0, int tile_w, int tile_h, int row_step,
+                   uint8_t* out_rgba, float* out_radiance, orc_counts* counts, int n_threads,
+                   int ext, float* accum);
 #endif

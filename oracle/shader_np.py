@@ -67,8 +67,10 @@ def random_in_unit_sphere(seed: np.ndarray):                  # :63-70
 
 
 def render(vertices, materials, nodes, camera_ubo: bytes, width: int, height: int, max_bounces: int,
-           rows=None):
-    """Returns (rgba[len(rows), W, 4], radiance[len(rows), W, 3], counts dict)."""
+           rows=None, ext: int = 0, accum=None):
+    """Returns (rgba[len(rows), W, 4], radiance[len(rows), W, 3], counts dict).
+    ext / accum: the non-reference extensions of oracle/rt_oracle.h (ORC_EXT_*),
+    restated independently; accum float32[len(rows), W, 3] is updated in place."""
     V = np.frombuffer(bytes(vertices), np.float32).reshape(-1, 3, 4)[:, :, :3]
     M = np.frombuffer(bytes(materials), np.float32).reshape(-1, 4)
     nb = np.frombuffer(bytes(nodes), np.uint8)
@@ -78,6 +80,7 @@ def render(vertices, materials, nodes, camera_ubo: bytes, width: int, height: in
     DATA = nb[:, 32:36].copy().view(np.int32).reshape(-1)
     COUNT = nb[:, 36:40].copy().view(np.int32).reshape(-1)
     cam = np.frombuffer(bytes(camera_ubo), np.float32)[:16].reshape(4, 4)[:, :3]
+    frame_count, sky_enabled = (int(x) for x in np.frombuffer(bytes(camera_ubo), np.int32)[16:18])
     org, llc, hor, ver = cam[0], cam[1], cam[2], cam[3]
 
     rows = np.arange(height) if rows is None else np.asarray(rows)
@@ -85,6 +88,9 @@ def render(vertices, materials, nodes, camera_ubo: bytes, width: int, height: in
     ys = ys.reshape(-1).astype(np.int64); xs = xs.reshape(-1).astype(np.int64)
     R = xs.size
     seed = (ys * width + xs).astype(np.uint32)                               # :164
+    if ext & 4:                                           # extension: a new sample per frame
+        seed = ((seed.astype(np.uint64) + np.uint64(frame_count % 2**32) * np.uint64(width * height))
+                % np.uint64(2**32)).astype(np.uint32)
     seed, ru = random_float(seed)
     seed, rv = random_float(seed)
     u = (xs.astype(F) + ru) / F(width)                                        # :167
@@ -123,7 +129,8 @@ def render(vertices, materials, nodes, camera_ubo: bytes, width: int, height: in
             sp[w] -= 1
             node = stack[w, sp[w]]
             counts["node_visits"] += w.size
-            ix = F(1.0) / rdx[w]; iy = F(1.0) / rdy[w]; iz = F(1.0) / rdz[w]    # hit_aabb :88-103
+            with np.errstate(divide="ignore"):                                 # 1/0 = inf, as on the GPU
+                ix = F(1.0) / rdx[w]; iy = F(1.0) / rdy[w]; iz = F(1.0) / rdz[w]    # hit_aabb :88-103
             t0x = (BMIN[node, 0] - rox[w]) * ix; t1x = (BMAX[node, 0] - rox[w]) * ix
             t0y = (BMIN[node, 1] - roy[w]) * iy; t1y = (BMAX[node, 1] - roy[w]) * iy
             t0z = (BMIN[node, 2] - roz[w]) * iz; t1z = (BMAX[node, 2] - roz[w]) * iz
@@ -177,6 +184,8 @@ def render(vertices, materials, nodes, camera_ubo: bytes, width: int, height: in
             omt = F(1.0) - t
             sky = np.stack([omt * F(1.0) + t * F(0.5), omt * F(1.0) + t * F(0.7), omt * F(1.0) + t * F(1.0)], 1)
             fin[ms] = att[ms] * sky
+            if (ext & 1) and sky_enabled == 0:            # extension: sky off, a miss is black
+                fin[ms] = F(0.0)
             alive[ms] = False
         hs = np.nonzero(gh)[0]
         if hs.size:
@@ -212,6 +221,9 @@ def render(vertices, materials, nodes, camera_ubo: bytes, width: int, height: in
                 qx, qy, qz = _normalize(rx + px * fuzz, ry + py * fuzz, rz + pz * fuzz)
                 ndx[met], ndy[met], ndz[met] = qx, qy, qz
                 scattered[met] = _dot(qx, qy, qz, hnx[met], hny[met], hnz[met]) > F(0.0)
+            if ext & 2:                                   # extension: type 3 emits its albedo
+                em = typ == F(3.0)
+                fin[ga[em]] = att[ga[em]] * mat[em, :3]
             ok = scattered
             att[ga[ok]] = att[ga[ok]] * mat[ok, :3]
             ox[ga[ok]] = hpx[ok]; oy[ga[ok]] = hpy[ok]; oz[ga[ok]] = hpz[ok]
@@ -223,6 +235,10 @@ def render(vertices, materials, nodes, camera_ubo: bytes, width: int, height: in
                 fin[ga[ok]] = F(0.0)
                 alive[ga[ok]] = False
 
+    if ext & 4:                                           # extension: running sum, sqrt(mean)
+        acc = accum.reshape(-1, 3)
+        acc[:] = fin if frame_count == 0 else acc + fin
+        fin = acc / F(frame_count + 1)
     rad = np.sqrt(fin).astype(F)                                               # :235
     q = np.where(rad > F(0.0), np.where(rad < F(1.0), np.rint(rad * F(255.0)), F(255.0)), F(0.0)).astype(np.uint8)
     rgba = np.concatenate([q, np.full((R, 1), 255, np.uint8)], 1)

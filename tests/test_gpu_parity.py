@@ -319,7 +319,8 @@ def test_golden_frames_on_gpu(renderer):
     import json
     import os
     from rtamd import configs
-    g_all = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "golden.json")))["frames"]
+    with open(os.path.join(os.path.dirname(__file__), "golden", "golden.json")) as f:
+        g_all = json.load(f)["frames"]
     for name, g in g_all.items():
         renderer.upload_scene(configs.get(g["config"]).build())
         cam = configs.Camera.default(g["width"], g["height"])
@@ -349,3 +350,50 @@ def test_unbalanced_bvh(renderer, shape, n, walk):
             assert st["tri_tests"] > 0
     finally:
         renderer.set_option("walk", 0)
+
+
+@pytest.mark.parametrize("ext,sky", [(1, 0), (2, 1), (3, 0)])
+def test_extensions_bit_exact(renderer, ext, sky):
+    """Option "extensions" (non-reference, off by default) matches the oracle's
+    ORC_EXT_* semantics bit for bit; the default stays the reference."""
+    from test_oracle_kat import _ext_scene
+    from rtamd import configs
+    built = _ext_scene()
+    renderer.upload_scene(built)
+    w, h, b = 200, 120, 5
+    cam = configs.Camera.default(w, h)
+    cam.ubo.sky_enabled = sky
+    try:
+        renderer.set_option("kernel", 2)            # extensions force kernel 0
+        renderer.set_option("extensions", ext)
+        rgba, rad, st = renderer.render(cam, w, h, b, radiance=True, stats=True)
+        _assert_same(rgba, rad, st, *_oracle(built, cam.ubo_bytes(), w, h, b, ext=ext))
+    finally:
+        renderer.set_option("extensions", 0)
+        renderer.set_option("kernel", 0)
+    rgba, rad, st = renderer.render(cam, w, h, b, radiance=True, stats=True)
+    _assert_same(rgba, rad, st, *_oracle(built, cam.ubo_bytes(), w, h, b))
+
+
+@pytest.mark.parametrize("devices", [(0,), (0, 0)])
+def test_accumulation_bit_exact(devices):
+    if not has_gpu():
+        pytest.skip("no GPU")
+    import rtamd
+    from test_oracle_kat import _ext_scene
+    from rtamd import configs
+    built = _ext_scene()
+    r = rtamd.Renderer(devices)
+    try:
+        r.upload_scene(built)
+        r.set_option("extensions", 7)
+        w, h, b = 150, 97, 4
+        cam = configs.Camera.default(w, h)
+        acc = np.zeros((h, w, 3), np.float32)
+        for f in range(4):
+            cam.ubo.frame_count = f
+            rgba, rad, _ = r.render(cam, w, h, b, radiance=True)
+            ref = _oracle(built, cam.ubo_bytes(), w, h, b, ext=7, accum=acc)
+            _assert_same(rgba, rad, None, *ref)
+    finally:
+        r.close()

@@ -9,9 +9,15 @@ import warnings
 import numpy as np
 import pytest
 
+
+def _load_json(path):
+    with open(path) as f:
+        return json.load(f)
+
+
 HERE = os.path.dirname(os.path.abspath(__file__))
-GOLDEN = json.load(open(os.path.join(HERE, "golden", "golden.json")))
-SPIRV = json.load(open(os.path.join(HERE, "golden", "spirv_facts.json")))
+GOLDEN = _load_json(os.path.join(HERE, "golden", "golden.json"))
+SPIRV = _load_json(os.path.join(HERE, "golden", "spirv_facts.json"))
 M32 = 0xFFFFFFFF
 
 
@@ -191,3 +197,62 @@ def test_row_subsets_and_tiles_compose():
     assert np.array_equal(sub, full[3::5])
     t, _, _ = oracle_lib.render(*args, tile=(17, 9, 50, 40))
     assert np.array_equal(t, full[9:49, 17:67])
+
+
+def _ext_scene():
+    """Cube + plane with the cube emissive (type 3, colour 4,4,4), as the UI's
+    "Emissive (Light)" material (VulkanApp.java:487)."""
+    from rtamd import build_buffers, configs, triangles_of
+    verts, mats = triangles_of(configs.config2().scene)
+    mats = mats.copy()
+    cube = mats[:, 0] == np.float32(0.6)
+    mats[cube] = (4.0, 4.0, 4.0, 3.0)
+    return build_buffers(verts, mats)
+
+
+@pytest.mark.parametrize("ext,sky", [(1, 0), (1, 1), (2, 1), (3, 0)])
+def test_extensions_c_vs_numpy(ext, sky):
+    """The non-reference extensions (ORC_EXT_*) agree bit for bit between the C
+    oracle and the independent numpy restatement (parity vs the reference is
+    not defined: the reference has none of them)."""
+    from oracle import oracle_lib, shader_np
+    from rtamd import configs
+    built = _ext_scene()
+    w, h = 96, 54
+    cam = configs.Camera.default(w, h)
+    cam.ubo.sky_enabled = sky
+    args = (built.model_vertex_data, built.model_material_data, built.flat_bvh_data, cam.ubo_bytes(), w, h, 5)
+    rgba_c, rad_c, cnt_c = oracle_lib.render(*args, ext=ext)
+    rgba_n, rad_n, cnt_n = shader_np.render(*args, ext=ext)
+    assert np.array_equal(rgba_c, rgba_n)
+    assert np.array_equal(rad_c.view(np.uint32), rad_n.view(np.uint32))
+    assert cnt_c == cnt_n
+    base = oracle_lib.render(*args)[0]
+    if ext & 2:
+        assert (rgba_c != base).any()           # the emitter lights the frame
+    if ext == 1 and sky == 1:
+        assert np.array_equal(rgba_c, base)     # sky on: the reference frame
+
+
+def test_accumulation_c_vs_numpy():
+    from oracle import oracle_lib, shader_np
+    from rtamd import configs
+    built = _ext_scene()
+    w, h = 64, 40
+    cam = configs.Camera.default(w, h)
+    acc_c = np.zeros((h, w, 3), np.float32)
+    acc_n = np.zeros((h, w, 3), np.float32)
+    frames = []
+    for f in range(3):
+        cam.ubo.frame_count = f
+        args = (built.model_vertex_data, built.model_material_data, built.flat_bvh_data, cam.ubo_bytes(), w, h, 4)
+        rgba_c, rad_c, _ = oracle_lib.render(*args, ext=4, accum=acc_c)
+        rgba_n, rad_n, _ = shader_np.render(*args, ext=4, accum=acc_n)
+        assert np.array_equal(rad_c.view(np.uint32), rad_n.view(np.uint32)), f
+        assert np.array_equal(acc_c.view(np.uint32), acc_n.view(np.uint32)), f
+        frames.append(rgba_c)
+    cam.ubo.frame_count = 0
+    ref = oracle_lib.render(built.model_vertex_data, built.model_material_data, built.flat_bvh_data,
+                            cam.ubo_bytes(), w, h, 4)[0]
+    assert np.array_equal(frames[0], ref)       # frame 0 is the reference's frame
+    assert (frames[1] != frames[0]).any()

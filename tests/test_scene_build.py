@@ -9,8 +9,14 @@ import pytest
 
 from conftest import reference_path
 
+
+def _load_json(path):
+    with open(path) as f:
+        return json.load(f)
+
+
 HERE = os.path.dirname(os.path.abspath(__file__))
-GOLDEN = json.load(open(os.path.join(HERE, "golden", "golden.json")))
+GOLDEN = _load_json(os.path.join(HERE, "golden", "golden.json"))
 
 
 def _oracle_build(verts, mats, seed):
