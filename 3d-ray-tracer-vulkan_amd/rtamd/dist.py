@@ -56,6 +56,63 @@ def gather_frame(local, height: int, band_h: int, group=None):
     return out
 
 
+# --- frame batches (weak scaling) -------------------------------------------
+#
+# One frame tiled over N GPUs is bounded by its slowest wave (a few pixels'
+# paths walk ~1,600 BVH nodes one dependent load after another),
+# so it cannot scale strongly.  A batch of N frames of the render loop is tiled
+# over the N GPUs instead: in frame f, rank r traces the bands b with
+# b % N == (r + f) % N.  Over the batch every rank traces each band exactly
+# once, so per-GPU work is one frame whatever N is; every frame is still split
+# across all ranks and gathered to rank 0 over RCCL.
+
+
+def batch_band_offset(frame: int, world: int, rank: int) -> int:
+    """Band offset (rt_render_bands_device band_off) of rank in batch frame `frame`."""
+    return (rank + frame) % world
+
+
+class BatchPlan:
+    """Row bookkeeping of an n_frames batch over world ranks (band_h-row bands)."""
+
+    def __init__(self, height: int, band_h: int, world: int, n_frames: int):
+        self.height, self.band_h, self.world, self.n_frames = height, band_h, world, n_frames
+        self.rows = [[band_rows(height, band_h, world, batch_band_offset(f, world, r)) for f in range(n_frames)]
+                     for r in range(world)]
+        self.max_rows = max(len(x) for per_rank in self.rows for x in per_rank)
+        # source row (in the gathered [world, n_frames, max_rows] stack) of every
+        # row of every frame: one index_select assembles the whole batch
+        src = np.empty(n_frames * height, np.int64)
+        for r in range(world):
+            for f in range(n_frames):
+                rows = self.rows[r][f]
+                src[f * height + rows] = (r * n_frames + f) * self.max_rows + np.arange(len(rows))
+        self.src = src
+
+    def local_rows(self, rank: int, frame: int) -> int:
+        return len(self.rows[rank][frame])
+
+
+def gather_batch(local, plan: BatchPlan, group=None, src_index=None):
+    """local: this rank's [n_frames, max_rows, W, C] packed bands (torch).
+    Returns the [n_frames, height, W, C] frames on rank 0, None elsewhere."""
+    import torch
+    import torch.distributed as dist
+    rank = dist.get_rank(group)
+    stack = gl = None
+    if rank == 0:                  # gather straight into one [world, ...] tensor (views, no extra copy)
+        stack = torch.empty((plan.world,) + tuple(local.shape), dtype=local.dtype, device=local.device)
+        gl = list(stack.unbind(0))
+    dist.gather(local, gl, dst=0, group=group)
+    if rank != 0:
+        return None
+    stack = stack.reshape(plan.world * plan.n_frames * plan.max_rows, -1)
+    if src_index is None:
+        src_index = torch.as_tensor(plan.src, device=local.device)
+    out = torch.index_select(stack, 0, src_index)
+    return out.reshape((plan.n_frames, plan.height) + tuple(local.shape[2:]))
+
+
 class DistRenderer:
     """Renders frames over all ranks: each rank traces its bands on its GPU
     with rt_render_bands_device, then gather_frame assembles rank 0's copy."""

@@ -3,13 +3,18 @@
 
 Workload (N = 1): BASELINE config 3 — the 50k-triangle synthetic scene at
 1920x1080, 4 bounces, default camera.  One step = one whole
-frame traced on the GPU(s): every pixel's full path, RGBA8 written to HBM.
-With N > 1 ranks (one process per GPU, torch.distributed over RCCL), the
-same frame is split into interleaved 16-row bands, rank r tracing bands
-r, r+N, ..., and the RGBA8 bands are gathered to rank 0 over xGMI
-(dist.gather) inside the timed step: strong scaling of one frame.
+frame traced on the GPU: every pixel's full path, RGBA8 written to HBM.
+With N > 1 ranks (one process per GPU, torch.distributed over RCCL; default
+--partition frames) a step is N frames of the render loop, each frame tiled
+over all ranks in rotating 16-row bands (rank r traces the bands b with
+b mod N = (r + f) mod N of frame f), so every rank traces one frame's worth of
+pixels per step (weak scaling); the packed bands are gathered to rank 0 over
+xGMI (dist.gather) and assembled there inside the timed step, and rank 0
+checks the assembled frames against a one-GPU frame afterwards
+(config.frames_verified).  --partition bands: one frame per step tiled over
+the ranks (strong scaling).
 
-value = segments of the frame x steps / wall time of the timed steps (max over
+value = segments of a step x steps / wall time of the timed steps (max over
 ranks), in millions.  A segment is one executed bounce-loop iteration
 (compute_dynamic_ray.comp:179-232); its count per frame is deterministic and is
 taken from a counting pass outside the timed region.
@@ -48,6 +53,9 @@ def main() -> None:
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", type=int, default=3, help="BASELINE config index (3 = headline)")
     ap.add_argument("--band", type=int, default=16, help="band height for N > 1")
+    ap.add_argument("--partition", choices=("frames", "bands"), default="frames",
+                    help="N > 1: frames = N frames per step, bands rotated over ranks (weak); "
+                         "bands = one frame per step tiled over ranks (strong)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU baseline sample time")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "latest_pmc_traffic.json"),
@@ -65,10 +73,14 @@ def main() -> None:
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         log(f"note: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE")
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
+    # BENCH_SHARE_GPU=1 (rehearsal only): ranks share the visible GPUs round-robin.
+    dev_index = local_rank % torch.cuda.device_count() if os.environ.get("BENCH_SHARE_GPU") else local_rank
+    torch.cuda.set_device(dev_index)
+    dev = torch.device("cuda", dev_index)
+    local_rank = dev_index
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        backend = os.environ.get("BENCH_DIST_BACKEND", "nccl")     # nccl = RCCL over xGMI
+        dist.init_process_group(backend, device_id=dev if backend == "nccl" else None)
 
     cfg = configs.get(args.config)
     t0 = time.time()
@@ -81,44 +93,68 @@ def main() -> None:
     renderer = rtamd.Renderer((local_rank,))
     renderer.upload_scene(built)
     L = rtamd.lib()
+    from rtamd.dist import BatchPlan, batch_band_offset, gather_batch, gather_frame
+
+    # Partition.  frames (default): a step renders N frames of the render loop
+    # (N = world size; the reference re-renders the current camera every loop
+    # iteration, VulkanEngine.java:240-276), each tiled over all ranks in
+    # rotating 16-row bands, so every rank traces one frame's worth of pixels per
+    # step (weak scaling).  bands: one frame per step tiled over the ranks
+    # (strong scaling; bounded by the frame's slowest wave).
+    # At N = 1 both are one whole frame per step.
+    frames_mode = args.partition == "frames"
+    F = world if frames_mode else 1
     band_h = H if world == 1 else args.band
-    rows = L.rt_band_rows(H, band_h, world, rank)
-    max_rows = max(L.rt_band_rows(H, band_h, world, r) for r in range(world))
-    d_rgba = torch.empty((max_rows, W, 4), dtype=torch.uint8, device=dev)
-    stream = torch.cuda.Stream(dev)           # a real stream: launches and events on the same queue
-    torch.cuda.set_stream(stream)
+    offsets = [batch_band_offset(f, world, rank) if frames_mode else rank for f in range(F)]
+    plan = BatchPlan(H, band_h, world, F) if frames_mode else None
+    rows_f = [L.rt_band_rows(H, band_h, world, off) for off in offsets]
+    max_rows = plan.max_rows if plan else max(L.rt_band_rows(H, band_h, world, r) for r in range(world))
+    d_rgba = torch.empty((F, max_rows, W, 4), dtype=torch.uint8, device=dev)
+    # One stream per frame in flight (launches and their events on the same
+    # queue); the gather runs on the main stream once every frame is traced.
+    streams = [torch.cuda.Stream(dev) for _ in range(min(F, 8))]
+    main_stream = streams[0]
+    torch.cuda.set_stream(main_stream)
+    src_index = torch.as_tensor(plan.src, device=dev) if (plan and world > 1) else None
 
     import ctypes as C
     from rtamd._lib import Stats, check
 
-    def trace(stats: bool = False):
-        s = Stats()
-        check(L.rt_render_bands_device(renderer._ctx, C.byref(cam.ubo), W, H, B, band_h, world, rank,
-                                       d_rgba.data_ptr(), None, stream.cuda_stream,
-                                       C.byref(s) if stats else None))
-        return s.as_dict() if stats else None
-
-    from rtamd.dist import gather_frame
-
-    def step(ev=None):
+    def trace(f, stats: bool = False, ev=None):
+        s = streams[f % len(streams)]
+        st = Stats()
         if ev is not None:
-            ev[0].record(stream)
-        trace()
+            ev[0].record(s)
+        check(L.rt_render_bands_device(renderer._ctx, C.byref(cam.ubo), W, H, B, band_h, world, offsets[f],
+                                       d_rgba[f].data_ptr(), None, s.cuda_stream,
+                                       C.byref(st) if stats else None))
         if ev is not None:
-            ev[1].record(stream)
+            ev[1].record(s)
+        return st.as_dict() if stats else None
+
+    def step(evs=None):
+        for s in streams[1:]:                      # the last step's gather has read d_rgba
+            s.wait_stream(main_stream)
+        for f in range(F):
+            trace(f, ev=evs[f] if evs is not None else None)
+        for s in streams[1:]:
+            main_stream.wait_stream(s)
         if world > 1:
-            gather_frame(d_rgba[:rows], H, band_h)     # RCCL gather + rank-0 assembly of the frame
+            if frames_mode:
+                return gather_batch(d_rgba, plan, src_index=src_index)
+            return gather_frame(d_rgba[0, :rows_f[0]], H, band_h)   # RCCL gather + rank-0 assembly
+        return None
 
-    # Counting pass (untimed): this rank's work, then the frame totals.
-    st = trace(stats=True)
-    counts = torch.tensor([st["pixels"], st["segments"], st["node_visits"], st["tri_tests"], st["mat_reads"]],
-                          dtype=torch.float64, device=dev)
+    # Counting pass (untimed): this rank's work, then the job totals.
+    per = [trace(f, stats=True) for f in range(F)]
+    counts = torch.tensor([sum(p[k] for p in per) for k in ("pixels", "segments", "node_visits", "tri_tests",
+                                                             "mat_reads")], dtype=torch.float64, device=dev)
     local = counts.clone()
     if world > 1:
         dist.all_reduce(counts)
     pixels, segments, node_visits, tri_tests, mat_reads = [float(x) for x in counts.tolist()]
-    l_pix, l_seg, l_nodes, l_tris, l_mats = [float(x) for x in local.tolist()]
-    log(f"[rank {rank}] frame: {segments:.0f} segments ({segments / pixels:.3f}/px), "
+    l_pix, l_seg, l_nodes, l_tris, l_mats = [float(x) / F for x in local.tolist()]   # per launch
+    log(f"[rank {rank}] step: {F} frame(s), {segments:.0f} segments ({segments / pixels:.3f}/px), "
         f"{node_visits / segments:.2f} node visits/seg, {tri_tests / segments:.3f} tri tests/seg")
 
     for _ in range(args.warmup):
@@ -128,16 +164,26 @@ def main() -> None:
         dist.barrier()
     torch.cuda.synchronize(dev)
 
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    evs = [[(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(F)]
+           for _ in range(args.steps)]
     t_start = time.perf_counter()
     for k in range(args.steps):
-        step(evs[k])
+        out = step(evs[k])
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t_start
-    kernel_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
+    kernel_ms = float(np.mean([a.elapsed_time(b) for e in evs for a, b in e]))
+
+    verified = None
+    if world > 1 and rank == 0:                    # the assembled frames equal the 1-GPU frame
+        full = torch.empty((H, W, 4), dtype=torch.uint8, device=dev)
+        check(L.rt_render_bands_device(renderer._ctx, C.byref(cam.ubo), W, H, B, H, 1, 0, full.data_ptr(), None,
+                                       main_stream.cuda_stream, None))
+        torch.cuda.synchronize(dev)
+        frames = out if frames_mode else out[None]
+        verified = bool(all(torch.equal(frames[f], full) for f in range(frames.shape[0])))
 
     t = torch.tensor([elapsed, kernel_ms], dtype=torch.float64, device=dev)
     if world > 1:
@@ -150,7 +196,8 @@ def main() -> None:
     achieved = alg_bytes / (kernel_ms * 1e-3) / 1e9
     traffic, traffic_src = None, None
     if args.traffic_json and os.path.exists(args.traffic_json):
-        tj = json.load(open(args.traffic_json))
+        with open(args.traffic_json) as fh:
+            tj = json.load(fh)
         if tj.get("config") == cfg.name and world == 1:   # PMC bytes of the same kernel on this workload
             traffic, traffic_src = tj.get("hbm_bytes_per_launch"), tj.get("source")
 
@@ -168,7 +215,7 @@ def main() -> None:
             "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 4),
             "higher_is_better": True,
-            "scaling": "strong",
+            "scaling": "weak" if frames_mode else "strong",
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic (seeded procedural 50k-triangle shell + ground plane + type-3 cube; default camera)",
@@ -180,9 +227,15 @@ def main() -> None:
                 "node_visits_per_segment": round(node_visits / segments, 3),
                 "tri_tests_per_segment": round(tri_tests / segments, 4),
                 "partition": "single frame" if world == 1 else
-                             f"interleaved {band_h}-row bands, RCCL gather + assembly on rank 0",
+                             (f"{F} frames per step, {band_h}-row bands rotated over {world} ranks "
+                              f"(rank r traces bands (r+f) mod {world} of frame f), RCCL gather + rank-0 assembly"
+                              if frames_mode else
+                              f"one frame per step, interleaved {band_h}-row bands, RCCL gather + rank-0 assembly"),
+                "frames_per_step": F,
+                "frames_verified": verified,
                 "parallelism": f"tile{world}",
                 "schedule": {k: renderer.get_option(k) for k in ("kernel", "walk", "wave_tile", "coop_lanes")},
+                "launches_per_step": F,
             },
             "roofline": {
                 "bound": "hbm",

@@ -68,3 +68,73 @@ def test_band_gather_reassembles_frame(world, band_h):
     ref, _, _ = oracle_lib.render(built.model_vertex_data, built.model_material_data, built.flat_bvh_data,
                                   cam.ubo_bytes(), 160, 90, 3)
     assert np.array_equal(frame, ref)
+
+
+def _batch_worker(rank, world, port, band_h, q):
+    import sys
+    sys.path[:0] = [os.path.join(ROOT, "3d-ray-tracer-vulkan_amd"), ROOT]
+    import torch
+    import torch.distributed as dist
+    from oracle import oracle_lib
+    from rtamd import configs
+    from rtamd.dist import BatchPlan, batch_band_offset, band_rows, gather_batch
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        cfg = configs.config2()
+        built = cfg.build()
+        W, H, B = 96, 53, 3
+        F = world
+        plan = BatchPlan(H, band_h, world, F)
+        local = torch.zeros((F, plan.max_rows, W, 4), dtype=torch.uint8)
+        traced = 0
+        for f in range(F):
+            cam = configs.Camera((-25.0 + 5 * f, 30.0, 140.0), (0.0, 0.0, 0.0), (0.0, 1.0, 0.0), 20.0, W / H)
+            rows = band_rows(H, band_h, world, batch_band_offset(f, world, rank))
+            assert len(rows) == plan.local_rows(rank, f)
+            for k, y in enumerate(rows):
+                rgba, _, _ = oracle_lib.render(built.model_vertex_data, built.model_material_data,
+                                               built.flat_bvh_data, cam.ubo_bytes(), W, H, B,
+                                               tile=(0, int(y), W, 1), n_threads=1)
+                local[f, k] = torch.from_numpy(rgba[0])
+            traced += len(rows)
+        q.put(("traced", rank, traced))
+        frames = gather_batch(local, plan)
+        if rank == 0:
+            q.put(("frames", frames.numpy()))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,band_h", [(2, 16), (3, 8)])
+def test_batch_gather_reassembles_frames(world, band_h):
+    """Weak-scaling batches: frame f's bands rotate over the ranks, every rank
+    traces one frame's worth of rows, and rank 0 reassembles all frames."""
+    from oracle import oracle_lib
+    from rtamd import configs
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_batch_worker, args=(r, world, port, band_h, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = {}
+    traced = {}
+    for _ in range(world + 1):
+        item = q.get(timeout=300)
+        if item[0] == "traced":
+            traced[item[1]] = item[2]
+        else:
+            got["frames"] = item[1]
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    cfg = configs.config2()
+    built = cfg.build()
+    W, H, B = 96, 53, 3
+    assert set(traced.values()) == {H}                       # one frame's rows per rank
+    for f in range(world):
+        cam = configs.Camera((-25.0 + 5 * f, 30.0, 140.0), (0.0, 0.0, 0.0), (0.0, 1.0, 0.0), 20.0, W / H)
+        ref = oracle_lib.render(built.model_vertex_data, built.model_material_data, built.flat_bvh_data,
+                                cam.ubo_bytes(), W, H, B)[0]
+        assert np.array_equal(got["frames"][f], ref), f

@@ -1,0 +1,18 @@
+#!/bin/bash
+# Rehearse bench.py's N>1 paths on a 1-GPU box: 2 ranks share the GPU.
+# (The real 1/2/4/8-GPU runs are the driver's.)
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+OUT=gpurun_out/${TAG:-dist}
+mkdir -p "$OUT"
+for part in frames bands; do
+  for be in ${BACKENDS:-nccl gloo}; do
+    BENCH_SHARE_GPU=1 BENCH_DIST_BACKEND=$be timeout -k 10 300 python -m torch.distributed.run --nnodes=1 \
+      --nproc-per-node 2 --master-addr 127.0.0.1 --master-port $((29500 + RANDOM % 1000)) bench.py --gpus 2 \
+      --steps 10 --warmup 3 --partition $part > "$OUT/bench_${part}_${be}.json" 2> "$OUT/bench_${part}_${be}.err"
+    rc=$?
+    echo "$part $be rc=$rc" >> "$OUT/status.txt"
+    if [ $rc -eq 0 ]; then break; fi
+    if [ $rc -ne 1 ]; then exit $rc; fi
+  done
+done
