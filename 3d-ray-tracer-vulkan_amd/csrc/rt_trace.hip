@@ -136,6 +136,12 @@ __device__ __forceinline__ bool tri_test(float4 P0, float4 P1, float4 P2, V3 o, 
     return t > kTMin;
 }
 
+// Keep loaded values where they are: an empty asm that "modifies" them stops
+// the compiler from sinking a load into the branch that uses it (which would
+// turn one memory round trip into two dependent ones).
+__device__ __forceinline__ void pin(float4& q) { asm volatile("" : "+v"(q.x), "+v"(q.y), "+v"(q.z), "+v"(q.w)); }
+__device__ __forceinline__ void pin(uint2& q) { asm volatile("" : "+v"(q.x), "+v"(q.y)); }
+
 // One node of the walk.  `leaf` says whether node i is a leaf (from its
 // predecessor's L bits), so the leaf's triangle is fetched in the same round
 // trip as the node.  Returns the next node index and updates `leaf`.
@@ -152,11 +158,16 @@ __device__ __forceinline__ int node_step(const float4* __restrict__ nodes, const
                                          unsigned long long& c_node, unsigned long long& c_tri) {
     const float4 A = nodes[2 * i];
     const float4 B = nodes[2 * i + 1];
-    float4 P0 = make_float4(0.f, 0.f, 0.f, 0.f), P1 = P0, P2 = P0;
+    // Read only when `leaf`: left undefined otherwise, so the compiler does
+    // not zero twelve registers on every step.
+    float4 P0, P1, P2;
     if (leaf) {
         P0 = leafs[3 * i + 0];
         P1 = leafs[3 * i + 1];
         P2 = leafs[3 * i + 2];
+        pin(P0);   // three whole 16-B loads, not five partial ones
+        pin(P1);
+        pin(P2);
     }
     float te;
     bool ind;
@@ -246,11 +257,6 @@ __device__ __forceinline__ int lanes_below(uint64_t mask) {
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
 }
 
-// Keep loaded values where they are: an empty asm that "modifies" them stops
-// the compiler from sinking a load into the branch that uses it (which would
-// turn one memory round trip into two dependent ones).
-__device__ __forceinline__ void pin(float4& q) { asm volatile("" : "+v"(q.x), "+v"(q.y), "+v"(q.z), "+v"(q.w)); }
-__device__ __forceinline__ void pin(uint2& q) { asm volatile("" : "+v"(q.x), "+v"(q.y)); }
 
 __device__ __forceinline__ int lane_i(int v, int k) { return __builtin_amdgcn_readlane(v, k); }
 __device__ __forceinline__ float lane_f(float v, int k) {
