@@ -313,14 +313,14 @@ static int set_schedule(const rt_ctx* ctx, PerDevice& p, TraceArgs& a, const rt_
     if (ctx->diag && a.kernel == kKernelSimple) {
         const int tw_w = 8 << a.wave_tile, th_w = 8 >> a.wave_tile;
         const size_t waves = (size_t)((a.tw + 4 * tw_w - 1) / (4 * tw_w)) * ((a.th + th_w - 1) / th_w) * 4;
-        if (waves * 4 > p.diag_cap) {
+        if (waves * 8 > p.diag_cap) {
             if (p.d_diag) (void)hipFree(p.d_diag);
             p.d_diag = nullptr;
             p.diag_cap = 0;
-            RT_HIP_CHECK(hipMalloc(&p.d_diag, waves * 4 * sizeof(unsigned long long)));
-            p.diag_cap = waves * 4;
+            RT_HIP_CHECK(hipMalloc(&p.d_diag, waves * 8 * sizeof(unsigned long long)));
+            p.diag_cap = waves * 8;
         }
-        p.diag_used = waves * 4;
+        p.diag_used = waves * 8;
         a.diag = p.d_diag;
     }
     a.spill = nullptr;

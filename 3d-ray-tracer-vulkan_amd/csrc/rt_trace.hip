@@ -280,11 +280,13 @@ __device__ __forceinline__ float lane_f(float v, int k) {
 // The float operations are node_step's, so closest_t, the hit and the visit /
 // triangle-test counts equal the per-lane walk's.
 template <bool COUNT>
-__device__ __forceinline__ void coop_walk(const float4* __restrict__ nodes, const float4* __restrict__ leafs,
-                                          int end, int n, V3 o, V3 d, V3 inv, float& closest, int& hit,
-                                          unsigned long long& c_node, unsigned long long& c_tri) {
+__device__ __forceinline__ int coop_walk(const float4* __restrict__ nodes, const float4* __restrict__ leafs,
+                                         int end, int n, V3 o, V3 d, V3 inv, float& closest, int& hit,
+                                         unsigned long long& c_node, unsigned long long& c_tri) {
     const int lane = threadIdx.x & 63;
+    int windows = 0;
     while (n < end) {
+        ++windows;
         const int j = n + lane;
         float te = 0.0f, tt = 0.0f;
         int sk = 0, tri = -1;
@@ -325,6 +327,7 @@ __device__ __forceinline__ void coop_walk(const float4* __restrict__ nodes, cons
         }
         n += k;
     }
+    return windows;
 }
 
 // ------------------------------------------------------------ simple kernel --
@@ -348,6 +351,7 @@ __device__ __forceinline__ void diag_stamp(unsigned long long* rec, int which) {
 
 // Optional features of trace_simple, compiled in only where a schedule needs
 // them so the default inner loop carries no extra work.
+constexpr int kDiagWords = 8;     // per-wave diag record (rtamd.h rt_diag_copy)
 constexpr int kFeatSpill = 1;     // split schedule: hand paths on after seg_limit segments
 constexpr int kFeatHeavy = 2;     // tiered schedule: hand walks on after heavy_budget visits
 constexpr int kFeatPrio = 4;      // raise wave priority after prio_after visits
@@ -364,7 +368,7 @@ __global__ __launch_bounds__(256) void trace_simple(TraceArgs a) {
     const int wave = threadIdx.x >> 6;
     unsigned long long* drec = nullptr;
     if (DIAG) {
-        drec = a.diag + 4 * (size_t)((blockIdx.y * gridDim.x + blockIdx.x) * 4 + wave);
+        drec = a.diag + kDiagWords * (size_t)((blockIdx.y * gridDim.x + blockIdx.x) * 4 + wave);
         diag_stamp(drec, 0);
     }
     // walk 1: the right siblings still to visit, as (t_enter or +inf, R | L(R) << 31),
@@ -386,6 +390,7 @@ __global__ __launch_bounds__(256) void trace_simple(TraceArgs a) {
     const V3 rhi = {a.scene.root_box[3], a.scene.root_box[4], a.scene.root_box[5]};
     unsigned long long c_seg = 0, c_node = 0, c_tri = 0, c_mat = 0;
     int steps = 0;
+    unsigned long long d_iters = 0, d_windows = 0, d_coop_t = 0;   // diag builds only
 
     uint32_t seed = 0;
     V3 o = {0.f, 0.f, 0.f}, d = {0.f, 0.f, 1.f};
@@ -443,6 +448,7 @@ __global__ __launch_bounds__(256) void trace_simple(TraceArgs a) {
         if (WALK == 0 && !(FEAT & (kFeatPrio | kFeatHeavy))) {
             // The per-node walk: one dependent load per visit, lanes in lockstep.
             while (walking) {
+                if (DIAG) ++d_iters;
                 n = node_step<COUNT>(nodes, leafs, n, nleaf, o, d, inv, closest, hit, c_node, c_tri);
                 walking = n < end;
                 if ((FEAT & kFeatCoopTail) && __popcll(__ballot(walking)) <= a.coop_lanes) break;
@@ -590,6 +596,8 @@ __global__ __launch_bounds__(256) void trace_simple(TraceArgs a) {
             // Every lane is here.  Finish the remaining walks one ray at a
             // time with the whole wave, each from its next node n.
             uint64_t rem = __ballot(walking);
+            unsigned long long tc0 = 0;
+            if (DIAG && rem != 0) tc0 = wall_clock64();
             while (rem != 0) {
                 const int L = __ffsll((long long)rem) - 1;
                 rem &= rem - 1;
@@ -601,7 +609,8 @@ __global__ __launch_bounds__(256) void trace_simple(TraceArgs a) {
                 unsigned long long cn = 0, ct = 0;   // wave-uniform: counted once, by lane L
                 int start = n;
                 if (WALK == 1 && kind == kSkip && lane == L) start = (int)(__float_as_uint(nodes[2 * n].w) & kIdx);
-                coop_walk<COUNT>(nodes, leafs, end, lane_i(start, L), bo, bd, bi, bc, bh, cn, ct);
+                const int nw = coop_walk<COUNT>(nodes, leafs, end, lane_i(start, L), bo, bd, bi, bc, bh, cn, ct);
+                if (DIAG) d_windows += nw;
                 if (lane == L) {
                     closest = bc;
                     hit = bh;
@@ -611,6 +620,7 @@ __global__ __launch_bounds__(256) void trace_simple(TraceArgs a) {
                     }
                 }
             }
+            if (DIAG && tc0) d_coop_t += wall_clock64() - tc0;
         }
         if (alive) {
             if (hit >= 0) {                                               // :212
@@ -654,7 +664,20 @@ __global__ __launch_bounds__(256) void trace_simple(TraceArgs a) {
     }
     if (pixel && !handed_on) write_pixel(a, lx, ly, fin);
     if (COUNT) flush_counters(a.counters, c_seg, c_node, c_tri, c_mat);
-    if (DIAG) diag_stamp(drec, 1);
+    if (DIAG) {
+        diag_stamp(drec, 1);
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) {   // the wave's iterations = the longest lane's
+            const unsigned long long o2 = __shfl_xor(d_iters, off);
+            d_iters = o2 > d_iters ? o2 : d_iters;
+        }
+        if (lane == 0) {
+            drec[4] = d_iters;
+            drec[5] = d_windows;
+            drec[6] = d_coop_t;
+            drec[7] = 0;
+        }
+    }
 }
 
 // -------------------------------------------------------- persistent kernel --

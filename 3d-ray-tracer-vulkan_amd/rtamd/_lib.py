@@ -12,7 +12,7 @@ import os
 import threading
 
 PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.path.join(PKG_ROOT, "lib", "librtamd.so")
+LIB_PATH = os.environ.get("RTAMD_LIB_PATH") or os.path.join(PKG_ROOT, "lib", "librtamd.so")   # override: experiments
 
 RT_OK = 0
 RT_ERR = {

@@ -191,9 +191,11 @@ int rt_render_wait(rt_ctx* ctx, uint64_t ticket);
  * RTAMD_SEG_LIMIT, RTAMD_SHADE_MIN and RTAMD_BLOCKS_PER_CU. */
 int rt_set_option(rt_ctx* ctx, const char* name, int64_t value);
 /* Diagnostics: with option "diag" = 1, kernel 0 records per wave
- * {start, end} (s_memrealtime, 100 MHz), {XCC id << 32 | HW_ID}, {block << 8 |
- * wave} into a device buffer; rt_diag_copy copies up to cap_words 64-bit words
- * of the last launch (n_words = words recorded).  Not for timing runs. */
+ * 8 words: {start, end} (s_memrealtime, 100 MHz), {XCC id << 32 | HW_ID},
+ * {block << 8 | wave}, {lockstep walk iterations}, {cooperative windows},
+ * {ticks spent in the cooperative tail}, {0} into a device buffer;
+ * rt_diag_copy copies up to cap_words 64-bit words of the last launch
+ * (n_words = words recorded).  Not for timing runs. */
 int rt_diag_copy(rt_ctx* ctx, void* dst, size_t cap_words, size_t* n_words);
 int rt_get_option(rt_ctx* ctx, const char* name, int64_t* value);
 

@@ -21,6 +21,7 @@ def main():
     ap.add_argument("--bounces", type=int, default=0)
     ap.add_argument("--wave-tile", type=int, default=0)
     ap.add_argument("--out", default="gpurun_out/diag.npz")
+    ap.add_argument("--opt", action="append", default=[], help="rt_set_option name=value (repeatable)")
     args = ap.parse_args()
     import torch
     import rtamd
@@ -35,6 +36,9 @@ def main():
     r.upload_scene(built)
     r.set_option("kernel", 0)
     r.set_option("wave_tile", args.wave_tile)
+    for kv in args.opt:
+        k, v = kv.split("=")
+        r.set_option(k, int(v))
     L = rtamd.lib()
     out = torch.empty((H, W, 4), dtype=torch.uint8, device="cuda:0")
     for diag in (0, 0, 1):
@@ -45,7 +49,9 @@ def main():
     check(L.rt_diag_copy(r._ctx, None, 0, C.byref(n)))
     rec = np.zeros(n.value, dtype=np.uint64)
     check(L.rt_diag_copy(r._ctx, rec.ctypes.data, n.value, C.byref(n)))
-    rec = rec.reshape(-1, 4)
+    rec = rec.reshape(-1, 8)
+    is_help = (rec[:, 2] >> 32) == 0xFFFFFFFF
+    help_rec, rec = rec[is_help], rec[~is_help]
     t0, t1 = rec[:, 0].astype(np.int64), rec[:, 1].astype(np.int64)
     hw, xcc = (rec[:, 2] & 0xFFFFFFFF).astype(np.int64), (rec[:, 2] >> 32).astype(np.int64)
     base = t0.min()
@@ -75,9 +81,36 @@ def main():
         print(f"tail: fewer than half the CUs busy from {grid[half[0]] / 100:.1f} us to end ({span / 100:.1f} us)")
     print("per-XCD wave-time share:", [round(float(dur[xcc == x].sum() / dur.sum()), 3) for x in range(8)])
     print("first start / last start / last end (us):", 0, t0.max() / 100, span / 100)
+    ends = np.sort(t1)
+    print("time by which 50/90/99/99.9/100% of waves ended (us):",
+          " ".join(f"{ends[min(len(ends) - 1, int(q * len(ends)))] / 100:.1f}" for q in (0.5, 0.9, 0.99, 0.999, 1.0)))
+    alive = [int(((t0 <= g) & (t1 > g)).sum()) for g in grid[::10]]
+    print("waves alive at 20 time points:", alive)
     blk = (rec[:, 3] >> 8).astype(np.int64)
     late = np.argsort(t1)[-20:]
     print("last 20 waves to finish: block ids", blk[late].tolist(), "durations us", (dur[late] / 100).astype(int).tolist())
+    iters, wins, coop_t = rec[:, 4].astype(np.int64), rec[:, 5].astype(np.int64), rec[:, 6].astype(np.int64)
+    print("lockstep iterations per wave: p50 %d p99 %d max %d; coop windows p50 %d max %d" % (
+        np.median(iters), np.percentile(iters, 99), iters.max(), np.median(wins), wins.max()))
+    for k in late[::-1][:8]:
+        lock_t = max(1, dur[k] - coop_t[k])
+        print(f"  slow wave block {blk[k]}: {dur[k] / 100:.0f} us, {iters[k]} lockstep iters "
+              f"({lock_t / 100 / max(1, iters[k]) * 1000:.0f} ns each incl. shading), "
+              f"{wins[k]} coop windows in {coop_t[k] / 100:.0f} us")
+    ho = rec[:, 7].astype(np.int64)
+    if (ho > 0).any():
+        hot = (ho[ho > 0] - base) / 100
+        print(f"tile waves that handed on: {(ho > 0).sum()}, at us p0 {hot.min():.0f} p50 {np.median(hot):.0f} max {hot.max():.0f}")
+    if len(help_rec):
+        hs, he = (help_rec[:, 0].astype(np.int64) - base) / 100, (help_rec[:, 1].astype(np.int64) - base) / 100
+        rays = help_rec[:, 4].astype(np.int64)
+        first = help_rec[:, 6].astype(np.int64)
+        busy = rays > 0
+        print(f"helper waves {len(help_rec)}: start p0 {hs.min():.0f} p50 {np.median(hs):.0f} us; end max {he.max():.0f} us; "
+              f"rays total {rays.sum()} (waves with work {busy.sum()}, max per wave {rays.max()})")
+        if busy.any():
+            ft = (first[busy] - base) / 100
+            print(f"  first ray taken at us p0 {ft.min():.0f} p50 {np.median(ft):.0f}; busy helpers end p50 {np.median(he[busy]):.0f} max {he[busy].max():.0f}")
     os.makedirs(os.path.dirname(args.out) or ".", exist_ok=True)
     np.savez(args.out, rec=rec)
 
