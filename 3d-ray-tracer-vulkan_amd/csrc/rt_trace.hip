@@ -107,9 +107,15 @@ __device__ __forceinline__ void primary_ray_seeded(const TraceArgs& a, int x, in
 
 // Slab test of hit_aabb (:88-103), split into the part that does not depend
 // on closest_t (ind) and t_enter; the box is hit iff ind && te < closest_t.
+typedef float f2 __attribute__((ext_vector_type(2)));
+
 __device__ __forceinline__ void slab(float4 A, float4 B, V3 o, V3 inv, float& te, bool& ind) {
-    const float t0x = (A.x - o.x) * inv.x, t1x = (B.x - o.x) * inv.x;
-    const float t0y = (A.y - o.y) * inv.y, t1y = (B.y - o.y) * inv.y;
+    // x and y in packed FP32 (v_pk_add_f32 / v_pk_mul_f32: two IEEE binary32
+    // operations per lane per instruction, each rounded exactly as the scalar one).
+    const f2 oxy = {o.x, o.y}, ixy = {inv.x, inv.y};
+    const f2 t0 = (f2{A.x, A.y} - oxy) * ixy;
+    const f2 t1 = (f2{B.x, B.y} - oxy) * ixy;
+    const float t0x = t0.x, t1x = t1.x, t0y = t0.y, t1y = t1.y;
     const float t0z = (A.z - o.z) * inv.z, t1z = (B.z - o.z) * inv.z;
     te = fmaxf(fmaxf(fminf(t0x, t1x), fminf(t0y, t1y)), fminf(t0z, t1z));
     const float tx = fminf(fminf(fmaxf(t0x, t1x), fmaxf(t0y, t1y)), fmaxf(t0z, t1z));
@@ -445,10 +451,13 @@ __global__ __launch_bounds__(256) void trace_simple(TraceArgs a) {
             ++c_seg;
             if (end > 0) ++c_node;                                       // the root visit
         }
-        if (WALK == 0 && !(FEAT & (kFeatPrio | kFeatHeavy))) {
+        if (WALK == 0 && !(FEAT & kFeatHeavy)) {
             // The per-node walk: one dependent load per visit, lanes in lockstep.
             while (walking) {
                 if (DIAG) ++d_iters;
+                // A wave still walking after prio_after steps holds the frame's
+                // critical path: let it win instruction arbitration.
+                if ((FEAT & kFeatPrio) && ++steps == a.prio_after) __builtin_amdgcn_s_setprio(3);
                 n = node_step<COUNT>(nodes, leafs, n, nleaf, o, d, inv, closest, hit, c_node, c_tri);
                 walking = n < end;
                 if ((FEAT & kFeatCoopTail) && __popcll(__ballot(walking)) <= a.coop_lanes) break;
@@ -943,6 +952,7 @@ hipError_t launch_trace(const TraceArgs& a, hipStream_t stream) {
             switch (feat) {
                 case 0: RT_SIMPLE(0, 0) break;
                 case kFeatCoopTail: RT_SIMPLE(kFeatCoopTail, 0) break;
+                case kFeatCoopTail | kFeatPrio: RT_SIMPLE(kFeatCoopTail | kFeatPrio, 0) break;
                 case kFeatCoopTail | kFeatExt: RT_SIMPLE(kFeatCoopTail | kFeatExt, 0) break;
                 default: RT_SIMPLE(kFeatSpill | kFeatHeavy | kFeatPrio | kFeatCoopTail | kFeatExt, 0) break;
             }
