@@ -138,6 +138,10 @@ struct TraceArgs {
     float*   accum;             // kExtAccumulate: running linear-colour sums, 3 floats per pixel (tw*th)
     int      walk;              // simple: 0 = one node per step (nodes/leafs),
                                 //   1 = child pairs + per-lane stack of t_enter (pairs)
+    int      block_waves;       // simple: waves per workgroup, 4 (256 threads) or 1 (64 threads)
+    Counters* sink;             // tiered: counters trace_coop adds into when counters is null
+    int      coop_walk;         // cooperative walks (coop tail, trace_coop): 0 = 64-node preorder
+                                //   windows (coop_walk), 1 = preorder frontier (frontier_walk)
 };
 
 // Host-side compact-scene build from the reference records; validates the

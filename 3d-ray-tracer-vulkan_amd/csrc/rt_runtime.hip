@@ -256,6 +256,8 @@ struct rt_ctx {
     int  coop_lanes = 2;           // kernel 0: cooperative tail once <= this many lanes walk (0 = off)
     int  ext = 0;                  // non-reference extensions (kExt* bits), off by default
     int  walk = 0;                 // kernel 0: 0 = node per step (fastest measured), 1 = child pairs + t_enter stack
+    int  coop_walk = 0;            // cooperative walks: 0 = 64-node windows, 1 = preorder frontier
+    int  block_waves = 1;          // kernel 0: waves per workgroup (1: a finished wave frees its slot at once; or 4)
     bool has_scene = false;
     int  n_nodes = 0, n_tris = 0, max_depth = 0;
     uint64_t issued = 0;           // rt_render_async tickets handed out
@@ -280,6 +282,9 @@ static int set_schedule(const rt_ctx* ctx, PerDevice& p, TraceArgs& a, const rt_
     a.prio_after = ctx->prio_after > 0 ? ctx->prio_after : -1;
     a.coop_lanes = ctx->coop_lanes;
     a.walk = ctx->walk;
+    a.coop_walk = ctx->coop_walk;
+    a.block_waves = ctx->block_waves;
+    a.sink = p.d_counters + 1;
     a.seg_limit = a.kernel == kKernelSplit ? ctx->seg_limit : (1 << 30);
     a.ext = ctx->ext;
     a.sky_enabled = cam->sky_enabled;
@@ -310,17 +315,19 @@ static int set_schedule(const rt_ctx* ctx, PerDevice& p, TraceArgs& a, const rt_
         a.grid_blocks = std::min(a.grid_blocks, std::max(1, (tiles + 3) / 4));
     }
     a.diag = nullptr;
-    if (ctx->diag && a.kernel == kKernelSimple) {
+    if (ctx->diag && (a.kernel == kKernelSimple || a.kernel == kKernelTiered)) {
+        // simple: 8 words per wave; tiered adds 4 words per suspended path (trace_coop)
         const int tw_w = 8 << a.wave_tile, th_w = 8 >> a.wave_tile;
         const size_t waves = (size_t)((a.tw + 4 * tw_w - 1) / (4 * tw_w)) * ((a.th + th_w - 1) / th_w) * 4;
-        if (waves * 8 > p.diag_cap) {
+        const size_t words = waves * 8 + (a.kernel == kKernelTiered ? (size_t)a.tw * a.th * 4 : 0);
+        if (words > p.diag_cap) {
             if (p.d_diag) (void)hipFree(p.d_diag);
             p.d_diag = nullptr;
             p.diag_cap = 0;
-            RT_HIP_CHECK(hipMalloc(&p.d_diag, waves * 8 * sizeof(unsigned long long)));
-            p.diag_cap = waves * 8;
+            RT_HIP_CHECK(hipMalloc(&p.d_diag, words * sizeof(unsigned long long)));
+            p.diag_cap = words;
         }
-        p.diag_used = waves * 8;
+        p.diag_used = words;
         a.diag = p.d_diag;
     }
     a.spill = nullptr;
@@ -385,6 +392,8 @@ int rt_create(const int* device_ids, int n_devices, rt_ctx** out) {
                     : std::strcmp(k, "split") == 0 ? kKernelSplit
                     : std::strcmp(k, "tiered") == 0 ? kKernelTiered : ctx->kernel;
     if (const char* v = std::getenv("RTAMD_WALK")) ctx->walk = std::atoi(v) ? 1 : 0;
+    if (const char* v = std::getenv("RTAMD_COOP_WALK")) ctx->coop_walk = std::atoi(v) ? 1 : 0;
+    if (const char* v = std::getenv("RTAMD_BLOCK_WAVES")) ctx->block_waves = std::atoi(v) == 1 ? 1 : 4;
     if (const char* v = std::getenv("RTAMD_COOP_LANES")) ctx->coop_lanes = std::max(0, std::min(64, std::atoi(v)));
     if (const char* v = std::getenv("RTAMD_SEG_LIMIT")) ctx->seg_limit = std::max(1, std::min(1024, std::atoi(v)));
     if (const char* v = std::getenv("RTAMD_SHADE_MIN")) ctx->shade_min = std::max(1, std::min(64, std::atoi(v)));
@@ -408,7 +417,7 @@ int rt_create(const int* device_ids, int n_devices, rt_ctx** out) {
         if (e == hipSuccess) e = hipStreamCreateWithFlags(&p.stream, hipStreamNonBlocking);
         if (e == hipSuccess) e = hipEventCreate(&p.ev0);
         if (e == hipSuccess) e = hipEventCreate(&p.ev1);
-        if (e == hipSuccess) e = hipMalloc(&p.d_counters, sizeof(Counters));
+        if (e == hipSuccess) e = hipMalloc(&p.d_counters, 2 * sizeof(Counters));   // [1]: trace_coop's sink
         if (e == hipSuccess) e = hipMalloc(&p.d_queue, sizeof(unsigned) * 3 * kQueueSlots);
         if (e == hipSuccess) e = hipStreamCreateWithFlags(&p.copy_stream, hipStreamNonBlocking);
         for (int k2 = 0; k2 < 2 && e == hipSuccess; ++k2) {
@@ -835,6 +844,10 @@ int rt_set_option(rt_ctx* ctx, const char* name, int64_t value) {
         ctx->ext = (int)value;
     } else if (std::strcmp(name, "walk") == 0 && (value == 0 || value == 1)) {
         ctx->walk = (int)value;
+    } else if (std::strcmp(name, "coop_walk") == 0 && (value == 0 || value == 1)) {
+        ctx->coop_walk = (int)value;
+    } else if (std::strcmp(name, "block_waves") == 0 && (value == 1 || value == 4)) {
+        ctx->block_waves = (int)value;
     } else if (std::strcmp(name, "diag") == 0 && (value == 0 || value == 1)) {
         ctx->diag = (int)value;
     } else if (std::strcmp(name, "wave_tile") == 0 && value >= 0 && value <= 3) {
@@ -856,6 +869,8 @@ int rt_get_option(rt_ctx* ctx, const char* name, int64_t* value) {
     else if (std::strcmp(name, "heavy_budget") == 0) *value = ctx->heavy_budget;
     else if (std::strcmp(name, "coop_lanes") == 0) *value = ctx->coop_lanes;
     else if (std::strcmp(name, "walk") == 0) *value = ctx->walk;
+    else if (std::strcmp(name, "coop_walk") == 0) *value = ctx->coop_walk;
+    else if (std::strcmp(name, "block_waves") == 0) *value = ctx->block_waves;
     else if (std::strcmp(name, "extensions") == 0) *value = ctx->ext;
     else if (std::strcmp(name, "blocks_per_cu") == 0)
         *value = ctx->blocks_per_cu > 0 ? ctx->blocks_per_cu : (ctx->dev.empty() ? 0 : ctx->dev[0].blocks_per_cu);

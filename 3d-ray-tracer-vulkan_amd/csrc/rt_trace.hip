@@ -26,6 +26,10 @@
 //                     shade_min lanes are ready.
 //   split / tiered    trace_simple for the first part of every path, then the
 //                     rest on trace_persistent (resume) or trace_coop.
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+
 #include "rt_internal.h"
 
 namespace rtamd {
@@ -336,6 +340,174 @@ __device__ __forceinline__ int coop_walk(const float4* __restrict__ nodes, const
     return windows;
 }
 
+// ------------------------------------------------------------ frontier walk --
+//
+// The whole wave walks ONE ray (arguments wave-uniform), like coop_walk, but
+// each round trip expands up to 64 subtrees of a preorder-sorted frontier
+// instead of a contiguous window, so a round follows the walk down every live
+// branch at once (a heavy segment takes ~17 rounds, about the tree depth,
+// against ~50 windows; tools/frontier_model.py).
+//
+// The frontier F (per-wave LDS stack, front = top) holds, in preorder, the
+// roots of the disjoint subtrees still to finish, some already tested:
+//   x = node | L(node) << 31, y = skip(node) (a tested leaf: its triangle),
+//   z = t_enter of the node's box (it hit at the closest_t of its insertion),
+//   w = kUnres, or 0 (internal: its live children follow it in F), or the
+//       leaf's triangle t (+inf: no valid intersection).
+// Each round:
+//   1. replay: entries are finalized from the front in preorder with the exact
+//      closest_t, as the reference visits them.  A box that misses now skips
+//      the entries of its subtree (node < skip); a tested leaf that hits and
+//      improves sets closest_t / hit; counts are node_step's (2 per hit
+//      internal node, 1 per hit leaf).  Stops at the first untested entry
+//      that still hits;
+//   2. expand: up to 64 untested entries that still hit, one per lane: an
+//      internal node loads its child-pair record and keeps the children whose
+//      boxes hit at this closest_t, a leaf loads its triangle and tests it up
+//      to "t < closest_t" (the compare itself is left to the replay).
+// closest_t only shrinks, so a box or triangle that misses at an earlier
+// closest_t misses at every later one: speculation can only add work, never
+// change a result.  When F is empty the walk continues along the skip chain
+// of the last finished subtree (the reference's stack below its position).
+// If the front cannot be expanded for lack of room (never seen: the cap is
+// 4x the reference's 64-entry stack), the walk stops with pos = the
+// reference's next node, to be finished by node_step.
+constexpr uint32_t kIdx = 0x7FFFFFFFu;      // node index bits of a link word
+constexpr int kFCap = 256;                   // frontier entries per wave (16 B each)
+constexpr uint32_t kUnres = 0xFFFFFFFFu;
+
+template <bool COUNT>
+__device__ __forceinline__ bool frontier_walk(const float4* __restrict__ nodes, const float4* __restrict__ leafs,
+                                              const float4* __restrict__ pairs, int end, int& pos, bool& pos_leaf,
+                                              V3 o, V3 d, V3 inv, float& closest, int& hit,
+                                              unsigned long long& c_node, unsigned long long& c_tri, uint4* F,
+                                              int& rounds) {
+    const int lane = threadIdx.x & 63;
+    int c = pos;          // next chain node (wave-uniform)
+    int top = 0;          // entries in F
+    int drop = -1;        // entries with node < drop lie in a subtree whose box missed
+    // Every iteration finalizes or expands the front; the bound only guards
+    // the GPU against a logic error (parity tests would then fail, not hang).
+    for (int guard = 0; guard < (1 << 24); ++guard) {
+        if (top == 0) {
+            if (c >= end) break;
+            ++rounds;
+            const float4 A = nodes[2 * c];
+            const float4 B = nodes[2 * c + 1];
+            float te;
+            bool ind;
+            slab(A, B, o, inv, te, ind);
+            const int sk = (int)(__float_as_uint(A.w) & kIdx);
+            if (ind && te < closest) {
+                if (lane == 0)
+                    F[0] = make_uint4((uint32_t)c | ((__float_as_uint(B.w) & 2u) << 30), (uint32_t)sk,
+                                      __float_as_uint(te), kUnres);
+                top = 1;
+            }
+            c = sk;
+            continue;
+        }
+        const int nl = min(top, 64);
+        const bool in = lane < nl;
+        uint4 e = make_uint4(0u, 0u, 0x7F800000u, 0u);
+        if (in) e = F[top - 1 - lane];
+        const int node = (int)(e.x & kIdx);
+        const bool lf = (e.x >> 31) != 0u;
+        const bool unres = in && e.w == kUnres;
+        const float te = __uint_as_float(e.z);
+        const float tt = __uint_as_float(e.w);
+        // 1. replay
+        const uint64_t U = __ballot(unres);
+        const uint64_t Lm = __ballot(in && lf);
+        uint64_t H = __ballot(in && te < closest);
+        uint64_t T = __ballot(in && lf && !unres && tt < closest);
+        uint64_t Dm = __ballot(in && node < drop);
+        int k = 0;
+        while (k < nl) {
+            const uint64_t bit = 1ull << k;
+            if (Dm & bit) {                                      // inside a missed subtree
+                ++k;
+                continue;
+            }
+            if (!(H & bit)) {                                    // box misses at this closest_t
+                if (!(Lm & bit) && !(U & bit)) {                 // its live children follow: skip them
+                    drop = lane_i((int)e.y, k);
+                    Dm = __ballot(in && node < drop);
+                }
+                ++k;
+                continue;
+            }
+            if (U & bit) break;                                  // hit, not expanded yet
+            if (Lm & bit) {
+                if (COUNT) ++c_tri;
+                if (T & bit) {
+                    closest = lane_f(tt, k);
+                    hit = lane_i((int)e.y, k);
+                    H = __ballot(in && te < closest);
+                    T = __ballot(in && lf && !unres && tt < closest);
+                }
+            } else if (COUNT) {
+                c_node += 2;
+            }
+            ++k;
+        }
+        top -= k;
+        if (k == nl) continue;
+        ++rounds;
+        // 2. expand (lanes k.. are the region [top - (nl - k), top) of F)
+        const int room = kFCap - top;
+        const bool cand = in && lane >= k && unres && node >= drop && te < closest;
+        const uint64_t CI = __ballot(cand && !lf);
+        if (room < 2 && ((CI >> k) & 1ull)) {                    // no room for the front's children
+            pos = lane_i(node, k);
+            pos_leaf = false;
+            return false;
+        }
+        const bool sel = cand && (lf || 2 * (lanes_below(CI) + 1) <= room);
+        bool hL = false, hR = false;
+        uint4 cL = e, cR = e;
+        if (sel) {
+            if (lf) {
+                const float4 P0 = leafs[3 * node + 0];
+                const float4 P1 = leafs[3 * node + 1];
+                const float4 P2 = leafs[3 * node + 2];
+                float t;
+                const bool v = tri_test(P0, P1, P2, o, d, t);
+                e.y = __float_as_uint(P0.w);
+                e.w = v ? __float_as_uint(t) : 0x7F800000u;
+            } else {
+                const float4 Q0 = pairs[4 * node + 0];
+                const float4 Q1 = pairs[4 * node + 1];
+                const float4 Q2 = pairs[4 * node + 2];
+                const float4 Q3 = pairs[4 * node + 3];
+                float teL, teR;
+                bool indL, indR;
+                slab(Q0, Q1, o, inv, teL, indL);
+                slab(make_float4(Q0.w, Q1.w, Q2.w, 0.f), Q2, o, inv, teR, indR);
+                const uint32_t rw = __float_as_uint(Q3.x);
+                hL = indL && teL < closest;
+                hR = indR && teR < closest;
+                cL = make_uint4((uint32_t)(node + 1) | (__float_as_uint(Q3.y) != 0u ? 0x80000000u : 0u), rw & kIdx,
+                                __float_as_uint(teL), kUnres);
+                cR = make_uint4(rw, e.y, __float_as_uint(teR), kUnres);
+                e.w = 0u;
+            }
+        }
+        const bool reg = in && lane >= k;
+        const uint64_t RM = __ballot(reg), LM = __ballot(hL), RRM = __ballot(hR);
+        const int P = lanes_below(RM) + lanes_below(LM) + lanes_below(RRM);
+        const int ntop = top - (nl - k) + __popcll(RM) + __popcll(LM) + __popcll(RRM);
+        if (reg) {
+            F[ntop - 1 - P] = e;
+            if (hL) F[ntop - 2 - P] = cL;
+            if (hR) F[ntop - 2 - (hL ? 1 : 0) - P] = cR;
+        }
+        top = ntop;
+    }
+    pos = end;
+    return true;
+}
+
 // ------------------------------------------------------------ simple kernel --
 
 // Diagnostic stamp (diag builds only): global realtime clock (100 MHz) and
@@ -363,9 +535,9 @@ constexpr int kFeatHeavy = 2;     // tiered schedule: hand walks on after heavy_
 constexpr int kFeatPrio = 4;      // raise wave priority after prio_after visits
 constexpr int kFeatCoopTail = 8;  // finish the last coop_lanes walks of a wave cooperatively
 constexpr int kFeatExt = 16;      // non-reference extensions (option "extensions", kExt*)
+constexpr int kFeatFrontier = 32; // cooperative tail uses frontier_walk (option coop_walk = 1)
 
 constexpr int kStack = 8;                    // per-lane t_enter stack entries in LDS (walk 1)
-constexpr uint32_t kIdx = 0x7FFFFFFFu;
 constexpr int kPair = 0, kLeaf = 1, kNode = 2, kSkip = 3;   // walk 1: record kinds
 
 template <bool COUNT, bool DIAG = false, int FEAT = 0, int WALK = 1>
@@ -374,18 +546,20 @@ __global__ __launch_bounds__(256) void trace_simple(TraceArgs a) {
     const int wave = threadIdx.x >> 6;
     unsigned long long* drec = nullptr;
     if (DIAG) {
-        drec = a.diag + kDiagWords * (size_t)((blockIdx.y * gridDim.x + blockIdx.x) * 4 + wave);
+        drec = a.diag + kDiagWords * (size_t)((blockIdx.y * gridDim.x + blockIdx.x) * a.block_waves + wave);
         diag_stamp(drec, 0);
     }
     // walk 1: the right siblings still to visit, as (t_enter or +inf, R | L(R) << 31),
     // newest kStack per lane; older ones are dropped and found again by skip pointers.
     __shared__ uint2 stk[WALK == 1 ? kStack : 1][256];
+    // frontier_walk's per-wave frontier (cooperative tail)
+    __shared__ uint4 fr[(FEAT & kFeatFrontier) ? 4 * kFCap : 1];
     // One wave = one tile of 64 pixels, (8 << s) x (8 >> s) with s = a.wave_tile
     // (s = 0: 8x8, the reference's local_size 8x8x1, compute_dynamic_ray.comp:157);
-    // a 256-thread block = 4 such tiles side by side.
+    // a workgroup = block_waves (4 or 1) such tiles side by side.
     const int s = a.wave_tile;
     const int tw_w = 8 << s, th_w = 8 >> s;
-    const int lx = (blockIdx.x * 4 + wave) * tw_w + (lane & (tw_w - 1));
+    const int lx = (blockIdx.x * a.block_waves + wave) * tw_w + (lane & (tw_w - 1));
     const int ly = blockIdx.y * th_w + (lane >> (3 + s));
     const bool pixel = lx < a.tw && ly < a.th;
     const float4* __restrict__ nodes = a.scene.nodes;
@@ -451,16 +625,29 @@ __global__ __launch_bounds__(256) void trace_simple(TraceArgs a) {
             ++c_seg;
             if (end > 0) ++c_node;                                       // the root visit
         }
-        if (WALK == 0 && !(FEAT & kFeatHeavy)) {
+        if (WALK == 0) {
             // The per-node walk: one dependent load per visit, lanes in lockstep.
             while (walking) {
                 if (DIAG) ++d_iters;
+                if (FEAT & (kFeatPrio | kFeatHeavy)) ++steps;
                 // A wave still walking after prio_after steps holds the frame's
                 // critical path: let it win instruction arbitration.
-                if ((FEAT & kFeatPrio) && ++steps == a.prio_after) __builtin_amdgcn_s_setprio(3);
+                if ((FEAT & kFeatPrio) && steps == a.prio_after) __builtin_amdgcn_s_setprio(3);
                 n = node_step<COUNT>(nodes, leafs, n, nleaf, o, d, inv, closest, hit, c_node, c_tri);
                 walking = n < end;
+                if (FEAT & kFeatHeavy) walking = walking && steps < a.heavy_budget;
                 if ((FEAT & kFeatCoopTail) && __popcll(__ballot(walking)) <= a.coop_lanes) break;
+            }
+            if ((FEAT & kFeatHeavy) && alive && n < end && steps >= a.heavy_budget) {   // hand the walk on
+                HeavyRay* hv = a.heavy + atomicAdd(a.heavy_count, 1u);
+                hv->p.q0 = make_float4(o.x, o.y, o.z, att.x);
+                hv->p.q1 = make_float4(d.x, d.y, d.z, att.y);
+                hv->p.q2 = make_float4(att.z, __uint_as_float(seed), __int_as_float(b),
+                                       __int_as_float(lx | (ly << 16)));
+                hv->q3 = make_float4(closest, __int_as_float(n), __int_as_float(hit), 0.f);
+                alive = false;
+                handed_on = true;
+                walking = false;
             }
         } else for (;;) {
             if (WALK == 1 && walking) {
@@ -618,7 +805,16 @@ __global__ __launch_bounds__(256) void trace_simple(TraceArgs a) {
                 unsigned long long cn = 0, ct = 0;   // wave-uniform: counted once, by lane L
                 int start = n;
                 if (WALK == 1 && kind == kSkip && lane == L) start = (int)(__float_as_uint(nodes[2 * n].w) & kIdx);
-                const int nw = coop_walk<COUNT>(nodes, leafs, end, lane_i(start, L), bo, bd, bi, bc, bh, cn, ct);
+                int nw = 0;
+                if ((FEAT & kFeatFrontier) && a.coop_walk) {
+                    int p = lane_i(start, L);
+                    bool pl = false;
+                    if (!frontier_walk<COUNT>(nodes, leafs, pairs, end, p, pl, bo, bd, bi, bc, bh, cn, ct,
+                                              fr + wave * kFCap, nw))
+                        while (p < end) p = node_step<COUNT>(nodes, leafs, p, pl, bo, bd, bi, bc, bh, cn, ct);
+                } else {
+                    nw = coop_walk<COUNT>(nodes, leafs, end, lane_i(start, L), bo, bd, bi, bc, bh, cn, ct);
+                }
                 if (DIAG) d_windows += nw;
                 if (lane == L) {
                     closest = bc;
@@ -829,17 +1025,25 @@ __global__ __launch_bounds__(256) void trace_persistent(TraceArgs a) {
 // ------------------------------------------------------- cooperative kernel --
 // Tier 2 of the tiered schedule: one wave per suspended path, coop_walk for
 // the rest of its current segment and all later ones.
-template <bool COUNT>
+template <bool COUNT, bool FRONTIER>
 __global__ __launch_bounds__(256) void trace_coop(TraceArgs a) {
     const int lane = threadIdx.x & 63;
+    __shared__ uint4 fr[FRONTIER ? 4 * kFCap : 1];
+    uint4* F = fr + (threadIdx.x >> 6) * kFCap;
     const int end = a.scene.end;
     const int n_rays = (int)*a.heavy_count;
     unsigned long long c_seg = 0, c_node = 0, c_tri = 0, c_mat = 0;   // wave-uniform
+    __shared__ int claim[4];
     for (;;) {
-        int r = 0;
-        if (lane == 0) r = (int)atomicAdd(a.queue, 1u);
-        r = __builtin_amdgcn_readfirstlane(r);
+        // Claim the next path: lane 0's atomic, broadcast through LDS (a
+        // uniform value from the start, so no lane-divergent loop structure).
+        if (lane == 0) claim[threadIdx.x >> 6] = (int)atomicAdd(a.queue, 1u);
+        __builtin_amdgcn_wave_barrier();
+        const int r = __builtin_amdgcn_readfirstlane(claim[threadIdx.x >> 6]);
+        __builtin_amdgcn_wave_barrier();
         if (r >= n_rays) break;
+        unsigned long long t_start = 0, rounds = 0, segs = 0;
+        if (a.diag) t_start = wall_clock64();
         const HeavyRay hv = a.heavy[r];
         V3 o = {hv.p.q0.x, hv.p.q0.y, hv.p.q0.z};
         V3 d = {hv.p.q1.x, hv.p.q1.y, hv.p.q1.z};
@@ -853,7 +1057,20 @@ __global__ __launch_bounds__(256) void trace_coop(TraceArgs a) {
         V3 fin = {0.0f, 0.0f, 0.0f};
         for (;;) {
             const V3 inv = {1.0f / d.x, 1.0f / d.y, 1.0f / d.z};
-            coop_walk<COUNT>(a.scene.nodes, a.scene.leafs, end, node, o, d, inv, closest, hit, c_node, c_tri);
+            if (FRONTIER) {
+                bool pl = false;
+                int nr = 0;
+                if (!frontier_walk<COUNT>(a.scene.nodes, a.scene.leafs, a.scene.pairs, end, node, pl, o, d, inv,
+                                          closest, hit, c_node, c_tri, F, nr))
+                    while (node < end)
+                        node = node_step<COUNT>(a.scene.nodes, a.scene.leafs, node, pl, o, d, inv, closest, hit,
+                                                c_node, c_tri);
+                rounds += nr;
+            } else {
+                rounds += coop_walk<COUNT>(a.scene.nodes, a.scene.leafs, end, node, o, d, inv, closest, hit, c_node,
+                                           c_tri);
+            }
+            ++segs;
             if (hit < 0) {
                 fin = vmul(att, sky_color(d));
                 break;
@@ -877,6 +1094,13 @@ __global__ __launch_bounds__(256) void trace_coop(TraceArgs a) {
             }
         }
         if (lane == 0) write_pixel(a, pix & 0xFFFF, pix >> 16, fin);
+        if (a.diag && lane == 0) {
+            unsigned long long* rec = a.diag + 4 * (size_t)r;
+            rec[0] = t_start;
+            rec[1] = wall_clock64();
+            rec[2] = rounds;
+            rec[3] = segs | ((unsigned long long)__float_as_uint(hv.q3.y) << 32);
+        }
     }
     if (COUNT && lane == 0) {
         atomicAdd(&a.counters->segments, c_seg);
@@ -901,17 +1125,57 @@ hipError_t launch_trace(const TraceArgs& a, hipStream_t stream) {
         // tier 1: lockstep tiles; paths over the visit budget are suspended
         TraceArgs s = a;
         s.kernel = kKernelSimple;
+        s.coop_walk = 0;      // tier 1's own cooperative tail keeps the 64-node windows
         hipError_t e = hipMemsetAsync(a.heavy_count, 0, sizeof(unsigned), stream);
         if (e != hipSuccess) return e;
         e = launch_trace(s, stream);
         if (e != hipSuccess) return e;
+        if (std::getenv("RTAMD_DEBUG_TIER1_ONLY")) {   // debug: skip tier 2, check the suspended paths
+            (void)hipStreamSynchronize(stream);
+            unsigned n = 0;
+            (void)hipMemcpy(&n, a.heavy_count, sizeof(n), hipMemcpyDeviceToHost);
+            HeavyRay* h = new HeavyRay[n ? n : 1];
+            (void)hipMemcpy(h, a.heavy, n * sizeof(HeavyRay), hipMemcpyDeviceToHost);
+            unsigned bad = 0;
+            for (unsigned i = 0; i < n; ++i) {
+                int b, node, hit, pix;
+                std::memcpy(&b, &h[i].p.q2.z, 4);
+                std::memcpy(&node, &h[i].q3.y, 4);
+                std::memcpy(&hit, &h[i].q3.z, 4);
+                std::memcpy(&pix, &h[i].p.q2.w, 4);
+                const float cl = h[i].q3.x;
+                if (b < 0 || b >= a.max_bounces || node < 0 || node > a.scene.end || !(cl > 0.f && cl <= 10000.f)) {
+                    if (bad++ < 5)
+                        std::fprintf(stderr, "heavy %u: b %d node %d closest %g hit %d pix %x\n", i, b, node, cl,
+                                     hit, pix);
+                }
+            }
+            std::fprintf(stderr, "tier 1: %u suspended paths, %u malformed\n", n, bad);
+            delete[] h;
+            return hipGetLastError();
+        }
         // tier 2: one wave per suspended path
         e = hipMemsetAsync(a.queue, 0, sizeof(unsigned), stream);
         if (e != hipSuccess) return e;
-        if (a.counters)
-            hipLaunchKernelGGL(trace_coop<true>, dim3(a.grid_blocks), block, 0, stream, a);
-        else
-            hipLaunchKernelGGL(trace_coop<false>, dim3(a.grid_blocks), block, 0, stream, a);
+        // Always the counting build (into a sink when no stats are asked
+        // for): the non-counting build of trace_coop hangs on gfx950 with
+        // this compiler (a code-generation issue not yet isolated; the
+        // counting build is exact on every GPU parity test).
+        TraceArgs c = a;
+        if (!c.counters) c.counters = a.sink;
+        if (a.diag) {   // trace_coop's records follow tier 1's per-wave records
+            const int tw_w = 8 << a.wave_tile, th_w = 8 >> a.wave_tile;
+            c.diag = a.diag + (size_t)((a.tw + 4 * tw_w - 1) / (4 * tw_w)) * ((a.th + th_w - 1) / th_w) * 4 * 8;
+        }
+        static int bpc[2] = {0, 0};
+        auto k2 = a.coop_walk ? trace_coop<true, true> : trace_coop<true, false>;
+        int& nb = bpc[a.coop_walk ? 1 : 0];
+        if (nb == 0 && (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k2, 256, 0) != hipSuccess || nb < 1)) nb = 1;
+        int dev = 0, n_cu = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n_cu < 1)
+            n_cu = 256;
+        hipLaunchKernelGGL(k2, dim3(n_cu * nb), block, 0, stream, c);
         return hipGetLastError();
     }
     if (a.kernel == kKernelSplit) {
@@ -939,11 +1203,13 @@ hipError_t launch_trace(const TraceArgs& a, hipStream_t stream) {
         else
             hipLaunchKernelGGL(trace_persistent<false>, grid, block, 0, stream, a);
     } else {
-        const int tw_w = 8 << a.wave_tile, th_w = 8 >> a.wave_tile;
-        const dim3 grid((a.tw + 4 * tw_w - 1) / (4 * tw_w), (a.th + th_w - 1) / th_w);
+        const int tw_w = 8 << a.wave_tile, th_w = 8 >> a.wave_tile, bw = a.block_waves;
+        const dim3 grid((a.tw + bw * tw_w - 1) / (bw * tw_w), (a.th + th_w - 1) / th_w);
+        const dim3 block(64 * bw);
         const int feat = (a.seg_limit < (1 << 30) ? kFeatSpill : 0) |
                          (a.heavy_budget < (1 << 30) ? kFeatHeavy : 0) | (a.prio_after > 0 ? kFeatPrio : 0) |
-                         (a.coop_lanes > 0 ? kFeatCoopTail : 0) | (a.ext != 0 ? kFeatExt : 0);
+                         (a.coop_lanes > 0 ? kFeatCoopTail : 0) | (a.ext != 0 ? kFeatExt : 0) |
+                         (a.coop_lanes > 0 && a.coop_walk ? kFeatFrontier : 0);
 #define RT_SIMPLE(F, W)                                                                                        \
         if (a.diag) hipLaunchKernelGGL((trace_simple<false, true, F, W>), grid, block, 0, stream, a);           \
         else if (a.counters) hipLaunchKernelGGL((trace_simple<true, false, F, W>), grid, block, 0, stream, a); \
@@ -954,7 +1220,10 @@ hipError_t launch_trace(const TraceArgs& a, hipStream_t stream) {
                 case kFeatCoopTail: RT_SIMPLE(kFeatCoopTail, 0) break;
                 case kFeatCoopTail | kFeatPrio: RT_SIMPLE(kFeatCoopTail | kFeatPrio, 0) break;
                 case kFeatCoopTail | kFeatExt: RT_SIMPLE(kFeatCoopTail | kFeatExt, 0) break;
-                default: RT_SIMPLE(kFeatSpill | kFeatHeavy | kFeatPrio | kFeatCoopTail | kFeatExt, 0) break;
+                case kFeatCoopTail | kFeatFrontier: RT_SIMPLE(kFeatCoopTail | kFeatFrontier, 0) break;
+                case kFeatCoopTail | kFeatHeavy: RT_SIMPLE(kFeatCoopTail | kFeatHeavy, 0) break;
+                case kFeatHeavy: RT_SIMPLE(kFeatHeavy, 0) break;
+                default: RT_SIMPLE(kFeatSpill | kFeatHeavy | kFeatPrio | kFeatCoopTail | kFeatExt | kFeatFrontier, 0) break;
             }
         } else {
             switch (feat) {
@@ -962,7 +1231,7 @@ hipError_t launch_trace(const TraceArgs& a, hipStream_t stream) {
                 case kFeatCoopTail: RT_SIMPLE(kFeatCoopTail, 1) break;
                 case kFeatSpill: RT_SIMPLE(kFeatSpill, 1) break;
                 case kFeatHeavy: RT_SIMPLE(kFeatHeavy, 1) break;
-                default: RT_SIMPLE(kFeatSpill | kFeatHeavy | kFeatPrio | kFeatCoopTail | kFeatExt, 1) break;
+                default: RT_SIMPLE(kFeatSpill | kFeatHeavy | kFeatPrio | kFeatCoopTail | kFeatExt | kFeatFrontier, 1) break;
             }
         }
 #undef RT_SIMPLE

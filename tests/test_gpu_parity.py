@@ -15,7 +15,8 @@ pytestmark = pytest.mark.gpu
 
 COUNTERS = ("segments", "node_visits", "tri_tests", "mat_reads")
 DEFAULT_OPTS = {"kernel": 0, "shade_min": 16, "blocks_per_cu": 0, "wave_tile": 2, "seg_limit": 2,
-                "heavy_budget": 256, "prio_after": 0, "coop_lanes": 2, "walk": 0}
+                "heavy_budget": 256, "prio_after": 0, "coop_lanes": 2, "walk": 0, "coop_walk": 0,
+                "block_waves": 1}
 
 
 def _oracle(built, cam_bytes, w, h, b, **kw):
@@ -130,6 +131,14 @@ def test_config5_1m_row_subset(renderer):
     {"kernel": 0, "coop_lanes": 8},
     {"kernel": 0, "coop_lanes": 64},
     {"kernel": 0, "coop_lanes": 4, "wave_tile": 0, "prio_after": 64},
+    {"kernel": 0, "coop_walk": 1},
+    {"kernel": 0, "block_waves": 4},
+    {"kernel": 0, "block_waves": 1, "wave_tile": 0, "coop_lanes": 0},
+    {"kernel": 0, "coop_walk": 1, "coop_lanes": 8},
+    {"kernel": 0, "coop_walk": 1, "coop_lanes": 64},
+    {"kernel": 0, "coop_walk": 1, "coop_lanes": 64, "walk": 1},
+    {"kernel": 3, "coop_walk": 1, "heavy_budget": 1},
+    {"kernel": 3, "coop_walk": 1, "heavy_budget": 40},
 ])
 def test_schedules_identical(renderer, opts):
     """Every schedule gives the oracle's frame and counters (config 2 at the
@@ -333,7 +342,7 @@ def test_golden_frames_on_gpu(renderer):
 
 
 @pytest.mark.parametrize("shape,n", [("left", 50), ("right", 200), ("random", 300)])
-@pytest.mark.parametrize("walk", [0, 1])
+@pytest.mark.parametrize("walk", [0, 1, "frontier"])
 def test_unbalanced_bvh(renderer, shape, n, walk):
     from rtamd import configs
     built = raw_bvh_scene(n, shape, seed=n)
@@ -342,14 +351,19 @@ def test_unbalanced_bvh(renderer, shape, n, walk):
     if shape == "random":
         assert renderer.scene_info()["max_depth"] < 60     # the oracle's reference stack is 64 deep
     try:
-        renderer.set_option("walk", walk)
+        if walk == "frontier":          # every walk cooperative: frontier_walk from the root
+            renderer.set_option("coop_walk", 1)
+            renderer.set_option("coop_lanes", 64)
+        else:
+            renderer.set_option("walk", walk)
         for (w, h, b) in [(160, 96, 6), (33, 17, 10)]:
             cam = configs.Camera.default(w, h)
             rgba, rad, st = renderer.render(cam, w, h, b, radiance=True, stats=True)
             _assert_same(rgba, rad, st, *_oracle(built, cam.ubo_bytes(), w, h, b))
             assert st["tri_tests"] > 0
     finally:
-        renderer.set_option("walk", 0)
+        for k, v in DEFAULT_OPTS.items():
+            renderer.set_option(k, v)
 
 
 @pytest.mark.parametrize("ext,sky", [(1, 0), (2, 1), (3, 0)])

@@ -18,6 +18,7 @@ def main():
     ap.add_argument("--config", type=int, default=3)
     ap.add_argument("--bounces", type=int, default=0)
     ap.add_argument("--launches", type=int, default=3)
+    ap.add_argument("--nostats", action="store_true", help="launch the non-counting kernels")
     args = ap.parse_args()
     import torch
     import rtamd
@@ -34,7 +35,11 @@ def main():
     out = torch.empty((H, W, 4), dtype=torch.uint8, device="cuda:0")
     for i in range(args.launches):
         t0 = time.time()
-        st = r.render_tile_device(cam, W, H, B, 0, 0, W, H, out.data_ptr(), None, None, stats=True)
+        st = r.render_tile_device(cam, W, H, B, 0, 0, W, H, out.data_ptr(), None, None, stats=not args.nostats)
+        if args.nostats:
+            torch.cuda.synchronize()
+            print(f"{args.variant} launch {i}: {1e3 * (time.time() - t0):.2f} ms wall (no stats)", flush=True)
+            continue
         print(f"{args.variant} launch {i}: {1e3 * (time.time() - t0):.2f} ms wall, {st['ms']:.3f} ms events, "
               f"segments {st['segments']} visits {st['node_visits']} handoffs {st['handoffs']}", flush=True)
     r.close()
