@@ -159,12 +159,17 @@ int rt_render_wait(rt_ctx* ctx, uint64_t ticket);
  *                       every path, then the surviving paths, compacted, on
  *                       persistent waves,
  *                   3 = tiered: kernel 0 with a per-path visit budget; walks
- *                       over budget finish one wave per ray (64-node windows)
+ *                       over budget finish one wave per ray (cooperative walk)
  *   "walk"          kernel 0: 0 = one node per step (default), 1 = child-pair
  *                   records + per-lane stack of right-child entry distances
  *   "coop_lanes"    kernel 0: once at most this many lanes of a wave are still
  *                   walking, the whole wave finishes their walks one ray at a
  *                   time (0..64, default 2; 0 = off)
+ *   "coop_walk"     cooperative walks (coop tail, tiered second pass):
+ *                   0 = 64-node preorder windows (default), 1 = preorder
+ *                   frontier (up to 64 live subtrees expanded per round trip)
+ *   "block_waves"   kernel 0: waves per workgroup, 1 (default: a finished
+ *                   wave frees its slot at once) or 4
  *   "wave_tile"     kernel 0: pixels per wave (8<<s) x (8>>s), s = 0..3
  *                   (default 2: 32x2)
  *   "extensions"    NON-REFERENCE features, bits (default 0 = the reference's
@@ -188,6 +193,7 @@ int rt_render_wait(rt_ctx* ctx, uint64_t ticket);
  *                   the occupancy query)
  * Defaults can also be set with the environment variables
  * RTAMD_KERNEL=simple|persistent|split|tiered, RTAMD_WALK, RTAMD_COOP_LANES,
+ * RTAMD_COOP_WALK, RTAMD_BLOCK_WAVES,
  * RTAMD_SEG_LIMIT, RTAMD_SHADE_MIN and RTAMD_BLOCKS_PER_CU. */
 int rt_set_option(rt_ctx* ctx, const char* name, int64_t value);
 /* Diagnostics: with option "diag" = 1, kernel 0 records per wave
