@@ -239,7 +239,23 @@ struct PerDevice {
     hipEvent_t   traced[2] = {nullptr, nullptr}, copied[2] = {nullptr, nullptr};
     float*       d_accum = nullptr;  // extension kExtAccumulate: running sums
     size_t       accum_n = 0;        // floats
+    // option heavy_first: per-wave costs of a learning launch, and the tile
+    // orders (most expensive first) learned so far, one per launch key (a
+    // band partition rotates through several keys), oldest dropped first
+    unsigned*    d_tile_cost = nullptr;
+    size_t       cost_cap = 0;
+    struct Order { std::vector<uint8_t> key; int* d_order; size_t n; };
+    std::vector<Order> orders;
+    std::vector<uint8_t> learning_key;
+    size_t       learning_n = 0;
 };
+
+static constexpr size_t kMaxOrders = 16;
+
+static void free_orders(PerDevice& p) {
+    for (auto& o : p.orders) (void)hipFree(o.d_order);
+    p.orders.clear();
+}
 
 static constexpr unsigned kQueueSlots = 64;
 
@@ -258,6 +274,9 @@ struct rt_ctx {
     int  walk = 0;                 // kernel 0: 0 = node per step (fastest measured), 1 = child pairs + t_enter stack
     int  coop_walk = 0;            // cooperative walks: 0 = 64-node windows, 1 = preorder frontier
     int  block_waves = 1;          // kernel 0: waves per workgroup (1: a finished wave frees its slot at once; or 4)
+    int  heavy_first = 1;          // kernel 0: dispatch tiles in the cost order of a learning launch
+    int  prio_tiles = 0;           // heavy_first: raise the priority of the first this-many tiles
+    uint64_t scene_gen = 0;        // bumped by every scene upload (invalidates learned tile orders)
     bool has_scene = false;
     int  n_nodes = 0, n_tris = 0, max_depth = 0;
     uint64_t issued = 0;           // rt_render_async tickets handed out
@@ -274,6 +293,68 @@ static void free_scene(PerDevice& p) {
 
 // The extensions exist in kernel 0 only; with any of them on, kernel 0 runs.
 static int effective_kernel(const rt_ctx* ctx) { return ctx->ext ? kKernelSimple : ctx->kernel; }
+
+// Heavy-first dispatch (option heavy_first, kernel 0 with one-wave
+// workgroups): the first launch of a given frame geometry + camera + scene
+// records every wave's duration; the host sorts the tiles by it, most
+// expensive first, and later launches with the same key dispatch in that
+// order, so the waves that set the frame time start first.  Results do not
+// change (a tile's pixels and seeds are the same whichever workgroup traces
+// it); the learning launch ends with a stream synchronisation.
+static int plan_order(const rt_ctx* ctx, PerDevice& p, TraceArgs& a, const rt_camera_ubo* cam) {
+    a.tile_order = nullptr;
+    a.tile_cost = nullptr;
+    a.prio_tiles = ctx->prio_tiles;
+    if (!ctx->heavy_first || a.kernel != kKernelSimple || a.block_waves != 1 || a.diag) return RT_OK;
+    const int tw_w = 8 << a.wave_tile, th_w = 8 >> a.wave_tile;
+    const size_t n = (size_t)((a.tw + tw_w - 1) / tw_w) * (size_t)((a.th + th_w - 1) / th_w);
+    const int geo[] = {a.width, a.height, a.max_bounces, a.x0, a.y0, a.tw, a.th, a.band_h, a.band_stride,
+                       a.band_off, a.wave_tile, a.ext, a.coop_lanes, a.walk};
+    std::vector<uint8_t> key(sizeof(geo) + sizeof(rt_camera_ubo) + sizeof(uint64_t));
+    std::memcpy(key.data(), geo, sizeof(geo));
+    std::memcpy(key.data() + sizeof(geo), cam, sizeof(rt_camera_ubo));
+    std::memcpy(key.data() + sizeof(geo) + sizeof(rt_camera_ubo), &ctx->scene_gen, sizeof(uint64_t));
+    for (const auto& o : p.orders)
+        if (o.n == n && o.key == key) {
+            a.tile_order = o.d_order;
+            return RT_OK;
+        }
+    if (n > p.cost_cap) {
+        if (p.d_tile_cost) (void)hipFree(p.d_tile_cost);
+        p.d_tile_cost = nullptr;
+        p.cost_cap = 0;
+        RT_HIP_CHECK(hipMalloc(&p.d_tile_cost, n * sizeof(unsigned)));
+        p.cost_cap = n;
+    }
+    p.learning_key = key;
+    p.learning_n = n;
+    a.tile_cost = p.d_tile_cost;
+    return RT_OK;
+}
+
+static int learn_order(PerDevice& p, const TraceArgs& a, hipStream_t s) {
+    if (!a.tile_cost) return RT_OK;
+    const size_t n = p.learning_n;
+    RT_HIP_CHECK(hipStreamSynchronize(s));
+    std::vector<unsigned> cost(n);
+    RT_HIP_CHECK(hipMemcpy(cost.data(), p.d_tile_cost, n * sizeof(unsigned), hipMemcpyDeviceToHost));
+    std::vector<int> order(n);
+    for (size_t k = 0; k < n; ++k) order[k] = (int)k;
+    std::stable_sort(order.begin(), order.end(), [&](int x, int y) { return cost[x] > cost[y]; });
+    if (p.orders.size() >= kMaxOrders) {
+        (void)hipFree(p.orders.front().d_order);
+        p.orders.erase(p.orders.begin());
+    }
+    int* d = nullptr;
+    RT_HIP_CHECK(hipMalloc(&d, n * sizeof(int)));
+    const hipError_t e = hipMemcpy(d, order.data(), n * sizeof(int), hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+        (void)hipFree(d);
+        RT_HIP_CHECK(e);
+    }
+    p.orders.push_back({p.learning_key, d, n});
+    return RT_OK;
+}
 
 static int set_schedule(const rt_ctx* ctx, PerDevice& p, TraceArgs& a, const rt_camera_ubo* cam) {
     a.kernel = effective_kernel(ctx);
@@ -357,7 +438,7 @@ static int set_schedule(const rt_ctx* ctx, PerDevice& p, TraceArgs& a, const rt_
         }
         a.heavy = p.d_heavy;
     }
-    return RT_OK;
+    return plan_order(ctx, p, a, cam);
 }
 
 static CamF cam_from_ubo(const rt_camera_ubo* c) {
@@ -393,6 +474,7 @@ int rt_create(const int* device_ids, int n_devices, rt_ctx** out) {
                     : std::strcmp(k, "tiered") == 0 ? kKernelTiered : ctx->kernel;
     if (const char* v = std::getenv("RTAMD_WALK")) ctx->walk = std::atoi(v) ? 1 : 0;
     if (const char* v = std::getenv("RTAMD_COOP_WALK")) ctx->coop_walk = std::atoi(v) ? 1 : 0;
+    if (const char* v = std::getenv("RTAMD_HEAVY_FIRST")) ctx->heavy_first = std::atoi(v) ? 1 : 0;
     if (const char* v = std::getenv("RTAMD_BLOCK_WAVES")) ctx->block_waves = std::atoi(v) == 1 ? 1 : 4;
     if (const char* v = std::getenv("RTAMD_COOP_LANES")) ctx->coop_lanes = std::max(0, std::min(64, std::atoi(v)));
     if (const char* v = std::getenv("RTAMD_SEG_LIMIT")) ctx->seg_limit = std::max(1, std::min(1024, std::atoi(v)));
@@ -455,6 +537,8 @@ int rt_destroy(rt_ctx* ctx) {
         if (p.d_spill) (void)hipFree(p.d_spill);
         if (p.d_heavy) (void)hipFree(p.d_heavy);
         if (p.d_diag) (void)hipFree(p.d_diag);
+        if (p.d_tile_cost) (void)hipFree(p.d_tile_cost);
+        free_orders(p);
         if (p.d_accum) (void)hipFree(p.d_accum);
         if (p.d_rgba) (void)hipFree(p.d_rgba);
         if (p.d_rad) (void)hipFree(p.d_rad);
@@ -517,6 +601,7 @@ int rt_upload_scene(rt_ctx* ctx, const void* vertices, size_t vertex_bytes,
     ctx->n_tris = hs.n_tris;
     ctx->max_depth = hs.max_depth;
     ctx->has_scene = true;
+    ++ctx->scene_gen;
     free_host_scene(&hs);
     return RT_OK;
 }
@@ -590,6 +675,7 @@ int rt_render_tile_device(rt_ctx* ctx, const rt_camera_ubo* cam, int width, int 
     }
     if (stats) RT_HIP_CHECK(hipEventRecord(p.ev0, s));
     RT_HIP_CHECK(launch_trace(a, s));
+    if (int ro = learn_order(p, a, s)) return ro;
     if (stats) {
         RT_HIP_CHECK(hipEventRecord(p.ev1, s));
         RT_HIP_CHECK(hipEventSynchronize(p.ev1));
@@ -624,6 +710,7 @@ static int render_bands_on(const rt_ctx* ctx, PerDevice& p, const rt_camera_ubo*
     if (count) RT_HIP_CHECK(hipMemsetAsync(p.d_counters, 0, sizeof(Counters), s));
     RT_HIP_CHECK(hipEventRecord(p.ev0, s));
     RT_HIP_CHECK(launch_trace(a, s));
+    if (int ro = learn_order(p, a, s)) return ro;
     RT_HIP_CHECK(hipEventRecord(p.ev1, s));
     return RT_OK;
 }
@@ -848,6 +935,10 @@ int rt_set_option(rt_ctx* ctx, const char* name, int64_t value) {
         ctx->coop_walk = (int)value;
     } else if (std::strcmp(name, "block_waves") == 0 && (value == 1 || value == 4)) {
         ctx->block_waves = (int)value;
+    } else if (std::strcmp(name, "heavy_first") == 0 && (value == 0 || value == 1)) {
+        ctx->heavy_first = (int)value;
+    } else if (std::strcmp(name, "prio_tiles") == 0 && value >= 0 && value <= (1 << 30)) {
+        ctx->prio_tiles = (int)value;
     } else if (std::strcmp(name, "diag") == 0 && (value == 0 || value == 1)) {
         ctx->diag = (int)value;
     } else if (std::strcmp(name, "wave_tile") == 0 && value >= 0 && value <= 3) {
@@ -871,6 +962,8 @@ int rt_get_option(rt_ctx* ctx, const char* name, int64_t* value) {
     else if (std::strcmp(name, "walk") == 0) *value = ctx->walk;
     else if (std::strcmp(name, "coop_walk") == 0) *value = ctx->coop_walk;
     else if (std::strcmp(name, "block_waves") == 0) *value = ctx->block_waves;
+    else if (std::strcmp(name, "heavy_first") == 0) *value = ctx->heavy_first;
+    else if (std::strcmp(name, "prio_tiles") == 0) *value = ctx->prio_tiles;
     else if (std::strcmp(name, "extensions") == 0) *value = ctx->ext;
     else if (std::strcmp(name, "blocks_per_cu") == 0)
         *value = ctx->blocks_per_cu > 0 ? ctx->blocks_per_cu : (ctx->dev.empty() ? 0 : ctx->dev[0].blocks_per_cu);

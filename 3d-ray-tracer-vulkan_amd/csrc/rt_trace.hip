@@ -269,6 +269,21 @@ __device__ __forceinline__ int lanes_below(uint64_t mask) {
 
 
 __device__ __forceinline__ int lane_i(int v, int k) { return __builtin_amdgcn_readlane(v, k); }
+
+// Bits [0, n) of a wave mask (n in 0..64).
+__device__ __forceinline__ uint64_t lanes_lt(int n) { return n >= 64 ? ~0ull : ((1ull << n) - 1ull); }
+
+// Exclusive prefix max over the wave's lanes (lane 0 gets -1): DPP row
+// shifts, row broadcasts, then a one-lane wave shift.
+__device__ __forceinline__ int wave_excl_max(int v) {
+    v = max(v, __builtin_amdgcn_update_dpp(-1, v, 0x111, 0xf, 0xf, false));   // row_shr:1
+    v = max(v, __builtin_amdgcn_update_dpp(-1, v, 0x112, 0xf, 0xf, false));   // row_shr:2
+    v = max(v, __builtin_amdgcn_update_dpp(-1, v, 0x114, 0xf, 0xf, false));   // row_shr:4
+    v = max(v, __builtin_amdgcn_update_dpp(-1, v, 0x118, 0xf, 0xf, false));   // row_shr:8
+    v = max(v, __builtin_amdgcn_update_dpp(-1, v, 0x142, 0xa, 0xf, false));   // row_bcast:15
+    v = max(v, __builtin_amdgcn_update_dpp(-1, v, 0x143, 0xc, 0xf, false));   // row_bcast:31
+    return __builtin_amdgcn_update_dpp(-1, v, 0x138, 0xf, 0xf, false);        // wave_shr:1
+}
 __device__ __forceinline__ float lane_f(float v, int k) {
     return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), k));
 }
@@ -374,6 +389,7 @@ __device__ __forceinline__ int coop_walk(const float4* __restrict__ nodes, const
 // reference's next node, to be finished by node_step.
 constexpr uint32_t kIdx = 0x7FFFFFFFu;      // node index bits of a link word
 constexpr int kFCap = 256;                   // frontier entries per wave (16 B each)
+constexpr int kFReserve = 80;                // slots speculation leaves to the front (> 64-deep descent)
 constexpr uint32_t kUnres = 0xFFFFFFFFu;
 
 template <bool COUNT>
@@ -391,7 +407,7 @@ __device__ __forceinline__ bool frontier_walk(const float4* __restrict__ nodes, 
     for (int guard = 0; guard < (1 << 24); ++guard) {
         if (top == 0) {
             if (c >= end) break;
-            ++rounds;
+            rounds += 1 << 16;                                   // chain rounds counted apart (diag)
             const float4 A = nodes[2 * c];
             const float4 B = nodes[2 * c + 1];
             float te;
@@ -416,54 +432,54 @@ __device__ __forceinline__ bool frontier_walk(const float4* __restrict__ nodes, 
         const bool unres = in && e.w == kUnres;
         const float te = __uint_as_float(e.z);
         const float tt = __uint_as_float(e.w);
-        // 1. replay
-        const uint64_t U = __ballot(unres);
-        const uint64_t Lm = __ballot(in && lf);
-        uint64_t H = __ballot(in && te < closest);
-        uint64_t T = __ballot(in && lf && !unres && tt < closest);
-        uint64_t Dm = __ballot(in && node < drop);
-        int k = 0;
-        while (k < nl) {
-            const uint64_t bit = 1ull << k;
-            if (Dm & bit) {                                      // inside a missed subtree
-                ++k;
-                continue;
+        // 1. replay, vectorised: between two improving hits closest_t is
+        // fixed, so every loaded entry's outcome is a lane-local compare; an
+        // expanded internal node whose box misses drops the entries of its
+        // subtree (node < its skip: a prefix max over the lanes before it).
+        // One pass per improving triangle hit.
+        bool miss_int = false;       // expanded internal node whose box missed when finalized
+        int base = 0, k, cover;
+        for (;;) {
+            const bool act = in && lane >= base;
+            const bool h = te < closest;
+            if (act) miss_int = !unres && !lf && !h;
+            cover = wave_excl_max(miss_int ? (int)e.y : -1);
+            const bool live = act && node >= max(drop, cover);
+            const uint64_t stop = __ballot(live && unres && h);
+            const int sidx = stop ? __ffsll((long long)stop) - 1 : nl;
+            const uint64_t tm = __ballot(live && lf && !unres && h && tt < closest) & lanes_lt(sidx);
+            const int f = tm ? __ffsll((long long)tm) - 1 : sidx;
+            if (COUNT) {
+                const uint64_t r = lanes_lt(f);
+                c_node += 2ull * (unsigned long long)__popcll(__ballot(live && !unres && !lf && h) & r);
+                c_tri += (unsigned long long)__popcll(__ballot(live && lf && !unres && h) & r);
             }
-            if (!(H & bit)) {                                    // box misses at this closest_t
-                if (!(Lm & bit) && !(U & bit)) {                 // its live children follow: skip them
-                    drop = lane_i((int)e.y, k);
-                    Dm = __ballot(in && node < drop);
-                }
-                ++k;
-                continue;
+            if (!tm) {
+                k = sidx;
+                if (k == nl) drop = max(drop, lane_i(max(cover, miss_int ? (int)e.y : -1), nl - 1));
+                break;
             }
-            if (U & bit) break;                                  // hit, not expanded yet
-            if (Lm & bit) {
-                if (COUNT) ++c_tri;
-                if (T & bit) {
-                    closest = lane_f(tt, k);
-                    hit = lane_i((int)e.y, k);
-                    H = __ballot(in && te < closest);
-                    T = __ballot(in && lf && !unres && tt < closest);
-                }
-            } else if (COUNT) {
-                c_node += 2;
-            }
-            ++k;
+            if (COUNT) ++c_tri;                                  // the improving triangle
+            closest = lane_f(tt, f);
+            hit = lane_i((int)e.y, f);
+            base = f + 1;
         }
         top -= k;
         if (k == nl) continue;
         ++rounds;
         // 2. expand (lanes k.. are the region [top - (nl - k), top) of F)
         const int room = kFCap - top;
-        const bool cand = in && lane >= k && unres && node >= drop && te < closest;
+        const bool cand = in && lane >= k && unres && node >= max(drop, cover) && te < closest;
         const uint64_t CI = __ballot(cand && !lf);
         if (room < 2 && ((CI >> k) & 1ull)) {                    // no room for the front's children
             pos = lane_i(node, k);
             pos_leaf = false;
             return false;
         }
-        const bool sel = cand && (lf || 2 * (lanes_below(CI) + 1) <= room);
+        // The front always fits (room >= 2); other internal nodes only while
+        // kFReserve slots stay free for the front's own descent, so the walk
+        // cannot stall on a frontier filled by speculation.
+        const bool sel = cand && (lf || lane == k || 2 * (lanes_below(CI) + 1) <= room - kFReserve);
         bool hL = false, hR = false;
         uint4 cL = e, cR = e;
         if (sel) {
@@ -559,8 +575,21 @@ __global__ __launch_bounds__(256) void trace_simple(TraceArgs a) {
     // a workgroup = block_waves (4 or 1) such tiles side by side.
     const int s = a.wave_tile;
     const int tw_w = 8 << s, th_w = 8 >> s;
-    const int lx = (blockIdx.x * a.block_waves + wave) * tw_w + (lane & (tw_w - 1));
-    const int ly = blockIdx.y * th_w + (lane >> (3 + s));
+    // Heavy-first order (option heavy_first): workgroup k takes the k-th most
+    // expensive tile of an earlier launch of the same frame, so the frame's
+    // longest waves start first.  Only the tile each wave traces changes.
+    int bx = blockIdx.x, by = blockIdx.y;
+    if (a.tile_order) {
+        const int k = blockIdx.y * gridDim.x + blockIdx.x;
+        const int t = a.tile_order[k];
+        bx = t % (int)gridDim.x;
+        by = t / (int)gridDim.x;
+        if (k < a.prio_tiles) __builtin_amdgcn_s_setprio(2);   // the frame's longest waves
+    }
+    unsigned long long t_wave0 = 0;
+    if (a.tile_cost) t_wave0 = wall_clock64();
+    const int lx = (bx * a.block_waves + wave) * tw_w + (lane & (tw_w - 1));
+    const int ly = by * th_w + (lane >> (3 + s));
     const bool pixel = lx < a.tw && ly < a.th;
     const float4* __restrict__ nodes = a.scene.nodes;
     const float4* __restrict__ leafs = a.scene.leafs;
@@ -868,6 +897,8 @@ __global__ __launch_bounds__(256) void trace_simple(TraceArgs a) {
         fin = {sum.x / nf, sum.y / nf, sum.z / nf};
     }
     if (pixel && !handed_on) write_pixel(a, lx, ly, fin);
+    if (a.tile_cost && lane == 0)
+        a.tile_cost[(by * (int)gridDim.x + bx) * a.block_waves + wave] = (unsigned)(wall_clock64() - t_wave0);
     if (COUNT) flush_counters(a.counters, c_seg, c_node, c_tri, c_mat);
     if (DIAG) {
         diag_stamp(drec, 1);
@@ -1042,7 +1073,7 @@ __global__ __launch_bounds__(256) void trace_coop(TraceArgs a) {
         const int r = __builtin_amdgcn_readfirstlane(claim[threadIdx.x >> 6]);
         __builtin_amdgcn_wave_barrier();
         if (r >= n_rays) break;
-        unsigned long long t_start = 0, rounds = 0, segs = 0;
+        unsigned long long t_start = 0, rounds = 0, segs = 0, fallbacks = 0, t_walk = 0, t_first = 0, r_first = 0;
         if (a.diag) t_start = wall_clock64();
         const HeavyRay hv = a.heavy[r];
         V3 o = {hv.p.q0.x, hv.p.q0.y, hv.p.q0.z};
@@ -1057,11 +1088,12 @@ __global__ __launch_bounds__(256) void trace_coop(TraceArgs a) {
         V3 fin = {0.0f, 0.0f, 0.0f};
         for (;;) {
             const V3 inv = {1.0f / d.x, 1.0f / d.y, 1.0f / d.z};
+            const unsigned long long tw0 = a.diag ? wall_clock64() : 0;
             if (FRONTIER) {
                 bool pl = false;
                 int nr = 0;
                 if (!frontier_walk<COUNT>(a.scene.nodes, a.scene.leafs, a.scene.pairs, end, node, pl, o, d, inv,
-                                          closest, hit, c_node, c_tri, F, nr))
+                                          closest, hit, c_node, c_tri, F, nr) && ++fallbacks)
                     while (node < end)
                         node = node_step<COUNT>(a.scene.nodes, a.scene.leafs, node, pl, o, d, inv, closest, hit,
                                                 c_node, c_tri);
@@ -1071,6 +1103,11 @@ __global__ __launch_bounds__(256) void trace_coop(TraceArgs a) {
                                            c_tri);
             }
             ++segs;
+            if (a.diag) {
+                const unsigned long long tw = wall_clock64() - tw0;
+                t_walk += tw;
+                if (segs == 1) { t_first = tw; r_first = rounds; }
+            }
             if (hit < 0) {
                 fin = vmul(att, sky_color(d));
                 break;
@@ -1098,8 +1135,8 @@ __global__ __launch_bounds__(256) void trace_coop(TraceArgs a) {
             unsigned long long* rec = a.diag + 4 * (size_t)r;
             rec[0] = t_start;
             rec[1] = wall_clock64();
-            rec[2] = rounds;
-            rec[3] = segs | ((unsigned long long)__float_as_uint(hv.q3.y) << 32);
+            rec[2] = rounds | (t_walk << 32);
+            rec[3] = segs | (fallbacks << 16) | ((r_first & 0xFFFFF) << 32) | ((t_first & 0xFFF) << 52);
         }
     }
     if (COUNT && lane == 0) {

@@ -16,7 +16,7 @@ pytestmark = pytest.mark.gpu
 COUNTERS = ("segments", "node_visits", "tri_tests", "mat_reads")
 DEFAULT_OPTS = {"kernel": 0, "shade_min": 16, "blocks_per_cu": 0, "wave_tile": 2, "seg_limit": 2,
                 "heavy_budget": 256, "prio_after": 0, "coop_lanes": 2, "walk": 0, "coop_walk": 0,
-                "block_waves": 1}
+                "block_waves": 1, "heavy_first": 1, "prio_tiles": 0}
 
 
 def _oracle(built, cam_bytes, w, h, b, **kw):
@@ -133,6 +133,7 @@ def test_config5_1m_row_subset(renderer):
     {"kernel": 0, "coop_lanes": 4, "wave_tile": 0, "prio_after": 64},
     {"kernel": 0, "coop_walk": 1},
     {"kernel": 0, "block_waves": 4},
+    {"kernel": 0, "heavy_first": 0},
     {"kernel": 0, "block_waves": 1, "wave_tile": 0, "coop_lanes": 0},
     {"kernel": 0, "coop_walk": 1, "coop_lanes": 8},
     {"kernel": 0, "coop_walk": 1, "coop_lanes": 64},
@@ -158,6 +159,26 @@ def test_schedules_identical(renderer, opts):
         ref = _oracle(built, cam.ubo_bytes(), cfg.width, cfg.height, cfg.max_bounces,
                       tile=(0, 1, cfg.width, cfg.height - 1), row_step=6)
         _assert_same(rgba, rad, st, *ref)
+    finally:
+        for k, v in DEFAULT_OPTS.items():
+            renderer.set_option(k, v)
+
+
+def test_heavy_first_order(renderer):
+    """heavy_first: the learning launch and the launches in the learned
+    order give the oracle's frame and counters; a new camera relearns."""
+    from rtamd import configs
+    try:
+        renderer.set_option("heavy_first", 1)
+        cfg = configs.config3()
+        built = cfg.build()
+        renderer.upload_scene(built)
+        for cam in (cfg.camera(), configs.Camera.default(cfg.width, cfg.height + 7)):
+            ref = _oracle(built, cam.ubo_bytes(), cfg.width, cfg.height, cfg.max_bounces,
+                          tile=(0, 2, cfg.width, cfg.height - 2), row_step=9)
+            for _ in range(3):          # learn, then twice in the learned order
+                rgba, rad, st = _bands_device(renderer, cam, cfg.width, cfg.height, cfg.max_bounces, 1, 9, 2)
+                _assert_same(rgba, rad, st, *ref)
     finally:
         for k, v in DEFAULT_OPTS.items():
             renderer.set_option(k, v)

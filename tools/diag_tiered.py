@@ -53,8 +53,24 @@ def main():
     nr = int(st["handoffs"])
     p = buf[waves * 8: waves * 8 + 4 * nr].reshape(-1, 4).astype(np.int64)
     dur = (p[:, 1] - p[:, 0]) / 100.0
-    rounds = p[:, 2]
-    segs = p[:, 3] & 0xFFFFFFFF
+    chain = (p[:, 2] >> 16) & 0xFFFF
+    rounds = (p[:, 2] & 0xFFFF) + chain
+    print(f"  chain rounds: p50 {np.percentile(chain, 50):.0f} max {chain.max()}; "
+          f"expansion rounds p50 {np.percentile(rounds - chain, 50):.0f}")
+    walk = (p[:, 2] >> 32) / 100.0
+    print(f"  time in walks: {walk.sum() / dur.sum():.3f} of path time")
+    segs = p[:, 3] & 0xFFFF
+    fb = (p[:, 3] >> 16) & 0xFFFF
+    r1 = (p[:, 3] >> 32) & 0xFFFFF
+    r1 = (r1 >> 16) + (r1 & 0xFFFF)
+    t1 = ((p[:, 3] >> 52) & 0xFFF) / 100.0
+    walk_all = (p[:, 2] >> 32) / 100.0
+    rall = ((p[:, 2] >> 16) & 0xFFFF) + (p[:, 2] & 0xFFFF)
+    later = segs_ = (p[:, 3] & 0xFFFF) > 1
+    print(f"  first walk: {np.median(t1 / np.maximum(r1, 1)):.2f} us/round (p50 rounds {np.median(r1):.0f}); "
+          f"later walks: {np.median((walk_all - t1)[later] / np.maximum(rall - r1, 1)[later]) if later.any() else 0:.2f} us/round "
+          f"over {int(later.sum())} paths")
+    print(f"  frontier overflows (node_step fallbacks): {int(fb.sum())} in {int((fb > 0).sum())} paths")
     print(f"tier 2: {nr} paths, first start {(p[:, 0].min() - t0) / 100:.1f} us, last end {(p[:, 1].max() - t0) / 100:.1f} us")
     for name, a in (("duration us", dur), ("rounds", rounds), ("segments", segs)):
         print(f"  {name}: p50 {np.percentile(a, 50):.1f} p90 {np.percentile(a, 90):.1f} "
