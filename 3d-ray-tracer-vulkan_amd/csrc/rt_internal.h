@@ -141,7 +141,6 @@ struct TraceArgs {
     int      block_waves;       // simple: waves per workgroup, 4 (256 threads) or 1 (64 threads)
     const int* tile_order;      // simple, block_waves 1: workgroup k traces wave tile tile_order[k] (or k)
     unsigned* tile_cost;        // simple: each wave stores its duration (100 MHz ticks) here, or null
-    int      prio_tiles;        // simple, with tile_order: the first prio_tiles workgroups run at raised priority
     Counters* sink;             // tiered: counters trace_coop adds into when counters is null
     int      coop_walk;         // cooperative walks (coop tail, trace_coop): 0 = 64-node preorder
                                 //   windows (coop_walk), 1 = preorder frontier (frontier_walk)

@@ -275,7 +275,6 @@ struct rt_ctx {
     int  coop_walk = 0;            // cooperative walks: 0 = 64-node windows, 1 = preorder frontier
     int  block_waves = 1;          // kernel 0: waves per workgroup (1: a finished wave frees its slot at once; or 4)
     int  heavy_first = 1;          // kernel 0: dispatch tiles in the cost order of a learning launch
-    int  prio_tiles = 0;           // heavy_first: raise the priority of the first this-many tiles
     uint64_t scene_gen = 0;        // bumped by every scene upload (invalidates learned tile orders)
     bool has_scene = false;
     int  n_nodes = 0, n_tris = 0, max_depth = 0;
@@ -304,8 +303,7 @@ static int effective_kernel(const rt_ctx* ctx) { return ctx->ext ? kKernelSimple
 static int plan_order(const rt_ctx* ctx, PerDevice& p, TraceArgs& a, const rt_camera_ubo* cam) {
     a.tile_order = nullptr;
     a.tile_cost = nullptr;
-    a.prio_tiles = ctx->prio_tiles;
-    if (!ctx->heavy_first || a.kernel != kKernelSimple || a.block_waves != 1 || a.diag) return RT_OK;
+    if (!ctx->heavy_first || a.kernel != kKernelSimple || a.block_waves != 1) return RT_OK;
     const int tw_w = 8 << a.wave_tile, th_w = 8 >> a.wave_tile;
     const size_t n = (size_t)((a.tw + tw_w - 1) / tw_w) * (size_t)((a.th + th_w - 1) / th_w);
     const int geo[] = {a.width, a.height, a.max_bounces, a.x0, a.y0, a.tw, a.th, a.band_h, a.band_stride,
@@ -319,6 +317,7 @@ static int plan_order(const rt_ctx* ctx, PerDevice& p, TraceArgs& a, const rt_ca
             a.tile_order = o.d_order;
             return RT_OK;
         }
+    if (a.diag) return RT_OK;          // diagnostic launches use a learned order but do not learn one
     if (n > p.cost_cap) {
         if (p.d_tile_cost) (void)hipFree(p.d_tile_cost);
         p.d_tile_cost = nullptr;
@@ -937,8 +936,6 @@ int rt_set_option(rt_ctx* ctx, const char* name, int64_t value) {
         ctx->block_waves = (int)value;
     } else if (std::strcmp(name, "heavy_first") == 0 && (value == 0 || value == 1)) {
         ctx->heavy_first = (int)value;
-    } else if (std::strcmp(name, "prio_tiles") == 0 && value >= 0 && value <= (1 << 30)) {
-        ctx->prio_tiles = (int)value;
     } else if (std::strcmp(name, "diag") == 0 && (value == 0 || value == 1)) {
         ctx->diag = (int)value;
     } else if (std::strcmp(name, "wave_tile") == 0 && value >= 0 && value <= 3) {
@@ -963,7 +960,6 @@ int rt_get_option(rt_ctx* ctx, const char* name, int64_t* value) {
     else if (std::strcmp(name, "coop_walk") == 0) *value = ctx->coop_walk;
     else if (std::strcmp(name, "block_waves") == 0) *value = ctx->block_waves;
     else if (std::strcmp(name, "heavy_first") == 0) *value = ctx->heavy_first;
-    else if (std::strcmp(name, "prio_tiles") == 0) *value = ctx->prio_tiles;
     else if (std::strcmp(name, "extensions") == 0) *value = ctx->ext;
     else if (std::strcmp(name, "blocks_per_cu") == 0)
         *value = ctx->blocks_per_cu > 0 ? ctx->blocks_per_cu : (ctx->dev.empty() ? 0 : ctx->dev[0].blocks_per_cu);

@@ -580,11 +580,9 @@ __global__ __launch_bounds__(256) void trace_simple(TraceArgs a) {
     // longest waves start first.  Only the tile each wave traces changes.
     int bx = blockIdx.x, by = blockIdx.y;
     if (a.tile_order) {
-        const int k = blockIdx.y * gridDim.x + blockIdx.x;
-        const int t = a.tile_order[k];
+        const int t = a.tile_order[blockIdx.y * gridDim.x + blockIdx.x];
         bx = t % (int)gridDim.x;
         by = t / (int)gridDim.x;
-        if (k < a.prio_tiles) __builtin_amdgcn_s_setprio(2);   // the frame's longest waves
     }
     unsigned long long t_wave0 = 0;
     if (a.tile_cost) t_wave0 = wall_clock64();

@@ -170,6 +170,11 @@ int rt_render_wait(rt_ctx* ctx, uint64_t ticket);
  *                   frontier (up to 64 live subtrees expanded per round trip)
  *   "block_waves"   kernel 0: waves per workgroup, 1 (default: a finished
  *                   wave frees its slot at once) or 4
+ *   "heavy_first"   kernel 0 with block_waves 1: 1 (default) = the first
+ *                   launch of a frame geometry + camera + scene records every
+ *                   wave's duration (and ends with a stream synchronisation);
+ *                   later launches with the same key dispatch the tiles most
+ *                   expensive first (up to 16 keys per device are kept)
  *   "wave_tile"     kernel 0: pixels per wave (8<<s) x (8>>s), s = 0..3
  *                   (default 2: 32x2)
  *   "extensions"    NON-REFERENCE features, bits (default 0 = the reference's
@@ -193,7 +198,7 @@ int rt_render_wait(rt_ctx* ctx, uint64_t ticket);
  *                   the occupancy query)
  * Defaults can also be set with the environment variables
  * RTAMD_KERNEL=simple|persistent|split|tiered, RTAMD_WALK, RTAMD_COOP_LANES,
- * RTAMD_COOP_WALK, RTAMD_BLOCK_WAVES,
+ * RTAMD_COOP_WALK, RTAMD_BLOCK_WAVES, RTAMD_HEAVY_FIRST,
  * RTAMD_SEG_LIMIT, RTAMD_SHADE_MIN and RTAMD_BLOCKS_PER_CU. */
 int rt_set_option(rt_ctx* ctx, const char* name, int64_t value);
 /* Diagnostics: with option "diag" = 1, kernel 0 records per wave
