@@ -271,7 +271,8 @@ struct rt_ctx {
     int  heavy_budget = 256;       // tiered: node visits per path in tier 1
     int  coop_lanes = 2;           // kernel 0: cooperative tail once <= this many lanes walk (0 = off)
     int  ext = 0;                  // non-reference extensions (kExt* bits), off by default
-    int  walk = 0;                 // kernel 0: 0 = node per step (fastest measured), 1 = child pairs + t_enter stack
+    int  walk = 2;                 // kernel 0: 0 = node per step, 1 = child pairs + t_enter stack,
+                                   //   2 = node per step, software-pipelined (fastest measured)
     int  coop_walk = 0;            // cooperative walks: 0 = 64-node windows, 1 = preorder frontier
     int  block_waves = 1;          // kernel 0: waves per workgroup (1: a finished wave frees its slot at once; or 4)
     int  heavy_first = 1;          // kernel 0: dispatch tiles in the cost order of a learning launch
@@ -471,7 +472,7 @@ int rt_create(const int* device_ids, int n_devices, rt_ctx** out) {
                     : std::strcmp(k, "persistent") == 0 ? kKernelPersistent
                     : std::strcmp(k, "split") == 0 ? kKernelSplit
                     : std::strcmp(k, "tiered") == 0 ? kKernelTiered : ctx->kernel;
-    if (const char* v = std::getenv("RTAMD_WALK")) ctx->walk = std::atoi(v) ? 1 : 0;
+    if (const char* v = std::getenv("RTAMD_WALK")) ctx->walk = std::max(0, std::min(2, std::atoi(v)));
     if (const char* v = std::getenv("RTAMD_COOP_WALK")) ctx->coop_walk = std::atoi(v) ? 1 : 0;
     if (const char* v = std::getenv("RTAMD_HEAVY_FIRST")) ctx->heavy_first = std::atoi(v) ? 1 : 0;
     if (const char* v = std::getenv("RTAMD_BLOCK_WAVES")) ctx->block_waves = std::atoi(v) == 1 ? 1 : 4;
@@ -928,7 +929,7 @@ int rt_set_option(rt_ctx* ctx, const char* name, int64_t value) {
         ctx->coop_lanes = (int)value;
     } else if (std::strcmp(name, "extensions") == 0 && value >= 0 && value <= 7) {
         ctx->ext = (int)value;
-    } else if (std::strcmp(name, "walk") == 0 && (value == 0 || value == 1)) {
+    } else if (std::strcmp(name, "walk") == 0 && value >= 0 && value <= 2) {
         ctx->walk = (int)value;
     } else if (std::strcmp(name, "coop_walk") == 0 && (value == 0 || value == 1)) {
         ctx->coop_walk = (int)value;

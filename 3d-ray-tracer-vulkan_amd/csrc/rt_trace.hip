@@ -652,15 +652,56 @@ __global__ __launch_bounds__(256) void trace_simple(TraceArgs a) {
             ++c_seg;
             if (end > 0) ++c_node;                                       // the root visit
         }
-        if (WALK == 0) {
+        if (WALK == 0 || WALK == 2) {
             // The per-node walk: one dependent load per visit, lanes in lockstep.
+            // walk 2, software-pipelined: the next node's box is requested as soon as
+            // this node's slab test has chosen it, before this node's triangle
+            // test and the loop control, which then overlap the load.
+            float4 A, B, P0, P1, P2;
+            if (WALK == 2 && walking) {
+                A = nodes[2 * n];
+                B = nodes[2 * n + 1];
+                if (nleaf) {
+                    P0 = leafs[3 * n + 0];
+                    P1 = leafs[3 * n + 1];
+                    P2 = leafs[3 * n + 2];
+                }
+            }
             while (walking) {
                 if (DIAG) ++d_iters;
                 if (FEAT & (kFeatPrio | kFeatHeavy)) ++steps;
                 // A wave still walking after prio_after steps holds the frame's
                 // critical path: let it win instruction arbitration.
                 if ((FEAT & kFeatPrio) && steps == a.prio_after) __builtin_amdgcn_s_setprio(3);
-                n = node_step<COUNT>(nodes, leafs, n, nleaf, o, d, inv, closest, hit, c_node, c_tri);
+                if (WALK == 0) {
+                    n = node_step<COUNT>(nodes, leafs, n, nleaf, o, d, inv, closest, hit, c_node, c_tri);
+                } else {
+                    float te;
+                    bool ind;
+                    slab(A, B, o, inv, te, ind);
+                    const bool hb = ind && te < closest;
+                    const uint32_t aw = __float_as_uint(A.w), bw = __float_as_uint(B.w);
+                    const int nxt = hb ? n + 1 : (int)(aw & kIdx);            // a leaf's skip is n+1
+                    const bool nl = ((hb ? bw : (aw >> 31)) & 1u) != 0u;           // one select, no branch
+                    if (COUNT && hb && !nleaf) c_node += 2;
+                    A = nodes[2 * nxt];                                      // index end is padding
+                    B = nodes[2 * nxt + 1];
+                    if (hb && nleaf) {                                       // hit_triangle (:196-200)
+                        if (COUNT) ++c_tri;
+                        float t;
+                        if (tri_test(P0, P1, P2, o, d, t) && t < closest) {
+                            closest = t;
+                            hit = __float_as_int(P0.w);
+                        }
+                    }
+                    if (nl && nxt < end) {
+                        P0 = leafs[3 * nxt + 0];
+                        P1 = leafs[3 * nxt + 1];
+                        P2 = leafs[3 * nxt + 2];
+                    }
+                    n = nxt;
+                    nleaf = nl;
+                }
                 walking = n < end;
                 if (FEAT & kFeatHeavy) walking = walking && steps < a.heavy_budget;
                 if ((FEAT & kFeatCoopTail) && __popcll(__ballot(walking)) <= a.coop_lanes) break;
@@ -1249,7 +1290,13 @@ hipError_t launch_trace(const TraceArgs& a, hipStream_t stream) {
         if (a.diag) hipLaunchKernelGGL((trace_simple<false, true, F, W>), grid, block, 0, stream, a);           \
         else if (a.counters) hipLaunchKernelGGL((trace_simple<true, false, F, W>), grid, block, 0, stream, a); \
         else hipLaunchKernelGGL((trace_simple<false, false, F, W>), grid, block, 0, stream, a);
-        if (a.walk == 0) {
+        if (a.walk == 2) {
+            switch (feat) {
+                case kFeatCoopTail: RT_SIMPLE(kFeatCoopTail, 2) break;
+                case 0: RT_SIMPLE(0, 2) break;
+                default: RT_SIMPLE(kFeatSpill | kFeatHeavy | kFeatPrio | kFeatCoopTail | kFeatExt | kFeatFrontier, 2) break;
+            }
+        } else if (a.walk == 0) {
             switch (feat) {
                 case 0: RT_SIMPLE(0, 0) break;
                 case kFeatCoopTail: RT_SIMPLE(kFeatCoopTail, 0) break;

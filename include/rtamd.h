@@ -160,8 +160,11 @@ int rt_render_wait(rt_ctx* ctx, uint64_t ticket);
  *                       persistent waves,
  *                   3 = tiered: kernel 0 with a per-path visit budget; walks
  *                       over budget finish one wave per ray (cooperative walk)
- *   "walk"          kernel 0: 0 = one node per step (default), 1 = child-pair
- *                   records + per-lane stack of right-child entry distances
+ *   "walk"          kernel 0: 0 = one node per step, 1 = child-pair
+ *                   records + per-lane stack of right-child entry distances,
+ *                   2 = one node per step, software-pipelined: the next
+ *                   node's box is requested before this node's triangle test
+ *                   and the loop control (default)
  *   "coop_lanes"    kernel 0: once at most this many lanes of a wave are still
  *                   walking, the whole wave finishes their walks one ray at a
  *                   time (0..64, default 2; 0 = off)

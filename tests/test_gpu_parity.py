@@ -15,7 +15,7 @@ pytestmark = pytest.mark.gpu
 
 COUNTERS = ("segments", "node_visits", "tri_tests", "mat_reads")
 DEFAULT_OPTS = {"kernel": 0, "shade_min": 16, "blocks_per_cu": 0, "wave_tile": 2, "seg_limit": 2,
-                "heavy_budget": 256, "prio_after": 0, "coop_lanes": 2, "walk": 0, "coop_walk": 0,
+                "heavy_budget": 256, "prio_after": 0, "coop_lanes": 2, "walk": 2, "coop_walk": 0,
                 "block_waves": 1, "heavy_first": 1}
 
 
@@ -134,6 +134,8 @@ def test_config5_1m_row_subset(renderer):
     {"kernel": 0, "coop_walk": 1},
     {"kernel": 0, "block_waves": 4},
     {"kernel": 0, "heavy_first": 0},
+    {"kernel": 0, "walk": 0},
+    {"kernel": 0, "walk": 0, "coop_lanes": 8},
     {"kernel": 0, "block_waves": 1, "wave_tile": 0, "coop_lanes": 0},
     {"kernel": 0, "coop_walk": 1, "coop_lanes": 8},
     {"kernel": 0, "coop_walk": 1, "coop_lanes": 64},
@@ -363,7 +365,7 @@ def test_golden_frames_on_gpu(renderer):
 
 
 @pytest.mark.parametrize("shape,n", [("left", 50), ("right", 200), ("random", 300)])
-@pytest.mark.parametrize("walk", [0, 1, "frontier"])
+@pytest.mark.parametrize("walk", [0, 1, 2, "frontier"])
 def test_unbalanced_bvh(renderer, shape, n, walk):
     from rtamd import configs
     built = raw_bvh_scene(n, shape, seed=n)
