@@ -140,7 +140,13 @@ struct TraceArgs {
                                 //   1 = child pairs + per-lane stack of t_enter (pairs)
     int      block_waves;       // simple: waves per workgroup, 4 (256 threads) or 1 (64 threads)
     const int* tile_order;      // simple, block_waves 1: workgroup k traces wave tile tile_order[k] (or k)
-    unsigned* tile_cost;        // simple: each wave stores its duration (100 MHz ticks) here, or null
+    int      tiles_x;           // simple, with tile_order (1-D grid): wave tiles per tile row
+    int      split_n;           // simple, with tile_order: the first split_n tiles of the order are traced
+                                //   one pixel per wave (64 workgroups each; launcher-internal)
+    int      heavy_tiles;       // simple, with tile_order: the first heavy_tiles tiles run in that split
+                                //   mode as a concurrent launch on aux_stream (fork ev_fork, join ev_join)
+    hipStream_t aux_stream;
+    hipEvent_t ev_fork, ev_join;
     Counters* sink;             // tiered: counters trace_coop adds into when counters is null
     int      coop_walk;         // cooperative walks (coop tail, trace_coop): 0 = 64-node preorder
                                 //   windows (coop_walk), 1 = preorder frontier (frontier_walk)

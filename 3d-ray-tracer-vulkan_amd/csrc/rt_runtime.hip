@@ -242,15 +242,23 @@ struct PerDevice {
     // option heavy_first: per-wave costs of a learning launch, and the tile
     // orders (most expensive first) learned so far, one per launch key (a
     // band partition rotates through several keys), oldest dropped first
-    unsigned*    d_tile_cost = nullptr;
-    size_t       cost_cap = 0;
-    struct Order { std::vector<uint8_t> key; int* d_order; size_t n; };
+    unsigned long long* d_learn = nullptr;   // per-wave diag records of the learning launch
+    size_t       learn_cap = 0;
+    struct Order { std::vector<uint8_t> key; int* d_order; size_t n; int heavy; };
+    // option heavy_tiles: auxiliary streams (round robin) for the concurrent heavy-tile launch
+    hipStream_t  aux[4] = {nullptr, nullptr, nullptr, nullptr};
+    hipEvent_t   aux_fork[4] = {nullptr, nullptr, nullptr, nullptr}, aux_join[4] = {nullptr, nullptr, nullptr, nullptr};
+    unsigned     aux_next = 0;
     std::vector<Order> orders;
     std::vector<uint8_t> learning_key;
     size_t       learning_n = 0;
 };
 
 static constexpr size_t kMaxOrders = 16;
+static constexpr int    kResidentPerCu = 24;    // resident trace waves per CU (diag timelines)
+static constexpr double kHeavyFactor = 1.5;     // a tile this much longer than the bulk is split
+static constexpr int    kMaxHeavy = 256;
+static constexpr size_t kDiagWords = 8;   // per-wave diag record (rt_trace.hip, rtamd.h rt_diag_copy)
 
 static void free_orders(PerDevice& p) {
     for (auto& o : p.orders) (void)hipFree(o.d_order);
@@ -276,6 +284,12 @@ struct rt_ctx {
     int  coop_walk = 0;            // cooperative walks: 0 = 64-node windows, 1 = preorder frontier
     int  block_waves = 1;          // kernel 0: waves per workgroup (1: a finished wave frees its slot at once; or 4)
     int  heavy_first = 1;          // kernel 0: dispatch tiles in the cost order of a learning launch
+    int  learn_cost = 1;           // heavy_first cost: 0 = lockstep steps + 2 x coop windows, 1 = wave duration
+    int  heavy_stream = 1;         // heavy_tiles: 1 = their launch runs on an auxiliary stream, concurrent
+                                   //   with the other tiles; 0 = before them on the same stream
+    int  heavy_tiles = -1;         // heavy_first: the this-many most expensive tiles are traced one pixel
+                                   //   per wave, walked cooperatively, in a separate launch
+                                   //   (-1 = automatic: the tiles that outlast the bulk, learn_order)
     uint64_t scene_gen = 0;        // bumped by every scene upload (invalidates learned tile orders)
     bool has_scene = false;
     int  n_nodes = 0, n_tris = 0, max_depth = 0;
@@ -303,12 +317,16 @@ static int effective_kernel(const rt_ctx* ctx) { return ctx->ext ? kKernelSimple
 // it); the learning launch ends with a stream synchronisation.
 static int plan_order(const rt_ctx* ctx, PerDevice& p, TraceArgs& a, const rt_camera_ubo* cam) {
     a.tile_order = nullptr;
-    a.tile_cost = nullptr;
+    a.tiles_x = 0;
+    a.split_n = 0;
+    a.heavy_tiles = 0;
+    a.aux_stream = nullptr;
+    a.ev_fork = a.ev_join = nullptr;
     if (!ctx->heavy_first || a.kernel != kKernelSimple || a.block_waves != 1) return RT_OK;
     const int tw_w = 8 << a.wave_tile, th_w = 8 >> a.wave_tile;
     const size_t n = (size_t)((a.tw + tw_w - 1) / tw_w) * (size_t)((a.th + th_w - 1) / th_w);
     const int geo[] = {a.width, a.height, a.max_bounces, a.x0, a.y0, a.tw, a.th, a.band_h, a.band_stride,
-                       a.band_off, a.wave_tile, a.ext, a.coop_lanes, a.walk};
+                       a.band_off, a.wave_tile, a.ext, a.coop_lanes, a.walk, ctx->learn_cost};
     std::vector<uint8_t> key(sizeof(geo) + sizeof(rt_camera_ubo) + sizeof(uint64_t));
     std::memcpy(key.data(), geo, sizeof(geo));
     std::memcpy(key.data() + sizeof(geo), cam, sizeof(rt_camera_ubo));
@@ -316,31 +334,70 @@ static int plan_order(const rt_ctx* ctx, PerDevice& p, TraceArgs& a, const rt_ca
     for (const auto& o : p.orders)
         if (o.n == n && o.key == key) {
             a.tile_order = o.d_order;
+            const int heavy = ctx->heavy_tiles >= 0 ? ctx->heavy_tiles : o.heavy;
+            if (heavy > 0 && n > 1) {
+                const unsigned k = p.aux_next++ % 4;
+                if (!p.aux[k]) {
+                    RT_HIP_CHECK(hipStreamCreateWithFlags(&p.aux[k], hipStreamNonBlocking));
+                    RT_HIP_CHECK(hipEventCreateWithFlags(&p.aux_fork[k], hipEventDisableTiming));
+                    RT_HIP_CHECK(hipEventCreateWithFlags(&p.aux_join[k], hipEventDisableTiming));
+                }
+                a.heavy_tiles = heavy;
+                a.aux_stream = ctx->heavy_stream ? p.aux[k] : nullptr;
+                a.ev_fork = p.aux_fork[k];
+                a.ev_join = p.aux_join[k];
+                if (a.diag)   // one record per workgroup of both launches
+                    p.diag_used = (n + 63 * (size_t)std::min(a.heavy_tiles, (int)n - 1)) * 8;
+            }
             return RT_OK;
         }
-    if (a.diag) return RT_OK;          // diagnostic launches use a learned order but do not learn one
-    if (n > p.cost_cap) {
-        if (p.d_tile_cost) (void)hipFree(p.d_tile_cost);
-        p.d_tile_cost = nullptr;
-        p.cost_cap = 0;
-        RT_HIP_CHECK(hipMalloc(&p.d_tile_cost, n * sizeof(unsigned)));
-        p.cost_cap = n;
+    // Learn on a plain launch: a diagnostic launch keeps its own records, and a
+    // counting launch (stats) runs the counting build, not the diagnostic one.
+    if (a.diag || a.counters) return RT_OK;
+    if (n * kDiagWords > p.learn_cap) {
+        if (p.d_learn) (void)hipFree(p.d_learn);
+        p.d_learn = nullptr;
+        p.learn_cap = 0;
+        RT_HIP_CHECK(hipMalloc(&p.d_learn, n * kDiagWords * sizeof(unsigned long long)));
+        p.learn_cap = n * kDiagWords;
     }
     p.learning_key = key;
     p.learning_n = n;
-    a.tile_cost = p.d_tile_cost;
+    a.diag = p.d_learn;                // the diagnostic build counts each wave's lockstep steps
     return RT_OK;
 }
 
-static int learn_order(PerDevice& p, const TraceArgs& a, hipStream_t s) {
-    if (!a.tile_cost) return RT_OK;
+// A tile's cost is its wave's lockstep walk iterations plus twice its
+// cooperative windows (diag record words 4 and 5): the length of the wave's
+// dependent chain, free of when the wave happened to run.
+static int learn_order(PerDevice& p, const TraceArgs& a, hipStream_t s, int learn_cost) {
+    if (!a.diag || a.diag != p.d_learn) return RT_OK;
     const size_t n = p.learning_n;
     RT_HIP_CHECK(hipStreamSynchronize(s));
-    std::vector<unsigned> cost(n);
-    RT_HIP_CHECK(hipMemcpy(cost.data(), p.d_tile_cost, n * sizeof(unsigned), hipMemcpyDeviceToHost));
+    std::vector<unsigned long long> rec(n * kDiagWords);
+    RT_HIP_CHECK(hipMemcpy(rec.data(), p.d_learn, rec.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+    std::vector<unsigned long long> cost(n);
+    for (size_t k = 0; k < n; ++k) {
+        const unsigned long long* r = &rec[k * kDiagWords];
+        cost[k] = learn_cost == 0 ? r[4] + 2 * r[5] : r[1] - r[0];
+    }
     std::vector<int> order(n);
     for (size_t k = 0; k < n; ++k) order[k] = (int)k;
     std::stable_sort(order.begin(), order.end(), [&](int x, int y) { return cost[x] > cost[y]; });
+    // Automatic heavy tiles: those whose cost exceeds kHeavyFactor times the
+    // bulk estimate, the total cost spread over the device's resident waves
+    // (kResidentPerCu per CU, measured).  A 1080p frame of config 3 gets a few
+    // dozen; a frame whose time is its throughput (config 5) gets none.
+    double total = 0.0;
+    for (size_t k = 0; k < n; ++k) total += (double)cost[k];
+    const double bulk = total / (double)std::max(1, p.n_cu * kResidentPerCu);
+    int heavy = 0;
+    while ((size_t)heavy < n - 1 && heavy < kMaxHeavy && (double)cost[order[heavy]] > kHeavyFactor * bulk) ++heavy;
+    if (std::getenv("RTAMD_DEBUG_ORDER")) {
+        std::fprintf(stderr, "learn_order: %zu tiles, bulk estimate %.0f, %d heavy; first:", n, bulk, heavy);
+        for (size_t k = 0; k < 6 && k < n; ++k) std::fprintf(stderr, " %d(%llu)", order[k], cost[order[k]]);
+        std::fprintf(stderr, "\n");
+    }
     if (p.orders.size() >= kMaxOrders) {
         (void)hipFree(p.orders.front().d_order);
         p.orders.erase(p.orders.begin());
@@ -352,7 +409,7 @@ static int learn_order(PerDevice& p, const TraceArgs& a, hipStream_t s) {
         (void)hipFree(d);
         RT_HIP_CHECK(e);
     }
-    p.orders.push_back({p.learning_key, d, n});
+    p.orders.push_back({p.learning_key, d, n, heavy});
     return RT_OK;
 }
 
@@ -400,7 +457,8 @@ static int set_schedule(const rt_ctx* ctx, PerDevice& p, TraceArgs& a, const rt_
         // simple: 8 words per wave; tiered adds 4 words per suspended path (trace_coop)
         const int tw_w = 8 << a.wave_tile, th_w = 8 >> a.wave_tile;
         const size_t waves = (size_t)((a.tw + 4 * tw_w - 1) / (4 * tw_w)) * ((a.th + th_w - 1) / th_w) * 4;
-        const size_t words = waves * 8 + (a.kernel == kKernelTiered ? (size_t)a.tw * a.th * 4 : 0);
+        const size_t split = ctx->heavy_first ? (size_t)(ctx->heavy_tiles < 0 ? kMaxHeavy : ctx->heavy_tiles) * 63 : 0;
+        const size_t words = (waves + split) * 8 + (a.kernel == kKernelTiered ? (size_t)a.tw * a.th * 4 : 0);
         if (words > p.diag_cap) {
             if (p.d_diag) (void)hipFree(p.d_diag);
             p.d_diag = nullptr;
@@ -475,6 +533,8 @@ int rt_create(const int* device_ids, int n_devices, rt_ctx** out) {
     if (const char* v = std::getenv("RTAMD_WALK")) ctx->walk = std::max(0, std::min(2, std::atoi(v)));
     if (const char* v = std::getenv("RTAMD_COOP_WALK")) ctx->coop_walk = std::atoi(v) ? 1 : 0;
     if (const char* v = std::getenv("RTAMD_HEAVY_FIRST")) ctx->heavy_first = std::atoi(v) ? 1 : 0;
+    if (const char* v = std::getenv("RTAMD_HEAVY_TILES")) ctx->heavy_tiles = std::max(-1, std::atoi(v));
+    if (const char* v = std::getenv("RTAMD_HEAVY_STREAM")) ctx->heavy_stream = std::atoi(v) ? 1 : 0;
     if (const char* v = std::getenv("RTAMD_BLOCK_WAVES")) ctx->block_waves = std::atoi(v) == 1 ? 1 : 4;
     if (const char* v = std::getenv("RTAMD_COOP_LANES")) ctx->coop_lanes = std::max(0, std::min(64, std::atoi(v)));
     if (const char* v = std::getenv("RTAMD_SEG_LIMIT")) ctx->seg_limit = std::max(1, std::min(1024, std::atoi(v)));
@@ -537,8 +597,13 @@ int rt_destroy(rt_ctx* ctx) {
         if (p.d_spill) (void)hipFree(p.d_spill);
         if (p.d_heavy) (void)hipFree(p.d_heavy);
         if (p.d_diag) (void)hipFree(p.d_diag);
-        if (p.d_tile_cost) (void)hipFree(p.d_tile_cost);
+        if (p.d_learn) (void)hipFree(p.d_learn);
         free_orders(p);
+        for (int k = 0; k < 4; ++k) {
+            if (p.aux[k]) (void)hipStreamDestroy(p.aux[k]);
+            if (p.aux_fork[k]) (void)hipEventDestroy(p.aux_fork[k]);
+            if (p.aux_join[k]) (void)hipEventDestroy(p.aux_join[k]);
+        }
         if (p.d_accum) (void)hipFree(p.d_accum);
         if (p.d_rgba) (void)hipFree(p.d_rgba);
         if (p.d_rad) (void)hipFree(p.d_rad);
@@ -675,7 +740,7 @@ int rt_render_tile_device(rt_ctx* ctx, const rt_camera_ubo* cam, int width, int 
     }
     if (stats) RT_HIP_CHECK(hipEventRecord(p.ev0, s));
     RT_HIP_CHECK(launch_trace(a, s));
-    if (int ro = learn_order(p, a, s)) return ro;
+    if (int ro = learn_order(p, a, s, ctx->learn_cost)) return ro;
     if (stats) {
         RT_HIP_CHECK(hipEventRecord(p.ev1, s));
         RT_HIP_CHECK(hipEventSynchronize(p.ev1));
@@ -710,7 +775,7 @@ static int render_bands_on(const rt_ctx* ctx, PerDevice& p, const rt_camera_ubo*
     if (count) RT_HIP_CHECK(hipMemsetAsync(p.d_counters, 0, sizeof(Counters), s));
     RT_HIP_CHECK(hipEventRecord(p.ev0, s));
     RT_HIP_CHECK(launch_trace(a, s));
-    if (int ro = learn_order(p, a, s)) return ro;
+    if (int ro = learn_order(p, a, s, ctx->learn_cost)) return ro;
     RT_HIP_CHECK(hipEventRecord(p.ev1, s));
     return RT_OK;
 }
@@ -937,6 +1002,12 @@ int rt_set_option(rt_ctx* ctx, const char* name, int64_t value) {
         ctx->block_waves = (int)value;
     } else if (std::strcmp(name, "heavy_first") == 0 && (value == 0 || value == 1)) {
         ctx->heavy_first = (int)value;
+    } else if (std::strcmp(name, "heavy_tiles") == 0 && value >= -1 && value <= (1 << 20)) {
+        ctx->heavy_tiles = (int)value;
+    } else if (std::strcmp(name, "learn_cost") == 0 && (value == 0 || value == 1)) {
+        ctx->learn_cost = (int)value;
+    } else if (std::strcmp(name, "heavy_stream") == 0 && (value == 0 || value == 1)) {
+        ctx->heavy_stream = (int)value;
     } else if (std::strcmp(name, "diag") == 0 && (value == 0 || value == 1)) {
         ctx->diag = (int)value;
     } else if (std::strcmp(name, "wave_tile") == 0 && value >= 0 && value <= 3) {
@@ -961,6 +1032,9 @@ int rt_get_option(rt_ctx* ctx, const char* name, int64_t* value) {
     else if (std::strcmp(name, "coop_walk") == 0) *value = ctx->coop_walk;
     else if (std::strcmp(name, "block_waves") == 0) *value = ctx->block_waves;
     else if (std::strcmp(name, "heavy_first") == 0) *value = ctx->heavy_first;
+    else if (std::strcmp(name, "heavy_tiles") == 0) *value = ctx->heavy_tiles;
+    else if (std::strcmp(name, "heavy_stream") == 0) *value = ctx->heavy_stream;
+    else if (std::strcmp(name, "learn_cost") == 0) *value = ctx->learn_cost;
     else if (std::strcmp(name, "extensions") == 0) *value = ctx->ext;
     else if (std::strcmp(name, "blocks_per_cu") == 0)
         *value = ctx->blocks_per_cu > 0 ? ctx->blocks_per_cu : (ctx->dev.empty() ? 0 : ctx->dev[0].blocks_per_cu);

@@ -26,6 +26,7 @@
 //                     shade_min lanes are ready.
 //   split / tiered    trace_simple for the first part of every path, then the
 //                     rest on trace_persistent (resume) or trace_coop.
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -569,7 +570,9 @@ __global__ __launch_bounds__(256) void trace_simple(TraceArgs a) {
     // newest kStack per lane; older ones are dropped and found again by skip pointers.
     __shared__ uint2 stk[WALK == 1 ? kStack : 1][256];
     // frontier_walk's per-wave frontier (cooperative tail)
-    __shared__ uint4 fr[(FEAT & kFeatFrontier) ? 4 * kFCap : 1];
+    // frontier_walk's per-wave frontiers (kFCap entries per wave; dynamic LDS,
+    // sized by the launch for variants with kFeatFrontier)
+    extern __shared__ uint4 fr[];
     // One wave = one tile of 64 pixels, (8 << s) x (8 >> s) with s = a.wave_tile
     // (s = 0: 8x8, the reference's local_size 8x8x1, compute_dynamic_ray.comp:157);
     // a workgroup = block_waves (4 or 1) such tiles side by side.
@@ -578,17 +581,27 @@ __global__ __launch_bounds__(256) void trace_simple(TraceArgs a) {
     // Heavy-first order (option heavy_first): workgroup k takes the k-th most
     // expensive tile of an earlier launch of the same frame, so the frame's
     // longest waves start first.  Only the tile each wave traces changes.
-    int bx = blockIdx.x, by = blockIdx.y;
-    if (a.tile_order) {
-        const int t = a.tile_order[blockIdx.y * gridDim.x + blockIdx.x];
-        bx = t % (int)gridDim.x;
-        by = t / (int)gridDim.x;
+    // With split_n > 0 (the heavy-tile launch) the first split_n tiles of the
+    // order are traced one pixel per wave (64 workgroups per tile): the wave's
+    // single live lane walks every segment cooperatively (frontier walk).
+    int bx = blockIdx.x, by = blockIdx.y, sub = -1;
+    if (a.tile_order) {                                  // 1-D grid over the ordered tiles
+        const int k = blockIdx.x;
+        int t;
+        if (k < 64 * a.split_n) {
+            t = a.tile_order[k >> 6];
+            sub = k & 63;
+        } else {
+            t = a.tile_order[k - 63 * a.split_n];
+        }
+        bx = t % a.tiles_x;
+        by = t / a.tiles_x;
     }
-    unsigned long long t_wave0 = 0;
-    if (a.tile_cost) t_wave0 = wall_clock64();
-    const int lx = (bx * a.block_waves + wave) * tw_w + (lane & (tw_w - 1));
-    const int ly = by * th_w + (lane >> (3 + s));
-    const bool pixel = lx < a.tw && ly < a.th;
+    const int tl = sub >= 0 ? sub : lane;                // the tile pixel this lane traces
+    const int lx = (bx * a.block_waves + wave) * tw_w + (tl & (tw_w - 1));
+    const int ly = by * th_w + (tl >> (3 + s));
+    const bool pixel = lx < a.tw && ly < a.th && (sub < 0 || lane == 0);
+    const int coop_lanes = sub >= 0 ? 64 : a.coop_lanes;
     const float4* __restrict__ nodes = a.scene.nodes;
     const float4* __restrict__ leafs = a.scene.leafs;
     const float4* __restrict__ pairs = a.scene.pairs;
@@ -704,7 +717,7 @@ __global__ __launch_bounds__(256) void trace_simple(TraceArgs a) {
                 }
                 walking = n < end;
                 if (FEAT & kFeatHeavy) walking = walking && steps < a.heavy_budget;
-                if ((FEAT & kFeatCoopTail) && __popcll(__ballot(walking)) <= a.coop_lanes) break;
+                if ((FEAT & kFeatCoopTail) && __popcll(__ballot(walking)) <= coop_lanes) break;
             }
             if ((FEAT & kFeatHeavy) && alive && n < end && steps >= a.heavy_budget) {   // hand the walk on
                 HeavyRay* hv = a.heavy + atomicAdd(a.heavy_count, 1u);
@@ -761,7 +774,7 @@ __global__ __launch_bounds__(256) void trace_simple(TraceArgs a) {
             }
             const uint64_t wm = __ballot(walking);
             if (wm == 0) break;
-            if ((FEAT & kFeatCoopTail) && __popcll(wm) <= a.coop_lanes) break;
+            if ((FEAT & kFeatCoopTail) && __popcll(wm) <= coop_lanes) break;
             if (!walking) continue;
             if (FEAT & (kFeatPrio | kFeatHeavy)) ++steps;
             // A wave still walking after prio_after steps holds the frame's
@@ -936,8 +949,6 @@ __global__ __launch_bounds__(256) void trace_simple(TraceArgs a) {
         fin = {sum.x / nf, sum.y / nf, sum.z / nf};
     }
     if (pixel && !handed_on) write_pixel(a, lx, ly, fin);
-    if (a.tile_cost && lane == 0)
-        a.tile_cost[(by * (int)gridDim.x + bx) * a.block_waves + wave] = (unsigned)(wall_clock64() - t_wave0);
     if (COUNT) flush_counters(a.counters, c_seg, c_node, c_tri, c_mat);
     if (DIAG) {
         diag_stamp(drec, 1);
@@ -1280,16 +1291,55 @@ hipError_t launch_trace(const TraceArgs& a, hipStream_t stream) {
             hipLaunchKernelGGL(trace_persistent<false>, grid, block, 0, stream, a);
     } else {
         const int tw_w = 8 << a.wave_tile, th_w = 8 >> a.wave_tile, bw = a.block_waves;
-        const dim3 grid((a.tw + bw * tw_w - 1) / (bw * tw_w), (a.th + th_w - 1) / th_w);
+        dim3 grid((a.tw + bw * tw_w - 1) / (bw * tw_w), (a.th + th_w - 1) / th_w);
         const dim3 block(64 * bw);
         const int feat = (a.seg_limit < (1 << 30) ? kFeatSpill : 0) |
                          (a.heavy_budget < (1 << 30) ? kFeatHeavy : 0) | (a.prio_after > 0 ? kFeatPrio : 0) |
                          (a.coop_lanes > 0 ? kFeatCoopTail : 0) | (a.ext != 0 ? kFeatExt : 0) |
                          (a.coop_lanes > 0 && a.coop_walk ? kFeatFrontier : 0);
-#define RT_SIMPLE(F, W)                                                                                        \
-        if (a.diag) hipLaunchKernelGGL((trace_simple<false, true, F, W>), grid, block, 0, stream, a);           \
-        else if (a.counters) hipLaunchKernelGGL((trace_simple<true, false, F, W>), grid, block, 0, stream, a); \
-        else hipLaunchKernelGGL((trace_simple<false, false, F, W>), grid, block, 0, stream, a);
+        TraceArgs ao = a;
+        bool join = false;
+        if (a.tile_order) {             // heavy-first: a 1-D grid over the ordered tiles
+            ao.tiles_x = (int)grid.x;
+            ao.split_n = 0;
+            const int n_tiles = (int)(grid.x * grid.y);
+            const int H = std::min(a.heavy_tiles, n_tiles - 1);
+            if (H > 0 && a.ev_fork && bw == 1 && (feat & ~kFeatFrontier) == kFeatCoopTail) {
+                // The H most expensive tiles, one pixel per wave, every segment
+                // walked cooperatively with the frontier walk, on an auxiliary
+                // stream concurrent with the other tiles' launch.
+                const hipStream_t hs = a.aux_stream ? a.aux_stream : stream;   // null: same stream, in sequence
+                hipError_t e = hipSuccess;
+                if (a.aux_stream) {
+                    e = hipEventRecord(a.ev_fork, stream);
+                    if (e == hipSuccess) e = hipStreamWaitEvent(a.aux_stream, a.ev_fork, 0);
+                    if (e != hipSuccess) return e;
+                }
+                TraceArgs ah = ao;
+                ah.split_n = H;
+                ah.coop_walk = 1;
+                const dim3 gh(64 * H);
+                const size_t shm = kFCap * sizeof(uint4);
+                constexpr int FH = kFeatCoopTail | kFeatFrontier;
+                if (a.diag) hipLaunchKernelGGL((trace_simple<false, true, FH, 2>), gh, block, shm, hs, ah);
+                else if (a.counters) hipLaunchKernelGGL((trace_simple<true, false, FH, 2>), gh, block, shm, hs, ah);
+                else hipLaunchKernelGGL((trace_simple<false, false, FH, 2>), gh, block, shm, hs, ah);
+                e = hipGetLastError();
+                if (e == hipSuccess && a.aux_stream) e = hipEventRecord(a.ev_join, a.aux_stream);
+                if (e != hipSuccess) return e;
+                ao.tile_order = a.tile_order + H;
+                if (a.diag) ao.diag = a.diag + (size_t)kDiagWords * gh.x;
+                grid = dim3(n_tiles - H);
+                join = a.aux_stream != nullptr;
+            } else {
+                grid = dim3(n_tiles);
+            }
+        }
+        const size_t shm_f = (size_t)bw * kFCap * sizeof(uint4);   // kFeatFrontier variants only
+#define RT_SIMPLE(F, W)                                                                                         \
+        if (a.diag) hipLaunchKernelGGL((trace_simple<false, true, F, W>), grid, block, ((F) & kFeatFrontier) ? shm_f : 0, stream, ao);           \
+        else if (a.counters) hipLaunchKernelGGL((trace_simple<true, false, F, W>), grid, block, ((F) & kFeatFrontier) ? shm_f : 0, stream, ao); \
+        else hipLaunchKernelGGL((trace_simple<false, false, F, W>), grid, block, ((F) & kFeatFrontier) ? shm_f : 0, stream, ao);
         if (a.walk == 2) {
             switch (feat) {
                 case kFeatCoopTail: RT_SIMPLE(kFeatCoopTail, 2) break;
@@ -1317,6 +1367,11 @@ hipError_t launch_trace(const TraceArgs& a, hipStream_t stream) {
             }
         }
 #undef RT_SIMPLE
+        if (join) {
+            hipError_t e = hipGetLastError();
+            if (e == hipSuccess) e = hipStreamWaitEvent(stream, a.ev_join, 0);
+            return e;
+        }
     }
     return hipGetLastError();
 }

@@ -16,7 +16,8 @@ pytestmark = pytest.mark.gpu
 COUNTERS = ("segments", "node_visits", "tri_tests", "mat_reads")
 DEFAULT_OPTS = {"kernel": 0, "shade_min": 16, "blocks_per_cu": 0, "wave_tile": 2, "seg_limit": 2,
                 "heavy_budget": 256, "prio_after": 0, "coop_lanes": 2, "walk": 2, "coop_walk": 0,
-                "block_waves": 1, "heavy_first": 1}
+                "block_waves": 1, "heavy_first": 1, "heavy_tiles": -1, "heavy_stream": 1,
+                "learn_cost": 1}
 
 
 def _oracle(built, cam_bytes, w, h, b, **kw):
@@ -63,7 +64,7 @@ def test_config2_reference_bounces(renderer):
     _assert_same(rgba, rad, st, *_oracle(built, cam.ubo_bytes(), cfg.width, cfg.height, 10))
 
 
-def _bands_device(renderer, cam, w, h, b, band_h, stride, off, radiance=True):
+def _bands_device(renderer, cam, w, h, b, band_h, stride, off, radiance=True, stats=True):
     import torch
     from rtamd import lib
     rows = lib().rt_band_rows(h, band_h, stride, off)
@@ -75,7 +76,7 @@ def _bands_device(renderer, cam, w, h, b, band_h, stride, off, radiance=True):
     s = Stats()
     check(lib().rt_render_bands_device(renderer._ctx, C.byref(cam.ubo), w, h, b, band_h, stride, off,
                                        d_rgba.data_ptr(), d_rad.data_ptr() if radiance else None,
-                                       torch.cuda.current_stream().cuda_stream, C.byref(s)))
+                                       torch.cuda.current_stream().cuda_stream, C.byref(s) if stats else None))
     torch.cuda.synchronize()
     return d_rgba.cpu().numpy(), (d_rad.cpu().numpy() if radiance else None), s.as_dict()
 
@@ -166,19 +167,26 @@ def test_schedules_identical(renderer, opts):
             renderer.set_option(k, v)
 
 
-def test_heavy_first_order(renderer):
+@pytest.mark.parametrize("heavy,heavy_stream", [(-1, 1), (0, 0), (40, 0), (40, 1), (100000, 0)])
+def test_heavy_first_order(renderer, heavy, heavy_stream):
     """heavy_first: the learning launch and the launches in the learned
     order give the oracle's frame and counters; a new camera relearns."""
     from rtamd import configs
     try:
         renderer.set_option("heavy_first", 1)
+        renderer.set_option("heavy_tiles", heavy)
+        renderer.set_option("heavy_stream", heavy_stream)
         cfg = configs.config3()
         built = cfg.build()
         renderer.upload_scene(built)
         for cam in (cfg.camera(), configs.Camera.default(cfg.width, cfg.height + 7)):
             ref = _oracle(built, cam.ubo_bytes(), cfg.width, cfg.height, cfg.max_bounces,
                           tile=(0, 2, cfg.width, cfg.height - 2), row_step=9)
-            for _ in range(3):          # learn, then twice in the learned order
+            # a plain launch learns the order (a counting launch does not), then
+            # counting launches run in the learned order
+            rgba, rad, _ = _bands_device(renderer, cam, cfg.width, cfg.height, cfg.max_bounces, 1, 9, 2, stats=False)
+            _assert_same(rgba, rad, None, *ref)
+            for _ in range(2):
                 rgba, rad, st = _bands_device(renderer, cam, cfg.width, cfg.height, cfg.max_bounces, 1, 9, 2)
                 _assert_same(rgba, rad, st, *ref)
     finally:
