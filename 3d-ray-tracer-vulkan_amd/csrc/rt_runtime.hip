@@ -256,7 +256,6 @@ struct PerDevice {
 
 static constexpr size_t kMaxOrders = 16;
 static constexpr int    kResidentPerCu = 24;    // resident trace waves per CU (diag timelines)
-static constexpr double kHeavyFactor = 1.5;     // a tile this much longer than the bulk is split
 static constexpr int    kMaxHeavy = 256;
 static constexpr size_t kDiagWords = 8;   // per-wave diag record (rt_trace.hip, rtamd.h rt_diag_copy)
 
@@ -284,6 +283,7 @@ struct rt_ctx {
     int  coop_walk = 0;            // cooperative walks: 0 = 64-node windows, 1 = preorder frontier
     int  block_waves = 1;          // kernel 0: waves per workgroup (1: a finished wave frees its slot at once; or 4)
     int  heavy_first = 1;          // kernel 0: dispatch tiles in the cost order of a learning launch
+    int  heavy_factor = 130;       // automatic heavy tiles: cost above this percentage of the bulk estimate
     int  learn_cost = 1;           // heavy_first cost: 0 = lockstep steps + 2 x coop windows, 1 = wave duration
     int  heavy_stream = 1;         // heavy_tiles: 1 = their launch runs on an auxiliary stream, concurrent
                                    //   with the other tiles; 0 = before them on the same stream
@@ -326,7 +326,7 @@ static int plan_order(const rt_ctx* ctx, PerDevice& p, TraceArgs& a, const rt_ca
     const int tw_w = 8 << a.wave_tile, th_w = 8 >> a.wave_tile;
     const size_t n = (size_t)((a.tw + tw_w - 1) / tw_w) * (size_t)((a.th + th_w - 1) / th_w);
     const int geo[] = {a.width, a.height, a.max_bounces, a.x0, a.y0, a.tw, a.th, a.band_h, a.band_stride,
-                       a.band_off, a.wave_tile, a.ext, a.coop_lanes, a.walk, ctx->learn_cost};
+                       a.band_off, a.wave_tile, a.ext, a.coop_lanes, a.walk, ctx->learn_cost, ctx->heavy_factor};
     std::vector<uint8_t> key(sizeof(geo) + sizeof(rt_camera_ubo) + sizeof(uint64_t));
     std::memcpy(key.data(), geo, sizeof(geo));
     std::memcpy(key.data() + sizeof(geo), cam, sizeof(rt_camera_ubo));
@@ -370,7 +370,7 @@ static int plan_order(const rt_ctx* ctx, PerDevice& p, TraceArgs& a, const rt_ca
 // A tile's cost is its wave's lockstep walk iterations plus twice its
 // cooperative windows (diag record words 4 and 5): the length of the wave's
 // dependent chain, free of when the wave happened to run.
-static int learn_order(PerDevice& p, const TraceArgs& a, hipStream_t s, int learn_cost) {
+static int learn_order(PerDevice& p, const TraceArgs& a, hipStream_t s, int learn_cost, double heavy_factor) {
     if (!a.diag || a.diag != p.d_learn) return RT_OK;
     const size_t n = p.learning_n;
     RT_HIP_CHECK(hipStreamSynchronize(s));
@@ -384,7 +384,7 @@ static int learn_order(PerDevice& p, const TraceArgs& a, hipStream_t s, int lear
     std::vector<int> order(n);
     for (size_t k = 0; k < n; ++k) order[k] = (int)k;
     std::stable_sort(order.begin(), order.end(), [&](int x, int y) { return cost[x] > cost[y]; });
-    // Automatic heavy tiles: those whose cost exceeds kHeavyFactor times the
+    // Automatic heavy tiles: those whose cost exceeds heavy_factor times the
     // bulk estimate, the total cost spread over the device's resident waves
     // (kResidentPerCu per CU, measured).  A 1080p frame of config 3 gets a few
     // dozen; a frame whose time is its throughput (config 5) gets none.
@@ -392,7 +392,7 @@ static int learn_order(PerDevice& p, const TraceArgs& a, hipStream_t s, int lear
     for (size_t k = 0; k < n; ++k) total += (double)cost[k];
     const double bulk = total / (double)std::max(1, p.n_cu * kResidentPerCu);
     int heavy = 0;
-    while ((size_t)heavy < n - 1 && heavy < kMaxHeavy && (double)cost[order[heavy]] > kHeavyFactor * bulk) ++heavy;
+    while ((size_t)heavy < n - 1 && heavy < kMaxHeavy && (double)cost[order[heavy]] > heavy_factor * bulk) ++heavy;
     if (std::getenv("RTAMD_DEBUG_ORDER")) {
         std::fprintf(stderr, "learn_order: %zu tiles, bulk estimate %.0f, %d heavy; first:", n, bulk, heavy);
         for (size_t k = 0; k < 6 && k < n; ++k) std::fprintf(stderr, " %d(%llu)", order[k], cost[order[k]]);
@@ -534,6 +534,7 @@ int rt_create(const int* device_ids, int n_devices, rt_ctx** out) {
     if (const char* v = std::getenv("RTAMD_COOP_WALK")) ctx->coop_walk = std::atoi(v) ? 1 : 0;
     if (const char* v = std::getenv("RTAMD_HEAVY_FIRST")) ctx->heavy_first = std::atoi(v) ? 1 : 0;
     if (const char* v = std::getenv("RTAMD_HEAVY_TILES")) ctx->heavy_tiles = std::max(-1, std::atoi(v));
+    if (const char* v = std::getenv("RTAMD_HEAVY_FACTOR")) ctx->heavy_factor = std::max(10, std::atoi(v));
     if (const char* v = std::getenv("RTAMD_HEAVY_STREAM")) ctx->heavy_stream = std::atoi(v) ? 1 : 0;
     if (const char* v = std::getenv("RTAMD_BLOCK_WAVES")) ctx->block_waves = std::atoi(v) == 1 ? 1 : 4;
     if (const char* v = std::getenv("RTAMD_COOP_LANES")) ctx->coop_lanes = std::max(0, std::min(64, std::atoi(v)));
@@ -740,7 +741,7 @@ int rt_render_tile_device(rt_ctx* ctx, const rt_camera_ubo* cam, int width, int 
     }
     if (stats) RT_HIP_CHECK(hipEventRecord(p.ev0, s));
     RT_HIP_CHECK(launch_trace(a, s));
-    if (int ro = learn_order(p, a, s, ctx->learn_cost)) return ro;
+    if (int ro = learn_order(p, a, s, ctx->learn_cost, ctx->heavy_factor / 100.0)) return ro;
     if (stats) {
         RT_HIP_CHECK(hipEventRecord(p.ev1, s));
         RT_HIP_CHECK(hipEventSynchronize(p.ev1));
@@ -775,7 +776,7 @@ static int render_bands_on(const rt_ctx* ctx, PerDevice& p, const rt_camera_ubo*
     if (count) RT_HIP_CHECK(hipMemsetAsync(p.d_counters, 0, sizeof(Counters), s));
     RT_HIP_CHECK(hipEventRecord(p.ev0, s));
     RT_HIP_CHECK(launch_trace(a, s));
-    if (int ro = learn_order(p, a, s, ctx->learn_cost)) return ro;
+    if (int ro = learn_order(p, a, s, ctx->learn_cost, ctx->heavy_factor / 100.0)) return ro;
     RT_HIP_CHECK(hipEventRecord(p.ev1, s));
     return RT_OK;
 }
@@ -1004,6 +1005,8 @@ int rt_set_option(rt_ctx* ctx, const char* name, int64_t value) {
         ctx->heavy_first = (int)value;
     } else if (std::strcmp(name, "heavy_tiles") == 0 && value >= -1 && value <= (1 << 20)) {
         ctx->heavy_tiles = (int)value;
+    } else if (std::strcmp(name, "heavy_factor") == 0 && value >= 10 && value <= 100000) {
+        ctx->heavy_factor = (int)value;
     } else if (std::strcmp(name, "learn_cost") == 0 && (value == 0 || value == 1)) {
         ctx->learn_cost = (int)value;
     } else if (std::strcmp(name, "heavy_stream") == 0 && (value == 0 || value == 1)) {
@@ -1035,6 +1038,7 @@ int rt_get_option(rt_ctx* ctx, const char* name, int64_t* value) {
     else if (std::strcmp(name, "heavy_tiles") == 0) *value = ctx->heavy_tiles;
     else if (std::strcmp(name, "heavy_stream") == 0) *value = ctx->heavy_stream;
     else if (std::strcmp(name, "learn_cost") == 0) *value = ctx->learn_cost;
+    else if (std::strcmp(name, "heavy_factor") == 0) *value = ctx->heavy_factor;
     else if (std::strcmp(name, "extensions") == 0) *value = ctx->ext;
     else if (std::strcmp(name, "blocks_per_cu") == 0)
         *value = ctx->blocks_per_cu > 0 ? ctx->blocks_per_cu : (ctx->dev.empty() ? 0 : ctx->dev[0].blocks_per_cu);
