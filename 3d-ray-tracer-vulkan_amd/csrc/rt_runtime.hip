@@ -252,6 +252,7 @@ struct PerDevice {
     std::vector<Order> orders;
     std::vector<uint8_t> learning_key;
     size_t       learning_n = 0;
+    int          last_heavy = 0;    // heavy tiles of the last launch (option "heavy_tiles_used", read only)
 };
 
 static constexpr size_t kMaxOrders = 16;
@@ -322,6 +323,7 @@ static int plan_order(const rt_ctx* ctx, PerDevice& p, TraceArgs& a, const rt_ca
     a.heavy_tiles = 0;
     a.aux_stream = nullptr;
     a.ev_fork = a.ev_join = nullptr;
+    p.last_heavy = 0;
     if (!ctx->heavy_first || a.kernel != kKernelSimple || a.block_waves != 1) return RT_OK;
     const int tw_w = 8 << a.wave_tile, th_w = 8 >> a.wave_tile;
     const size_t n = (size_t)((a.tw + tw_w - 1) / tw_w) * (size_t)((a.th + th_w - 1) / th_w);
@@ -343,6 +345,7 @@ static int plan_order(const rt_ctx* ctx, PerDevice& p, TraceArgs& a, const rt_ca
                     RT_HIP_CHECK(hipEventCreateWithFlags(&p.aux_join[k], hipEventDisableTiming));
                 }
                 a.heavy_tiles = heavy;
+                p.last_heavy = (int)std::min<size_t>((size_t)heavy, n - 1);
                 a.aux_stream = ctx->heavy_stream ? p.aux[k] : nullptr;
                 a.ev_fork = p.aux_fork[k];
                 a.ev_join = p.aux_join[k];
@@ -1039,6 +1042,7 @@ int rt_get_option(rt_ctx* ctx, const char* name, int64_t* value) {
     else if (std::strcmp(name, "heavy_stream") == 0) *value = ctx->heavy_stream;
     else if (std::strcmp(name, "learn_cost") == 0) *value = ctx->learn_cost;
     else if (std::strcmp(name, "heavy_factor") == 0) *value = ctx->heavy_factor;
+    else if (std::strcmp(name, "heavy_tiles_used") == 0) *value = ctx->dev.empty() ? 0 : ctx->dev[0].last_heavy;
     else if (std::strcmp(name, "extensions") == 0) *value = ctx->ext;
     else if (std::strcmp(name, "blocks_per_cu") == 0)
         *value = ctx->blocks_per_cu > 0 ? ctx->blocks_per_cu : (ctx->dev.empty() ? 0 : ctx->dev[0].blocks_per_cu);

@@ -19,10 +19,14 @@ ranks), in millions.  A segment is one executed bounce-loop iteration
 (compute_dynamic_ray.comp:179-232); its count per frame is deterministic and is
 taken from a counting pass outside the timed region.
 
-roofline: algorithmic bytes of one trace launch (32 B per BVH node visit +
+roofline: algorithmic bytes of one frame's trace (32 B per BVH node visit +
 36 B per triangle test + 16 B per material read + 4 B per pixel; DESIGN.md
-§Roofline) / the launch's average device time from HIP events recorded on the
-launch stream, against 8 TB/s HBM.
+§Roofline) / the frame's average device time from HIP events recorded on the
+launch stream around it, against 8 TB/s HBM.  With heavy tiles a frame is two
+concurrent launches (the heaviest tiles one pixel per wave on an auxiliary
+stream, forked from and joined back to the launch stream), so the events span
+both; tools/rocprof_frames.py gives the same per-frame span from a rocprofv3
+kernel trace.
 cpu_baseline: the CPU oracle (oracle/rt_oracle.c, OpenMP) on a bounded row
 sample of the same frame, rank 0 at N = 1 only.
 """
@@ -185,6 +189,7 @@ def main() -> None:
         frames = out if frames_mode else out[None]
         verified = bool(all(torch.equal(frames[f], full) for f in range(frames.shape[0])))
 
+    heavy_used = renderer.get_option("heavy_tiles_used")   # of the last timed launch
     t = torch.tensor([elapsed, kernel_ms], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -234,8 +239,10 @@ def main() -> None:
                 "frames_per_step": F,
                 "frames_verified": verified,
                 "parallelism": f"tile{world}",
-                "schedule": {k: renderer.get_option(k) for k in ("kernel", "walk", "wave_tile", "coop_lanes")},
-                "launches_per_step": F,
+                "schedule": {**{k: renderer.get_option(k) for k in ("kernel", "walk", "wave_tile", "coop_lanes",
+                                                                      "heavy_first", "heavy_tiles", "heavy_factor")},
+                             "heavy_tiles_used": heavy_used},
+                "launches_per_step": F * (2 if heavy_used > 0 else 1),
             },
             "roofline": {
                 "bound": "hbm",
@@ -245,7 +252,9 @@ def main() -> None:
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": traffic,
                 "traffic_source": traffic_src,
-                "kernel": "trace_simple" if renderer.get_option("kernel") == 0 else "trace_*",
+                "kernel": ("trace_simple" if renderer.get_option("kernel") == 0 else "trace_*") +
+                          (f" (frame = the {heavy_used} heaviest tiles' one-pixel-wave launch concurrent with the "
+                           f"other tiles' launch; kernel_ms spans both)" if heavy_used > 0 else ""),
                 "kernel_ms": round(kernel_ms, 4),
                 "alg_bytes_per_launch": int(alg_bytes),
                 "alg_bytes_per_segment": round(alg_bytes / l_seg, 1),
