@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """HBM traffic per launch of one kernel from tools/pmc.sh passes.
 
-Usage: python tools/pmc_traffic.py gpurun_out/<TAG> "<kernel name substring>" [--out profiles/latest_pmc_traffic.json]
+Usage: python tools/pmc_traffic.py gpurun_out/<TAG> "<kernel substring>[|<kernel substring>...]" [--out ...]
 
 FETCH_SIZE (pass C) is in KiB and, on gfx950, counts 64-B halves of 128-B
 requests, so bytes = FETCH_SIZE x 1024 x 2 (MI355X_MICROARCH.md, HBM /
@@ -24,7 +24,12 @@ def main():
     ap.add_argument("--out", default="")
     ap.add_argument("--source", default="")
     args = ap.parse_args()
-    s = summarise(args.root, args.kernel)
+    # A frame may be several launches (heavy tiles + the other tiles): the
+    # kernel argument is a "|"-separated list, and per-launch means are summed.
+    s = {}
+    for name in args.kernel.split("|"):
+        for k, v in summarise(args.root, name).items():
+            s[k] = s.get(k, 0.0) + v
     if "FETCH_SIZE" not in s:
         sys.exit(f"no FETCH_SIZE rows for kernel {args.kernel!r} under {args.root}")
     out = {
