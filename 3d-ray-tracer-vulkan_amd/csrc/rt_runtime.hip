@@ -537,6 +537,7 @@ int rt_create(const int* device_ids, int n_devices, rt_ctx** out) {
     if (const char* v = std::getenv("RTAMD_COOP_WALK")) ctx->coop_walk = std::atoi(v) ? 1 : 0;
     if (const char* v = std::getenv("RTAMD_HEAVY_FIRST")) ctx->heavy_first = std::atoi(v) ? 1 : 0;
     if (const char* v = std::getenv("RTAMD_HEAVY_TILES")) ctx->heavy_tiles = std::max(-1, std::atoi(v));
+    if (const char* v = std::getenv("RTAMD_LEARN_COST")) ctx->learn_cost = std::atoi(v) ? 1 : 0;
     if (const char* v = std::getenv("RTAMD_HEAVY_FACTOR")) ctx->heavy_factor = std::max(10, std::atoi(v));
     if (const char* v = std::getenv("RTAMD_HEAVY_STREAM")) ctx->heavy_stream = std::atoi(v) ? 1 : 0;
     if (const char* v = std::getenv("RTAMD_BLOCK_WAVES")) ctx->block_waves = std::atoi(v) == 1 ? 1 : 4;
