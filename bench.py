@@ -113,44 +113,63 @@ def main() -> None:
     plan = BatchPlan(H, band_h, world, F) if frames_mode else None
     rows_f = [L.rt_band_rows(H, band_h, world, off) for off in offsets]
     max_rows = plan.max_rows if plan else max(L.rt_band_rows(H, band_h, world, r) for r in range(world))
-    d_rgba = torch.empty((F, max_rows, W, 4), dtype=torch.uint8, device=dev)
+    # Two frame buffers at N > 1: step k traces into buffer k % 2 while step
+    # k-1's gather (RCCL, its own stream) still reads the other one.
+    n_buf = 2 if world > 1 else 1
+    d_bufs = [torch.empty((F, max_rows, W, 4), dtype=torch.uint8, device=dev) for _ in range(n_buf)]
+    gathered = [None] * n_buf                # event: the last gather that read buffer b is done
     # One stream per frame in flight (launches and their events on the same
-    # queue); the gather runs on the main stream once every frame is traced.
+    # queue); the gather runs on main_stream once every frame is traced.
     streams = [torch.cuda.Stream(dev) for _ in range(min(F, 8))]
-    main_stream = streams[0]
+    # The gathers run on their own stream order (main_stream): a trace stream
+    # never waits for the latest gather, only for the one that last read the
+    # buffer it is about to overwrite.
+    main_stream = torch.cuda.Stream(dev) if world > 1 else streams[0]
     torch.cuda.set_stream(main_stream)
     src_index = torch.as_tensor(plan.src, device=dev) if (plan and world > 1) else None
 
     import ctypes as C
     from rtamd._lib import Stats, check
 
-    def trace(f, stats: bool = False, ev=None):
+    def trace(f, stats: bool = False, ev=None, buf=0):
         s = streams[f % len(streams)]
         st = Stats()
         if ev is not None:
             ev[0].record(s)
         check(L.rt_render_bands_device(renderer._ctx, C.byref(cam.ubo), W, H, B, band_h, world, offsets[f],
-                                       d_rgba[f].data_ptr(), None, s.cuda_stream,
+                                       d_bufs[buf][f].data_ptr(), None, s.cuda_stream,
                                        C.byref(st) if stats else None))
         if ev is not None:
             ev[1].record(s)
         return st.as_dict() if stats else None
 
+    k_step = [0]
+
     def step(evs=None):
-        for s in streams[1:]:                      # the last step's gather has read d_rgba
-            s.wait_stream(main_stream)
+        b = k_step[0] % n_buf
+        k_step[0] += 1
+        d_rgba = d_bufs[b]
+        for s in streams:                          # the gather that last read this buffer is done
+            if gathered[b] is not None:
+                s.wait_event(gathered[b])
         for f in range(F):
-            trace(f, ev=evs[f] if evs is not None else None)
-        for s in streams[1:]:
-            main_stream.wait_stream(s)
+            trace(f, ev=evs[f] if evs is not None else None, buf=b)
+        for s in streams:
+            if s is not main_stream:
+                main_stream.wait_stream(s)
         if world > 1:
             if frames_mode:
-                return gather_batch(d_rgba, plan, src_index=src_index)
-            return gather_frame(d_rgba[0, :rows_f[0]], H, band_h)   # RCCL gather + rank-0 assembly
+                out = gather_batch(d_rgba, plan, src_index=src_index)
+            else:
+                out = gather_frame(d_rgba[0, :rows_f[0]], H, band_h)   # RCCL gather + rank-0 assembly
+            gathered[b] = torch.cuda.Event()
+            gathered[b].record(main_stream)
+            return out
         return None
 
     # Counting pass (untimed): this rank's work, then the job totals.
     per = [trace(f, stats=True) for f in range(F)]
+    torch.cuda.synchronize(dev)
     counts = torch.tensor([sum(p[k] for p in per) for k in ("pixels", "segments", "node_visits", "tri_tests",
                                                              "mat_reads")], dtype=torch.float64, device=dev)
     local = counts.clone()
