@@ -284,7 +284,7 @@ struct rt_ctx {
     int  coop_walk = 0;            // cooperative walks: 0 = 64-node windows, 1 = preorder frontier
     int  block_waves = 1;          // kernel 0: waves per workgroup (1: a finished wave frees its slot at once; or 4)
     int  heavy_first = 1;          // kernel 0: dispatch tiles in the cost order of a learning launch
-    int  heavy_factor = 130;       // automatic heavy tiles: cost above this percentage of the bulk estimate
+    int  heavy_factor = 150;       // automatic heavy tiles: walk length above this percentage of the bulk estimate
     int  learn_cost = 1;           // heavy_first cost: 0 = lockstep steps + 2 x coop windows, 1 = wave duration
     int  heavy_stream = 1;         // heavy_tiles: 1 = their launch runs on an auxiliary stream, concurrent
                                    //   with the other tiles; 0 = before them on the same stream
@@ -379,23 +379,29 @@ static int learn_order(PerDevice& p, const TraceArgs& a, hipStream_t s, int lear
     RT_HIP_CHECK(hipStreamSynchronize(s));
     std::vector<unsigned long long> rec(n * kDiagWords);
     RT_HIP_CHECK(hipMemcpy(rec.data(), p.d_learn, rec.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
-    std::vector<unsigned long long> cost(n);
+    // Two costs per tile: its wave's duration (orders the tiles: it also sees
+    // when and beside what the wave ran) and its lockstep steps + 2 x
+    // cooperative windows (a deterministic walk length: counts the heavy tiles).
+    std::vector<unsigned long long> cost(n), steps(n);
     for (size_t k = 0; k < n; ++k) {
         const unsigned long long* r = &rec[k * kDiagWords];
-        cost[k] = learn_cost == 0 ? r[4] + 2 * r[5] : r[1] - r[0];
+        steps[k] = r[4] + 2 * r[5];
+        cost[k] = learn_cost == 0 ? steps[k] : r[1] - r[0];
     }
     std::vector<int> order(n);
     for (size_t k = 0; k < n; ++k) order[k] = (int)k;
     std::stable_sort(order.begin(), order.end(), [&](int x, int y) { return cost[x] > cost[y]; });
-    // Automatic heavy tiles: those whose cost exceeds heavy_factor times the
-    // bulk estimate, the total cost spread over the device's resident waves
-    // (kResidentPerCu per CU, measured).  A 1080p frame of config 3 gets a few
-    // dozen; a frame whose time is its throughput (config 5) gets none.
+    // Automatic heavy tiles: the tiles whose walk length exceeds heavy_factor
+    // times the bulk estimate, the total walk length spread over the device's
+    // resident waves (kResidentPerCu per CU, measured).  A 1080p frame of
+    // config 3 gets a few dozen; a frame whose time is its throughput
+    // (config 5) gets none.
     double total = 0.0;
-    for (size_t k = 0; k < n; ++k) total += (double)cost[k];
+    for (size_t k = 0; k < n; ++k) total += (double)steps[k];
     const double bulk = total / (double)std::max(1, p.n_cu * kResidentPerCu);
     int heavy = 0;
-    while ((size_t)heavy < n - 1 && heavy < kMaxHeavy && (double)cost[order[heavy]] > heavy_factor * bulk) ++heavy;
+    for (size_t k = 0; k < n - 1 && heavy < kMaxHeavy; ++k)
+        if ((double)steps[k] > heavy_factor * bulk) ++heavy;
     if (std::getenv("RTAMD_DEBUG_ORDER")) {
         std::fprintf(stderr, "learn_order: %zu tiles, bulk estimate %.0f, %d heavy; first:", n, bulk, heavy);
         for (size_t k = 0; k < 6 && k < n; ++k) std::fprintf(stderr, " %d(%llu)", order[k], cost[order[k]]);

@@ -247,6 +247,25 @@ __device__ __forceinline__ void write_pixel(const TraceArgs& a, int lx, int ly, 
     }
 }
 
+constexpr int kFeatExtBit = 16;   // = kFeatExt (defined with the other feature flags below)
+
+// The end of a path: (extension) the accumulation of the linear colour,
+// then the sqrt'd RGBA8 store (:235).
+template <int FEAT>
+__device__ __forceinline__ void finish_pixel(const TraceArgs& a, int lx, int ly, V3 fin) {
+    if ((FEAT & kFeatExtBit) && (a.ext & kExtAccumulate)) {
+        // extension: running sum of the linear colour, shown as sqrt(mean)
+        float* acc = a.accum + 3 * ((size_t)ly * (size_t)a.tw + (size_t)lx);
+        const float nf = (float)(a.frame_count + 1);
+        const V3 sum = a.frame_count == 0 ? fin : V3{acc[0] + fin.x, acc[1] + fin.y, acc[2] + fin.z};
+        acc[0] = sum.x;
+        acc[1] = sum.y;
+        acc[2] = sum.z;
+        fin = {sum.x / nf, sum.y / nf, sum.z / nf};
+    }
+    write_pixel(a, lx, ly, fin);
+}
+
 __device__ __forceinline__ void flush_counters(Counters* c, unsigned long long s, unsigned long long n,
                                                unsigned long long t, unsigned long long m) {
 #pragma unroll
@@ -551,7 +570,7 @@ constexpr int kFeatSpill = 1;     // split schedule: hand paths on after seg_lim
 constexpr int kFeatHeavy = 2;     // tiered schedule: hand walks on after heavy_budget visits
 constexpr int kFeatPrio = 4;      // raise wave priority after prio_after visits
 constexpr int kFeatCoopTail = 8;  // finish the last coop_lanes walks of a wave cooperatively
-constexpr int kFeatExt = 16;      // non-reference extensions (option "extensions", kExt*)
+constexpr int kFeatExt = kFeatExtBit;   // non-reference extensions (option "extensions", kExt*)
 constexpr int kFeatFrontier = 32; // cooperative tail uses frontier_walk (option coop_walk = 1)
 
 constexpr int kStack = 8;                    // per-lane t_enter stack entries in LDS (walk 1)
@@ -624,9 +643,8 @@ __global__ __launch_bounds__(256) void trace_simple(TraceArgs a) {
             primary_ray(a, x, y, seed, o, d);
         }
     }
-    V3 fin = {0.0f, 0.0f, 0.0f};
     V3 att = {1.0f, 1.0f, 1.0f};
-    bool alive = pixel, handed_on = false;
+    bool alive = pixel;
 
     // The bounce loop (:179) is wave-uniform: a lane whose path has ended
     // stays in it with alive = false, so the cooperative tail below can use
@@ -639,7 +657,6 @@ __global__ __launch_bounds__(256) void trace_simple(TraceArgs a) {
             st->q1 = make_float4(d.x, d.y, d.z, att.y);
             st->q2 = make_float4(att.z, __uint_as_float(seed), __int_as_float(b), __int_as_float(lx | (ly << 16)));
             alive = false;
-            handed_on = true;
         }
         float closest = kTMax;
         int hit = -1;
@@ -727,7 +744,6 @@ __global__ __launch_bounds__(256) void trace_simple(TraceArgs a) {
                                        __int_as_float(lx | (ly << 16)));
                 hv->q3 = make_float4(closest, __int_as_float(n), __int_as_float(hit), 0.f);
                 alive = false;
-                handed_on = true;
                 walking = false;
             }
         } else for (;;) {
@@ -789,7 +805,6 @@ __global__ __launch_bounds__(256) void trace_simple(TraceArgs a) {
                                        __int_as_float(lx | (ly << 16)));
                 hv->q3 = make_float4(closest, __int_as_float(start), __int_as_float(hit), 0.f);
                 alive = false;
-                handed_on = true;
                 walking = false;
                 continue;
             }
@@ -909,6 +924,9 @@ __global__ __launch_bounds__(256) void trace_simple(TraceArgs a) {
             if (DIAG && tc0) d_coop_t += wall_clock64() - tc0;
         }
         if (alive) {
+            // A path that ends here writes its pixel now, so its final colour
+            // is not carried (in registers) through the remaining bounces.
+            V3 fin = {0.0f, 0.0f, 0.0f};
             if (hit >= 0) {                                               // :212
                 if (COUNT) ++c_mat;
                 const V3 nrm = hit_normal(a.scene.norms, hit, d);
@@ -924,31 +942,18 @@ __global__ __launch_bounds__(256) void trace_simple(TraceArgs a) {
                     att = vmul(att, V3{M.x, M.y, M.z});
                     o = hp;
                     d = nd;
-                    if (b == a.max_bounces - 1) {                         // :229-231
-                        fin = {0.0f, 0.0f, 0.0f};
-                        alive = false;
-                    }
+                    if (b == a.max_bounces - 1) alive = false;            // :229-231: black
                 }
             } else {
-                if ((FEAT & kFeatExt) && (a.ext & kExtSkyToggle) && a.sky_enabled == 0)
-                    fin = {0.0f, 0.0f, 0.0f};                             // extension: sky off
-                else
-                    fin = vmul(att, sky_color(d));
+                if (!((FEAT & kFeatExt) && (a.ext & kExtSkyToggle) && a.sky_enabled == 0))
+                    fin = vmul(att, sky_color(d));                        // (extension: sky off is black)
                 alive = false;
             }
+            if (!alive) finish_pixel<FEAT>(a, lx, ly, fin);
         }
     }
-    if ((FEAT & kFeatExt) && (a.ext & kExtAccumulate) && pixel && !handed_on) {
-        // extension: running sum of the linear colour, shown as sqrt(mean)
-        float* acc = a.accum + 3 * ((size_t)ly * (size_t)a.tw + (size_t)lx);
-        const float nf = (float)(a.frame_count + 1);
-        const V3 sum = a.frame_count == 0 ? fin : V3{acc[0] + fin.x, acc[1] + fin.y, acc[2] + fin.z};
-        acc[0] = sum.x;
-        acc[1] = sum.y;
-        acc[2] = sum.z;
-        fin = {sum.x / nf, sum.y / nf, sum.z / nf};
-    }
-    if (pixel && !handed_on) write_pixel(a, lx, ly, fin);
+    // A path still alive here ran no bounce at all (max_bounces 0): black.
+    if (alive) finish_pixel<FEAT>(a, lx, ly, V3{0.0f, 0.0f, 0.0f});
     if (COUNT) flush_counters(a.counters, c_seg, c_node, c_tri, c_mat);
     if (DIAG) {
         diag_stamp(drec, 1);

@@ -77,7 +77,7 @@ def main():
             e1.record(stream)
             e1.synchronize()
             times[v].append(e0.elapsed_time(e1) / args.iters)
-        apply("kernel=0,shade_min=16,blocks_per_cu=0,wave_tile=2,heavy_budget=256,prio_after=0,coop_lanes=2,walk=2,coop_walk=0,block_waves=1,heavy_first=1,heavy_tiles=-1,heavy_stream=1,learn_cost=1,heavy_factor=130")
+        apply("kernel=0,shade_min=16,blocks_per_cu=0,wave_tile=2,heavy_budget=256,prio_after=0,coop_lanes=2,walk=2,coop_walk=0,block_waves=1,heavy_first=1,heavy_tiles=-1,heavy_stream=1,learn_cost=1,heavy_factor=150")
     for v in variants:
         med = statistics.median(times[v])
         print(json.dumps({"variant": v, "config": cfg.name, "median_ms": round(med, 4),
