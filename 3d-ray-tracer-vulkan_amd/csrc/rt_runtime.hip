@@ -340,6 +340,7 @@ static int plan_order(const rt_ctx* ctx, PerDevice& p, TraceArgs& a, const rt_ca
             if (heavy > 0 && n > 1) {
                 const unsigned k = p.aux_next++ % 4;
                 if (!p.aux[k]) {
+                    // normal priority: a high-priority stream measured slower (0.715 vs 0.59 ms)
                     RT_HIP_CHECK(hipStreamCreateWithFlags(&p.aux[k], hipStreamNonBlocking));
                     RT_HIP_CHECK(hipEventCreateWithFlags(&p.aux_fork[k], hipEventDisableTiming));
                     RT_HIP_CHECK(hipEventCreateWithFlags(&p.aux_join[k], hipEventDisableTiming));
