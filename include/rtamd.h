@@ -174,10 +174,25 @@ int rt_render_wait(rt_ctx* ctx, uint64_t ticket);
  *   "block_waves"   kernel 0: waves per workgroup, 1 (default: a finished
  *                   wave frees its slot at once) or 4
  *   "heavy_first"   kernel 0 with block_waves 1: 1 (default) = the first
- *                   launch of a frame geometry + camera + scene records every
- *                   wave's duration (and ends with a stream synchronisation);
- *                   later launches with the same key dispatch the tiles most
- *                   expensive first (up to 16 keys per device are kept)
+ *                   plain (non-stats) launch of a frame geometry + camera +
+ *                   scene runs the diagnostic build, records every wave's
+ *                   duration and walk length, and ends with a stream
+ *                   synchronisation; later launches with the same key
+ *                   dispatch the tiles most expensive first (up to 16 keys
+ *                   per device are kept)
+ *   "heavy_tiles"   with heavy_first: the first this-many tiles of the order
+ *                   are traced one pixel per wave (64 one-wave workgroups per
+ *                   tile), every segment walked cooperatively with the
+ *                   frontier walk, in a launch of their own.  -1 (default) =
+ *                   automatic: the tiles whose walk length exceeds
+ *                   "heavy_factor" percent (default 150) of the bulk estimate
+ *   "heavy_stream"  1 (default) = that launch runs on an auxiliary stream,
+ *                   forked from and joined back to the caller's stream,
+ *                   concurrently with the other tiles; 0 = before them on the
+ *                   caller's stream
+ *   "learn_cost"    heavy_first order by 1 = wave duration (default) or 0 =
+ *                   walk length
+ *   "heavy_tiles_used" (rt_get_option only) heavy tiles of the last launch
  *   "wave_tile"     kernel 0: pixels per wave (8<<s) x (8>>s), s = 0..3
  *                   (default 2: 32x2)
  *   "extensions"    NON-REFERENCE features, bits (default 0 = the reference's
@@ -201,7 +216,8 @@ int rt_render_wait(rt_ctx* ctx, uint64_t ticket);
  *                   the occupancy query)
  * Defaults can also be set with the environment variables
  * RTAMD_KERNEL=simple|persistent|split|tiered, RTAMD_WALK, RTAMD_COOP_LANES,
- * RTAMD_COOP_WALK, RTAMD_BLOCK_WAVES, RTAMD_HEAVY_FIRST,
+ * RTAMD_COOP_WALK, RTAMD_BLOCK_WAVES, RTAMD_HEAVY_FIRST, RTAMD_HEAVY_TILES,
+ * RTAMD_HEAVY_FACTOR, RTAMD_HEAVY_STREAM, RTAMD_LEARN_COST,
  * RTAMD_SEG_LIMIT, RTAMD_SHADE_MIN and RTAMD_BLOCKS_PER_CU. */
 int rt_set_option(rt_ctx* ctx, const char* name, int64_t value);
 /* Diagnostics: with option "diag" = 1, kernel 0 records per wave
