@@ -396,9 +396,13 @@ static int learn_order(PerDevice& p, const TraceArgs& a, hipStream_t s, int lear
     // times the bulk estimate, the total walk length spread over the device's
     // resident waves (kResidentPerCu per CU, measured).  A 1080p frame of
     // config 3 gets a few dozen; a frame whose time is its throughput
-    // (config 5) gets none.
+    // (config 5) gets none.  A band partition of band_stride bands counts as
+    // band_stride times its own work: bench.py's frame batches trace all the
+    // bands of a frame on one device at once (with the bands on other devices
+    // this only splits fewer tiles).
     double total = 0.0;
     for (size_t k = 0; k < n; ++k) total += (double)steps[k];
+    total *= (double)std::max(1, a.band_stride);
     const double bulk = total / (double)std::max(1, p.n_cu * kResidentPerCu);
     int heavy = 0;
     for (size_t k = 0; k < n - 1 && heavy < kMaxHeavy; ++k)

@@ -199,6 +199,7 @@ def main() -> None:
     elapsed = time.perf_counter() - t_start
     kernel_ms = float(np.mean([a.elapsed_time(b) for e in evs for a, b in e]))
 
+    heavy_used = renderer.get_option("heavy_tiles_used")   # of the last timed launch
     verified = None
     if world > 1 and rank == 0:                    # the assembled frames equal the 1-GPU frame
         full = torch.empty((H, W, 4), dtype=torch.uint8, device=dev)
@@ -208,7 +209,6 @@ def main() -> None:
         frames = out if frames_mode else out[None]
         verified = bool(all(torch.equal(frames[f], full) for f in range(frames.shape[0])))
 
-    heavy_used = renderer.get_option("heavy_tiles_used")   # of the last timed launch
     t = torch.tensor([elapsed, kernel_ms], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
