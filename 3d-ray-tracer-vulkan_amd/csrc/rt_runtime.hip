@@ -748,13 +748,14 @@ int rt_render_tile_device(rt_ctx* ctx, const rt_camera_ubo* cam, int width, int 
     a.band_h = tile_h; a.band_stride = 1; a.band_off = 0;
     a.out_rgba = static_cast<uchar4*>(d_out_rgba);
     a.out_rad = static_cast<float*>(d_out_radiance);
-    a.counters = nullptr;
+    // counters before set_schedule: a counting launch must not become the
+    // (non-counting) learning launch of the heavy-first order
+    a.counters = stats ? p.d_counters : nullptr;
     if (int rs = set_schedule(ctx, p, a, cam)) return rs;
     if (stats) {
-        a.counters = p.d_counters;
         RT_HIP_CHECK(hipMemsetAsync(p.d_counters, 0, sizeof(Counters), s));
+        RT_HIP_CHECK(hipEventRecord(p.ev0, s));
     }
-    if (stats) RT_HIP_CHECK(hipEventRecord(p.ev0, s));
     RT_HIP_CHECK(launch_trace(a, s));
     if (int ro = learn_order(p, a, s, ctx->learn_cost, ctx->heavy_factor / 100.0)) return ro;
     if (stats) {

@@ -194,6 +194,29 @@ def test_heavy_first_order(renderer, heavy, heavy_stream):
             renderer.set_option(k, v)
 
 
+def test_first_tile_launch_counts(renderer):
+    """The first launch for a key that asks for stats through
+    rt_render_tile_device counts (it must not become the learning launch,
+    whose diagnostic build does not count), then a plain launch learns and a
+    counting launch in the learned order counts the same."""
+    import torch
+    from rtamd import configs
+    cfg = configs.config2()
+    built = cfg.build()
+    cam = configs.Camera.default(cfg.width, cfg.height + 3)   # a key no other test has learned
+    renderer.upload_scene(built)
+    x0, y0, tw, th = 560, 300, 160, 96
+    ref = _oracle(built, cam.ubo_bytes(), cfg.width, cfg.height, cfg.max_bounces, tile=(x0, y0, tw, th))
+    stream = torch.cuda.current_stream().cuda_stream
+    for stats in (True, False, True):
+        d_rgba = torch.empty((th, tw, 4), dtype=torch.uint8, device="cuda:0")
+        d_rad = torch.empty((th, tw, 3), dtype=torch.float32, device="cuda:0")
+        st = renderer.render_tile_device(cam, cfg.width, cfg.height, cfg.max_bounces, x0, y0, tw, th,
+                                         d_rgba.data_ptr(), d_rad.data_ptr(), stream, stats=stats)
+        torch.cuda.synchronize()
+        _assert_same(d_rgba.cpu().numpy(), d_rad.cpu().numpy(), st, *ref)
+
+
 def test_tiles_compose_to_frame(renderer):
     """Tiles and interleaved bands reassemble into the full frame bit for bit
     (the seed depends on global pixel coordinates only, :164)."""
