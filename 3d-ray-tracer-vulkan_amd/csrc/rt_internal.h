@@ -55,6 +55,10 @@ struct DevScene {
     float4*  pairs   = nullptr;
     float4*  norms   = nullptr;
     float4*  mats    = nullptr;
+    // extension kExtSpheres: 2 x float4 per sphere (centre.xyz, radius),
+    // (albedo.rgb, type); n_spheres is 0 unless the extension is on
+    const float4* spheres = nullptr;
+    int      n_spheres = 0;
 };
 
 struct Counters {               // device-side work counters (see rt_stats)
@@ -83,6 +87,7 @@ constexpr int kKernelSplit = 2;        // simple for the first seg_limit segment
 constexpr int kExtSkyToggle = 1;    // a miss is black when sky_enabled == 0
 constexpr int kExtEmissive = 2;     // a type-3 hit ends the path with attenuation * albedo
 constexpr int kExtAccumulate = 4;   // seed += frame_count*W*H; output sqrt(mean of linear colour)
+constexpr int kExtSpheres = 8;      // spheres (rt_upload_spheres) after the BVH walk, in index order
 
 // A path suspended between two segments (48 B): everything the bounce loop
 // (compute_dynamic_ray.comp:179-232) carries from one iteration to the next.

@@ -238,6 +238,8 @@ struct PerDevice {
     size_t       ring_cap = 0;     // pixels per slot
     hipEvent_t   traced[2] = {nullptr, nullptr}, copied[2] = {nullptr, nullptr};
     float*       d_accum = nullptr;  // extension kExtAccumulate: running sums
+    float4*      d_spheres = nullptr; // extension kExtSpheres: 2 float4 per sphere
+    int          n_spheres = 0;
     size_t       accum_n = 0;        // floats
     // option heavy_first: per-wave costs of a learning launch, and the tile
     // orders (most expensive first) learned so far, one per launch key (a
@@ -439,6 +441,8 @@ static int set_schedule(const rt_ctx* ctx, PerDevice& p, TraceArgs& a, const rt_
     a.sink = p.d_counters + 1;
     a.seg_limit = a.kernel == kKernelSplit ? ctx->seg_limit : (1 << 30);
     a.ext = ctx->ext;
+    a.scene.spheres = p.d_spheres;
+    a.scene.n_spheres = (a.ext & kExtSpheres) ? p.n_spheres : 0;
     a.sky_enabled = cam->sky_enabled;
     a.frame_count = cam->frame_count;
     a.accum = nullptr;
@@ -621,6 +625,7 @@ int rt_destroy(rt_ctx* ctx) {
             if (p.aux_join[k]) (void)hipEventDestroy(p.aux_join[k]);
         }
         if (p.d_accum) (void)hipFree(p.d_accum);
+        if (p.d_spheres) (void)hipFree(p.d_spheres);
         if (p.d_rgba) (void)hipFree(p.d_rgba);
         if (p.d_rad) (void)hipFree(p.d_rad);
         if (p.ev0) (void)hipEventDestroy(p.ev0);
@@ -684,6 +689,42 @@ int rt_upload_scene(rt_ctx* ctx, const void* vertices, size_t vertex_bytes,
     ctx->has_scene = true;
     ++ctx->scene_gen;
     free_host_scene(&hs);
+    return RT_OK;
+}
+
+int rt_upload_spheres(rt_ctx* ctx, const float* spheres, int n_spheres) {
+    if (!ctx) { set_error("rt_upload_spheres: null context"); return RT_ERR_INVALID_ARG; }
+    if (n_spheres < 0 || n_spheres > 65536 || (n_spheres > 0 && !spheres)) {
+        set_error("rt_upload_spheres: need 0 <= n_spheres <= 65536 and a buffer of 8 floats per sphere");
+        return RT_ERR_INVALID_ARG;
+    }
+    for (int k = 0; k < n_spheres; ++k) {
+        const float* s = spheres + 8 * (size_t)k;
+        if (!std::isfinite(s[0]) || !std::isfinite(s[1]) || !std::isfinite(s[2]) || !std::isfinite(s[3]) ||
+            !(s[3] > 0.0f)) {
+            set_error("rt_upload_spheres: sphere %d: centre must be finite and radius finite and > 0", k);
+            return RT_ERR_INVALID_ARG;
+        }
+    }
+    for (PerDevice& p : ctx->dev) {
+        RT_HIP_CHECK(hipSetDevice(p.device));
+        RT_HIP_CHECK(hipStreamSynchronize(p.stream));
+        if (p.d_spheres) (void)hipFree(p.d_spheres);
+        p.d_spheres = nullptr;
+        p.n_spheres = 0;
+        if (n_spheres == 0) continue;
+        const size_t bytes = sizeof(float) * 8 * (size_t)n_spheres;
+        hipError_t e = hipMalloc(&p.d_spheres, bytes);
+        if (e == hipSuccess) e = hipMemcpy(p.d_spheres, spheres, bytes, hipMemcpyHostToDevice);
+        if (e != hipSuccess) {
+            set_error("rt_upload_spheres: device %d: %s", p.device, hipGetErrorString(e));
+            if (p.d_spheres) (void)hipFree(p.d_spheres);
+            p.d_spheres = nullptr;
+            return e == hipErrorOutOfMemory ? RT_ERR_OOM : RT_ERR_HIP;
+        }
+        p.n_spheres = n_spheres;
+    }
+    ++ctx->scene_gen;    // learned tile orders see the new work
     return RT_OK;
 }
 
@@ -1009,7 +1050,7 @@ int rt_set_option(rt_ctx* ctx, const char* name, int64_t value) {
         ctx->prio_after = (int)value;
     } else if (std::strcmp(name, "coop_lanes") == 0 && value >= 0 && value <= 64) {
         ctx->coop_lanes = (int)value;
-    } else if (std::strcmp(name, "extensions") == 0 && value >= 0 && value <= 7) {
+    } else if (std::strcmp(name, "extensions") == 0 && value >= 0 && value <= 15) {
         ctx->ext = (int)value;
     } else if (std::strcmp(name, "walk") == 0 && value >= 0 && value <= 2) {
         ctx->walk = (int)value;

@@ -207,6 +207,38 @@ __device__ __forceinline__ V3 hit_normal(const float4* __restrict__ norms, int h
     return n;
 }
 
+// Extension kExtSpheres (no reference counterpart; oracle/rt_oracle.h
+// ORC_EXT_SPHERES states the same arithmetic): after the BVH walk, every
+// sphere in index order against (T_MIN, closest); a hit sets hit = -2 - k.
+// The sphere index is wave-uniform, so every lane reads the same record.
+__device__ __forceinline__ void sphere_tests(const float4* __restrict__ sph, int n, V3 o, V3 d,
+                                             float& closest, int& hit) {
+    const float qa = vdot(d, d);
+    for (int k = 0; k < n; ++k) {
+        const float4 S = sph[2 * k];
+        const V3 oc = {o.x - S.x, o.y - S.y, o.z - S.z};
+        const float hb = vdot(oc, d);
+        const float qc = vdot(oc, oc) - S.w * S.w;
+        const float disc = hb * hb - qa * qc;
+        if (!(disc >= 0.0f)) continue;
+        const float sq = sqrtf(disc);
+        float root = (-hb - sq) / qa;
+        if (!(root > kTMin && root < closest)) {
+            root = (-hb + sq) / qa;
+            if (!(root > kTMin && root < closest)) continue;
+        }
+        closest = root;
+        hit = -2 - k;
+    }
+}
+
+// The sphere normal (p - c) / r at the hit point, turned to face against d.
+__device__ __forceinline__ V3 sphere_normal(float4 S, V3 hp, V3 d) {
+    V3 n = {(hp.x - S.x) / S.w, (hp.y - S.y) / S.w, (hp.z - S.z) / S.w};
+    if (vdot(d, n) > 0.0f) n = {-n.x, -n.y, -n.z};
+    return n;
+}
+
 // scatter (:132-154).  Returns true and the new direction on scatter.
 __device__ __forceinline__ bool scatter(float4 M, V3 d, V3 n, uint32_t& seed, V3& nd) {
     if (M.w == 0.0f) {                                                    // Lambertian :137-143
@@ -923,15 +955,24 @@ __global__ __launch_bounds__(256) void trace_simple(TraceArgs a) {
             }
             if (DIAG && tc0) d_coop_t += wall_clock64() - tc0;
         }
+        if ((FEAT & kFeatExt) && alive && a.scene.n_spheres > 0)
+            sphere_tests(a.scene.spheres, a.scene.n_spheres, o, d, closest, hit);   // extension: spheres
         if (alive) {
             // A path that ends here writes its pixel now, so its final colour
             // is not carried (in registers) through the remaining bounces.
             V3 fin = {0.0f, 0.0f, 0.0f};
-            if (hit >= 0) {                                               // :212
+            if ((FEAT & kFeatExt) ? hit != -1 : hit >= 0) {               // :212
                 if (COUNT) ++c_mat;
-                const V3 nrm = hit_normal(a.scene.norms, hit, d);
                 const V3 hp = vadd(o, vscale(d, closest));                  // ray_at :77-79
-                const float4 M = a.scene.mats[hit];
+                V3 nrm;
+                float4 M;
+                if ((FEAT & kFeatExt) && hit < -1) {                      // extension: a sphere
+                    nrm = sphere_normal(a.scene.spheres[2 * (-2 - hit)], hp, d);
+                    M = a.scene.spheres[2 * (-2 - hit) + 1];
+                } else {
+                    nrm = hit_normal(a.scene.norms, hit, d);
+                    M = a.scene.mats[hit];
+                }
                 V3 nd;
                 if ((FEAT & kFeatExt) && (a.ext & kExtEmissive) && M.w == 3.0f) {
                     fin = vmul(att, V3{M.x, M.y, M.z});                   // extension: type 3 emits

@@ -32,7 +32,7 @@ EXPORTED = (
     "rt_camera_from_lookat", "rt_mesh_load_obj", "rt_mesh_tri_count", "rt_mesh_transform",
     "rt_mesh_free", "rt_mesh_procedural", "rt_render_bands_device", "rt_band_rows",
     "rt_scene_validate", "rt_set_option", "rt_get_option", "rt_diag_copy",
-    "rt_host_alloc", "rt_host_free", "rt_render_async", "rt_render_wait",
+    "rt_host_alloc", "rt_host_free", "rt_render_async", "rt_render_wait", "rt_upload_spheres",
 )
 
 
@@ -97,6 +97,7 @@ def lib() -> C.CDLL:
             sig = {
                 "rt_create": (i32, [C.POINTER(C.c_int), i32, C.POINTER(vp)]),
                 "rt_upload_scene": (i32, [vp, vp, sz, vp, sz, vp, sz]),
+                "rt_upload_spheres": (i32, [vp, vp, i32]),
                 "rt_render": (i32, [vp, C.POINTER(CameraUBO), i32, i32, i32, vp, vp, C.POINTER(Stats)]),
                 "rt_render_tile_device": (i32, [vp, C.POINTER(CameraUBO), i32, i32, i32, i32, i32, i32, i32,
                                                 vp, vp, vp, C.POINTER(Stats)]),

@@ -82,6 +82,13 @@ class Renderer:
         check(lib().rt_upload_scene(self._ctx, v.ctypes.data, v.nbytes, m.ctypes.data, m.nbytes,
                                     b.ctypes.data, b.nbytes))
 
+    def upload_spheres(self, spheres) -> None:
+        """Extension (option "extensions" bit 8; no reference counterpart):
+        float32[n, 8] = (centre.xyz, radius, albedo.rgb, type); n = 0 removes
+        them.  Deep copy; independent of upload_scene."""
+        s = np.ascontiguousarray(np.asarray(spheres, dtype=np.float32).reshape(-1, 8))
+        check(lib().rt_upload_spheres(self._ctx, s.ctypes.data if len(s) else None, len(s)))
+
     def upload_raw(self, vertices: bytes, materials: bytes, nodes: bytes) -> None:
         check(lib().rt_upload_scene(self._ctx, vertices, len(vertices), materials, len(materials),
                                     nodes, len(nodes)))

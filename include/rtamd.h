@@ -93,6 +93,16 @@ int rt_upload_scene(rt_ctx* ctx,
                     const void* materials, size_t material_bytes,
                     const void* bvh_nodes, size_t bvh_bytes);
 
+/* NON-REFERENCE extension (option "extensions" bit 8; the reference scene is
+ * triangles only): spheres, 8 floats each
+ * (centre.xyz, radius, albedo.rgb, material type 0-3 as the triangle
+ * materials), tested after every segment's BVH walk in index order against
+ * (T_MIN, closest_t); semantics in oracle/rt_oracle.h ORC_EXT_SPHERES.
+ * Deep-copies; n_spheres 0 removes them.  Independent of rt_upload_scene
+ * (a scene upload keeps them).  Radii must be finite and > 0, centres finite,
+ * n_spheres <= 65536. */
+int rt_upload_spheres(rt_ctx* ctx, const float* spheres, int n_spheres);
+
 /* Replaces VulkanEngine.renderFrame (VulkanEngine.java:401-431): renders one
  * width x height frame synchronously and copies it to host memory.
  * out_rgba    : width*height*4 bytes, RGBA8 UNORM, row 0 = top (required)
@@ -206,6 +216,7 @@ int rt_render_wait(rt_ctx* ctx, uint64_t ticket);
  *                       keeps the running sum of the linear colour (frame_count
  *                       0 overwrites it; a new frame partition starts from
  *                       zero) and the output is sqrt(sum / (frame_count+1))
+ *                   8 = spheres (rt_upload_spheres) after the BVH walk
  *   "prio_after"    kernel 0: raise a wave's priority after this many walk
  *                   steps (0 = never, default)
  *   "seg_limit"     split: segments traced in the first pass (default 2)

@@ -40,11 +40,13 @@ def lib() -> C.CDLL:
         L.orc_random_in_unit_sphere.argtypes = [C.POINTER(C.c_uint32), f3]
         L.orc_hit_aabb.argtypes = [f3, f3, f3, f3, C.c_float, C.c_float]
         L.orc_hit_triangle.argtypes = [f3, f3, f3, f3, f3, f3, f3]
+        L.orc_hit_sphere.argtypes = [f3, f3, f3, f3, f3]
         L.orc_scatter.argtypes = [f3, C.POINTER(C.c_uint32), f3, f3, f3, f3, f3]
         L.orc_render.argtypes = [C.c_void_p, C.c_size_t, C.c_void_p, C.c_size_t, C.c_void_p, C.c_size_t,
                                  C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
                                  C.c_int, C.c_void_p, C.c_void_p, C.POINTER(Counts), C.c_int]
         L.orc_render_ext.argtypes = L.orc_render.argtypes + [C.c_int, C.c_void_p]
+        L.orc_render_spheres.argtypes = L.orc_render_ext.argtypes + [C.c_void_p, C.c_int]
         _lib = L
     return _lib
 
@@ -54,15 +56,16 @@ def _buf(x):
     return a, a.ctypes.data, a.nbytes
 
 
-EXT_SKY_TOGGLE, EXT_EMISSIVE, EXT_ACCUMULATE = 1, 2, 4   # rt_oracle.h ORC_EXT_*
+EXT_SKY_TOGGLE, EXT_EMISSIVE, EXT_ACCUMULATE, EXT_SPHERES = 1, 2, 4, 8   # rt_oracle.h ORC_EXT_*
 
 
 def render(vertices, materials, nodes, camera_ubo: bytes, width: int, height: int, max_bounces: int,
            tile=None, row_step: int = 1, radiance: bool = True, n_threads: int = 0, ext: int = 0,
-           accum: "np.ndarray | None" = None):
+           accum: "np.ndarray | None" = None, spheres: "np.ndarray | None" = None):
     """Returns (rgba[rows, w, 4], radiance[rows, w, 3] or None, counts dict).
     ext: ORC_EXT_* bits (non-reference extensions); accum: float32[rows, w, 3],
-    updated in place, required with EXT_ACCUMULATE."""
+    updated in place, required with EXT_ACCUMULATE; spheres: float32[n, 8]
+    (centre.xyz, radius, albedo.rgb, type), tested with EXT_SPHERES."""
     x0, y0, tw, th = tile if tile is not None else (0, 0, width, height)
     rows = (th + row_step - 1) // row_step
     v, vp, vn = _buf(vertices)
@@ -74,10 +77,13 @@ def render(vertices, materials, nodes, camera_ubo: bytes, width: int, height: in
     c = Counts()
     if accum is not None:
         assert accum.dtype == np.float32 and accum.shape == (rows, tw, 3) and accum.flags.c_contiguous
-    rc = lib().orc_render_ext(vp, vn, mp, mn, bp, bn, cam.ctypes.data, width, height, max_bounces,
-                              x0, y0, tw, th, row_step, rgba.ctypes.data,
-                              rad.ctypes.data if rad is not None else None, C.byref(c), n_threads,
-                              ext, accum.ctypes.data if accum is not None else None)
+    sph = np.ascontiguousarray(spheres if spheres is not None else np.zeros((0, 8)), dtype=np.float32)
+    assert sph.ndim == 2 and sph.shape[1] == 8
+    rc = lib().orc_render_spheres(vp, vn, mp, mn, bp, bn, cam.ctypes.data, width, height, max_bounces,
+                                  x0, y0, tw, th, row_step, rgba.ctypes.data,
+                                  rad.ctypes.data if rad is not None else None, C.byref(c), n_threads,
+                                  ext, accum.ctypes.data if accum is not None else None,
+                                  sph.ctypes.data if len(sph) else None, len(sph))
     if rc != 0:
         raise RuntimeError(f"orc_render failed ({rc})")
     return rgba, rad, c.as_dict()

@@ -153,6 +153,31 @@ static int hit_triangle(ray r, vec3 v0, vec3 v1, vec3 v2,        /* :105-129 */
     return 0;
 }
 
+/* Extension ORC_EXT_SPHERES (no reference counterpart; the reference is
+ * triangles only).  The usual quadratic with half-b,
+ * the nearer root first, both against (T_MIN, closest_t); the normal is
+ * (p - c) / r, turned to face the ray like hit_triangle's (:125-127). */
+static int hit_sphere(ray r, vec3 c, float radius, float* closest_t, vec3* hit_normal) {
+    vec3 oc = sub3(r.origin, c);
+    float a = dot3(r.dir, r.dir);
+    float half_b = dot3(oc, r.dir);
+    float cc = dot3(oc, oc) - radius * radius;
+    float disc = half_b * half_b - a * cc;
+    if (!(disc >= 0.0f)) return 0;
+    float sq = sqrtf(disc);
+    float root = (-half_b - sq) / a;
+    if (!(root > T_MIN && root < *closest_t)) {
+        root = (-half_b + sq) / a;
+        if (!(root > T_MIN && root < *closest_t)) return 0;
+    }
+    *closest_t = root;
+    vec3 p = ray_at(r, root);
+    vec3 n = v3((p.x - c.x) / radius, (p.y - c.y) / radius, (p.z - c.z) / radius);
+    if (dot3(r.dir, n) > 0.0f) n = scale3(n, -1.0f);
+    *hit_normal = n;
+    return 1;
+}
+
 /* --------------------------------------------------------------- buffers -- */
 
 static float f32_at(const unsigned char* p, size_t off) { float f; memcpy(&f, p + off, 4); return f; }
@@ -163,6 +188,8 @@ typedef struct {
     const unsigned char* mats;    /* 16 B per triangle */
     const unsigned char* nodes;   /* 48 B per node */
     size_t n_nodes, n_tris, n_mats;
+    const float* spheres;         /* extension ORC_EXT_SPHERES: 8 floats per sphere */
+    int n_spheres;
 } scene;
 
 static vec3 vertex_pos(const scene* s, size_t i) {
@@ -170,9 +197,8 @@ static vec3 vertex_pos(const scene* s, size_t i) {
     return v3(f32_at(p, 0), f32_at(p, 4), f32_at(p, 8));
 }
 
-static int scatter(const scene* s, uint32_t* seed, ray r_in, int mat_index,   /* :132-154 */
+static int scatter(const unsigned char* m, uint32_t* seed, ray r_in,   /* :132-154; m = the 16-B material */
                    vec3 hit_pos, vec3 hit_normal, vec3* attenuation, ray* scattered) {
-    const unsigned char* m = s->mats + (size_t)mat_index * 16;
     vec3 albedo = v3(f32_at(m, 0), f32_at(m, 4), f32_at(m, 8));
     float type = f32_at(m, 12);
     if (type == 0.0f) {
@@ -259,18 +285,29 @@ static int shade_pixel(const scene* s, const orc_camera* cam, int W, int H, int 
             }
         }
         if (prof) prof[b] = (uint32_t)(cnt->node_visits - nv0) | ((uint32_t)(cnt->tri_tests - tt0) << 20);
-        if (hit_triangle_index != -1) {                                        /* :212 */
+        const unsigned char* hit_mat = hit_triangle_index != -1 ? s->mats + (size_t)hit_triangle_index * 16 : NULL;
+        if (ext & ORC_EXT_SPHERES) {
+            /* extension: after the BVH, every sphere in index order at the closest_t so far */
+            for (int k = 0; k < s->n_spheres; ++k) {
+                const float* sp_k = s->spheres + 8 * (size_t)k;
+                vec3 temp_normal;
+                if (hit_sphere(r, v3(sp_k[0], sp_k[1], sp_k[2]), sp_k[3], &closest_t, &temp_normal)) {
+                    hit_mat = (const unsigned char*)(sp_k + 4);
+                    hit_normal = temp_normal;
+                }
+            }
+        }
+        if (hit_mat) {                                                         /* :212 */
             vec3 hit_pos = ray_at(r, closest_t);
             vec3 mat_att;
             ray scattered;
             cnt->mat_reads++;
-            if ((ext & ORC_EXT_EMISSIVE) && f32_at(s->mats, (size_t)hit_triangle_index * 16 + 12) == 3.0f) {
+            if ((ext & ORC_EXT_EMISSIVE) && f32_at(hit_mat, 12) == 3.0f) {
                 /* extension: a type-3 material emits its albedo (the reference renders it black) */
-                const unsigned char* m = s->mats + (size_t)hit_triangle_index * 16;
-                final_color = mul3(attenuation, v3(f32_at(m, 0), f32_at(m, 4), f32_at(m, 8)));
+                final_color = mul3(attenuation, v3(f32_at(hit_mat, 0), f32_at(hit_mat, 4), f32_at(hit_mat, 8)));
                 break;
             }
-            if (scatter(s, &seed, r, hit_triangle_index, hit_pos, hit_normal, &mat_att, &scattered)) {
+            if (scatter(hit_mat, &seed, r, hit_pos, hit_normal, &mat_att, &scattered)) {
                 attenuation = mul3(attenuation, mat_att);
                 r = scattered;
             } else {
@@ -314,7 +351,7 @@ static int render_core(const void* vertices, size_t vertex_bytes,
                const orc_camera* cam, int width, int height, int max_bounces,
                int x0, int y0, int tile_w, int tile_h, int row_step,
                uint8_t* out_rgba, float* out_radiance, orc_counts* counts, int n_threads,
-               uint32_t* profile, int ext, float* accum);
+               uint32_t* profile, int ext, float* accum, const float* spheres, int n_spheres);
 
 int orc_render_profile(const void* vertices, size_t vertex_bytes,
                const void* materials, size_t material_bytes,
@@ -325,7 +362,7 @@ int orc_render_profile(const void* vertices, size_t vertex_bytes,
                uint32_t* profile) {
     return render_core(vertices, vertex_bytes, materials, material_bytes, bvh_nodes, bvh_bytes, cam, width,
                        height, max_bounces, x0, y0, tile_w, tile_h, row_step, out_rgba, out_radiance, counts,
-                       n_threads, profile, 0, NULL);
+                       n_threads, profile, 0, NULL, NULL, 0);
 }
 
 int orc_render_ext(const void* vertices, size_t vertex_bytes,
@@ -338,7 +375,21 @@ int orc_render_ext(const void* vertices, size_t vertex_bytes,
     if ((ext & ORC_EXT_ACCUMULATE) && !accum) return -2;
     return render_core(vertices, vertex_bytes, materials, material_bytes, bvh_nodes, bvh_bytes, cam, width,
                        height, max_bounces, x0, y0, tile_w, tile_h, row_step, out_rgba, out_radiance, counts,
-                       n_threads, NULL, ext, accum);
+                       n_threads, NULL, ext, accum, NULL, 0);
+}
+
+int orc_render_spheres(const void* vertices, size_t vertex_bytes,
+                       const void* materials, size_t material_bytes,
+                       const void* bvh_nodes, size_t bvh_bytes,
+                       const orc_camera* cam, int width, int height, int max_bounces,
+                       int x0, int y0, int tile_w, int tile_h, int row_step,
+                       uint8_t* out_rgba, float* out_radiance, orc_counts* counts, int n_threads,
+                       int ext, float* accum, const float* spheres, int n_spheres) {
+    if ((ext & ORC_EXT_ACCUMULATE) && !accum) return -2;
+    if (n_spheres < 0 || (n_spheres > 0 && !spheres)) return -2;
+    return render_core(vertices, vertex_bytes, materials, material_bytes, bvh_nodes, bvh_bytes, cam, width,
+                       height, max_bounces, x0, y0, tile_w, tile_h, row_step, out_rgba, out_radiance, counts,
+                       n_threads, NULL, ext, accum, spheres, n_spheres);
 }
 
 static int render_core(const void* vertices, size_t vertex_bytes,
@@ -347,7 +398,7 @@ static int render_core(const void* vertices, size_t vertex_bytes,
                const orc_camera* cam, int width, int height, int max_bounces,
                int x0, int y0, int tile_w, int tile_h, int row_step,
                uint8_t* out_rgba, float* out_radiance, orc_counts* counts, int n_threads,
-               uint32_t* profile, int ext, float* accum) {
+               uint32_t* profile, int ext, float* accum, const float* spheres, int n_spheres) {
     if (!cam || width < 1 || height < 1 || max_bounces < 1 || tile_w < 1 || tile_h < 1 ||
         x0 < 0 || y0 < 0 || x0 + tile_w > width || y0 + tile_h > height || row_step < 1)
         return -2;
@@ -358,6 +409,8 @@ static int render_core(const void* vertices, size_t vertex_bytes,
     s.n_nodes = bvh_bytes / 48;
     s.n_tris = vertex_bytes / 48;
     s.n_mats = material_bytes / 16;
+    s.spheres = spheres;
+    s.n_spheres = (ext & ORC_EXT_SPHERES) ? n_spheres : 0;
     const int rows = (tile_h + row_step - 1) / row_step;
     uint64_t seg = 0, nodes = 0, tris = 0, mats = 0;
     int err = 0;
@@ -433,6 +486,18 @@ int orc_hit_triangle(const float origin[3], const float dir[3], const float v0[3
     return h;
 }
 
+int orc_hit_sphere(const float origin[3], const float dir[3], const float centre_radius[4],
+                   float* closest_t, float normal[3]) {
+    ray r;
+    r.origin = v3(origin[0], origin[1], origin[2]);
+    r.dir = v3(dir[0], dir[1], dir[2]);
+    vec3 n = v3(0.0f, 0.0f, 0.0f);
+    int h = hit_sphere(r, v3(centre_radius[0], centre_radius[1], centre_radius[2]), centre_radius[3],
+                       closest_t, &n);
+    normal[0] = n.x; normal[1] = n.y; normal[2] = n.z;
+    return h;
+}
+
 int orc_scatter(const float material[4], uint32_t* seed, const float dir_in[3],
                 const float hit_pos[3], const float normal[3], float att[3], float dir_out[3]) {
     scene s;
@@ -445,7 +510,7 @@ int orc_scatter(const float material[4], uint32_t* seed, const float dir_in[3],
     vec3 a = v3(0.0f, 0.0f, 0.0f);
     sc.origin = v3(0.0f, 0.0f, 0.0f);
     sc.dir = v3(0.0f, 0.0f, 0.0f);
-    int ok = scatter(&s, seed, r_in, 0, v3(hit_pos[0], hit_pos[1], hit_pos[2]),
+    int ok = scatter(s.mats, seed, r_in, v3(hit_pos[0], hit_pos[1], hit_pos[2]),
                      v3(normal[0], normal[1], normal[2]), &a, &sc);
     att[0] = a.x; att[1] = a.y; att[2] = a.z;
     dir_out[0] = sc.dir.x; dir_out[1] = sc.dir.y; dir_out[2] = sc.dir.z;
@@ -465,6 +530,8 @@ int orc_trace_pixel(const void* vertices, size_t vertex_bytes, const void* mater
     s.n_nodes = bvh_bytes / 48;
     s.n_tris = vertex_bytes / 48;
     s.n_mats = material_bytes / 16;
+    s.spheres = NULL;
+    s.n_spheres = 0;
     g_trace = out;
     g_trace_cap = cap;
     g_trace_n = 0;

@@ -23,6 +23,8 @@ int      orc_hit_aabb(const float origin[3], const float dir[3], const float bmi
                       const float bmax[3], float t_min, float t_max);
 int      orc_hit_triangle(const float origin[3], const float dir[3], const float v0[3],
                           const float v1[3], const float v2[3], float* closest_t, float normal[3]);
+int      orc_hit_sphere(const float origin[3], const float dir[3], const float centre_radius[4],
+                        float* closest_t, float normal[3]);   /* extension ORC_EXT_SPHERES */
 int      orc_scatter(const float material[4], uint32_t* seed, const float dir_in[3],
                      const float hit_pos[3], const float normal[3], float att[3], float dir_out[3]);
 
@@ -53,10 +55,21 @@ int orc_render_profile(const void* vertices, size_t vertex_bytes,
  *   ORC_EXT_ACCUMULATE  seed += frame_count * W * H; accum (3 floats per output
  *                       pixel, packed like out_rgba) holds the running sum of the
  *                       linear colour (frame_count 0 overwrites it); the output is
- *                       sqrt(sum / (frame_count + 1)) */
+ *                       sqrt(sum / (frame_count + 1))
+ *   ORC_EXT_SPHERES     orc_render_spheres' spheres (8 floats each: centre.xyz,
+ *                       radius, albedo.rgb, material type) are tested after the
+ *                       BVH walk of every segment, in index order, against
+ *                       (T_MIN, closest_t): oc = o - c, a = dot(d,d), half_b =
+ *                       dot(oc,d), disc = half_b^2 - a*(dot(oc,oc) - r*r); the
+ *                       root (-half_b - sqrt(disc))/a, else (-half_b +
+ *                       sqrt(disc))/a; normal (p - c)/r turned to face the ray.
+ *                       A sphere hit shades with the sphere's material and
+ *                       counts one material read; node / triangle counts are
+ *                       unchanged. */
 #define ORC_EXT_SKY_TOGGLE 1
 #define ORC_EXT_EMISSIVE   2
 #define ORC_EXT_ACCUMULATE 4
+#define ORC_EXT_SPHERES    8
 int orc_render_ext(const void* vertices, size_t vertex_bytes,
                    const void* materials, size_t material_bytes,
                    const void* bvh_nodes, size_t bvh_bytes,
@@ -64,4 +77,11 @@ int orc_render_ext(const void* vertices, size_t vertex_bytes,
                    int x0, int y0, int tile_w, int tile_h, int row_step,
                    uint8_t* out_rgba, float* out_radiance, orc_counts* counts, int n_threads,
                    int ext, float* accum);
+int orc_render_spheres(const void* vertices, size_t vertex_bytes,
+                       const void* materials, size_t material_bytes,
+                       const void* bvh_nodes, size_t bvh_bytes,
+                       const orc_camera* cam, int width, int height, int max_bounces,
+                       int x0, int y0, int tile_w, int tile_h, int row_step,
+                       uint8_t* out_rgba, float* out_radiance, orc_counts* counts, int n_threads,
+                       int ext, float* accum, const float* spheres, int n_spheres);
 #endif

@@ -67,12 +67,17 @@ def random_in_unit_sphere(seed: np.ndarray):                  # :63-70
 
 
 def render(vertices, materials, nodes, camera_ubo: bytes, width: int, height: int, max_bounces: int,
-           rows=None, ext: int = 0, accum=None):
+           rows=None, ext: int = 0, accum=None, spheres=None):
     """Returns (rgba[len(rows), W, 4], radiance[len(rows), W, 3], counts dict).
-    ext / accum: the non-reference extensions of oracle/rt_oracle.h (ORC_EXT_*),
-    restated independently; accum float32[len(rows), W, 3] is updated in place."""
-    V = np.frombuffer(bytes(vertices), np.float32).reshape(-1, 3, 4)[:, :, :3]
-    M = np.frombuffer(bytes(materials), np.float32).reshape(-1, 4)
+    ext / accum / spheres: the non-reference extensions of oracle/rt_oracle.h
+    (ORC_EXT_*), restated independently; accum float32[len(rows), W, 3] is
+    updated in place; spheres float32[n, 8] = (centre.xyz, radius, albedo.rgb,
+    type), hit-tested after the BVH walk with ext bit 8."""
+    V = np.frombuffer(bytes(vertices), np.float32)
+    V = V[: (V.size // 12) * 12].reshape(-1, 3, 4)[:, :, :3]    # (the empty scene's 1-float dummy: none)
+    M = np.frombuffer(bytes(materials), np.float32)
+    M = M[: (M.size // 4) * 4].reshape(-1, 4)
+    S = np.asarray(spheres if (spheres is not None and ext & 8) else np.zeros((0, 8)), F).reshape(-1, 8)
     nb = np.frombuffer(bytes(nodes), np.uint8)
     nb = nb[: (nb.size // 48) * 48].reshape(-1, 48)
     BMIN = nb[:, 0:12].copy().view(np.float32).reshape(-1, 3)
@@ -175,7 +180,33 @@ def render(vertices, materials, nodes, camera_ubo: bytes, width: int, height: in
             if (sp > 62).any():
                 raise RuntimeError("stack overflow (reference int stack[64])")
 
-        gh = hit >= 0
+        # extension: spheres after the BVH walk, in index order; hit = -2 - k
+        for k in range(S.shape[0]):
+            cx, cy, cz, rad_k = S[k, 0], S[k, 1], S[k, 2], S[k, 3]
+            ocx = rox - cx; ocy = roy - cy; ocz = roz - cz
+            qa = _dot(rdx, rdy, rdz, rdx, rdy, rdz)
+            hb_ = _dot(ocx, ocy, ocz, rdx, rdy, rdz)
+            qc = _dot(ocx, ocy, ocz, ocx, ocy, ocz) - rad_k * rad_k
+            with np.errstate(invalid="ignore", divide="ignore", over="ignore"):
+                disc = hb_ * hb_ - qa * qc
+                sq = np.sqrt(np.where(disc >= F(0.0), disc, F(0.0)))
+                r1 = (-hb_ - sq) / qa
+                r2 = (-hb_ + sq) / qa
+            in1 = (r1 > T_MIN) & (r1 < closest)
+            in2 = (r2 > T_MIN) & (r2 < closest)
+            root = np.where(in1, r1, r2)
+            ok = (disc >= F(0.0)) & (in1 | in2)
+            g = np.nonzero(ok)[0]
+            if g.size == 0:
+                continue
+            closest[g] = root[g]
+            hit[g] = -2 - k
+            px_ = rox[g] + rdx[g] * root[g]; py_ = roy[g] + rdy[g] * root[g]; pz_ = roz[g] + rdz[g] * root[g]
+            snx = (px_ - cx) / rad_k; sny = (py_ - cy) / rad_k; snz = (pz_ - cz) / rad_k
+            flip = _dot(rdx[g], rdy[g], rdz[g], snx, sny, snz) > F(0.0)
+            nx[g] = np.where(flip, -snx, snx); ny[g] = np.where(flip, -sny, sny); nz[g] = np.where(flip, -snz, snz)
+
+        gh = hit != -1
         # miss: final = att * sky, path ends (:224-227)
         ms = act[~gh]
         if ms.size:
@@ -193,7 +224,9 @@ def render(vertices, materials, nodes, camera_ubo: bytes, width: int, height: in
             ga = act[hs]
             hpx = rox[hs] + rdx[hs] * closest[hs]; hpy = roy[hs] + rdy[hs] * closest[hs]
             hpz = roz[hs] + rdz[hs] * closest[hs]
-            mat = M[hit[hs]]
+            hh = hit[hs]
+            mat = np.where((hh >= 0)[:, None], M[np.maximum(hh, 0)] if M.shape[0] else F(0.0),
+                           S[np.maximum(-2 - hh, 0), 4:8] if S.shape[0] else F(0.0)).astype(F)
             typ = mat[:, 3]
             hnx, hny, hnz = nx[hs], ny[hs], nz[hs]
             ndx = dx[ga].copy(); ndy = dy[ga].copy(); ndz = dz[ga].copy()

@@ -465,3 +465,81 @@ def test_accumulation_bit_exact(devices):
             _assert_same(rgba, rad, None, *ref)
     finally:
         r.close()
+
+
+@pytest.mark.parametrize("ext,sky,walk", [(8, 1, 2), (10, 1, 2), (9, 0, 2), (11, 0, 0), (10, 1, 1)])
+def test_spheres_bit_exact(renderer, ext, sky, walk):
+    """Extension bit 8 (spheres after the BVH walk; no reference counterpart)
+    matches the oracle's ORC_EXT_SPHERES bit for bit, with counters, in every
+    walk; spheres stay uploaded but unused with the bit off."""
+    from test_oracle_kat import SPHERES
+    from rtamd import build_buffers, configs, triangles_of
+    verts, mats = triangles_of(configs.config2().scene)
+    built = build_buffers(verts, mats)
+    renderer.upload_scene(built)
+    renderer.upload_spheres(SPHERES)
+    w, h, b = 200, 120, 5
+    cam = configs.Camera.default(w, h)
+    cam.ubo.sky_enabled = sky
+    try:
+        renderer.set_option("walk", walk)
+        renderer.set_option("extensions", ext)
+        for _ in range(2):          # the learning launch, then the learned order
+            rgba, rad, st = renderer.render(cam, w, h, b, radiance=True, stats=True)
+            _assert_same(rgba, rad, st, *_oracle(built, cam.ubo_bytes(), w, h, b, ext=ext, spheres=SPHERES))
+        renderer.set_option("extensions", ext & ~8)
+        rgba, rad, st = renderer.render(cam, w, h, b, radiance=True, stats=True)
+        _assert_same(rgba, rad, st, *_oracle(built, cam.ubo_bytes(), w, h, b, ext=ext & ~8))
+    finally:
+        renderer.set_option("extensions", 0)
+        renderer.upload_spheres(np.zeros((0, 8), np.float32))
+        for k, v in DEFAULT_OPTS.items():
+            renderer.set_option(k, v)
+
+
+def test_spheres_large_scene_and_empty_scene(renderer):
+    """Spheres beside the 50k-triangle scene (sampled rows), and spheres alone
+    with the reference's empty-scene dummies."""
+    from test_oracle_kat import SPHERES
+    from rtamd import build_buffers, configs, triangles_of
+    cfg = configs.config3()
+    built = cfg.build()
+    big = SPHERES.copy()
+    big[:, :3] *= 3.0
+    big[:, 3] *= 2.5
+    try:
+        renderer.upload_scene(built)
+        renderer.upload_spheres(big)
+        renderer.set_option("extensions", 8 | 2)
+        cam = cfg.camera()
+        rgba, rad, st = _bands_device(renderer, cam, cfg.width, cfg.height, cfg.max_bounces, 1, 16, 5)
+        ref = _oracle(built, cam.ubo_bytes(), cfg.width, cfg.height, cfg.max_bounces,
+                      tile=(0, 5, cfg.width, cfg.height - 5), row_step=16, ext=8 | 2, spheres=big)
+        _assert_same(rgba, rad, st, *ref)
+        verts, mats = triangles_of(configs.config2().scene)
+        empty = build_buffers(verts[:0], mats[:0])
+        renderer.upload_scene(empty)            # a scene upload keeps the spheres
+        w, h, b = 96, 64, 4
+        cam = configs.Camera.default(w, h)
+        rgba, rad, st = renderer.render(cam, w, h, b, radiance=True, stats=True)
+        _assert_same(rgba, rad, st, *_oracle(empty, cam.ubo_bytes(), w, h, b, ext=8 | 2, spheres=big))
+        assert st["mat_reads"] > 0 and st["node_visits"] == 0
+    finally:
+        renderer.set_option("extensions", 0)
+        renderer.upload_spheres(np.zeros((0, 8), np.float32))
+
+
+def test_spheres_upload_validation(renderer):
+    from rtamd import RtError
+    bad = np.zeros((1, 8), np.float32)
+    for r in (0.0, -1.0, np.inf, np.nan):
+        bad[0, 3] = r
+        with pytest.raises(RtError, match="INVALID_ARG"):
+            renderer.upload_spheres(bad)
+    bad[0, 3] = 1.0
+    bad[0, 0] = np.nan
+    with pytest.raises(RtError, match="INVALID_ARG"):
+        renderer.upload_spheres(bad)
+    with pytest.raises(RtError, match="INVALID_ARG"):
+        renderer.upload_spheres(np.zeros((65537, 8), np.float32) + np.float32(1.0))
+    renderer.upload_spheres(np.zeros((0, 8), np.float32))

@@ -256,3 +256,91 @@ def test_accumulation_c_vs_numpy():
                             cam.ubo_bytes(), w, h, 4)[0]
     assert np.array_equal(frames[0], ref)       # frame 0 is the reference's frame
     assert (frames[1] != frames[0]).any()
+
+
+# ---- extension ORC_EXT_SPHERES (no reference counterpart) -------------------
+
+SPHERES = np.array([
+    (-14.0, -4.0, 4.0, 6.0, 0.8, 0.3, 0.3, 0.0),    # Lambert, resting on the ground plane
+    (14.0, -5.0, -6.0, 5.0, 0.9, 0.9, 0.9, 1.0),    # mirror
+    (0.0, 10.0, -12.0, 4.0, 0.7, 0.8, 0.3, 2.0),    # fuzzy metal
+    (7.0, -8.0, 14.0, 2.0, 6.0, 6.0, 6.0, 3.0),     # type 3 (an emitter with EXT_EMISSIVE)
+    (-3.0, 3.0, 3.0, 3.0, 0.2, 0.4, 0.9, 0.0),      # cuts a corner of the cube
+], np.float32)
+
+
+def _f3(*v):
+    import ctypes as C
+    return (C.c_float * len(v))(*v)
+
+
+def test_hit_sphere_kat():
+    import ctypes as C
+    from oracle import oracle_lib
+    L = oracle_lib.lib()
+    t = C.c_float(10000.0)
+    n = _f3(0, 0, 0)
+    # from outside, head on: the nearer root, t = 4, normal +z
+    assert L.orc_hit_sphere(_f3(0, 0, 5), _f3(0, 0, -1), _f3(0, 0, 0, 1), C.byref(t), n) == 1
+    assert t.value == 4.0 and list(n) == [0.0, 0.0, 1.0]
+    # from inside: the far root; the normal is turned to face the ray
+    t = C.c_float(10000.0)
+    assert L.orc_hit_sphere(_f3(0, 0, 0), _f3(0, 0, -1), _f3(0, 0, 0, 2), C.byref(t), n) == 1
+    assert t.value == 2.0 and list(n) == [0.0, 0.0, 1.0]
+    # closest_t bounds both roots; a miss leaves closest_t alone
+    t = C.c_float(3.5)
+    assert L.orc_hit_sphere(_f3(0, 0, 5), _f3(0, 0, -1), _f3(0, 0, 0, 1), C.byref(t), n) == 0
+    assert t.value == np.float32(3.5)
+    t = C.c_float(10000.0)
+    assert L.orc_hit_sphere(_f3(0, 3, 5), _f3(0, 0, -1), _f3(0, 0, 0, 1), C.byref(t), n) == 0
+    # behind the origin: both roots <= T_MIN
+    assert L.orc_hit_sphere(_f3(0, 0, -5), _f3(0, 0, -1), _f3(0, 0, 0, 1), C.byref(t), n) == 0
+    # grazing: disc == 0 hits at the tangent point
+    t = C.c_float(10000.0)
+    assert L.orc_hit_sphere(_f3(1, 0, 5), _f3(0, 0, -1), _f3(0, 0, 0, 1), C.byref(t), n) == 1
+    assert t.value == 5.0
+
+
+@pytest.mark.parametrize("ext,sky", [(8, 1), (10, 1), (9, 0), (8 | 2 | 1, 0)])
+def test_spheres_c_vs_numpy(ext, sky):
+    """Spheres after the BVH walk agree bit for bit between the C oracle and
+    the numpy restatement; primary-segment BVH counts are unchanged by them."""
+    from oracle import oracle_lib, shader_np
+    from rtamd import build_buffers, configs, triangles_of
+    verts, mats = triangles_of(configs.config2().scene)
+    built = build_buffers(verts, mats)
+    w, h = 96, 54
+    cam = configs.Camera.default(w, h)
+    cam.ubo.sky_enabled = sky
+    args = (built.model_vertex_data, built.model_material_data, built.flat_bvh_data, cam.ubo_bytes(), w, h, 5)
+    rgba_c, rad_c, cnt_c = oracle_lib.render(*args, ext=ext, spheres=SPHERES)
+    rgba_n, rad_n, cnt_n = shader_np.render(*args, ext=ext, spheres=SPHERES)
+    assert np.array_equal(rgba_c, rgba_n)
+    assert np.array_equal(rad_c.view(np.uint32), rad_n.view(np.uint32))
+    assert cnt_c == cnt_n
+    base, _, cnt_b = oracle_lib.render(*args, ext=ext & ~8)
+    if sky or ext & 2:                          # (sky off and no emitter: all black)
+        assert (rgba_c != base).any()
+    # spheres passed without the bit are ignored
+    assert np.array_equal(oracle_lib.render(*args, ext=ext & ~8, spheres=SPHERES)[0], base)
+    # one bounce: the same BVH walk; mat_reads grows by the sphere hits
+    one = args[:-1] + (1,)
+    _, _, c1 = oracle_lib.render(*one, ext=ext, spheres=SPHERES)
+    _, _, b1 = oracle_lib.render(*one, ext=ext & ~8)
+    assert (c1["node_visits"], c1["tri_tests"]) == (b1["node_visits"], b1["tri_tests"])
+    assert c1["mat_reads"] > b1["mat_reads"]
+
+
+def test_spheres_only_scene():
+    """Spheres with the reference's empty-scene dummies (no triangles)."""
+    from oracle import oracle_lib, shader_np
+    from rtamd import build_buffers, configs, triangles_of
+    verts, mats = triangles_of(configs.config2().scene)
+    built = build_buffers(verts[:0], mats[:0])
+    w, h = 64, 36
+    cam = configs.Camera.default(w, h)
+    args = (built.model_vertex_data, built.model_material_data, built.flat_bvh_data, cam.ubo_bytes(), w, h, 4)
+    rgba_c, rad_c, cnt_c = oracle_lib.render(*args, ext=8 | 2, spheres=SPHERES)
+    rgba_n, rad_n, cnt_n = shader_np.render(*args, ext=8 | 2, spheres=SPHERES)
+    assert np.array_equal(rad_c.view(np.uint32), rad_n.view(np.uint32)) and cnt_c == cnt_n
+    assert cnt_c["node_visits"] == 0 and cnt_c["mat_reads"] > 0
