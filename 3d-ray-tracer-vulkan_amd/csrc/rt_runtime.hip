@@ -255,6 +255,11 @@ struct PerDevice {
     std::vector<uint8_t> learning_key;
     size_t       learning_n = 0;
     int          last_heavy = 0;    // heavy tiles of the last launch (option "heavy_tiles_used", read only)
+    // option graph: plain launches captured once per launch key into a HIP
+    // graph and replayed (the heavy-tile fork / join becomes graph edges)
+    struct Graph { std::vector<uint64_t> key; hipGraphExec_t exec; };
+    std::vector<Graph> graphs;
+    unsigned     graph_next = 0;
 };
 
 static constexpr size_t kMaxOrders = 16;
@@ -266,6 +271,12 @@ static void free_orders(PerDevice& p) {
     for (auto& o : p.orders) (void)hipFree(o.d_order);
     p.orders.clear();
 }
+
+static void free_graphs(PerDevice& p) {
+    for (auto& g : p.graphs) (void)hipGraphExecDestroy(g.exec);
+    p.graphs.clear();
+}
+static constexpr size_t kMaxGraphs = 8;
 
 static constexpr unsigned kQueueSlots = 64;
 
@@ -288,6 +299,7 @@ struct rt_ctx {
     int  heavy_first = 1;          // kernel 0: dispatch tiles in the cost order of a learning launch
     int  heavy_factor = 150;       // automatic heavy tiles: walk length above this percentage of the bulk estimate
     int  learn_cost = 1;           // heavy_first cost: 0 = lockstep steps + 2 x coop windows, 1 = wave duration
+    int  graph = 1;                // kernel 0 plain launches: replay a captured HIP graph per launch key
     int  heavy_stream = 1;         // heavy_tiles: 1 = their launch runs on an auxiliary stream, concurrent
                                    //   with the other tiles; 0 = before them on the same stream
     int  heavy_tiles = -1;         // heavy_first: the this-many most expensive tiles are traced one pixel
@@ -517,6 +529,67 @@ static int set_schedule(const rt_ctx* ctx, PerDevice& p, TraceArgs& a, const rt_
     return plan_order(ctx, p, a, cam);
 }
 
+// Option graph: a plain kernel-0 launch (no counters, no diagnostics) is
+// captured once per launch key into a HIP graph and replayed afterwards.  The
+// key is every launch parameter the kernels read (scene, camera, frame
+// geometry, schedule, learned order, heavy-tile count, outputs) plus the
+// stream; the work counters, queue slots and the auxiliary stream / events a
+// launch rotates through are not kernel inputs of the simple kernel.  In the
+// captured graph the heavy-tile fork / join are edges, not events.
+static std::vector<uint64_t> launch_key(const TraceArgs& a, hipStream_t s) {
+    auto P = [](const void* q) { return (uint64_t)(uintptr_t)q; };
+    auto F = [](float f) { uint32_t u; std::memcpy(&u, &f, 4); return (uint64_t)u; };
+    const DevScene& sc = a.scene;
+    const CamF& c = a.cam;
+    return {P(s), P(sc.nodes), P(sc.leafs), P(sc.pairs), P(sc.norms), P(sc.mats), P(sc.spheres),
+            (uint64_t)sc.n_spheres, (uint64_t)sc.n_nodes, (uint64_t)sc.end, (uint64_t)sc.n_tris,
+            (uint64_t)sc.root_leaf, F(sc.root_box[0]), F(sc.root_box[1]), F(sc.root_box[2]), F(sc.root_box[3]),
+            F(sc.root_box[4]), F(sc.root_box[5]),
+            F(c.ox), F(c.oy), F(c.oz), F(c.lx), F(c.ly), F(c.lz), F(c.hx), F(c.hy), F(c.hz), F(c.vx), F(c.vy), F(c.vz),
+            (uint64_t)a.width, (uint64_t)a.height, (uint64_t)a.max_bounces, (uint64_t)a.x0, (uint64_t)a.y0,
+            (uint64_t)a.tw, (uint64_t)a.th, (uint64_t)a.band_h, (uint64_t)a.band_stride, (uint64_t)a.band_off,
+            P(a.out_rgba), P(a.out_rad), (uint64_t)a.wave_tile, (uint64_t)a.seg_limit, (uint64_t)a.prio_after,
+            (uint64_t)a.heavy_budget, (uint64_t)a.coop_lanes, (uint64_t)a.ext, (uint64_t)a.sky_enabled,
+            (uint64_t)a.frame_count, P(a.accum), (uint64_t)a.walk, (uint64_t)a.block_waves, P(a.tile_order),
+            (uint64_t)a.heavy_tiles, (uint64_t)(a.aux_stream != nullptr), (uint64_t)a.coop_walk,
+            (uint64_t)a.kernel};
+}
+
+static int launch(const rt_ctx* ctx, PerDevice& p, const TraceArgs& a, hipStream_t s) {
+    if (!ctx->graph || s == nullptr || a.counters || a.diag || a.kernel != kKernelSimple) {
+        RT_HIP_CHECK(launch_trace(a, s));
+        return RT_OK;
+    }
+    std::vector<uint64_t> key = launch_key(a, s);
+    for (auto& g : p.graphs)
+        if (g.key == key) {
+            RT_HIP_CHECK(hipGraphLaunch(g.exec, s));
+            return RT_OK;
+        }
+    hipGraph_t graph = nullptr;
+    RT_HIP_CHECK(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+    const hipError_t le = launch_trace(a, s);
+    const hipError_t ce = hipStreamEndCapture(s, &graph);
+    if (le != hipSuccess || ce != hipSuccess) {
+        if (graph) (void)hipGraphDestroy(graph);
+        set_error("graph capture: %s", hipGetErrorString(le != hipSuccess ? le : ce));
+        return RT_ERR_HIP;
+    }
+    hipGraphExec_t exec = nullptr;
+    const hipError_t ie = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
+    (void)hipGraphDestroy(graph);
+    if (ie != hipSuccess) { set_error("graph instantiate: %s", hipGetErrorString(ie)); return RT_ERR_HIP; }
+    if (p.graphs.size() >= kMaxGraphs) {          // replace the oldest-inserted entry
+        const size_t k = p.graph_next++ % kMaxGraphs;
+        (void)hipGraphExecDestroy(p.graphs[k].exec);
+        p.graphs[k] = PerDevice::Graph{std::move(key), exec};
+    } else {
+        p.graphs.push_back(PerDevice::Graph{std::move(key), exec});
+    }
+    RT_HIP_CHECK(hipGraphLaunch(exec, s));
+    return RT_OK;
+}
+
 static CamF cam_from_ubo(const rt_camera_ubo* c) {
     CamF f;
     f.ox = c->origin[0];     f.oy = c->origin[1];     f.oz = c->origin[2];
@@ -555,6 +628,7 @@ int rt_create(const int* device_ids, int n_devices, rt_ctx** out) {
     if (const char* v = std::getenv("RTAMD_LEARN_COST")) ctx->learn_cost = std::atoi(v) ? 1 : 0;
     if (const char* v = std::getenv("RTAMD_HEAVY_FACTOR")) ctx->heavy_factor = std::max(10, std::atoi(v));
     if (const char* v = std::getenv("RTAMD_HEAVY_STREAM")) ctx->heavy_stream = std::atoi(v) ? 1 : 0;
+    if (const char* v = std::getenv("RTAMD_GRAPH")) ctx->graph = std::atoi(v) ? 1 : 0;
     if (const char* v = std::getenv("RTAMD_BLOCK_WAVES")) ctx->block_waves = std::atoi(v) == 1 ? 1 : 4;
     if (const char* v = std::getenv("RTAMD_COOP_LANES")) ctx->coop_lanes = std::max(0, std::min(64, std::atoi(v)));
     if (const char* v = std::getenv("RTAMD_SEG_LIMIT")) ctx->seg_limit = std::max(1, std::min(1024, std::atoi(v)));
@@ -619,6 +693,7 @@ int rt_destroy(rt_ctx* ctx) {
         if (p.d_diag) (void)hipFree(p.d_diag);
         if (p.d_learn) (void)hipFree(p.d_learn);
         free_orders(p);
+        free_graphs(p);
         for (int k = 0; k < 4; ++k) {
             if (p.aux[k]) (void)hipStreamDestroy(p.aux[k]);
             if (p.aux_fork[k]) (void)hipEventDestroy(p.aux_fork[k]);
@@ -797,7 +872,7 @@ int rt_render_tile_device(rt_ctx* ctx, const rt_camera_ubo* cam, int width, int 
         RT_HIP_CHECK(hipMemsetAsync(p.d_counters, 0, sizeof(Counters), s));
         RT_HIP_CHECK(hipEventRecord(p.ev0, s));
     }
-    RT_HIP_CHECK(launch_trace(a, s));
+    if (int rl = launch(ctx, p, a, s)) return rl;
     if (int ro = learn_order(p, a, s, ctx->learn_cost, ctx->heavy_factor / 100.0)) return ro;
     if (stats) {
         RT_HIP_CHECK(hipEventRecord(p.ev1, s));
@@ -830,11 +905,13 @@ static int render_bands_on(const rt_ctx* ctx, PerDevice& p, const rt_camera_ubo*
     a.out_rad = d_rad;
     a.counters = count ? p.d_counters : nullptr;
     if (int rs = set_schedule(ctx, p, a, cam)) return rs;
-    if (count) RT_HIP_CHECK(hipMemsetAsync(p.d_counters, 0, sizeof(Counters), s));
-    RT_HIP_CHECK(hipEventRecord(p.ev0, s));
-    RT_HIP_CHECK(launch_trace(a, s));
+    if (count) {
+        RT_HIP_CHECK(hipMemsetAsync(p.d_counters, 0, sizeof(Counters), s));
+        RT_HIP_CHECK(hipEventRecord(p.ev0, s));   // the timing events exist for stats only
+    }
+    if (int rl = launch(ctx, p, a, s)) return rl;
     if (int ro = learn_order(p, a, s, ctx->learn_cost, ctx->heavy_factor / 100.0)) return ro;
-    RT_HIP_CHECK(hipEventRecord(p.ev1, s));
+    if (count) RT_HIP_CHECK(hipEventRecord(p.ev1, s));
     return RT_OK;
 }
 
@@ -1068,6 +1145,8 @@ int rt_set_option(rt_ctx* ctx, const char* name, int64_t value) {
         ctx->learn_cost = (int)value;
     } else if (std::strcmp(name, "heavy_stream") == 0 && (value == 0 || value == 1)) {
         ctx->heavy_stream = (int)value;
+    } else if (std::strcmp(name, "graph") == 0 && (value == 0 || value == 1)) {
+        ctx->graph = (int)value;
     } else if (std::strcmp(name, "diag") == 0 && (value == 0 || value == 1)) {
         ctx->diag = (int)value;
     } else if (std::strcmp(name, "wave_tile") == 0 && value >= 0 && value <= 3) {
@@ -1094,6 +1173,7 @@ int rt_get_option(rt_ctx* ctx, const char* name, int64_t* value) {
     else if (std::strcmp(name, "heavy_first") == 0) *value = ctx->heavy_first;
     else if (std::strcmp(name, "heavy_tiles") == 0) *value = ctx->heavy_tiles;
     else if (std::strcmp(name, "heavy_stream") == 0) *value = ctx->heavy_stream;
+    else if (std::strcmp(name, "graph") == 0) *value = ctx->graph;
     else if (std::strcmp(name, "learn_cost") == 0) *value = ctx->learn_cost;
     else if (std::strcmp(name, "heavy_factor") == 0) *value = ctx->heavy_factor;
     else if (std::strcmp(name, "heavy_tiles_used") == 0) *value = ctx->dev.empty() ? 0 : ctx->dev[0].last_heavy;

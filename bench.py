@@ -259,7 +259,7 @@ def main() -> None:
                 "frames_verified": verified,
                 "parallelism": f"tile{world}",
                 "schedule": {**{k: renderer.get_option(k) for k in ("kernel", "walk", "wave_tile", "coop_lanes",
-                                                                      "heavy_first", "heavy_tiles", "heavy_factor")},
+                                                                      "heavy_first", "heavy_tiles", "heavy_factor", "graph")},
                              "heavy_tiles_used": heavy_used},
                 "launches_per_step": F * (2 if heavy_used > 0 else 1),
             },

@@ -200,6 +200,11 @@ int rt_render_wait(rt_ctx* ctx, uint64_t ticket);
  *                   forked from and joined back to the caller's stream,
  *                   concurrently with the other tiles; 0 = before them on the
  *                   caller's stream
+ *   "graph"         kernel 0, plain launches on a non-null stream: 1 (default)
+ *                   = captured once per launch key (scene, camera, frame,
+ *                   schedule, learned order, outputs, stream) into a HIP
+ *                   graph and replayed; 0 = launched directly.  Counting and
+ *                   learning launches are never captured.  Same results.
  *   "learn_cost"    heavy_first order by 1 = wave duration (default) or 0 =
  *                   walk length
  *   "heavy_tiles_used" (rt_get_option only) heavy tiles of the last launch

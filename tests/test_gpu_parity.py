@@ -17,7 +17,7 @@ COUNTERS = ("segments", "node_visits", "tri_tests", "mat_reads")
 DEFAULT_OPTS = {"kernel": 0, "shade_min": 16, "blocks_per_cu": 0, "wave_tile": 2, "seg_limit": 2,
                 "heavy_budget": 256, "prio_after": 0, "coop_lanes": 2, "walk": 2, "coop_walk": 0,
                 "block_waves": 1, "heavy_first": 1, "heavy_tiles": -1, "heavy_stream": 1,
-                "learn_cost": 1, "heavy_factor": 150}
+                "learn_cost": 1, "heavy_factor": 150, "graph": 1}
 
 
 def _oracle(built, cam_bytes, w, h, b, **kw):
@@ -135,6 +135,8 @@ def test_config5_1m_row_subset(renderer):
     {"kernel": 0, "coop_walk": 1},
     {"kernel": 0, "block_waves": 4},
     {"kernel": 0, "heavy_first": 0},
+    {"kernel": 0, "graph": 0},
+    {"kernel": 0, "graph": 0, "heavy_stream": 0},
     {"kernel": 0, "walk": 0},
     {"kernel": 0, "walk": 0, "coop_lanes": 8},
     {"kernel": 0, "block_waves": 1, "wave_tile": 0, "coop_lanes": 0},
