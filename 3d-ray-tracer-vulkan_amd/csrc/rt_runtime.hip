@@ -276,7 +276,7 @@ static void free_graphs(PerDevice& p) {
     for (auto& g : p.graphs) (void)hipGraphExecDestroy(g.exec);
     p.graphs.clear();
 }
-static constexpr size_t kMaxGraphs = 8;
+static constexpr size_t kMaxGraphs = 64;   // an 8-rank frame batch with two buffers uses 16 keys
 
 static constexpr unsigned kQueueSlots = 64;
 
@@ -297,7 +297,7 @@ struct rt_ctx {
     int  coop_walk = 0;            // cooperative walks: 0 = 64-node windows, 1 = preorder frontier
     int  block_waves = 1;          // kernel 0: waves per workgroup (1: a finished wave frees its slot at once; or 4)
     int  heavy_first = 1;          // kernel 0: dispatch tiles in the cost order of a learning launch
-    int  heavy_factor = 150;       // automatic heavy tiles: walk length above this percentage of the bulk estimate
+    int  heavy_factor = 130;       // automatic heavy tiles: walk length above this percentage of the bulk estimate
     int  learn_cost = 1;           // heavy_first cost: 0 = lockstep steps + 2 x coop windows, 1 = wave duration
     int  graph = 1;                // kernel 0 plain launches: replay a captured HIP graph per launch key
     int  heavy_stream = 1;         // heavy_tiles: 1 = their launch runs on an auxiliary stream, concurrent

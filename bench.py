@@ -61,6 +61,8 @@ def main() -> None:
                     help="N > 1: frames = N frames per step, bands rotated over ranks (weak); "
                          "bands = one frame per step tiled over ranks (strong)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--events", choices=("region", "frame"), default="region",
+                    help="HIP events around the whole timed region (one frame per step only) or around every frame")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU baseline sample time")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "latest_pmc_traffic.json"),
                     help="PMC-derived HBM bytes per launch (profiles/*.json) to report as roofline.traffic")
@@ -187,17 +189,25 @@ def main() -> None:
         dist.barrier()
     torch.cuda.synchronize(dev)
 
+    # Events on the launch stream: around the whole timed region (default; one
+    # frame per step, so the mean frame duration is the region / steps), or
+    # around every frame (every frame's own events; always at F > 1).
+    region = args.events == "region" and F == 1
     evs = [[(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(F)]
-           for _ in range(args.steps)]
+           for _ in range(1 if region else args.steps)]
     t_start = time.perf_counter()
+    if region:
+        evs[0][0][0].record(streams[0])
     for k in range(args.steps):
-        out = step(evs[k])
+        out = step(None if region else evs[k])
+    if region:
+        evs[0][0][1].record(streams[0])
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t_start
-    kernel_ms = float(np.mean([a.elapsed_time(b) for e in evs for a, b in e]))
+    kernel_ms = float(np.mean([a.elapsed_time(b) for e in evs for a, b in e])) / (args.steps if region else 1)
 
     heavy_used = renderer.get_option("heavy_tiles_used")   # of the last timed launch
     verified = None
@@ -275,6 +285,8 @@ def main() -> None:
                           (f" (frame = the {heavy_used} heaviest tiles' one-pixel-wave launch concurrent with the "
                            f"other tiles' launch; kernel_ms spans both)" if heavy_used > 0 else ""),
                 "kernel_ms": round(kernel_ms, 4),
+                "events": ("launch stream, around the timed region / steps" if region
+                           else "launch stream, around every frame"),
                 "alg_bytes_per_launch": int(alg_bytes),
                 "alg_bytes_per_segment": round(alg_bytes / l_seg, 1),
                 "reference_layout_frac": round(ref_layout_bytes / (kernel_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),

@@ -17,7 +17,7 @@ COUNTERS = ("segments", "node_visits", "tri_tests", "mat_reads")
 DEFAULT_OPTS = {"kernel": 0, "shade_min": 16, "blocks_per_cu": 0, "wave_tile": 2, "seg_limit": 2,
                 "heavy_budget": 256, "prio_after": 0, "coop_lanes": 2, "walk": 2, "coop_walk": 0,
                 "block_waves": 1, "heavy_first": 1, "heavy_tiles": -1, "heavy_stream": 1,
-                "learn_cost": 1, "heavy_factor": 150, "graph": 1}
+                "learn_cost": 1, "heavy_factor": 130, "graph": 1}
 
 
 def _oracle(built, cam_bytes, w, h, b, **kw):
