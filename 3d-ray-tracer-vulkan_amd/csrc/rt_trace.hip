@@ -608,8 +608,16 @@ constexpr int kFeatFrontier = 32; // cooperative tail uses frontier_walk (option
 constexpr int kStack = 8;                    // per-lane t_enter stack entries in LDS (walk 1)
 constexpr int kPair = 0, kLeaf = 1, kNode = 2, kSkip = 3;   // walk 1: record kinds
 
+// Occupancy floor for trace_simple (waves per SIMD): the default walk-2
+// build needs 73 VGPRs (6 waves); RT_SIMPLE_WPE asks the compiler for more
+// resident waves at the price of a few per-segment spills.  The frontier
+// (heavy-tile) instantiations keep their registers.
+#ifndef RT_SIMPLE_WPE
+#define RT_SIMPLE_WPE 1
+#endif
 template <bool COUNT, bool DIAG = false, int FEAT = 0, int WALK = 1>
-__global__ __launch_bounds__(256) void trace_simple(TraceArgs a) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((FEAT & kFeatFrontier) ? 1 : RT_SIMPLE_WPE)))
+void trace_simple(TraceArgs a) {
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
     unsigned long long* drec = nullptr;
@@ -1382,10 +1390,17 @@ hipError_t launch_trace(const TraceArgs& a, hipStream_t stream) {
             }
         }
         const size_t shm_f = (size_t)bw * kFCap * sizeof(uint4);   // kFeatFrontier variants only
+        // Experiment knob RTAMD_LDS_PAD: unused dynamic LDS per workgroup, which
+        // caps the resident waves per CU (160 KB / pad) below the VGPR limit.
+        static const size_t lds_pad = [] {
+            const char* v = std::getenv("RTAMD_LDS_PAD");
+            const long x = v ? std::atol(v) : 0;
+            return (size_t)(x > 0 && x <= 65536 ? x : 0);
+        }();
 #define RT_SIMPLE(F, W)                                                                                         \
-        if (a.diag) hipLaunchKernelGGL((trace_simple<false, true, F, W>), grid, block, ((F) & kFeatFrontier) ? shm_f : 0, stream, ao);           \
-        else if (a.counters) hipLaunchKernelGGL((trace_simple<true, false, F, W>), grid, block, ((F) & kFeatFrontier) ? shm_f : 0, stream, ao); \
-        else hipLaunchKernelGGL((trace_simple<false, false, F, W>), grid, block, ((F) & kFeatFrontier) ? shm_f : 0, stream, ao);
+        if (a.diag) hipLaunchKernelGGL((trace_simple<false, true, F, W>), grid, block, ((F) & kFeatFrontier) ? shm_f : lds_pad, stream, ao);           \
+        else if (a.counters) hipLaunchKernelGGL((trace_simple<true, false, F, W>), grid, block, ((F) & kFeatFrontier) ? shm_f : lds_pad, stream, ao); \
+        else hipLaunchKernelGGL((trace_simple<false, false, F, W>), grid, block, ((F) & kFeatFrontier) ? shm_f : lds_pad, stream, ao);
         if (a.walk == 2) {
             switch (feat) {
                 case kFeatCoopTail: RT_SIMPLE(kFeatCoopTail, 2) break;
