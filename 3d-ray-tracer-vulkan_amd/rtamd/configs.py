@@ -9,6 +9,10 @@ these against the OBJ files themselves when the reference is present.
 """
 from __future__ import annotations
 
+import gzip
+import os
+import tempfile
+
 from dataclasses import dataclass
 from typing import Optional
 
@@ -134,7 +138,46 @@ def config5() -> RenderConfig:
                         "1M triangles, material types 0/1/2/3")
 
 
-CONFIGS = {1: config1, 2: config2, 3: config3, 4: config4, 5: config5}
+# The reference's own objects/FinalBaseMesh.obj (24,459 quads), committed
+# gzip'd as a data fixture so that the GPU box, which has no /root/reference,
+# can render the real mesh ("also run FinalBaseMesh itself").
+FINAL_BASE_MESH_GZ = os.path.join(os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))),
+                                  "tests", "golden", "FinalBaseMesh.obj.gz")
+
+
+def final_base_mesh() -> Mesh:
+    """objects/FinalBaseMesh.obj through the OBJ loader (SceneBuilder.loadModel,
+    SceneBuilder.java:129-191; Assimp's quad rule): 48,918 triangles."""
+    with gzip.open(FINAL_BASE_MESH_GZ, "rb") as f:
+        data = f.read()
+    with tempfile.TemporaryDirectory() as d:
+        path = os.path.join(d, "FinalBaseMesh.obj")
+        with open(path, "wb") as g:
+            g.write(data)
+        return Mesh.load_obj(path)
+
+
+def config6() -> RenderConfig:
+    """Config 3's placement and material with the real FinalBaseMesh in place of
+    the procedural shell: the SURVEY's probe scene (mesh + plane + type-3 cube)."""
+    s = Scene()
+    s.add_instance(ground_plane_instance())
+    m = ModelInstance("./objects/FinalBaseMesh.obj", "FinalBaseMesh", mesh=final_base_mesh())
+    m.set_position((0.0, -10.0, 0.0))
+    m.set_color((0.8, 0.8, 0.8))
+    m.set_material_type(1.0)
+    s.add_instance(m)
+    light = ModelInstance("./objects/cube.obj", "Light Source", mesh=cube_mesh())
+    light.set_position((0.0, 40.0, 0.0))
+    light.set_scale((5.0, 5.0, 5.0))
+    light.set_color((4.0, 4.0, 4.0))
+    light.set_material_type(3.0)
+    s.add_instance(light)
+    return RenderConfig("cfg6_fbm_1920x1080_b4", s, 1920, 1080, 4,
+                        "the reference's FinalBaseMesh.obj (metal) + plane + type-3 cube")
+
+
+CONFIGS = {1: config1, 2: config2, 3: config3, 4: config4, 5: config5, 6: config6}
 
 
 def get(k: int) -> RenderConfig:

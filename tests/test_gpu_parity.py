@@ -81,9 +81,10 @@ def _bands_device(renderer, cam, w, h, b, band_h, stride, off, radiance=True, st
     return d_rgba.cpu().numpy(), (d_rad.cpu().numpy() if radiance else None), s.as_dict()
 
 
-@pytest.mark.parametrize("cfg_k,row_step", [(3, 4), (4, 8)])
+@pytest.mark.parametrize("cfg_k,row_step", [(3, 4), (4, 8), (6, 4)])
 def test_synthetic_50k_row_subset(renderer, cfg_k, row_step):
-    """Configs 3/4 (50k triangles, 1080p, 4 / 8 bounces): every row_step-th row,
+    """Configs 3/4 (50k triangles, 1080p, 4 / 8 bounces) and 6 (the real
+    FinalBaseMesh, 1080p, 4 bounces): every row_step-th row,
     rendered on the GPU as interleaved 1-row bands, vs the oracle on the same rows."""
     from rtamd import configs
     cfg = configs.get(cfg_k)

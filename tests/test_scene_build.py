@@ -200,3 +200,25 @@ def test_scene_builder_skips_unloadable_models(tmp_path):
     assert b.triangle_count == 2                # 2 plane triangles -> one node with 2 leaves
     empty = SceneBuilder().build_scene(Scene())
     assert empty.triangle_count == 0 and empty.flat_bvh_data.size == 1   # the 1-byte dummy
+
+
+def test_final_base_mesh_fixture():
+    """Config 6 renders the reference's own objects/FinalBaseMesh.obj from the
+    gzip'd fixture (tests/golden/FinalBaseMesh.obj.gz): the OBJ loader gives
+    48,918 triangles (24,459 quads), and with the plane and the cube the
+    reference builder's split rule gives 2·flat − 1 nodes."""
+    from rtamd import configs
+    m = configs.final_base_mesh()
+    assert len(m) == 48_918
+    lo, hi = m.tris.min(axis=(0, 1)), m.tris.max(axis=(0, 1))
+    assert np.allclose(lo, configs.FINAL_BASE_MESH_BMIN, atol=1e-4)
+    assert np.allclose(hi, configs.FINAL_BASE_MESH_BMAX, atol=1e-4)
+    built = configs.get(6).build()
+    flat = built.triangle_count
+    assert flat == 65_096
+    assert built.flat_bvh_data.nbytes == 48 * (2 * flat - 1)
+    from conftest import REFERENCE
+    src = os.path.join(REFERENCE, "objects", "FinalBaseMesh.obj")
+    if os.path.exists(src):                     # the fixture is the reference's file, unchanged
+        from rtamd import Mesh
+        assert np.array_equal(Mesh.load_obj(src).tris, m.tris)
