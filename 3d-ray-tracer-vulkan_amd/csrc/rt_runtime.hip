@@ -421,6 +421,11 @@ static int learn_order(PerDevice& p, const TraceArgs& a, hipStream_t s, int lear
     int heavy = 0;
     for (size_t k = 0; k < n - 1 && heavy < kMaxHeavy; ++k)
         if ((double)steps[k] > heavy_factor * bulk) ++heavy;
+    // At most one generation of one-pixel waves (64 per heavy tile) in the
+    // concurrent launch: past it the heavy launch becomes the frame's critical
+    // path (the real FinalBaseMesh, config 6: 196 tiles 0.686 ms, 87 tiles
+    // 0.666-0.684 ms; config 3's 79 tiles are under the cap).
+    heavy = std::min(heavy, std::max(1, p.n_cu * kResidentPerCu / 64));
     if (std::getenv("RTAMD_DEBUG_ORDER")) {
         std::fprintf(stderr, "learn_order: %zu tiles, bulk estimate %.0f, %d heavy; first:", n, bulk, heavy);
         for (size_t k = 0; k < 6 && k < n; ++k) std::fprintf(stderr, " %d(%llu)", order[k], cost[order[k]]);

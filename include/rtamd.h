@@ -195,7 +195,9 @@ int rt_render_wait(rt_ctx* ctx, uint64_t ticket);
  *                   tile), every segment walked cooperatively with the
  *                   frontier walk, in a launch of their own.  -1 (default) =
  *                   automatic: the tiles whose walk length exceeds
- *                   "heavy_factor" percent (default 130) of the bulk estimate
+ *                   "heavy_factor" percent (default 130) of the bulk estimate,
+ *                   at most one generation of one-pixel waves (CUs x 24 / 64
+ *                   tiles: 96 on MI355X)
  *   "heavy_stream"  1 (default) = that launch runs on an auxiliary stream,
  *                   forked from and joined back to the caller's stream,
  *                   concurrently with the other tiles; 0 = before them on the
