@@ -240,6 +240,7 @@ def main() -> None:
         cpu = cpu_baseline(built, cam, W, H, B, segments, args.cpu_seconds)
 
     if rank == 0:
+        gather_kind = "RCCL" if os.environ.get("BENCH_DIST_BACKEND", "nccl") == "nccl" else "gloo"
         out = {
             "metric": BASELINE["metric"],
             "value": round(value, 2),
@@ -252,7 +253,8 @@ def main() -> None:
             "scaling": "weak" if frames_mode else "strong",
             "vs_baseline": None,
             "dtype": "f32",
-            "data": "synthetic (seeded procedural 50k-triangle shell + ground plane + type-3 cube; default camera)",
+            "data": f"{'reference asset' if args.config == 6 else 'synthetic'} "
+                    f"({cfg.note}; default camera)",
             "config": {
                 "workload": cfg.name,
                 "width": W, "height": H, "max_bounces": B,
@@ -262,9 +264,9 @@ def main() -> None:
                 "tri_tests_per_segment": round(tri_tests / segments, 4),
                 "partition": "single frame" if world == 1 else
                              (f"{F} frames per step, {band_h}-row bands rotated over {world} ranks "
-                              f"(rank r traces bands (r+f) mod {world} of frame f), RCCL gather + rank-0 assembly"
+                              f"(rank r traces bands (r+f) mod {world} of frame f), {gather_kind} gather + rank-0 assembly"
                               if frames_mode else
-                              f"one frame per step, interleaved {band_h}-row bands, RCCL gather + rank-0 assembly"),
+                              f"one frame per step, interleaved {band_h}-row bands, {gather_kind} gather + rank-0 assembly"),
                 "frames_per_step": F,
                 "frames_verified": verified,
                 "parallelism": f"tile{world}",
