@@ -298,6 +298,8 @@ struct rt_ctx {
     int  block_waves = 1;          // kernel 0: waves per workgroup (1: a finished wave frees its slot at once; or 4)
     int  heavy_first = 1;          // kernel 0: dispatch tiles in the cost order of a learning launch
     int  heavy_factor = 130;       // automatic heavy tiles: walk length above this percentage of the bulk estimate
+    int  concurrent_launches = 1;  // launches of similar work the caller keeps in flight on a device at once
+                                   //   (the heavy-tile bulk estimate counts this launch's work that many times)
     int  learn_cost = 1;           // heavy_first cost: 0 = lockstep steps + 2 x coop windows, 1 = wave duration
     int  graph = 1;                // kernel 0 plain launches: replay a captured HIP graph per launch key
     int  heavy_stream = 1;         // heavy_tiles: 1 = their launch runs on an auxiliary stream, concurrent
@@ -342,7 +344,8 @@ static int plan_order(const rt_ctx* ctx, PerDevice& p, TraceArgs& a, const rt_ca
     const int tw_w = 8 << a.wave_tile, th_w = 8 >> a.wave_tile;
     const size_t n = (size_t)((a.tw + tw_w - 1) / tw_w) * (size_t)((a.th + th_w - 1) / th_w);
     const int geo[] = {a.width, a.height, a.max_bounces, a.x0, a.y0, a.tw, a.th, a.band_h, a.band_stride,
-                       a.band_off, a.wave_tile, a.ext, a.coop_lanes, a.walk, ctx->learn_cost, ctx->heavy_factor};
+                       a.band_off, a.wave_tile, a.ext, a.coop_lanes, a.walk, ctx->learn_cost, ctx->heavy_factor,
+                       ctx->concurrent_launches};
     std::vector<uint8_t> key(sizeof(geo) + sizeof(rt_camera_ubo) + sizeof(uint64_t));
     std::memcpy(key.data(), geo, sizeof(geo));
     std::memcpy(key.data() + sizeof(geo), cam, sizeof(rt_camera_ubo));
@@ -388,7 +391,8 @@ static int plan_order(const rt_ctx* ctx, PerDevice& p, TraceArgs& a, const rt_ca
 // A tile's cost is its wave's lockstep walk iterations plus twice its
 // cooperative windows (diag record words 4 and 5): the length of the wave's
 // dependent chain, free of when the wave happened to run.
-static int learn_order(PerDevice& p, const TraceArgs& a, hipStream_t s, int learn_cost, double heavy_factor) {
+static int learn_order(PerDevice& p, const TraceArgs& a, hipStream_t s, int learn_cost, double heavy_factor,
+                       int concurrent) {
     if (!a.diag || a.diag != p.d_learn) return RT_OK;
     const size_t n = p.learning_n;
     RT_HIP_CHECK(hipStreamSynchronize(s));
@@ -410,22 +414,24 @@ static int learn_order(PerDevice& p, const TraceArgs& a, hipStream_t s, int lear
     // times the bulk estimate, the total walk length spread over the device's
     // resident waves (kResidentPerCu per CU, measured).  A 1080p frame of
     // config 3 gets a few dozen; a frame whose time is its throughput
-    // (config 5) gets none.  A band partition of band_stride bands counts as
-    // band_stride times its own work: bench.py's frame batches trace all the
-    // bands of a frame on one device at once (with the bands on other devices
-    // this only splits fewer tiles).
+    // (config 5) gets none.  The caller states how many launches of similar
+    // work it keeps in flight on the device at once (option
+    // concurrent_launches: bench.py's frame batches trace every band offset of
+    // a frame concurrently, a render loop with frames in flight two or three);
+    // the bulk counts this launch's work that many times.
     double total = 0.0;
     for (size_t k = 0; k < n; ++k) total += (double)steps[k];
-    total *= (double)std::max(1, a.band_stride);
+    total *= (double)std::max(1, concurrent);
     const double bulk = total / (double)std::max(1, p.n_cu * kResidentPerCu);
     int heavy = 0;
     for (size_t k = 0; k < n - 1 && heavy < kMaxHeavy; ++k)
         if ((double)steps[k] > heavy_factor * bulk) ++heavy;
     // At most one generation of one-pixel waves (64 per heavy tile) in the
-    // concurrent launch: past it the heavy launch becomes the frame's critical
-    // path (the real FinalBaseMesh, config 6: 196 tiles 0.686 ms, 87 tiles
-    // 0.666-0.684 ms; config 3's 79 tiles are under the cap).
-    heavy = std::min(heavy, std::max(1, p.n_cu * kResidentPerCu / 64));
+    // concurrent launch, shared by the launches in flight: past it the heavy
+    // launch becomes the frame's critical path (the real FinalBaseMesh,
+    // config 6: 196 tiles 0.686 ms, 87 tiles 0.666-0.684 ms; config 3's 79
+    // tiles are under the cap).
+    heavy = std::min(heavy, std::max(1, p.n_cu * kResidentPerCu / 64 / std::max(1, concurrent)));
     if (std::getenv("RTAMD_DEBUG_ORDER")) {
         std::fprintf(stderr, "learn_order: %zu tiles, bulk estimate %.0f, %d heavy; first:", n, bulk, heavy);
         for (size_t k = 0; k < 6 && k < n; ++k) std::fprintf(stderr, " %d(%llu)", order[k], cost[order[k]]);
@@ -878,7 +884,7 @@ int rt_render_tile_device(rt_ctx* ctx, const rt_camera_ubo* cam, int width, int 
         RT_HIP_CHECK(hipEventRecord(p.ev0, s));
     }
     if (int rl = launch(ctx, p, a, s)) return rl;
-    if (int ro = learn_order(p, a, s, ctx->learn_cost, ctx->heavy_factor / 100.0)) return ro;
+    if (int ro = learn_order(p, a, s, ctx->learn_cost, ctx->heavy_factor / 100.0, ctx->concurrent_launches)) return ro;
     if (stats) {
         RT_HIP_CHECK(hipEventRecord(p.ev1, s));
         RT_HIP_CHECK(hipEventSynchronize(p.ev1));
@@ -915,7 +921,7 @@ static int render_bands_on(const rt_ctx* ctx, PerDevice& p, const rt_camera_ubo*
         RT_HIP_CHECK(hipEventRecord(p.ev0, s));   // the timing events exist for stats only
     }
     if (int rl = launch(ctx, p, a, s)) return rl;
-    if (int ro = learn_order(p, a, s, ctx->learn_cost, ctx->heavy_factor / 100.0)) return ro;
+    if (int ro = learn_order(p, a, s, ctx->learn_cost, ctx->heavy_factor / 100.0, ctx->concurrent_launches)) return ro;
     if (count) RT_HIP_CHECK(hipEventRecord(p.ev1, s));
     return RT_OK;
 }
@@ -1146,6 +1152,8 @@ int rt_set_option(rt_ctx* ctx, const char* name, int64_t value) {
         ctx->heavy_tiles = (int)value;
     } else if (std::strcmp(name, "heavy_factor") == 0 && value >= 10 && value <= 100000) {
         ctx->heavy_factor = (int)value;
+    } else if (std::strcmp(name, "concurrent_launches") == 0 && value >= 1 && value <= 64) {
+        ctx->concurrent_launches = (int)value;
     } else if (std::strcmp(name, "learn_cost") == 0 && (value == 0 || value == 1)) {
         ctx->learn_cost = (int)value;
     } else if (std::strcmp(name, "heavy_stream") == 0 && (value == 0 || value == 1)) {
@@ -1181,6 +1189,7 @@ int rt_get_option(rt_ctx* ctx, const char* name, int64_t* value) {
     else if (std::strcmp(name, "graph") == 0) *value = ctx->graph;
     else if (std::strcmp(name, "learn_cost") == 0) *value = ctx->learn_cost;
     else if (std::strcmp(name, "heavy_factor") == 0) *value = ctx->heavy_factor;
+    else if (std::strcmp(name, "concurrent_launches") == 0) *value = ctx->concurrent_launches;
     else if (std::strcmp(name, "heavy_tiles_used") == 0) *value = ctx->dev.empty() ? 0 : ctx->dev[0].last_heavy;
     else if (std::strcmp(name, "extensions") == 0) *value = ctx->ext;
     else if (std::strcmp(name, "blocks_per_cu") == 0)

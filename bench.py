@@ -4,26 +4,31 @@
 Workload (N = 1): BASELINE config 3 — the 50k-triangle synthetic scene at
 1920x1080, 4 bounces, default camera.  One step = one whole
 frame traced on the GPU: every pixel's full path, RGBA8 written to HBM.
-With N > 1 ranks (one process per GPU, torch.distributed over RCCL; default
---partition frames) a step is N frames of the render loop, each frame tiled
-over all ranks in rotating 16-row bands (rank r traces the bands b with
-b mod N = (r + f) mod N of frame f), so every rank traces one frame's worth of
-pixels per step (weak scaling); the packed bands are gathered to rank 0 over
-xGMI (dist.gather) and assembled there inside the timed step, and rank 0
-checks the assembled frames against a one-GPU frame afterwards
-(config.frames_verified).  --partition bands: one frame per step tiled over
-the ranks (strong scaling).
+With N > 1 ranks (one process per GPU, torch.distributed over RCCL), default
+--partition bands: a step is still ONE frame, tiled over the ranks in
+interleaved 16-row bands (rank r traces the bands b with b mod N = r), the
+packed bands gathered to rank 0 over xGMI (dist.gather) and assembled there
+inside the timed step (strong scaling: the work per step is fixed; step k's
+gather overlaps step k+1's trace).  --partition frames: a step is N frames of
+the render loop, each frame's bands rotated over the ranks, so every rank
+traces one frame's worth of pixels per step (weak scaling).  Rank 0 checks the
+assembled frames against a one-GPU frame afterwards (config.frames_verified)
+and times the same frames on its GPU alone (speedup_vs_1gpu).
 
 value = segments of a step x steps / wall time of the timed steps (max over
 ranks), in millions.  A segment is one executed bounce-loop iteration
 (compute_dynamic_ray.comp:179-232); its count per frame is deterministic and is
 taken from a counting pass outside the timed region.
 
-roofline: algorithmic bytes of one frame's trace (32 B per BVH node visit +
+roofline: algorithmic bytes of one launch's trace (32 B per BVH node visit +
 36 B per triangle test + 16 B per material read + 4 B per pixel; DESIGN.md
-§Roofline) / the frame's average device time from HIP events recorded on the
-launch stream around it, against 8 TB/s HBM.  With heavy tiles a frame is two
-concurrent launches (the heaviest tiles one pixel per wave on an auxiliary
+§Roofline) / the launch's average device time from HIP events recorded on the
+launch stream around it, against 8 TB/s HBM (the contract's "achieved" and
+"frac").  The scene is L2/MALL-resident, so these bytes are mostly served from
+cache: "frac" is an algorithmic-throughput fraction, not HBM utilisation.  The
+measured HBM traffic (PMC, tools/pmc.sh) and its fraction of the peak are
+reported beside it ("hbm_GBps", "hbm_frac").  With heavy tiles a launch is two
+concurrent kernels (the heaviest tiles one pixel per wave on an auxiliary
 stream, forked from and joined back to the launch stream), so the events span
 both; tools/rocprof_frames.py gives the same per-frame span from a rocprofv3
 kernel trace.
@@ -50,6 +55,12 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+def file_sha16(path: str) -> str:
+    import hashlib
+    with open(path, "rb") as fh:
+        return hashlib.sha256(fh.read()).hexdigest()[:16]
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -57,12 +68,19 @@ def main() -> None:
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", type=int, default=3, help="BASELINE config index (3 = headline)")
     ap.add_argument("--band", type=int, default=16, help="band height for N > 1")
-    ap.add_argument("--partition", choices=("frames", "bands"), default="frames",
-                    help="N > 1: frames = N frames per step, bands rotated over ranks (weak); "
-                         "bands = one frame per step tiled over ranks (strong)")
+    ap.add_argument("--partition", choices=("bands", "frames"), default="bands",
+                    help="N > 1: bands = one frame per step tiled over the ranks (strong scaling, default); "
+                         "frames = N frames per step, bands rotated over ranks (weak)")
+    ap.add_argument("--inflight", type=int, default=0,
+                    help="frames in flight per rank (bands partition): each step's trace goes on the next of this "
+                         "many streams, so one frame's gather and serial tail overlap the next frame's trace "
+                         "(0 = auto: 1 at N = 1, the reference's one-frame-at-a-time loop; 2 at N > 1)")
+    ap.add_argument("--set", default="", help="schedule options name=value,... (rt_set_option) before timing")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-single", action="store_true", help="N > 1: skip rank 0's one-GPU timing")
     ap.add_argument("--events", choices=("region", "frame"), default="region",
-                    help="HIP events around the whole timed region (one frame per step only) or around every frame")
+                    help="N = 1: HIP events around the whole timed region, or around every frame "
+                         "(always per frame at N > 1, so a trace's events never include a gather wait)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU baseline sample time")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "latest_pmc_traffic.json"),
                     help="PMC-derived HBM bytes per launch (profiles/*.json) to report as roofline.traffic")
@@ -84,6 +102,7 @@ def main() -> None:
     torch.cuda.set_device(dev_index)
     dev = torch.device("cuda", dev_index)
     local_rank = dev_index
+    backend = None
     if world > 1:
         backend = os.environ.get("BENCH_DIST_BACKEND", "nccl")     # nccl = RCCL over xGMI
         dist.init_process_group(backend, device_id=dev if backend == "nccl" else None)
@@ -98,45 +117,56 @@ def main() -> None:
 
     renderer = rtamd.Renderer((local_rank,))
     renderer.upload_scene(built)
+    for kv in filter(None, args.set.split(",")):
+        k, v = kv.split("=")
+        renderer.set_option(k.strip(), int(v))
     L = rtamd.lib()
     from rtamd.dist import BatchPlan, batch_band_offset, gather_batch, gather_frame
 
-    # Partition.  frames (default): a step renders N frames of the render loop
-    # (N = world size; the reference re-renders the current camera every loop
+    # Partition.  bands (default): one frame per step tiled over the ranks in
+    # interleaved band_h-row bands (strong scaling; a frame lasts as long as
+    # its slowest wave).  frames: a step renders N frames of the
+    # render loop (the reference re-renders the current camera every loop
     # iteration, VulkanEngine.java:240-276), each tiled over all ranks in
-    # rotating 16-row bands, so every rank traces one frame's worth of pixels per
-    # step (weak scaling).  bands: one frame per step tiled over the ranks
-    # (strong scaling; bounded by the frame's slowest wave).
-    # At N = 1 both are one whole frame per step.
-    frames_mode = args.partition == "frames"
+    # rotating bands, so every rank traces one frame's worth of pixels per
+    # step (weak scaling).  At N = 1 both are one whole frame per step.
+    frames_mode = args.partition == "frames" and world > 1
     F = world if frames_mode else 1
     band_h = H if world == 1 else args.band
     offsets = [batch_band_offset(f, world, rank) if frames_mode else rank for f in range(F)]
     plan = BatchPlan(H, band_h, world, F) if frames_mode else None
     rows_f = [L.rt_band_rows(H, band_h, world, off) for off in offsets]
     max_rows = plan.max_rows if plan else max(L.rt_band_rows(H, band_h, world, r) for r in range(world))
-    # Two frame buffers at N > 1: step k traces into buffer k % 2 while step
-    # k-1's gather (RCCL, its own stream) still reads the other one.
-    n_buf = 2 if world > 1 else 1
+    # Frames in flight (bands partition): step k traces on stream k mod D.
+    D = 1 if frames_mode else (args.inflight if args.inflight > 0 else (1 if world == 1 else 2))
+    # A frame batch traces F launches of one frame's bands on the device at
+    # once: the automatic heavy-tile estimate must count all of them (option
+    # concurrent_launches).  Frames in flight are not counted: each frame's
+    # heavy tiles still end its tail (counting them split almost none and
+    # measured 0.77 vs 0.52 ms per frame at D = 2, profiles/r02/inflight).
+    renderer.set_option("concurrent_launches", F)
+    # D + 1 frame buffers at N > 1: step k traces into buffer k mod (D+1)
+    # while earlier steps' gathers (RCCL, their own stream) still read the others.
+    n_buf = D + 1 if world > 1 else D
     d_bufs = [torch.empty((F, max_rows, W, 4), dtype=torch.uint8, device=dev) for _ in range(n_buf)]
     gathered = [None] * n_buf                # event: the last gather that read buffer b is done
-    # One stream per frame in flight (launches and their events on the same
+    # One stream per launch in flight (launches and their events on the same
     # queue); the gather runs on main_stream once every frame is traced.
-    streams = [torch.cuda.Stream(dev) for _ in range(min(F, 8))]
+    streams = [torch.cuda.Stream(dev) for _ in range(min(F * D, 8))]
     # The gathers run on their own stream order (main_stream): a trace stream
     # never waits for the latest gather, only for the one that last read the
     # buffer it is about to overwrite.
-    main_stream = torch.cuda.Stream(dev) if world > 1 else streams[0]
+    main_stream = torch.cuda.Stream(dev) if (world > 1 or len(streams) > 1) else streams[0]
     torch.cuda.set_stream(main_stream)
     src_index = torch.as_tensor(plan.src, device=dev) if (plan and world > 1) else None
 
     import ctypes as C
     from rtamd._lib import Stats, check
 
-    def trace(f, stats: bool = False, ev=None, buf=0):
-        s = streams[f % len(streams)]
+    def trace(f, stats: bool = False, ev=None, buf=0, si=None):
+        s = streams[(f if si is None else si) % len(streams)]
         st = Stats()
-        if ev is not None:
+        if ev is not None:          # recorded after the stream's wait for the gather: the trace only
             ev[0].record(s)
         check(L.rt_render_bands_device(renderer._ctx, C.byref(cam.ubo), W, H, B, band_h, world, offsets[f],
                                        d_bufs[buf][f].data_ptr(), None, s.cuda_stream,
@@ -148,15 +178,17 @@ def main() -> None:
     k_step = [0]
 
     def step(evs=None):
-        b = k_step[0] % n_buf
+        k = k_step[0]
+        b = k % n_buf
         k_step[0] += 1
         d_rgba = d_bufs[b]
-        for s in streams:                          # the gather that last read this buffer is done
+        mine = [streams[(k * F + f) % len(streams)] for f in range(F)]
+        for s in mine:                             # the gather that last read this buffer is done
             if gathered[b] is not None:
                 s.wait_event(gathered[b])
         for f in range(F):
-            trace(f, ev=evs[f] if evs is not None else None, buf=b)
-        for s in streams:
+            trace(f, ev=evs[f] if evs is not None else None, buf=b, si=k * F + f)
+        for s in mine:
             if s is not main_stream:
                 main_stream.wait_stream(s)
         if world > 1:
@@ -189,10 +221,11 @@ def main() -> None:
         dist.barrier()
     torch.cuda.synchronize(dev)
 
-    # Events on the launch stream: around the whole timed region (default; one
-    # frame per step, so the mean frame duration is the region / steps), or
-    # around every frame (every frame's own events; always at F > 1).
-    region = args.events == "region" and F == 1
+    # Events on the launch stream: around the whole timed region (N = 1
+    # default: one frame per step, so the mean frame duration is the region /
+    # steps), or around every launch (always at N > 1, where a trace stream
+    # also waits for the gather that last read its buffer).
+    region = args.events == "region" and world == 1 and D == 1
     evs = [[(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(F)]
            for _ in range(1 if region else args.steps)]
     t_start = time.perf_counter()
@@ -211,13 +244,35 @@ def main() -> None:
 
     heavy_used = renderer.get_option("heavy_tiles_used")   # of the last timed launch
     verified = None
-    if world > 1 and rank == 0:                    # the assembled frames equal the 1-GPU frame
+    single = None
+    if world > 1 and rank == 0:
+        # the assembled frames equal the 1-GPU frame
         full = torch.empty((H, W, 4), dtype=torch.uint8, device=dev)
         check(L.rt_render_bands_device(renderer._ctx, C.byref(cam.ubo), W, H, B, H, 1, 0, full.data_ptr(), None,
                                        main_stream.cuda_stream, None))
         torch.cuda.synchronize(dev)
         frames = out if frames_mode else out[None]
         verified = bool(all(torch.equal(frames[f], full) for f in range(frames.shape[0])))
+        if not args.no_single:
+            # The same frames on this GPU alone: whole frames, one per
+            # launch, with the same frames in flight, for the speedup of this
+            # partition.
+            renderer.set_option("concurrent_launches", 1)
+            fulls = [full] + [torch.empty_like(full) for _ in range(D - 1)]
+
+            def one(j):
+                check(L.rt_render_bands_device(renderer._ctx, C.byref(cam.ubo), W, H, B, H, 1, 0,
+                                               fulls[j % D].data_ptr(), None, streams[j % D].cuda_stream, None))
+            one(0)                                    # learns the whole-frame order
+            torch.cuda.synchronize(dev)
+            for j in range(2 * D):                    # captures the graphs
+                one(j)
+            torch.cuda.synchronize(dev)
+            t1 = time.perf_counter()
+            for j in range(args.steps * F):
+                one(j)
+            torch.cuda.synchronize(dev)
+            single = time.perf_counter() - t1
 
     t = torch.tensor([elapsed, kernel_ms], dtype=torch.float64, device=dev)
     if world > 1:
@@ -234,13 +289,15 @@ def main() -> None:
             tj = json.load(fh)
         if tj.get("config") == cfg.name and world == 1:   # PMC bytes of the same kernel on this workload
             traffic, traffic_src = tj.get("hbm_bytes_per_launch"), tj.get("source")
+    hbm_gbs = traffic / (kernel_ms * 1e-3) / 1e9 if traffic else None
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(built, cam, W, H, B, segments, args.cpu_seconds)
 
     if rank == 0:
-        gather_kind = "RCCL" if os.environ.get("BENCH_DIST_BACKEND", "nccl") == "nccl" else "gloo"
+        gather_kind = "RCCL" if backend == "nccl" else (backend or "none")
+        shared = " (ranks share one GPU: rehearsal)" if os.environ.get("BENCH_SHARE_GPU") else ""
         out = {
             "metric": BASELINE["metric"],
             "value": round(value, 2),
@@ -259,20 +316,23 @@ def main() -> None:
                 "workload": cfg.name,
                 "width": W, "height": H, "max_bounces": B,
                 "triangles_flat": built.triangle_count, "bvh_nodes": built.n_nodes,
-                "segments_per_frame": int(segments),
+                "segments_per_frame": int(segments / F),
                 "node_visits_per_segment": round(node_visits / segments, 3),
                 "tri_tests_per_segment": round(tri_tests / segments, 4),
                 "partition": "single frame" if world == 1 else
                              (f"{F} frames per step, {band_h}-row bands rotated over {world} ranks "
-                              f"(rank r traces bands (r+f) mod {world} of frame f), {gather_kind} gather + rank-0 assembly"
+                              f"(rank r traces bands (r+f) mod {world} of frame f), {gather_kind} gather + rank-0 "
+                              f"assembly{shared}"
                               if frames_mode else
-                              f"one frame per step, interleaved {band_h}-row bands, {gather_kind} gather + rank-0 assembly"),
+                              f"one frame per step, interleaved {band_h}-row bands over {world} ranks, "
+                              f"{D} frames in flight per rank, {gather_kind} gather + rank-0 assembly{shared}"),
                 "frames_per_step": F,
+                "frames_in_flight": D,
                 "frames_verified": verified,
                 "parallelism": f"tile{world}",
                 "schedule": {**{k: renderer.get_option(k) for k in ("kernel", "walk", "wave_tile", "coop_lanes",
                                                                       "heavy_first", "heavy_tiles", "heavy_factor", "graph")},
-                             "heavy_tiles_used": heavy_used},
+                             "concurrent_launches": F, "heavy_tiles_used": heavy_used},
                 "launches_per_step": F * (2 if heavy_used > 0 else 1),
             },
             "roofline": {
@@ -282,20 +342,34 @@ def main() -> None:
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": traffic,
+                "basis": "achieved/frac = ALGORITHMIC bytes (the reference's visit counts x compact record sizes) per "
+                         "launch / launch time; the scene is L2/MALL-resident, so most of these bytes are cache "
+                         "hits and frac is not HBM utilisation: measured HBM traffic is hbm_GBps / hbm_frac. "
+                         "The kernel is bound by dependent-load latency and instruction issue (DESIGN.md §7)",
+                "hbm_GBps": round(hbm_gbs, 1) if hbm_gbs else None,
+                "hbm_frac": round(hbm_gbs / HBM_PEAK_GBS, 4) if hbm_gbs else None,
                 "traffic_source": traffic_src,
                 "kernel": ("trace_simple" if renderer.get_option("kernel") == 0 else "trace_*") +
                           (f" (frame = the {heavy_used} heaviest tiles' one-pixel-wave launch concurrent with the "
                            f"other tiles' launch; kernel_ms spans both)" if heavy_used > 0 else ""),
                 "kernel_ms": round(kernel_ms, 4),
+                "kernel_ms_max_over_ranks": round(kernel_ms_max, 4) if world > 1 else None,
                 "events": ("launch stream, around the timed region / steps" if region
-                           else "launch stream, around every frame"),
+                           else "launch stream, around every launch (after its wait for the gather)"),
                 "alg_bytes_per_launch": int(alg_bytes),
                 "alg_bytes_per_segment": round(alg_bytes / l_seg, 1),
                 "reference_layout_frac": round(ref_layout_bytes / (kernel_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
             },
             "primary_mrays_s": round(pixels * args.steps / elapsed / 1e6, 2),
             "cpu_baseline": cpu,
+            "bench_sha16": file_sha16(os.path.abspath(__file__)),
         }
+        if single is not None:
+            sv = segments * args.steps / single / 1e6
+            out["single_gpu"] = {"value": round(sv, 2), "ms_per_frame": round(single / (args.steps * F) * 1e3, 4),
+                                 "what": f"the same frames traced whole on rank 0's GPU alone, one per launch, "
+                                         f"{D} in flight"}
+            out["speedup_vs_1gpu"] = round(value / sv, 3)
         print(json.dumps(out), flush=True)
     renderer.close()
     if world > 1:

@@ -197,7 +197,13 @@ int rt_render_wait(rt_ctx* ctx, uint64_t ticket);
  *                   automatic: the tiles whose walk length exceeds
  *                   "heavy_factor" percent (default 130) of the bulk estimate,
  *                   at most one generation of one-pixel waves (CUs x 24 / 64
- *                   tiles: 96 on MI355X)
+ *                   tiles: 96 on MI355X), shared by the concurrent launches
+ *   "concurrent_launches" the number of launches of similar work the caller
+ *                   keeps in flight on a device at once (1..64, default 1): a
+ *                   render loop with two frames in flight says 2, a batch of N
+ *                   band offsets traced together says N.  The automatic
+ *                   heavy-tile estimate counts a launch's work that many times
+ *                   and divides the heavy-tile cap by it.
  *   "heavy_stream"  1 (default) = that launch runs on an auxiliary stream,
  *                   forked from and joined back to the caller's stream,
  *                   concurrently with the other tiles; 0 = before them on the

@@ -17,7 +17,7 @@ COUNTERS = ("segments", "node_visits", "tri_tests", "mat_reads")
 DEFAULT_OPTS = {"kernel": 0, "shade_min": 16, "blocks_per_cu": 0, "wave_tile": 2, "seg_limit": 2,
                 "heavy_budget": 256, "prio_after": 0, "coop_lanes": 2, "walk": 2, "coop_walk": 0,
                 "block_waves": 1, "heavy_first": 1, "heavy_tiles": -1, "heavy_stream": 1,
-                "learn_cost": 1, "heavy_factor": 130, "graph": 1}
+                "learn_cost": 1, "heavy_factor": 130, "graph": 1, "concurrent_launches": 1}
 
 
 def _oracle(built, cam_bytes, w, h, b, **kw):
@@ -192,6 +192,43 @@ def test_heavy_first_order(renderer, heavy, heavy_stream):
             for _ in range(2):
                 rgba, rad, st = _bands_device(renderer, cam, cfg.width, cfg.height, cfg.max_bounces, 1, 9, 2)
                 _assert_same(rgba, rad, st, *ref)
+    finally:
+        for k, v in DEFAULT_OPTS.items():
+            renderer.set_option(k, v)
+
+
+@pytest.mark.parametrize("concurrent", [1, 4])
+def test_heavy_tiles_automatic_at_cap(renderer, concurrent):
+    """The real FinalBaseMesh (config 6) as one whole frame (band stride 1)
+    with automatic heavy tiles: its tail is the heaviest of the configs, so
+    the automatic count reaches the cap (one generation of one-pixel waves,
+    CUs x 24 / 64 tiles, shared by the concurrent_launches in flight), and the
+    learned-order launches with their one-pixel-wave launch give the oracle's
+    frame and counters.  With four launches in flight the bulk is four
+    times longer, so fewer tiles outlast it."""
+    import torch
+    from rtamd import configs
+    try:
+        renderer.set_option("heavy_first", 1)
+        renderer.set_option("heavy_tiles", -1)
+        renderer.set_option("concurrent_launches", concurrent)
+        cfg = configs.get(6)
+        built = cfg.build()
+        cam = cfg.camera()
+        renderer.upload_scene(built)
+        ref = _oracle(built, cam.ubo_bytes(), cfg.width, cfg.height, cfg.max_bounces)
+        rgba, rad, _ = _bands_device(renderer, cam, cfg.width, cfg.height, cfg.max_bounces, cfg.height, 1, 0,
+                                     stats=False)                       # learns the order
+        _assert_same(rgba, rad, None, *ref)
+        rgba, rad, st = _bands_device(renderer, cam, cfg.width, cfg.height, cfg.max_bounces, cfg.height, 1, 0)
+        _assert_same(rgba, rad, st, *ref)
+        n_cu = torch.cuda.get_device_properties(0).multi_processor_count
+        cap = max(1, n_cu * 24 // 64 // concurrent)
+        used = renderer.get_option("heavy_tiles_used")
+        if concurrent == 1:
+            assert used == cap
+        else:   # four launches' bulk: fewer tiles outlast it, never more than the shared cap
+            assert used <= cap
     finally:
         for k, v in DEFAULT_OPTS.items():
             renderer.set_option(k, v)

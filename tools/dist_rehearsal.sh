@@ -1,11 +1,12 @@
 #!/bin/bash
-# Rehearse bench.py's N>1 paths on a 1-GPU box: 2 ranks share the GPU.
-# (The real 1/2/4/8-GPU runs are the driver's.)
+# Rehearse bench.py's N>1 paths on a 1-GPU box: NPROC ranks share the GPU
+# (BENCH_SHARE_GPU=1; the JSON says so).  The real 1/2/4/8-GPU runs are the
+# driver's.  Every artifact carries bench.py's sha (bench_sha16).
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 OUT=gpurun_out/${TAG:-dist}
 mkdir -p "$OUT"
-for part in frames bands; do
+for part in ${PARTS:-bands frames}; do
   for be in ${BACKENDS:-nccl gloo}; do
     BENCH_SHARE_GPU=1 BENCH_DIST_BACKEND=$be timeout -k 10 300 python -m torch.distributed.run --nnodes=1 \
       --nproc-per-node ${NPROC:-2} --master-addr 127.0.0.1 --master-port $((29500 + RANDOM % 1000)) bench.py --gpus ${NPROC:-2} \
