@@ -150,6 +150,8 @@ struct TraceArgs {
                                 //   one pixel per wave (64 workgroups each; launcher-internal)
     int      heavy_tiles;       // simple, with tile_order: the first heavy_tiles tiles run in that split
                                 //   mode as a concurrent launch on aux_stream (fork ev_fork, join ev_join)
+    int      heavy_fused;       // simple, with heavy_tiles: 1 = the heavy tiles' one-pixel workgroups come
+                                //   first in the same launch (option heavy_stream 2), no aux stream
     hipStream_t aux_stream;
     hipEvent_t ev_fork, ev_join;
     Counters* sink;             // tiered: counters trace_coop adds into when counters is null

@@ -298,11 +298,15 @@ struct rt_ctx {
     int  block_waves = 1;          // kernel 0: waves per workgroup (1: a finished wave frees its slot at once; or 4)
     int  heavy_first = 1;          // kernel 0: dispatch tiles in the cost order of a learning launch
     int  heavy_factor = 130;       // automatic heavy tiles: walk length above this percentage of the bulk estimate
+    int  heavy_cap = 75;           // automatic heavy tiles: at most this percentage of one generation of
+                                   //   one-pixel waves (CUs x 24 / 64 tiles)
     int  concurrent_launches = 1;  // launches of similar work the caller keeps in flight on a device at once
                                    //   (the heavy-tile bulk estimate counts this launch's work that many times)
     int  learn_cost = 1;           // heavy_first cost: 0 = lockstep steps + 2 x coop windows, 1 = wave duration
     int  graph = 1;                // kernel 0 plain launches: replay a captured HIP graph per launch key
-    int  heavy_stream = 1;         // heavy_tiles: 1 = their launch runs on an auxiliary stream, concurrent
+    int  heavy_stream = 2;         // heavy_tiles: 1 = their launch runs on an auxiliary stream, concurrent
+                                   //   with the other tiles; 2 = their workgroups come first in the
+                                   //   other tiles' launch (one launch per frame)
                                    //   with the other tiles; 0 = before them on the same stream
     int  heavy_tiles = -1;         // heavy_first: the this-many most expensive tiles are traced one pixel
                                    //   per wave, walked cooperatively, in a separate launch
@@ -338,6 +342,7 @@ static int plan_order(const rt_ctx* ctx, PerDevice& p, TraceArgs& a, const rt_ca
     a.split_n = 0;
     a.heavy_tiles = 0;
     a.aux_stream = nullptr;
+    a.heavy_fused = 0;
     a.ev_fork = a.ev_join = nullptr;
     p.last_heavy = 0;
     if (!ctx->heavy_first || a.kernel != kKernelSimple || a.block_waves != 1) return RT_OK;
@@ -345,7 +350,7 @@ static int plan_order(const rt_ctx* ctx, PerDevice& p, TraceArgs& a, const rt_ca
     const size_t n = (size_t)((a.tw + tw_w - 1) / tw_w) * (size_t)((a.th + th_w - 1) / th_w);
     const int geo[] = {a.width, a.height, a.max_bounces, a.x0, a.y0, a.tw, a.th, a.band_h, a.band_stride,
                        a.band_off, a.wave_tile, a.ext, a.coop_lanes, a.walk, ctx->learn_cost, ctx->heavy_factor,
-                       ctx->concurrent_launches};
+                       ctx->concurrent_launches, ctx->heavy_cap};
     std::vector<uint8_t> key(sizeof(geo) + sizeof(rt_camera_ubo) + sizeof(uint64_t));
     std::memcpy(key.data(), geo, sizeof(geo));
     std::memcpy(key.data() + sizeof(geo), cam, sizeof(rt_camera_ubo));
@@ -364,7 +369,8 @@ static int plan_order(const rt_ctx* ctx, PerDevice& p, TraceArgs& a, const rt_ca
                 }
                 a.heavy_tiles = heavy;
                 p.last_heavy = (int)std::min<size_t>((size_t)heavy, n - 1);
-                a.aux_stream = ctx->heavy_stream ? p.aux[k] : nullptr;
+                a.aux_stream = ctx->heavy_stream == 1 ? p.aux[k] : nullptr;
+                a.heavy_fused = ctx->heavy_stream == 2 ? 1 : 0;
                 a.ev_fork = p.aux_fork[k];
                 a.ev_join = p.aux_join[k];
                 if (a.diag)   // one record per workgroup of both launches
@@ -391,8 +397,9 @@ static int plan_order(const rt_ctx* ctx, PerDevice& p, TraceArgs& a, const rt_ca
 // A tile's cost is its wave's lockstep walk iterations plus twice its
 // cooperative windows (diag record words 4 and 5): the length of the wave's
 // dependent chain, free of when the wave happened to run.
-static int learn_order(PerDevice& p, const TraceArgs& a, hipStream_t s, int learn_cost, double heavy_factor,
-                       int concurrent) {
+static int learn_order(const rt_ctx* ctx, PerDevice& p, const TraceArgs& a, hipStream_t s) {
+    const int learn_cost = ctx->learn_cost, concurrent = ctx->concurrent_launches;
+    const double heavy_factor = ctx->heavy_factor / 100.0;
     if (!a.diag || a.diag != p.d_learn) return RT_OK;
     const size_t n = p.learning_n;
     RT_HIP_CHECK(hipStreamSynchronize(s));
@@ -431,7 +438,7 @@ static int learn_order(PerDevice& p, const TraceArgs& a, hipStream_t s, int lear
     // launch becomes the frame's critical path (the real FinalBaseMesh,
     // config 6: 196 tiles 0.686 ms, 87 tiles 0.666-0.684 ms; config 3's 79
     // tiles are under the cap).
-    heavy = std::min(heavy, std::max(1, p.n_cu * kResidentPerCu / 64 / std::max(1, concurrent)));
+    heavy = std::min(heavy, std::max(1, p.n_cu * kResidentPerCu / 64 * ctx->heavy_cap / 100 / std::max(1, concurrent)));
     if (std::getenv("RTAMD_DEBUG_ORDER")) {
         std::fprintf(stderr, "learn_order: %zu tiles, bulk estimate %.0f, %d heavy; first:", n, bulk, heavy);
         for (size_t k = 0; k < 6 && k < n; ++k) std::fprintf(stderr, " %d(%llu)", order[k], cost[order[k]]);
@@ -562,7 +569,7 @@ static std::vector<uint64_t> launch_key(const TraceArgs& a, hipStream_t s) {
             P(a.out_rgba), P(a.out_rad), (uint64_t)a.wave_tile, (uint64_t)a.seg_limit, (uint64_t)a.prio_after,
             (uint64_t)a.heavy_budget, (uint64_t)a.coop_lanes, (uint64_t)a.ext, (uint64_t)a.sky_enabled,
             (uint64_t)a.frame_count, P(a.accum), (uint64_t)a.walk, (uint64_t)a.block_waves, P(a.tile_order),
-            (uint64_t)a.heavy_tiles, (uint64_t)(a.aux_stream != nullptr), (uint64_t)a.coop_walk,
+            (uint64_t)a.heavy_tiles, (uint64_t)(a.aux_stream != nullptr), (uint64_t)a.heavy_fused, (uint64_t)a.coop_walk,
             (uint64_t)a.kernel};
 }
 
@@ -638,7 +645,7 @@ int rt_create(const int* device_ids, int n_devices, rt_ctx** out) {
     if (const char* v = std::getenv("RTAMD_HEAVY_TILES")) ctx->heavy_tiles = std::max(-1, std::atoi(v));
     if (const char* v = std::getenv("RTAMD_LEARN_COST")) ctx->learn_cost = std::atoi(v) ? 1 : 0;
     if (const char* v = std::getenv("RTAMD_HEAVY_FACTOR")) ctx->heavy_factor = std::max(10, std::atoi(v));
-    if (const char* v = std::getenv("RTAMD_HEAVY_STREAM")) ctx->heavy_stream = std::atoi(v) ? 1 : 0;
+    if (const char* v = std::getenv("RTAMD_HEAVY_STREAM")) ctx->heavy_stream = std::max(0, std::min(2, std::atoi(v)));
     if (const char* v = std::getenv("RTAMD_GRAPH")) ctx->graph = std::atoi(v) ? 1 : 0;
     if (const char* v = std::getenv("RTAMD_BLOCK_WAVES")) ctx->block_waves = std::atoi(v) == 1 ? 1 : 4;
     if (const char* v = std::getenv("RTAMD_COOP_LANES")) ctx->coop_lanes = std::max(0, std::min(64, std::atoi(v)));
@@ -884,7 +891,7 @@ int rt_render_tile_device(rt_ctx* ctx, const rt_camera_ubo* cam, int width, int 
         RT_HIP_CHECK(hipEventRecord(p.ev0, s));
     }
     if (int rl = launch(ctx, p, a, s)) return rl;
-    if (int ro = learn_order(p, a, s, ctx->learn_cost, ctx->heavy_factor / 100.0, ctx->concurrent_launches)) return ro;
+    if (int ro = learn_order(ctx, p, a, s)) return ro;
     if (stats) {
         RT_HIP_CHECK(hipEventRecord(p.ev1, s));
         RT_HIP_CHECK(hipEventSynchronize(p.ev1));
@@ -921,7 +928,7 @@ static int render_bands_on(const rt_ctx* ctx, PerDevice& p, const rt_camera_ubo*
         RT_HIP_CHECK(hipEventRecord(p.ev0, s));   // the timing events exist for stats only
     }
     if (int rl = launch(ctx, p, a, s)) return rl;
-    if (int ro = learn_order(p, a, s, ctx->learn_cost, ctx->heavy_factor / 100.0, ctx->concurrent_launches)) return ro;
+    if (int ro = learn_order(ctx, p, a, s)) return ro;
     if (count) RT_HIP_CHECK(hipEventRecord(p.ev1, s));
     return RT_OK;
 }
@@ -1152,11 +1159,13 @@ int rt_set_option(rt_ctx* ctx, const char* name, int64_t value) {
         ctx->heavy_tiles = (int)value;
     } else if (std::strcmp(name, "heavy_factor") == 0 && value >= 10 && value <= 100000) {
         ctx->heavy_factor = (int)value;
+    } else if (std::strcmp(name, "heavy_cap") == 0 && value >= 1 && value <= 100) {
+        ctx->heavy_cap = (int)value;
     } else if (std::strcmp(name, "concurrent_launches") == 0 && value >= 1 && value <= 64) {
         ctx->concurrent_launches = (int)value;
     } else if (std::strcmp(name, "learn_cost") == 0 && (value == 0 || value == 1)) {
         ctx->learn_cost = (int)value;
-    } else if (std::strcmp(name, "heavy_stream") == 0 && (value == 0 || value == 1)) {
+    } else if (std::strcmp(name, "heavy_stream") == 0 && value >= 0 && value <= 2) {
         ctx->heavy_stream = (int)value;
     } else if (std::strcmp(name, "graph") == 0 && (value == 0 || value == 1)) {
         ctx->graph = (int)value;
@@ -1190,6 +1199,7 @@ int rt_get_option(rt_ctx* ctx, const char* name, int64_t* value) {
     else if (std::strcmp(name, "learn_cost") == 0) *value = ctx->learn_cost;
     else if (std::strcmp(name, "heavy_factor") == 0) *value = ctx->heavy_factor;
     else if (std::strcmp(name, "concurrent_launches") == 0) *value = ctx->concurrent_launches;
+    else if (std::strcmp(name, "heavy_cap") == 0) *value = ctx->heavy_cap;
     else if (std::strcmp(name, "heavy_tiles_used") == 0) *value = ctx->dev.empty() ? 0 : ctx->dev[0].last_heavy;
     else if (std::strcmp(name, "extensions") == 0) *value = ctx->ext;
     else if (std::strcmp(name, "blocks_per_cu") == 0)

@@ -605,7 +605,69 @@ constexpr int kFeatCoopTail = 8;  // finish the last coop_lanes walks of a wave 
 constexpr int kFeatExt = kFeatExtBit;   // non-reference extensions (option "extensions", kExt*)
 constexpr int kFeatFrontier = 32; // cooperative tail uses frontier_walk (option coop_walk = 1)
 
+constexpr int kFeatFused = 64;    // heavy tiles in the same launch: workgroups k < 64 * split_n run heavy_pixel
+
 constexpr int kStack = 8;                    // per-lane t_enter stack entries in LDS (walk 1)
+
+// One pixel of a heavy tile, the whole wave on it (option heavy_fused, the
+// workgroups in front of the tile workgroups of the same launch): every
+// segment is walked with frontier_walk from the root; the ray, its
+// attenuation and the walk are wave-uniform, so every lane computes the same
+// values and lane 0 writes the pixel and the counts.  The arithmetic is the
+// lockstep kernel's (slab, tri_test, scatter, sky_color), so pixel and counts
+// are identical.  It is a branch of its own at the top of the kernel, so the
+// tile path's registers are not live in it and the launch keeps the tile
+// path's 73 VGPRs (out of line it would need 119 and spill the arguments).
+template <bool COUNT>
+__device__ __forceinline__ void heavy_pixel(const TraceArgs& a, int lx, int ly, uint4* F) {
+    const int lane = threadIdx.x & 63;
+    const int end = a.scene.end;
+    unsigned long long c_seg = 0, c_node = 0, c_tri = 0, c_mat = 0;
+    if (lx < a.tw && ly < a.th) {
+        uint32_t seed;
+        V3 o, d;
+        primary_ray(a, a.x0 + lx, frame_row(a, ly), seed, o, d);
+        V3 att = {1.0f, 1.0f, 1.0f};
+        V3 fin = {0.0f, 0.0f, 0.0f};
+        int rounds = 0;
+        for (int b = 0; b < a.max_bounces; ++b) {
+            float closest = kTMax;
+            int hit = -1;
+            const V3 inv = {1.0f / d.x, 1.0f / d.y, 1.0f / d.z};              // :89
+            if (COUNT) {
+                ++c_seg;
+                if (end > 0) ++c_node;                                       // the root visit
+            }
+            if (end > 0) {
+                int p = 0;
+                bool pl = false;
+                if (!frontier_walk<COUNT>(a.scene.nodes, a.scene.leafs, a.scene.pairs, end, p, pl, o, d, inv, closest,
+                                          hit, c_node, c_tri, F, rounds))
+                    while (p < end) p = node_step<COUNT>(a.scene.nodes, a.scene.leafs, p, pl, o, d, inv, closest, hit,
+                                                         c_node, c_tri);
+            }
+            if (hit < 0) {                                                    // :224-226
+                fin = vmul(att, sky_color(d));
+                break;
+            }
+            if (COUNT) ++c_mat;
+            const V3 hp = vadd(o, vscale(d, closest));                        // ray_at :77-79
+            const V3 nrm = hit_normal(a.scene.norms, hit, d);
+            const float4 M = a.scene.mats[hit];
+            V3 nd;
+            if (!scatter(M, d, nrm, seed, nd)) break;                        // attenuation = 0: black
+            att = vmul(att, V3{M.x, M.y, M.z});
+            o = hp;
+            d = nd;
+            // b == max_bounces - 1 leaves fin black (:229-231)
+        }
+        if (lane == 0) write_pixel(a, lx, ly, fin);
+    }
+    if (COUNT) {
+        if (lane != 0) c_seg = c_node = c_tri = c_mat = 0;                  // wave-uniform: counted once
+        flush_counters(a.counters, c_seg, c_node, c_tri, c_mat);
+    }
+}
 constexpr int kPair = 0, kLeaf = 1, kNode = 2, kSkip = 3;   // walk 1: record kinds
 
 // Occupancy floor for trace_simple (waves per SIMD): the default walk-2
@@ -655,6 +717,19 @@ void trace_simple(TraceArgs a) {
         }
         bx = t % a.tiles_x;
         by = t / a.tiles_x;
+        if ((FEAT & kFeatFused) && sub >= 0) {           // a heavy tile's pixel, dispatched first
+            heavy_pixel<COUNT>(a, bx * tw_w + (sub & (tw_w - 1)), by * th_w + (sub >> (3 + s)), fr);
+            if (DIAG) {
+                diag_stamp(drec, 1);
+                if (lane == 0) {
+                    drec[4] = 0;
+                    drec[5] = 0;
+                    drec[6] = 0;
+                    drec[7] = 0;
+                }
+            }
+            return;
+        }
     }
     const int tl = sub >= 0 ? sub : lane;                // the tile pixel this lane traces
     const int lx = (bx * a.block_waves + wave) * tw_w + (tl & (tw_w - 1));
@@ -1358,6 +1433,19 @@ hipError_t launch_trace(const TraceArgs& a, hipStream_t stream) {
             ao.split_n = 0;
             const int n_tiles = (int)(grid.x * grid.y);
             const int H = std::min(a.heavy_tiles, n_tiles - 1);
+            if (H > 0 && a.heavy_fused && bw == 1 && (feat & ~kFeatFrontier) == kFeatCoopTail) {
+                // One launch: the H heaviest tiles' one-pixel workgroups first
+                // (dispatched in index order, so they start at once), then the
+                // other tiles.
+                ao.split_n = H;
+                const dim3 gf(64 * H + (n_tiles - H));
+                const size_t shm = kFCap * sizeof(uint4);
+                constexpr int FF = kFeatCoopTail | kFeatFused;
+                if (a.diag) hipLaunchKernelGGL((trace_simple<false, true, FF, 2>), gf, block, shm, stream, ao);
+                else if (a.counters) hipLaunchKernelGGL((trace_simple<true, false, FF, 2>), gf, block, shm, stream, ao);
+                else hipLaunchKernelGGL((trace_simple<false, false, FF, 2>), gf, block, shm, stream, ao);
+                return hipGetLastError();
+            }
             if (H > 0 && a.ev_fork && bw == 1 && (feat & ~kFeatFrontier) == kFeatCoopTail) {
                 // The H most expensive tiles, one pixel per wave, every segment
                 // walked cooperatively with the frontier walk, on an auxiliary

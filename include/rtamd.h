@@ -196,18 +196,24 @@ int rt_render_wait(rt_ctx* ctx, uint64_t ticket);
  *                   frontier walk, in a launch of their own.  -1 (default) =
  *                   automatic: the tiles whose walk length exceeds
  *                   "heavy_factor" percent (default 130) of the bulk estimate,
- *                   at most one generation of one-pixel waves (CUs x 24 / 64
- *                   tiles: 96 on MI355X), shared by the concurrent launches
+ *                   at most "heavy_cap" percent of one generation of
+ *                   one-pixel waves (CUs x 24 / 64 tiles: 96 on MI355X, so 72
+ *                   by default), shared by the concurrent launches
  *   "concurrent_launches" the number of launches of similar work the caller
  *                   keeps in flight on a device at once (1..64, default 1): a
  *                   render loop with two frames in flight says 2, a batch of N
  *                   band offsets traced together says N.  The automatic
  *                   heavy-tile estimate counts a launch's work that many times
  *                   and divides the heavy-tile cap by it.
- *   "heavy_stream"  1 (default) = that launch runs on an auxiliary stream,
- *                   forked from and joined back to the caller's stream,
- *                   concurrently with the other tiles; 0 = before them on the
- *                   caller's stream
+ *   "heavy_stream"  2 (default) = the heavy tiles' one-pixel workgroups come
+ *                   first in the same launch as the other tiles (dispatched in
+ *                   index order, so every heavy wave starts at once; one
+ *                   launch per frame, no fork / join); 1 = their own launch
+ *                   on an auxiliary stream, forked from and joined back to the
+ *                   caller's stream, concurrent with the other tiles; 0 = their
+ *                   own launch before the other tiles on the caller's stream
+ *   "heavy_cap"     automatic heavy tiles: at most this percentage (1..100,
+ *                   default 75) of one generation of one-pixel waves
  *   "graph"         kernel 0, plain launches on a non-null stream: 1 (default)
  *                   = captured once per launch key (scene, camera, frame,
  *                   schedule, learned order, outputs, stream) into a HIP
@@ -241,7 +247,7 @@ int rt_render_wait(rt_ctx* ctx, uint64_t ticket);
  * Defaults can also be set with the environment variables
  * RTAMD_KERNEL=simple|persistent|split|tiered, RTAMD_WALK, RTAMD_COOP_LANES,
  * RTAMD_COOP_WALK, RTAMD_BLOCK_WAVES, RTAMD_HEAVY_FIRST, RTAMD_HEAVY_TILES,
- * RTAMD_HEAVY_FACTOR, RTAMD_HEAVY_STREAM, RTAMD_LEARN_COST,
+ * RTAMD_HEAVY_FACTOR, RTAMD_HEAVY_STREAM (0 / 1 / 2), RTAMD_LEARN_COST,
  * RTAMD_SEG_LIMIT, RTAMD_SHADE_MIN and RTAMD_BLOCKS_PER_CU. */
 int rt_set_option(rt_ctx* ctx, const char* name, int64_t value);
 /* Diagnostics: with option "diag" = 1, kernel 0 records per wave

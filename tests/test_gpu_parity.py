@@ -16,8 +16,8 @@ pytestmark = pytest.mark.gpu
 COUNTERS = ("segments", "node_visits", "tri_tests", "mat_reads")
 DEFAULT_OPTS = {"kernel": 0, "shade_min": 16, "blocks_per_cu": 0, "wave_tile": 2, "seg_limit": 2,
                 "heavy_budget": 256, "prio_after": 0, "coop_lanes": 2, "walk": 2, "coop_walk": 0,
-                "block_waves": 1, "heavy_first": 1, "heavy_tiles": -1, "heavy_stream": 1,
-                "learn_cost": 1, "heavy_factor": 130, "graph": 1, "concurrent_launches": 1}
+                "block_waves": 1, "heavy_first": 1, "heavy_tiles": -1, "heavy_stream": 2,
+                "learn_cost": 1, "heavy_factor": 130, "graph": 1, "concurrent_launches": 1, "heavy_cap": 75}
 
 
 def _oracle(built, cam_bytes, w, h, b, **kw):
@@ -170,7 +170,8 @@ def test_schedules_identical(renderer, opts):
             renderer.set_option(k, v)
 
 
-@pytest.mark.parametrize("heavy,heavy_stream", [(-1, 1), (0, 0), (40, 0), (40, 1), (100000, 0)])
+@pytest.mark.parametrize("heavy,heavy_stream", [(-1, 1), (0, 0), (40, 0), (40, 1), (100000, 0), (-1, 2), (40, 2),
+                                                (100000, 2)])
 def test_heavy_first_order(renderer, heavy, heavy_stream):
     """heavy_first: the learning launch and the launches in the learned
     order give the oracle's frame and counters; a new camera relearns."""
@@ -197,8 +198,8 @@ def test_heavy_first_order(renderer, heavy, heavy_stream):
             renderer.set_option(k, v)
 
 
-@pytest.mark.parametrize("concurrent", [1, 4])
-def test_heavy_tiles_automatic_at_cap(renderer, concurrent):
+@pytest.mark.parametrize("concurrent,heavy_stream", [(1, 1), (4, 1), (1, 2)])
+def test_heavy_tiles_automatic_at_cap(renderer, concurrent, heavy_stream):
     """The real FinalBaseMesh (config 6) as one whole frame (band stride 1)
     with automatic heavy tiles: its tail is the heaviest of the configs, so
     the automatic count reaches the cap (one generation of one-pixel waves,
@@ -212,6 +213,7 @@ def test_heavy_tiles_automatic_at_cap(renderer, concurrent):
         renderer.set_option("heavy_first", 1)
         renderer.set_option("heavy_tiles", -1)
         renderer.set_option("concurrent_launches", concurrent)
+        renderer.set_option("heavy_stream", heavy_stream)
         cfg = configs.get(6)
         built = cfg.build()
         cam = cfg.camera()
@@ -223,7 +225,7 @@ def test_heavy_tiles_automatic_at_cap(renderer, concurrent):
         rgba, rad, st = _bands_device(renderer, cam, cfg.width, cfg.height, cfg.max_bounces, cfg.height, 1, 0)
         _assert_same(rgba, rad, st, *ref)
         n_cu = torch.cuda.get_device_properties(0).multi_processor_count
-        cap = max(1, n_cu * 24 // 64 // concurrent)
+        cap = max(1, n_cu * 24 // 64 * renderer.get_option("heavy_cap") // 100 // concurrent)
         used = renderer.get_option("heavy_tiles_used")
         if concurrent == 1:
             assert used == cap

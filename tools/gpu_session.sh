@@ -24,7 +24,7 @@ run() {  # run NAME SECONDS CMD...
 rocminfo 2>/dev/null | grep -m1 -E "gfx950" > "$OUT/rocminfo.txt"
 for s in $STEPS; do
   case $s in
-    test)  run pytest 900 python -m pytest tests -m gpu -q -rA > "$OUT/pytest_gpu.log" 2>&1 ;;
+    test)  run pytest 900 python -u -m pytest tests -m gpu -q -rA --timeout 120 --timeout-method thread > "$OUT/pytest_gpu.log" 2>&1 ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 ;;
     bench) run bench 600 python bench.py --steps 20 --warmup 5 > "$OUT/bench.json" 2> "$OUT/bench.err" ;;
     prof)  run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- \
