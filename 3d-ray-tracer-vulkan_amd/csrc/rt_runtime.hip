@@ -574,7 +574,11 @@ static std::vector<uint64_t> launch_key(const TraceArgs& a, hipStream_t s) {
 }
 
 static int launch(const rt_ctx* ctx, PerDevice& p, const TraceArgs& a, hipStream_t s) {
-    if (!ctx->graph || s == nullptr || a.counters || a.diag || a.kernel != kKernelSimple) {
+    // Only a frame of two launches (heavy tiles on an auxiliary stream,
+    // heavy_stream 1) gains from a graph: its fork and join become edges.  A
+    // single launch (the fused heavy tiles, or none) goes straight to the
+    // stream: a graph launch adds ~9 us between frames (profiles/r02/graph).
+    if (!ctx->graph || s == nullptr || a.counters || a.diag || a.kernel != kKernelSimple || !a.aux_stream) {
         RT_HIP_CHECK(launch_trace(a, s));
         return RT_OK;
     }
