@@ -82,8 +82,9 @@ def main() -> None:
                     help="N = 1: HIP events around the whole timed region, or around every frame "
                          "(always per frame at N > 1, so a trace's events never include a gather wait)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU baseline sample time")
-    ap.add_argument("--settle-s", type=float, default=0.05,
-                    help="untimed rendering before the warmup steps, seconds (steady clocks and caches)")
+    ap.add_argument("--settle-s", type=float, default=0.2,
+                    help="untimed frames before the warmup steps: this many seconds of counting-pass time "
+                         "(5-100 frames; steady clocks and caches)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "latest_pmc_traffic.json"),
                     help="PMC-derived HBM bytes per launch (profiles/*.json) to report as roofline.traffic")
     args = ap.parse_args()
@@ -216,15 +217,20 @@ def main() -> None:
     log(f"[rank {rank}] step: {F} frame(s), {segments:.0f} segments ({segments / pixels:.3f}/px), "
         f"{node_visits / segments:.2f} node visits/seg, {tri_tests / segments:.3f} tri tests/seg")
 
-    # Settle (untimed): frames until ~50 ms of rendering have passed, so the
-    # timed steps see the steady state of a running render loop (the first
-    # frames after start-up run 3-4% slower: profiles/r02/warmup), then the W
-    # warmup steps of the contract.
-    t_settle = time.perf_counter()
-    while time.perf_counter() - t_settle < args.settle_s:
-        for _ in range(10):
-            step()
-        torch.cuda.synchronize(dev)
+    # Settle (untimed): 5-100 frames, about settle_s / (the counting pass's
+    # device time; a counting launch runs ~4x a plain one), so the timed steps
+    # see the steady state of a running render loop (the first frames after
+    # start-up run 3-4% slower: profiles/r02/warmup), then the W warmup steps
+    # of the contract.
+    # The count is fixed up front (from the counting pass's device time) and
+    # agreed over the ranks, so every rank runs the same collectives.
+    est_ms = max(0.05, float(per[0].get("ms", 1.0)))
+    n_settle = torch.tensor([max(5, min(100, int(args.settle_s * 1e3 / est_ms)))], dtype=torch.int64, device=dev)
+    if world > 1:
+        dist.all_reduce(n_settle, op=dist.ReduceOp.MIN)
+    for _ in range(int(n_settle.item())):
+        step()
+    torch.cuda.synchronize(dev)
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize(dev)
