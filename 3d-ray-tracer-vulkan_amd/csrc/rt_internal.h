@@ -152,6 +152,10 @@ struct TraceArgs {
                                 //   mode as a concurrent launch on aux_stream (fork ev_fork, join ev_join)
     int      heavy_fused;       // simple, with heavy_tiles: 1 = the heavy tiles' one-pixel workgroups come
                                 //   first in the same launch (option heavy_stream 2), no aux stream
+    const int* heavy_px;        // simple, fused, with tile_order: heavy pixels (tile * 64 + lane), traced one
+    int      n_heavy_px;        //   per wave by the first n_heavy_px workgroups of the launch
+    const unsigned long long* tile_mask;   // per tile: the lanes (heavy pixels) its tile wave skips, or null
+    unsigned* diag_lane;        // learning launch: each pixel's walk length (64 per wave), or null
     hipStream_t aux_stream;
     hipEvent_t ev_fork, ev_join;
     Counters* sink;             // tiered: counters trace_coop adds into when counters is null

@@ -246,7 +246,13 @@ struct PerDevice {
     // band partition rotates through several keys), oldest dropped first
     unsigned long long* d_learn = nullptr;   // per-wave diag records of the learning launch
     size_t       learn_cap = 0;
-    struct Order { std::vector<uint8_t> key; int* d_order; size_t n; int heavy; };
+    unsigned*    d_learn_lane = nullptr;    // per-pixel walk lengths of the learning launch (64 per wave)
+    size_t       learn_lane_cap = 0;
+    // a learned order: tiles most expensive first, the heavy-tile count, and
+    // the heavy pixels (tile * 64 + lane, most expensive first) with every
+    // tile's mask of them (option heavy_pixels)
+    struct Order { std::vector<uint8_t> key; int* d_order; size_t n; int heavy;
+                   int* d_hpix; int n_hpix; unsigned long long* d_mask; };
     // option heavy_tiles: auxiliary streams (round robin) for the concurrent heavy-tile launch
     hipStream_t  aux[4] = {nullptr, nullptr, nullptr, nullptr};
     hipEvent_t   aux_fork[4] = {nullptr, nullptr, nullptr, nullptr}, aux_join[4] = {nullptr, nullptr, nullptr, nullptr};
@@ -255,6 +261,7 @@ struct PerDevice {
     std::vector<uint8_t> learning_key;
     size_t       learning_n = 0;
     int          last_heavy = 0;    // heavy tiles of the last launch (option "heavy_tiles_used", read only)
+    int          last_heavy_px = 0; // heavy pixels of the last launch (option "heavy_pixels_used", read only)
     // option graph: plain launches captured once per launch key into a HIP
     // graph and replayed (the heavy-tile fork / join becomes graph edges)
     struct Graph { std::vector<uint64_t> key; hipGraphExec_t exec; };
@@ -267,8 +274,14 @@ static constexpr int    kResidentPerCu = 24;    // resident trace waves per CU (
 static constexpr int    kMaxHeavy = 256;
 static constexpr size_t kDiagWords = 8;   // per-wave diag record (rt_trace.hip, rtamd.h rt_diag_copy)
 
+static void free_order(PerDevice::Order& o) {
+    (void)hipFree(o.d_order);
+    if (o.d_hpix) (void)hipFree(o.d_hpix);
+    if (o.d_mask) (void)hipFree(o.d_mask);
+}
+
 static void free_orders(PerDevice& p) {
-    for (auto& o : p.orders) (void)hipFree(o.d_order);
+    for (auto& o : p.orders) free_order(o);
     p.orders.clear();
 }
 
@@ -298,6 +311,9 @@ struct rt_ctx {
     int  block_waves = 1;          // kernel 0: waves per workgroup (1: a finished wave frees its slot at once; or 4)
     int  heavy_first = 1;          // kernel 0: dispatch tiles in the cost order of a learning launch
     int  heavy_factor = 130;       // automatic heavy tiles: walk length above this percentage of the bulk estimate
+    int  heavy_pixels = 1;         // heavy_stream 2 with automatic heavy tiles: split heavy PIXELS (1) or
+                                   //   whole tiles (0) into one-pixel waves
+    int  heavy_pixel_factor = 75;  // heavy pixels: walk length above this percentage of the bulk estimate
     int  heavy_cap = 75;           // automatic heavy tiles: at most this percentage of one generation of
                                    //   one-pixel waves (CUs x 24 / 64 tiles)
     int  concurrent_launches = 1;  // launches of similar work the caller keeps in flight on a device at once
@@ -343,14 +359,19 @@ static int plan_order(const rt_ctx* ctx, PerDevice& p, TraceArgs& a, const rt_ca
     a.heavy_tiles = 0;
     a.aux_stream = nullptr;
     a.heavy_fused = 0;
+    a.heavy_px = nullptr;
+    a.n_heavy_px = 0;
+    a.tile_mask = nullptr;
+    a.diag_lane = nullptr;
     a.ev_fork = a.ev_join = nullptr;
     p.last_heavy = 0;
+    p.last_heavy_px = 0;
     if (!ctx->heavy_first || a.kernel != kKernelSimple || a.block_waves != 1) return RT_OK;
     const int tw_w = 8 << a.wave_tile, th_w = 8 >> a.wave_tile;
     const size_t n = (size_t)((a.tw + tw_w - 1) / tw_w) * (size_t)((a.th + th_w - 1) / th_w);
     const int geo[] = {a.width, a.height, a.max_bounces, a.x0, a.y0, a.tw, a.th, a.band_h, a.band_stride,
                        a.band_off, a.wave_tile, a.ext, a.coop_lanes, a.walk, ctx->learn_cost, ctx->heavy_factor,
-                       ctx->concurrent_launches, ctx->heavy_cap};
+                       ctx->concurrent_launches, ctx->heavy_cap, ctx->heavy_pixel_factor};
     std::vector<uint8_t> key(sizeof(geo) + sizeof(rt_camera_ubo) + sizeof(uint64_t));
     std::memcpy(key.data(), geo, sizeof(geo));
     std::memcpy(key.data() + sizeof(geo), cam, sizeof(rt_camera_ubo));
@@ -358,6 +379,17 @@ static int plan_order(const rt_ctx* ctx, PerDevice& p, TraceArgs& a, const rt_ca
     for (const auto& o : p.orders)
         if (o.n == n && o.key == key) {
             a.tile_order = o.d_order;
+            if (ctx->heavy_stream == 2 && ctx->heavy_pixels && ctx->heavy_tiles < 0 && n > 1) {
+                // heavy pixels, fused: their one-pixel workgroups come first
+                // in the launch, and their tiles skip them
+                a.heavy_fused = 1;
+                a.heavy_px = o.d_hpix;
+                a.n_heavy_px = o.n_hpix;
+                a.tile_mask = o.d_mask;
+                p.last_heavy_px = o.n_hpix;
+                if (a.diag) p.diag_used = (n + (size_t)o.n_hpix) * 8;
+                return RT_OK;
+            }
             const int heavy = ctx->heavy_tiles >= 0 ? ctx->heavy_tiles : o.heavy;
             if (heavy > 0 && n > 1) {
                 const unsigned k = p.aux_next++ % 4;
@@ -388,9 +420,17 @@ static int plan_order(const rt_ctx* ctx, PerDevice& p, TraceArgs& a, const rt_ca
         RT_HIP_CHECK(hipMalloc(&p.d_learn, n * kDiagWords * sizeof(unsigned long long)));
         p.learn_cap = n * kDiagWords;
     }
+    if (n * 64 > p.learn_lane_cap) {
+        if (p.d_learn_lane) (void)hipFree(p.d_learn_lane);
+        p.d_learn_lane = nullptr;
+        p.learn_lane_cap = 0;
+        RT_HIP_CHECK(hipMalloc(&p.d_learn_lane, n * 64 * sizeof(unsigned)));
+        p.learn_lane_cap = n * 64;
+    }
     p.learning_key = key;
     p.learning_n = n;
     a.diag = p.d_learn;                // the diagnostic build counts each wave's lockstep steps
+    a.diag_lane = p.d_learn_lane;      // and each pixel's own walk length
     return RT_OK;
 }
 
@@ -438,24 +478,47 @@ static int learn_order(const rt_ctx* ctx, PerDevice& p, const TraceArgs& a, hipS
     // launch becomes the frame's critical path (the real FinalBaseMesh,
     // config 6: 196 tiles 0.686 ms, 87 tiles 0.666-0.684 ms; config 3's 79
     // tiles are under the cap).
-    heavy = std::min(heavy, std::max(1, p.n_cu * kResidentPerCu / 64 * ctx->heavy_cap / 100 / std::max(1, concurrent)));
+    const int cap_waves = std::max(1, p.n_cu * kResidentPerCu * ctx->heavy_cap / 100 / std::max(1, concurrent));
+    heavy = std::min(heavy, std::max(1, cap_waves / 64));
+    // Heavy pixels (option heavy_pixels): the pixels whose own walk length
+    // (their lockstep steps + 2 x the cooperative windows spent on them)
+    // exceeds heavy_pixel_factor times the bulk estimate, most expensive
+    // first, at most cap_waves of them.  A heavy tile holds a few dozen of its
+    // 64 pixels over that bar (tools/heavy_pixel_model.py); splitting only
+    // those keeps the rest of the tile in its lockstep wave.
+    std::vector<unsigned> lane(n * 64);
+    RT_HIP_CHECK(hipMemcpy(lane.data(), p.d_learn_lane, lane.size() * sizeof(unsigned), hipMemcpyDeviceToHost));
+    const double px_bar = ctx->heavy_pixel_factor / 100.0 * bulk;
+    std::vector<int> hpix;
+    for (size_t q = 0; q < n * 64; ++q)
+        if ((double)lane[q] > px_bar) hpix.push_back((int)q);
+    std::stable_sort(hpix.begin(), hpix.end(), [&](int x, int y) { return lane[x] > lane[y]; });
+    if ((int)hpix.size() > cap_waves) hpix.resize(cap_waves);
+    std::vector<unsigned long long> mask(n, 0ull);
+    for (int q : hpix) mask[q >> 6] |= 1ull << (q & 63);
     if (std::getenv("RTAMD_DEBUG_ORDER")) {
-        std::fprintf(stderr, "learn_order: %zu tiles, bulk estimate %.0f, %d heavy; first:", n, bulk, heavy);
+        std::fprintf(stderr, "learn_order: %zu tiles, bulk estimate %.0f, %d heavy tiles, %zu heavy pixels; first:",
+                     n, bulk, heavy, hpix.size());
         for (size_t k = 0; k < 6 && k < n; ++k) std::fprintf(stderr, " %d(%llu)", order[k], cost[order[k]]);
         std::fprintf(stderr, "\n");
     }
     if (p.orders.size() >= kMaxOrders) {
-        (void)hipFree(p.orders.front().d_order);
+        free_order(p.orders.front());
         p.orders.erase(p.orders.begin());
     }
-    int* d = nullptr;
-    RT_HIP_CHECK(hipMalloc(&d, n * sizeof(int)));
-    const hipError_t e = hipMemcpy(d, order.data(), n * sizeof(int), hipMemcpyHostToDevice);
+    PerDevice::Order o{p.learning_key, nullptr, n, heavy, nullptr, (int)hpix.size(), nullptr};
+    hipError_t e = hipMalloc(&o.d_order, n * sizeof(int));
+    if (e == hipSuccess) e = hipMemcpy(o.d_order, order.data(), n * sizeof(int), hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMalloc(&o.d_mask, n * sizeof(unsigned long long));
+    if (e == hipSuccess) e = hipMemcpy(o.d_mask, mask.data(), n * sizeof(unsigned long long), hipMemcpyHostToDevice);
+    if (e == hipSuccess && !hpix.empty()) e = hipMalloc(&o.d_hpix, hpix.size() * sizeof(int));
+    if (e == hipSuccess && !hpix.empty())
+        e = hipMemcpy(o.d_hpix, hpix.data(), hpix.size() * sizeof(int), hipMemcpyHostToDevice);
     if (e != hipSuccess) {
-        (void)hipFree(d);
+        if (o.d_order) free_order(o);
         RT_HIP_CHECK(e);
     }
-    p.orders.push_back({p.learning_key, d, n, heavy});
+    p.orders.push_back(std::move(o));
     return RT_OK;
 }
 
@@ -569,7 +632,8 @@ static std::vector<uint64_t> launch_key(const TraceArgs& a, hipStream_t s) {
             P(a.out_rgba), P(a.out_rad), (uint64_t)a.wave_tile, (uint64_t)a.seg_limit, (uint64_t)a.prio_after,
             (uint64_t)a.heavy_budget, (uint64_t)a.coop_lanes, (uint64_t)a.ext, (uint64_t)a.sky_enabled,
             (uint64_t)a.frame_count, P(a.accum), (uint64_t)a.walk, (uint64_t)a.block_waves, P(a.tile_order),
-            (uint64_t)a.heavy_tiles, (uint64_t)(a.aux_stream != nullptr), (uint64_t)a.heavy_fused, (uint64_t)a.coop_walk,
+            (uint64_t)a.heavy_tiles, (uint64_t)(a.aux_stream != nullptr), (uint64_t)a.heavy_fused, P(a.heavy_px),
+            (uint64_t)a.n_heavy_px, P(a.tile_mask), (uint64_t)a.coop_walk,
             (uint64_t)a.kernel};
 }
 
@@ -650,6 +714,7 @@ int rt_create(const int* device_ids, int n_devices, rt_ctx** out) {
     if (const char* v = std::getenv("RTAMD_LEARN_COST")) ctx->learn_cost = std::atoi(v) ? 1 : 0;
     if (const char* v = std::getenv("RTAMD_HEAVY_FACTOR")) ctx->heavy_factor = std::max(10, std::atoi(v));
     if (const char* v = std::getenv("RTAMD_HEAVY_STREAM")) ctx->heavy_stream = std::max(0, std::min(2, std::atoi(v)));
+    if (const char* v = std::getenv("RTAMD_HEAVY_PIXELS")) ctx->heavy_pixels = std::atoi(v) ? 1 : 0;
     if (const char* v = std::getenv("RTAMD_GRAPH")) ctx->graph = std::atoi(v) ? 1 : 0;
     if (const char* v = std::getenv("RTAMD_BLOCK_WAVES")) ctx->block_waves = std::atoi(v) == 1 ? 1 : 4;
     if (const char* v = std::getenv("RTAMD_COOP_LANES")) ctx->coop_lanes = std::max(0, std::min(64, std::atoi(v)));
@@ -714,6 +779,7 @@ int rt_destroy(rt_ctx* ctx) {
         if (p.d_heavy) (void)hipFree(p.d_heavy);
         if (p.d_diag) (void)hipFree(p.d_diag);
         if (p.d_learn) (void)hipFree(p.d_learn);
+        if (p.d_learn_lane) (void)hipFree(p.d_learn_lane);
         free_orders(p);
         free_graphs(p);
         for (int k = 0; k < 4; ++k) {
@@ -1163,6 +1229,10 @@ int rt_set_option(rt_ctx* ctx, const char* name, int64_t value) {
         ctx->heavy_tiles = (int)value;
     } else if (std::strcmp(name, "heavy_factor") == 0 && value >= 10 && value <= 100000) {
         ctx->heavy_factor = (int)value;
+    } else if (std::strcmp(name, "heavy_pixels") == 0 && (value == 0 || value == 1)) {
+        ctx->heavy_pixels = (int)value;
+    } else if (std::strcmp(name, "heavy_pixel_factor") == 0 && value >= 1 && value <= 100000) {
+        ctx->heavy_pixel_factor = (int)value;
     } else if (std::strcmp(name, "heavy_cap") == 0 && value >= 1 && value <= 100) {
         ctx->heavy_cap = (int)value;
     } else if (std::strcmp(name, "concurrent_launches") == 0 && value >= 1 && value <= 64) {
@@ -1204,6 +1274,9 @@ int rt_get_option(rt_ctx* ctx, const char* name, int64_t* value) {
     else if (std::strcmp(name, "heavy_factor") == 0) *value = ctx->heavy_factor;
     else if (std::strcmp(name, "concurrent_launches") == 0) *value = ctx->concurrent_launches;
     else if (std::strcmp(name, "heavy_cap") == 0) *value = ctx->heavy_cap;
+    else if (std::strcmp(name, "heavy_pixels") == 0) *value = ctx->heavy_pixels;
+    else if (std::strcmp(name, "heavy_pixel_factor") == 0) *value = ctx->heavy_pixel_factor;
+    else if (std::strcmp(name, "heavy_pixels_used") == 0) *value = ctx->dev.empty() ? 0 : ctx->dev[0].last_heavy_px;
     else if (std::strcmp(name, "heavy_tiles_used") == 0) *value = ctx->dev.empty() ? 0 : ctx->dev[0].last_heavy;
     else if (std::strcmp(name, "extensions") == 0) *value = ctx->ext;
     else if (std::strcmp(name, "blocks_per_cu") == 0)

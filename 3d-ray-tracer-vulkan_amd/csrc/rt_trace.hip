@@ -706,14 +706,20 @@ void trace_simple(TraceArgs a) {
     // order are traced one pixel per wave (64 workgroups per tile): the wave's
     // single live lane walks every segment cooperatively (frontier walk).
     int bx = blockIdx.x, by = blockIdx.y, sub = -1;
+    unsigned long long skip_lanes = 0;                   // heavy pixels this tile wave leaves out
     if (a.tile_order) {                                  // 1-D grid over the ordered tiles
         const int k = blockIdx.x;
         int t;
-        if (k < 64 * a.split_n) {
+        if ((FEAT & kFeatFused) && k < a.n_heavy_px) {   // a heavy pixel (tile * 64 + lane), dispatched first
+            const int q = a.heavy_px[k];
+            t = q >> 6;
+            sub = q & 63;
+        } else if (k < 64 * a.split_n) {
             t = a.tile_order[k >> 6];
             sub = k & 63;
         } else {
-            t = a.tile_order[k - 63 * a.split_n];
+            t = a.tile_order[k - 63 * a.split_n - ((FEAT & kFeatFused) ? a.n_heavy_px : 0)];
+            if ((FEAT & kFeatFused) && a.tile_mask) skip_lanes = a.tile_mask[t];
         }
         bx = t % a.tiles_x;
         by = t / a.tiles_x;
@@ -734,7 +740,7 @@ void trace_simple(TraceArgs a) {
     const int tl = sub >= 0 ? sub : lane;                // the tile pixel this lane traces
     const int lx = (bx * a.block_waves + wave) * tw_w + (tl & (tw_w - 1));
     const int ly = by * th_w + (tl >> (3 + s));
-    const bool pixel = lx < a.tw && ly < a.th && (sub < 0 || lane == 0);
+    const bool pixel = lx < a.tw && ly < a.th && (sub < 0 || lane == 0) && !((skip_lanes >> lane) & 1ull);
     const int coop_lanes = sub >= 0 ? 64 : a.coop_lanes;
     const float4* __restrict__ nodes = a.scene.nodes;
     const float4* __restrict__ leafs = a.scene.leafs;
@@ -745,6 +751,7 @@ void trace_simple(TraceArgs a) {
     unsigned long long c_seg = 0, c_node = 0, c_tri = 0, c_mat = 0;
     int steps = 0;
     unsigned long long d_iters = 0, d_windows = 0, d_coop_t = 0;   // diag builds only
+    unsigned long long d_lane_windows = 0;           // diag: cooperative windows spent on this lane's walks
 
     uint32_t seed = 0;
     V3 o = {0.f, 0.f, 0.f}, d = {0.f, 0.f, 1.f};
@@ -1026,7 +1033,10 @@ void trace_simple(TraceArgs a) {
                 } else {
                     nw = coop_walk<COUNT>(nodes, leafs, end, lane_i(start, L), bo, bd, bi, bc, bh, cn, ct);
                 }
-                if (DIAG) d_windows += nw;
+                if (DIAG) {
+                    d_windows += nw;
+                    if (lane == L) d_lane_windows += nw;
+                }
                 if (lane == L) {
                     closest = bc;
                     hit = bh;
@@ -1081,6 +1091,11 @@ void trace_simple(TraceArgs a) {
     if (COUNT) flush_counters(a.counters, c_seg, c_node, c_tri, c_mat);
     if (DIAG) {
         diag_stamp(drec, 1);
+        // each pixel's own walk length: its lockstep steps (d_iters counts the
+        // loop iterations this lane walked) + 2 x the windows spent on it
+        if (a.diag_lane)
+            a.diag_lane[((size_t)(blockIdx.y * gridDim.x + blockIdx.x) * a.block_waves + wave) * 64 + lane] =
+                (unsigned)(d_iters + 2 * d_lane_windows);
 #pragma unroll
         for (int off = 32; off > 0; off >>= 1) {   // the wave's iterations = the longest lane's
             const unsigned long long o2 = __shfl_xor(d_iters, off);
@@ -1433,6 +1448,18 @@ hipError_t launch_trace(const TraceArgs& a, hipStream_t stream) {
             ao.split_n = 0;
             const int n_tiles = (int)(grid.x * grid.y);
             const int H = std::min(a.heavy_tiles, n_tiles - 1);
+            if (a.n_heavy_px > 0 && a.heavy_fused && bw == 1 && (feat & ~kFeatFrontier) == kFeatCoopTail) {
+                // One launch: the heavy pixels' one-pixel workgroups first, then
+                // every tile without its heavy pixels.
+                ao.split_n = 0;
+                const dim3 gf(a.n_heavy_px + n_tiles);
+                const size_t shm = kFCap * sizeof(uint4);
+                constexpr int FF = kFeatCoopTail | kFeatFused;
+                if (a.diag) hipLaunchKernelGGL((trace_simple<false, true, FF, 2>), gf, block, shm, stream, ao);
+                else if (a.counters) hipLaunchKernelGGL((trace_simple<true, false, FF, 2>), gf, block, shm, stream, ao);
+                else hipLaunchKernelGGL((trace_simple<false, false, FF, 2>), gf, block, shm, stream, ao);
+                return hipGetLastError();
+            }
             if (H > 0 && a.heavy_fused && bw == 1 && (feat & ~kFeatFrontier) == kFeatCoopTail) {
                 // One launch: the H heaviest tiles' one-pixel workgroups first
                 // (dispatched in index order, so they start at once), then the

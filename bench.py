@@ -348,9 +348,12 @@ def main() -> None:
                 "frames_verified": verified,
                 "parallelism": f"tile{world}",
                 "schedule": {**{k: renderer.get_option(k) for k in ("kernel", "walk", "wave_tile", "coop_lanes",
-                                                                      "heavy_first", "heavy_tiles", "heavy_factor", "graph")},
-                             "concurrent_launches": F, "heavy_tiles_used": heavy_used},
-                "launches_per_step": F * (2 if heavy_used > 0 else 1),
+                                                                      "heavy_first", "heavy_tiles", "heavy_factor",
+                                                                      "heavy_stream", "heavy_pixels",
+                                                                      "heavy_pixel_factor", "heavy_cap", "graph")},
+                             "concurrent_launches": F, "heavy_tiles_used": heavy_used,
+                             "heavy_pixels_used": renderer.get_option("heavy_pixels_used")},
+                "launches_per_step": F * (2 if heavy_used > 0 and renderer.get_option("heavy_stream") != 2 else 1),
             },
             "roofline": {
                 "bound": "hbm",
@@ -366,9 +369,13 @@ def main() -> None:
                 "hbm_GBps": round(hbm_gbs, 1) if hbm_gbs else None,
                 "hbm_frac": round(hbm_gbs / HBM_PEAK_GBS, 4) if hbm_gbs else None,
                 "traffic_source": traffic_src,
-                "kernel": ("trace_simple" if renderer.get_option("kernel") == 0 else "trace_*") +
-                          (f" (frame = the {heavy_used} heaviest tiles' one-pixel-wave launch concurrent with the "
-                           f"other tiles' launch; kernel_ms spans both)" if heavy_used > 0 else ""),
+                "kernel": ("trace_simple" if renderer.get_option("kernel") == 0 else "trace_*") + (
+                    f" (one launch per frame: the {renderer.get_option('heavy_pixels_used')} heaviest pixels one per "
+                    f"wave first, then every 32x2 tile without them)" if renderer.get_option("heavy_pixels_used") > 0
+                    else f" (one launch per frame: the {heavy_used} heaviest tiles one pixel per wave first)"
+                    if heavy_used > 0 and renderer.get_option("heavy_stream") == 2
+                    else f" (frame = the {heavy_used} heaviest tiles' one-pixel-wave launch concurrent with the "
+                         f"other tiles' launch; kernel_ms spans both)" if heavy_used > 0 else ""),
                 "kernel_ms": round(kernel_ms, 4),
                 "kernel_ms_max_over_ranks": round(kernel_ms_max, 4) if world > 1 else None,
                 "events": ("launch stream, around the timed region / steps" if region

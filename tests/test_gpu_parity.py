@@ -17,7 +17,8 @@ COUNTERS = ("segments", "node_visits", "tri_tests", "mat_reads")
 DEFAULT_OPTS = {"kernel": 0, "shade_min": 16, "blocks_per_cu": 0, "wave_tile": 2, "seg_limit": 2,
                 "heavy_budget": 256, "prio_after": 0, "coop_lanes": 2, "walk": 2, "coop_walk": 0,
                 "block_waves": 1, "heavy_first": 1, "heavy_tiles": -1, "heavy_stream": 2,
-                "learn_cost": 1, "heavy_factor": 130, "graph": 1, "concurrent_launches": 1, "heavy_cap": 75}
+                "learn_cost": 1, "heavy_factor": 130, "graph": 1, "concurrent_launches": 1, "heavy_cap": 75,
+                "heavy_pixels": 1, "heavy_pixel_factor": 75}
 
 
 def _oracle(built, cam_bytes, w, h, b, **kw):
@@ -214,6 +215,7 @@ def test_heavy_tiles_automatic_at_cap(renderer, concurrent, heavy_stream):
         renderer.set_option("heavy_tiles", -1)
         renderer.set_option("concurrent_launches", concurrent)
         renderer.set_option("heavy_stream", heavy_stream)
+        renderer.set_option("heavy_pixels", 0)          # whole heavy tiles
         cfg = configs.get(6)
         built = cfg.build()
         cam = cfg.camera()
@@ -231,6 +233,38 @@ def test_heavy_tiles_automatic_at_cap(renderer, concurrent, heavy_stream):
             assert used == cap
         else:   # four launches' bulk: fewer tiles outlast it, never more than the shared cap
             assert used <= cap
+    finally:
+        for k, v in DEFAULT_OPTS.items():
+            renderer.set_option(k, v)
+
+
+@pytest.mark.parametrize("cfg_k,factor", [(6, 75), (3, 75), (3, 30)])
+def test_heavy_pixels(renderer, cfg_k, factor):
+    """Heavy pixels (option heavy_pixels, the default with heavy_stream 2):
+    the learning launch records every pixel's walk length; later launches
+    trace the pixels over the bar one per wave, first in the launch, and
+    every tile wave skips its heavy pixels.  Each pixel is traced exactly
+    once: the frame and the counters equal the oracle's."""
+    from rtamd import configs
+    try:
+        renderer.set_option("heavy_stream", 2)
+        renderer.set_option("heavy_pixels", 1)
+        renderer.set_option("heavy_pixel_factor", factor)
+        cfg = configs.get(cfg_k)
+        built = cfg.build()
+        cam = cfg.camera()
+        renderer.upload_scene(built)
+        ref = _oracle(built, cam.ubo_bytes(), cfg.width, cfg.height, cfg.max_bounces)
+        rgba, rad, _ = _bands_device(renderer, cam, cfg.width, cfg.height, cfg.max_bounces, cfg.height, 1, 0,
+                                     stats=False)                       # learns the order and the pixels
+        _assert_same(rgba, rad, None, *ref)
+        rgba, rad, st = _bands_device(renderer, cam, cfg.width, cfg.height, cfg.max_bounces, cfg.height, 1, 0)
+        _assert_same(rgba, rad, st, *ref)
+        assert renderer.get_option("heavy_pixels_used") > 0
+        assert renderer.get_option("heavy_tiles_used") == 0
+        rgba, rad, _ = _bands_device(renderer, cam, cfg.width, cfg.height, cfg.max_bounces, cfg.height, 1, 0,
+                                     stats=False)                       # a plain launch in the learned order
+        _assert_same(rgba, rad, None, *ref)
     finally:
         for k, v in DEFAULT_OPTS.items():
             renderer.set_option(k, v)
