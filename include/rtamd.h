@@ -212,8 +212,17 @@ int rt_render_wait(rt_ctx* ctx, uint64_t ticket);
  *                   on an auxiliary stream, forked from and joined back to the
  *                   caller's stream, concurrent with the other tiles; 0 = their
  *                   own launch before the other tiles on the caller's stream
- *   "heavy_cap"     automatic heavy tiles: at most this percentage (1..100,
- *                   default 75) of one generation of one-pixel waves
+ *   "heavy_cap"     automatic heavy tiles / pixels: at most this percentage
+ *                   (1..100, default 75) of one generation of one-pixel waves
+ *   "heavy_pixels"  with heavy_stream 2 and automatic heavy tiles: 1 (default)
+ *                   = split heavy PIXELS, not whole tiles: the learning launch
+ *                   also records every pixel's walk length; the pixels whose
+ *                   walk exceeds "heavy_pixel_factor" percent (default 75) of
+ *                   the bulk estimate are traced one per wave by the first
+ *                   workgroups of the launch, and every tile wave skips its
+ *                   heavy pixels; 0 = whole heavy tiles
+ *   "heavy_pixel_factor" see heavy_pixels (1..100000, default 75)
+ *   "heavy_pixels_used" (rt_get_option only) heavy pixels of the last launch
  *   "graph"         kernel 0, plain launches on a non-null stream: 1 (default)
  *                   = captured once per launch key (scene, camera, frame,
  *                   schedule, learned order, outputs, stream) into a HIP
@@ -247,7 +256,7 @@ int rt_render_wait(rt_ctx* ctx, uint64_t ticket);
  * Defaults can also be set with the environment variables
  * RTAMD_KERNEL=simple|persistent|split|tiered, RTAMD_WALK, RTAMD_COOP_LANES,
  * RTAMD_COOP_WALK, RTAMD_BLOCK_WAVES, RTAMD_HEAVY_FIRST, RTAMD_HEAVY_TILES,
- * RTAMD_HEAVY_FACTOR, RTAMD_HEAVY_STREAM (0 / 1 / 2), RTAMD_LEARN_COST,
+ * RTAMD_HEAVY_FACTOR, RTAMD_HEAVY_STREAM (0 / 1 / 2), RTAMD_HEAVY_PIXELS, RTAMD_LEARN_COST,
  * RTAMD_SEG_LIMIT, RTAMD_SHADE_MIN and RTAMD_BLOCKS_PER_CU. */
 int rt_set_option(rt_ctx* ctx, const char* name, int64_t value);
 /* Diagnostics: with option "diag" = 1, kernel 0 records per wave
