@@ -259,6 +259,7 @@ struct PerDevice {
     unsigned     aux_next = 0;
     std::vector<Order> orders;
     std::vector<uint8_t> learning_key;
+    std::vector<uint8_t> prev_key;   // the launch key of the previous heavy_first launch (option reuse_order)
     size_t       learning_n = 0;
     int          last_heavy = 0;    // heavy tiles of the last launch (option "heavy_tiles_used", read only)
     int          last_heavy_px = 0; // heavy pixels of the last launch (option "heavy_pixels_used", read only)
@@ -314,6 +315,7 @@ struct rt_ctx {
     int  heavy_pixels = 1;         // heavy_stream 2 with automatic heavy tiles: split heavy PIXELS (1) or
                                    //   whole tiles (0) into one-pixel waves
     int  heavy_pixel_factor = 75;  // heavy pixels: walk length above this percentage of the bulk estimate
+    int  reuse_order = 1;          // heavy_first: a moving camera reuses the order learned at another camera
     int  heavy_cap = 75;           // automatic heavy tiles: at most this percentage of one generation of
                                    //   one-pixel waves (CUs x 24 / 64 tiles)
     int  concurrent_launches = 1;  // launches of similar work the caller keeps in flight on a device at once
@@ -376,40 +378,57 @@ static int plan_order(const rt_ctx* ctx, PerDevice& p, TraceArgs& a, const rt_ca
     std::memcpy(key.data(), geo, sizeof(geo));
     std::memcpy(key.data() + sizeof(geo), cam, sizeof(rt_camera_ubo));
     std::memcpy(key.data() + sizeof(geo) + sizeof(rt_camera_ubo), &ctx->scene_gen, sizeof(uint64_t));
-    for (const auto& o : p.orders)
-        if (o.n == n && o.key == key) {
-            a.tile_order = o.d_order;
-            if (ctx->heavy_stream == 2 && ctx->heavy_pixels && ctx->heavy_tiles < 0 && n > 1) {
-                // heavy pixels, fused: their one-pixel workgroups come first
-                // in the launch, and their tiles skip them
-                a.heavy_fused = 1;
-                a.heavy_px = o.d_hpix;
-                a.n_heavy_px = o.n_hpix;
-                a.tile_mask = o.d_mask;
-                p.last_heavy_px = o.n_hpix;
-                if (a.diag) p.diag_used = (n + (size_t)o.n_hpix) * 8;
-                return RT_OK;
-            }
-            const int heavy = ctx->heavy_tiles >= 0 ? ctx->heavy_tiles : o.heavy;
-            if (heavy > 0 && n > 1) {
-                const unsigned k = p.aux_next++ % 4;
-                if (!p.aux[k]) {
-                    // normal priority: a high-priority stream measured slower (0.715 vs 0.59 ms)
-                    RT_HIP_CHECK(hipStreamCreateWithFlags(&p.aux[k], hipStreamNonBlocking));
-                    RT_HIP_CHECK(hipEventCreateWithFlags(&p.aux_fork[k], hipEventDisableTiming));
-                    RT_HIP_CHECK(hipEventCreateWithFlags(&p.aux_join[k], hipEventDisableTiming));
-                }
-                a.heavy_tiles = heavy;
-                p.last_heavy = (int)std::min<size_t>((size_t)heavy, n - 1);
-                a.aux_stream = ctx->heavy_stream == 1 ? p.aux[k] : nullptr;
-                a.heavy_fused = ctx->heavy_stream == 2 ? 1 : 0;
-                a.ev_fork = p.aux_fork[k];
-                a.ev_join = p.aux_join[k];
-                if (a.diag)   // one record per workgroup of both launches
-                    p.diag_used = (n + 63 * (size_t)std::min(a.heavy_tiles, (int)n - 1)) * 8;
-            }
+    // Use a learned order: the exact key's; or, when only the camera differs
+    // from a learned key and the camera has just moved (option reuse_order),
+    // the newest order of the same frame geometry and scene.  The order and the
+    // heavy pixels only decide which wave traces a pixel and when, never what
+    // it computes, so an order learned at another camera is exact, only less
+    // well balanced; a camera in motion pays no learning frame, and the first
+    // repeat of a camera (the camera has stopped) learns its own order.
+    auto use = [&](const PerDevice::Order& o) -> int {
+        a.tile_order = o.d_order;
+        if (ctx->heavy_stream == 2 && ctx->heavy_pixels && ctx->heavy_tiles < 0 && n > 1) {
+            // heavy pixels, fused: their one-pixel workgroups come first
+            // in the launch, and their tiles skip them
+            a.heavy_fused = 1;
+            a.heavy_px = o.d_hpix;
+            a.n_heavy_px = o.n_hpix;
+            a.tile_mask = o.d_mask;
+            p.last_heavy_px = o.n_hpix;
+            if (a.diag) p.diag_used = (n + (size_t)o.n_hpix) * 8;
             return RT_OK;
         }
+        const int heavy = ctx->heavy_tiles >= 0 ? ctx->heavy_tiles : o.heavy;
+        if (heavy > 0 && n > 1) {
+            const unsigned k = p.aux_next++ % 4;
+            if (!p.aux[k]) {
+                // normal priority: a high-priority stream measured slower (0.715 vs 0.59 ms)
+                RT_HIP_CHECK(hipStreamCreateWithFlags(&p.aux[k], hipStreamNonBlocking));
+                RT_HIP_CHECK(hipEventCreateWithFlags(&p.aux_fork[k], hipEventDisableTiming));
+                RT_HIP_CHECK(hipEventCreateWithFlags(&p.aux_join[k], hipEventDisableTiming));
+            }
+            a.heavy_tiles = heavy;
+            p.last_heavy = (int)std::min<size_t>((size_t)heavy, n - 1);
+            a.aux_stream = ctx->heavy_stream == 1 ? p.aux[k] : nullptr;
+            a.heavy_fused = ctx->heavy_stream == 2 ? 1 : 0;
+            a.ev_fork = p.aux_fork[k];
+            a.ev_join = p.aux_join[k];
+            if (a.diag)   // one record per workgroup of both launches
+                p.diag_used = (n + 63 * (size_t)std::min(a.heavy_tiles, (int)n - 1)) * 8;
+        }
+        return RT_OK;
+    };
+    const bool repeat = key == p.prev_key;
+    p.prev_key = key;
+    for (const auto& o : p.orders)
+        if (o.n == n && o.key == key) return use(o);
+    if (ctx->reuse_order && !repeat) {
+        const size_t g = sizeof(geo), c = sizeof(rt_camera_ubo);
+        for (auto it = p.orders.rbegin(); it != p.orders.rend(); ++it)
+            if (it->n == n && std::memcmp(it->key.data(), key.data(), g) == 0 &&
+                std::memcmp(it->key.data() + g + c, key.data() + g + c, sizeof(uint64_t)) == 0)
+                return use(*it);
+    }
     // Learn on a plain launch: a diagnostic launch keeps its own records, and a
     // counting launch (stats) runs the counting build, not the diagnostic one.
     if (a.diag || a.counters) return RT_OK;
@@ -1233,6 +1252,8 @@ int rt_set_option(rt_ctx* ctx, const char* name, int64_t value) {
         ctx->heavy_pixels = (int)value;
     } else if (std::strcmp(name, "heavy_pixel_factor") == 0 && value >= 1 && value <= 100000) {
         ctx->heavy_pixel_factor = (int)value;
+    } else if (std::strcmp(name, "reuse_order") == 0 && (value == 0 || value == 1)) {
+        ctx->reuse_order = (int)value;
     } else if (std::strcmp(name, "heavy_cap") == 0 && value >= 1 && value <= 100) {
         ctx->heavy_cap = (int)value;
     } else if (std::strcmp(name, "concurrent_launches") == 0 && value >= 1 && value <= 64) {
@@ -1274,6 +1295,7 @@ int rt_get_option(rt_ctx* ctx, const char* name, int64_t* value) {
     else if (std::strcmp(name, "heavy_factor") == 0) *value = ctx->heavy_factor;
     else if (std::strcmp(name, "concurrent_launches") == 0) *value = ctx->concurrent_launches;
     else if (std::strcmp(name, "heavy_cap") == 0) *value = ctx->heavy_cap;
+    else if (std::strcmp(name, "reuse_order") == 0) *value = ctx->reuse_order;
     else if (std::strcmp(name, "heavy_pixels") == 0) *value = ctx->heavy_pixels;
     else if (std::strcmp(name, "heavy_pixel_factor") == 0) *value = ctx->heavy_pixel_factor;
     else if (std::strcmp(name, "heavy_pixels_used") == 0) *value = ctx->dev.empty() ? 0 : ctx->dev[0].last_heavy_px;

@@ -222,6 +222,12 @@ int rt_render_wait(rt_ctx* ctx, uint64_t ticket);
  *                   workgroups of the launch, and every tile wave skips its
  *                   heavy pixels; 0 = whole heavy tiles
  *   "heavy_pixel_factor" see heavy_pixels (1..100000, default 75)
+ *   "reuse_order"   heavy_first: 1 (default) = a camera that has just moved
+ *                   (the launch key differs from the previous launch's only in
+ *                   the camera) uses the newest order learned for the same
+ *                   frame geometry and scene instead of learning (no learning
+ *                   frame while the camera moves; the first repeat of a camera
+ *                   learns); 0 = every new camera learns
  *   "heavy_pixels_used" (rt_get_option only) heavy pixels of the last launch
  *   "graph"         kernel 0, plain launches on a non-null stream: 1 (default)
  *                   = captured once per launch key (scene, camera, frame,

@@ -18,7 +18,7 @@ DEFAULT_OPTS = {"kernel": 0, "shade_min": 16, "blocks_per_cu": 0, "wave_tile": 2
                 "heavy_budget": 256, "prio_after": 0, "coop_lanes": 2, "walk": 2, "coop_walk": 0,
                 "block_waves": 1, "heavy_first": 1, "heavy_tiles": -1, "heavy_stream": 2,
                 "learn_cost": 1, "heavy_factor": 130, "graph": 1, "concurrent_launches": 1, "heavy_cap": 75,
-                "heavy_pixels": 1, "heavy_pixel_factor": 75}
+                "heavy_pixels": 1, "heavy_pixel_factor": 75, "reuse_order": 1}
 
 
 def _oracle(built, cam_bytes, w, h, b, **kw):
@@ -268,6 +268,33 @@ def test_heavy_pixels(renderer, cfg_k, factor):
     finally:
         for k, v in DEFAULT_OPTS.items():
             renderer.set_option(k, v)
+
+
+def test_moving_camera_reuses_order(renderer):
+    """Option reuse_order: a camera that has just moved uses the order and
+    heavy pixels learned at another camera (no learning frame), which only
+    changes the schedule; the first repeat of a camera learns its own.  Every
+    frame equals the oracle's."""
+    from rtamd import configs
+    cfg = configs.get(3)
+    built = cfg.build()
+    renderer.upload_scene(built)
+    W, H, B = cfg.width, cfg.height, cfg.max_bounces
+    cams = [configs.Camera((-25.0, 30.0, 140.0 + dz), (0.0, 0.0, 0.0), (0.0, 1.0, 0.0), 20.0, W / H)
+            for dz in (1.0, 3.0, 5.0)]
+    seq = [0, 0, 1, 2, 2, 2]                      # learn at 0; 1 and 2 move; 2 repeats (learns), then stays
+    used = []
+    for c in seq:
+        cam = cams[c]
+        rgba, rad, _ = _bands_device(renderer, cam, W, H, B, H, 1, 0, stats=False)
+        used.append(renderer.get_option("heavy_pixels_used"))
+        ref = _oracle(built, cam.ubo_bytes(), W, H, B, row_step=16)
+        _assert_same(rgba[::16], rad[::16], None, *ref)
+    assert used[0] == 0                           # the learning launch itself runs without an order
+    assert used[1] > 0                            # camera 0's own order
+    assert used[2] == used[1] and used[3] == used[1]   # moving: camera 0's order reused, no learning
+    assert used[4] == 0                           # camera 2 repeated: this launch learns
+    assert used[5] > 0                            # camera 2's own order
 
 
 def test_first_tile_launch_counts(renderer):
