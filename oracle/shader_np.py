@@ -67,12 +67,15 @@ def random_in_unit_sphere(seed: np.ndarray):                  # :63-70
 
 
 def render(vertices, materials, nodes, camera_ubo: bytes, width: int, height: int, max_bounces: int,
-           rows=None, ext: int = 0, accum=None, spheres=None):
+           rows=None, ext: int = 0, accum=None, spheres=None, on_segment=None):
     """Returns (rgba[len(rows), W, 4], radiance[len(rows), W, 3], counts dict).
     ext / accum / spheres: the non-reference extensions of oracle/rt_oracle.h
     (ORC_EXT_*), restated independently; accum float32[len(rows), W, 3] is
     updated in place; spheres float32[n, 8] = (centre.xyz, radius, albedo.rgb,
-    type), hit-tested after the BVH walk with ext bit 8."""
+    type), hit-tested after the BVH walk with ext bit 8.
+    on_segment (analysis aid, tools/): called after every bounce's walks with
+    (b, pixel indices, ray origins (n,3), directions (n,3), node visits (n,));
+    it changes nothing."""
     V = np.frombuffer(bytes(vertices), np.float32)
     V = V[: (V.size // 12) * 12].reshape(-1, 3, 4)[:, :, :3]    # (the empty scene's 1-float dummy: none)
     M = np.frombuffer(bytes(materials), np.float32)
@@ -125,6 +128,7 @@ def render(vertices, materials, nodes, camera_ubo: bytes, width: int, height: in
         rdx, rdy, rdz = dx[act], dy[act], dz[act]
         stack = np.zeros((A, 64), np.int64)
         sp = np.zeros(A, np.int64)
+        ray_visits = np.zeros(A, np.int64) if on_segment is not None else None
         if n_nodes > 0:
             sp[:] = 1
         while True:
@@ -134,6 +138,8 @@ def render(vertices, materials, nodes, camera_ubo: bytes, width: int, height: in
             sp[w] -= 1
             node = stack[w, sp[w]]
             counts["node_visits"] += w.size
+            if ray_visits is not None:
+                ray_visits[w] += 1
             with np.errstate(divide="ignore"):                                 # 1/0 = inf, as on the GPU
                 ix = F(1.0) / rdx[w]; iy = F(1.0) / rdy[w]; iz = F(1.0) / rdz[w]    # hit_aabb :88-103
             t0x = (BMIN[node, 0] - rox[w]) * ix; t1x = (BMAX[node, 0] - rox[w]) * ix
@@ -206,6 +212,8 @@ def render(vertices, materials, nodes, camera_ubo: bytes, width: int, height: in
             flip = _dot(rdx[g], rdy[g], rdz[g], snx, sny, snz) > F(0.0)
             nx[g] = np.where(flip, -snx, snx); ny[g] = np.where(flip, -sny, sny); nz[g] = np.where(flip, -snz, snz)
 
+        if on_segment is not None:
+            on_segment(b, act, np.stack([rox, roy, roz], 1), np.stack([rdx, rdy, rdz], 1), ray_visits)
         gh = hit != -1
         # miss: final = att * sky, path ends (:224-227)
         ms = act[~gh]
