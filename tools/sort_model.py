@@ -56,7 +56,7 @@ def main():
 
     shader_np.render(b.model_vertex_data, b.model_material_data, b.flat_bvh_data, cfg.camera().ubo_bytes(), W, H,
                      cfg.max_bounces, rows=rows, on_segment=on_segment)
-    tot = {"tile": 0, "octant_morton": 0, "cube_morton": 0, "ideal": 0}
+    tot = {"tile": 0, "octant_morton": 0, "cube_morton": 0, "coarse_stable": 0, "coarse_random": 0, "ideal": 0}
     for bb, act, o, d, vis in rec:
         # 32x2 tiles: pixel index p -> (row, col) in the rows block
         r, c = act // W, act % W
@@ -79,14 +79,22 @@ def main():
         a2 = np.take_along_axis(d, ((ax + 2) % 3)[:, None], 1)[:, 0] / np.abs(d[np.arange(len(d)), ax])
         cell = (face * 64 + np.clip(((a1 + 1) * 4).astype(np.int64), 0, 7) * 8 + np.clip(((a2 + 1) * 4).astype(np.int64), 0, 7))
         s2, u2 = lockstep(vis, np.lexsort((mo, cell)))
+        coarse = (mo >> np.uint64(24)).astype(np.int64)
+        key = cell * 64 + coarse
+        s4, u4 = lockstep(vis, np.lexsort((np.arange(len(key)), key)))          # stable: pixel order in a bucket
+        rng = np.random.default_rng(1)
+        s5, u5 = lockstep(vis, np.lexsort((rng.permutation(len(key)), key)))    # atomics: random order in a bucket
         s3, u3 = lockstep(vis, np.argsort(vis))
         tot["tile"] += steps_tile
         tot["octant_morton"] += s1
         tot["cube_morton"] += s2
+        tot["coarse_stable"] += s4
+        tot["coarse_random"] += s5
         tot["ideal"] += s3
         print(f"bounce {bb}: {len(act)} rays, {int(vis.sum())} visits; wave steps: tiles {steps_tile} "
               f"(util {vis.sum() / (64 * steps_tile):.3f}), octant+Morton {s1} ({u1:.3f}), "
-              f"cube cell+Morton {s2} ({u2:.3f}), ideal {s3} ({u3:.3f})", flush=True)
+              f"cube cell+Morton {s2} ({u2:.3f}), cell+coarse6 stable {s4} ({u4:.3f}), "
+              f"cell+coarse6 random {s5} ({u5:.3f}), ideal {s3} ({u3:.3f})", flush=True)
     print("total", tot)
 
 
