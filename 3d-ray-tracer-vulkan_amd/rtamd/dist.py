@@ -33,27 +33,38 @@ def band_rows(height: int, band_h: int, world: int, rank: int) -> np.ndarray:
 
 
 def gather_frame(local, height: int, band_h: int, group=None):
-    """Gather every rank's packed band rows (torch tensor [rows_r, W, C]) to
-    rank 0 and assemble the [height, W, C] frame there (None elsewhere)."""
+    """Gather every rank's packed band rows (torch tensor [rows_r, W, C], or
+    the padded [max_rows, W, C] buffer) to rank 0 and assemble the
+    [height, W, C] frame there (None elsewhere).  A one-frame batch: one
+    gather into a single stack and one index_select with a cached device
+    index, so a step issues no host-to-device copy and never waits on the GPU."""
     import torch
     import torch.distributed as dist
     world = dist.get_world_size(group)
-    rank = dist.get_rank(group)
-    counts = [band_row_count(height, band_h, world, r) for r in range(world)]
-    max_rows = max(counts)
-    if local.shape[0] < max_rows:
-        pad = torch.zeros((max_rows - local.shape[0],) + tuple(local.shape[1:]), dtype=local.dtype,
+    plan, src_index = _cached_plan(height, band_h, world, 1, local.device)
+    if local.shape[0] < plan.max_rows:
+        pad = torch.zeros((plan.max_rows - local.shape[0],) + tuple(local.shape[1:]), dtype=local.dtype,
                           device=local.device)
         local = torch.cat([local, pad])
-    gl = [torch.empty_like(local) for _ in range(world)] if rank == 0 else None
-    dist.gather(local, gl, dst=0, group=group)
-    if rank != 0:
-        return None
-    out = torch.empty((height,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
-    for r in range(world):
-        rows = torch.as_tensor(band_rows(height, band_h, world, r), device=local.device)
-        out[rows] = gl[r][: counts[r]]
-    return out
+    elif local.shape[0] > plan.max_rows:
+        local = local[: plan.max_rows]
+    out = gather_batch(local.unsqueeze(0), plan, group, src_index=src_index)
+    return None if out is None else out[0]
+
+
+def gather_frames(local, height: int, band_h: int, group=None):
+    """Several one-frame steps of the bands partition gathered at once:
+    local is this rank's [n_frames, max_rows, W, C] packed bands of n_frames
+    frames (rank r traced the bands r of each); returns the
+    [n_frames, height, W, C] frames on rank 0, None elsewhere.  One collective
+    and one index_select for the whole batch, so the per-frame host cost of
+    the exchange shrinks with the batch."""
+    import torch.distributed as dist
+    world = dist.get_world_size(group)
+    plan, src_index = _cached_plan(height, band_h, world, local.shape[0], local.device, rotate=False)
+    if local.shape[1] != plan.max_rows:
+        raise ValueError(f"gather_frames: {local.shape[1]} rows per frame, the partition packs {plan.max_rows}")
+    return gather_batch(local, plan, group, src_index=src_index)
 
 
 # --- frame batches (weak scaling) -------------------------------------------
@@ -75,10 +86,13 @@ def batch_band_offset(frame: int, world: int, rank: int) -> int:
 class BatchPlan:
     """Row bookkeeping of an n_frames batch over world ranks (band_h-row bands)."""
 
-    def __init__(self, height: int, band_h: int, world: int, n_frames: int):
+    def __init__(self, height: int, band_h: int, world: int, n_frames: int, rotate: bool = True):
+        # rotate: frame f of the batch gives rank r the bands (r + f) mod world
+        # (frames partition); else every frame gives rank r the bands r (a
+        # batch of consecutive one-frame steps of the bands partition)
         self.height, self.band_h, self.world, self.n_frames = height, band_h, world, n_frames
-        self.rows = [[band_rows(height, band_h, world, batch_band_offset(f, world, r)) for f in range(n_frames)]
-                     for r in range(world)]
+        self.rows = [[band_rows(height, band_h, world, batch_band_offset(f, world, r) if rotate else r)
+                      for f in range(n_frames)] for r in range(world)]
         self.max_rows = max(len(x) for per_rank in self.rows for x in per_rank)
         # source row (in the gathered [world, n_frames, max_rows] stack) of every
         # row of every frame: one index_select assembles the whole batch
@@ -91,6 +105,21 @@ class BatchPlan:
 
     def local_rows(self, rank: int, frame: int) -> int:
         return len(self.rows[rank][frame])
+
+
+_PLANS: dict = {}
+
+
+def _cached_plan(height: int, band_h: int, world: int, n_frames: int, device, rotate: bool = True):
+    """BatchPlan and its source-row index on `device`, built once per layout."""
+    import torch
+    key = (height, band_h, world, n_frames, str(device), rotate)
+    hit = _PLANS.get(key)
+    if hit is None:
+        plan = BatchPlan(height, band_h, world, n_frames, rotate)
+        hit = (plan, torch.as_tensor(plan.src, device=device))
+        _PLANS[key] = hit
+    return hit
 
 
 def gather_batch(local, plan: BatchPlan, group=None, src_index=None):

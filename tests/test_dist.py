@@ -70,27 +70,27 @@ def test_band_gather_reassembles_frame(world, band_h):
     assert np.array_equal(frame, ref)
 
 
-def _batch_worker(rank, world, port, band_h, q):
+def _batch_worker(rank, world, port, band_h, q, rotate=True):
     import sys
     sys.path[:0] = [os.path.join(ROOT, "3d-ray-tracer-vulkan_amd"), ROOT]
     import torch
     import torch.distributed as dist
     from oracle import oracle_lib
     from rtamd import configs
-    from rtamd.dist import BatchPlan, batch_band_offset, band_rows, gather_batch
+    from rtamd.dist import BatchPlan, batch_band_offset, band_rows, gather_batch, gather_frames
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         cfg = configs.config2()
         built = cfg.build()
         W, H, B = 96, 53, 3
-        F = world
-        plan = BatchPlan(H, band_h, world, F)
+        F = world if rotate else 3
+        plan = BatchPlan(H, band_h, world, F, rotate)
         local = torch.zeros((F, plan.max_rows, W, 4), dtype=torch.uint8)
         traced = 0
         for f in range(F):
             cam = configs.Camera((-25.0 + 5 * f, 30.0, 140.0), (0.0, 0.0, 0.0), (0.0, 1.0, 0.0), 20.0, W / H)
-            rows = band_rows(H, band_h, world, batch_band_offset(f, world, rank))
+            rows = band_rows(H, band_h, world, batch_band_offset(f, world, rank) if rotate else rank)
             assert len(rows) == plan.local_rows(rank, f)
             for k, y in enumerate(rows):
                 rgba, _, _ = oracle_lib.render(built.model_vertex_data, built.model_material_data,
@@ -99,7 +99,7 @@ def _batch_worker(rank, world, port, band_h, q):
                 local[f, k] = torch.from_numpy(rgba[0])
             traced += len(rows)
         q.put(("traced", rank, traced))
-        frames = gather_batch(local, plan)
+        frames = gather_batch(local, plan) if rotate else gather_frames(local, H, band_h)
         if rank == 0:
             q.put(("frames", frames.numpy()))
     finally:
@@ -138,3 +138,34 @@ def test_batch_gather_reassembles_frames(world, band_h):
         ref = oracle_lib.render(built.model_vertex_data, built.model_material_data, built.flat_bvh_data,
                                 cam.ubo_bytes(), W, H, B)[0]
         assert np.array_equal(got["frames"][f], ref), f
+
+
+@pytest.mark.parametrize("world,band_h", [(2, 16), (3, 8)])
+def test_bands_steps_gathered_in_one_batch(world, band_h):
+    """Strong scaling with the exchange batched: three consecutive one-frame
+    steps (rank r traces the bands r of each) gathered by one collective
+    (gather_frames, as bench.py does every few steps) give the three frames."""
+    from oracle import oracle_lib
+    from rtamd import configs
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_batch_worker, args=(r, world, port, band_h, q, False)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = None
+    for _ in range(world + 1):
+        item = q.get(timeout=300)
+        if item[0] == "frames":
+            got = item[1]
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    built = configs.config2().build()
+    W, H, B = 96, 53, 3
+    assert got.shape == (3, H, W, 4)
+    for f in range(3):
+        cam = configs.Camera((-25.0 + 5 * f, 30.0, 140.0), (0.0, 0.0, 0.0), (0.0, 1.0, 0.0), 20.0, W / H)
+        ref = oracle_lib.render(built.model_vertex_data, built.model_material_data, built.flat_bvh_data,
+                                cam.ubo_bytes(), W, H, B)[0]
+        assert np.array_equal(got[f], ref), f

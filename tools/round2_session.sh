@@ -5,6 +5,7 @@
 # limit; a failure ends the session.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export GPU_MAX_HW_QUEUES=16      # as bench.py sets it: one hardware queue per stream
 TAG=${1:-r2final}
 OUT=gpurun_out/$TAG
 mkdir -p "$OUT"
@@ -17,7 +18,7 @@ for c in 4 5 6; do
 done
 step pipeline 300 python tools/pipeline_bench.py > "$OUT/pipeline.jsonl" 2> "$OUT/pipeline.err" || exit $?
 step inflight 300 python tools/inflight_bench.py > "$OUT/inflight.jsonl" 2> "$OUT/inflight.err" || exit $?
-step share 300 python tools/rank_share_bench.py > "$OUT/rank_share.jsonl" 2> "$OUT/rank_share.err" || exit $?
+step share 300 python tools/share_inflight_bench.py --ranks 1,2,4,8 > "$OUT/share_inflight.jsonl" 2> "$OUT/share_inflight.err" || exit $?
 TAG=$TAG BACKENDS=gloo NPROC=2 step rehearsal2 600 bash tools/dist_rehearsal.sh || exit $?
 TAG=$TAG BACKENDS=gloo NPROC=4 PARTS=bands step rehearsal4 600 bash tools/dist_rehearsal.sh || exit $?
 echo "$(date +%T) round2 session done" >> "$OUT/status.txt"
