@@ -212,6 +212,8 @@ int build_host_scene(const void* vertices, size_t vertex_bytes,
 
 using namespace rtamd;
 
+static constexpr int kMaxSlots = 8;   // rt_render_async frame slots per device
+
 struct PerDevice {
     int          device = 0;
     hipStream_t  stream = nullptr;
@@ -232,11 +234,14 @@ struct PerDevice {
     size_t       heavy_cap = 0;
     int          n_cu = 0;
     int          blocks_per_cu = 1;
-    // rt_render_async: two frame slots, a copy stream, per-slot events
+    // rt_render_async: frame slots (option async_slots), each with its own
+    // trace stream, one copy stream, per-slot events and the last ticket of a slot
     hipStream_t  copy_stream = nullptr;
-    uchar4*      d_ring[2] = {nullptr, nullptr};
+    uchar4*      d_ring[kMaxSlots] = {};
     size_t       ring_cap = 0;     // pixels per slot
-    hipEvent_t   traced[2] = {nullptr, nullptr}, copied[2] = {nullptr, nullptr};
+    hipStream_t  slot_stream[kMaxSlots] = {};
+    hipEvent_t   traced[kMaxSlots] = {}, copied[kMaxSlots] = {};
+    uint64_t     slot_ticket[kMaxSlots] = {};
     float*       d_accum = nullptr;  // extension kExtAccumulate: running sums
     float4*      d_spheres = nullptr; // extension kExtSpheres: 2 float4 per sphere
     int          n_spheres = 0;
@@ -318,6 +323,8 @@ struct rt_ctx {
     int  reuse_order = 1;          // heavy_first: a moving camera reuses the order learned at another camera
     int  heavy_cap = 75;           // automatic heavy tiles: at most this percentage of one generation of
                                    //   one-pixel waves (CUs x 24 / 64 tiles)
+    int  async_slots = 4;          // rt_render_async: frames in flight per device, each on its own stream
+    int  in_async = 0;             // set while rt_render_async plans a launch: its frames in flight
     int  concurrent_launches = 1;  // launches of similar work the caller keeps in flight on a device at once
                                    //   (the heavy-tile bulk estimate counts this launch's work that many times)
     int  learn_cost = 1;           // heavy_first cost: 0 = lockstep steps + 2 x coop windows, 1 = wave duration
@@ -343,6 +350,11 @@ static void free_scene(PerDevice& p) {
     if (p.scene.mats) (void)hipFree(p.scene.mats);
     p.scene = DevScene{};
 }
+
+// Launches of similar work on a device at once, for the heavy-pixel bar: the
+// caller's statement (option concurrent_launches), or rt_render_async's own
+// frames in flight.
+static int concurrency(const rt_ctx* ctx) { return std::max(ctx->concurrent_launches, ctx->in_async); }
 
 // The extensions exist in kernel 0 only; with any of them on, kernel 0 runs.
 static int effective_kernel(const rt_ctx* ctx) { return ctx->ext ? kKernelSimple : ctx->kernel; }
@@ -373,7 +385,7 @@ static int plan_order(const rt_ctx* ctx, PerDevice& p, TraceArgs& a, const rt_ca
     const size_t n = (size_t)((a.tw + tw_w - 1) / tw_w) * (size_t)((a.th + th_w - 1) / th_w);
     const int geo[] = {a.width, a.height, a.max_bounces, a.x0, a.y0, a.tw, a.th, a.band_h, a.band_stride,
                        a.band_off, a.wave_tile, a.ext, a.coop_lanes, a.walk, ctx->learn_cost, ctx->heavy_factor,
-                       ctx->concurrent_launches, ctx->heavy_cap, ctx->heavy_pixel_factor};
+                       concurrency(ctx), ctx->heavy_cap, ctx->heavy_pixel_factor};
     std::vector<uint8_t> key(sizeof(geo) + sizeof(rt_camera_ubo) + sizeof(uint64_t));
     std::memcpy(key.data(), geo, sizeof(geo));
     std::memcpy(key.data() + sizeof(geo), cam, sizeof(rt_camera_ubo));
@@ -457,7 +469,7 @@ static int plan_order(const rt_ctx* ctx, PerDevice& p, TraceArgs& a, const rt_ca
 // cooperative windows (diag record words 4 and 5): the length of the wave's
 // dependent chain, free of when the wave happened to run.
 static int learn_order(const rt_ctx* ctx, PerDevice& p, const TraceArgs& a, hipStream_t s) {
-    const int learn_cost = ctx->learn_cost, concurrent = ctx->concurrent_launches;
+    const int learn_cost = ctx->learn_cost, concurrent = concurrency(ctx);
     const double heavy_factor = ctx->heavy_factor / 100.0;
     if (!a.diag || a.diag != p.d_learn) return RT_OK;
     const size_t n = p.learning_n;
@@ -762,7 +774,7 @@ int rt_create(const int* device_ids, int n_devices, rt_ctx** out) {
         if (e == hipSuccess) e = hipMalloc(&p.d_counters, 2 * sizeof(Counters));   // [1]: trace_coop's sink
         if (e == hipSuccess) e = hipMalloc(&p.d_queue, sizeof(unsigned) * 3 * kQueueSlots);
         if (e == hipSuccess) e = hipStreamCreateWithFlags(&p.copy_stream, hipStreamNonBlocking);
-        for (int k2 = 0; k2 < 2 && e == hipSuccess; ++k2) {
+        for (int k2 = 0; k2 < kMaxSlots && e == hipSuccess; ++k2) {
             e = hipEventCreateWithFlags(&p.traced[k2], hipEventDisableTiming);
             if (e == hipSuccess) e = hipEventCreateWithFlags(&p.copied[k2], hipEventDisableTiming);
         }
@@ -786,10 +798,12 @@ int rt_destroy(rt_ctx* ctx) {
         if (p.stream) (void)hipStreamSynchronize(p.stream);
         if (p.copy_stream) (void)hipStreamSynchronize(p.copy_stream);
         free_scene(p);
-        for (int k2 = 0; k2 < 2; ++k2) {
+        for (int k2 = 0; k2 < kMaxSlots; ++k2) {
+            if (p.slot_stream[k2]) (void)hipStreamSynchronize(p.slot_stream[k2]);
             if (p.d_ring[k2]) (void)hipFree(p.d_ring[k2]);
             if (p.traced[k2]) (void)hipEventDestroy(p.traced[k2]);
             if (p.copied[k2]) (void)hipEventDestroy(p.copied[k2]);
+            if (p.slot_stream[k2]) (void)hipStreamDestroy(p.slot_stream[k2]);
         }
         if (p.copy_stream) (void)hipStreamDestroy(p.copy_stream);
         if (p.d_counters) (void)hipFree(p.d_counters);
@@ -1152,30 +1166,39 @@ int rt_render_async(rt_ctx* ctx, const rt_camera_ubo* cam, int width, int height
     const int n_bands = (height + bh - 1) / bh;
     const size_t band_bytes = (size_t)bh * (size_t)width * 4;
     const uint64_t t = ctx->issued + 1;
-    const int slot = (int)(t & 1);
+    const int S = ctx->async_slots;
+    const int slot = (int)(t % (uint64_t)S);
     for (int k = 0; k < nd; ++k) {
         const int rows = rt_band_rows(height, bh, nd, k);
         if (rows == 0) continue;
         PerDevice& p = ctx->dev[k];
         RT_HIP_CHECK(hipSetDevice(p.device));
         const size_t px = (size_t)width * rows;
-        if (px > p.ring_cap) {                      // grow both slots once nothing is in flight
-            RT_HIP_CHECK(hipStreamSynchronize(p.stream));
+        if (px > p.ring_cap) {                      // grow every slot once nothing is in flight
+            for (int k2 = 0; k2 < kMaxSlots; ++k2)
+                if (p.slot_stream[k2]) RT_HIP_CHECK(hipStreamSynchronize(p.slot_stream[k2]));
             RT_HIP_CHECK(hipStreamSynchronize(p.copy_stream));
-            for (int k2 = 0; k2 < 2; ++k2) {
+            for (int k2 = 0; k2 < kMaxSlots; ++k2) {
                 if (p.d_ring[k2]) (void)hipFree(p.d_ring[k2]);
                 p.d_ring[k2] = nullptr;
             }
-            p.ring_cap = 0;
-            for (int k2 = 0; k2 < 2; ++k2) RT_HIP_CHECK(hipMalloc(&p.d_ring[k2], px * 4));
             p.ring_cap = px;
         }
-        // The slot's previous frame (ticket t-2) must be read back before it is overwritten.
-        RT_HIP_CHECK(hipStreamWaitEvent(p.stream, p.copied[slot], 0));
-        rc = render_bands_on(ctx, p, cam, width, height, max_bounces, bh, nd, k, rows, p.d_ring[slot], nullptr,
-                             p.stream, false);
+        if (!p.d_ring[slot]) RT_HIP_CHECK(hipMalloc(&p.d_ring[slot], p.ring_cap * 4));
+        // Each slot traces on its own stream (its own hardware queue with
+        // GPU_MAX_HW_QUEUES >= slots + 2), so the frames in flight run at once.
+        if (!p.slot_stream[slot]) RT_HIP_CHECK(hipStreamCreateWithFlags(&p.slot_stream[slot], hipStreamNonBlocking));
+        const hipStream_t ts = p.slot_stream[slot];
+        // The slot's previous frame must be read back before it is overwritten.
+        RT_HIP_CHECK(hipStreamWaitEvent(ts, p.copied[slot], 0));
+        ctx->in_async = S;
+        rc = render_bands_on(ctx, p, cam, width, height, max_bounces, bh, nd, k, rows, p.d_ring[slot], nullptr, ts,
+                             false);
+        ctx->in_async = 0;
         if (rc) return rc;
-        RT_HIP_CHECK(hipEventRecord(p.traced[slot], p.stream));
+        RT_HIP_CHECK(hipEventRecord(p.traced[slot], ts));
+        // Copies run in ticket order on the one copy stream, whatever order the
+        // traces finish in.
         RT_HIP_CHECK(hipStreamWaitEvent(p.copy_stream, p.traced[slot], 0));
         if (nd == 1) {
             RT_HIP_CHECK(hipMemcpyAsync(out_rgba, p.d_ring[slot], px * 4, hipMemcpyDeviceToHost, p.copy_stream));
@@ -1196,6 +1219,7 @@ int rt_render_async(rt_ctx* ctx, const rt_camera_ubo* cam, int width, int height
                                             p.copy_stream));
         }
         RT_HIP_CHECK(hipEventRecord(p.copied[slot], p.copy_stream));
+        p.slot_ticket[slot] = t;
     }
     ctx->issued = t;
     *ticket = t;
@@ -1209,11 +1233,15 @@ int rt_render_wait(rt_ctx* ctx, uint64_t ticket) {
                   (unsigned long long)ctx->issued);
         return RT_ERR_INVALID_ARG;
     }
-    // A slot's event may since have been re-recorded by a newer frame; copies
-    // complete in issue order, so waiting for the newer one covers this one.
+    // Copies complete in ticket order, so the copy event of any slot whose
+    // last ticket is >= this one covers it (the oldest such slot waits least).
     for (PerDevice& p : ctx->dev) {
         RT_HIP_CHECK(hipSetDevice(p.device));
-        RT_HIP_CHECK(hipEventSynchronize(p.copied[ticket & 1]));
+        int best = -1;
+        for (int k2 = 0; k2 < kMaxSlots; ++k2)
+            if (p.slot_ticket[k2] >= ticket && (best < 0 || p.slot_ticket[k2] < p.slot_ticket[best])) best = k2;
+        if (best >= 0) RT_HIP_CHECK(hipEventSynchronize(p.copied[best]));
+        else RT_HIP_CHECK(hipStreamSynchronize(p.copy_stream));   // a device with no rows of that frame
     }
     return RT_OK;
 }
@@ -1256,6 +1284,8 @@ int rt_set_option(rt_ctx* ctx, const char* name, int64_t value) {
         ctx->reuse_order = (int)value;
     } else if (std::strcmp(name, "heavy_cap") == 0 && value >= 1 && value <= 100) {
         ctx->heavy_cap = (int)value;
+    } else if (std::strcmp(name, "async_slots") == 0 && value >= 1 && value <= kMaxSlots) {
+        ctx->async_slots = (int)value;
     } else if (std::strcmp(name, "concurrent_launches") == 0 && value >= 1 && value <= 64) {
         ctx->concurrent_launches = (int)value;
     } else if (std::strcmp(name, "learn_cost") == 0 && (value == 0 || value == 1)) {
@@ -1294,6 +1324,7 @@ int rt_get_option(rt_ctx* ctx, const char* name, int64_t* value) {
     else if (std::strcmp(name, "learn_cost") == 0) *value = ctx->learn_cost;
     else if (std::strcmp(name, "heavy_factor") == 0) *value = ctx->heavy_factor;
     else if (std::strcmp(name, "concurrent_launches") == 0) *value = ctx->concurrent_launches;
+    else if (std::strcmp(name, "async_slots") == 0) *value = ctx->async_slots;
     else if (std::strcmp(name, "heavy_cap") == 0) *value = ctx->heavy_cap;
     else if (std::strcmp(name, "reuse_order") == 0) *value = ctx->reuse_order;
     else if (std::strcmp(name, "heavy_pixels") == 0) *value = ctx->heavy_pixels;

@@ -191,12 +191,15 @@ class HipEngine:
 
     def __init__(self, frame_queue: AtomicReference, width: int = REFERENCE_WIDTH,
                  height: int = REFERENCE_HEIGHT, max_bounces: int = REFERENCE_MAX_BOUNCES,
-                 device_ids: Sequence[int] = (0,), collect_stats: bool = False, pipelined: bool = True):
+                 device_ids: Sequence[int] = (0,), collect_stats: bool = False, pipelined: bool = True,
+                 inflight: int = 4):
         self.frame_queue = frame_queue
-        # pipelined: two frames in flight (rt_render_async), so frame k's readback
-        # overlaps frame k+1's trace; the reference waits for each frame
+        # pipelined: `inflight` frames in flight (rt_render_async, one slot and
+        # trace stream each), so the frames' traces overlap each other and
+        # their readbacks; the reference waits for each frame
         # (VulkanEngine.java:410-429).  Stats need the synchronous path.
         self.pipelined = pipelined and not collect_stats
+        self.inflight = max(1, min(8, int(inflight)))
         self.width, self.height, self.max_bounces = width, height, max_bounces
         self.device_ids = tuple(device_ids)
         self.collect_stats = collect_stats
@@ -234,6 +237,7 @@ class HipEngine:
         slots, pending = None, []
         try:
             renderer = Renderer(self.device_ids)
+            renderer.set_option("async_slots", self.inflight)
             have_scene, camera = False, None
             while self._running:
                 try:                                        # one scene per pass (:281-285)
@@ -265,11 +269,11 @@ class HipEngine:
                     self._publish(FrameData(rgba, st))
                     continue
                 if slots is None:
-                    slots = [PinnedFrame(self.height, self.width) for _ in range(2)]
-                k = self.frames_submitted % 2
+                    slots = [PinnedFrame(self.height, self.width) for _ in range(self.inflight)]
+                k = self.frames_submitted % self.inflight
                 pending.append((renderer.render_async(ubo, self.width, self.height, self.max_bounces, slots[k]), k))
                 self.frames_submitted += 1
-                if len(pending) == 2:
+                if len(pending) == self.inflight:
                     self._finish(renderer, slots, pending.pop(0))
             while pending:                                  # drain on stop
                 self._finish(renderer, slots, pending.pop(0))

@@ -148,8 +148,14 @@ int rt_band_rows(int height, int band_h, int band_stride, int band_off);
  *
  * rt_render_async enqueues one whole frame (trace + RGBA8 readback into
  * out_rgba) and returns at once with a ticket; rt_render_wait blocks until that
- * frame is complete in out_rgba.  Two frame slots rotate per device, so with two
- * frames in flight the readback of frame k overlaps the trace of frame k+1.
+ * frame is complete in out_rgba.  Option "async_slots" (1..8, default 4) frame
+ * slots rotate per device, each tracing on a stream of its own, so with that
+ * many frames in flight the frames' traces run at once and every readback
+ * overlaps later traces (copies complete in ticket order).  The heavy-pixel
+ * bar counts the slots as concurrent launches.  Concurrent streams need a
+ * hardware queue each, and HIP's default is 4 per process, fixed when the HIP
+ * runtime loads: start the host process with GPU_MAX_HW_QUEUES=16 (JVM:
+ * `GPU_MAX_HW_QUEUES=16 java ...`; the Python package sets it on import).
  * out_rgba must stay valid until its ticket completes; it should come from
  * rt_host_alloc (pinned, portable), since a copy into pageable memory cannot run
  * asynchronously.  A Java host wraps rt_host_alloc memory with JNI

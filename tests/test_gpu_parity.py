@@ -414,10 +414,13 @@ def test_multi_device_context_interleaves(renderer):
         assert st[k] == ref_st[k]
 
 
-@pytest.mark.parametrize("devices", [(0,), (0, 0)])
-def test_render_async_matches_sync(devices):
-    """rt_render_async (two slots, copy stream, strided band readback) gives
-    rt_render's frames, in order, with frames in flight and a new camera per frame."""
+@pytest.mark.parametrize("devices,slots", [((0,), 2), ((0, 0), 2), ((0,), 4), ((0, 0), 3), ((0,), 8)])
+def test_render_async_matches_sync(devices, slots):
+    """rt_render_async (option async_slots frame slots, each tracing on its own
+    stream; one copy stream; strided band readback) gives rt_render's frames,
+    in order, with that many frames in flight and a new camera per frame; a
+    wait on an older ticket returns once it is done even after newer frames
+    reused its slot."""
     if not has_gpu():
         pytest.skip("no GPU")
     import rtamd
@@ -427,24 +430,30 @@ def test_render_async_matches_sync(devices):
     built = cfg.build()
     w, h, b = 333, 201, 3            # 201 rows: a partial last 16-row band
     r = rtamd.Renderer(devices)
-    frames = [PinnedFrame(h, w) for _ in range(2)]
+    frames = [PinnedFrame(h, w) for _ in range(slots)]
     try:
+        r.set_option("async_slots", slots)
+        assert r.get_option("async_slots") == slots
         r.upload_scene(built)
         cams = [rtamd.Camera((-25.0 + 7 * k, 30.0, 140.0 - 9 * k), (0.0, 0.0, 0.0), (0.0, 1.0, 0.0), 20.0, w / h)
-                for k in range(5)]
+                for k in range(2 * slots + 3)]
         refs = [r.render(c, w, h, b)[0] for c in cams]
         pending = []
         for k, c in enumerate(cams):
-            pending.append((r.render_async(c, w, h, b, frames[k % 2]), k))
-            if len(pending) == 2:
+            pending.append((r.render_async(c, w, h, b, frames[k % slots]), k))
+            if len(pending) == slots:
                 t, j = pending.pop(0)
                 r.wait(t)
-                assert np.array_equal(frames[j % 2].array, refs[j]), f"frame {j}"
-        t, j = pending.pop(0)
-        r.wait(t)
-        assert np.array_equal(frames[j % 2].array, refs[j])
+                assert np.array_equal(frames[j % slots].array, refs[j]), f"frame {j}"
+        while pending:
+            t, j = pending.pop(0)
+            r.wait(t)
+            assert np.array_equal(frames[j % slots].array, refs[j]), f"frame {j}"
+        r.wait(1)                    # long since done; its slot has been reused
         with pytest.raises(rtamd.RtError, match="INVALID_ARG"):
             r.wait(t + 1)
+        with pytest.raises(rtamd.RtError, match="INVALID_ARG"):
+            r.set_option("async_slots", 9)
     finally:
         r.close()
         for f in frames:

@@ -23,8 +23,8 @@ def main():
     ap.add_argument("--streams", default="1,2,3,4")
     ap.add_argument("--rounds", type=int, default=3)
     args = ap.parse_args()
+    import rtamd  # first: sets GPU_MAX_HW_QUEUES before torch loads HIP
     import torch
-    import rtamd
     from rtamd import configs
     from rtamd._lib import check
 

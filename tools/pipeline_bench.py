@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
 """PCIe-inclusive frame rate: synchronous rt_render vs pipelined rt_render_async
-(two frames in flight, pinned host frames), whole frames of a config.
+(--slots frames in flight, one slot and trace stream each, pinned host frames),
+whole frames of a config.
 
 Usage: python tools/pipeline_bench.py [--config 3] [--frames 60]
 Prints one JSON line per mode: frames/s, ms/frame, Mrays/s including the
@@ -20,10 +21,10 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", type=int, default=3)
     ap.add_argument("--frames", type=int, default=60)
+    ap.add_argument("--slots", default="2,4,8", help="rt_render_async frames in flight (async_slots) to time")
     args = ap.parse_args()
     import numpy as np
-    import torch  # noqa: F401  (load torch's HIP runtime first, as rtamd does)
-    import rtamd
+    import rtamd          # sets GPU_MAX_HW_QUEUES, then loads torch's HIP runtime first
     from rtamd import configs
     from rtamd.engine import PinnedFrame
 
@@ -35,31 +36,34 @@ def main():
     r.upload_scene(built)
     segs = r.render(cam, W, H, B, stats=True)[2]["segments"]
     pageable = np.empty((H, W, 4), np.uint8)
-    frames = [PinnedFrame(H, W) for _ in range(2)]
+    slots = [int(x) for x in args.slots.split(",")]
+    frames = [PinnedFrame(H, W) for _ in range(max(slots))]
 
     def sync_run(n):
         for _ in range(n):
             r.render(cam, W, H, B)
 
-    def async_run(n):
+    def async_run(n, d):
+        r.set_option("async_slots", d)
         pending = []
         for k in range(n):
-            pending.append(r.render_async(cam, W, H, B, frames[k % 2]))
-            if len(pending) == 2:
+            pending.append(r.render_async(cam, W, H, B, frames[k % d]))
+            if len(pending) == d:
                 r.wait(pending.pop(0))
         for t in pending:
             r.wait(t)
 
-    for name, fn in (("sync rt_render (pageable copy, fence per frame)", sync_run),
-                     ("rt_render_async, 2 in flight, pinned", async_run)):
-        fn(5)
+    modes = [("sync rt_render (pageable copy, fence per frame)", sync_run)]
+    modes += [(f"rt_render_async, {d} in flight, pinned", (lambda d: lambda n: async_run(n, d))(d)) for d in slots]
+    for name, fn in modes:
+        fn(20)
         t0 = time.perf_counter()
         fn(args.frames)
         dt = time.perf_counter() - t0
         print(json.dumps({"mode": name, "config": cfg.name, "frames": args.frames,
                           "fps": round(args.frames / dt, 1), "ms_per_frame": round(dt / args.frames * 1e3, 3),
                           "mrays_s_incl_pcie": round(segs * args.frames / dt / 1e6, 1)}), flush=True)
-    assert np.array_equal(frames[(args.frames - 1) % 2].array, r.render(cam, W, H, B)[0])
+    assert np.array_equal(frames[(args.frames - 1) % slots[-1]].array, r.render(cam, W, H, B)[0])
     del pageable
     r.close()
     for f in frames:
