@@ -304,12 +304,12 @@ struct rt_ctx {
     int  kernel = kKernelSimple;   // fastest measured on config 3
     int  shade_min = 16;
     int  blocks_per_cu = 0;        // 0 = from the occupancy query
-    int  wave_tile = 2;            // simple kernel: 8x8 / 16x4 / 32x2 (default) / 64x1
+    int  wave_tile = 0;            // simple kernel: 8x8 (default) / 16x4 / 32x2 / 64x1
     int  seg_limit = 2;            // split: segments traced in the lockstep pass
     int  diag = 0;                 // record per-wave timestamps (kernel 0 only)
     int  prio_after = 0;           // kernel 0: s_setprio(3) after this many node steps
     int  heavy_budget = 256;       // tiered: node visits per path in tier 1
-    int  coop_lanes = 2;           // kernel 0: cooperative tail once <= this many lanes walk (0 = off)
+    int  coop_lanes = 1;           // kernel 0: cooperative tail once <= this many lanes walk (0 = off)
     int  ext = 0;                  // non-reference extensions (kExt* bits), off by default
     int  walk = 2;                 // kernel 0: 0 = node per step, 1 = child pairs + t_enter stack,
                                    //   2 = node per step, software-pipelined (fastest measured)

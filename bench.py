@@ -424,7 +424,8 @@ def main() -> None:
                                                                       "heavy_first", "heavy_tiles", "heavy_factor",
                                                                       "heavy_stream", "heavy_pixels",
                                                                       "heavy_pixel_factor", "heavy_cap", "graph")},
-                             "concurrent_launches": F, "heavy_tiles_used": heavy_used,
+                             "concurrent_launches": renderer.get_option("concurrent_launches"),
+                             "heavy_tiles_used": heavy_used,
                              "heavy_pixels_used": renderer.get_option("heavy_pixels_used")},
                 "launches_per_step": F * (2 if heavy_used > 0 and renderer.get_option("heavy_stream") != 2 else 1),
             },

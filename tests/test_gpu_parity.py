@@ -14,8 +14,8 @@ from raw_bvh import raw_bvh_scene
 pytestmark = pytest.mark.gpu
 
 COUNTERS = ("segments", "node_visits", "tri_tests", "mat_reads")
-DEFAULT_OPTS = {"kernel": 0, "shade_min": 16, "blocks_per_cu": 0, "wave_tile": 2, "seg_limit": 2,
-                "heavy_budget": 256, "prio_after": 0, "coop_lanes": 2, "walk": 2, "coop_walk": 0,
+DEFAULT_OPTS = {"kernel": 0, "shade_min": 16, "blocks_per_cu": 0, "wave_tile": 0, "seg_limit": 2,
+                "heavy_budget": 256, "prio_after": 0, "coop_lanes": 1, "walk": 2, "coop_walk": 0,
                 "block_waves": 1, "heavy_first": 1, "heavy_tiles": -1, "heavy_stream": 2,
                 "learn_cost": 1, "heavy_factor": 130, "graph": 1, "concurrent_launches": 1, "heavy_cap": 75,
                 "heavy_pixels": 1, "heavy_pixel_factor": 75, "reuse_order": 1}
@@ -124,6 +124,8 @@ def test_config5_1m_row_subset(renderer):
     {"kernel": 1, "shade_min": 64},
     {"kernel": 1, "shade_min": 24, "blocks_per_cu": 1},
     {"kernel": 0, "wave_tile": 3},
+    {"kernel": 0, "wave_tile": 2, "coop_lanes": 2},
+    {"kernel": 0, "wave_tile": 1},
     {"kernel": 2, "seg_limit": 1},
     {"kernel": 2, "seg_limit": 2},
     {"kernel": 2, "seg_limit": 3, "shade_min": 1},
