@@ -70,11 +70,13 @@ if int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < 16:
 
 def default_inflight(world: int) -> int:
     """Frames in flight per rank (bands partition), measured best for config 3
-    (tools/share_inflight_bench.py on one MI355X, 16 queues): N = 1: 4
-    (0.359 vs 0.419 ms per frame at 1); N = 2, 4: 8; N = 8: 12 (0.053 ms per
-    1/8 share vs 0.259 at 1).  At most 12: with the main stream, the
-    collective's stream and the runtime's own, 16 queues stay one per stream."""
-    return 4 if world == 1 else (8 if world <= 4 else 12)
+    (tools/share_inflight_bench.py on one MI355X, 16 queues, the default
+    schedule; profiles/r02/inflight16/share4_q16.jsonl): N = 1: 4 (0.338 ms
+    per frame); N = 2: 8 (0.175 ms per half frame); N = 4, 8: 12 (0.092 /
+    0.050 ms per share vs 0.104 / 0.077 at 4).  At most 12: with the main
+    stream, the collective's and the runtime's own, 16 queues stay one per
+    stream."""
+    return 4 if world == 1 else (8 if world == 2 else 12)
 
 
 def file_sha16(path: str) -> str:
@@ -96,7 +98,7 @@ def main() -> None:
     ap.add_argument("--inflight", type=int, default=0,
                     help="frames in flight per rank (bands partition): each step's trace goes on the next of this "
                          "many streams, so frames overlap each other's serial tails and the gathers "
-                         "(0 = auto, default_inflight(): 4 at N = 1, 8 at N = 2-4, 12 at N > 4)")
+                         "(0 = auto, default_inflight(): 4 at N = 1, 8 at N = 2, 12 at N > 2)")
     ap.add_argument("--set", default="", help="schedule options name=value,... (rt_set_option) before timing")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-single", action="store_true", help="N > 1: skip rank 0's one-GPU timing")
