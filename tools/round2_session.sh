@@ -14,7 +14,7 @@ PMC_PASSES="A B C D E" bash tools/pmc.sh "${TAG}_pmc" || exit $?
 step() { local name=$1 secs=$2; shift 2; echo "$(date +%T) start $name" >> "$OUT/status.txt"
   timeout -k 10 "$secs" "$@"; local rc=$?; echo "$(date +%T) end $name rc=$rc" >> "$OUT/status.txt"; return $rc; }
 for c in 4 5 6; do
-  step cfg$c 300 python bench.py --config $c --steps 10 --warmup 3 > "$OUT/bench_cfg$c.json" 2> "$OUT/bench_cfg$c.err" || exit $?
+  step cfg$c 300 python bench.py --config $c --steps 50 --warmup 3 --no-cpu-baseline > "$OUT/bench_cfg$c.json" 2> "$OUT/bench_cfg$c.err" || exit $?
 done
 step pipeline 300 python tools/pipeline_bench.py > "$OUT/pipeline.jsonl" 2> "$OUT/pipeline.err" || exit $?
 step inflight 300 python tools/inflight_bench.py > "$OUT/inflight.jsonl" 2> "$OUT/inflight.err" || exit $?
