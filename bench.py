@@ -88,7 +88,9 @@ def file_sha16(path: str) -> str:
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
+    # 200 frames of config 3 are ~70 ms: with 4-12 frames in flight, 20 steps
+    # would spend a fifth of the timed region filling and draining the pipeline.
+    ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", type=int, default=3, help="BASELINE config index (3 = headline)")
     ap.add_argument("--band", type=int, default=16, help="band height for N > 1")
