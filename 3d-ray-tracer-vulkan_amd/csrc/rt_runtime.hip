@@ -319,7 +319,7 @@ struct rt_ctx {
     int  heavy_factor = 130;       // automatic heavy tiles: walk length above this percentage of the bulk estimate
     int  heavy_pixels = 1;         // heavy_stream 2 with automatic heavy tiles: split heavy PIXELS (1) or
                                    //   whole tiles (0) into one-pixel waves
-    int  heavy_pixel_factor = 75;  // heavy pixels: walk length above this percentage of the bulk estimate
+    int  heavy_pixel_factor = 50;  // heavy pixels: walk length above this percentage of the bulk estimate
     int  reuse_order = 1;          // heavy_first: a moving camera reuses the order learned at another camera
     int  heavy_cap = 75;           // automatic heavy tiles: at most this percentage of one generation of
                                    //   one-pixel waves (CUs x 24 / 64 tiles)

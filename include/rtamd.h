@@ -223,11 +223,11 @@ int rt_render_wait(rt_ctx* ctx, uint64_t ticket);
  *   "heavy_pixels"  with heavy_stream 2 and automatic heavy tiles: 1 (default)
  *                   = split heavy PIXELS, not whole tiles: the learning launch
  *                   also records every pixel's walk length; the pixels whose
- *                   walk exceeds "heavy_pixel_factor" percent (default 75) of
+ *                   walk exceeds "heavy_pixel_factor" percent (default 50) of
  *                   the bulk estimate are traced one per wave by the first
  *                   workgroups of the launch, and every tile wave skips its
  *                   heavy pixels; 0 = whole heavy tiles
- *   "heavy_pixel_factor" see heavy_pixels (1..100000, default 75)
+ *   "heavy_pixel_factor" see heavy_pixels (1..100000, default 50)
  *   "reuse_order"   heavy_first: 1 (default) = a camera that has just moved
  *                   (the launch key differs from the previous launch's only in
  *                   the camera) uses the newest order learned for the same

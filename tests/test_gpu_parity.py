@@ -18,7 +18,7 @@ DEFAULT_OPTS = {"kernel": 0, "shade_min": 16, "blocks_per_cu": 0, "wave_tile": 0
                 "heavy_budget": 256, "prio_after": 0, "coop_lanes": 1, "walk": 2, "coop_walk": 0,
                 "block_waves": 1, "heavy_first": 1, "heavy_tiles": -1, "heavy_stream": 2,
                 "learn_cost": 1, "heavy_factor": 130, "graph": 1, "concurrent_launches": 1, "heavy_cap": 75,
-                "heavy_pixels": 1, "heavy_pixel_factor": 75, "reuse_order": 1}
+                "heavy_pixels": 1, "heavy_pixel_factor": 50, "reuse_order": 1}
 
 
 def _oracle(built, cam_bytes, w, h, b, **kw):
