@@ -53,6 +53,14 @@ struct DevScene {
     float4*  nodes   = nullptr;
     float4*  leafs   = nullptr;
     float4*  pairs   = nullptr;
+    // walk 2's compact records: 2 x float4 per node index in nodes2 (an
+    // internal node's record as in nodes; a leaf's [1].w holds v0.x and its
+    // [0].w the triangle index | L(i+1) << 31, since a leaf's skip is always
+    // i+1) and 2 x float4 per node index in leafs2 (a leaf's v0.yz, e1, e2), so
+    // a leaf visit loads 4 float4 instead of 5 and the walk carries 8 leaf
+    // registers instead of 12
+    float4*  nodes2  = nullptr;
+    float4*  leafs2  = nullptr;
     float4*  norms   = nullptr;
     float4*  mats    = nullptr;
     // extension kExtSpheres: 2 x float4 per sphere (centre.xyz, radius),

@@ -345,6 +345,8 @@ struct rt_ctx {
 static void free_scene(PerDevice& p) {
     if (p.scene.nodes) (void)hipFree(p.scene.nodes);
     if (p.scene.leafs) (void)hipFree(p.scene.leafs);
+    if (p.scene.nodes2) (void)hipFree(p.scene.nodes2);
+    if (p.scene.leafs2) (void)hipFree(p.scene.leafs2);
     if (p.scene.pairs) (void)hipFree(p.scene.pairs);
     if (p.scene.norms) (void)hipFree(p.scene.norms);
     if (p.scene.mats) (void)hipFree(p.scene.mats);
@@ -653,7 +655,7 @@ static std::vector<uint64_t> launch_key(const TraceArgs& a, hipStream_t s) {
     auto F = [](float f) { uint32_t u; std::memcpy(&u, &f, 4); return (uint64_t)u; };
     const DevScene& sc = a.scene;
     const CamF& c = a.cam;
-    return {P(s), P(sc.nodes), P(sc.leafs), P(sc.pairs), P(sc.norms), P(sc.mats), P(sc.spheres),
+    return {P(s), P(sc.nodes), P(sc.leafs), P(sc.pairs), P(sc.nodes2), P(sc.leafs2), P(sc.norms), P(sc.mats), P(sc.spheres),
             (uint64_t)sc.n_spheres, (uint64_t)sc.n_nodes, (uint64_t)sc.end, (uint64_t)sc.n_tris,
             (uint64_t)sc.root_leaf, F(sc.root_box[0]), F(sc.root_box[1]), F(sc.root_box[2]), F(sc.root_box[3]),
             F(sc.root_box[4]), F(sc.root_box[5]),
@@ -841,6 +843,33 @@ int rt_upload_scene(rt_ctx* ctx, const void* vertices, size_t vertex_bytes,
     int rc = build_host_scene(vertices, vertex_bytes, materials, material_bytes,
                               bvh_nodes, bvh_bytes, &hs, &err);
     if (rc != RT_OK) { set_error("rt_upload_scene: %s", err); return rc; }
+    // walk 2's compact records (DevScene::nodes2 / leafs2), built from the
+    // compact scene: a leaf's skip is always i+1 (preorder), so its link word
+    // carries the triangle index instead, and its flags word v0.x
+    const size_t n2 = (size_t)hs.n_nodes;
+    std::vector<float4> nodes2(2 * n2 + 2, make_float4(0.f, 0.f, 0.f, 0.f)), leafs2(2 * n2 + 2, nodes2[0]);
+    for (size_t i = 0; i < n2; ++i) {
+        nodes2[2 * i] = hs.nodes[2 * i];
+        nodes2[2 * i + 1] = hs.nodes[2 * i + 1];
+        uint32_t fl;
+        std::memcpy(&fl, &hs.nodes[2 * i + 1].w, 4);
+        if (!(fl & 2u)) continue;                           // internal node
+        uint32_t link, tri;
+        std::memcpy(&link, &hs.nodes[2 * i].w, 4);
+        std::memcpy(&tri, &hs.leafs[3 * i].w, 4);
+        if ((link & 0x7FFFFFFFu) != i + 1 || (tri & 0x80000000u)) {
+            free_host_scene(&hs);
+            set_error("rt_upload_scene: leaf %zu: skip %u is not i+1 or triangle index %u too large", i,
+                      link & 0x7FFFFFFFu, tri);
+            return RT_ERR_BAD_SCENE;
+        }
+        const uint32_t w0 = tri | (link & 0x80000000u);
+        std::memcpy(&nodes2[2 * i].w, &w0, 4);
+        nodes2[2 * i + 1].w = hs.leafs[3 * i].x;                              // v0.x
+        const float4 P0 = hs.leafs[3 * i], P1 = hs.leafs[3 * i + 1], P2 = hs.leafs[3 * i + 2];
+        leafs2[2 * i] = make_float4(P0.y, P0.z, P1.x, P1.y);                   // v0.yz, e1.xy
+        leafs2[2 * i + 1] = make_float4(P1.z, P2.x, P2.y, P2.z);               // e1.z, e2
+    }
     ctx->has_scene = false;
     for (PerDevice& p : ctx->dev) {
         RT_HIP_CHECK(hipSetDevice(p.device));
@@ -864,6 +893,10 @@ int rt_upload_scene(rt_ctx* ctx, const void* vertices, size_t vertex_bytes,
         if (e == hipSuccess) e = hipMalloc(&s.pairs, pb);
         if (e == hipSuccess) e = hipMemset(s.nodes + 2 * nn, 0, 2 * sizeof(float4));
         if (e == hipSuccess) e = hipMemset(s.leafs + 3 * nn, 0, sizeof(float4));
+        if (e == hipSuccess) e = hipMalloc(&s.nodes2, nodes2.size() * sizeof(float4));
+        if (e == hipSuccess) e = hipMalloc(&s.leafs2, leafs2.size() * sizeof(float4));
+        if (e == hipSuccess) e = hipMemcpy(s.nodes2, nodes2.data(), nodes2.size() * sizeof(float4), hipMemcpyHostToDevice);
+        if (e == hipSuccess) e = hipMemcpy(s.leafs2, leafs2.data(), leafs2.size() * sizeof(float4), hipMemcpyHostToDevice);
         if (e == hipSuccess) e = hipMalloc(&s.norms, mb);
         if (e == hipSuccess) e = hipMalloc(&s.mats, mb);
         if (e == hipSuccess && hs.n_nodes) e = hipMemcpy(s.nodes, hs.nodes, nb - 2 * sizeof(float4), hipMemcpyHostToDevice);

@@ -813,14 +813,18 @@ void trace_simple(TraceArgs a) {
             // walk 2, software-pipelined: the next node's box is requested as soon as
             // this node's slab test has chosen it, before this node's triangle
             // test and the loop control, which then overlap the load.
-            float4 A, B, P0, P1, P2;
+            // walk 2 reads the compact records (DevScene::nodes2 / leafs2): a
+            // leaf's node record carries its triangle index and v0.x, and Q0, Q1
+            // the rest of its triangle.
+            float4 A, B, Q0, Q1;
+            const float4* __restrict__ nodes2 = a.scene.nodes2;
+            const float4* __restrict__ leafs2 = a.scene.leafs2;
             if (WALK == 2 && walking) {
-                A = nodes[2 * n];
-                B = nodes[2 * n + 1];
+                A = nodes2[2 * n];
+                B = nodes2[2 * n + 1];
                 if (nleaf) {
-                    P0 = leafs[3 * n + 0];
-                    P1 = leafs[3 * n + 1];
-                    P2 = leafs[3 * n + 2];
+                    Q0 = leafs2[2 * n + 0];
+                    Q1 = leafs2[2 * n + 1];
                 }
             }
             while (walking) {
@@ -837,23 +841,25 @@ void trace_simple(TraceArgs a) {
                     slab(A, B, o, inv, te, ind);
                     const bool hb = ind && te < closest;
                     const uint32_t aw = __float_as_uint(A.w), bw = __float_as_uint(B.w);
-                    const int nxt = hb ? n + 1 : (int)(aw & kIdx);            // a leaf's skip is n+1
-                    const bool nl = ((hb ? bw : (aw >> 31)) & 1u) != 0u;           // one select, no branch
+                    // a leaf's next node is n+1 whether it is hit or not (its skip)
+                    const int nxt = (hb || nleaf) ? n + 1 : (int)(aw & kIdx);
+                    const bool nl = (((hb && !nleaf) ? bw : (aw >> 31)) & 1u) != 0u;
+                    const float v0x = B.w;                                   // a leaf's v0.x
                     if (COUNT && hb && !nleaf) c_node += 2;
-                    A = nodes[2 * nxt];                                      // index end is padding
-                    B = nodes[2 * nxt + 1];
+                    A = nodes2[2 * nxt];                                     // index end is padding
+                    B = nodes2[2 * nxt + 1];
                     if (hb && nleaf) {                                       // hit_triangle (:196-200)
                         if (COUNT) ++c_tri;
                         float t;
-                        if (tri_test(P0, P1, P2, o, d, t) && t < closest) {
+                        if (tri_test(make_float4(v0x, Q0.x, Q0.y, 0.f), make_float4(Q0.z, Q0.w, Q1.x, 0.f),
+                                     make_float4(Q1.y, Q1.z, Q1.w, 0.f), o, d, t) && t < closest) {
                             closest = t;
-                            hit = __float_as_int(P0.w);
+                            hit = (int)(aw & kIdx);
                         }
                     }
                     if (nl && nxt < end) {
-                        P0 = leafs[3 * nxt + 0];
-                        P1 = leafs[3 * nxt + 1];
-                        P2 = leafs[3 * nxt + 2];
+                        Q0 = leafs2[2 * nxt + 0];
+                        Q1 = leafs2[2 * nxt + 1];
                     }
                     n = nxt;
                     nleaf = nl;
