@@ -20,7 +20,7 @@ sys.path[:0] = [os.path.join(ROOT, "3d-ray-tracer-vulkan_amd"), ROOT]
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", type=int, default=3)
-    ap.add_argument("--frames", type=int, default=60)
+    ap.add_argument("--frames", type=int, default=400)
     ap.add_argument("--slots", default="2,4,8", help="rt_render_async frames in flight (async_slots) to time")
     args = ap.parse_args()
     import numpy as np
