@@ -53,11 +53,12 @@ struct DevScene {
     float4*  nodes   = nullptr;
     float4*  leafs   = nullptr;
     float4*  pairs   = nullptr;
-    // walk 2's compact records: 2 x float4 per node index in nodes2 (an
-    // internal node's record as in nodes; a leaf's [1].w holds v0.x and its
-    // [0].w the triangle index | L(i+1) << 31, since a leaf's skip is always
-    // i+1) and 2 x float4 per node index in leafs2 (a leaf's v0.yz, e1, e2), so
-    // a leaf visit loads 4 float4 instead of 5 and the walk carries 8 leaf
+    // Compact records (walk 2 and the cooperative tail): 2 x float4 per node
+    // index in nodes2 (an internal node's record as in nodes; a leaf's [1].w
+    // holds v0.x and its [0].w the triangle index | 1 << 30 | L(i+1) << 31,
+    // since a leaf's skip is always i+1, so bit 30 of [0].w is L(i) for every
+    // node) and 2 x float4 per node index in leafs2 (a leaf's v0.yz, e1, e2): a
+    // leaf visit loads 4 float4 instead of 5 and the walk carries 8 leaf
     // registers instead of 12
     float4*  nodes2  = nullptr;
     float4*  leafs2  = nullptr;

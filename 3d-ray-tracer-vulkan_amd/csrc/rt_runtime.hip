@@ -853,17 +853,24 @@ int rt_upload_scene(rt_ctx* ctx, const void* vertices, size_t vertex_bytes,
         nodes2[2 * i + 1] = hs.nodes[2 * i + 1];
         uint32_t fl;
         std::memcpy(&fl, &hs.nodes[2 * i + 1].w, 4);
-        if (!(fl & 2u)) continue;                           // internal node
+        if (!(fl & 2u)) {                                   // internal node: skip < 2^30 keeps bit 30 clear
+            if (n2 >= (1u << 30)) {
+                free_host_scene(&hs);
+                set_error("rt_upload_scene: %zu nodes: at most 2^30 supported", n2);
+                return RT_ERR_BAD_SCENE;
+            }
+            continue;
+        }
         uint32_t link, tri;
         std::memcpy(&link, &hs.nodes[2 * i].w, 4);
         std::memcpy(&tri, &hs.leafs[3 * i].w, 4);
-        if ((link & 0x7FFFFFFFu) != i + 1 || (tri & 0x80000000u)) {
+        if ((link & 0x7FFFFFFFu) != i + 1 || tri >= (1u << 30)) {
             free_host_scene(&hs);
             set_error("rt_upload_scene: leaf %zu: skip %u is not i+1 or triangle index %u too large", i,
                       link & 0x7FFFFFFFu, tri);
             return RT_ERR_BAD_SCENE;
         }
-        const uint32_t w0 = tri | (link & 0x80000000u);
+        const uint32_t w0 = tri | (1u << 30) | (link & 0x80000000u);
         std::memcpy(&nodes2[2 * i].w, &w0, 4);
         nodes2[2 * i + 1].w = hs.leafs[3 * i].x;                              // v0.x
         const float4 P0 = hs.leafs[3 * i], P1 = hs.leafs[3 * i + 1], P2 = hs.leafs[3 * i + 2];

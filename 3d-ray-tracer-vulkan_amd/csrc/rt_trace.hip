@@ -345,8 +345,9 @@ __device__ __forceinline__ float lane_f(float v, int k) {
 // The whole wave walks ONE ray (arguments wave-uniform), replaying the
 // reference's visit sequence exactly:
 //   1. lane k loads node n+k of the window [n, n+64) and, in the same round
-//      trip, the leaf record indexed by that node (2 + 3 coalesced 16-B
-//      loads per lane); it runs the slab test and, for a leaf whose box is hit
+//      trip, the leaf record indexed by that node (the compact records
+//      nodes2 / leafs2: 2 + 2 coalesced 16-B loads per lane; bit 30 of the
+//      link word says leaf); it runs the slab test and, for a leaf whose box is hit
 //      at the current closest_t, the triangle test up to "t < closest_t";
 //   2. ballots make 64-bit masks: box hit at closest_t (H), triangle hit that
 //      improves closest_t (T), is a leaf (Lf);
@@ -357,7 +358,7 @@ __device__ __forceinline__ float lane_f(float v, int k) {
 // The float operations are node_step's, so closest_t, the hit and the visit /
 // triangle-test counts equal the per-lane walk's.
 template <bool COUNT>
-__device__ __forceinline__ int coop_walk(const float4* __restrict__ nodes, const float4* __restrict__ leafs,
+__device__ __forceinline__ int coop_walk(const float4* __restrict__ nodes2, const float4* __restrict__ leafs2,
                                          int end, int n, V3 o, V3 d, V3 inv, float& closest, int& hit,
                                          unsigned long long& c_node, unsigned long long& c_tri) {
     const int lane = threadIdx.x & 63;
@@ -369,16 +370,18 @@ __device__ __forceinline__ int coop_walk(const float4* __restrict__ nodes, const
         int sk = 0, tri = -1;
         bool ind = false, tv = false, lf = false;
         if (j < end) {
-            const float4 A = nodes[2 * j];
-            const float4 B = nodes[2 * j + 1];
-            const float4 P0 = leafs[3 * j + 0];
-            const float4 P1 = leafs[3 * j + 1];
-            const float4 P2 = leafs[3 * j + 2];
+            const float4 A = nodes2[2 * j];
+            const float4 B = nodes2[2 * j + 1];
+            const float4 Q0 = leafs2[2 * j + 0];
+            const float4 Q1 = leafs2[2 * j + 1];
             slab(A, B, o, inv, te, ind);
-            sk = (int)(__float_as_uint(A.w) & 0x7FFFFFFFu);
-            lf = (__float_as_uint(B.w) & 2u) != 0;
-            tri = __float_as_int(P0.w);
-            if (lf && ind && te < closest) tv = tri_test(P0, P1, P2, o, d, tt);
+            const uint32_t aw = __float_as_uint(A.w);
+            lf = ((aw >> 30) & 1u) != 0u;
+            sk = lf ? j + 1 : (int)(aw & 0x7FFFFFFFu);               // a leaf's skip is j+1
+            tri = (int)(aw & 0x3FFFFFFFu);
+            if (lf && ind && te < closest)
+                tv = tri_test(make_float4(B.w, Q0.x, Q0.y, 0.f), make_float4(Q0.z, Q0.w, Q1.x, 0.f),
+                              make_float4(Q1.y, Q1.z, Q1.w, 0.f), o, d, tt);
         }
         uint64_t H = __ballot(ind && te < closest);
         uint64_t T = __ballot(tv && tt < closest);
@@ -440,6 +443,7 @@ __device__ __forceinline__ int coop_walk(const float4* __restrict__ nodes, const
 // 4x the reference's 64-entry stack), the walk stops with pos = the
 // reference's next node, to be finished by node_step.
 constexpr uint32_t kIdx = 0x7FFFFFFFu;      // node index bits of a link word
+constexpr uint32_t kTri = 0x3FFFFFFFu;      // triangle index bits of a compact leaf record's link word
 constexpr int kFCap = 256;                   // frontier entries per wave (16 B each)
 constexpr int kFReserve = 80;                // slots speculation leaves to the front (> 64-deep descent)
 constexpr uint32_t kUnres = 0xFFFFFFFFu;
@@ -854,7 +858,7 @@ void trace_simple(TraceArgs a) {
                         if (tri_test(make_float4(v0x, Q0.x, Q0.y, 0.f), make_float4(Q0.z, Q0.w, Q1.x, 0.f),
                                      make_float4(Q1.y, Q1.z, Q1.w, 0.f), o, d, t) && t < closest) {
                             closest = t;
-                            hit = (int)(aw & kIdx);
+                            hit = (int)(aw & kTri);
                         }
                     }
                     if (nl && nxt < end) {
@@ -1041,7 +1045,7 @@ void trace_simple(TraceArgs a) {
                                               fr + wave * kFCap, nw))
                         while (p < end) p = node_step<COUNT>(nodes, leafs, p, pl, bo, bd, bi, bc, bh, cn, ct);
                 } else {
-                    nw = coop_walk<COUNT>(nodes, leafs, end, lane_i(start, L), bo, bd, bi, bc, bh, cn, ct);
+                    nw = coop_walk<COUNT>(a.scene.nodes2, a.scene.leafs2, end, lane_i(start, L), bo, bd, bi, bc, bh, cn, ct);
                 }
                 if (DIAG) {
                     d_windows += nw;
@@ -1303,7 +1307,7 @@ __global__ __launch_bounds__(256) void trace_coop(TraceArgs a) {
                                                 c_node, c_tri);
                 rounds += nr;
             } else {
-                rounds += coop_walk<COUNT>(a.scene.nodes, a.scene.leafs, end, node, o, d, inv, closest, hit, c_node,
+                rounds += coop_walk<COUNT>(a.scene.nodes2, a.scene.leafs2, end, node, o, d, inv, closest, hit, c_node,
                                            c_tri);
             }
             ++segs;
