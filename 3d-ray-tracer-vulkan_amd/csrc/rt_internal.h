@@ -44,6 +44,8 @@
 
 namespace rtamd {
 
+constexpr int kShadeStride = 2;
+
 struct DevScene {
     int      n_nodes = 0;     // nodes in the compact array
     int      end     = 0;     // traversal ends when the node index reaches this (= skip of root)
@@ -62,6 +64,9 @@ struct DevScene {
     // registers instead of 12
     float4*  nodes2  = nullptr;
     float4*  leafs2  = nullptr;
+    // norms and mats interleave in one allocation (kShadeStride float4 per
+    // triangle: normal, then albedo/type), so shading a hit touches one 32-B
+    // record; norms points at the allocation, mats one float4 in
     float4*  norms   = nullptr;
     float4*  mats    = nullptr;
     // extension kExtSpheres: 2 x float4 per sphere (centre.xyz, radius),

@@ -348,8 +348,7 @@ static void free_scene(PerDevice& p) {
     if (p.scene.nodes2) (void)hipFree(p.scene.nodes2);
     if (p.scene.leafs2) (void)hipFree(p.scene.leafs2);
     if (p.scene.pairs) (void)hipFree(p.scene.pairs);
-    if (p.scene.norms) (void)hipFree(p.scene.norms);
-    if (p.scene.mats) (void)hipFree(p.scene.mats);
+    if (p.scene.norms) (void)hipFree(p.scene.norms);   // mats lives in the same allocation
     p.scene = DevScene{};
 }
 
@@ -904,13 +903,17 @@ int rt_upload_scene(rt_ctx* ctx, const void* vertices, size_t vertex_bytes,
         if (e == hipSuccess) e = hipMalloc(&s.leafs2, leafs2.size() * sizeof(float4));
         if (e == hipSuccess) e = hipMemcpy(s.nodes2, nodes2.data(), nodes2.size() * sizeof(float4), hipMemcpyHostToDevice);
         if (e == hipSuccess) e = hipMemcpy(s.leafs2, leafs2.data(), leafs2.size() * sizeof(float4), hipMemcpyHostToDevice);
-        if (e == hipSuccess) e = hipMalloc(&s.norms, mb);
-        if (e == hipSuccess) e = hipMalloc(&s.mats, mb);
+        if (e == hipSuccess) e = hipMalloc(&s.norms, kShadeStride * mb);
+        if (e == hipSuccess) s.mats = s.norms + 1;
         if (e == hipSuccess && hs.n_nodes) e = hipMemcpy(s.nodes, hs.nodes, nb - 2 * sizeof(float4), hipMemcpyHostToDevice);
         if (e == hipSuccess && hs.n_nodes) e = hipMemcpy(s.leafs, hs.leafs, lb - sizeof(float4), hipMemcpyHostToDevice);
         if (e == hipSuccess && hs.n_nodes) e = hipMemcpy(s.pairs, hs.pairs, pb, hipMemcpyHostToDevice);
-        if (e == hipSuccess && hs.n_tris) e = hipMemcpy(s.norms, hs.norms, mb, hipMemcpyHostToDevice);
-        if (e == hipSuccess && hs.n_tris) e = hipMemcpy(s.mats, hs.mats, mb, hipMemcpyHostToDevice);
+        if (e == hipSuccess && hs.n_tris)
+            e = hipMemcpy2D(s.norms, kShadeStride * sizeof(float4), hs.norms, sizeof(float4), sizeof(float4),
+                            (size_t)hs.n_tris, hipMemcpyHostToDevice);
+        if (e == hipSuccess && hs.n_tris)
+            e = hipMemcpy2D(s.mats, kShadeStride * sizeof(float4), hs.mats, sizeof(float4), sizeof(float4),
+                            (size_t)hs.n_tris, hipMemcpyHostToDevice);
         p.scene = s;
         if (e != hipSuccess) {
             set_error("rt_upload_scene: device %d: %s", p.device, hipGetErrorString(e));

@@ -201,7 +201,7 @@ __device__ __forceinline__ int node_step(const float4* __restrict__ nodes, const
 // The hit normal of :124-125: normalize(cross(e1,e2)) (precomputed per
 // triangle, rt_internal.h), flipped to face against d.
 __device__ __forceinline__ V3 hit_normal(const float4* __restrict__ norms, int hit, V3 d) {
-    const float4 N = norms[hit];
+    const float4 N = norms[kShadeStride * hit];
     V3 n = {N.x, N.y, N.z};
     if (vdot(d, n) > 0.0f) n = {-n.x, -n.y, -n.z};
     return n;
@@ -657,7 +657,7 @@ __device__ __forceinline__ void heavy_pixel(const TraceArgs& a, int lx, int ly, 
             if (COUNT) ++c_mat;
             const V3 hp = vadd(o, vscale(d, closest));                        // ray_at :77-79
             const V3 nrm = hit_normal(a.scene.norms, hit, d);
-            const float4 M = a.scene.mats[hit];
+            const float4 M = a.scene.mats[kShadeStride * hit];
             V3 nd;
             if (!scatter(M, d, nrm, seed, nd)) break;                        // attenuation = 0: black
             att = vmul(att, V3{M.x, M.y, M.z});
@@ -1078,7 +1078,7 @@ void trace_simple(TraceArgs a) {
                     M = a.scene.spheres[2 * (-2 - hit) + 1];
                 } else {
                     nrm = hit_normal(a.scene.norms, hit, d);
-                    M = a.scene.mats[hit];
+                    M = a.scene.mats[kShadeStride * hit];
                 }
                 V3 nd;
                 if ((FEAT & kFeatExt) && (a.ext & kExtEmissive) && M.w == 3.0f) {
@@ -1228,7 +1228,7 @@ __global__ __launch_bounds__(256) void trace_persistent(TraceArgs a) {
                 if (COUNT) ++c_mat;
                 const V3 n = hit_normal(a.scene.norms, hit, d);
                 const V3 hp = vadd(o, vscale(d, closest));
-                const float4 M = a.scene.mats[hit];
+                const float4 M = a.scene.mats[kShadeStride * hit];
                 V3 nd;
                 if (scatter(M, d, n, seed, nd) && b < a.max_bounces - 1) {
                     att = vmul(att, V3{M.x, M.y, M.z});
@@ -1323,7 +1323,7 @@ __global__ __launch_bounds__(256) void trace_coop(TraceArgs a) {
             if (COUNT) ++c_mat;
             const V3 n = hit_normal(a.scene.norms, hit, d);
             const V3 hp = vadd(o, vscale(d, closest));
-            const float4 M = a.scene.mats[hit];
+            const float4 M = a.scene.mats[kShadeStride * hit];
             V3 nd;
             if (!scatter(M, d, n, seed, nd) || b == a.max_bounces - 1) break;   // black
             att = vmul(att, V3{M.x, M.y, M.z});
