@@ -675,15 +675,16 @@ __device__ __forceinline__ void heavy_pixel(const TraceArgs& a, int lx, int ly, 
 constexpr int kPair = 0, kLeaf = 1, kNode = 2, kSkip = 3;   // walk 1: record kinds
 
 // Occupancy floor for trace_simple (waves per SIMD).  Unconstrained, the
-// walk-2 build takes 73 VGPRs (6 waves); at 7 it fits 72 with no spills in the
-// plain variant (12 B per lane in the fused heavy-pixel one).  One frame at a
-// time the two ran even (round 1); with frames in flight the device is
-// throughput-bound and the 7th wave per SIMD pays: config 3 0.328-0.330 vs
-// 0.344-0.346 ms, config 6 0.381-0.390 vs 0.394 (profiles/r02/occupancy/wpe7).
-// 8 spills per segment and loses.  The frontier (heavy-tile) instantiations
-// keep their registers.
+// walk-2 build takes ~70 VGPRs (7 waves).  One frame at a time more waves did
+// not pay (round 1); with frames in flight the device is throughput-bound and
+// they do: at 7 (round 2, before the compact records) config 3 0.328-0.330 vs
+// 0.344-0.346 ms (profiles/r02/occupancy/wpe7); with the compact records, 8
+// waves (64 VGPRs, ~20 B per lane of per-segment spills) beat 7 on config 3
+// (0.298-0.299 vs 0.301-0.302 ms) and config 6 (0.343-0.344 vs 0.364-0.365),
+// config 5 even (profiles/r02/occupancy/wpe8).  The frontier (heavy-tile)
+// instantiations keep their registers.
 #ifndef RT_SIMPLE_WPE
-#define RT_SIMPLE_WPE 7
+#define RT_SIMPLE_WPE 8
 #endif
 template <bool COUNT, bool DIAG = false, int FEAT = 0, int WALK = 1>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((FEAT & kFeatFrontier) ? 1 : RT_SIMPLE_WPE)))
