@@ -45,6 +45,12 @@
 namespace rtamd {
 
 constexpr int kShadeStride = 2;
+#ifndef RT_TOP_BITS
+#define RT_TOP_BITS 10
+#endif
+constexpr int kTopBits = RT_TOP_BITS;            // walk 13: slot+1 field width (10: 32 KB of LDS, 11: 64 KB)
+constexpr int kTopSlots = (1 << kTopBits) - 1;   // top-tree slots
+constexpr int kWalkTop = 13;      // option walk: walk 2 with the top tree's records in LDS
 
 struct DevScene {
     int      n_nodes = 0;     // nodes in the compact array
@@ -64,6 +70,18 @@ struct DevScene {
     // registers instead of 12
     float4*  nodes2  = nullptr;
     float4*  leafs2  = nullptr;
+    // Top tree (walk 13): the internal nodes of the deepest prefix of levels
+    // that fits kTopSlots, in preorder, get slots 0..n_top-1; their records (top, 2 x float4 per
+    // slot) are copied into each workgroup's LDS at launch.  nodes3 is nodes2
+    // with the slot of each possible next node in free bits, so a walker
+    // knows from the record it holds whether its next node is in LDS:
+    //   internal [1].w |= (slot(skip)+1) << 2 | (slot(i+1)+1) << (2 + kTopBits)
+    //   leaf     [0].w  = triangle (20 bits) | (slot(i+1)+1) << 20 | L(i+1) << 31
+    // (slot+1 = 0: not in the top tree).  Null when the scene has more than
+    // 2^20 triangles (walk 13 then runs as walk 2).
+    float4*  nodes3  = nullptr;
+    float4*  top     = nullptr;
+    int      n_top   = 0;
     // norms and mats interleave in one allocation (kShadeStride float4 per
     // triangle: normal, then albedo/type), so shading a hit touches one 32-B
     // record; norms points at the allocation, mats one float4 in

@@ -347,6 +347,8 @@ static void free_scene(PerDevice& p) {
     if (p.scene.leafs) (void)hipFree(p.scene.leafs);
     if (p.scene.nodes2) (void)hipFree(p.scene.nodes2);
     if (p.scene.leafs2) (void)hipFree(p.scene.leafs2);
+    if (p.scene.nodes3) (void)hipFree(p.scene.nodes3);
+    if (p.scene.top) (void)hipFree(p.scene.top);
     if (p.scene.pairs) (void)hipFree(p.scene.pairs);
     if (p.scene.norms) (void)hipFree(p.scene.norms);   // mats lives in the same allocation
     p.scene = DevScene{};
@@ -381,9 +383,12 @@ static int plan_order(const rt_ctx* ctx, PerDevice& p, TraceArgs& a, const rt_ca
     a.ev_fork = a.ev_join = nullptr;
     p.last_heavy = 0;
     p.last_heavy_px = 0;
-    if (!ctx->heavy_first || a.kernel != kKernelSimple || a.block_waves != 1) return RT_OK;
-    const int tw_w = 8 << a.wave_tile, th_w = 8 >> a.wave_tile;
-    const size_t n = (size_t)((a.tw + tw_w - 1) / tw_w) * (size_t)((a.th + th_w - 1) / th_w);
+    // walk 13 orders the wave tiles of its multi-wave workgroups (a workgroup
+    // takes block_waves consecutive tiles of the order)
+    const bool top_walk = a.walk == kWalkTop && a.scene.nodes3;
+    if (!ctx->heavy_first || a.kernel != kKernelSimple || (a.block_waves != 1 && !top_walk)) return RT_OK;
+    const int tw_w = 8 << a.wave_tile, th_w = 8 >> a.wave_tile, bw = a.block_waves;
+    const size_t n = (size_t)((a.tw + bw * tw_w - 1) / (bw * tw_w)) * bw * (size_t)((a.th + th_w - 1) / th_w);
     const int geo[] = {a.width, a.height, a.max_bounces, a.x0, a.y0, a.tw, a.th, a.band_h, a.band_stride,
                        a.band_off, a.wave_tile, a.ext, a.coop_lanes, a.walk, ctx->learn_cost, ctx->heavy_factor,
                        concurrency(ctx), ctx->heavy_cap, ctx->heavy_pixel_factor};
@@ -563,6 +568,12 @@ static int set_schedule(const rt_ctx* ctx, PerDevice& p, TraceArgs& a, const rt_
     a.walk = ctx->walk;
     a.coop_walk = ctx->coop_walk;
     a.block_waves = ctx->block_waves;
+    // walk 13 needs its top tree (none past 2^20 triangles: walk 2 then) and
+    // runs 8- or 16-wave workgroups (its LDS copy is per workgroup); the
+    // other walks' kernels are built for at most 4 waves per workgroup.
+    if (a.walk == kWalkTop && (!p.scene.nodes3 || a.kernel != kKernelSimple || ctx->coop_walk)) a.walk = 2;
+    if (a.walk == kWalkTop && a.block_waves < 8) a.block_waves = 16;
+    if (a.walk != kWalkTop && a.block_waves > 4) a.block_waves = 1;
     a.sink = p.d_counters + 1;
     a.seg_limit = a.kernel == kKernelSplit ? ctx->seg_limit : (1 << 30);
     a.ext = ctx->ext;
@@ -599,7 +610,8 @@ static int set_schedule(const rt_ctx* ctx, PerDevice& p, TraceArgs& a, const rt_
     if (ctx->diag && (a.kernel == kKernelSimple || a.kernel == kKernelTiered)) {
         // simple: 8 words per wave; tiered adds 4 words per suspended path (trace_coop)
         const int tw_w = 8 << a.wave_tile, th_w = 8 >> a.wave_tile;
-        const size_t waves = (size_t)((a.tw + 4 * tw_w - 1) / (4 * tw_w)) * ((a.th + th_w - 1) / th_w) * 4;
+        const int gw = std::max(4, a.block_waves);   // columns are rounded up to whole workgroups
+        const size_t waves = (size_t)((a.tw + gw * tw_w - 1) / (gw * tw_w)) * ((a.th + th_w - 1) / th_w) * gw;
         const size_t split = ctx->heavy_first ? (size_t)(ctx->heavy_tiles < 0 ? kMaxHeavy : ctx->heavy_tiles) * 63 : 0;
         const size_t words = (waves + split) * 8 + (a.kernel == kKernelTiered ? (size_t)a.tw * a.th * 4 : 0);
         if (words > p.diag_cap) {
@@ -739,7 +751,10 @@ int rt_create(const int* device_ids, int n_devices, rt_ctx** out) {
                     : std::strcmp(k, "persistent") == 0 ? kKernelPersistent
                     : std::strcmp(k, "split") == 0 ? kKernelSplit
                     : std::strcmp(k, "tiered") == 0 ? kKernelTiered : ctx->kernel;
-    if (const char* v = std::getenv("RTAMD_WALK")) ctx->walk = std::max(0, std::min(2, std::atoi(v)));
+    if (const char* v = std::getenv("RTAMD_WALK")) {
+        const int w = std::atoi(v);
+        ctx->walk = w == kWalkTop ? w : std::max(0, std::min(2, w));
+    }
     if (const char* v = std::getenv("RTAMD_COOP_WALK")) ctx->coop_walk = std::atoi(v) ? 1 : 0;
     if (const char* v = std::getenv("RTAMD_HEAVY_FIRST")) ctx->heavy_first = std::atoi(v) ? 1 : 0;
     if (const char* v = std::getenv("RTAMD_HEAVY_TILES")) ctx->heavy_tiles = std::max(-1, std::atoi(v));
@@ -748,7 +763,10 @@ int rt_create(const int* device_ids, int n_devices, rt_ctx** out) {
     if (const char* v = std::getenv("RTAMD_HEAVY_STREAM")) ctx->heavy_stream = std::max(0, std::min(2, std::atoi(v)));
     if (const char* v = std::getenv("RTAMD_HEAVY_PIXELS")) ctx->heavy_pixels = std::atoi(v) ? 1 : 0;
     if (const char* v = std::getenv("RTAMD_GRAPH")) ctx->graph = std::atoi(v) ? 1 : 0;
-    if (const char* v = std::getenv("RTAMD_BLOCK_WAVES")) ctx->block_waves = std::atoi(v) == 1 ? 1 : 4;
+    if (const char* v = std::getenv("RTAMD_BLOCK_WAVES")) {
+        const int bw = std::atoi(v);
+        ctx->block_waves = (bw == 1 || bw == 8 || bw == 16) ? bw : 4;
+    }
     if (const char* v = std::getenv("RTAMD_COOP_LANES")) ctx->coop_lanes = std::max(0, std::min(64, std::atoi(v)));
     if (const char* v = std::getenv("RTAMD_SEG_LIMIT")) ctx->seg_limit = std::max(1, std::min(1024, std::atoi(v)));
     if (const char* v = std::getenv("RTAMD_SHADE_MIN")) ctx->shade_min = std::max(1, std::min(64, std::atoi(v)));
@@ -876,6 +894,48 @@ int rt_upload_scene(rt_ctx* ctx, const void* vertices, size_t vertex_bytes,
         leafs2[2 * i] = make_float4(P0.y, P0.z, P1.x, P1.y);                   // v0.yz, e1.xy
         leafs2[2 * i + 1] = make_float4(P1.z, P2.x, P2.y, P2.z);               // e1.z, e2
     }
+    // walk 13's top tree (DevScene::nodes3 / top): the internal nodes of the
+    // deepest prefix of levels that fits kTopSlots, slots in preorder.
+    std::vector<float4> nodes3, top;
+    if (n2 > 0 && (size_t)hs.n_tris <= (1u << 20)) {
+        std::vector<int> depth(n2, 0), slot(n2 + 1, -1), per_level;
+        auto word = [&](size_t i, int k) { uint32_t w; std::memcpy(&w, k ? &hs.nodes[2 * i + 1].w : &hs.nodes[2 * i].w, 4); return w; };
+        auto is_leaf = [&](size_t i) { return (word(i, 1) & 2u) != 0u; };
+        for (size_t i = 0; i < n2; ++i) {
+            if ((size_t)depth[i] >= per_level.size()) per_level.resize(depth[i] + 1, 0);
+            if (is_leaf(i)) continue;
+            ++per_level[depth[i]];
+            const size_t r = word(i + 1, 0) & 0x7FFFFFFFu;      // right child = skip(left child)
+            depth[i + 1] = depth[i] + 1;
+            if (r < n2) depth[r] = depth[i] + 1;
+        }
+        int levels = 0, count = 0;
+        while (levels < (int)per_level.size() && count + per_level[levels] <= kTopSlots) count += per_level[levels++];
+        int n_top = 0;
+        for (size_t i = 0; i < n2; ++i)
+            if (!is_leaf(i) && depth[i] < levels) slot[i] = n_top++;
+        nodes3 = nodes2;
+        for (size_t i = 0; i < n2; ++i) {
+            uint32_t w;
+            if (is_leaf(i)) {
+                std::memcpy(&w, &nodes2[2 * i].w, 4);
+                w = (w & 0x800FFFFFu) | ((uint32_t)(slot[i + 1] + 1) << 20);
+                std::memcpy(&nodes3[2 * i].w, &w, 4);
+            } else {
+                const size_t sk = word(i, 0) & 0x7FFFFFFFu;
+                std::memcpy(&w, &nodes2[2 * i + 1].w, 4);
+                w |= (uint32_t)(slot[sk <= n2 ? sk : n2] + 1) << 2 | (uint32_t)(slot[i + 1] + 1) << (2 + kTopBits);
+                std::memcpy(&nodes3[2 * i + 1].w, &w, 4);
+            }
+        }
+        top.resize(2 * (size_t)std::max(1, n_top), make_float4(0.f, 0.f, 0.f, 0.f));
+        for (size_t i = 0; i < n2; ++i)
+            if (slot[i] >= 0) {
+                top[2 * slot[i]] = nodes3[2 * i];
+                top[2 * slot[i] + 1] = nodes3[2 * i + 1];
+            }
+        top.resize(2 * (size_t)n_top);
+    }
     ctx->has_scene = false;
     for (PerDevice& p : ctx->dev) {
         RT_HIP_CHECK(hipSetDevice(p.device));
@@ -903,6 +963,15 @@ int rt_upload_scene(rt_ctx* ctx, const void* vertices, size_t vertex_bytes,
         if (e == hipSuccess) e = hipMalloc(&s.leafs2, leafs2.size() * sizeof(float4));
         if (e == hipSuccess) e = hipMemcpy(s.nodes2, nodes2.data(), nodes2.size() * sizeof(float4), hipMemcpyHostToDevice);
         if (e == hipSuccess) e = hipMemcpy(s.leafs2, leafs2.data(), leafs2.size() * sizeof(float4), hipMemcpyHostToDevice);
+        if (e == hipSuccess && !nodes3.empty()) {
+            e = hipMalloc(&s.nodes3, nodes3.size() * sizeof(float4));
+            if (e == hipSuccess) e = hipMalloc(&s.top, std::max<size_t>(1, top.size()) * sizeof(float4));
+            if (e == hipSuccess)
+                e = hipMemcpy(s.nodes3, nodes3.data(), nodes3.size() * sizeof(float4), hipMemcpyHostToDevice);
+            if (e == hipSuccess && !top.empty())
+                e = hipMemcpy(s.top, top.data(), top.size() * sizeof(float4), hipMemcpyHostToDevice);
+            s.n_top = (int)(top.size() / 2);
+        }
         if (e == hipSuccess) e = hipMalloc(&s.norms, kShadeStride * mb);
         if (e == hipSuccess) s.mats = s.norms + 1;
         if (e == hipSuccess && hs.n_nodes) e = hipMemcpy(s.nodes, hs.nodes, nb - 2 * sizeof(float4), hipMemcpyHostToDevice);
@@ -1307,11 +1376,11 @@ int rt_set_option(rt_ctx* ctx, const char* name, int64_t value) {
         ctx->coop_lanes = (int)value;
     } else if (std::strcmp(name, "extensions") == 0 && value >= 0 && value <= 15) {
         ctx->ext = (int)value;
-    } else if (std::strcmp(name, "walk") == 0 && value >= 0 && value <= 2) {
+    } else if (std::strcmp(name, "walk") == 0 && ((value >= 0 && value <= 2) || value == kWalkTop)) {
         ctx->walk = (int)value;
     } else if (std::strcmp(name, "coop_walk") == 0 && (value == 0 || value == 1)) {
         ctx->coop_walk = (int)value;
-    } else if (std::strcmp(name, "block_waves") == 0 && (value == 1 || value == 4)) {
+    } else if (std::strcmp(name, "block_waves") == 0 && (value == 1 || value == 4 || value == 8 || value == 16)) {
         ctx->block_waves = (int)value;
     } else if (std::strcmp(name, "heavy_first") == 0 && (value == 0 || value == 1)) {
         ctx->heavy_first = (int)value;

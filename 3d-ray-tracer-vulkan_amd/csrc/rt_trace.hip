@@ -687,10 +687,20 @@ constexpr int kPair = 0, kLeaf = 1, kNode = 2, kSkip = 3;   // walk 1: record ki
 #define RT_SIMPLE_WPE 8
 #endif
 template <bool COUNT, bool DIAG = false, int FEAT = 0, int WALK = 1>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((FEAT & kFeatFrontier) ? 1 : RT_SIMPLE_WPE)))
+__global__ __launch_bounds__(WALK == kWalkTop ? 1024 : 256)
+__attribute__((amdgpu_waves_per_eu((FEAT & kFeatFrontier) ? 1 : RT_SIMPLE_WPE)))
 void trace_simple(TraceArgs a) {
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
+    // walk 13: the top tree's records (DevScene::top), one copy per workgroup
+    // of block_waves (8 or 16) waves, read by every walking lane whose next
+    // node is in it instead of a global load
+    __shared__ float4 topl[WALK == kWalkTop ? 2 * kTopSlots : 1];
+    if (WALK == kWalkTop) {
+        const int nt2 = 2 * a.scene.n_top;
+        for (int i = threadIdx.x; i < nt2; i += blockDim.x) topl[i] = a.scene.top[i];
+        __syncthreads();
+    }
     unsigned long long* drec = nullptr;
     if (DIAG) {
         drec = a.diag + kDiagWords * (size_t)((blockIdx.y * gridDim.x + blockIdx.x) * a.block_waves + wave);
@@ -717,7 +727,8 @@ void trace_simple(TraceArgs a) {
     int bx = blockIdx.x, by = blockIdx.y, sub = -1;
     unsigned long long skip_lanes = 0;                   // heavy pixels this tile wave leaves out
     if (a.tile_order) {                                  // 1-D grid over the ordered tiles
-        const int k = blockIdx.x;
+        // walk 13: a workgroup's waves take consecutive tiles of the order
+        const int k = WALK == kWalkTop ? blockIdx.x * a.block_waves + wave : blockIdx.x;
         int t;
         if ((FEAT & kFeatFused) && k < a.n_heavy_px) {   // a heavy pixel (tile * 64 + lane), dispatched first
             const int q = a.heavy_px[k];
@@ -747,7 +758,8 @@ void trace_simple(TraceArgs a) {
         }
     }
     const int tl = sub >= 0 ? sub : lane;                // the tile pixel this lane traces
-    const int lx = (bx * a.block_waves + wave) * tw_w + (tl & (tw_w - 1));
+    const int col = (WALK == kWalkTop && a.tile_order) ? bx : bx * a.block_waves + wave;   // wave-tile column
+    const int lx = col * tw_w + (tl & (tw_w - 1));
     const int ly = by * th_w + (tl >> (3 + s));
     const bool pixel = lx < a.tw && ly < a.th && (sub < 0 || lane == 0) && !((skip_lanes >> lane) & 1ull);
     const int coop_lanes = sub >= 0 ? 64 : a.coop_lanes;
@@ -813,7 +825,7 @@ void trace_simple(TraceArgs a) {
             ++c_seg;
             if (end > 0) ++c_node;                                       // the root visit
         }
-        if (WALK == 0 || WALK == 2) {
+        if (WALK == 0 || WALK == 2 || WALK == kWalkTop) {
             // The per-node walk: one dependent load per visit, lanes in lockstep.
             // walk 2, software-pipelined: the next node's box is requested as soon as
             // this node's slab test has chosen it, before this node's triangle
@@ -821,12 +833,21 @@ void trace_simple(TraceArgs a) {
             // walk 2 reads the compact records (DevScene::nodes2 / leafs2): a
             // leaf's node record carries its triangle index and v0.x, and Q0, Q1
             // the rest of its triangle.
+            // walk 13 reads nodes3 (nodes2 + the top-tree slots of the next
+            // nodes) and, for a next node in the top tree, its LDS copy.
             float4 A, B, Q0, Q1;
-            const float4* __restrict__ nodes2 = a.scene.nodes2;
+            const float4* __restrict__ nodes2 = WALK == kWalkTop ? a.scene.nodes3 : a.scene.nodes2;
             const float4* __restrict__ leafs2 = a.scene.leafs2;
-            if (WALK == 2 && walking) {
-                A = nodes2[2 * n];
-                B = nodes2[2 * n + 1];
+            if ((WALK == 2 || WALK == kWalkTop) && walking) {
+                if (WALK == kWalkTop && !nleaf && a.scene.n_top > 0) {   // an internal root is slot 0
+                    A = topl[0];
+                    B = topl[1];
+                    pin(A);
+                    pin(B);
+                } else {
+                    A = nodes2[2 * n];
+                    B = nodes2[2 * n + 1];
+                }
                 if (nleaf) {
                     Q0 = leafs2[2 * n + 0];
                     Q1 = leafs2[2 * n + 1];
@@ -851,15 +872,33 @@ void trace_simple(TraceArgs a) {
                     const bool nl = (((hb && !nleaf) ? bw : (aw >> 31)) & 1u) != 0u;
                     const float v0x = B.w;                                   // a leaf's v0.x
                     if (COUNT && hb && !nleaf) c_node += 2;
-                    A = nodes2[2 * nxt];                                     // index end is padding
-                    B = nodes2[2 * nxt + 1];
+                    if (WALK == kWalkTop) {
+                        // the next node's top-tree slot (-1: not in it): a leaf's
+                        // next is i+1; an internal node's i+1 on a hit, skip on a miss
+                        const int ts = (int)((nleaf ? (aw >> 20) : (bw >> (hb ? 2 + kTopBits : 2))) &
+                                             (uint32_t)kTopSlots) - 1;
+                        if (ts >= 0) {
+                            // the pins keep the compiler from merging this and
+                            // the global load into one flat (TA-path) load
+                            A = topl[2 * ts];
+                            B = topl[2 * ts + 1];
+                            pin(A);
+                            pin(B);
+                        } else {
+                            A = nodes2[2 * nxt];
+                            B = nodes2[2 * nxt + 1];
+                        }
+                    } else {
+                        A = nodes2[2 * nxt];                                 // index end is padding
+                        B = nodes2[2 * nxt + 1];
+                    }
                     if (hb && nleaf) {                                       // hit_triangle (:196-200)
                         if (COUNT) ++c_tri;
                         float t;
                         if (tri_test(make_float4(v0x, Q0.x, Q0.y, 0.f), make_float4(Q0.z, Q0.w, Q1.x, 0.f),
                                      make_float4(Q1.y, Q1.z, Q1.w, 0.f), o, d, t) && t < closest) {
                             closest = t;
-                            hit = (int)(aw & kTri);
+                            hit = (int)(aw & (WALK == kWalkTop ? 0xFFFFFu : kTri));
                         }
                     }
                     if (nl && nxt < end) {
@@ -1458,7 +1497,11 @@ hipError_t launch_trace(const TraceArgs& a, hipStream_t stream) {
                          (a.coop_lanes > 0 && a.coop_walk ? kFeatFrontier : 0);
         TraceArgs ao = a;
         bool join = false;
-        if (a.tile_order) {             // heavy-first: a 1-D grid over the ordered tiles
+        if (a.tile_order && a.walk == kWalkTop) {   // heavy-first, walk 13: bw consecutive tiles per workgroup
+            ao.tiles_x = (int)grid.x * bw;
+            ao.split_n = 0;
+            grid = dim3(grid.x * grid.y);
+        } else if (a.tile_order) {      // heavy-first: a 1-D grid over the ordered tiles
             ao.tiles_x = (int)grid.x;
             ao.split_n = 0;
             const int n_tiles = (int)(grid.x * grid.y);
@@ -1531,7 +1574,14 @@ hipError_t launch_trace(const TraceArgs& a, hipStream_t stream) {
         if (a.diag) hipLaunchKernelGGL((trace_simple<false, true, F, W>), grid, block, ((F) & kFeatFrontier) ? shm_f : lds_pad, stream, ao);           \
         else if (a.counters) hipLaunchKernelGGL((trace_simple<true, false, F, W>), grid, block, ((F) & kFeatFrontier) ? shm_f : lds_pad, stream, ao); \
         else hipLaunchKernelGGL((trace_simple<false, false, F, W>), grid, block, ((F) & kFeatFrontier) ? shm_f : lds_pad, stream, ao);
-        if (a.walk == 2) {
+        if (a.walk == kWalkTop) {
+            switch (feat) {
+                case kFeatCoopTail: RT_SIMPLE(kFeatCoopTail, kWalkTop) break;
+                case 0: RT_SIMPLE(0, kWalkTop) break;
+                case kFeatCoopTail | kFeatExt: RT_SIMPLE(kFeatCoopTail | kFeatExt, kWalkTop) break;
+                default: return hipErrorInvalidValue;
+            }
+        } else if (a.walk == 2) {
             switch (feat) {
                 case kFeatCoopTail: RT_SIMPLE(kFeatCoopTail, 2) break;
                 case 0: RT_SIMPLE(0, 2) break;

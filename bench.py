@@ -101,6 +101,9 @@ def main() -> None:
                     help="frames in flight per rank (bands partition): each step's trace goes on the next of this "
                          "many streams, so frames overlap each other's serial tails and the gathers "
                          "(0 = auto, default_inflight(): 4 at N = 1, 8 at N = 2, 12 at N > 2)")
+    ap.add_argument("--drain", type=int, default=1,
+                    help="1: the last frames of a run of steps plan their heavy pixels for the frames still in "
+                         "flight beside them (concurrent_launches min(D, frames left)); 0: every frame for D")
     ap.add_argument("--set", default="", help="schedule options name=value,... (rt_set_option) before timing")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-single", action="store_true", help="N > 1: skip rank 0's one-GPU timing")
@@ -278,9 +281,25 @@ def main() -> None:
         f"{node_visits / segments:.2f} node visits/seg, {tri_tests / segments:.3f} tri tests/seg; "
         f"{D} frame(s) in flight, exchange every {G} step(s)")
 
+    # Drain (option --drain, default on): a launch's heavy-pixel bar counts
+    # the launches that will run beside it, and at the end of a run of frames
+    # fewer do: step j of n has min(D, n - j) frames in flight from its launch
+    # on, so the last frames split their slowest pixels into one-pixel waves
+    # as a lone frame does, instead of leaving the run's end to one frame's
+    # serial tail.  Pixels and results do not change.
+    conc_now = [F * D]
+
+    def set_conc(c):
+        if c != conc_now[0]:
+            renderer.set_option("concurrent_launches", c)
+            conc_now[0] = c
+
     def phase(n, evs=None):
         for j in range(n):
+            if args.drain:
+                set_conc(F * min(D, n - j))
             step(evs[j] if evs is not None else None)
+        set_conc(F * D)
         if world > 1 and not frames_mode:
             flush()
 
@@ -292,7 +311,10 @@ def main() -> None:
     # The count is fixed up front (from the counting pass's device time) and
     # agreed over the ranks, so every rank runs the same collectives.
     est_ms = max(0.05, float(per[0].get("ms", 1.0)))
-    n_settle = torch.tensor([max(5, min(100, int(args.settle_s * 1e3 / est_ms)))], dtype=torch.int64, device=dev)
+    # at least 2D: the drain's launch keys (concurrency 1..D) learn their
+    # orders here, not in the timed region
+    n_settle = torch.tensor([max(5, 2 * D, min(100, int(args.settle_s * 1e3 / est_ms)))], dtype=torch.int64,
+                            device=dev)
     if world > 1:
         dist.all_reduce(n_settle, op=dist.ReduceOp.MIN)
     phase(int(n_settle.item()))
@@ -429,6 +451,7 @@ def main() -> None:
                                                                       "heavy_stream", "heavy_pixels",
                                                                       "heavy_pixel_factor", "heavy_cap", "graph")},
                              "concurrent_launches": renderer.get_option("concurrent_launches"),
+                             "drain": args.drain,
                              "heavy_tiles_used": heavy_used,
                              "heavy_pixels_used": renderer.get_option("heavy_pixels_used")},
                 "launches_per_step": F * (2 if heavy_used > 0 and renderer.get_option("heavy_stream") != 2 else 1),

@@ -149,6 +149,11 @@ def test_config5_1m_row_subset(renderer):
     {"kernel": 0, "coop_walk": 1, "coop_lanes": 64, "walk": 1},
     {"kernel": 3, "coop_walk": 1, "heavy_budget": 1},
     {"kernel": 3, "coop_walk": 1, "heavy_budget": 40},
+    {"kernel": 0, "walk": 13},
+    {"kernel": 0, "walk": 13, "block_waves": 8},
+    {"kernel": 0, "walk": 13, "coop_lanes": 0},
+    {"kernel": 0, "walk": 13, "heavy_first": 0},
+    {"kernel": 0, "walk": 13, "wave_tile": 2, "coop_lanes": 4},
 ])
 def test_schedules_identical(renderer, opts):
     """Every schedule gives the oracle's frame and counters (config 2 at the
@@ -267,6 +272,49 @@ def test_heavy_pixels(renderer, cfg_k, factor):
         rgba, rad, _ = _bands_device(renderer, cam, cfg.width, cfg.height, cfg.max_bounces, cfg.height, 1, 0,
                                      stats=False)                       # a plain launch in the learned order
         _assert_same(rgba, rad, None, *ref)
+    finally:
+        for k, v in DEFAULT_OPTS.items():
+            renderer.set_option(k, v)
+
+
+@pytest.mark.parametrize("cfg_k,bw", [(3, 16), (6, 8), (4, 16)])
+def test_top_tree_walk_whole_frame(renderer, cfg_k, bw):
+    """Walk 13 (the top tree's records in each workgroup's LDS, 8- or
+    16-wave workgroups taking consecutive tiles of the learned order): the
+    learning launch, a counting launch and a plain launch in the learned
+    order give the oracle's whole frame and counters."""
+    from rtamd import configs
+    try:
+        renderer.set_option("walk", 13)
+        renderer.set_option("block_waves", bw)
+        cfg = configs.get(cfg_k)
+        built = cfg.build()
+        cam = cfg.camera()
+        renderer.upload_scene(built)
+        ref = _oracle(built, cam.ubo_bytes(), cfg.width, cfg.height, cfg.max_bounces)
+        for stats in (False, True, False):
+            rgba, rad, st = _bands_device(renderer, cam, cfg.width, cfg.height, cfg.max_bounces, cfg.height, 1, 0,
+                                          stats=stats)
+            _assert_same(rgba, rad, st if stats else None, *ref)
+    finally:
+        for k, v in DEFAULT_OPTS.items():
+            renderer.set_option(k, v)
+
+
+def test_top_tree_walk_1m(renderer):
+    """Walk 13 on config 5 (2^20 triangles, the most its 20-bit leaf field
+    holds): every 64th row of the 4K frame."""
+    from rtamd import configs
+    try:
+        renderer.set_option("walk", 13)
+        cfg = configs.config5()
+        built = cfg.build()
+        cam = cfg.camera()
+        renderer.upload_scene(built)
+        rgba, rad, st = _bands_device(renderer, cam, cfg.width, cfg.height, cfg.max_bounces, 1, 64, 3)
+        ref = _oracle(built, cam.ubo_bytes(), cfg.width, cfg.height, cfg.max_bounces,
+                      tile=(0, 3, cfg.width, cfg.height - 3), row_step=64)
+        _assert_same(rgba, rad, st, *ref)
     finally:
         for k, v in DEFAULT_OPTS.items():
             renderer.set_option(k, v)
@@ -510,7 +558,7 @@ def test_golden_frames_on_gpu(renderer):
 
 
 @pytest.mark.parametrize("shape,n", [("left", 50), ("right", 200), ("random", 300)])
-@pytest.mark.parametrize("walk", [0, 1, 2, "frontier"])
+@pytest.mark.parametrize("walk", [0, 1, 2, 13, "frontier"])
 def test_unbalanced_bvh(renderer, shape, n, walk):
     from rtamd import configs
     built = raw_bvh_scene(n, shape, seed=n)
@@ -581,7 +629,7 @@ def test_accumulation_bit_exact(devices):
         r.close()
 
 
-@pytest.mark.parametrize("ext,sky,walk", [(8, 1, 2), (10, 1, 2), (9, 0, 2), (11, 0, 0), (10, 1, 1)])
+@pytest.mark.parametrize("ext,sky,walk", [(8, 1, 2), (10, 1, 2), (9, 0, 2), (11, 0, 0), (10, 1, 1), (10, 1, 13)])
 def test_spheres_bit_exact(renderer, ext, sky, walk):
     """Extension bit 8 (spheres after the BVH walk; no reference counterpart)
     matches the oracle's ORC_EXT_SPHERES bit for bit, with counters, in every
