@@ -909,8 +909,15 @@ int rt_upload_scene(rt_ctx* ctx, const void* vertices, size_t vertex_bytes,
             depth[i + 1] = depth[i] + 1;
             if (r < n2) depth[r] = depth[i] + 1;
         }
+        // experiment knob RTAMD_TOP_LEVELS: at most this many levels (0: an
+        // empty top tree, walk 13 then loads every node from HBM/L2)
+        static const int max_levels = [] {
+            const char* v = std::getenv("RTAMD_TOP_LEVELS");
+            return v ? std::max(0, std::atoi(v)) : 64;
+        }();
         int levels = 0, count = 0;
-        while (levels < (int)per_level.size() && count + per_level[levels] <= kTopSlots) count += per_level[levels++];
+        while (levels < std::min(max_levels, (int)per_level.size()) && count + per_level[levels] <= kTopSlots)
+            count += per_level[levels++];
         int n_top = 0;
         for (size_t i = 0; i < n2; ++i)
             if (!is_leaf(i) && depth[i] < levels) slot[i] = n_top++;

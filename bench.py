@@ -101,9 +101,11 @@ def main() -> None:
                     help="frames in flight per rank (bands partition): each step's trace goes on the next of this "
                          "many streams, so frames overlap each other's serial tails and the gathers "
                          "(0 = auto, default_inflight(): 4 at N = 1, 8 at N = 2, 12 at N > 2)")
-    ap.add_argument("--drain", type=int, default=1,
+    ap.add_argument("--drain", type=int, default=0,
                     help="1: the last frames of a run of steps plan their heavy pixels for the frames still in "
-                         "flight beside them (concurrent_launches min(D, frames left)); 0: every frame for D")
+                         "flight beside them (concurrent_launches min(D, frames left)); 0 (default): every frame "
+                         "for D.  Measured slower at 20 steps (0.329-0.332 vs 0.309-0.312 ms/frame, "
+                         "profiles/r02/drain)")
     ap.add_argument("--set", default="", help="schedule options name=value,... (rt_set_option) before timing")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-single", action="store_true", help="N > 1: skip rank 0's one-GPU timing")
@@ -281,7 +283,7 @@ def main() -> None:
         f"{node_visits / segments:.2f} node visits/seg, {tri_tests / segments:.3f} tri tests/seg; "
         f"{D} frame(s) in flight, exchange every {G} step(s)")
 
-    # Drain (option --drain, default on): a launch's heavy-pixel bar counts
+    # Drain (option --drain, off by default: measured slower): a launch's heavy-pixel bar counts
     # the launches that will run beside it, and at the end of a run of frames
     # fewer do: step j of n has min(D, n - j) frames in flight from its launch
     # on, so the last frames split their slowest pixels into one-pixel waves
