@@ -476,7 +476,9 @@ def main() -> None:
                 "traffic_source": traffic_src,
                 "kernel": ("trace_simple" if renderer.get_option("kernel") == 0 else "trace_*") + (
                     f" (one launch per frame: the {renderer.get_option('heavy_pixels_used')} heaviest pixels one per "
-                    f"wave first, then every 32x2 tile without them)" if renderer.get_option("heavy_pixels_used") > 0
+                    f"wave first, then every {8 << renderer.get_option('wave_tile')}x"
+                    f"{8 >> renderer.get_option('wave_tile')} tile without them)"
+                    if renderer.get_option("heavy_pixels_used") > 0
                     else f" (one launch per frame: the {heavy_used} heaviest tiles one pixel per wave first)"
                     if heavy_used > 0 and renderer.get_option("heavy_stream") == 2
                     else f" (frame = the {heavy_used} heaviest tiles' one-pixel-wave launch concurrent with the "
