@@ -271,7 +271,17 @@ __device__ __forceinline__ V3 sky_color(V3 d) {                          // getS
 __device__ __forceinline__ void write_pixel(const TraceArgs& a, int lx, int ly, V3 fin) {
     const V3 g = {sqrtf(fin.x), sqrtf(fin.y), sqrtf(fin.z)};              // :235
     const size_t p = (size_t)ly * (size_t)a.tw + (size_t)lx;
+#if RT_NT_STORE
+    // experiment: the frame is written once and read by the next stage, not by
+    // this kernel; a non-temporal store keeps it from evicting walk records
+    if (a.out_rgba) {
+        const uchar4 c = make_uchar4(unorm8(g.x), unorm8(g.y), unorm8(g.z), 255);
+        const uint32_t v = (uint32_t)c.x | ((uint32_t)c.y << 8) | ((uint32_t)c.z << 16) | ((uint32_t)c.w << 24);
+        __builtin_nontemporal_store(v, reinterpret_cast<uint32_t*>(a.out_rgba) + p);
+    }
+#else
     if (a.out_rgba) a.out_rgba[p] = make_uchar4(unorm8(g.x), unorm8(g.y), unorm8(g.z), 255);
+#endif
     if (a.out_rad) {
         a.out_rad[3 * p + 0] = g.x;
         a.out_rad[3 * p + 1] = g.y;

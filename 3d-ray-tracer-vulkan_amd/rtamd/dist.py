@@ -67,6 +67,77 @@ def gather_frames(local, height: int, band_h: int, group=None):
     return gather_batch(local, plan, group, src_index=src_index)
 
 
+# --- rotating row blocks (strong scaling, bench.py's N > 1 default) ----------
+#
+# Each frame is cut into N contiguous row blocks of ceil(H / N) rows (the
+# bands partition with band_h = ceil(H / N): exactly one band per rank).  In
+# frame k rank r traces block (r + k) mod N, so over any N consecutive frames
+# every rank traces every block once: the sky blocks and the mesh blocks are
+# shared evenly across ranks while frames are in flight, as the interleaved
+# bands share them within one frame.  What contiguity buys is the exchange:
+# a rank's block is one contiguous run of frame rows, so rank 0 receives it
+# straight into the frame (RCCL point-to-point receives in one group, the
+# gather's own primitive) and traces its own block in place.  There is no
+# assembly pass and no stack of packed bands: rank 0's device work per frame
+# is its block and the receive of the others, which is what bounds N = 8
+# (tools/rank0_exchange_bench.py, profiles/r02/rccl/).
+
+
+def block_height(height: int, world: int) -> int:
+    return -(-height // world)
+
+
+def block_offset(frame: int, world: int, rank: int) -> int:
+    """The block rank traces in frame `frame` (the band_off of rt_render_bands_device
+    with band_h = block_height, stride = world)."""
+    return (rank + frame) % world
+
+
+def block_range(height: int, world: int, block: int):
+    """Frame rows [y0, y1) of block `block`."""
+    h = block_height(height, world)
+    y0 = min(height, block * h)
+    return y0, min(height, y0 + h)
+
+
+def exchange_blocks(frames, local, frame_ids, height: int, group=None) -> None:
+    """One batch of the blocks partition.  local[i]: this rank's packed block
+    of frame frame_ids[i] ([>= rows, W, C]).  frames[i] (rank 0 only): that
+    frame's [height, W, C] buffer, whose own block rank 0 has traced in
+    place; every other rank's block is received straight into its rows.  One
+    batch_isend_irecv (one RCCL group of sends / receives); on return the
+    current stream is ordered after it."""
+    import torch.distributed as dist
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    # gloo moves host memory only: device tensors are staged through the host
+    # (CPU tests and one-GPU rehearsals; RCCL sends and receives device memory)
+    staged = dist.get_backend(group) == "gloo" and local is not None and local.is_cuda
+    ops, landings = [], []
+    for i, f in enumerate(frame_ids):
+        if rank == 0:
+            for r in range(1, world):
+                y0, y1 = block_range(height, world, block_offset(f, world, r))
+                if y1 > y0:
+                    dst = frames[i][y0:y1]
+                    if staged:
+                        landings.append((dst, dst.cpu()))
+                        dst = landings[-1][1]
+                    ops.append(dist.P2POp(dist.irecv, dst, dist.get_global_rank(group, r)
+                                          if group is not None else r, group))
+        else:
+            y0, y1 = block_range(height, world, block_offset(f, world, rank))
+            if y1 > y0:
+                src = local[i][: y1 - y0]
+                ops.append(dist.P2POp(dist.isend, src.cpu() if staged else src,
+                                      dist.get_global_rank(group, 0) if group is not None else 0, group))
+    if ops:
+        for w in dist.batch_isend_irecv(ops):
+            w.wait()
+    for dst, host in landings:
+        dst.copy_(host)
+
+
 # --- frame batches (weak scaling) -------------------------------------------
 #
 # One frame tiled over N GPUs is bounded by its slowest wave (a few pixels'

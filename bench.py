@@ -94,9 +94,11 @@ def main() -> None:
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", type=int, default=3, help="BASELINE config index (3 = headline)")
     ap.add_argument("--band", type=int, default=16, help="band height for N > 1")
-    ap.add_argument("--partition", choices=("bands", "frames"), default="bands",
-                    help="N > 1: bands = one frame per step tiled over the ranks (strong scaling, default); "
-                         "frames = N frames per step, bands rotated over ranks (weak)")
+    ap.add_argument("--partition", choices=("blocks", "bands", "frames"), default="blocks",
+                    help="N > 1: blocks = one frame per step in N contiguous row blocks, rank r tracing block "
+                         "(r + k) mod N of frame k, received by rank 0 straight into the frame (strong scaling, "
+                         "default); bands = one frame per step in interleaved --band-row bands, gathered and "
+                         "assembled on rank 0 (strong); frames = N frames per step, bands rotated over ranks (weak)")
     ap.add_argument("--inflight", type=int, default=0,
                     help="frames in flight per rank (bands partition): each step's trace goes on the next of this "
                          "many streams, so frames overlap each other's serial tails and the gathers "
@@ -109,6 +111,9 @@ def main() -> None:
     ap.add_argument("--set", default="", help="schedule options name=value,... (rt_set_option) before timing")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-single", action="store_true", help="N > 1: skip rank 0's one-GPU timing")
+    ap.add_argument("--exchange-priority", type=int, default=1,
+                    help="N > 1: 1 = the collective's stream and the assembly stream at high priority, so the "
+                         "exchange is not starved of workgroup slots by the traces in flight")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU baseline sample time")
     ap.add_argument("--settle-s", type=float, default=0.2,
                     help="untimed frames before the warmup steps: this many seconds of counting-pass time "
@@ -128,15 +133,26 @@ def main() -> None:
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         log(f"note: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE")
+    # BENCH_FORCE_DIST=1 (rehearsal only): the N > 1 code path at any world size,
+    # so one GPU runs the bands partition, its RCCL gather and the rank-0 checks.
+    dist_on = world > 1 or os.environ.get("BENCH_FORCE_DIST") == "1"
     # BENCH_SHARE_GPU=1 (rehearsal only): ranks share the visible GPUs round-robin.
     dev_index = local_rank % torch.cuda.device_count() if os.environ.get("BENCH_SHARE_GPU") else local_rank
     torch.cuda.set_device(dev_index)
     dev = torch.device("cuda", dev_index)
     local_rank = dev_index
     backend = None
-    if world > 1:
+    if dist_on:
         backend = os.environ.get("BENCH_DIST_BACKEND", "nccl")     # nccl = RCCL over xGMI
-        dist.init_process_group(backend, device_id=dev if backend == "nccl" else None)
+        pg_options = None
+        if backend == "nccl" and args.exchange_priority:
+            # RCCL's internal stream at high priority: with D traces in flight
+            # every CU slot is taken, and a normal-priority collective gets
+            # slots only as trace waves end
+            from torch.distributed import ProcessGroupNCCL
+            pg_options = ProcessGroupNCCL.Options()
+            pg_options.is_high_priority_stream = True
+        dist.init_process_group(backend, device_id=dev if backend == "nccl" else None, pg_options=pg_options)
 
     cfg = configs.get(args.config)
     t0 = time.time()
@@ -152,7 +168,8 @@ def main() -> None:
         k, v = kv.split("=")
         renderer.set_option(k.strip(), int(v))
     L = rtamd.lib()
-    from rtamd.dist import BatchPlan, batch_band_offset, gather_batch, gather_frames
+    from rtamd.dist import (BatchPlan, batch_band_offset, block_height, block_offset, block_range,
+                            exchange_blocks, gather_batch, gather_frames)
 
     # Partition.  bands (default): one frame per step tiled over the ranks in
     # interleaved band_h-row bands (strong scaling; a frame lasts as long as
@@ -162,8 +179,9 @@ def main() -> None:
     # rotating bands, so every rank traces one frame's worth of pixels per
     # step (weak scaling).  At N = 1 both are one whole frame per step.
     frames_mode = args.partition == "frames" and world > 1
+    blocks_mode = args.partition == "blocks" and dist_on
     F = world if frames_mode else 1
-    band_h = H if world == 1 else args.band
+    band_h = H if not dist_on else (block_height(H, world) if blocks_mode else args.band)
     offsets = [batch_band_offset(f, world, rank) if frames_mode else rank for f in range(F)]
     plan = BatchPlan(H, band_h, world, F) if frames_mode else None
     rows_f = [L.rt_band_rows(H, band_h, world, off) for off in offsets]
@@ -186,34 +204,40 @@ def main() -> None:
     # previous one is gathered; a slot is retraced only after the gather that
     # read it.  N = 1: one slot per stream.  frames partition: one gather per
     # step of F frames, D + 1 buffers.
-    G = D if (world > 1 and not frames_mode) else 1
+    G = D if (dist_on and not frames_mode) else 1
     if frames_mode:
         n_slots = D + 1
-    elif world > 1:
+    elif dist_on:
         n_slots = 2 * G
     else:
         n_slots = D
     d_bufs = [torch.empty((F, max_rows, W, 4), dtype=torch.uint8, device=dev) for _ in range(n_slots)] \
         if frames_mode else None
     slots = torch.empty((n_slots, max_rows, W, 4), dtype=torch.uint8, device=dev) if not frames_mode else None
+    # blocks: rank 0 traces its block of frame k in place in fring[k mod n_slots]
+    # and receives the other blocks there
+    fring = torch.empty((n_slots, H, W, 4), dtype=torch.uint8, device=dev) if (blocks_mode and rank == 0) else None
     gathered = [None] * (n_slots if frames_mode else 2)   # event: the last gather that read a buffer / half
     # One stream per launch in flight (launches and their events on the same
     # queue); the gathers run on main_stream.
     streams = [torch.cuda.Stream(dev) for _ in range(min(F * D, 12))]
-    main_stream = torch.cuda.Stream(dev) if (world > 1 or len(streams) > 1) else streams[0]
+    hi = -1 if (dist_on and args.exchange_priority) else 0   # the assembly (index_select) at high priority
+    main_stream = torch.cuda.Stream(dev, priority=hi) if (dist_on or len(streams) > 1) else streams[0]
     torch.cuda.set_stream(main_stream)
-    src_index = torch.as_tensor(plan.src, device=dev) if (plan and world > 1) else None
+    src_index = torch.as_tensor(plan.src, device=dev) if (plan and dist_on) else None
 
     import ctypes as C
     from rtamd._lib import Stats, check
 
-    def trace(f, stats: bool = False, ev=None, out=None, si=0):
+    def trace(f, stats: bool = False, ev=None, out=None, si=0, off=None):
         s = streams[si % len(streams)]
         st = Stats()
         if ev is not None:          # recorded after the stream's wait for the gather: the trace only
             ev[0].record(s)
-        check(L.rt_render_bands_device(renderer._ctx, C.byref(cam.ubo), W, H, B, band_h, world, offsets[f],
-                                       out.data_ptr(), None, s.cuda_stream, C.byref(st) if stats else None))
+        if out.shape[0] > 0:
+            check(L.rt_render_bands_device(renderer._ctx, C.byref(cam.ubo), W, H, B, band_h, world,
+                                           offsets[f] if off is None else off, out.data_ptr(), None,
+                                           s.cuda_stream, C.byref(st) if stats else None))
         if ev is not None:
             ev[1].record(s)
         return st.as_dict() if stats else None
@@ -231,7 +255,13 @@ def main() -> None:
         half = ((k - 1) // G) % 2
         for s in streams:
             main_stream.wait_stream(s)
-        out = gather_frames(slots[half * G: half * G + n], H, band_h)   # RCCL gather + rank-0 assembly
+        if blocks_mode:         # RCCL sends / receives straight into rank 0's frames
+            base = half * G
+            exchange_blocks(fring[base: base + n] if rank == 0 else None, slots[base: base + n],
+                            list(range(k - n, k)), H)
+            out = fring[base: base + n] if rank == 0 else None
+        else:
+            out = gather_frames(slots[half * G: half * G + n], H, band_h)   # RCCL gather + rank-0 assembly
         gathered[half] = torch.cuda.Event()
         gathered[half].record(main_stream)
         k_step[0] = ((k + G - 1) // G) * G       # the next phase starts a fresh batch
@@ -257,7 +287,18 @@ def main() -> None:
             gathered[b].record(main_stream)
             return
         s = streams[k % len(streams)]
-        if world > 1:
+        if blocks_mode:
+            half = (k // G) % 2
+            if k % G == 0 and gathered[half] is not None:
+                for t in streams:                      # the exchange that last used this half is done
+                    t.wait_event(gathered[half])
+            off = block_offset(k, world, rank)
+            y0, y1 = block_range(H, world, off)
+            out = fring[k % n_slots, y0:y1] if rank == 0 else slots[k % n_slots, : y1 - y0]
+            trace(0, ev=evs[0] if evs is not None else None, out=out, si=k, off=off)
+            if k % G == G - 1:
+                flush()
+        elif dist_on:
             half = (k // G) % 2
             if k % G == 0 and gathered[half] is not None:
                 for t in streams:                      # the gather that last read this half is done
@@ -275,10 +316,12 @@ def main() -> None:
     counts = torch.tensor([sum(p[k] for p in per) for k in ("pixels", "segments", "node_visits", "tri_tests",
                                                              "mat_reads")], dtype=torch.float64, device=dev)
     local = counts.clone()
-    if world > 1:
+    if dist_on:
         dist.all_reduce(counts)
     pixels, segments, node_visits, tri_tests, mat_reads = [float(x) for x in counts.tolist()]
-    l_pix, l_seg, l_nodes, l_tris, l_mats = [float(x) / F for x in local.tolist()]   # per launch
+    # per launch (blocks: the mean over the ranks' blocks, which differ in cost)
+    per_launch = (counts / world) if blocks_mode else local
+    l_pix, l_seg, l_nodes, l_tris, l_mats = [float(x) / F for x in per_launch.tolist()]
     log(f"[rank {rank}] step: {F} frame(s), {segments:.0f} segments ({segments / pixels:.3f}/px), "
         f"{node_visits / segments:.2f} node visits/seg, {tri_tests / segments:.3f} tri tests/seg; "
         f"{D} frame(s) in flight, exchange every {G} step(s)")
@@ -302,7 +345,7 @@ def main() -> None:
                 set_conc(F * min(D, n - j))
             step(evs[j] if evs is not None else None)
         set_conc(F * D)
-        if world > 1 and not frames_mode:
+        if dist_on and not frames_mode:
             flush()
 
     # Settle (untimed): 5-100 frames, about settle_s / (the counting pass's
@@ -317,13 +360,13 @@ def main() -> None:
     # orders here, not in the timed region
     n_settle = torch.tensor([max(5, 2 * D, min(100, int(args.settle_s * 1e3 / est_ms)))], dtype=torch.int64,
                             device=dev)
-    if world > 1:
+    if dist_on:
         dist.all_reduce(n_settle, op=dist.ReduceOp.MIN)
     phase(int(n_settle.item()))
     torch.cuda.synchronize(dev)
     phase(args.warmup)
     torch.cuda.synchronize(dev)
-    if world > 1:
+    if dist_on:
         dist.barrier()
     torch.cuda.synchronize(dev)
 
@@ -345,7 +388,7 @@ def main() -> None:
             main_stream.wait_stream(s)
     reg[1].record(main_stream)
     torch.cuda.synchronize(dev)
-    if world > 1:
+    if dist_on:
         dist.barrier()
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t_start
@@ -357,7 +400,7 @@ def main() -> None:
     heavy_used = renderer.get_option("heavy_tiles_used")   # of the last timed launch
     verified = None
     single = None
-    if world > 1 and rank == 0:
+    if dist_on and rank == 0:
         # the assembled frames equal the 1-GPU frame
         full = torch.empty((H, W, 4), dtype=torch.uint8, device=dev)
         check(L.rt_render_bands_device(renderer._ctx, C.byref(cam.ubo), W, H, B, H, 1, 0, full.data_ptr(), None,
@@ -389,7 +432,7 @@ def main() -> None:
             single = time.perf_counter() - t1
 
     t = torch.tensor([elapsed, launch_ms, frame_ms], dtype=torch.float64, device=dev)
-    if world > 1:
+    if dist_on:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed, launch_ms_max, frame_ms_max = float(t[0]), float(t[1]), float(t[2])
 
@@ -436,11 +479,15 @@ def main() -> None:
                 "segments_per_frame": int(segments / F),
                 "node_visits_per_segment": round(node_visits / segments, 3),
                 "tri_tests_per_segment": round(tri_tests / segments, 4),
-                "partition": f"one whole frame per step, {D} frames in flight" if world == 1 else
+                "partition": f"one whole frame per step, {D} frames in flight" if not dist_on else
                              (f"{F} frames per step, {band_h}-row bands rotated over {world} ranks "
                               f"(rank r traces bands (r+f) mod {world} of frame f), {gather_kind} gather + rank-0 "
                               f"assembly{shared}"
                               if frames_mode else
+                              f"one frame per step in {world} contiguous {band_h}-row blocks, rank r tracing block "
+                              f"(r + k) mod {world} of frame k, {D} frames in flight per rank, {gather_kind} "
+                              f"sends / receives of every {G} frames straight into rank 0's frames{shared}"
+                              if blocks_mode else
                               f"one frame per step, interleaved {band_h}-row bands over {world} ranks, "
                               f"{D} frames in flight per rank, {gather_kind} gather of every {G} frames + rank-0 "
                               f"assembly{shared}"),
@@ -484,9 +531,9 @@ def main() -> None:
                     else f" (frame = the {heavy_used} heaviest tiles' one-pixel-wave launch concurrent with the "
                          f"other tiles' launch; kernel_ms spans both)" if heavy_used > 0 else ""),
                 "kernel_ms": round(launch_ms, 4),
-                "kernel_ms_max_over_ranks": round(launch_ms_max, 4) if world > 1 else None,
+                "kernel_ms_max_over_ranks": round(launch_ms_max, 4) if dist_on else None,
                 "frame_ms_device": round(frame_ms, 4),
-                "frame_ms_device_max_over_ranks": round(frame_ms_max, 4) if world > 1 else None,
+                "frame_ms_device_max_over_ranks": round(frame_ms_max, 4) if dist_on else None,
                 "launches_in_flight_avg": round(launch_ms / frame_ms, 2),
                 "events": "kernel_ms: each launch's own stream, around every launch (after its wait for the "
                           "gather); frame_ms_device: main stream around the timed region after joining every "
@@ -507,7 +554,7 @@ def main() -> None:
             out["speedup_vs_1gpu"] = round(value / sv, 3)
         print(json.dumps(out), flush=True)
     renderer.close()
-    if world > 1:
+    if dist_on:
         dist.destroy_process_group()
 
 

@@ -169,3 +169,78 @@ def test_bands_steps_gathered_in_one_batch(world, band_h):
         ref = oracle_lib.render(built.model_vertex_data, built.model_material_data, built.flat_bvh_data,
                                 cam.ubo_bytes(), W, H, B)[0]
         assert np.array_equal(got[f], ref), f
+
+
+def _blocks_worker(rank, world, port, q, first_frame):
+    import sys
+    sys.path[:0] = [os.path.join(ROOT, "3d-ray-tracer-vulkan_amd"), ROOT]
+    import torch
+    import torch.distributed as dist
+    from oracle import oracle_lib
+    from rtamd import configs, lib
+    from rtamd.dist import block_height, block_offset, block_range, exchange_blocks
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        cfg = configs.config2()
+        built = cfg.build()
+        W, H, B = 96, 53, 3
+        ids = list(range(first_frame, first_frame + 4))           # one batch of 4 consecutive steps
+        bh = block_height(H, world)
+        local = torch.zeros((len(ids), bh, W, 4), dtype=torch.uint8)
+        frames = torch.zeros((len(ids), H, W, 4), dtype=torch.uint8) if rank == 0 else None
+        traced = []
+        for i, f in enumerate(ids):
+            cam = configs.Camera((-25.0 + 5 * f, 30.0, 140.0), (0.0, 0.0, 0.0), (0.0, 1.0, 0.0), 20.0, W / H)
+            b = block_offset(f, world, rank)
+            y0, y1 = block_range(H, world, b)
+            # the kernels' packing of the one band of this rank is the block's rows in order
+            assert lib().rt_band_rows(H, bh, world, b) == y1 - y0
+            if y1 > y0:
+                rgba, _, _ = oracle_lib.render(built.model_vertex_data, built.model_material_data,
+                                               built.flat_bvh_data, cam.ubo_bytes(), W, H, B,
+                                               tile=(0, y0, W, y1 - y0), n_threads=1)
+                (frames[i, y0:y1] if rank == 0 else local[i, : y1 - y0]).copy_(torch.from_numpy(rgba))
+            traced.append(b)
+        q.put(("traced", rank, traced))
+        exchange_blocks(frames, local, ids, H)
+        if rank == 0:
+            q.put(("frames", frames.numpy()))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,first", [(2, 0), (3, 5), (4, 2)])
+def test_blocks_exchange_assembles_frames(world, first):
+    """Rotating row blocks (bench.py's N > 1 default): in frame k rank r
+    traces block (r + k) mod N; rank 0 traces its block in place and receives
+    every other rank's block straight into the frame (one batch of
+    point-to-point receives).  53 rows over 3 / 4 ranks leaves a short last
+    block.  Every frame of the batch equals the oracle's frame."""
+    from oracle import oracle_lib
+    from rtamd import configs
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_blocks_worker, args=(r, world, port, q, first)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got, traced = None, {}
+    for _ in range(world + 1):
+        item = q.get(timeout=300)
+        if item[0] == "frames":
+            got = item[1]
+        else:
+            traced[item[1]] = item[2]
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    for i in range(4):                                    # each frame's blocks: one per rank, all different
+        assert sorted(traced[r][i] for r in range(world)) == list(range(world))
+    built = configs.config2().build()
+    W, H, B = 96, 53, 3
+    for i, f in enumerate(range(first, first + 4)):
+        cam = configs.Camera((-25.0 + 5 * f, 30.0, 140.0), (0.0, 0.0, 0.0), (0.0, 1.0, 0.0), 20.0, W / H)
+        ref = oracle_lib.render(built.model_vertex_data, built.model_material_data, built.flat_bvh_data,
+                                cam.ubo_bytes(), W, H, B)[0]
+        assert np.array_equal(got[i], ref), f

@@ -277,6 +277,32 @@ def test_heavy_pixels(renderer, cfg_k, factor):
             renderer.set_option(k, v)
 
 
+@pytest.mark.parametrize("cfg_k", [3, 4, 5])
+def test_bench_setting_whole_frame(renderer, cfg_k):
+    """BASELINE configs 3, 4 and 5 as whole frames (config 5: 1M triangles,
+    3840x2160, 8 bounces) under bench.py's N = 1 setting: the default
+    schedule with 4 launches in flight counted by the heavy-pixel bar
+    (concurrent_launches 4).  The learning launch, then the production kernel
+    (no counters) in the learned order, then a counting launch: each frame
+    equals the oracle's whole frame, and the counters its counts."""
+    from rtamd import configs
+    try:
+        renderer.set_option("concurrent_launches", 4)
+        cfg = configs.get(cfg_k)
+        built = cfg.build()
+        cam = cfg.camera()
+        renderer.upload_scene(built)
+        ref = _oracle(built, cam.ubo_bytes(), cfg.width, cfg.height, cfg.max_bounces)
+        for stats in (False, False, True):
+            rgba, rad, st = _bands_device(renderer, cam, cfg.width, cfg.height, cfg.max_bounces, cfg.height, 1, 0,
+                                          stats=stats)
+            _assert_same(rgba, rad, st if stats else None, *ref)
+        assert st["pixels"] == cfg.width * cfg.height
+    finally:
+        for k, v in DEFAULT_OPTS.items():
+            renderer.set_option(k, v)
+
+
 @pytest.mark.parametrize("cfg_k,bw", [(3, 16), (6, 8), (4, 16)])
 def test_top_tree_walk_whole_frame(renderer, cfg_k, bw):
     """Walk 13 (the top tree's records in each workgroup's LDS, 8- or

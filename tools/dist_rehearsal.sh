@@ -10,7 +10,7 @@ for part in ${PARTS:-bands frames}; do
   for be in ${BACKENDS:-nccl gloo}; do
     BENCH_SHARE_GPU=1 BENCH_DIST_BACKEND=$be timeout -k 10 300 python -m torch.distributed.run --nnodes=1 \
       --nproc-per-node ${NPROC:-2} --master-addr 127.0.0.1 --master-port $((29500 + RANDOM % 1000)) bench.py --gpus ${NPROC:-2} \
-      --steps 10 --warmup 3 --partition $part > "$OUT/bench_${part}_${be}_n${NPROC:-2}.json" 2> "$OUT/bench_${part}_${be}_n${NPROC:-2}.err"
+      --steps ${STEPS:-24} --warmup 3 --partition $part > "$OUT/bench_${part}_${be}_n${NPROC:-2}.json" 2> "$OUT/bench_${part}_${be}_n${NPROC:-2}.err"
     rc=$?
     echo "$part $be n=${NPROC:-2} rc=$rc" >> "$OUT/status.txt"
     if [ $rc -eq 0 ]; then break; fi
