@@ -1,13 +1,20 @@
 """Multi-GPU frame tiling: one process per GPU (torch.distributed; backend
 "nccl" = RCCL over xGMI on MI355X, "gloo" for CPU tests).
 
-The frame is split into interleaved row bands: rank r of N traces the
-band_h-row bands r, r+N, r+2N, ... (so sky rows and geometry rows spread
-evenly over the ranks).  The scene is replicated on every rank (uploaded once
-per rank); pixels are independent and seeded by their global (x, y)
-(compute_dynamic_ray.comp:164), so the assembled frame equals the one-GPU
-frame bit for bit.  The one exchange is a gather of each rank's packed band
-rows to rank 0, which scatters them into the frame.
+Two strong-scaling partitions of a frame, and a weak-scaling batch:
+
+* rotating row pieces (bench.py's N > 1 default; block_layout,
+  exchange_blocks): one contiguous run of rows per rank, laid out in an order
+  that rotates every frame; rank 0 traces its piece in place and receives the
+  others straight into the frame (RCCL point-to-point in one group);
+* interleaved row bands (gather_frame, gather_frames): rank r of N traces the
+  band_h-row bands r, r+N, r+2N, ...; one gather of the packed bands to rank
+  0, which assembles the frame with one index_select;
+* frame batches (BatchPlan, gather_batch): N frames per step, bands rotated.
+
+The scene is replicated on every rank (uploaded once per rank); pixels are
+independent and seeded by their global (x, y) (compute_dynamic_ray.comp:164),
+so every partition's frame equals the one-GPU frame bit for bit.
 """
 from __future__ import annotations
 
@@ -69,42 +76,48 @@ def gather_frames(local, height: int, band_h: int, group=None):
 
 # --- rotating row blocks (strong scaling, bench.py's N > 1 default) ----------
 #
-# Each frame is cut into N contiguous row blocks of ceil(H / N) rows (the
-# bands partition with band_h = ceil(H / N): exactly one band per rank).  In
-# frame k rank r traces block (r + k) mod N, so over any N consecutive frames
-# every rank traces every block once: the sky blocks and the mesh blocks are
-# shared evenly across ranks while frames are in flight, as the interleaved
-# bands share them within one frame.  What contiguity buys is the exchange:
-# a rank's block is one contiguous run of frame rows, so rank 0 receives it
-# straight into the frame (RCCL point-to-point receives in one group, the
-# gather's own primitive) and traces its own block in place.  There is no
-# assembly pass and no stack of packed bands: rank 0's device work per frame
-# is its block and the receive of the others, which is what bounds N = 8
-# (tools/rank0_exchange_bench.py, profiles/r02/rccl/).
+# Each frame is cut into N contiguous row pieces, one per rank: rank 0's piece
+# has h0 = root_share x H / N rows and the other N - 1 pieces split the rest
+# evenly.  In frame k the pieces are laid out from row 0 in the rotated order
+# k, k+1, ..., k-1 (mod N), so over any N consecutive frames every rank's
+# piece visits N positions spread over the frame: the sky rows and the mesh
+# rows are shared out while frames are in flight, as the interleaved bands
+# share them within one frame.  What contiguity buys is the exchange: a
+# rank's piece is one run of frame rows, so rank 0 receives it straight into
+# the frame (RCCL point-to-point receives in one group, the gather's own
+# primitive) and traces its own piece in place; there is no assembly pass.
+# Rank 0 still does the most device work (its piece and every receive), so
+# root_share < 1 gives it fewer rows (tools/rank0_exchange_bench.py,
+# profiles/r02/rccl/).
 
 
-def block_height(height: int, world: int) -> int:
-    return -(-height // world)
+def block_sizes(height: int, world: int, root_share: float = 1.0):
+    """Rows of each rank's piece (rank 0 first)."""
+    if world == 1:
+        return [height]
+    h0 = max(0, min(height, int(round(root_share * height / world))))
+    rest = height - h0
+    base, extra = divmod(rest, world - 1)
+    return [h0] + [base + (1 if j < extra else 0) for j in range(world - 1)]
 
 
-def block_offset(frame: int, world: int, rank: int) -> int:
-    """The block rank traces in frame `frame` (the band_off of rt_render_bands_device
-    with band_h = block_height, stride = world)."""
-    return (rank + frame) % world
+def block_layout(height: int, world: int, frame: int, root_share: float = 1.0):
+    """Frame rows [y0, y1) of every rank's piece in frame `frame` (indexed by rank)."""
+    sizes = block_sizes(height, world, root_share)
+    out = [None] * world
+    y = 0
+    for j in range(world):
+        r = (frame + j) % world
+        out[r] = (y, y + sizes[r])
+        y += sizes[r]
+    return out
 
 
-def block_range(height: int, world: int, block: int):
-    """Frame rows [y0, y1) of block `block`."""
-    h = block_height(height, world)
-    y0 = min(height, block * h)
-    return y0, min(height, y0 + h)
-
-
-def exchange_blocks(frames, local, frame_ids, height: int, group=None) -> None:
-    """One batch of the blocks partition.  local[i]: this rank's packed block
-    of frame frame_ids[i] ([>= rows, W, C]).  frames[i] (rank 0 only): that
-    frame's [height, W, C] buffer, whose own block rank 0 has traced in
-    place; every other rank's block is received straight into its rows.  One
+def exchange_blocks(frames, local, frame_ids, height: int, root_share: float = 1.0, group=None) -> None:
+    """One batch of the blocks partition.  local[i]: this rank's piece of
+    frame frame_ids[i] ([>= rows, W, C]).  frames[i] (rank 0 only): that
+    frame's [height, W, C] buffer, whose own piece rank 0 has traced in place;
+    every other rank's piece is received straight into its rows.  One
     batch_isend_irecv (one RCCL group of sends / receives); on return the
     current stream is ordered after it."""
     import torch.distributed as dist
@@ -113,24 +126,24 @@ def exchange_blocks(frames, local, frame_ids, height: int, group=None) -> None:
     # gloo moves host memory only: device tensors are staged through the host
     # (CPU tests and one-GPU rehearsals; RCCL sends and receives device memory)
     staged = dist.get_backend(group) == "gloo" and local is not None and local.is_cuda
+    glob = (lambda r: dist.get_global_rank(group, r)) if group is not None else (lambda r: r)
     ops, landings = [], []
     for i, f in enumerate(frame_ids):
+        lay = block_layout(height, world, f, root_share)
         if rank == 0:
             for r in range(1, world):
-                y0, y1 = block_range(height, world, block_offset(f, world, r))
+                y0, y1 = lay[r]
                 if y1 > y0:
                     dst = frames[i][y0:y1]
                     if staged:
                         landings.append((dst, dst.cpu()))
                         dst = landings[-1][1]
-                    ops.append(dist.P2POp(dist.irecv, dst, dist.get_global_rank(group, r)
-                                          if group is not None else r, group))
+                    ops.append(dist.P2POp(dist.irecv, dst, glob(r), group))
         else:
-            y0, y1 = block_range(height, world, block_offset(f, world, rank))
+            y0, y1 = lay[rank]
             if y1 > y0:
                 src = local[i][: y1 - y0]
-                ops.append(dist.P2POp(dist.isend, src.cpu() if staged else src,
-                                      dist.get_global_rank(group, 0) if group is not None else 0, group))
+                ops.append(dist.P2POp(dist.isend, src.cpu() if staged else src, glob(0), group))
     if ops:
         for w in dist.batch_isend_irecv(ops):
             w.wait()

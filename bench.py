@@ -79,6 +79,17 @@ def default_inflight(world: int) -> int:
     return 4 if world == 1 else (8 if world == 2 else 12)
 
 
+def default_root_share(world: int) -> float:
+    """blocks partition: rank 0's piece in units of H / N rows.  Rank 0 also
+    receives the other N - 1 pieces of every frame into place, which costs it
+    device time the other ranks do not spend; balancing trace + exchange time
+    per frame, rank 0's share is 1 - X (N - 1) / T (X: its exchange time per
+    frame, T: N x a share's trace time).  The one-GPU emulation of rank 0
+    (tools/rank0_exchange_bench.py, profiles/r02/rccl/) puts X at ~0.019 ms
+    per frame at N = 8 and ~0.01 at N = 4 for config 3."""
+    return 1.0 if world <= 2 else (0.9 if world <= 4 else 0.6)
+
+
 def file_sha16(path: str) -> str:
     import hashlib
     with open(path, "rb") as fh:
@@ -111,6 +122,9 @@ def main() -> None:
     ap.add_argument("--set", default="", help="schedule options name=value,... (rt_set_option) before timing")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-single", action="store_true", help="N > 1: skip rank 0's one-GPU timing")
+    ap.add_argument("--root-share", type=float, default=-1.0,
+                    help="blocks: rank 0's piece in units of H / N rows (it also receives every other piece); "
+                         "-1 = default_root_share(N)")
     ap.add_argument("--exchange-priority", type=int, default=1,
                     help="N > 1: 1 = the collective's stream and the assembly stream at high priority, so the "
                          "exchange is not starved of workgroup slots by the traces in flight")
@@ -168,8 +182,8 @@ def main() -> None:
         k, v = kv.split("=")
         renderer.set_option(k.strip(), int(v))
     L = rtamd.lib()
-    from rtamd.dist import (BatchPlan, batch_band_offset, block_height, block_offset, block_range,
-                            exchange_blocks, gather_batch, gather_frames)
+    from rtamd.dist import (BatchPlan, batch_band_offset, block_layout, block_sizes, exchange_blocks, gather_batch,
+                            gather_frames)
 
     # Partition.  bands (default): one frame per step tiled over the ranks in
     # interleaved band_h-row bands (strong scaling; a frame lasts as long as
@@ -181,11 +195,16 @@ def main() -> None:
     frames_mode = args.partition == "frames" and world > 1
     blocks_mode = args.partition == "blocks" and dist_on
     F = world if frames_mode else 1
-    band_h = H if not dist_on else (block_height(H, world) if blocks_mode else args.band)
+    band_h = H if (not dist_on or blocks_mode) else args.band
     offsets = [batch_band_offset(f, world, rank) if frames_mode else rank for f in range(F)]
     plan = BatchPlan(H, band_h, world, F) if frames_mode else None
     rows_f = [L.rt_band_rows(H, band_h, world, off) for off in offsets]
     max_rows = plan.max_rows if plan else max(L.rt_band_rows(H, band_h, world, r) for r in range(world))
+    # blocks: rank 0's piece is root_share x H / N rows (it also receives the
+    # other pieces of every frame), the other ranks split the rest
+    share = (args.root_share if args.root_share >= 0 else default_root_share(world)) if blocks_mode else 1.0
+    if blocks_mode:
+        max_rows = max(block_sizes(H, world, share))
     # Frames in flight (bands partition): step k traces on stream k mod D.  A
     # frame's own time is bounded by its slowest pixel's dependent chain
     # (DESIGN.md §7), so the render loop keeps D frames on the device at once
@@ -229,15 +248,19 @@ def main() -> None:
     import ctypes as C
     from rtamd._lib import Stats, check
 
-    def trace(f, stats: bool = False, ev=None, out=None, si=0, off=None):
+    def trace(f, stats: bool = False, ev=None, out=None, si=0, rect=None):
         s = streams[si % len(streams)]
         st = Stats()
         if ev is not None:          # recorded after the stream's wait for the gather: the trace only
             ev[0].record(s)
-        if out.shape[0] > 0:
-            check(L.rt_render_bands_device(renderer._ctx, C.byref(cam.ubo), W, H, B, band_h, world,
-                                           offsets[f] if off is None else off, out.data_ptr(), None,
-                                           s.cuda_stream, C.byref(st) if stats else None))
+        if rect is not None:        # blocks: frame rows [y0, y1), packed into out
+            if rect[1] > rect[0]:
+                check(L.rt_render_tile_device(renderer._ctx, C.byref(cam.ubo), W, H, B, 0, rect[0], W,
+                                              rect[1] - rect[0], out.data_ptr(), None, s.cuda_stream,
+                                              C.byref(st) if stats else None))
+        else:
+            check(L.rt_render_bands_device(renderer._ctx, C.byref(cam.ubo), W, H, B, band_h, world, offsets[f],
+                                           out.data_ptr(), None, s.cuda_stream, C.byref(st) if stats else None))
         if ev is not None:
             ev[1].record(s)
         return st.as_dict() if stats else None
@@ -258,7 +281,7 @@ def main() -> None:
         if blocks_mode:         # RCCL sends / receives straight into rank 0's frames
             base = half * G
             exchange_blocks(fring[base: base + n] if rank == 0 else None, slots[base: base + n],
-                            list(range(k - n, k)), H)
+                            list(range(k - n, k)), H, share)
             out = fring[base: base + n] if rank == 0 else None
         else:
             out = gather_frames(slots[half * G: half * G + n], H, band_h)   # RCCL gather + rank-0 assembly
@@ -292,10 +315,9 @@ def main() -> None:
             if k % G == 0 and gathered[half] is not None:
                 for t in streams:                      # the exchange that last used this half is done
                     t.wait_event(gathered[half])
-            off = block_offset(k, world, rank)
-            y0, y1 = block_range(H, world, off)
+            y0, y1 = block_layout(H, world, k, share)[rank]
             out = fring[k % n_slots, y0:y1] if rank == 0 else slots[k % n_slots, : y1 - y0]
-            trace(0, ev=evs[0] if evs is not None else None, out=out, si=k, off=off)
+            trace(0, ev=evs[0] if evs is not None else None, out=out, si=k, rect=(y0, y1))
             if k % G == G - 1:
                 flush()
         elif dist_on:
@@ -311,7 +333,8 @@ def main() -> None:
 
     # Counting pass (untimed): this rank's work, then the job totals.
     count_out = torch.empty((max_rows, W, 4), dtype=torch.uint8, device=dev)
-    per = [trace(f, stats=True, out=count_out) for f in range(F)]
+    per = [trace(f, stats=True, out=count_out, rect=block_layout(H, world, 0, share)[rank] if blocks_mode else None)
+           for f in range(F)]
     torch.cuda.synchronize(dev)
     counts = torch.tensor([sum(p[k] for p in per) for k in ("pixels", "segments", "node_visits", "tri_tests",
                                                              "mat_reads")], dtype=torch.float64, device=dev)
@@ -484,9 +507,10 @@ def main() -> None:
                               f"(rank r traces bands (r+f) mod {world} of frame f), {gather_kind} gather + rank-0 "
                               f"assembly{shared}"
                               if frames_mode else
-                              f"one frame per step in {world} contiguous {band_h}-row blocks, rank r tracing block "
-                              f"(r + k) mod {world} of frame k, {D} frames in flight per rank, {gather_kind} "
-                              f"sends / receives of every {G} frames straight into rank 0's frames{shared}"
+                              f"one frame per step in {world} contiguous row pieces (rows per rank "
+                              f"{block_sizes(H, world, share)}, root_share {share}) laid out in an order rotated "
+                              f"every frame, {D} frames in flight per rank, {gather_kind} sends / receives of every "
+                              f"{G} frames straight into rank 0's frames{shared}"
                               if blocks_mode else
                               f"one frame per step, interleaved {band_h}-row bands over {world} ranks, "
                               f"{D} frames in flight per rank, {gather_kind} gather of every {G} frames + rank-0 "

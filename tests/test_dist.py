@@ -171,14 +171,14 @@ def test_bands_steps_gathered_in_one_batch(world, band_h):
         assert np.array_equal(got[f], ref), f
 
 
-def _blocks_worker(rank, world, port, q, first_frame):
+def _blocks_worker(rank, world, port, q, first_frame, share):
     import sys
     sys.path[:0] = [os.path.join(ROOT, "3d-ray-tracer-vulkan_amd"), ROOT]
     import torch
     import torch.distributed as dist
     from oracle import oracle_lib
-    from rtamd import configs, lib
-    from rtamd.dist import block_height, block_offset, block_range, exchange_blocks
+    from rtamd import configs
+    from rtamd.dist import block_layout, block_sizes, exchange_blocks
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
@@ -186,43 +186,44 @@ def _blocks_worker(rank, world, port, q, first_frame):
         built = cfg.build()
         W, H, B = 96, 53, 3
         ids = list(range(first_frame, first_frame + 4))           # one batch of 4 consecutive steps
-        bh = block_height(H, world)
+        bh = max(block_sizes(H, world, share))
         local = torch.zeros((len(ids), bh, W, 4), dtype=torch.uint8)
         frames = torch.zeros((len(ids), H, W, 4), dtype=torch.uint8) if rank == 0 else None
         traced = []
         for i, f in enumerate(ids):
             cam = configs.Camera((-25.0 + 5 * f, 30.0, 140.0), (0.0, 0.0, 0.0), (0.0, 1.0, 0.0), 20.0, W / H)
-            b = block_offset(f, world, rank)
-            y0, y1 = block_range(H, world, b)
-            # the kernels' packing of the one band of this rank is the block's rows in order
-            assert lib().rt_band_rows(H, bh, world, b) == y1 - y0
+            lay = block_layout(H, world, f, share)
+            assert sorted(lay) == [(a, b) for a, b in zip([0] + [y for _, y in sorted(lay)][:-1],
+                                                          [y for _, y in sorted(lay)])]   # tiles the frame
+            y0, y1 = lay[rank]
             if y1 > y0:
                 rgba, _, _ = oracle_lib.render(built.model_vertex_data, built.model_material_data,
                                                built.flat_bvh_data, cam.ubo_bytes(), W, H, B,
                                                tile=(0, y0, W, y1 - y0), n_threads=1)
                 (frames[i, y0:y1] if rank == 0 else local[i, : y1 - y0]).copy_(torch.from_numpy(rgba))
-            traced.append(b)
+            traced.append(y0)
         q.put(("traced", rank, traced))
-        exchange_blocks(frames, local, ids, H)
+        exchange_blocks(frames, local, ids, H, share)
         if rank == 0:
             q.put(("frames", frames.numpy()))
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,first", [(2, 0), (3, 5), (4, 2)])
-def test_blocks_exchange_assembles_frames(world, first):
-    """Rotating row blocks (bench.py's N > 1 default): in frame k rank r
-    traces block (r + k) mod N; rank 0 traces its block in place and receives
-    every other rank's block straight into the frame (one batch of
-    point-to-point receives).  53 rows over 3 / 4 ranks leaves a short last
-    block.  Every frame of the batch equals the oracle's frame."""
+@pytest.mark.parametrize("world,first,share", [(2, 0, 1.0), (3, 5, 1.0), (4, 2, 0.6), (3, 1, 0.0)])
+def test_blocks_exchange_assembles_frames(world, first, share):
+    """Rotating row pieces (bench.py's N > 1 default): frame k lays the ranks'
+    pieces out in the rotated order k, k+1, ...; rank 0 traces its piece (of
+    root_share x H / N rows, 0 to a full share) in place and receives every
+    other rank's piece straight into the frame (one batch of point-to-point
+    receives).  53 rows over 3 / 4 ranks leaves unequal pieces.  Every frame of
+    the batch equals the oracle's frame."""
     from oracle import oracle_lib
     from rtamd import configs
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_blocks_worker, args=(r, world, port, q, first)) for r in range(world)]
+    procs = [ctx.Process(target=_blocks_worker, args=(r, world, port, q, first, share)) for r in range(world)]
     for p in procs:
         p.start()
     got, traced = None, {}
@@ -235,8 +236,8 @@ def test_blocks_exchange_assembles_frames(world, first):
     for p in procs:
         p.join(60)
         assert p.exitcode == 0
-    for i in range(4):                                    # each frame's blocks: one per rank, all different
-        assert sorted(traced[r][i] for r in range(world)) == list(range(world))
+    for i in range(4):                                    # each frame's pieces start at different rows
+        assert len({traced[r][i] for r in range(world)}) == world or share == 0.0
     built = configs.config2().build()
     W, H, B = 96, 53, 3
     for i, f in enumerate(range(first, first + 4)):

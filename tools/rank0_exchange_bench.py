@@ -10,10 +10,12 @@ that on one GPU: rank 0's share of each frame, and per batch an RCCL gather
 (world size 1, so a device copy) of the volume rank 0 receives at N (N x G
 packed shares) followed by the assembly of the G frames, with bench.py's
 ring of 2G slots and its waits.  Partition blocks (bench.py's default):
-rank 0 traces block k mod N of frame k in place, and the receive of the
-other N - 1 blocks of each frame is emulated by device copies into the
-frame's rows on the exchange stream (an RCCL receive is a copy kernel from
-its staging buffer into the destination).  The other ranks' rows are
+rank 0 traces its piece of frame k (rtamd.dist.block_layout, root_share) in
+place, and the receive of the other N - 1 pieces of the batch's frames is
+emulated by one RCCL gather at world size 1 of that volume, with no assembly
+(an RCCL receive is a copy kernel from its staging buffer into the
+destination).  --rank r > 0 (blocks only) emulates a sending rank instead: its
+piece, and a copy of the volume it sends.  The other ranks' rows are
 whatever the buffers hold: the frames are not checked.  Reports ms per frame with and
 without the exchange, and with the exchange streams at normal or high
 priority (bench.py --exchange-priority).
@@ -48,15 +50,16 @@ def main():
     ap.add_argument("--ranks", default="2,4,8")
     ap.add_argument("--frames", type=int, default=240)
     ap.add_argument("--band", type=int, default=16)
-    ap.add_argument("--arms", default="bands:0:0,bands:1:1,blocks:0:0,blocks:1:0,blocks:1:1",
-                    help="partition:exchange:priority triples")
+    ap.add_argument("--arms", default="bands:0:0,bands:1:1,blocks:0:0,blocks:1:1",
+                    help="partition:exchange:priority[:root_share] (root_share: blocks only, default 1)")
+    ap.add_argument("--rank", type=int, default=0, help="blocks: the rank emulated (0 receives, others send)")
     args = ap.parse_args()
     import torch
     import torch.distributed as dist
     import rtamd
     from rtamd import configs
     from rtamd._lib import check
-    from rtamd.dist import BatchPlan
+    from rtamd.dist import BatchPlan, block_layout, block_sizes
 
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
@@ -67,9 +70,10 @@ def main():
     r = rtamd.Renderer((0,))
     r.upload_scene(built)
     L = rtamd.lib()
-    arms = [(a.split(":")[0], int(a.split(":")[1]), int(a.split(":")[2])) for a in args.arms.split(",")]
+    arms = [(a.split(":")[0], int(a.split(":")[1]), int(a.split(":")[2]),
+             float(a.split(":")[3]) if len(a.split(":")) > 3 else 1.0) for a in args.arms.split(",")]
     pgs = {}
-    for prio in sorted({p for _, _, p in arms}):
+    for prio in sorted({a[2] for a in arms}):
         from torch.distributed import ProcessGroupNCCL
         opts = ProcessGroupNCCL.Options()
         opts.is_high_priority_stream = bool(prio)
@@ -89,12 +93,16 @@ def main():
         # per half: [N * G, max_rows, W, 4]; rank 0's frame f of the batch is block f
         slots = torch.zeros((2, N * G, plan.max_rows, W, 4), dtype=torch.uint8, device=dev)
         streams = [torch.cuda.Stream(dev) for _ in range(D)]
-        bh = -(-H // N)
         fring = torch.zeros((2 * G, H, W, 4), dtype=torch.uint8, device=dev)
-        other = torch.zeros((H, W, 4), dtype=torch.uint8, device=dev)     # the other ranks' blocks
-        for mode, exch, prio in arms:
+        for mode, exch, prio, share in arms:
             main_s = torch.cuda.Stream(dev, priority=-1 if prio else 0)
             gathered = [None, None]
+            sizes = block_sizes(H, N, share)
+            me = args.rank if mode == "blocks" else 0
+            # rows this rank moves per frame: rank 0 receives every other piece, a sender sends its own
+            moved = (H - sizes[0]) if me == 0 else sizes[me]
+            other = torch.zeros((G, max(1, moved), W, 4), dtype=torch.uint8, device=dev)
+            landing = torch.empty_like(other)
 
             def trace(k):
                 s = streams[k % D]
@@ -103,12 +111,11 @@ def main():
                     for t in streams:
                         t.wait_event(gathered[half])
                 if mode == "blocks":
-                    b = k % N
-                    y0 = min(H, b * bh)
-                    y1 = min(H, y0 + bh)
-                    check(L.rt_render_bands_device(r._ctx, C.byref(cam.ubo), W, H, B, bh, N, b,
-                                                   fring[k % (2 * G), y0:y1].data_ptr(), None, s.cuda_stream,
-                                                   None))
+                    y0, y1 = block_layout(H, N, k, share)[me]
+                    if y1 > y0:
+                        check(L.rt_render_tile_device(r._ctx, C.byref(cam.ubo), W, H, B, 0, y0, W, y1 - y0,
+                                                      fring[k % (2 * G), y0:y1].data_ptr(), None, s.cuda_stream,
+                                                      None))
                 else:
                     check(L.rt_render_bands_device(r._ctx, C.byref(cam.ubo), W, H, B, args.band, N, 0,
                                                    slots[half, k % G, :rows].data_ptr(), None, s.cuda_stream,
@@ -118,11 +125,8 @@ def main():
                         main_s.wait_stream(t)
                     with torch.cuda.stream(main_s):
                         if mode == "blocks":
-                            for j in range(k - G + 1, k + 1):
-                                for q in range(1, N):
-                                    bq = (q + j) % N
-                                    z0, z1 = min(H, bq * bh), min(H, bq * bh + bh)
-                                    fring[j % (2 * G), z0:z1].copy_(other[z0:z1])
+                            if N > 1 and moved > 0:
+                                dist.gather(other, [landing], dst=0, group=pgs[prio])
                         else:
                             stack = torch.empty_like(slots[half])
                             dist.gather(slots[half], [stack], dst=0, group=pgs[prio])
@@ -143,7 +147,8 @@ def main():
                 main_s.wait_stream(t)
             torch.cuda.synchronize()
             dt = time.perf_counter() - t0
-            print(json.dumps({"config": args.config, "N": N, "inflight": D, "partition": mode, "exchange": exch,
+            print(json.dumps({"config": args.config, "N": N, "inflight": D, "partition": mode, "rank": me,
+                              "root_share": share if mode == "blocks" else None, "exchange": exch,
                               "exchange_priority": prio, "frames": n,
                               "ms_per_frame": round(dt * 1e3 / n, 4),
                               "gather_MB_per_batch": round(N * G * plan.max_rows * W * 4 / 1e6, 1)}), flush=True)
