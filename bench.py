@@ -122,6 +122,9 @@ def main() -> None:
     ap.add_argument("--set", default="", help="schedule options name=value,... (rt_set_option) before timing")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-single", action="store_true", help="N > 1: skip rank 0's one-GPU timing")
+    ap.add_argument("--ring", type=int, default=4,
+                    help="N > 1 (blocks, bands): batches of frame slots in the ring (>= 2); the traces of a batch "
+                         "wait for the exchange of the batch that used its slots, ring - 1 batches back")
     ap.add_argument("--root-share", type=float, default=-1.0,
                     help="blocks: rank 0's piece in units of H / N rows (it also receives every other piece); "
                          "-1 = default_root_share(N)")
@@ -216,18 +219,24 @@ def main() -> None:
     # once (option concurrent_launches): a frame batch's F launches, or the D
     # frames in flight.
     renderer.set_option("concurrent_launches", F * D)
-    # Exchange (N > 1, bands): every G = D steps the G frames traced since the
-    # last exchange are gathered to rank 0 by one collective and assembled by
-    # one index_select (dist.gather_frames), so the host cost of the exchange
-    # is paid once per G frames.  2G frame slots: one batch is traced while the
-    # previous one is gathered; a slot is retraced only after the gather that
-    # read it.  N = 1: one slot per stream.  frames partition: one gather per
-    # step of F frames, D + 1 buffers.
+    # Exchange (N > 1, blocks / bands): every G = D steps the G frames traced
+    # since the last exchange go to rank 0 in one RCCL group (blocks: sends /
+    # receives straight into rank 0's frames; bands: one gather and one
+    # index_select, dist.gather_frames), so the host cost of the exchange is
+    # paid once per G frames.  R x G frame slots: batches are traced while
+    # earlier ones are exchanged; a slot is retraced only after the exchange
+    # that used it.  N = 1: one slot per stream.  frames partition: one gather
+    # per step of F frames, D + 1 buffers.
     G = D if (dist_on and not frames_mode) else 1
+    # R batches of slots in the ring: a batch's slots are retraced only after
+    # the exchange R - 1 batches back has finished.  The exchange kernels get
+    # workgroup slots only as trace waves end, so a deep ring keeps a late
+    # exchange from stalling the traces.
+    R = max(2, args.ring)
     if frames_mode:
         n_slots = D + 1
     elif dist_on:
-        n_slots = 2 * G
+        n_slots = R * G
     else:
         n_slots = D
     d_bufs = [torch.empty((F, max_rows, W, 4), dtype=torch.uint8, device=dev) for _ in range(n_slots)] \
@@ -236,7 +245,7 @@ def main() -> None:
     # blocks: rank 0 traces its block of frame k in place in fring[k mod n_slots]
     # and receives the other blocks there
     fring = torch.empty((n_slots, H, W, 4), dtype=torch.uint8, device=dev) if (blocks_mode and rank == 0) else None
-    gathered = [None] * (n_slots if frames_mode else 2)   # event: the last gather that read a buffer / half
+    gathered = [None] * (n_slots if frames_mode else R)   # event: the last exchange that used a buffer / batch slot
     # One stream per launch in flight (launches and their events on the same
     # queue); the gathers run on main_stream.
     streams = [torch.cuda.Stream(dev) for _ in range(min(F * D, 12))]
@@ -275,7 +284,7 @@ def main() -> None:
         n = k % G if k % G else (G if k else 0)
         if n == 0:
             return None
-        half = ((k - 1) // G) % 2
+        half = ((k - 1) // G) % R
         for s in streams:
             main_stream.wait_stream(s)
         if blocks_mode:         # RCCL sends / receives straight into rank 0's frames
@@ -311,7 +320,7 @@ def main() -> None:
             return
         s = streams[k % len(streams)]
         if blocks_mode:
-            half = (k // G) % 2
+            half = (k // G) % R
             if k % G == 0 and gathered[half] is not None:
                 for t in streams:                      # the exchange that last used this half is done
                     t.wait_event(gathered[half])
@@ -321,7 +330,7 @@ def main() -> None:
             if k % G == G - 1:
                 flush()
         elif dist_on:
-            half = (k // G) % 2
+            half = (k // G) % R
             if k % G == 0 and gathered[half] is not None:
                 for t in streams:                      # the gather that last read this half is done
                     t.wait_event(gathered[half])

@@ -52,6 +52,7 @@ def main():
     ap.add_argument("--band", type=int, default=16)
     ap.add_argument("--arms", default="bands:0:0,bands:1:1,blocks:0:0,blocks:1:1",
                     help="partition:exchange:priority[:root_share] (root_share: blocks only, default 1)")
+    ap.add_argument("--ring", type=int, default=2, help="batches of slots in the ring (bench.py --ring)")
     ap.add_argument("--rank", type=int, default=0, help="blocks: the rank emulated (0 receives, others send)")
     args = ap.parse_args()
     import torch
@@ -91,12 +92,13 @@ def main():
         src = torch.as_tensor(plan.src, device=dev)
         rows = L.rt_band_rows(H, args.band, N, 0)
         # per half: [N * G, max_rows, W, 4]; rank 0's frame f of the batch is block f
-        slots = torch.zeros((2, N * G, plan.max_rows, W, 4), dtype=torch.uint8, device=dev)
+        R = args.ring
+        slots = torch.zeros((R, N * G, plan.max_rows, W, 4), dtype=torch.uint8, device=dev)
         streams = [torch.cuda.Stream(dev) for _ in range(D)]
-        fring = torch.zeros((2 * G, H, W, 4), dtype=torch.uint8, device=dev)
+        fring = torch.zeros((R * G, H, W, 4), dtype=torch.uint8, device=dev)
         for mode, exch, prio, share in arms:
             main_s = torch.cuda.Stream(dev, priority=-1 if prio else 0)
-            gathered = [None, None]
+            gathered = [None] * R
             sizes = block_sizes(H, N, share)
             me = args.rank if mode == "blocks" else 0
             # rows this rank moves per frame: rank 0 receives every other piece, a sender sends its own
@@ -106,7 +108,7 @@ def main():
 
             def trace(k):
                 s = streams[k % D]
-                half = (k // G) % 2
+                half = (k // G) % R
                 if k % G == 0 and gathered[half] is not None:
                     for t in streams:
                         t.wait_event(gathered[half])
@@ -114,7 +116,7 @@ def main():
                     y0, y1 = block_layout(H, N, k, share)[me]
                     if y1 > y0:
                         check(L.rt_render_tile_device(r._ctx, C.byref(cam.ubo), W, H, B, 0, y0, W, y1 - y0,
-                                                      fring[k % (2 * G), y0:y1].data_ptr(), None, s.cuda_stream,
+                                                      fring[k % (R * G), y0:y1].data_ptr(), None, s.cuda_stream,
                                                       None))
                 else:
                     check(L.rt_render_bands_device(r._ctx, C.byref(cam.ubo), W, H, B, args.band, N, 0,
@@ -136,7 +138,7 @@ def main():
                     ev.record(main_s)
                     gathered[half] = ev
 
-            for k in range(2 * G + 1):                 # learns this share's order; fills the ring
+            for k in range(R * G + 1):                 # learns this share's order; fills the ring
                 trace(k)
             torch.cuda.synchronize()
             n = (args.frames // G) * G
@@ -147,7 +149,7 @@ def main():
                 main_s.wait_stream(t)
             torch.cuda.synchronize()
             dt = time.perf_counter() - t0
-            print(json.dumps({"config": args.config, "N": N, "inflight": D, "partition": mode, "rank": me,
+            print(json.dumps({"config": args.config, "N": N, "inflight": D, "ring": R, "partition": mode, "rank": me,
                               "root_share": share if mode == "blocks" else None, "exchange": exch,
                               "exchange_priority": prio, "frames": n,
                               "ms_per_frame": round(dt * 1e3 / n, 4),
