@@ -105,11 +105,12 @@ def main() -> None:
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", type=int, default=3, help="BASELINE config index (3 = headline)")
     ap.add_argument("--band", type=int, default=16, help="band height for N > 1")
-    ap.add_argument("--partition", choices=("blocks", "bands", "frames"), default="blocks",
-                    help="N > 1: blocks = one frame per step in N contiguous row blocks, rank r tracing block "
-                         "(r + k) mod N of frame k, received by rank 0 straight into the frame (strong scaling, "
-                         "default); bands = one frame per step in interleaved --band-row bands, gathered and "
-                         "assembled on rank 0 (strong); frames = N frames per step, bands rotated over ranks (weak)")
+    ap.add_argument("--partition", choices=("bands", "blocks", "frames"), default="bands",
+                    help="N > 1: bands = one frame per step in interleaved --band-row bands, gathered and "
+                         "assembled on rank 0 (strong scaling, default); blocks = one frame per step in N "
+                         "contiguous row pieces laid out in an order rotated every frame, received by rank 0 "
+                         "straight into the frame (strong; emulated slower on the sending ranks, "
+                         "profiles/r02/rccl/README.md); frames = N frames per step, bands rotated over ranks (weak)")
     ap.add_argument("--inflight", type=int, default=0,
                     help="frames in flight per rank (bands partition): each step's trace goes on the next of this "
                          "many streams, so frames overlap each other's serial tails and the gathers "
@@ -122,7 +123,7 @@ def main() -> None:
     ap.add_argument("--set", default="", help="schedule options name=value,... (rt_set_option) before timing")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-single", action="store_true", help="N > 1: skip rank 0's one-GPU timing")
-    ap.add_argument("--ring", type=int, default=4,
+    ap.add_argument("--ring", type=int, default=2,
                     help="N > 1 (blocks, bands): batches of frame slots in the ring (>= 2); the traces of a batch "
                          "wait for the exchange of the batch that used its slots, ring - 1 batches back")
     ap.add_argument("--root-share", type=float, default=-1.0,
