@@ -51,6 +51,7 @@ constexpr int kShadeStride = 2;
 constexpr int kTopBits = RT_TOP_BITS;            // walk 13: slot+1 field width (10: 32 KB of LDS, 11: 64 KB)
 constexpr int kTopSlots = (1 << kTopBits) - 1;   // top-tree slots
 constexpr int kWalkTop = 13;      // option walk: walk 2 with the top tree's records in LDS
+constexpr int kWalkScalar = 5;    // option walk: walk 2 with scalar loads on wave-uniform steps
 
 struct DevScene {
     int      n_nodes = 0;     // nodes in the compact array

@@ -151,6 +151,16 @@ __device__ __forceinline__ bool tri_test(float4 P0, float4 P1, float4 P2, V3 o, 
 // the compiler from sinking a load into the branch that uses it (which would
 // turn one memory round trip into two dependent ones).
 __device__ __forceinline__ void pin(float4& q) { asm volatile("" : "+v"(q.x), "+v"(q.y), "+v"(q.z), "+v"(q.w)); }
+
+// walk 5: a read-only scene array seen through the constant address space, so
+// that a load at a wave-uniform index is a scalar load (scalar cache), which
+// costs the vector memory pipeline nothing
+typedef float v4f __attribute__((ext_vector_type(4)));
+typedef const v4f __attribute__((address_space(4)))* ConstF4;
+__device__ __forceinline__ float4 ld_const(const float4* p, int i) {
+    const v4f v = ((ConstF4)(uintptr_t)p)[i];
+    return make_float4(v.x, v.y, v.z, v.w);
+}
 __device__ __forceinline__ void pin(uint2& q) { asm volatile("" : "+v"(q.x), "+v"(q.y)); }
 
 // One node of the walk.  `leaf` says whether node i is a leaf (from its
@@ -835,7 +845,7 @@ void trace_simple(TraceArgs a) {
             ++c_seg;
             if (end > 0) ++c_node;                                       // the root visit
         }
-        if (WALK == 0 || WALK == 2 || WALK == kWalkTop) {
+        if (WALK == 0 || WALK == 2 || WALK == kWalkScalar || WALK == kWalkTop) {
             // The per-node walk: one dependent load per visit, lanes in lockstep.
             // walk 2, software-pipelined: the next node's box is requested as soon as
             // this node's slab test has chosen it, before this node's triangle
@@ -848,7 +858,7 @@ void trace_simple(TraceArgs a) {
             float4 A, B, Q0, Q1;
             const float4* __restrict__ nodes2 = WALK == kWalkTop ? a.scene.nodes3 : a.scene.nodes2;
             const float4* __restrict__ leafs2 = a.scene.leafs2;
-            if ((WALK == 2 || WALK == kWalkTop) && walking) {
+            if ((WALK == 2 || WALK == kWalkScalar || WALK == kWalkTop) && walking) {
                 if (WALK == kWalkTop && !nleaf && a.scene.n_top > 0) {   // an internal root is slot 0
                     A = topl[0];
                     B = topl[1];
@@ -881,6 +891,8 @@ void trace_simple(TraceArgs a) {
                     const int nxt = (hb || nleaf) ? n + 1 : (int)(aw & kIdx);
                     const bool nl = (((hb && !nleaf) ? bw : (aw >> 31)) & 1u) != 0u;
                     const float v0x = B.w;                                   // a leaf's v0.x
+                    int u = 0;                                               // walk 5: the uniform next node
+                    bool uni = false;
                     if (COUNT && hb && !nleaf) c_node += 2;
                     if (WALK == kWalkTop) {
                         // the next node's top-tree slot (-1: not in it): a leaf's
@@ -898,6 +910,19 @@ void trace_simple(TraceArgs a) {
                             A = nodes2[2 * nxt];
                             B = nodes2[2 * nxt + 1];
                         }
+                    } else if (WALK == kWalkScalar) {
+                        // walk 5: when every walking lane moves to one node (~9
+                        // steps in 10), its records come through the scalar cache;
+                        // the vector memory pipeline bounds the lockstep walk (§7)
+                        u = __builtin_amdgcn_readfirstlane(nxt);
+                        uni = __ballot(nxt != u) == 0;
+                        if (uni) {
+                            A = ld_const(nodes2, 2 * u);                     // index end is padding
+                            B = ld_const(nodes2, 2 * u + 1);
+                        } else {
+                            A = nodes2[2 * nxt];
+                            B = nodes2[2 * nxt + 1];
+                        }
                     } else {
                         A = nodes2[2 * nxt];                                 // index end is padding
                         B = nodes2[2 * nxt + 1];
@@ -911,7 +936,13 @@ void trace_simple(TraceArgs a) {
                             hit = (int)(aw & (WALK == kWalkTop ? 0xFFFFFu : kTri));
                         }
                     }
-                    if (nl && nxt < end) {
+                    if (WALK == kWalkScalar && uni) {
+                        // the leaf bit belongs to node u: the same in every lane
+                        if (__builtin_amdgcn_readfirstlane(nl ? 1 : 0) && u < end) {
+                            Q0 = ld_const(leafs2, 2 * u + 0);
+                            Q1 = ld_const(leafs2, 2 * u + 1);
+                        }
+                    } else if (nl && nxt < end) {
                         Q0 = leafs2[2 * nxt + 0];
                         Q1 = leafs2[2 * nxt + 1];
                     }
@@ -1523,6 +1554,12 @@ hipError_t launch_trace(const TraceArgs& a, hipStream_t stream) {
                 const dim3 gf(a.n_heavy_px + n_tiles);
                 const size_t shm = kFCap * sizeof(uint4);
                 constexpr int FF = kFeatCoopTail | kFeatFused;
+                if (a.walk == kWalkScalar) {
+                    if (a.diag) hipLaunchKernelGGL((trace_simple<false, true, FF, kWalkScalar>), gf, block, shm, stream, ao);
+                    else if (a.counters) hipLaunchKernelGGL((trace_simple<true, false, FF, kWalkScalar>), gf, block, shm, stream, ao);
+                    else hipLaunchKernelGGL((trace_simple<false, false, FF, kWalkScalar>), gf, block, shm, stream, ao);
+                    return hipGetLastError();
+                }
                 if (a.diag) hipLaunchKernelGGL((trace_simple<false, true, FF, 2>), gf, block, shm, stream, ao);
                 else if (a.counters) hipLaunchKernelGGL((trace_simple<true, false, FF, 2>), gf, block, shm, stream, ao);
                 else hipLaunchKernelGGL((trace_simple<false, false, FF, 2>), gf, block, shm, stream, ao);
@@ -1589,6 +1626,13 @@ hipError_t launch_trace(const TraceArgs& a, hipStream_t stream) {
                 case kFeatCoopTail: RT_SIMPLE(kFeatCoopTail, kWalkTop) break;
                 case 0: RT_SIMPLE(0, kWalkTop) break;
                 case kFeatCoopTail | kFeatExt: RT_SIMPLE(kFeatCoopTail | kFeatExt, kWalkTop) break;
+                default: return hipErrorInvalidValue;
+            }
+        } else if (a.walk == kWalkScalar) {
+            switch (feat) {
+                case kFeatCoopTail: RT_SIMPLE(kFeatCoopTail, kWalkScalar) break;
+                case 0: RT_SIMPLE(0, kWalkScalar) break;
+                case kFeatCoopTail | kFeatExt: RT_SIMPLE(kFeatCoopTail | kFeatExt, kWalkScalar) break;
                 default: return hipErrorInvalidValue;
             }
         } else if (a.walk == 2) {

@@ -154,6 +154,10 @@ def test_config5_1m_row_subset(renderer):
     {"kernel": 0, "walk": 13, "coop_lanes": 0},
     {"kernel": 0, "walk": 13, "heavy_first": 0},
     {"kernel": 0, "walk": 13, "wave_tile": 2, "coop_lanes": 4},
+    {"kernel": 0, "walk": 5},
+    {"kernel": 0, "walk": 5, "coop_lanes": 0},
+    {"kernel": 0, "walk": 5, "heavy_first": 0},
+    {"kernel": 0, "walk": 5, "wave_tile": 3, "coop_lanes": 8},
 ])
 def test_schedules_identical(renderer, opts):
     """Every schedule gives the oracle's frame and counters (config 2 at the
@@ -277,8 +281,8 @@ def test_heavy_pixels(renderer, cfg_k, factor):
             renderer.set_option(k, v)
 
 
-@pytest.mark.parametrize("cfg_k", [3, 4, 5])
-def test_bench_setting_whole_frame(renderer, cfg_k):
+@pytest.mark.parametrize("cfg_k,walk", [(3, 2), (4, 2), (5, 2), (3, 5), (5, 5)])
+def test_bench_setting_whole_frame(renderer, cfg_k, walk):
     """BASELINE configs 3, 4 and 5 as whole frames (config 5: 1M triangles,
     3840x2160, 8 bounces) under bench.py's N = 1 setting: the default
     schedule with 4 launches in flight counted by the heavy-pixel bar
@@ -288,6 +292,7 @@ def test_bench_setting_whole_frame(renderer, cfg_k):
     from rtamd import configs
     try:
         renderer.set_option("concurrent_launches", 4)
+        renderer.set_option("walk", walk)
         cfg = configs.get(cfg_k)
         built = cfg.build()
         cam = cfg.camera()
@@ -584,7 +589,7 @@ def test_golden_frames_on_gpu(renderer):
 
 
 @pytest.mark.parametrize("shape,n", [("left", 50), ("right", 200), ("random", 300)])
-@pytest.mark.parametrize("walk", [0, 1, 2, 13, "frontier"])
+@pytest.mark.parametrize("walk", [0, 1, 2, 5, 13, "frontier"])
 def test_unbalanced_bvh(renderer, shape, n, walk):
     from rtamd import configs
     built = raw_bvh_scene(n, shape, seed=n)
