@@ -52,6 +52,7 @@ constexpr int kTopBits = RT_TOP_BITS;            // walk 13: slot+1 field width 
 constexpr int kTopSlots = (1 << kTopBits) - 1;   // top-tree slots
 constexpr int kWalkTop = 13;      // option walk: walk 2 with the top tree's records in LDS
 constexpr int kWalkScalar = 5;    // option walk: walk 2 with scalar loads on wave-uniform steps
+constexpr int kWalkDma = 14;      // option walk: walk 2 with LDS-DMA record fetches on wave-uniform steps
 
 struct DevScene {
     int      n_nodes = 0;     // nodes in the compact array

@@ -1384,7 +1384,7 @@ int rt_set_option(rt_ctx* ctx, const char* name, int64_t value) {
     } else if (std::strcmp(name, "extensions") == 0 && value >= 0 && value <= 15) {
         ctx->ext = (int)value;
     } else if (std::strcmp(name, "walk") == 0 && ((value >= 0 && value <= 2) || value == kWalkScalar ||
-                                                  value == kWalkTop)) {
+                                                  value == kWalkDma || value == kWalkTop)) {
         ctx->walk = (int)value;
     } else if (std::strcmp(name, "coop_walk") == 0 && (value == 0 || value == 1)) {
         ctx->coop_walk = (int)value;

@@ -716,6 +716,9 @@ void trace_simple(TraceArgs a) {
     // of block_waves (8 or 16) waves, read by every walking lane whose next
     // node is in it instead of a global load
     __shared__ float4 topl[WALK == kWalkTop ? 2 * kTopSlots : 1];
+    // walk 14: the stage a uniform step's LDS-DMA fetch lands in (one float4
+    // per lane: global_load_lds writes base + lane x 16; one-wave workgroups)
+    __shared__ float4 dstage[WALK == kWalkDma ? 64 : 1];
     if (WALK == kWalkTop) {
         const int nt2 = 2 * a.scene.n_top;
         for (int i = threadIdx.x; i < nt2; i += blockDim.x) topl[i] = a.scene.top[i];
@@ -845,7 +848,7 @@ void trace_simple(TraceArgs a) {
             ++c_seg;
             if (end > 0) ++c_node;                                       // the root visit
         }
-        if (WALK == 0 || WALK == 2 || WALK == kWalkScalar || WALK == kWalkTop) {
+        if (WALK == 0 || WALK == 2 || WALK == kWalkScalar || WALK == kWalkDma || WALK == kWalkTop) {
             // The per-node walk: one dependent load per visit, lanes in lockstep.
             // walk 2, software-pipelined: the next node's box is requested as soon as
             // this node's slab test has chosen it, before this node's triangle
@@ -858,7 +861,7 @@ void trace_simple(TraceArgs a) {
             float4 A, B, Q0, Q1;
             const float4* __restrict__ nodes2 = WALK == kWalkTop ? a.scene.nodes3 : a.scene.nodes2;
             const float4* __restrict__ leafs2 = a.scene.leafs2;
-            if ((WALK == 2 || WALK == kWalkScalar || WALK == kWalkTop) && walking) {
+            if ((WALK == 2 || WALK == kWalkScalar || WALK == kWalkDma || WALK == kWalkTop) && walking) {
                 if (WALK == kWalkTop && !nleaf && a.scene.n_top > 0) {   // an internal root is slot 0
                     A = topl[0];
                     B = topl[1];
@@ -893,6 +896,8 @@ void trace_simple(TraceArgs a) {
                     const float v0x = B.w;                                   // a leaf's v0.x
                     int u = 0;                                               // walk 5: the uniform next node
                     bool uni = false;
+                    bool staged = false;                                     // walk 14: records in dstage
+                    int l0 = 0, l1 = 0, l2 = 0, l3 = 0;                      // walk 14: lanes holding them
                     if (COUNT && hb && !nleaf) c_node += 2;
                     if (WALK == kWalkTop) {
                         // the next node's top-tree slot (-1: not in it): a leaf's
@@ -906,6 +911,40 @@ void trace_simple(TraceArgs a) {
                             B = topl[2 * ts + 1];
                             pin(A);
                             pin(B);
+                        } else {
+                            A = nodes2[2 * nxt];
+                            B = nodes2[2 * nxt + 1];
+                        }
+                    } else if (WALK == kWalkDma) {
+                        // walk 14: when every walking lane moves to one node, the
+                        // first 2 (4 with its leaf) walking lanes fetch its records
+                        // straight into LDS, one float4 each, in ONE instruction
+                        // (global_load_lds_dwordx4: ~20 cycles of the vector memory
+                        // pipeline against ~36 for two dwordx4 in every lane,
+                        // tools/ubench/lds_dma_cost.hip); the wave reads them back
+                        // after this node's triangle test
+                        u = __builtin_amdgcn_readfirstlane(nxt);
+                        const uint64_t act = __ballot(true);
+                        const bool nlu = __builtin_amdgcn_readfirstlane(nl ? 1 : 0) != 0 && u < end;
+                        const int need = nlu ? 4 : 2;
+                        staged = __ballot(nxt != u) == 0 && __popcll(act) >= need;
+                        if (staged) {
+                            const int rank = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(act >> 32),
+                                                                            __builtin_amdgcn_mbcnt_lo((uint32_t)act, 0u));
+                            if (rank < need) {
+                                const float4* src = rank < 2 ? nodes2 + 2 * u + rank : leafs2 + 2 * u + (rank - 2);
+                                __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(src),
+                                                                 (__attribute__((address_space(3))) void*)(dstage),
+                                                                 16, 0, 0);
+                            }
+                            uint64_t m = act;
+                            l0 = __builtin_ctzll(m);
+                            m &= m - 1;
+                            l1 = __builtin_ctzll(m);
+                            m &= m - 1;
+                            l2 = nlu ? __builtin_ctzll(m) : 0;
+                            m &= m - 1;
+                            l3 = nlu ? __builtin_ctzll(m) : 0;
                         } else {
                             A = nodes2[2 * nxt];
                             B = nodes2[2 * nxt + 1];
@@ -936,7 +975,15 @@ void trace_simple(TraceArgs a) {
                             hit = (int)(aw & (WALK == kWalkTop ? 0xFFFFFu : kTri));
                         }
                     }
-                    if (WALK == kWalkScalar && uni) {
+                    if (WALK == kWalkDma && staged) {
+                        __builtin_amdgcn_s_waitcnt(0);                       // the LDS-DMA fetch has landed
+                        A = dstage[l0];
+                        B = dstage[l1];
+                        if (nl && nxt < end) {
+                            Q0 = dstage[l2];
+                            Q1 = dstage[l3];
+                        }
+                    } else if (WALK == kWalkScalar && uni) {
                         // the leaf bit belongs to node u: the same in every lane
                         if (__builtin_amdgcn_readfirstlane(nl ? 1 : 0) && u < end) {
                             Q0 = ld_const(leafs2, 2 * u + 0);
@@ -1560,6 +1607,12 @@ hipError_t launch_trace(const TraceArgs& a, hipStream_t stream) {
                     else hipLaunchKernelGGL((trace_simple<false, false, FF, kWalkScalar>), gf, block, shm, stream, ao);
                     return hipGetLastError();
                 }
+                if (a.walk == kWalkDma) {
+                    if (a.diag) hipLaunchKernelGGL((trace_simple<false, true, FF, kWalkDma>), gf, block, shm, stream, ao);
+                    else if (a.counters) hipLaunchKernelGGL((trace_simple<true, false, FF, kWalkDma>), gf, block, shm, stream, ao);
+                    else hipLaunchKernelGGL((trace_simple<false, false, FF, kWalkDma>), gf, block, shm, stream, ao);
+                    return hipGetLastError();
+                }
                 if (a.diag) hipLaunchKernelGGL((trace_simple<false, true, FF, 2>), gf, block, shm, stream, ao);
                 else if (a.counters) hipLaunchKernelGGL((trace_simple<true, false, FF, 2>), gf, block, shm, stream, ao);
                 else hipLaunchKernelGGL((trace_simple<false, false, FF, 2>), gf, block, shm, stream, ao);
@@ -1626,6 +1679,14 @@ hipError_t launch_trace(const TraceArgs& a, hipStream_t stream) {
                 case kFeatCoopTail: RT_SIMPLE(kFeatCoopTail, kWalkTop) break;
                 case 0: RT_SIMPLE(0, kWalkTop) break;
                 case kFeatCoopTail | kFeatExt: RT_SIMPLE(kFeatCoopTail | kFeatExt, kWalkTop) break;
+                default: return hipErrorInvalidValue;
+            }
+        } else if (a.walk == kWalkDma) {
+            if (bw != 1) return hipErrorInvalidValue;   // one stage per workgroup: one-wave workgroups
+            switch (feat) {
+                case kFeatCoopTail: RT_SIMPLE(kFeatCoopTail, kWalkDma) break;
+                case 0: RT_SIMPLE(0, kWalkDma) break;
+                case kFeatCoopTail | kFeatExt: RT_SIMPLE(kFeatCoopTail | kFeatExt, kWalkDma) break;
                 default: return hipErrorInvalidValue;
             }
         } else if (a.walk == kWalkScalar) {

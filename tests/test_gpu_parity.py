@@ -158,6 +158,10 @@ def test_config5_1m_row_subset(renderer):
     {"kernel": 0, "walk": 5, "coop_lanes": 0},
     {"kernel": 0, "walk": 5, "heavy_first": 0},
     {"kernel": 0, "walk": 5, "wave_tile": 3, "coop_lanes": 8},
+    {"kernel": 0, "walk": 14},
+    {"kernel": 0, "walk": 14, "coop_lanes": 0},
+    {"kernel": 0, "walk": 14, "heavy_first": 0},
+    {"kernel": 0, "walk": 14, "wave_tile": 3, "coop_lanes": 8},
 ])
 def test_schedules_identical(renderer, opts):
     """Every schedule gives the oracle's frame and counters (config 2 at the
@@ -281,7 +285,7 @@ def test_heavy_pixels(renderer, cfg_k, factor):
             renderer.set_option(k, v)
 
 
-@pytest.mark.parametrize("cfg_k,walk", [(3, 2), (4, 2), (5, 2), (3, 5), (5, 5)])
+@pytest.mark.parametrize("cfg_k,walk", [(3, 2), (4, 2), (5, 2), (3, 5), (5, 5), (3, 14), (6, 14), (5, 14)])
 def test_bench_setting_whole_frame(renderer, cfg_k, walk):
     """BASELINE configs 3, 4 and 5 as whole frames (config 5: 1M triangles,
     3840x2160, 8 bounces) under bench.py's N = 1 setting: the default
@@ -589,7 +593,7 @@ def test_golden_frames_on_gpu(renderer):
 
 
 @pytest.mark.parametrize("shape,n", [("left", 50), ("right", 200), ("random", 300)])
-@pytest.mark.parametrize("walk", [0, 1, 2, 5, 13, "frontier"])
+@pytest.mark.parametrize("walk", [0, 1, 2, 5, 13, 14, "frontier"])
 def test_unbalanced_bvh(renderer, shape, n, walk):
     from rtamd import configs
     built = raw_bvh_scene(n, shape, seed=n)
