@@ -12,7 +12,12 @@ With N > 1 ranks (one process per GPU, torch.distributed over RCCL), default
 interleaved 16-row bands (rank r traces the bands b with b mod N = r); every
 D steps the D frames traced since the last exchange are gathered to rank 0
 over xGMI (one dist.gather) and assembled there (one index_select), all
-inside the timed region (strong scaling: the work per step is fixed).
+inside the timed region (strong scaling: the work per step is fixed).  The
+collective's and the assembly's streams run at high priority
+(--exchange-priority), so the traces in flight do not starve them of CU slots.
+--partition blocks: one contiguous row piece per rank, the pieces' order
+rotated every frame, received by rank 0 straight into the frame (RCCL
+send/recv, no assembly); rank 0's piece sized by --root-share.
 --partition frames: a step is N frames of the render loop, each frame's bands
 rotated over the ranks, so every rank traces one frame's worth of pixels per
 step (weak scaling).  Rank 0 checks the assembled frames against a one-GPU
