@@ -157,6 +157,10 @@ __device__ __forceinline__ void pin(float4& q) { asm volatile("" : "+v"(q.x), "+
 // costs the vector memory pipeline nothing
 typedef float v4f __attribute__((ext_vector_type(4)));
 typedef const v4f __attribute__((address_space(4)))* ConstF4;
+__device__ __forceinline__ float4 ld_nt(const float4* p) {   // RT_NT_LEAF experiment
+    const v4f v = __builtin_nontemporal_load(reinterpret_cast<const v4f*>(p));
+    return make_float4(v.x, v.y, v.z, v.w);
+}
 __device__ __forceinline__ float4 ld_const(const float4* p, int i) {
     const v4f v = ((ConstF4)(uintptr_t)p)[i];
     return make_float4(v.x, v.y, v.z, v.w);
@@ -990,8 +994,15 @@ void trace_simple(TraceArgs a) {
                             Q1 = ld_const(leafs2, 2 * u + 1);
                         }
                     } else if (nl && nxt < end) {
+#if RT_NT_LEAF
+                        // experiment: a leaf's triangle is read by few waves;
+                        // non-temporal loads keep it from evicting node records
+                        Q0 = ld_nt(leafs2 + 2 * nxt + 0);
+                        Q1 = ld_nt(leafs2 + 2 * nxt + 1);
+#else
                         Q0 = leafs2[2 * nxt + 0];
                         Q1 = leafs2[2 * nxt + 1];
+#endif
                     }
                     n = nxt;
                     nleaf = nl;
