@@ -180,7 +180,11 @@ int rt_render_wait(rt_ctx* ctx, uint64_t ticket);
  *                   records + per-lane stack of right-child entry distances,
  *                   2 = one node per step, software-pipelined: the next
  *                   node's box is requested before this node's triangle test
- *                   and the loop control (default)
+ *                   and the loop control (default); 5 = walk 2 with scalar
+ *                   loads when every walking lane moves to one node; 13 = walk
+ *                   2 with the top tree's records in each workgroup's LDS;
+ *                   14 = walk 2 with LDS-DMA fetches of a uniform step's
+ *                   records (5, 13, 14: measured slower)
  *   "coop_lanes"    kernel 0: once at most this many lanes of a wave are still
  *                   walking, the whole wave finishes their walks one ray at a
  *                   time (0..64, default 1; 0 = off)
