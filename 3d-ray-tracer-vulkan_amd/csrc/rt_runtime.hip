@@ -235,12 +235,13 @@ struct PerDevice {
     int          n_cu = 0;
     int          blocks_per_cu = 1;
     // rt_render_async: frame slots (option async_slots), each with its own
-    // trace stream, one copy stream, per-slot events and the last ticket of a slot
-    hipStream_t  copy_stream = nullptr;
+    // trace stream, one copy stream (two for a one-device frame, option
+    // copy_streams), per-slot events and the last ticket of a slot
+    hipStream_t  copy_stream = nullptr, copy_stream2 = nullptr;
     uchar4*      d_ring[kMaxSlots] = {};
     size_t       ring_cap = 0;     // pixels per slot
     hipStream_t  slot_stream[kMaxSlots] = {};
-    hipEvent_t   traced[kMaxSlots] = {}, copied[kMaxSlots] = {};
+    hipEvent_t   traced[kMaxSlots] = {}, copied[kMaxSlots] = {}, copied2[kMaxSlots] = {};
     uint64_t     slot_ticket[kMaxSlots] = {};
     float*       d_accum = nullptr;  // extension kExtAccumulate: running sums
     float4*      d_spheres = nullptr; // extension kExtSpheres: 2 float4 per sphere
@@ -324,6 +325,7 @@ struct rt_ctx {
     int  heavy_cap = 75;           // automatic heavy tiles: at most this percentage of one generation of
                                    //   one-pixel waves (CUs x 24 / 64 tiles)
     int  async_slots = 4;          // rt_render_async: frames in flight per device, each on its own stream
+    int  copy_streams = 1;         // rt_render_async, one device: the readback split over this many copy streams (2 measured slower)
     int  in_async = 0;             // set while rt_render_async plans a launch: its frames in flight
     int  concurrent_launches = 1;  // launches of similar work the caller keeps in flight on a device at once
                                    //   (the heavy-tile bulk estimate counts this launch's work that many times)
@@ -793,9 +795,11 @@ int rt_create(const int* device_ids, int n_devices, rt_ctx** out) {
         if (e == hipSuccess) e = hipMalloc(&p.d_counters, 2 * sizeof(Counters));   // [1]: trace_coop's sink
         if (e == hipSuccess) e = hipMalloc(&p.d_queue, sizeof(unsigned) * 3 * kQueueSlots);
         if (e == hipSuccess) e = hipStreamCreateWithFlags(&p.copy_stream, hipStreamNonBlocking);
+        if (e == hipSuccess) e = hipStreamCreateWithFlags(&p.copy_stream2, hipStreamNonBlocking);
         for (int k2 = 0; k2 < kMaxSlots && e == hipSuccess; ++k2) {
             e = hipEventCreateWithFlags(&p.traced[k2], hipEventDisableTiming);
             if (e == hipSuccess) e = hipEventCreateWithFlags(&p.copied[k2], hipEventDisableTiming);
+            if (e == hipSuccess) e = hipEventCreateWithFlags(&p.copied2[k2], hipEventDisableTiming);
         }
         p.n_cu = prop.multiProcessorCount;
         p.blocks_per_cu = persistent_blocks_per_cu();
@@ -816,15 +820,18 @@ int rt_destroy(rt_ctx* ctx) {
         (void)hipSetDevice(p.device);
         if (p.stream) (void)hipStreamSynchronize(p.stream);
         if (p.copy_stream) (void)hipStreamSynchronize(p.copy_stream);
+        if (p.copy_stream2) (void)hipStreamSynchronize(p.copy_stream2);
         free_scene(p);
         for (int k2 = 0; k2 < kMaxSlots; ++k2) {
             if (p.slot_stream[k2]) (void)hipStreamSynchronize(p.slot_stream[k2]);
             if (p.d_ring[k2]) (void)hipFree(p.d_ring[k2]);
             if (p.traced[k2]) (void)hipEventDestroy(p.traced[k2]);
             if (p.copied[k2]) (void)hipEventDestroy(p.copied[k2]);
+            if (p.copied2[k2]) (void)hipEventDestroy(p.copied2[k2]);
             if (p.slot_stream[k2]) (void)hipStreamDestroy(p.slot_stream[k2]);
         }
         if (p.copy_stream) (void)hipStreamDestroy(p.copy_stream);
+        if (p.copy_stream2) (void)hipStreamDestroy(p.copy_stream2);
         if (p.d_counters) (void)hipFree(p.d_counters);
         if (p.d_queue) (void)hipFree(p.d_queue);
         if (p.d_spill) (void)hipFree(p.d_spill);
@@ -1297,6 +1304,7 @@ int rt_render_async(rt_ctx* ctx, const rt_camera_ubo* cam, int width, int height
             for (int k2 = 0; k2 < kMaxSlots; ++k2)
                 if (p.slot_stream[k2]) RT_HIP_CHECK(hipStreamSynchronize(p.slot_stream[k2]));
             RT_HIP_CHECK(hipStreamSynchronize(p.copy_stream));
+            RT_HIP_CHECK(hipStreamSynchronize(p.copy_stream2));
             for (int k2 = 0; k2 < kMaxSlots; ++k2) {
                 if (p.d_ring[k2]) (void)hipFree(p.d_ring[k2]);
                 p.d_ring[k2] = nullptr;
@@ -1310,6 +1318,7 @@ int rt_render_async(rt_ctx* ctx, const rt_camera_ubo* cam, int width, int height
         const hipStream_t ts = p.slot_stream[slot];
         // The slot's previous frame must be read back before it is overwritten.
         RT_HIP_CHECK(hipStreamWaitEvent(ts, p.copied[slot], 0));
+        RT_HIP_CHECK(hipStreamWaitEvent(ts, p.copied2[slot], 0));
         ctx->in_async = S;
         rc = render_bands_on(ctx, p, cam, width, height, max_bounces, bh, nd, k, rows, p.d_ring[slot], nullptr, ts,
                              false);
@@ -1319,7 +1328,16 @@ int rt_render_async(rt_ctx* ctx, const rt_camera_ubo* cam, int width, int height
         // Copies run in ticket order on the one copy stream, whatever order the
         // traces finish in.
         RT_HIP_CHECK(hipStreamWaitEvent(p.copy_stream, p.traced[slot], 0));
-        if (nd == 1) {
+        if (nd == 1 && ctx->copy_streams == 2 && rows > 1) {
+            // the frame's top and bottom halves on two copy streams, so two copy
+            // engines read the frame back at once
+            const size_t top = (size_t)width * (size_t)(rows / 2) * 4;
+            RT_HIP_CHECK(hipStreamWaitEvent(p.copy_stream2, p.traced[slot], 0));
+            RT_HIP_CHECK(hipMemcpyAsync(out_rgba, p.d_ring[slot], top, hipMemcpyDeviceToHost, p.copy_stream));
+            RT_HIP_CHECK(hipMemcpyAsync(out_rgba + top, reinterpret_cast<uint8_t*>(p.d_ring[slot]) + top,
+                                        px * 4 - top, hipMemcpyDeviceToHost, p.copy_stream2));
+            RT_HIP_CHECK(hipEventRecord(p.copied2[slot], p.copy_stream2));
+        } else if (nd == 1) {
             RT_HIP_CHECK(hipMemcpyAsync(out_rgba, p.d_ring[slot], px * 4, hipMemcpyDeviceToHost, p.copy_stream));
         } else {
             // bands k, k+nd, ...: every full band in one strided copy, a partial last band on its own
@@ -1359,8 +1377,13 @@ int rt_render_wait(rt_ctx* ctx, uint64_t ticket) {
         int best = -1;
         for (int k2 = 0; k2 < kMaxSlots; ++k2)
             if (p.slot_ticket[k2] >= ticket && (best < 0 || p.slot_ticket[k2] < p.slot_ticket[best])) best = k2;
-        if (best >= 0) RT_HIP_CHECK(hipEventSynchronize(p.copied[best]));
-        else RT_HIP_CHECK(hipStreamSynchronize(p.copy_stream));   // a device with no rows of that frame
+        if (best >= 0) {
+            RT_HIP_CHECK(hipEventSynchronize(p.copied[best]));
+            RT_HIP_CHECK(hipEventSynchronize(p.copied2[best]));   // not recorded (one copy stream): returns at once
+        } else {
+            RT_HIP_CHECK(hipStreamSynchronize(p.copy_stream));   // a device with no rows of that frame
+            RT_HIP_CHECK(hipStreamSynchronize(p.copy_stream2));
+        }
     }
     return RT_OK;
 }
@@ -1406,6 +1429,8 @@ int rt_set_option(rt_ctx* ctx, const char* name, int64_t value) {
         ctx->heavy_cap = (int)value;
     } else if (std::strcmp(name, "async_slots") == 0 && value >= 1 && value <= kMaxSlots) {
         ctx->async_slots = (int)value;
+    } else if (std::strcmp(name, "copy_streams") == 0 && (value == 1 || value == 2)) {
+        ctx->copy_streams = (int)value;
     } else if (std::strcmp(name, "concurrent_launches") == 0 && value >= 1 && value <= 64) {
         ctx->concurrent_launches = (int)value;
     } else if (std::strcmp(name, "learn_cost") == 0 && (value == 0 || value == 1)) {
@@ -1445,6 +1470,7 @@ int rt_get_option(rt_ctx* ctx, const char* name, int64_t* value) {
     else if (std::strcmp(name, "heavy_factor") == 0) *value = ctx->heavy_factor;
     else if (std::strcmp(name, "concurrent_launches") == 0) *value = ctx->concurrent_launches;
     else if (std::strcmp(name, "async_slots") == 0) *value = ctx->async_slots;
+    else if (std::strcmp(name, "copy_streams") == 0) *value = ctx->copy_streams;
     else if (std::strcmp(name, "heavy_cap") == 0) *value = ctx->heavy_cap;
     else if (std::strcmp(name, "reuse_order") == 0) *value = ctx->reuse_order;
     else if (std::strcmp(name, "heavy_pixels") == 0) *value = ctx->heavy_pixels;

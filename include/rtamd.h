@@ -151,7 +151,11 @@ int rt_band_rows(int height, int band_h, int band_stride, int band_off);
  * frame is complete in out_rgba.  Option "async_slots" (1..8, default 4) frame
  * slots rotate per device, each tracing on a stream of its own, so with that
  * many frames in flight the frames' traces run at once and every readback
- * overlaps later traces (copies complete in ticket order).  The heavy-pixel
+ * overlaps later traces (copies complete in ticket order).  Option
+ * "copy_streams" (1 or 2, default 1): 2 splits a one-device frame's readback
+ * in two halves on two copy streams (measured slower: 0.40 vs 0.37 ms per
+ * frame, profiles/r02/async/copy_streams).
+ * The heavy-pixel
  * bar counts the slots as concurrent launches.  Concurrent streams need a
  * hardware queue each, and HIP's default is 4 per process, fixed when the HIP
  * runtime loads: start the host process with GPU_MAX_HW_QUEUES=16 (JVM:

@@ -500,9 +500,11 @@ def test_multi_device_context_interleaves(renderer):
 
 
 @pytest.mark.parametrize("devices,slots", [((0,), 2), ((0, 0), 2), ((0,), 4), ((0, 0), 3), ((0,), 8)])
-def test_render_async_matches_sync(devices, slots):
+@pytest.mark.parametrize("copies", [1, 2])
+def test_render_async_matches_sync(devices, slots, copies):
     """rt_render_async (option async_slots frame slots, each tracing on its own
-    stream; one copy stream; strided band readback) gives rt_render's frames,
+    stream; one copy stream, or a one-device frame's two halves on two (option
+    copy_streams); strided band readback) gives rt_render's frames,
     in order, with that many frames in flight and a new camera per frame; a
     wait on an older ticket returns once it is done even after newer frames
     reused its slot."""
@@ -519,6 +521,8 @@ def test_render_async_matches_sync(devices, slots):
     try:
         r.set_option("async_slots", slots)
         assert r.get_option("async_slots") == slots
+        r.set_option("copy_streams", copies)
+        assert r.get_option("copy_streams") == copies
         r.upload_scene(built)
         cams = [rtamd.Camera((-25.0 + 7 * k, 30.0, 140.0 - 9 * k), (0.0, 0.0, 0.0), (0.0, 1.0, 0.0), 20.0, w / h)
                 for k in range(2 * slots + 3)]

@@ -22,6 +22,7 @@ def main():
     ap.add_argument("--config", type=int, default=3)
     ap.add_argument("--frames", type=int, default=400)
     ap.add_argument("--slots", default="2,4,8", help="rt_render_async frames in flight (async_slots) to time")
+    ap.add_argument("--copy-streams", default="2", help="rt option copy_streams values to time (1, 2 or 1,2)")
     args = ap.parse_args()
     import numpy as np
     import rtamd          # sets GPU_MAX_HW_QUEUES, then loads torch's HIP runtime first
@@ -54,7 +55,13 @@ def main():
             r.wait(t)
 
     modes = [("sync rt_render (pageable copy, fence per frame)", sync_run)]
-    modes += [(f"rt_render_async, {d} in flight, pinned", (lambda d: lambda n: async_run(n, d))(d)) for d in slots]
+    def with_copies(c, d):
+        def run(n):
+            r.set_option("copy_streams", c)
+            async_run(n, d)
+        return run
+    modes += [(f"rt_render_async, {d} in flight, pinned, {c} copy stream(s)", with_copies(c, d))
+              for d in slots for c in [int(x) for x in args.copy_streams.split(",")]]
     for name, fn in modes:
         fn(20)
         t0 = time.perf_counter()
