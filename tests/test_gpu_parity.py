@@ -500,8 +500,8 @@ def test_multi_device_context_interleaves(renderer):
 
 
 @pytest.mark.parametrize("devices,slots", [((0,), 2), ((0, 0), 2), ((0,), 4), ((0, 0), 3), ((0,), 8)])
-@pytest.mark.parametrize("copies", [1, 2])
-def test_render_async_matches_sync(devices, slots, copies):
+@pytest.mark.parametrize("copies,depth", [(1, 1), (2, 1), (1, 2)])
+def test_render_async_matches_sync(devices, slots, copies, depth):
     """rt_render_async (option async_slots frame slots, each tracing on its own
     stream; one copy stream, or a one-device frame's two halves on two (option
     copy_streams); strided band readback) gives rt_render's frames,
@@ -517,7 +517,8 @@ def test_render_async_matches_sync(devices, slots, copies):
     built = cfg.build()
     w, h, b = 333, 201, 3            # 201 rows: a partial last 16-row band
     r = rtamd.Renderer(devices)
-    frames = [PinnedFrame(h, w) for _ in range(slots)]
+    q = slots * depth                # host frames pending (depth 2: a slot's next trace overlaps its last readback)
+    frames = [PinnedFrame(h, w) for _ in range(q)]
     try:
         r.set_option("async_slots", slots)
         assert r.get_option("async_slots") == slots
@@ -525,19 +526,19 @@ def test_render_async_matches_sync(devices, slots, copies):
         assert r.get_option("copy_streams") == copies
         r.upload_scene(built)
         cams = [rtamd.Camera((-25.0 + 7 * k, 30.0, 140.0 - 9 * k), (0.0, 0.0, 0.0), (0.0, 1.0, 0.0), 20.0, w / h)
-                for k in range(2 * slots + 3)]
+                for k in range(2 * q + 3)]
         refs = [r.render(c, w, h, b)[0] for c in cams]
         pending = []
         for k, c in enumerate(cams):
-            pending.append((r.render_async(c, w, h, b, frames[k % slots]), k))
-            if len(pending) == slots:
+            pending.append((r.render_async(c, w, h, b, frames[k % q]), k))
+            if len(pending) == q:
                 t, j = pending.pop(0)
                 r.wait(t)
-                assert np.array_equal(frames[j % slots].array, refs[j]), f"frame {j}"
+                assert np.array_equal(frames[j % q].array, refs[j]), f"frame {j}"
         while pending:
             t, j = pending.pop(0)
             r.wait(t)
-            assert np.array_equal(frames[j % slots].array, refs[j]), f"frame {j}"
+            assert np.array_equal(frames[j % q].array, refs[j]), f"frame {j}"
         r.wait(1)                    # long since done; its slot has been reused
         with pytest.raises(rtamd.RtError, match="INVALID_ARG"):
             r.wait(t + 1)

@@ -22,7 +22,9 @@ def main():
     ap.add_argument("--config", type=int, default=3)
     ap.add_argument("--frames", type=int, default=400)
     ap.add_argument("--slots", default="2,4,8", help="rt_render_async frames in flight (async_slots) to time")
-    ap.add_argument("--copy-streams", default="2", help="rt option copy_streams values to time (1, 2 or 1,2)")
+    ap.add_argument("--copy-streams", default="1", help="rt option copy_streams values to time (1, 2 or 1,2)")
+    ap.add_argument("--depth", default="1", help="host frames pending per slot (1, 2 or 1,2): the caller waits "
+                                                  "for its oldest frame once slots x depth are pending")
     args = ap.parse_args()
     import numpy as np
     import rtamd          # sets GPU_MAX_HW_QUEUES, then loads torch's HIP runtime first
@@ -38,30 +40,32 @@ def main():
     segs = r.render(cam, W, H, B, stats=True)[2]["segments"]
     pageable = np.empty((H, W, 4), np.uint8)
     slots = [int(x) for x in args.slots.split(",")]
-    frames = [PinnedFrame(H, W) for _ in range(max(slots))]
+    depths = [int(x) for x in args.depth.split(",")]
+    frames = [PinnedFrame(H, W) for _ in range(max(slots) * max(depths))]
 
     def sync_run(n):
         for _ in range(n):
             r.render(cam, W, H, B)
 
-    def async_run(n, d):
+    def async_run(n, d, depth=1):
         r.set_option("async_slots", d)
         pending = []
         for k in range(n):
-            pending.append(r.render_async(cam, W, H, B, frames[k % d]))
-            if len(pending) == d:
+            pending.append(r.render_async(cam, W, H, B, frames[k % (d * depth)]))
+            if len(pending) == d * depth:
                 r.wait(pending.pop(0))
         for t in pending:
             r.wait(t)
 
     modes = [("sync rt_render (pageable copy, fence per frame)", sync_run)]
-    def with_copies(c, d):
+    def with_copies(c, d, depth):
         def run(n):
             r.set_option("copy_streams", c)
-            async_run(n, d)
+            async_run(n, d, depth)
         return run
-    modes += [(f"rt_render_async, {d} in flight, pinned, {c} copy stream(s)", with_copies(c, d))
-              for d in slots for c in [int(x) for x in args.copy_streams.split(",")]]
+    modes += [(f"rt_render_async, {d} in flight, pinned, {c} copy stream(s), {d * depth} host frames pending",
+               with_copies(c, d, depth))
+              for d in slots for c in [int(x) for x in args.copy_streams.split(",")] for depth in depths]
     for name, fn in modes:
         fn(20)
         t0 = time.perf_counter()
@@ -70,7 +74,7 @@ def main():
         print(json.dumps({"mode": name, "config": cfg.name, "frames": args.frames,
                           "fps": round(args.frames / dt, 1), "ms_per_frame": round(dt / args.frames * 1e3, 3),
                           "mrays_s_incl_pcie": round(segs * args.frames / dt / 1e6, 1)}), flush=True)
-    assert np.array_equal(frames[(args.frames - 1) % slots[-1]].array, r.render(cam, W, H, B)[0])
+    assert np.array_equal(frames[(args.frames - 1) % (slots[-1] * depths[-1])].array, r.render(cam, W, H, B)[0])
     del pageable
     r.close()
     for f in frames:
