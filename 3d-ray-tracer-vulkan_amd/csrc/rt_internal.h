@@ -25,13 +25,9 @@
 //           the boxes of both children of node i and where they are
 //           [0] = (L.min.xyz, R.min.x) [1] = (L.max.xyz, R.min.y)
 //           [2] = (R.max.xyz, R.min.z) [3] = (R | L(R) << 31, L(i+1), skip(i), 0)
-//           with L = i+1 and R = the right child.  The default walk
-//           (trace_simple, "walk" 1) loads this one record when node i is hit
-//           and runs both children's slab tests at once.  A slab test does
-//           not depend on closest_t; only the final "t_enter < closest_t"
-//           does, so the right child's t_enter is kept on a short per-lane
-//           stack and compared when the reference would pop it — the same
-//           float bits, compared at the same point in the visit sequence.
+//           with L = i+1 and R = the right child.  The frontier walk (heavy
+//           pixels, option coop_walk 1) expands a hit internal node by
+//           loading this one record and testing both children's boxes.
 //   norms : 1 x float4 per flattened triangle: normalize(cross(e1,e2)) (:124),
 //           likewise precomputed; read once per hit when shading.
 //   mats  : 1 x float4 per flattened triangle (albedo.rgb, type)
@@ -45,14 +41,6 @@
 namespace rtamd {
 
 constexpr int kShadeStride = 2;
-#ifndef RT_TOP_BITS
-#define RT_TOP_BITS 10
-#endif
-constexpr int kTopBits = RT_TOP_BITS;            // walk 13: slot+1 field width (10: 32 KB of LDS, 11: 64 KB)
-constexpr int kTopSlots = (1 << kTopBits) - 1;   // top-tree slots
-constexpr int kWalkTop = 13;      // option walk: walk 2 with the top tree's records in LDS
-constexpr int kWalkScalar = 5;    // option walk: walk 2 with scalar loads on wave-uniform steps
-constexpr int kWalkDma = 14;      // option walk: walk 2 with LDS-DMA record fetches on wave-uniform steps
 
 struct DevScene {
     int      n_nodes = 0;     // nodes in the compact array
@@ -72,18 +60,6 @@ struct DevScene {
     // registers instead of 12
     float4*  nodes2  = nullptr;
     float4*  leafs2  = nullptr;
-    // Top tree (walk 13): the internal nodes of the deepest prefix of levels
-    // that fits kTopSlots, in preorder, get slots 0..n_top-1; their records (top, 2 x float4 per
-    // slot) are copied into each workgroup's LDS at launch.  nodes3 is nodes2
-    // with the slot of each possible next node in free bits, so a walker
-    // knows from the record it holds whether its next node is in LDS:
-    //   internal [1].w |= (slot(skip)+1) << 2 | (slot(i+1)+1) << (2 + kTopBits)
-    //   leaf     [0].w  = triangle (20 bits) | (slot(i+1)+1) << 20 | L(i+1) << 31
-    // (slot+1 = 0: not in the top tree).  Null when the scene has more than
-    // 2^20 triangles (walk 13 then runs as walk 2).
-    float4*  nodes3  = nullptr;
-    float4*  top     = nullptr;
-    int      n_top   = 0;
     // norms and mats interleave in one allocation (kShadeStride float4 per
     // triangle: normal, then albedo/type), so shading a hit touches one 32-B
     // record; norms points at the allocation, mats one float4 in
@@ -109,12 +85,6 @@ struct CamF {                   // the four vec3 of the CameraUBO
     float vx, vy, vz;
 };
 
-constexpr int kKernelSimple = 0;       // one lane per pixel, 8x8 pixels per wave
-constexpr int kKernelPersistent = 1;   // persistent waves + tile queue + deferred shading
-constexpr int kKernelSplit = 2;        // simple for the first seg_limit segments, then the
-                                       // surviving paths are spilled to a compacted queue and
-                                       // finished by the persistent kernel
-
 // Non-reference extensions (option "extensions", off by
 // default, kernel 0 only).  The reference has none of them (SURVEY.md §0 facts
 // 3-4); oracle/rt_oracle.h ORC_EXT_* states the same semantics.
@@ -122,24 +92,6 @@ constexpr int kExtSkyToggle = 1;    // a miss is black when sky_enabled == 0
 constexpr int kExtEmissive = 2;     // a type-3 hit ends the path with attenuation * albedo
 constexpr int kExtAccumulate = 4;   // seed += frame_count*W*H; output sqrt(mean of linear colour)
 constexpr int kExtSpheres = 8;      // spheres (rt_upload_spheres) after the BVH walk, in index order
-
-// A path suspended between two segments (48 B): everything the bounce loop
-// (compute_dynamic_ray.comp:179-232) carries from one iteration to the next.
-struct PathState {
-    float4 q0;   // origin.xyz, attenuation.x
-    float4 q1;   // direction.xyz, attenuation.y
-    float4 q2;   // attenuation.z, seed (bits), bounce index b (bits), lx | ly << 16 (bits)
-};
-
-constexpr int kKernelTiered = 3;       // simple with a per-path visit budget; paths over budget
-                                       // are suspended mid-walk and finished by trace_coop (one
-                                       // wave per ray, 64-node windows, exact scalar replay)
-
-// A path suspended inside a segment (64 B): PathState + the walk's position.
-struct HeavyRay {
-    PathState p;
-    float4    q3;   // closest_t, next node (bits), hit triangle (bits), unused
-};
 
 struct TraceArgs {
     DevScene scene;
@@ -154,47 +106,33 @@ struct TraceArgs {
     uchar4*  out_rgba;          // tw*th, nullable
     float*   out_rad;           // tw*th*3, nullable
     Counters* counters;         // nullable
-    int      kernel;            // kKernelSimple / kKernelPersistent
-    unsigned* queue;            // persistent: zeroed work counter for this launch
-    int      shade_min;         // persistent: shade once this many lanes of a wave are ready
-    int      grid_blocks;       // persistent: blocks of 256 threads
-    int      wave_tile;         // simple: wave tile (8<<s) x (8>>s), s in 0..3
-    int      seg_limit;         // simple: segments before a live path is spilled (>= max_bounces: never)
-    PathState* spill;           // split: spilled paths (capacity tw*th)
-    unsigned* spill_count;      // split: number of spilled paths (zeroed before the simple pass)
-    int      resume;            // persistent: take paths from spill[] instead of pixel tiles
-    unsigned long long* diag;   // simple kernel diagnostics: 4 words per wave, or null
-    int      prio_after;        // simple: raise wave priority after this many node steps (0 = never)
-    int      heavy_budget;      // simple: node visits per path before it is handed to the
-                                //   cooperative pass (<= 0: never)
-    HeavyRay* heavy;            // tiered: suspended heavy paths (capacity tw*th)
-    unsigned* heavy_count;      // tiered: number of heavy paths (zeroed before the simple pass)
-    int      coop_lanes;        // simple: finish a wave's walks cooperatively once at most
+    int      wave_tile;         // wave tile (8<<s) x (8>>s), s in 0..3
+    unsigned long long* diag;   // diagnostics: 8 words per wave, or null
+    int      coop_lanes;        // finish a wave's walks cooperatively once at most
                                 //   this many lanes are still walking (0 = never)
-    int      ext;               // simple: non-reference extensions, kExt* bits (0 = the reference)
+    int      ext;               // non-reference extensions, kExt* bits (0 = the reference)
     int      sky_enabled;       // CameraUBO.sky_enabled (@68), read only with kExtSkyToggle
     int      frame_count;       // CameraUBO.frame_count (@64), read only with kExtAccumulate
     float*   accum;             // kExtAccumulate: running linear-colour sums, 3 floats per pixel (tw*th)
-    int      walk;              // simple: 0 = one node per step (nodes/leafs),
-                                //   1 = child pairs + per-lane stack of t_enter (pairs)
-    int      block_waves;       // simple: waves per workgroup, 4 (256 threads) or 1 (64 threads)
-    const int* tile_order;      // simple, block_waves 1: workgroup k traces wave tile tile_order[k] (or k)
-    int      tiles_x;           // simple, with tile_order (1-D grid): wave tiles per tile row
-    int      split_n;           // simple, with tile_order: the first split_n tiles of the order are traced
+    int      walk;              // 0 = one node per step (nodes/leafs), 2 = the same software-pipelined
+                                //   over the compact records (nodes2/leafs2; default)
+    int      block_waves;       // waves per workgroup, 4 (256 threads) or 1 (64 threads)
+    const int* tile_order;      // block_waves 1: workgroup k traces wave tile tile_order[k] (or k)
+    int      tiles_x;           // with tile_order (1-D grid): wave tiles per tile row
+    int      split_n;           // with tile_order: the first split_n tiles of the order are traced
                                 //   one pixel per wave (64 workgroups each; launcher-internal)
-    int      heavy_tiles;       // simple, with tile_order: the first heavy_tiles tiles run in that split
+    int      heavy_tiles;       // with tile_order: the first heavy_tiles tiles run in that split
                                 //   mode as a concurrent launch on aux_stream (fork ev_fork, join ev_join)
-    int      heavy_fused;       // simple, with heavy_tiles: 1 = the heavy tiles' one-pixel workgroups come
+    int      heavy_fused;       // with heavy_tiles: 1 = the heavy tiles' one-pixel workgroups come
                                 //   first in the same launch (option heavy_stream 2), no aux stream
-    const int* heavy_px;        // simple, fused, with tile_order: heavy pixels (tile * 64 + lane), traced one
+    const int* heavy_px;        // fused, with tile_order: heavy pixels (tile * 64 + lane), traced one
     int      n_heavy_px;        //   per wave by the first n_heavy_px workgroups of the launch
     const unsigned long long* tile_mask;   // per tile: the lanes (heavy pixels) its tile wave skips, or null
     unsigned* diag_lane;        // learning launch: each pixel's walk length (64 per wave), or null
     hipStream_t aux_stream;
     hipEvent_t ev_fork, ev_join;
-    Counters* sink;             // tiered: counters trace_coop adds into when counters is null
-    int      coop_walk;         // cooperative walks (coop tail, trace_coop): 0 = 64-node preorder
-                                //   windows (coop_walk), 1 = preorder frontier (frontier_walk)
+    int      coop_walk;         // cooperative tail: 0 = 64-node preorder windows (coop_walk),
+                                //   1 = preorder frontier (frontier_walk)
 };
 
 // Host-side compact-scene build from the reference records; validates the
@@ -216,7 +154,6 @@ void free_host_scene(HostScene* s);
 
 // Kernel launcher (rt_trace.hip).
 hipError_t launch_trace(const TraceArgs& a, hipStream_t stream);
-int persistent_blocks_per_cu();   // occupancy of trace_persistent (current device), capped at 8
 
 void set_error(const char* fmt, ...);
 

@@ -223,17 +223,9 @@ struct PerDevice {
     uchar4*      d_rgba = nullptr;
     float*       d_rad = nullptr;
     size_t       out_cap = 0;      // pixels
-    unsigned*    d_queue = nullptr; // ring of kQueueSlots work counters + kQueueSlots spill counters
-    unsigned     queue_slot = 0;
-    unsigned     last_slot = 0;
-    PathState*   d_spill = nullptr; // split schedule: suspended paths
-    size_t       spill_cap = 0;
     unsigned long long* d_diag = nullptr;   // diagnostics (option "diag")
     size_t       diag_cap = 0, diag_used = 0;
-    HeavyRay*    d_heavy = nullptr; // tiered schedule: paths suspended over budget
-    size_t       heavy_cap = 0;
     int          n_cu = 0;
-    int          blocks_per_cu = 1;
     // rt_render_async: frame slots (option async_slots), each with its own
     // trace stream, one copy stream (two for a one-device frame, option
     // copy_streams), per-slot events and the last ticket of a slot
@@ -265,7 +257,12 @@ struct PerDevice {
     unsigned     aux_next = 0;
     std::vector<Order> orders;
     std::vector<uint8_t> learning_key;
-    std::vector<uint8_t> prev_key;   // the launch key of the previous heavy_first launch (option reuse_order)
+    // option reuse_order: the camera of the last heavy_first launch of each
+    // frame geometry + scene (key without its camera bytes), newest last, so
+    // several geometries interleaved on one device (band offsets, rotating
+    // pieces, callers' streams) each see their own camera stop
+    struct LastCam { std::vector<uint8_t> geo; std::vector<uint8_t> cam; };
+    std::vector<LastCam> last_cam;
     size_t       learning_n = 0;
     int          last_heavy = 0;    // heavy tiles of the last launch (option "heavy_tiles_used", read only)
     int          last_heavy_px = 0; // heavy pixels of the last launch (option "heavy_pixels_used", read only)
@@ -298,25 +295,19 @@ static void free_graphs(PerDevice& p) {
 }
 static constexpr size_t kMaxGraphs = 64;   // an 8-rank frame batch with two buffers uses 16 keys
 
-static constexpr unsigned kQueueSlots = 64;
+static constexpr size_t kMaxLastCams = 64;
 
 struct rt_ctx {
     std::vector<PerDevice> dev;
-    int  kernel = kKernelSimple;   // fastest measured on config 3
-    int  shade_min = 16;
-    int  blocks_per_cu = 0;        // 0 = from the occupancy query
-    int  wave_tile = 0;            // simple kernel: 8x8 (default) / 16x4 / 32x2 / 64x1
-    int  seg_limit = 2;            // split: segments traced in the lockstep pass
-    int  diag = 0;                 // record per-wave timestamps (kernel 0 only)
-    int  prio_after = 0;           // kernel 0: s_setprio(3) after this many node steps
-    int  heavy_budget = 256;       // tiered: node visits per path in tier 1
-    int  coop_lanes = 1;           // kernel 0: cooperative tail once <= this many lanes walk (0 = off)
+    int  wave_tile = 0;            // 8x8 (default) / 16x4 / 32x2 / 64x1 pixels per wave
+    int  diag = 0;                 // record per-wave timestamps
+    int  coop_lanes = 1;           // cooperative tail once <= this many lanes walk (0 = off)
     int  ext = 0;                  // non-reference extensions (kExt* bits), off by default
-    int  walk = 2;                 // kernel 0: 0 = node per step, 1 = child pairs + t_enter stack,
-                                   //   2 = node per step, software-pipelined (fastest measured)
+    int  walk = 2;                 // 0 = node per step, 2 = node per step, software-pipelined over the
+                                   //   compact records (fastest measured)
     int  coop_walk = 0;            // cooperative walks: 0 = 64-node windows, 1 = preorder frontier
-    int  block_waves = 1;          // kernel 0: waves per workgroup (1: a finished wave frees its slot at once; or 4)
-    int  heavy_first = 1;          // kernel 0: dispatch tiles in the cost order of a learning launch
+    int  block_waves = 1;          // waves per workgroup (1: a finished wave frees its slot at once; or 4)
+    int  heavy_first = 1;          // dispatch tiles in the cost order of a learning launch
     int  heavy_factor = 130;       // automatic heavy tiles: walk length above this percentage of the bulk estimate
     int  heavy_pixels = 1;         // heavy_stream 2 with automatic heavy tiles: split heavy PIXELS (1) or
                                    //   whole tiles (0) into one-pixel waves
@@ -339,6 +330,8 @@ struct rt_ctx {
                                    //   per wave, walked cooperatively, in a separate launch
                                    //   (-1 = automatic: the tiles that outlast the bulk, learn_order)
     uint64_t scene_gen = 0;        // bumped by every scene upload (invalidates learned tile orders)
+    int  hw_queues = 4;            // GPU_MAX_HW_QUEUES seen at rt_create (HIP's default 4); frames in
+                                   //   flight on more streams than queues - 2 share queues and serialise
     bool has_scene = false;
     int  n_nodes = 0, n_tris = 0, max_depth = 0;
     uint64_t issued = 0;           // rt_render_async tickets handed out
@@ -349,8 +342,6 @@ static void free_scene(PerDevice& p) {
     if (p.scene.leafs) (void)hipFree(p.scene.leafs);
     if (p.scene.nodes2) (void)hipFree(p.scene.nodes2);
     if (p.scene.leafs2) (void)hipFree(p.scene.leafs2);
-    if (p.scene.nodes3) (void)hipFree(p.scene.nodes3);
-    if (p.scene.top) (void)hipFree(p.scene.top);
     if (p.scene.pairs) (void)hipFree(p.scene.pairs);
     if (p.scene.norms) (void)hipFree(p.scene.norms);   // mats lives in the same allocation
     p.scene = DevScene{};
@@ -360,9 +351,6 @@ static void free_scene(PerDevice& p) {
 // caller's statement (option concurrent_launches), or rt_render_async's own
 // frames in flight.
 static int concurrency(const rt_ctx* ctx) { return std::max(ctx->concurrent_launches, ctx->in_async); }
-
-// The extensions exist in kernel 0 only; with any of them on, kernel 0 runs.
-static int effective_kernel(const rt_ctx* ctx) { return ctx->ext ? kKernelSimple : ctx->kernel; }
 
 // Heavy-first dispatch (option heavy_first, kernel 0 with one-wave
 // workgroups): the first launch of a given frame geometry + camera + scene
@@ -385,10 +373,7 @@ static int plan_order(const rt_ctx* ctx, PerDevice& p, TraceArgs& a, const rt_ca
     a.ev_fork = a.ev_join = nullptr;
     p.last_heavy = 0;
     p.last_heavy_px = 0;
-    // walk 13 orders the wave tiles of its multi-wave workgroups (a workgroup
-    // takes block_waves consecutive tiles of the order)
-    const bool top_walk = a.walk == kWalkTop && a.scene.nodes3;
-    if (!ctx->heavy_first || a.kernel != kKernelSimple || (a.block_waves != 1 && !top_walk)) return RT_OK;
+    if (!ctx->heavy_first || a.block_waves != 1) return RT_OK;
     const int tw_w = 8 << a.wave_tile, th_w = 8 >> a.wave_tile, bw = a.block_waves;
     const size_t n = (size_t)((a.tw + bw * tw_w - 1) / (bw * tw_w)) * bw * (size_t)((a.th + th_w - 1) / th_w);
     const int geo[] = {a.width, a.height, a.max_bounces, a.x0, a.y0, a.tw, a.th, a.band_h, a.band_stride,
@@ -405,8 +390,15 @@ static int plan_order(const rt_ctx* ctx, PerDevice& p, TraceArgs& a, const rt_ca
     // it computes, so an order learned at another camera is exact, only less
     // well balanced; a camera in motion pays no learning frame, and the first
     // repeat of a camera (the camera has stopped) learns its own order.
+    // Heavy pixels / tiles are split out only where the launcher can do it:
+    // the cooperative tail on and no extensions (the one-pixel waves are a
+    // branch of the cooperative-tail kernel), and for the fused launch
+    // (heavy_stream 2) the default walk 2, which that launch runs.  Otherwise
+    // a launch uses the learned order alone (and reports no heavy work).
+    const bool splittable = a.coop_lanes > 0 && a.ext == 0 && (ctx->heavy_stream != 2 || a.walk == 2);
     auto use = [&](const PerDevice::Order& o) -> int {
         a.tile_order = o.d_order;
+        if (!splittable) return RT_OK;
         if (ctx->heavy_stream == 2 && ctx->heavy_pixels && ctx->heavy_tiles < 0 && n > 1) {
             // heavy pixels, fused: their one-pixel workgroups come first
             // in the launch, and their tiles skip them
@@ -438,12 +430,29 @@ static int plan_order(const rt_ctx* ctx, PerDevice& p, TraceArgs& a, const rt_ca
         }
         return RT_OK;
     };
-    const bool repeat = key == p.prev_key;
-    p.prev_key = key;
+    // Has the camera stopped?  Compared with the last launch of the same
+    // frame geometry and scene, not with the device's last launch: several
+    // geometries interleave on one device (band offsets, callers' streams).
+    const size_t g = sizeof(geo), c = sizeof(rt_camera_ubo);
+    bool repeat = false;
+    {
+        std::vector<uint8_t> geo_scene(key.begin(), key.begin() + g);
+        geo_scene.insert(geo_scene.end(), key.begin() + g + c, key.end());
+        std::vector<uint8_t> camk(key.begin() + g, key.begin() + g + c);
+        auto it = std::find_if(p.last_cam.begin(), p.last_cam.end(),
+                               [&](const PerDevice::LastCam& l) { return l.geo == geo_scene; });
+        if (it != p.last_cam.end()) {
+            repeat = it->cam == camk;
+            it->cam = std::move(camk);
+            std::rotate(it, it + 1, p.last_cam.end());      // newest last
+        } else {
+            if (p.last_cam.size() >= kMaxLastCams) p.last_cam.erase(p.last_cam.begin());
+            p.last_cam.push_back(PerDevice::LastCam{std::move(geo_scene), std::move(camk)});
+        }
+    }
     for (const auto& o : p.orders)
         if (o.n == n && o.key == key) return use(o);
     if (ctx->reuse_order && !repeat) {
-        const size_t g = sizeof(geo), c = sizeof(rt_camera_ubo);
         for (auto it = p.orders.rbegin(); it != p.orders.rend(); ++it)
             if (it->n == n && std::memcmp(it->key.data(), key.data(), g) == 0 &&
                 std::memcmp(it->key.data() + g + c, key.data() + g + c, sizeof(uint64_t)) == 0)
@@ -562,22 +571,11 @@ static int learn_order(const rt_ctx* ctx, PerDevice& p, const TraceArgs& a, hipS
 }
 
 static int set_schedule(const rt_ctx* ctx, PerDevice& p, TraceArgs& a, const rt_camera_ubo* cam) {
-    a.kernel = effective_kernel(ctx);
-    a.shade_min = ctx->shade_min;
     a.wave_tile = ctx->wave_tile;
-    a.prio_after = ctx->prio_after > 0 ? ctx->prio_after : -1;
     a.coop_lanes = ctx->coop_lanes;
     a.walk = ctx->walk;
     a.coop_walk = ctx->coop_walk;
     a.block_waves = ctx->block_waves;
-    // walk 13 needs its top tree (none past 2^20 triangles: walk 2 then) and
-    // runs 8- or 16-wave workgroups (its LDS copy is per workgroup); the
-    // other walks' kernels are built for at most 4 waves per workgroup.
-    if (a.walk == kWalkTop && (!p.scene.nodes3 || a.kernel != kKernelSimple || ctx->coop_walk)) a.walk = 2;
-    if (a.walk == kWalkTop && a.block_waves < 8) a.block_waves = 16;
-    if (a.walk != kWalkTop && a.block_waves > 4) a.block_waves = 1;
-    a.sink = p.d_counters + 1;
-    a.seg_limit = a.kernel == kKernelSplit ? ctx->seg_limit : (1 << 30);
     a.ext = ctx->ext;
     a.scene.spheres = p.d_spheres;
     a.scene.n_spheres = (a.ext & kExtSpheres) ? p.n_spheres : 0;
@@ -596,26 +594,14 @@ static int set_schedule(const rt_ctx* ctx, PerDevice& p, TraceArgs& a, const rt_
         }
         a.accum = p.d_accum;
     }
-    a.resume = 0;
-    const unsigned slot = p.queue_slot++ % kQueueSlots;
-    p.last_slot = slot;
-    a.queue = p.d_queue + slot;
-    a.spill_count = p.d_queue + kQueueSlots + slot;
-    const int bpc = ctx->blocks_per_cu > 0 ? ctx->blocks_per_cu : p.blocks_per_cu;
-    a.grid_blocks = std::max(1, p.n_cu * bpc);
-    if (a.kernel == kKernelPersistent) {
-        // never more waves than 8x8 pixel tiles
-        const int tiles = ((a.tw + 7) / 8) * ((a.th + 7) / 8);
-        a.grid_blocks = std::min(a.grid_blocks, std::max(1, (tiles + 3) / 4));
-    }
     a.diag = nullptr;
-    if (ctx->diag && (a.kernel == kKernelSimple || a.kernel == kKernelTiered)) {
-        // simple: 8 words per wave; tiered adds 4 words per suspended path (trace_coop)
+    if (ctx->diag) {
+        // 8 words per wave (+ 63 per heavy tile traced one pixel per wave)
         const int tw_w = 8 << a.wave_tile, th_w = 8 >> a.wave_tile;
         const int gw = std::max(4, a.block_waves);   // columns are rounded up to whole workgroups
         const size_t waves = (size_t)((a.tw + gw * tw_w - 1) / (gw * tw_w)) * ((a.th + th_w - 1) / th_w) * gw;
         const size_t split = ctx->heavy_first ? (size_t)(ctx->heavy_tiles < 0 ? kMaxHeavy : ctx->heavy_tiles) * 63 : 0;
-        const size_t words = (waves + split) * 8 + (a.kernel == kKernelTiered ? (size_t)a.tw * a.th * 4 : 0);
+        const size_t words = (waves + split) * 8;
         if (words > p.diag_cap) {
             if (p.d_diag) (void)hipFree(p.d_diag);
             p.d_diag = nullptr;
@@ -625,33 +611,6 @@ static int set_schedule(const rt_ctx* ctx, PerDevice& p, TraceArgs& a, const rt_
         }
         p.diag_used = words;
         a.diag = p.d_diag;
-    }
-    a.spill = nullptr;
-    if (a.kernel == kKernelSplit) {
-        const size_t need = (size_t)a.tw * (size_t)a.th;
-        if (need > p.spill_cap) {
-            if (p.d_spill) (void)hipFree(p.d_spill);
-            p.d_spill = nullptr;
-            p.spill_cap = 0;
-            RT_HIP_CHECK(hipMalloc(&p.d_spill, need * sizeof(PathState)));
-            p.spill_cap = need;
-        }
-        a.spill = p.d_spill;
-    }
-    a.heavy_budget = 1 << 30;
-    a.heavy = nullptr;
-    a.heavy_count = p.d_queue + 2 * kQueueSlots + slot;
-    if (a.kernel == kKernelTiered) {
-        a.heavy_budget = ctx->heavy_budget;
-        const size_t need = (size_t)a.tw * (size_t)a.th;
-        if (need > p.heavy_cap) {
-            if (p.d_heavy) (void)hipFree(p.d_heavy);
-            p.d_heavy = nullptr;
-            p.heavy_cap = 0;
-            RT_HIP_CHECK(hipMalloc(&p.d_heavy, need * sizeof(HeavyRay)));
-            p.heavy_cap = need;
-        }
-        a.heavy = p.d_heavy;
     }
     return plan_order(ctx, p, a, cam);
 }
@@ -675,12 +634,11 @@ static std::vector<uint64_t> launch_key(const TraceArgs& a, hipStream_t s) {
             F(c.ox), F(c.oy), F(c.oz), F(c.lx), F(c.ly), F(c.lz), F(c.hx), F(c.hy), F(c.hz), F(c.vx), F(c.vy), F(c.vz),
             (uint64_t)a.width, (uint64_t)a.height, (uint64_t)a.max_bounces, (uint64_t)a.x0, (uint64_t)a.y0,
             (uint64_t)a.tw, (uint64_t)a.th, (uint64_t)a.band_h, (uint64_t)a.band_stride, (uint64_t)a.band_off,
-            P(a.out_rgba), P(a.out_rad), (uint64_t)a.wave_tile, (uint64_t)a.seg_limit, (uint64_t)a.prio_after,
-            (uint64_t)a.heavy_budget, (uint64_t)a.coop_lanes, (uint64_t)a.ext, (uint64_t)a.sky_enabled,
+            P(a.out_rgba), P(a.out_rad), (uint64_t)a.wave_tile,
+            (uint64_t)a.coop_lanes, (uint64_t)a.ext, (uint64_t)a.sky_enabled,
             (uint64_t)a.frame_count, P(a.accum), (uint64_t)a.walk, (uint64_t)a.block_waves, P(a.tile_order),
             (uint64_t)a.heavy_tiles, (uint64_t)(a.aux_stream != nullptr), (uint64_t)a.heavy_fused, P(a.heavy_px),
-            (uint64_t)a.n_heavy_px, P(a.tile_mask), (uint64_t)a.coop_walk,
-            (uint64_t)a.kernel};
+            (uint64_t)a.n_heavy_px, P(a.tile_mask), (uint64_t)a.coop_walk};
 }
 
 static int launch(const rt_ctx* ctx, PerDevice& p, const TraceArgs& a, hipStream_t s) {
@@ -688,7 +646,7 @@ static int launch(const rt_ctx* ctx, PerDevice& p, const TraceArgs& a, hipStream
     // heavy_stream 1) gains from a graph: its fork and join become edges.  A
     // single launch (the fused heavy tiles, or none) goes straight to the
     // stream: a graph launch adds ~9 us between frames (profiles/r02/graph).
-    if (!ctx->graph || s == nullptr || a.counters || a.diag || a.kernel != kKernelSimple || !a.aux_stream) {
+    if (!ctx->graph || s == nullptr || a.counters || a.diag || !a.aux_stream) {
         RT_HIP_CHECK(launch_trace(a, s));
         return RT_OK;
     }
@@ -748,14 +706,14 @@ int rt_create(const int* device_ids, int n_devices, rt_ctx** out) {
     }
     rt_ctx* ctx = new (std::nothrow) rt_ctx;
     if (!ctx) { set_error("rt_create: out of memory"); return RT_ERR_OOM; }
-    if (const char* k = std::getenv("RTAMD_KERNEL"))
-        ctx->kernel = std::strcmp(k, "simple") == 0 ? kKernelSimple
-                    : std::strcmp(k, "persistent") == 0 ? kKernelPersistent
-                    : std::strcmp(k, "split") == 0 ? kKernelSplit
-                    : std::strcmp(k, "tiered") == 0 ? kKernelTiered : ctx->kernel;
-    if (const char* v = std::getenv("RTAMD_WALK")) {
-        const int w = std::atoi(v);
-        ctx->walk = w == kWalkTop ? w : std::max(0, std::min(2, w));
+    if (const char* v = std::getenv("RTAMD_WALK")) ctx->walk = std::atoi(v) == 0 ? 0 : 2;
+    // HIP reads GPU_MAX_HW_QUEUES once, when the runtime initialises (HIP's
+    // default is 4 hardware queues per process); reported as option
+    // "hw_queues" so a host can see whether its frames in flight get queues of
+    // their own (rt_render_async's slots need async_slots + 2).
+    if (const char* v = std::getenv("GPU_MAX_HW_QUEUES")) {
+        const int q = std::atoi(v);
+        if (q > 0) ctx->hw_queues = q;
     }
     if (const char* v = std::getenv("RTAMD_COOP_WALK")) ctx->coop_walk = std::atoi(v) ? 1 : 0;
     if (const char* v = std::getenv("RTAMD_HEAVY_FIRST")) ctx->heavy_first = std::atoi(v) ? 1 : 0;
@@ -767,12 +725,9 @@ int rt_create(const int* device_ids, int n_devices, rt_ctx** out) {
     if (const char* v = std::getenv("RTAMD_GRAPH")) ctx->graph = std::atoi(v) ? 1 : 0;
     if (const char* v = std::getenv("RTAMD_BLOCK_WAVES")) {
         const int bw = std::atoi(v);
-        ctx->block_waves = (bw == 1 || bw == 8 || bw == 16) ? bw : 4;
+        ctx->block_waves = bw == 1 ? 1 : 4;
     }
     if (const char* v = std::getenv("RTAMD_COOP_LANES")) ctx->coop_lanes = std::max(0, std::min(64, std::atoi(v)));
-    if (const char* v = std::getenv("RTAMD_SEG_LIMIT")) ctx->seg_limit = std::max(1, std::min(1024, std::atoi(v)));
-    if (const char* v = std::getenv("RTAMD_SHADE_MIN")) ctx->shade_min = std::max(1, std::min(64, std::atoi(v)));
-    if (const char* v = std::getenv("RTAMD_BLOCKS_PER_CU")) ctx->blocks_per_cu = std::max(0, std::min(32, std::atoi(v)));
     for (int k = 0; k < n_devices; ++k) {
         const int d = device_ids[k];
         if (d < 0 || d >= count) {
@@ -792,8 +747,7 @@ int rt_create(const int* device_ids, int n_devices, rt_ctx** out) {
         if (e == hipSuccess) e = hipStreamCreateWithFlags(&p.stream, hipStreamNonBlocking);
         if (e == hipSuccess) e = hipEventCreate(&p.ev0);
         if (e == hipSuccess) e = hipEventCreate(&p.ev1);
-        if (e == hipSuccess) e = hipMalloc(&p.d_counters, 2 * sizeof(Counters));   // [1]: trace_coop's sink
-        if (e == hipSuccess) e = hipMalloc(&p.d_queue, sizeof(unsigned) * 3 * kQueueSlots);
+        if (e == hipSuccess) e = hipMalloc(&p.d_counters, sizeof(Counters));
         if (e == hipSuccess) e = hipStreamCreateWithFlags(&p.copy_stream, hipStreamNonBlocking);
         if (e == hipSuccess) e = hipStreamCreateWithFlags(&p.copy_stream2, hipStreamNonBlocking);
         for (int k2 = 0; k2 < kMaxSlots && e == hipSuccess; ++k2) {
@@ -802,7 +756,6 @@ int rt_create(const int* device_ids, int n_devices, rt_ctx** out) {
             if (e == hipSuccess) e = hipEventCreateWithFlags(&p.copied2[k2], hipEventDisableTiming);
         }
         p.n_cu = prop.multiProcessorCount;
-        p.blocks_per_cu = persistent_blocks_per_cu();
         ctx->dev.push_back(p);
         if (e != hipSuccess) {
             set_error("rt_create: HIP setup on device %d failed: %s", d, hipGetErrorString(e));
@@ -833,9 +786,6 @@ int rt_destroy(rt_ctx* ctx) {
         if (p.copy_stream) (void)hipStreamDestroy(p.copy_stream);
         if (p.copy_stream2) (void)hipStreamDestroy(p.copy_stream2);
         if (p.d_counters) (void)hipFree(p.d_counters);
-        if (p.d_queue) (void)hipFree(p.d_queue);
-        if (p.d_spill) (void)hipFree(p.d_spill);
-        if (p.d_heavy) (void)hipFree(p.d_heavy);
         if (p.d_diag) (void)hipFree(p.d_diag);
         if (p.d_learn) (void)hipFree(p.d_learn);
         if (p.d_learn_lane) (void)hipFree(p.d_learn_lane);
@@ -901,55 +851,6 @@ int rt_upload_scene(rt_ctx* ctx, const void* vertices, size_t vertex_bytes,
         leafs2[2 * i] = make_float4(P0.y, P0.z, P1.x, P1.y);                   // v0.yz, e1.xy
         leafs2[2 * i + 1] = make_float4(P1.z, P2.x, P2.y, P2.z);               // e1.z, e2
     }
-    // walk 13's top tree (DevScene::nodes3 / top): the internal nodes of the
-    // deepest prefix of levels that fits kTopSlots, slots in preorder.
-    std::vector<float4> nodes3, top;
-    if (n2 > 0 && (size_t)hs.n_tris <= (1u << 20)) {
-        std::vector<int> depth(n2, 0), slot(n2 + 1, -1), per_level;
-        auto word = [&](size_t i, int k) { uint32_t w; std::memcpy(&w, k ? &hs.nodes[2 * i + 1].w : &hs.nodes[2 * i].w, 4); return w; };
-        auto is_leaf = [&](size_t i) { return (word(i, 1) & 2u) != 0u; };
-        for (size_t i = 0; i < n2; ++i) {
-            if ((size_t)depth[i] >= per_level.size()) per_level.resize(depth[i] + 1, 0);
-            if (is_leaf(i)) continue;
-            ++per_level[depth[i]];
-            const size_t r = word(i + 1, 0) & 0x7FFFFFFFu;      // right child = skip(left child)
-            depth[i + 1] = depth[i] + 1;
-            if (r < n2) depth[r] = depth[i] + 1;
-        }
-        // experiment knob RTAMD_TOP_LEVELS: at most this many levels (0: an
-        // empty top tree, walk 13 then loads every node from HBM/L2)
-        static const int max_levels = [] {
-            const char* v = std::getenv("RTAMD_TOP_LEVELS");
-            return v ? std::max(0, std::atoi(v)) : 64;
-        }();
-        int levels = 0, count = 0;
-        while (levels < std::min(max_levels, (int)per_level.size()) && count + per_level[levels] <= kTopSlots)
-            count += per_level[levels++];
-        int n_top = 0;
-        for (size_t i = 0; i < n2; ++i)
-            if (!is_leaf(i) && depth[i] < levels) slot[i] = n_top++;
-        nodes3 = nodes2;
-        for (size_t i = 0; i < n2; ++i) {
-            uint32_t w;
-            if (is_leaf(i)) {
-                std::memcpy(&w, &nodes2[2 * i].w, 4);
-                w = (w & 0x800FFFFFu) | ((uint32_t)(slot[i + 1] + 1) << 20);
-                std::memcpy(&nodes3[2 * i].w, &w, 4);
-            } else {
-                const size_t sk = word(i, 0) & 0x7FFFFFFFu;
-                std::memcpy(&w, &nodes2[2 * i + 1].w, 4);
-                w |= (uint32_t)(slot[sk <= n2 ? sk : n2] + 1) << 2 | (uint32_t)(slot[i + 1] + 1) << (2 + kTopBits);
-                std::memcpy(&nodes3[2 * i + 1].w, &w, 4);
-            }
-        }
-        top.resize(2 * (size_t)std::max(1, n_top), make_float4(0.f, 0.f, 0.f, 0.f));
-        for (size_t i = 0; i < n2; ++i)
-            if (slot[i] >= 0) {
-                top[2 * slot[i]] = nodes3[2 * i];
-                top[2 * slot[i] + 1] = nodes3[2 * i + 1];
-            }
-        top.resize(2 * (size_t)n_top);
-    }
     ctx->has_scene = false;
     for (PerDevice& p : ctx->dev) {
         RT_HIP_CHECK(hipSetDevice(p.device));
@@ -961,8 +862,8 @@ int rt_upload_scene(rt_ctx* ctx, const void* vertices, size_t vertex_bytes,
         s.n_tris = hs.n_tris;
         s.root_leaf = hs.root_leaf;
         std::memcpy(s.root_box, hs.root_box, sizeof s.root_box);
-        // nodes and leafs are padded so that a walker may always read four
-        // float4 from any record start (rt_trace.hip, walk 1).
+        // nodes and leafs are padded by one record: walks read the record at
+        // index end (the node after the last) before they test for the end.
         const size_t nn = (size_t)hs.n_nodes;
         const size_t nb = sizeof(float4) * (2 * nn + 2);
         const size_t lb = sizeof(float4) * (3 * nn + 1);
@@ -977,15 +878,6 @@ int rt_upload_scene(rt_ctx* ctx, const void* vertices, size_t vertex_bytes,
         if (e == hipSuccess) e = hipMalloc(&s.leafs2, leafs2.size() * sizeof(float4));
         if (e == hipSuccess) e = hipMemcpy(s.nodes2, nodes2.data(), nodes2.size() * sizeof(float4), hipMemcpyHostToDevice);
         if (e == hipSuccess) e = hipMemcpy(s.leafs2, leafs2.data(), leafs2.size() * sizeof(float4), hipMemcpyHostToDevice);
-        if (e == hipSuccess && !nodes3.empty()) {
-            e = hipMalloc(&s.nodes3, nodes3.size() * sizeof(float4));
-            if (e == hipSuccess) e = hipMalloc(&s.top, std::max<size_t>(1, top.size()) * sizeof(float4));
-            if (e == hipSuccess)
-                e = hipMemcpy(s.nodes3, nodes3.data(), nodes3.size() * sizeof(float4), hipMemcpyHostToDevice);
-            if (e == hipSuccess && !top.empty())
-                e = hipMemcpy(s.top, top.data(), top.size() * sizeof(float4), hipMemcpyHostToDevice);
-            s.n_top = (int)(top.size() / 2);
-        }
         if (e == hipSuccess) e = hipMalloc(&s.norms, kShadeStride * mb);
         if (e == hipSuccess) s.mats = s.norms + 1;
         if (e == hipSuccess && hs.n_nodes) e = hipMemcpy(s.nodes, hs.nodes, nb - 2 * sizeof(float4), hipMemcpyHostToDevice);
@@ -1163,14 +1055,10 @@ static int render_bands_on(const rt_ctx* ctx, PerDevice& p, const rt_camera_ubo*
 }
 
 static int collect_stats(const rt_ctx* ctx, PerDevice& p, uint64_t pixels, rt_stats* stats, bool accumulate) {
+    (void)ctx;
     Counters c;
     RT_HIP_CHECK(hipMemcpy(&c, p.d_counters, sizeof c, hipMemcpyDeviceToHost));
-    unsigned handoffs = 0;
-    const int kernel = effective_kernel(ctx);
-    if (kernel == kKernelSplit || kernel == kKernelTiered) {
-        const unsigned* src = p.d_queue + (kernel == kKernelSplit ? 1 : 2) * kQueueSlots + p.last_slot;
-        RT_HIP_CHECK(hipMemcpy(&handoffs, src, sizeof handoffs, hipMemcpyDeviceToHost));
-    }
+    const unsigned handoffs = 0;   // the schedules with a second pass are archived (round 3)
     float ms = 0.f;
     RT_HIP_CHECK(hipEventElapsedTime(&ms, p.ev0, p.ev1));
     if (!accumulate) std::memset(stats, 0, sizeof *stats);
@@ -1319,6 +1207,13 @@ int rt_render_async(rt_ctx* ctx, const rt_camera_ubo* cam, int width, int height
         // The slot's previous frame must be read back before it is overwritten.
         RT_HIP_CHECK(hipStreamWaitEvent(ts, p.copied[slot], 0));
         RT_HIP_CHECK(hipStreamWaitEvent(ts, p.copied2[slot], 0));
+        // A frame that reads and writes per-device state shared by the slots
+        // (the accumulation extension's running sums; the diagnostic records)
+        // must not overlap the previous frame: its trace waits for that one.
+        if (((ctx->ext & kExtAccumulate) || ctx->diag) && t > 1) {
+            const int prev = (int)((t - 1) % (uint64_t)S);
+            if (p.slot_ticket[prev] == t - 1) RT_HIP_CHECK(hipStreamWaitEvent(ts, p.traced[prev], 0));
+        }
         ctx->in_async = S;
         rc = render_bands_on(ctx, p, cam, width, height, max_bounces, bh, nd, k, rows, p.d_ring[slot], nullptr, ts,
                              false);
@@ -1328,15 +1223,16 @@ int rt_render_async(rt_ctx* ctx, const rt_camera_ubo* cam, int width, int height
         // Copies run in ticket order on the one copy stream, whatever order the
         // traces finish in.
         RT_HIP_CHECK(hipStreamWaitEvent(p.copy_stream, p.traced[slot], 0));
+        // copy_stream2 joins every frame, copying or not, so copied2[slot]
+        // always belongs to this slot's newest ticket (rt_render_wait)
+        RT_HIP_CHECK(hipStreamWaitEvent(p.copy_stream2, p.traced[slot], 0));
         if (nd == 1 && ctx->copy_streams == 2 && rows > 1) {
             // the frame's top and bottom halves on two copy streams, so two copy
             // engines read the frame back at once
             const size_t top = (size_t)width * (size_t)(rows / 2) * 4;
-            RT_HIP_CHECK(hipStreamWaitEvent(p.copy_stream2, p.traced[slot], 0));
             RT_HIP_CHECK(hipMemcpyAsync(out_rgba, p.d_ring[slot], top, hipMemcpyDeviceToHost, p.copy_stream));
             RT_HIP_CHECK(hipMemcpyAsync(out_rgba + top, reinterpret_cast<uint8_t*>(p.d_ring[slot]) + top,
                                         px * 4 - top, hipMemcpyDeviceToHost, p.copy_stream2));
-            RT_HIP_CHECK(hipEventRecord(p.copied2[slot], p.copy_stream2));
         } else if (nd == 1) {
             RT_HIP_CHECK(hipMemcpyAsync(out_rgba, p.d_ring[slot], px * 4, hipMemcpyDeviceToHost, p.copy_stream));
         } else {
@@ -1356,6 +1252,7 @@ int rt_render_async(rt_ctx* ctx, const rt_camera_ubo* cam, int width, int height
                                             p.copy_stream));
         }
         RT_HIP_CHECK(hipEventRecord(p.copied[slot], p.copy_stream));
+        RT_HIP_CHECK(hipEventRecord(p.copied2[slot], p.copy_stream2));
         p.slot_ticket[slot] = t;
     }
     ctx->issued = t;
@@ -1379,7 +1276,7 @@ int rt_render_wait(rt_ctx* ctx, uint64_t ticket) {
             if (p.slot_ticket[k2] >= ticket && (best < 0 || p.slot_ticket[k2] < p.slot_ticket[best])) best = k2;
         if (best >= 0) {
             RT_HIP_CHECK(hipEventSynchronize(p.copied[best]));
-            RT_HIP_CHECK(hipEventSynchronize(p.copied2[best]));   // not recorded (one copy stream): returns at once
+            RT_HIP_CHECK(hipEventSynchronize(p.copied2[best]));   // recorded for every frame (rt_render_async)
         } else {
             RT_HIP_CHECK(hipStreamSynchronize(p.copy_stream));   // a device with no rows of that frame
             RT_HIP_CHECK(hipStreamSynchronize(p.copy_stream2));
@@ -1390,28 +1287,23 @@ int rt_render_wait(rt_ctx* ctx, uint64_t ticket) {
 
 int rt_set_option(rt_ctx* ctx, const char* name, int64_t value) {
     if (!ctx || !name) { set_error("rt_set_option: null argument"); return RT_ERR_INVALID_ARG; }
-    if (std::strcmp(name, "kernel") == 0 && value >= kKernelSimple && value <= kKernelTiered) {
-        ctx->kernel = (int)value;
-    } else if (std::strcmp(name, "shade_min") == 0 && value >= 1 && value <= 64) {
-        ctx->shade_min = (int)value;
-    } else if (std::strcmp(name, "blocks_per_cu") == 0 && value >= 0 && value <= 32) {
-        ctx->blocks_per_cu = (int)value;
-    } else if (std::strcmp(name, "seg_limit") == 0 && value >= 1 && value <= 1024) {
-        ctx->seg_limit = (int)value;
-    } else if (std::strcmp(name, "heavy_budget") == 0 && value >= 1 && value <= (1 << 30)) {
-        ctx->heavy_budget = (int)value;
-    } else if (std::strcmp(name, "prio_after") == 0 && value >= 0 && value <= (1 << 30)) {
-        ctx->prio_after = (int)value;
+    static const char* const archived[] = {"shade_min", "blocks_per_cu", "seg_limit", "heavy_budget", "prio_after"};
+    for (const char* a : archived)
+        if (std::strcmp(name, a) == 0) {
+            set_error("rt_set_option: %s belonged to a schedule archived in round 3 (profiles/r03/archive)", name);
+            return RT_ERR_INVALID_ARG;
+        }
+    if (std::strcmp(name, "kernel") == 0 && value == 0) {
+        // the one kernel (kernels 1-3, persistent / split / tiered, are archived)
     } else if (std::strcmp(name, "coop_lanes") == 0 && value >= 0 && value <= 64) {
         ctx->coop_lanes = (int)value;
     } else if (std::strcmp(name, "extensions") == 0 && value >= 0 && value <= 15) {
         ctx->ext = (int)value;
-    } else if (std::strcmp(name, "walk") == 0 && ((value >= 0 && value <= 2) || value == kWalkScalar ||
-                                                  value == kWalkDma || value == kWalkTop)) {
+    } else if (std::strcmp(name, "walk") == 0 && (value == 0 || value == 2)) {
         ctx->walk = (int)value;
     } else if (std::strcmp(name, "coop_walk") == 0 && (value == 0 || value == 1)) {
         ctx->coop_walk = (int)value;
-    } else if (std::strcmp(name, "block_waves") == 0 && (value == 1 || value == 4 || value == 8 || value == 16)) {
+    } else if (std::strcmp(name, "block_waves") == 0 && (value == 1 || value == 4)) {
         ctx->block_waves = (int)value;
     } else if (std::strcmp(name, "heavy_first") == 0 && (value == 0 || value == 1)) {
         ctx->heavy_first = (int)value;
@@ -1452,12 +1344,8 @@ int rt_set_option(rt_ctx* ctx, const char* name, int64_t value) {
 
 int rt_get_option(rt_ctx* ctx, const char* name, int64_t* value) {
     if (!ctx || !name || !value) { set_error("rt_get_option: null argument"); return RT_ERR_INVALID_ARG; }
-    if (std::strcmp(name, "kernel") == 0) *value = ctx->kernel;
-    else if (std::strcmp(name, "shade_min") == 0) *value = ctx->shade_min;
+    if (std::strcmp(name, "kernel") == 0) *value = 0;
     else if (std::strcmp(name, "wave_tile") == 0) *value = ctx->wave_tile;
-    else if (std::strcmp(name, "seg_limit") == 0) *value = ctx->seg_limit;
-    else if (std::strcmp(name, "prio_after") == 0) *value = ctx->prio_after;
-    else if (std::strcmp(name, "heavy_budget") == 0) *value = ctx->heavy_budget;
     else if (std::strcmp(name, "coop_lanes") == 0) *value = ctx->coop_lanes;
     else if (std::strcmp(name, "walk") == 0) *value = ctx->walk;
     else if (std::strcmp(name, "coop_walk") == 0) *value = ctx->coop_walk;
@@ -1478,8 +1366,11 @@ int rt_get_option(rt_ctx* ctx, const char* name, int64_t* value) {
     else if (std::strcmp(name, "heavy_pixels_used") == 0) *value = ctx->dev.empty() ? 0 : ctx->dev[0].last_heavy_px;
     else if (std::strcmp(name, "heavy_tiles_used") == 0) *value = ctx->dev.empty() ? 0 : ctx->dev[0].last_heavy;
     else if (std::strcmp(name, "extensions") == 0) *value = ctx->ext;
-    else if (std::strcmp(name, "blocks_per_cu") == 0)
-        *value = ctx->blocks_per_cu > 0 ? ctx->blocks_per_cu : (ctx->dev.empty() ? 0 : ctx->dev[0].blocks_per_cu);
+    else if (std::strcmp(name, "hw_queues") == 0) *value = ctx->hw_queues;
+    // 1 when rt_render_async's slots cannot each have a hardware queue of their
+    // own (async_slots + 2 > hw_queues: the slots' traces then share queues and
+    // run one after another); start the host with GPU_MAX_HW_QUEUES >= slots + 2
+    else if (std::strcmp(name, "queues_short") == 0) *value = ctx->async_slots + 2 > ctx->hw_queues ? 1 : 0;
     else { set_error("rt_get_option: unknown option %s", name); return RT_ERR_INVALID_ARG; }
     return RT_OK;
 }

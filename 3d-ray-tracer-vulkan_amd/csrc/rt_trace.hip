@@ -14,18 +14,18 @@
 // same nodes, runs the same triangle tests in the same order and sees the same
 // closest_t at each test, so frames and work counters are identical.
 //
-// Schedules of the same per-pixel work:
-//   trace_simple      one lane = one pixel for its whole path; a wave is a
-//                     tile of 64 pixels (the reference's 8x8 dispatch shape, or
-//                     16x4 / 32x2 / 64x1).  With the cooperative tail, once at
-//                     most coop_lanes lanes of a wave are still walking, the
-//                     whole wave finishes their walks one ray at a time with
-//                     coop_walk.
-//   trace_persistent  persistent waves pulling 8x8 tiles from a queue; lanes
-//                     refill when their path ends; shading is deferred until
-//                     shade_min lanes are ready.
-//   split / tiered    trace_simple for the first part of every path, then the
-//                     rest on trace_persistent (resume) or trace_coop.
+// The kernel, trace_simple: one lane = one pixel for its whole path; a wave
+// is a tile of 64 pixels (the reference's 8x8 dispatch shape, or 16x4 / 32x2
+// / 64x1).  With the cooperative tail, once at most coop_lanes lanes of a wave
+// are still walking, the whole wave finishes their walks one ray at a time
+// with coop_walk; with a learned heavy-first order the heaviest pixels are
+// traced one per wave (heavy_pixel) at the front of the same launch.  A launch
+// covers one frame's tile, its interleaved / listed row bands, or the same
+// rows of a batch of frames (one camera and output slice each).
+//
+// Round 3 archived the schedules that measured slower (persistent waves,
+// split, tiered, child-pair walk 1, scalar walk 5, LDS top-tree walk 13,
+// LDS-DMA walk 14): profiles/r03/archive/README.md.
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
@@ -152,21 +152,6 @@ __device__ __forceinline__ bool tri_test(float4 P0, float4 P1, float4 P2, V3 o, 
 // turn one memory round trip into two dependent ones).
 __device__ __forceinline__ void pin(float4& q) { asm volatile("" : "+v"(q.x), "+v"(q.y), "+v"(q.z), "+v"(q.w)); }
 
-// walk 5: a read-only scene array seen through the constant address space, so
-// that a load at a wave-uniform index is a scalar load (scalar cache), which
-// costs the vector memory pipeline nothing
-typedef float v4f __attribute__((ext_vector_type(4)));
-typedef const v4f __attribute__((address_space(4)))* ConstF4;
-__device__ __forceinline__ float4 ld_nt(const float4* p) {   // RT_NT_LEAF experiment
-    const v4f v = __builtin_nontemporal_load(reinterpret_cast<const v4f*>(p));
-    return make_float4(v.x, v.y, v.z, v.w);
-}
-__device__ __forceinline__ float4 ld_const(const float4* p, int i) {
-    const v4f v = ((ConstF4)(uintptr_t)p)[i];
-    return make_float4(v.x, v.y, v.z, v.w);
-}
-__device__ __forceinline__ void pin(uint2& q) { asm volatile("" : "+v"(q.x), "+v"(q.y)); }
-
 // One node of the walk.  `leaf` says whether node i is a leaf (from its
 // predecessor's L bits), so the leaf's triangle is fetched in the same round
 // trip as the node.  Returns the next node index and updates `leaf`.
@@ -285,17 +270,7 @@ __device__ __forceinline__ V3 sky_color(V3 d) {                          // getS
 __device__ __forceinline__ void write_pixel(const TraceArgs& a, int lx, int ly, V3 fin) {
     const V3 g = {sqrtf(fin.x), sqrtf(fin.y), sqrtf(fin.z)};              // :235
     const size_t p = (size_t)ly * (size_t)a.tw + (size_t)lx;
-#if RT_NT_STORE
-    // experiment: the frame is written once and read by the next stage, not by
-    // this kernel; a non-temporal store keeps it from evicting walk records
-    if (a.out_rgba) {
-        const uchar4 c = make_uchar4(unorm8(g.x), unorm8(g.y), unorm8(g.z), 255);
-        const uint32_t v = (uint32_t)c.x | ((uint32_t)c.y << 8) | ((uint32_t)c.z << 16) | ((uint32_t)c.w << 24);
-        __builtin_nontemporal_store(v, reinterpret_cast<uint32_t*>(a.out_rgba) + p);
-    }
-#else
     if (a.out_rgba) a.out_rgba[p] = make_uchar4(unorm8(g.x), unorm8(g.y), unorm8(g.z), 255);
-#endif
     if (a.out_rad) {
         a.out_rad[3 * p + 0] = g.x;
         a.out_rad[3 * p + 1] = g.y;
@@ -625,17 +600,14 @@ __device__ __forceinline__ void diag_stamp(unsigned long long* rec, int which) {
 
 // Optional features of trace_simple, compiled in only where a schedule needs
 // them so the default inner loop carries no extra work.
+// (Bits 1, 2 and 4 belonged to the archived split / tiered / priority
+// schedules; the values are kept so kernel names in old profiles still match.)
 constexpr int kDiagWords = 8;     // per-wave diag record (rtamd.h rt_diag_copy)
-constexpr int kFeatSpill = 1;     // split schedule: hand paths on after seg_limit segments
-constexpr int kFeatHeavy = 2;     // tiered schedule: hand walks on after heavy_budget visits
-constexpr int kFeatPrio = 4;      // raise wave priority after prio_after visits
 constexpr int kFeatCoopTail = 8;  // finish the last coop_lanes walks of a wave cooperatively
 constexpr int kFeatExt = kFeatExtBit;   // non-reference extensions (option "extensions", kExt*)
 constexpr int kFeatFrontier = 32; // cooperative tail uses frontier_walk (option coop_walk = 1)
 
 constexpr int kFeatFused = 64;    // heavy tiles in the same launch: workgroups k < 64 * split_n run heavy_pixel
-
-constexpr int kStack = 8;                    // per-lane t_enter stack entries in LDS (walk 1)
 
 // One pixel of a heavy tile, the whole wave on it (option heavy_fused, the
 // workgroups in front of the tile workgroups of the same launch): every
@@ -696,7 +668,6 @@ __device__ __forceinline__ void heavy_pixel(const TraceArgs& a, int lx, int ly, 
         flush_counters(a.counters, c_seg, c_node, c_tri, c_mat);
     }
 }
-constexpr int kPair = 0, kLeaf = 1, kNode = 2, kSkip = 3;   // walk 1: record kinds
 
 // Occupancy floor for trace_simple (waves per SIMD).  Unconstrained, the
 // walk-2 build takes ~70 VGPRs (7 waves).  One frame at a time more waves did
@@ -710,35 +681,19 @@ constexpr int kPair = 0, kLeaf = 1, kNode = 2, kSkip = 3;   // walk 1: record ki
 #ifndef RT_SIMPLE_WPE
 #define RT_SIMPLE_WPE 8
 #endif
-template <bool COUNT, bool DIAG = false, int FEAT = 0, int WALK = 1>
-__global__ __launch_bounds__(WALK == kWalkTop ? 1024 : 256)
+template <bool COUNT, bool DIAG = false, int FEAT = 0, int WALK = 2>
+__global__ __launch_bounds__(256)
 __attribute__((amdgpu_waves_per_eu((FEAT & kFeatFrontier) ? 1 : RT_SIMPLE_WPE)))
 void trace_simple(TraceArgs a) {
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
-    // walk 13: the top tree's records (DevScene::top), one copy per workgroup
-    // of block_waves (8 or 16) waves, read by every walking lane whose next
-    // node is in it instead of a global load
-    __shared__ float4 topl[WALK == kWalkTop ? 2 * kTopSlots : 1];
-    // walk 14: the stage a uniform step's LDS-DMA fetch lands in (one float4
-    // per lane: global_load_lds writes base + lane x 16; one-wave workgroups)
-    __shared__ float4 dstage[WALK == kWalkDma ? 64 : 1];
-    if (WALK == kWalkTop) {
-        const int nt2 = 2 * a.scene.n_top;
-        for (int i = threadIdx.x; i < nt2; i += blockDim.x) topl[i] = a.scene.top[i];
-        __syncthreads();
-    }
     unsigned long long* drec = nullptr;
     if (DIAG) {
         drec = a.diag + kDiagWords * (size_t)((blockIdx.y * gridDim.x + blockIdx.x) * a.block_waves + wave);
         diag_stamp(drec, 0);
     }
-    // walk 1: the right siblings still to visit, as (t_enter or +inf, R | L(R) << 31),
-    // newest kStack per lane; older ones are dropped and found again by skip pointers.
-    __shared__ uint2 stk[WALK == 1 ? kStack : 1][256];
-    // frontier_walk's per-wave frontier (cooperative tail)
     // frontier_walk's per-wave frontiers (kFCap entries per wave; dynamic LDS,
-    // sized by the launch for variants with kFeatFrontier)
+    // sized by the launch for variants with kFeatFrontier or kFeatFused)
     extern __shared__ uint4 fr[];
     // One wave = one tile of 64 pixels, (8 << s) x (8 >> s) with s = a.wave_tile
     // (s = 0: 8x8, the reference's local_size 8x8x1, compute_dynamic_ray.comp:157);
@@ -754,8 +709,7 @@ void trace_simple(TraceArgs a) {
     int bx = blockIdx.x, by = blockIdx.y, sub = -1;
     unsigned long long skip_lanes = 0;                   // heavy pixels this tile wave leaves out
     if (a.tile_order) {                                  // 1-D grid over the ordered tiles
-        // walk 13: a workgroup's waves take consecutive tiles of the order
-        const int k = WALK == kWalkTop ? blockIdx.x * a.block_waves + wave : blockIdx.x;
+        const int k = blockIdx.x;
         int t;
         if ((FEAT & kFeatFused) && k < a.n_heavy_px) {   // a heavy pixel (tile * 64 + lane), dispatched first
             const int q = a.heavy_px[k];
@@ -785,7 +739,7 @@ void trace_simple(TraceArgs a) {
         }
     }
     const int tl = sub >= 0 ? sub : lane;                // the tile pixel this lane traces
-    const int col = (WALK == kWalkTop && a.tile_order) ? bx : bx * a.block_waves + wave;   // wave-tile column
+    const int col = bx * a.block_waves + wave;           // wave-tile column
     const int lx = col * tw_w + (tl & (tw_w - 1));
     const int ly = by * th_w + (tl >> (3 + s));
     const bool pixel = lx < a.tw && ly < a.th && (sub < 0 || lane == 0) && !((skip_lanes >> lane) & 1ull);
@@ -794,10 +748,7 @@ void trace_simple(TraceArgs a) {
     const float4* __restrict__ leafs = a.scene.leafs;
     const float4* __restrict__ pairs = a.scene.pairs;
     const int end = a.scene.end;
-    const V3 rlo = {a.scene.root_box[0], a.scene.root_box[1], a.scene.root_box[2]};
-    const V3 rhi = {a.scene.root_box[3], a.scene.root_box[4], a.scene.root_box[5]};
     unsigned long long c_seg = 0, c_node = 0, c_tri = 0, c_mat = 0;
-    int steps = 0;
     unsigned long long d_iters = 0, d_windows = 0, d_coop_t = 0;   // diag builds only
     unsigned long long d_lane_windows = 0;           // diag: cooperative windows spent on this lane's walks
 
@@ -821,13 +772,6 @@ void trace_simple(TraceArgs a) {
     // every lane of the wave.
     for (int b = 0; b < a.max_bounces; ++b) {
         if (__ballot(alive) == 0) break;
-        if ((FEAT & kFeatSpill) && alive && b == a.seg_limit) {           // hand the path on
-            PathState* st = a.spill + atomicAdd(a.spill_count, 1u);
-            st->q0 = make_float4(o.x, o.y, o.z, att.x);
-            st->q1 = make_float4(d.x, d.y, d.z, att.y);
-            st->q2 = make_float4(att.z, __uint_as_float(seed), __int_as_float(b), __int_as_float(lx | (ly << 16)));
-            alive = false;
-        }
         float closest = kTMax;
         int hit = -1;
         const V3 inv = {1.0f / d.x, 1.0f / d.y, 1.0f / d.z};              // :89
@@ -835,24 +779,11 @@ void trace_simple(TraceArgs a) {
         int n = 0;
         bool nleaf = a.scene.root_leaf != 0;
         bool walking = alive && end > 0;
-        // walk 1 state: n's t_enter (+inf: its slab test failed) unless nload
-        // (n's own box still to be read); done_n: n is finished; skip(n) if known
-        // (else -1); the stack depth and its lowest entry still held; the kind
-        // of record the next load fetches.
-        float nte = __builtin_inff();
-        int nskip = end, sp = 0, lo = 0, kind = kPair;
-        bool lost = false, nload = false, done_n = false;
-        if (WALK == 1 && walking) {
-            float te;
-            bool ind;
-            slab(make_float4(rlo.x, rlo.y, rlo.z, 0.f), make_float4(rhi.x, rhi.y, rhi.z, 0.f), o, inv, te, ind);
-            nte = ind ? te : __builtin_inff();
-        }
         if (COUNT && alive) {
             ++c_seg;
             if (end > 0) ++c_node;                                       // the root visit
         }
-        if (WALK == 0 || WALK == 2 || WALK == kWalkScalar || WALK == kWalkDma || WALK == kWalkTop) {
+        {
             // The per-node walk: one dependent load per visit, lanes in lockstep.
             // walk 2, software-pipelined: the next node's box is requested as soon as
             // this node's slab test has chosen it, before this node's triangle
@@ -860,21 +791,12 @@ void trace_simple(TraceArgs a) {
             // walk 2 reads the compact records (DevScene::nodes2 / leafs2): a
             // leaf's node record carries its triangle index and v0.x, and Q0, Q1
             // the rest of its triangle.
-            // walk 13 reads nodes3 (nodes2 + the top-tree slots of the next
-            // nodes) and, for a next node in the top tree, its LDS copy.
             float4 A, B, Q0, Q1;
-            const float4* __restrict__ nodes2 = WALK == kWalkTop ? a.scene.nodes3 : a.scene.nodes2;
+            const float4* __restrict__ nodes2 = a.scene.nodes2;
             const float4* __restrict__ leafs2 = a.scene.leafs2;
-            if ((WALK == 2 || WALK == kWalkScalar || WALK == kWalkDma || WALK == kWalkTop) && walking) {
-                if (WALK == kWalkTop && !nleaf && a.scene.n_top > 0) {   // an internal root is slot 0
-                    A = topl[0];
-                    B = topl[1];
-                    pin(A);
-                    pin(B);
-                } else {
-                    A = nodes2[2 * n];
-                    B = nodes2[2 * n + 1];
-                }
+            if (WALK == 2 && walking) {
+                A = nodes2[2 * n];
+                B = nodes2[2 * n + 1];
                 if (nleaf) {
                     Q0 = leafs2[2 * n + 0];
                     Q1 = leafs2[2 * n + 1];
@@ -882,10 +804,6 @@ void trace_simple(TraceArgs a) {
             }
             while (walking) {
                 if (DIAG) ++d_iters;
-                if (FEAT & (kFeatPrio | kFeatHeavy)) ++steps;
-                // A wave still walking after prio_after steps holds the frame's
-                // critical path: let it win instruction arbitration.
-                if ((FEAT & kFeatPrio) && steps == a.prio_after) __builtin_amdgcn_s_setprio(3);
                 if (WALK == 0) {
                     n = node_step<COUNT>(nodes, leafs, n, nleaf, o, d, inv, closest, hit, c_node, c_tri);
                 } else {
@@ -898,265 +816,27 @@ void trace_simple(TraceArgs a) {
                     const int nxt = (hb || nleaf) ? n + 1 : (int)(aw & kIdx);
                     const bool nl = (((hb && !nleaf) ? bw : (aw >> 31)) & 1u) != 0u;
                     const float v0x = B.w;                                   // a leaf's v0.x
-                    int u = 0;                                               // walk 5: the uniform next node
-                    bool uni = false;
-                    bool staged = false;                                     // walk 14: records in dstage
-                    int l0 = 0, l1 = 0, l2 = 0, l3 = 0;                      // walk 14: lanes holding them
                     if (COUNT && hb && !nleaf) c_node += 2;
-                    if (WALK == kWalkTop) {
-                        // the next node's top-tree slot (-1: not in it): a leaf's
-                        // next is i+1; an internal node's i+1 on a hit, skip on a miss
-                        const int ts = (int)((nleaf ? (aw >> 20) : (bw >> (hb ? 2 + kTopBits : 2))) &
-                                             (uint32_t)kTopSlots) - 1;
-                        if (ts >= 0) {
-                            // the pins keep the compiler from merging this and
-                            // the global load into one flat (TA-path) load
-                            A = topl[2 * ts];
-                            B = topl[2 * ts + 1];
-                            pin(A);
-                            pin(B);
-                        } else {
-                            A = nodes2[2 * nxt];
-                            B = nodes2[2 * nxt + 1];
-                        }
-                    } else if (WALK == kWalkDma) {
-                        // walk 14: when every walking lane moves to one node, the
-                        // first 2 (4 with its leaf) walking lanes fetch its records
-                        // straight into LDS, one float4 each, in ONE instruction
-                        // (global_load_lds_dwordx4: ~20 cycles of the vector memory
-                        // pipeline against ~36 for two dwordx4 in every lane,
-                        // tools/ubench/lds_dma_cost.hip); the wave reads them back
-                        // after this node's triangle test
-                        u = __builtin_amdgcn_readfirstlane(nxt);
-                        const uint64_t act = __ballot(true);
-                        const bool nlu = __builtin_amdgcn_readfirstlane(nl ? 1 : 0) != 0 && u < end;
-                        const int need = nlu ? 4 : 2;
-                        staged = __ballot(nxt != u) == 0 && __popcll(act) >= need;
-                        if (staged) {
-                            const int rank = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(act >> 32),
-                                                                            __builtin_amdgcn_mbcnt_lo((uint32_t)act, 0u));
-                            if (rank < need) {
-                                const float4* src = rank < 2 ? nodes2 + 2 * u + rank : leafs2 + 2 * u + (rank - 2);
-                                __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(src),
-                                                                 (__attribute__((address_space(3))) void*)(dstage),
-                                                                 16, 0, 0);
-                            }
-                            uint64_t m = act;
-                            l0 = __builtin_ctzll(m);
-                            m &= m - 1;
-                            l1 = __builtin_ctzll(m);
-                            m &= m - 1;
-                            l2 = nlu ? __builtin_ctzll(m) : 0;
-                            m &= m - 1;
-                            l3 = nlu ? __builtin_ctzll(m) : 0;
-                        } else {
-                            A = nodes2[2 * nxt];
-                            B = nodes2[2 * nxt + 1];
-                        }
-                    } else if (WALK == kWalkScalar) {
-                        // walk 5: when every walking lane moves to one node (~9
-                        // steps in 10), its records come through the scalar cache;
-                        // the vector memory pipeline bounds the lockstep walk (§7)
-                        u = __builtin_amdgcn_readfirstlane(nxt);
-                        uni = __ballot(nxt != u) == 0;
-                        if (uni) {
-                            A = ld_const(nodes2, 2 * u);                     // index end is padding
-                            B = ld_const(nodes2, 2 * u + 1);
-                        } else {
-                            A = nodes2[2 * nxt];
-                            B = nodes2[2 * nxt + 1];
-                        }
-                    } else {
-                        A = nodes2[2 * nxt];                                 // index end is padding
-                        B = nodes2[2 * nxt + 1];
-                    }
+                    A = nodes2[2 * nxt];                                     // index end is padding
+                    B = nodes2[2 * nxt + 1];
                     if (hb && nleaf) {                                       // hit_triangle (:196-200)
                         if (COUNT) ++c_tri;
                         float t;
                         if (tri_test(make_float4(v0x, Q0.x, Q0.y, 0.f), make_float4(Q0.z, Q0.w, Q1.x, 0.f),
                                      make_float4(Q1.y, Q1.z, Q1.w, 0.f), o, d, t) && t < closest) {
                             closest = t;
-                            hit = (int)(aw & (WALK == kWalkTop ? 0xFFFFFu : kTri));
+                            hit = (int)(aw & kTri);
                         }
                     }
-                    if (WALK == kWalkDma && staged) {
-                        __builtin_amdgcn_s_waitcnt(0);                       // the LDS-DMA fetch has landed
-                        A = dstage[l0];
-                        B = dstage[l1];
-                        if (nl && nxt < end) {
-                            Q0 = dstage[l2];
-                            Q1 = dstage[l3];
-                        }
-                    } else if (WALK == kWalkScalar && uni) {
-                        // the leaf bit belongs to node u: the same in every lane
-                        if (__builtin_amdgcn_readfirstlane(nl ? 1 : 0) && u < end) {
-                            Q0 = ld_const(leafs2, 2 * u + 0);
-                            Q1 = ld_const(leafs2, 2 * u + 1);
-                        }
-                    } else if (nl && nxt < end) {
-#if RT_NT_LEAF
-                        // experiment: a leaf's triangle is read by few waves;
-                        // non-temporal loads keep it from evicting node records
-                        Q0 = ld_nt(leafs2 + 2 * nxt + 0);
-                        Q1 = ld_nt(leafs2 + 2 * nxt + 1);
-#else
+                    if (nl && nxt < end) {
                         Q0 = leafs2[2 * nxt + 0];
                         Q1 = leafs2[2 * nxt + 1];
-#endif
                     }
                     n = nxt;
                     nleaf = nl;
                 }
                 walking = n < end;
-                if (FEAT & kFeatHeavy) walking = walking && steps < a.heavy_budget;
                 if ((FEAT & kFeatCoopTail) && __popcll(__ballot(walking)) <= coop_lanes) break;
-            }
-            if ((FEAT & kFeatHeavy) && alive && n < end && steps >= a.heavy_budget) {   // hand the walk on
-                HeavyRay* hv = a.heavy + atomicAdd(a.heavy_count, 1u);
-                hv->p.q0 = make_float4(o.x, o.y, o.z, att.x);
-                hv->p.q1 = make_float4(d.x, d.y, d.z, att.y);
-                hv->p.q2 = make_float4(att.z, __uint_as_float(seed), __int_as_float(b),
-                                       __int_as_float(lx | (ly << 16)));
-                hv->q3 = make_float4(closest, __int_as_float(n), __int_as_float(hit), 0.f);
-                alive = false;
-                walking = false;
-            }
-        } else for (;;) {
-            if (WALK == 1 && walking) {
-                // Advance, without memory traffic, to the next visit that
-                // needs a record: misses are counted and popped here.
-                for (;;) {
-                    if (!done_n) {
-                        if (nload) {
-                            if (n >= end) walking = false;
-                            kind = kNode;
-                            break;
-                        }
-                        if (nte < closest) {
-                            kind = nleaf ? kLeaf : kPair;
-                            break;
-                        }
-                        // n's box is missed: its subtree is finished
-                    }
-                    done_n = false;
-                    if (sp > lo) {                                // the reference's next pop
-                        --sp;
-                        uint2 e = stk[sp & (kStack - 1)][threadIdx.x];
-                        pin(e);
-                        nte = __uint_as_float(e.x);
-                        n = (int)(e.y & kIdx);
-                        nleaf = (e.y >> 31) != 0u;
-                        nskip = -1;
-                        continue;
-                    }
-                    if (!lost) {
-                        walking = false;
-                        break;
-                    }
-                    // Entries were dropped: the next node is skip(n) in preorder.
-                    if (nskip >= 0) {
-                        n = nskip;
-                        nload = true;
-                        continue;
-                    }
-                    kind = kSkip;                                 // skip(n) is in n's own record
-                    break;
-                }
-            }
-            const uint64_t wm = __ballot(walking);
-            if (wm == 0) break;
-            if ((FEAT & kFeatCoopTail) && __popcll(wm) <= coop_lanes) break;
-            if (!walking) continue;
-            if (FEAT & (kFeatPrio | kFeatHeavy)) ++steps;
-            // A wave still walking after prio_after steps holds the frame's
-            // critical path: let it win instruction arbitration.
-            if ((FEAT & kFeatPrio) && steps == a.prio_after) __builtin_amdgcn_s_setprio(3);
-            if ((FEAT & kFeatHeavy) && steps >= a.heavy_budget) {      // hand the walk on
-                const int start = (WALK == 1 && kind == kSkip) ? (int)(__float_as_uint(nodes[2 * n].w) & kIdx) : n;
-                HeavyRay* hv = a.heavy + atomicAdd(a.heavy_count, 1u);
-                hv->p.q0 = make_float4(o.x, o.y, o.z, att.x);
-                hv->p.q1 = make_float4(d.x, d.y, d.z, att.y);
-                hv->p.q2 = make_float4(att.z, __uint_as_float(seed), __int_as_float(b),
-                                       __int_as_float(lx | (ly << 16)));
-                hv->q3 = make_float4(closest, __int_as_float(start), __int_as_float(hit), 0.f);
-                alive = false;
-                walking = false;
-                continue;
-            }
-            if (WALK == 0) {
-                n = node_step<COUNT>(nodes, leafs, n, nleaf, o, d, inv, closest, hit, c_node, c_tri);
-                walking = n < end;
-                continue;
-            }
-            // One record per lane per step, whatever its kind (arrays padded
-            // so that four float4 are always readable).
-            const float4* rp = kind == kPair ? pairs + 4 * n : kind == kLeaf ? leafs + 3 * n : nodes + 2 * n;
-            float4 Q0 = rp[0];
-            float4 Q1 = rp[1];
-            float4 Q2 = rp[2];
-            float4 Q3 = rp[3];
-            pin(Q0);
-            pin(Q1);
-            pin(Q2);
-            pin(Q3);
-            if (kind == kPair) {
-                // n is a hit internal node: its two children are visited
-                // (counted here).  Both slab tests at once; a child whose box
-                // already misses at this closest_t misses at every later one,
-                // so only live children are walked or stacked.
-                if (COUNT) c_node += 2;
-                float teL, teR;
-                bool indL, indR;
-                slab(Q0, Q1, o, inv, teL, indL);
-                slab(make_float4(Q0.w, Q1.w, Q2.w, 0.f), Q2, o, inv, teR, indR);
-                const uint32_t rw = __float_as_uint(Q3.x);
-                const int skp = (int)__float_as_uint(Q3.z);
-                const float tL = indL ? teL : __builtin_inff();
-                const float tR = indR ? teR : __builtin_inff();
-                const bool hL = tL < closest, hR = tR < closest;
-                if (hL) {
-                    if (hR) {                                     // R waits on the stack
-                        stk[sp & (kStack - 1)][threadIdx.x] = make_uint2(__float_as_uint(tR), rw);
-                        ++sp;
-                        if (sp - lo > kStack) {
-                            lo = sp - kStack;
-                            lost = true;
-                        }
-                    }
-                    n = n + 1;
-                    nte = tL;
-                    nleaf = __float_as_uint(Q3.y) != 0u;
-                    nskip = hR ? (int)(rw & kIdx) : skp;
-                } else if (hR) {
-                    n = (int)(rw & kIdx);
-                    nte = tR;
-                    nleaf = (rw >> 31) != 0u;
-                    nskip = skp;
-                } else {
-                    done_n = true;
-                    nskip = skp;
-                }
-            } else if (kind == kLeaf) {
-                // n is a hit leaf: the triangle test (:196-200).
-                if (COUNT) ++c_tri;
-                float t;
-                if (tri_test(Q0, Q1, Q2, o, d, t) && t < closest) {
-                    closest = t;
-                    hit = __float_as_int(Q0.w);
-                }
-                done_n = true;
-                nskip = n + 1;
-            } else if (kind == kNode) {
-                float te;
-                bool ind;
-                slab(Q0, Q1, o, inv, te, ind);
-                nte = ind ? te : __builtin_inff();
-                nleaf = (__float_as_uint(Q1.w) & 2u) != 0u;
-                nskip = (int)(__float_as_uint(Q0.w) & kIdx);
-                nload = false;
-            } else {
-                n = (int)(__float_as_uint(Q0.w) & kIdx);
-                nload = true;
             }
         }
         if (FEAT & kFeatCoopTail) {
@@ -1174,8 +854,7 @@ void trace_simple(TraceArgs a) {
                 float bc = lane_f(closest, L);
                 int bh = lane_i(hit, L);
                 unsigned long long cn = 0, ct = 0;   // wave-uniform: counted once, by lane L
-                int start = n;
-                if (WALK == 1 && kind == kSkip && lane == L) start = (int)(__float_as_uint(nodes[2 * n].w) & kIdx);
+                const int start = n;
                 int nw = 0;
                 if ((FEAT & kFeatFrontier) && a.coop_walk) {
                     int p = lane_i(start, L);
@@ -1263,482 +942,100 @@ void trace_simple(TraceArgs a) {
     }
 }
 
-// -------------------------------------------------------- persistent kernel --
-
-constexpr int kIdle = 0, kTrace = 1, kReady = 2;
-
-template <bool COUNT>
-__global__ __launch_bounds__(256) void trace_persistent(TraceArgs a) {
-    const int lane = threadIdx.x & 63;
-    const int tiles_x = (a.tw + 7) >> 3;
-    // Work slots: 8x8 pixel tiles in row-major tile order, or (resume) the
-    // paths the simple pass spilled, in spill order.
-    const int n_slots = a.resume ? (int)*a.spill_count : tiles_x * ((a.th + 7) >> 3) * 64;
-    const float4* __restrict__ nodes = a.scene.nodes;
-    const float4* __restrict__ leafs = a.scene.leafs;
-    const int end = a.scene.end;
-    const int shade_min = a.shade_min;
-    const bool root_leaf = a.scene.root_leaf != 0;
-
-    unsigned long long c_seg = 0, c_node = 0, c_tri = 0, c_mat = 0;
-    int pool_next = 0, pool_end = 0;     // wave-uniform: this wave's unclaimed slots
-    bool exhausted = false;              // wave-uniform: the global queue is empty
-
-    int mode = kIdle;
-    int lx = 0, ly = 0, b = 0, node = 0, hit = -1;
-    bool leaf = root_leaf;
-    uint32_t seed = 0;
-    float closest = kTMax;
-    V3 o = {0.f, 0.f, 0.f}, d = {0.f, 0.f, 1.f}, inv = {0.f, 0.f, 1.f}, att = {1.f, 1.f, 1.f};
-
-    for (;;) {
-        // ---- refill idle lanes (consecutive slots = one 8x8 tile / spill order)
-        uint64_t idle = __ballot(mode == kIdle);
-        while (idle != 0 && !exhausted) {
-            if (pool_next >= pool_end) {
-                int base = 0;
-                if (lane == 0) base = (int)atomicAdd(a.queue, 64u);
-                base = __shfl(base, 0);
-                if (base >= n_slots) { exhausted = true; break; }
-                pool_next = base;
-                pool_end = base + 64;
-            }
-            const int avail = pool_end - pool_next;
-            const int rank = lanes_below(idle);
-            if (mode == kIdle && rank < avail) {
-                const int slot = pool_next + rank;
-                bool start = false;
-                if (a.resume) {
-                    if (slot < n_slots) {
-                        const PathState p = a.spill[slot];
-                        o = {p.q0.x, p.q0.y, p.q0.z};
-                        d = {p.q1.x, p.q1.y, p.q1.z};
-                        att = {p.q0.w, p.q1.w, p.q2.x};
-                        seed = __float_as_uint(p.q2.y);
-                        b = __float_as_int(p.q2.z);
-                        const int pix = __float_as_int(p.q2.w);
-                        lx = pix & 0xFFFF;
-                        ly = pix >> 16;
-                        start = true;
-                    }
-                } else {
-                    const int tile = slot >> 6, w = slot & 63;
-                    lx = (tile % tiles_x) * 8 + (w & 7);
-                    ly = (tile / tiles_x) * 8 + (w >> 3);
-                    if (lx < a.tw && ly < a.th) {
-                        primary_ray(a, a.x0 + lx, frame_row(a, ly), seed, o, d);
-                        att = {1.0f, 1.0f, 1.0f};
-                        b = 0;
-                        start = true;
-                    }
-                }
-                if (start) {
-                    inv = {1.0f / d.x, 1.0f / d.y, 1.0f / d.z};
-                    closest = kTMax;
-                    hit = -1;
-                    node = 0;
-                    leaf = root_leaf;
-                    mode = end > 0 ? kTrace : kReady;
-                    if (COUNT) {
-                        ++c_seg;
-                        if (end > 0) ++c_node;              // the root visit
-                    }
-                }
-            }
-            pool_next += min(__popcll(idle), avail);
-            idle = __ballot(mode == kIdle);
-        }
-
-        // ---- traversal: step until enough lanes wait to be shaded
-        for (;;) {
-            if (mode == kTrace) {
-                node = node_step<COUNT>(nodes, leafs, node, leaf, o, d, inv, closest, hit, c_node, c_tri);
-                if (node >= end) mode = kReady;
-            }
-            const uint64_t trace = __ballot(mode == kTrace);
-            if (trace == 0 || __popcll(__ballot(mode == kReady)) >= shade_min) break;
-        }
-
-        // ---- shading: scatter or sky; next segment, or finish the pixel
-        if (mode == kReady) {
-            bool finish = true;
-            V3 fin = {0.0f, 0.0f, 0.0f};
-            if (hit >= 0) {
-                if (COUNT) ++c_mat;
-                const V3 n = hit_normal(a.scene.norms, hit, d);
-                const V3 hp = vadd(o, vscale(d, closest));
-                const float4 M = a.scene.mats[kShadeStride * hit];
-                V3 nd;
-                if (scatter(M, d, n, seed, nd) && b < a.max_bounces - 1) {
-                    att = vmul(att, V3{M.x, M.y, M.z});
-                    o = hp;
-                    d = nd;
-                    ++b;
-                    inv = {1.0f / d.x, 1.0f / d.y, 1.0f / d.z};
-                    closest = kTMax;
-                    hit = -1;
-                    node = 0;
-                    leaf = root_leaf;
-                    mode = end > 0 ? kTrace : kReady;
-                    finish = false;
-                    if (COUNT) {
-                        ++c_seg;
-                        if (end > 0) ++c_node;              // the root visit
-                    }
-                }
-                // absorbed (:220-222) or scattered on the last bounce (:229-231): black
-            } else {
-                fin = vmul(att, sky_color(d));
-            }
-            if (finish) {
-                write_pixel(a, lx, ly, fin);
-                mode = kIdle;
-            }
-        }
-        if (exhausted && __ballot(mode != kIdle) == 0) break;
-    }
-    if (COUNT) flush_counters(a.counters, c_seg, c_node, c_tri, c_mat);
-}
-
-// ------------------------------------------------------- cooperative kernel --
-// Tier 2 of the tiered schedule: one wave per suspended path, coop_walk for
-// the rest of its current segment and all later ones.
-template <bool COUNT, bool FRONTIER>
-__global__ __launch_bounds__(256) void trace_coop(TraceArgs a) {
-    const int lane = threadIdx.x & 63;
-    __shared__ uint4 fr[FRONTIER ? 4 * kFCap : 1];
-    uint4* F = fr + (threadIdx.x >> 6) * kFCap;
-    const int end = a.scene.end;
-    const int n_rays = (int)*a.heavy_count;
-    unsigned long long c_seg = 0, c_node = 0, c_tri = 0, c_mat = 0;   // wave-uniform
-    __shared__ int claim[4];
-    for (;;) {
-        // Claim the next path: lane 0's atomic, broadcast through LDS (a
-        // uniform value from the start, so no lane-divergent loop structure).
-        if (lane == 0) claim[threadIdx.x >> 6] = (int)atomicAdd(a.queue, 1u);
-        __builtin_amdgcn_wave_barrier();
-        const int r = __builtin_amdgcn_readfirstlane(claim[threadIdx.x >> 6]);
-        __builtin_amdgcn_wave_barrier();
-        if (r >= n_rays) break;
-        unsigned long long t_start = 0, rounds = 0, segs = 0, fallbacks = 0, t_walk = 0, t_first = 0, r_first = 0;
-        if (a.diag) t_start = wall_clock64();
-        const HeavyRay hv = a.heavy[r];
-        V3 o = {hv.p.q0.x, hv.p.q0.y, hv.p.q0.z};
-        V3 d = {hv.p.q1.x, hv.p.q1.y, hv.p.q1.z};
-        V3 att = {hv.p.q0.w, hv.p.q1.w, hv.p.q2.x};
-        uint32_t seed = __float_as_uint(hv.p.q2.y);
-        int b = __float_as_int(hv.p.q2.z);
-        const int pix = __float_as_int(hv.p.q2.w);
-        float closest = hv.q3.x;
-        int node = __float_as_int(hv.q3.y);
-        int hit = __float_as_int(hv.q3.z);
-        V3 fin = {0.0f, 0.0f, 0.0f};
-        for (;;) {
-            const V3 inv = {1.0f / d.x, 1.0f / d.y, 1.0f / d.z};
-            const unsigned long long tw0 = a.diag ? wall_clock64() : 0;
-            if (FRONTIER) {
-                bool pl = false;
-                int nr = 0;
-                if (!frontier_walk<COUNT>(a.scene.nodes, a.scene.leafs, a.scene.pairs, end, node, pl, o, d, inv,
-                                          closest, hit, c_node, c_tri, F, nr) && ++fallbacks)
-                    while (node < end)
-                        node = node_step<COUNT>(a.scene.nodes, a.scene.leafs, node, pl, o, d, inv, closest, hit,
-                                                c_node, c_tri);
-                rounds += nr;
-            } else {
-                rounds += coop_walk<COUNT>(a.scene.nodes2, a.scene.leafs2, end, node, o, d, inv, closest, hit, c_node,
-                                           c_tri);
-            }
-            ++segs;
-            if (a.diag) {
-                const unsigned long long tw = wall_clock64() - tw0;
-                t_walk += tw;
-                if (segs == 1) { t_first = tw; r_first = rounds; }
-            }
-            if (hit < 0) {
-                fin = vmul(att, sky_color(d));
-                break;
-            }
-            if (COUNT) ++c_mat;
-            const V3 n = hit_normal(a.scene.norms, hit, d);
-            const V3 hp = vadd(o, vscale(d, closest));
-            const float4 M = a.scene.mats[kShadeStride * hit];
-            V3 nd;
-            if (!scatter(M, d, n, seed, nd) || b == a.max_bounces - 1) break;   // black
-            att = vmul(att, V3{M.x, M.y, M.z});
-            o = hp;
-            d = nd;
-            ++b;
-            closest = kTMax;
-            hit = -1;
-            node = 0;
-            if (COUNT) {
-                ++c_seg;
-                if (end > 0) ++c_node;              // the root visit
-            }
-        }
-        if (lane == 0) write_pixel(a, pix & 0xFFFF, pix >> 16, fin);
-        if (a.diag && lane == 0) {
-            unsigned long long* rec = a.diag + 4 * (size_t)r;
-            rec[0] = t_start;
-            rec[1] = wall_clock64();
-            rec[2] = rounds | (t_walk << 32);
-            rec[3] = segs | (fallbacks << 16) | ((r_first & 0xFFFFF) << 32) | ((t_first & 0xFFF) << 52);
-        }
-    }
-    if (COUNT && lane == 0) {
-        atomicAdd(&a.counters->segments, c_seg);
-        atomicAdd(&a.counters->node_visits, c_node);
-        atomicAdd(&a.counters->tri_tests, c_tri);
-        atomicAdd(&a.counters->mat_reads, c_mat);
-    }
-}
-
 }  // namespace
 
-int persistent_blocks_per_cu() {
-    int n = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, trace_persistent<false>, 256, 0) != hipSuccess || n < 1)
-        n = 1;
-    return n > 8 ? 8 : n;
-}
-
 hipError_t launch_trace(const TraceArgs& a, hipStream_t stream) {
-    const dim3 block(256);
-    if (a.kernel == kKernelTiered) {
-        // tier 1: lockstep tiles; paths over the visit budget are suspended
-        TraceArgs s = a;
-        s.kernel = kKernelSimple;
-        s.coop_walk = 0;      // tier 1's own cooperative tail keeps the 64-node windows
-        hipError_t e = hipMemsetAsync(a.heavy_count, 0, sizeof(unsigned), stream);
-        if (e != hipSuccess) return e;
-        e = launch_trace(s, stream);
-        if (e != hipSuccess) return e;
-        if (std::getenv("RTAMD_DEBUG_TIER1_ONLY")) {   // debug: skip tier 2, check the suspended paths
-            (void)hipStreamSynchronize(stream);
-            unsigned n = 0;
-            (void)hipMemcpy(&n, a.heavy_count, sizeof(n), hipMemcpyDeviceToHost);
-            HeavyRay* h = new HeavyRay[n ? n : 1];
-            (void)hipMemcpy(h, a.heavy, n * sizeof(HeavyRay), hipMemcpyDeviceToHost);
-            unsigned bad = 0;
-            for (unsigned i = 0; i < n; ++i) {
-                int b, node, hit, pix;
-                std::memcpy(&b, &h[i].p.q2.z, 4);
-                std::memcpy(&node, &h[i].q3.y, 4);
-                std::memcpy(&hit, &h[i].q3.z, 4);
-                std::memcpy(&pix, &h[i].p.q2.w, 4);
-                const float cl = h[i].q3.x;
-                if (b < 0 || b >= a.max_bounces || node < 0 || node > a.scene.end || !(cl > 0.f && cl <= 10000.f)) {
-                    if (bad++ < 5)
-                        std::fprintf(stderr, "heavy %u: b %d node %d closest %g hit %d pix %x\n", i, b, node, cl,
-                                     hit, pix);
-                }
-            }
-            std::fprintf(stderr, "tier 1: %u suspended paths, %u malformed\n", n, bad);
-            delete[] h;
+    const int tw_w = 8 << a.wave_tile, th_w = 8 >> a.wave_tile, bw = a.block_waves;
+    dim3 grid((a.tw + bw * tw_w - 1) / (bw * tw_w), (a.th + th_w - 1) / th_w);
+    const dim3 block(64 * bw);
+    const int feat = (a.coop_lanes > 0 ? kFeatCoopTail : 0) | (a.ext != 0 ? kFeatExt : 0) |
+                     (a.coop_lanes > 0 && a.coop_walk ? kFeatFrontier : 0);
+    TraceArgs ao = a;
+    bool join = false;
+    if (a.tile_order) {      // heavy-first: a 1-D grid over the ordered tiles
+        ao.tiles_x = (int)grid.x;
+        ao.split_n = 0;
+        const int n_tiles = (int)(grid.x * grid.y);
+        const int H = std::min(a.heavy_tiles, n_tiles - 1);
+        if (a.n_heavy_px > 0 && a.heavy_fused && bw == 1 && (feat & ~kFeatFrontier) == kFeatCoopTail) {
+            // One launch: the heavy pixels' one-pixel workgroups first, then
+            // every tile without its heavy pixels.
+            ao.split_n = 0;
+            const dim3 gf(a.n_heavy_px + n_tiles);
+            const size_t shm = kFCap * sizeof(uint4);
+            constexpr int FF = kFeatCoopTail | kFeatFused;
+            if (a.diag) hipLaunchKernelGGL((trace_simple<false, true, FF, 2>), gf, block, shm, stream, ao);
+            else if (a.counters) hipLaunchKernelGGL((trace_simple<true, false, FF, 2>), gf, block, shm, stream, ao);
+            else hipLaunchKernelGGL((trace_simple<false, false, FF, 2>), gf, block, shm, stream, ao);
             return hipGetLastError();
         }
-        // tier 2: one wave per suspended path
-        e = hipMemsetAsync(a.queue, 0, sizeof(unsigned), stream);
-        if (e != hipSuccess) return e;
-        // Always the counting build (into a sink when no stats are asked
-        // for): the non-counting build of trace_coop hangs on gfx950 with
-        // this compiler (a code-generation issue not yet isolated; the
-        // counting build is exact on every GPU parity test).
-        TraceArgs c = a;
-        if (!c.counters) c.counters = a.sink;
-        if (a.diag) {   // trace_coop's records follow tier 1's per-wave records
-            const int tw_w = 8 << a.wave_tile, th_w = 8 >> a.wave_tile;
-            c.diag = a.diag + (size_t)((a.tw + 4 * tw_w - 1) / (4 * tw_w)) * ((a.th + th_w - 1) / th_w) * 4 * 8;
+        if (H > 0 && a.heavy_fused && bw == 1 && (feat & ~kFeatFrontier) == kFeatCoopTail) {
+            // One launch: the H heaviest tiles' one-pixel workgroups first
+            // (dispatched in index order, so they start at once), then the
+            // other tiles.
+            ao.split_n = H;
+            const dim3 gf(64 * H + (n_tiles - H));
+            const size_t shm = kFCap * sizeof(uint4);
+            constexpr int FF = kFeatCoopTail | kFeatFused;
+            if (a.diag) hipLaunchKernelGGL((trace_simple<false, true, FF, 2>), gf, block, shm, stream, ao);
+            else if (a.counters) hipLaunchKernelGGL((trace_simple<true, false, FF, 2>), gf, block, shm, stream, ao);
+            else hipLaunchKernelGGL((trace_simple<false, false, FF, 2>), gf, block, shm, stream, ao);
+            return hipGetLastError();
         }
-        static int bpc[2] = {0, 0};
-        auto k2 = a.coop_walk ? trace_coop<true, true> : trace_coop<true, false>;
-        int& nb = bpc[a.coop_walk ? 1 : 0];
-        if (nb == 0 && (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k2, 256, 0) != hipSuccess || nb < 1)) nb = 1;
-        int dev = 0, n_cu = 0;
-        if (hipGetDevice(&dev) != hipSuccess ||
-            hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n_cu < 1)
-            n_cu = 256;
-        hipLaunchKernelGGL(k2, dim3(n_cu * nb), block, 0, stream, c);
-        return hipGetLastError();
-    }
-    if (a.kernel == kKernelSplit) {
-        // pass 1: lockstep tiles for the first seg_limit segments
-        TraceArgs s = a;
-        s.kernel = kKernelSimple;
-        s.resume = 0;
-        hipError_t e = hipMemsetAsync(a.spill_count, 0, sizeof(unsigned), stream);
-        if (e != hipSuccess) return e;
-        e = launch_trace(s, stream);
-        if (e != hipSuccess) return e;
-        // pass 2: the surviving paths, compacted, on persistent waves
-        TraceArgs p = a;
-        p.kernel = kKernelPersistent;
-        p.resume = 1;
-        p.seg_limit = 1 << 30;
-        return launch_trace(p, stream);
-    }
-    if (a.kernel == kKernelPersistent) {
-        const dim3 grid(a.grid_blocks);
-        hipError_t e = hipMemsetAsync(a.queue, 0, sizeof(unsigned), stream);
-        if (e != hipSuccess) return e;
-        if (a.counters)
-            hipLaunchKernelGGL(trace_persistent<true>, grid, block, 0, stream, a);
-        else
-            hipLaunchKernelGGL(trace_persistent<false>, grid, block, 0, stream, a);
-    } else {
-        const int tw_w = 8 << a.wave_tile, th_w = 8 >> a.wave_tile, bw = a.block_waves;
-        dim3 grid((a.tw + bw * tw_w - 1) / (bw * tw_w), (a.th + th_w - 1) / th_w);
-        const dim3 block(64 * bw);
-        const int feat = (a.seg_limit < (1 << 30) ? kFeatSpill : 0) |
-                         (a.heavy_budget < (1 << 30) ? kFeatHeavy : 0) | (a.prio_after > 0 ? kFeatPrio : 0) |
-                         (a.coop_lanes > 0 ? kFeatCoopTail : 0) | (a.ext != 0 ? kFeatExt : 0) |
-                         (a.coop_lanes > 0 && a.coop_walk ? kFeatFrontier : 0);
-        TraceArgs ao = a;
-        bool join = false;
-        if (a.tile_order && a.walk == kWalkTop) {   // heavy-first, walk 13: bw consecutive tiles per workgroup
-            ao.tiles_x = (int)grid.x * bw;
-            ao.split_n = 0;
-            grid = dim3(grid.x * grid.y);
-        } else if (a.tile_order) {      // heavy-first: a 1-D grid over the ordered tiles
-            ao.tiles_x = (int)grid.x;
-            ao.split_n = 0;
-            const int n_tiles = (int)(grid.x * grid.y);
-            const int H = std::min(a.heavy_tiles, n_tiles - 1);
-            if (a.n_heavy_px > 0 && a.heavy_fused && bw == 1 && (feat & ~kFeatFrontier) == kFeatCoopTail) {
-                // One launch: the heavy pixels' one-pixel workgroups first, then
-                // every tile without its heavy pixels.
-                ao.split_n = 0;
-                const dim3 gf(a.n_heavy_px + n_tiles);
-                const size_t shm = kFCap * sizeof(uint4);
-                constexpr int FF = kFeatCoopTail | kFeatFused;
-                if (a.walk == kWalkScalar) {
-                    if (a.diag) hipLaunchKernelGGL((trace_simple<false, true, FF, kWalkScalar>), gf, block, shm, stream, ao);
-                    else if (a.counters) hipLaunchKernelGGL((trace_simple<true, false, FF, kWalkScalar>), gf, block, shm, stream, ao);
-                    else hipLaunchKernelGGL((trace_simple<false, false, FF, kWalkScalar>), gf, block, shm, stream, ao);
-                    return hipGetLastError();
-                }
-                if (a.walk == kWalkDma) {
-                    if (a.diag) hipLaunchKernelGGL((trace_simple<false, true, FF, kWalkDma>), gf, block, shm, stream, ao);
-                    else if (a.counters) hipLaunchKernelGGL((trace_simple<true, false, FF, kWalkDma>), gf, block, shm, stream, ao);
-                    else hipLaunchKernelGGL((trace_simple<false, false, FF, kWalkDma>), gf, block, shm, stream, ao);
-                    return hipGetLastError();
-                }
-                if (a.diag) hipLaunchKernelGGL((trace_simple<false, true, FF, 2>), gf, block, shm, stream, ao);
-                else if (a.counters) hipLaunchKernelGGL((trace_simple<true, false, FF, 2>), gf, block, shm, stream, ao);
-                else hipLaunchKernelGGL((trace_simple<false, false, FF, 2>), gf, block, shm, stream, ao);
-                return hipGetLastError();
-            }
-            if (H > 0 && a.heavy_fused && bw == 1 && (feat & ~kFeatFrontier) == kFeatCoopTail) {
-                // One launch: the H heaviest tiles' one-pixel workgroups first
-                // (dispatched in index order, so they start at once), then the
-                // other tiles.
-                ao.split_n = H;
-                const dim3 gf(64 * H + (n_tiles - H));
-                const size_t shm = kFCap * sizeof(uint4);
-                constexpr int FF = kFeatCoopTail | kFeatFused;
-                if (a.diag) hipLaunchKernelGGL((trace_simple<false, true, FF, 2>), gf, block, shm, stream, ao);
-                else if (a.counters) hipLaunchKernelGGL((trace_simple<true, false, FF, 2>), gf, block, shm, stream, ao);
-                else hipLaunchKernelGGL((trace_simple<false, false, FF, 2>), gf, block, shm, stream, ao);
-                return hipGetLastError();
-            }
-            if (H > 0 && a.ev_fork && bw == 1 && (feat & ~kFeatFrontier) == kFeatCoopTail) {
-                // The H most expensive tiles, one pixel per wave, every segment
-                // walked cooperatively with the frontier walk, on an auxiliary
-                // stream concurrent with the other tiles' launch.
-                const hipStream_t hs = a.aux_stream ? a.aux_stream : stream;   // null: same stream, in sequence
-                hipError_t e = hipSuccess;
-                if (a.aux_stream) {
-                    e = hipEventRecord(a.ev_fork, stream);
-                    if (e == hipSuccess) e = hipStreamWaitEvent(a.aux_stream, a.ev_fork, 0);
-                    if (e != hipSuccess) return e;
-                }
-                TraceArgs ah = ao;
-                ah.split_n = H;
-                ah.coop_walk = 1;
-                const dim3 gh(64 * H);
-                const size_t shm = kFCap * sizeof(uint4);
-                constexpr int FH = kFeatCoopTail | kFeatFrontier;
-                if (a.diag) hipLaunchKernelGGL((trace_simple<false, true, FH, 2>), gh, block, shm, hs, ah);
-                else if (a.counters) hipLaunchKernelGGL((trace_simple<true, false, FH, 2>), gh, block, shm, hs, ah);
-                else hipLaunchKernelGGL((trace_simple<false, false, FH, 2>), gh, block, shm, hs, ah);
-                e = hipGetLastError();
-                if (e == hipSuccess && a.aux_stream) e = hipEventRecord(a.ev_join, a.aux_stream);
+        if (H > 0 && a.ev_fork && bw == 1 && (feat & ~kFeatFrontier) == kFeatCoopTail) {
+            // The H most expensive tiles, one pixel per wave, every segment
+            // walked cooperatively with the frontier walk, on an auxiliary
+            // stream concurrent with the other tiles' launch.
+            const hipStream_t hs = a.aux_stream ? a.aux_stream : stream;   // null: same stream, in sequence
+            hipError_t e = hipSuccess;
+            if (a.aux_stream) {
+                e = hipEventRecord(a.ev_fork, stream);
+                if (e == hipSuccess) e = hipStreamWaitEvent(a.aux_stream, a.ev_fork, 0);
                 if (e != hipSuccess) return e;
-                ao.tile_order = a.tile_order + H;
-                if (a.diag) ao.diag = a.diag + (size_t)kDiagWords * gh.x;
-                grid = dim3(n_tiles - H);
-                join = a.aux_stream != nullptr;
-            } else {
-                grid = dim3(n_tiles);
             }
-        }
-        const size_t shm_f = (size_t)bw * kFCap * sizeof(uint4);   // kFeatFrontier variants only
-        // Experiment knob RTAMD_LDS_PAD: unused dynamic LDS per workgroup, which
-        // caps the resident waves per CU (160 KB / pad) below the VGPR limit.
-        static const size_t lds_pad = [] {
-            const char* v = std::getenv("RTAMD_LDS_PAD");
-            const long x = v ? std::atol(v) : 0;
-            return (size_t)(x > 0 && x <= 65536 ? x : 0);
-        }();
-#define RT_SIMPLE(F, W)                                                                                         \
-        if (a.diag) hipLaunchKernelGGL((trace_simple<false, true, F, W>), grid, block, ((F) & kFeatFrontier) ? shm_f : lds_pad, stream, ao);           \
-        else if (a.counters) hipLaunchKernelGGL((trace_simple<true, false, F, W>), grid, block, ((F) & kFeatFrontier) ? shm_f : lds_pad, stream, ao); \
-        else hipLaunchKernelGGL((trace_simple<false, false, F, W>), grid, block, ((F) & kFeatFrontier) ? shm_f : lds_pad, stream, ao);
-        if (a.walk == kWalkTop) {
-            switch (feat) {
-                case kFeatCoopTail: RT_SIMPLE(kFeatCoopTail, kWalkTop) break;
-                case 0: RT_SIMPLE(0, kWalkTop) break;
-                case kFeatCoopTail | kFeatExt: RT_SIMPLE(kFeatCoopTail | kFeatExt, kWalkTop) break;
-                default: return hipErrorInvalidValue;
-            }
-        } else if (a.walk == kWalkDma) {
-            if (bw != 1) return hipErrorInvalidValue;   // one stage per workgroup: one-wave workgroups
-            switch (feat) {
-                case kFeatCoopTail: RT_SIMPLE(kFeatCoopTail, kWalkDma) break;
-                case 0: RT_SIMPLE(0, kWalkDma) break;
-                case kFeatCoopTail | kFeatExt: RT_SIMPLE(kFeatCoopTail | kFeatExt, kWalkDma) break;
-                default: return hipErrorInvalidValue;
-            }
-        } else if (a.walk == kWalkScalar) {
-            switch (feat) {
-                case kFeatCoopTail: RT_SIMPLE(kFeatCoopTail, kWalkScalar) break;
-                case 0: RT_SIMPLE(0, kWalkScalar) break;
-                case kFeatCoopTail | kFeatExt: RT_SIMPLE(kFeatCoopTail | kFeatExt, kWalkScalar) break;
-                default: return hipErrorInvalidValue;
-            }
-        } else if (a.walk == 2) {
-            switch (feat) {
-                case kFeatCoopTail: RT_SIMPLE(kFeatCoopTail, 2) break;
-                case 0: RT_SIMPLE(0, 2) break;
-                default: RT_SIMPLE(kFeatSpill | kFeatHeavy | kFeatPrio | kFeatCoopTail | kFeatExt | kFeatFrontier, 2) break;
-            }
-        } else if (a.walk == 0) {
-            switch (feat) {
-                case 0: RT_SIMPLE(0, 0) break;
-                case kFeatCoopTail: RT_SIMPLE(kFeatCoopTail, 0) break;
-                case kFeatCoopTail | kFeatPrio: RT_SIMPLE(kFeatCoopTail | kFeatPrio, 0) break;
-                case kFeatCoopTail | kFeatExt: RT_SIMPLE(kFeatCoopTail | kFeatExt, 0) break;
-                case kFeatCoopTail | kFeatFrontier: RT_SIMPLE(kFeatCoopTail | kFeatFrontier, 0) break;
-                case kFeatCoopTail | kFeatHeavy: RT_SIMPLE(kFeatCoopTail | kFeatHeavy, 0) break;
-                case kFeatHeavy: RT_SIMPLE(kFeatHeavy, 0) break;
-                default: RT_SIMPLE(kFeatSpill | kFeatHeavy | kFeatPrio | kFeatCoopTail | kFeatExt | kFeatFrontier, 0) break;
-            }
+            TraceArgs ah = ao;
+            ah.split_n = H;
+            ah.coop_walk = 1;
+            const dim3 gh(64 * H);
+            const size_t shm = kFCap * sizeof(uint4);
+            constexpr int FH = kFeatCoopTail | kFeatFrontier;
+            if (a.diag) hipLaunchKernelGGL((trace_simple<false, true, FH, 2>), gh, block, shm, hs, ah);
+            else if (a.counters) hipLaunchKernelGGL((trace_simple<true, false, FH, 2>), gh, block, shm, hs, ah);
+            else hipLaunchKernelGGL((trace_simple<false, false, FH, 2>), gh, block, shm, hs, ah);
+            e = hipGetLastError();
+            if (e == hipSuccess && a.aux_stream) e = hipEventRecord(a.ev_join, a.aux_stream);
+            if (e != hipSuccess) return e;
+            ao.tile_order = a.tile_order + H;
+            if (a.diag) ao.diag = a.diag + (size_t)kDiagWords * gh.x;
+            grid = dim3(n_tiles - H);
+            join = a.aux_stream != nullptr;
         } else {
-            switch (feat) {
-                case 0: RT_SIMPLE(0, 1) break;
-                case kFeatCoopTail: RT_SIMPLE(kFeatCoopTail, 1) break;
-                case kFeatSpill: RT_SIMPLE(kFeatSpill, 1) break;
-                case kFeatHeavy: RT_SIMPLE(kFeatHeavy, 1) break;
-                default: RT_SIMPLE(kFeatSpill | kFeatHeavy | kFeatPrio | kFeatCoopTail | kFeatExt | kFeatFrontier, 1) break;
-            }
+            grid = dim3(n_tiles);
         }
+    }
+    const size_t shm_f = (size_t)bw * kFCap * sizeof(uint4);   // kFeatFrontier variants only
+#define RT_SIMPLE(F, W)                                                                                         \
+    if (a.diag) hipLaunchKernelGGL((trace_simple<false, true, F, W>), grid, block, ((F) & kFeatFrontier) ? shm_f : 0, stream, ao);           \
+    else if (a.counters) hipLaunchKernelGGL((trace_simple<true, false, F, W>), grid, block, ((F) & kFeatFrontier) ? shm_f : 0, stream, ao); \
+    else hipLaunchKernelGGL((trace_simple<false, false, F, W>), grid, block, ((F) & kFeatFrontier) ? shm_f : 0, stream, ao);
+    if (a.walk == 2) {
+        switch (feat) {
+            case kFeatCoopTail: RT_SIMPLE(kFeatCoopTail, 2) break;
+            case 0: RT_SIMPLE(0, 2) break;
+            default: RT_SIMPLE(kFeatCoopTail | kFeatExt | kFeatFrontier, 2) break;
+        }
+    } else {
+        switch (feat) {
+            case 0: RT_SIMPLE(0, 0) break;
+            case kFeatCoopTail: RT_SIMPLE(kFeatCoopTail, 0) break;
+            default: RT_SIMPLE(kFeatCoopTail | kFeatExt | kFeatFrontier, 0) break;
+        }
+    }
 #undef RT_SIMPLE
-        if (join) {
-            hipError_t e = hipGetLastError();
-            if (e == hipSuccess) e = hipStreamWaitEvent(stream, a.ev_join, 0);
-            return e;
-        }
+    if (join) {
+        hipError_t e = hipGetLastError();
+        if (e == hipSuccess) e = hipStreamWaitEvent(stream, a.ev_join, 0);
+        return e;
     }
     return hipGetLastError();
 }

@@ -65,8 +65,9 @@ class Renderer:
             pass
 
     def set_option(self, name: str, value: int) -> None:
-        """Schedule options (rt_set_option): "kernel" (0 simple, 1 persistent),
-        "shade_min", "blocks_per_cu".  Results do not depend on them."""
+        """Schedule options (rt_set_option; the list is in include/rtamd.h):
+        "walk", "coop_lanes", "heavy_first", "concurrent_launches", ...
+        Results do not depend on them."""
         check(lib().rt_set_option(self._ctx, name.encode(), int(value)))
 
     def get_option(self, name: str) -> int:

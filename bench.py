@@ -29,20 +29,27 @@ ranks), in millions.  A segment is one executed bounce-loop iteration
 (compute_dynamic_ray.comp:179-232); its count per frame is deterministic and is
 taken from a counting pass outside the timed region.
 
-roofline: algorithmic bytes of one launch's trace (32 B per BVH node visit +
-36 B per triangle test + 16 B per material read + 4 B per pixel; DESIGN.md
-§5) / the device time per launch of the running loop (HIP events around the
-timed region on the main stream after joining every launch stream, divided by
-the launches), against 8 TB/s HBM (the contract's "achieved" and "frac").
-kernel_ms is the mean duration of one launch (HIP events on its own stream;
-what rocprofv3 reports per kernel); with D frames in flight launches overlap,
-and kernel_ms / frame_ms_device is the average number running at once.  The
-scene is L2/MALL-resident, so these bytes are mostly served from cache:
-"frac" is an algorithmic-throughput fraction, not HBM utilisation.  The
-measured HBM traffic (PMC, tools/pmc.sh) and its fraction of the peak are
-reported beside it ("hbm_GBps", "hbm_frac").
+roofline: the walk is bound by the issue of its vector memory
+instructions (the texture addresser / data path), not by HBM
+bandwidth (the 8-MB scene stays in L2 / MALL).  bound "vmem_issue":
+achieved = SQ_INSTS_VMEM_RD per launch (PMC, tools/pmc.sh, committed in
+profiles/pmc_latest.json for this config) / frame_ms_device, the device time
+per launch of the running loop (HIP events around the timed region on the
+main stream after joining every launch stream, divided by the launches); peak
+= CUs / TA_NS_PER_VMEM, the measured floor of one wave-level
+global_load_dwordx4 per CU (tools/ubench/ta_cost.hip,
+profiles/r02/walks/ubench_ta_cost.txt:1); frac = achieved / peak.  Beside it:
+"hbm" = the PMC HBM bytes per launch (FETCH_SIZE, corrected) over the same
+time against 8 TB/s, and "algorithmic" = the contract's algorithmic bytes
+(32 B per BVH node visit + 36 B per triangle test + 16 B per material read +
+4 B per pixel) over that time against 8 TB/s, which can exceed 1 because
+those bytes are cache hits.  kernel_ms is the mean duration of one launch
+(HIP events on its own stream; what rocprofv3 reports per kernel); with D
+frames in flight launches overlap, and kernel_ms / frame_ms_device is the
+average number running at once.
 cpu_baseline: the CPU oracle (oracle/rt_oracle.c, OpenMP) on a bounded row
-sample of the same frame, rank 0 at N = 1 only.
+sample of the same frame, rank 0 at N = 1 only (the reference has no CPU
+render path: BVHNode.hit throws, BVHNode.java:35-41).
 """
 from __future__ import annotations
 
@@ -57,6 +64,12 @@ sys.path.insert(0, os.path.join(ROOT, "3d-ray-tracer-vulkan_amd"))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0      # MI355X HBM3E, MI355X_MICROARCH.md chip table
+# ns of the vector memory pipeline per wave-level global_load_dwordx4 per CU
+# when every lane reads one address: the cheapest form a walk step's loads take
+# (tools/ubench/ta_cost.hip; profiles/r02/walks/ubench_ta_cost.txt:1, 7.39 ns
+# = 17.7 cycles at 2.4 GHz)
+TA_NS_PER_VMEM = 7.39
+TA_NS_SOURCE = "profiles/r02/walks/ubench_ta_cost.txt:1 (tools/ubench/ta_cost.hip: width 16 B, stride 0, 64 lanes)"
 BASELINE = json.load(open(os.path.join(ROOT, "BASELINE.json")))
 
 
@@ -141,8 +154,9 @@ def main() -> None:
     ap.add_argument("--settle-s", type=float, default=0.2,
                     help="untimed frames before the warmup steps: this many seconds of counting-pass time "
                          "(5-100 frames; steady clocks and caches)")
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "latest_pmc_traffic.json"),
-                    help="PMC-derived HBM bytes per launch (profiles/*.json) to report as roofline.traffic")
+    ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_latest.json"),
+                    help="PMC per launch of each config (tools/pmc_traffic.py: SQ_INSTS_VMEM_RD, HBM bytes) for "
+                         "the roofline")
     args = ap.parse_args()
 
     import numpy as np
@@ -477,18 +491,9 @@ def main() -> None:
     value = segments * args.steps / elapsed / 1e6
     alg_bytes = 32.0 * l_nodes + 36.0 * l_tris + 16.0 * l_mats + 4.0 * l_pix
     ref_layout_bytes = 48.0 * l_nodes + 48.0 * l_tris + 16.0 * l_mats + 4.0 * l_pix
-    # Aggregate algorithmic throughput: bytes per launch over the device time
-    # per launch of the running loop (= bytes x launches in flight / launch
-    # duration, the launches overlapping on the device).
-    achieved = alg_bytes / (frame_ms * 1e-3) / 1e9
-    traffic, traffic_src = None, None
-    if args.traffic_json and os.path.exists(args.traffic_json):
-        with open(args.traffic_json) as fh:
-            tj = json.load(fh)
-        if tj.get("config") == cfg.name and world == 1:   # PMC bytes of the same kernel on this workload
-            traffic, traffic_src = tj.get("hbm_bytes_per_launch"), tj.get("source")
-    hbm_gbs = traffic / (frame_ms * 1e-3) / 1e9 if traffic else None
-
+    n_cu = torch.cuda.get_device_properties(dev).multi_processor_count
+    pmc = load_pmc(args.pmc_json, cfg.name) if (world == 1 and F == 1) else None
+    roof = roofline(pmc, alg_bytes, ref_layout_bytes, l_seg, frame_ms, n_cu)
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(built, cam, W, H, B, segments, args.cpu_seconds)
@@ -545,21 +550,7 @@ def main() -> None:
                 "launches_per_step": F * (2 if heavy_used > 0 and renderer.get_option("heavy_stream") != 2 else 1),
             },
             "roofline": {
-                "bound": "hbm",
-                "achieved": round(achieved, 1),
-                "peak": HBM_PEAK_GBS,
-                "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4),
-                "traffic": traffic,
-                "basis": "achieved/frac = ALGORITHMIC bytes (the reference's visit counts x compact record sizes) per "
-                         "launch / frame_ms_device (the device time per launch of the running loop = kernel_ms, "
-                         "the mean launch duration, / launches_in_flight_avg); the scene is L2/MALL-resident, so "
-                         "most of these bytes are cache hits and frac is not HBM utilisation: measured HBM traffic "
-                         "is hbm_GBps / hbm_frac. The kernel is bound by its vector memory instructions "
-                         "(DESIGN.md §7)",
-                "hbm_GBps": round(hbm_gbs, 1) if hbm_gbs else None,
-                "hbm_frac": round(hbm_gbs / HBM_PEAK_GBS, 4) if hbm_gbs else None,
-                "traffic_source": traffic_src,
+                **roof,
                 "kernel": ("trace_simple" if renderer.get_option("kernel") == 0 else "trace_*") + (
                     f" (one launch per frame: the {renderer.get_option('heavy_pixels_used')} heaviest pixels one per "
                     f"wave first, then every {8 << renderer.get_option('wave_tile')}x"
@@ -577,9 +568,6 @@ def main() -> None:
                 "events": "kernel_ms: each launch's own stream, around every launch (after its wait for the "
                           "gather); frame_ms_device: main stream around the timed region after joining every "
                           "launch stream, / launches",
-                "alg_bytes_per_launch": int(alg_bytes),
-                "alg_bytes_per_segment": round(alg_bytes / l_seg, 1),
-                "reference_layout_frac": round(ref_layout_bytes / (frame_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
             },
             "primary_mrays_s": round(pixels * args.steps / elapsed / 1e6, 2),
             "cpu_baseline": cpu,
@@ -597,10 +585,74 @@ def main() -> None:
         dist.destroy_process_group()
 
 
+def load_pmc(path, config_name):
+    """PMC per launch for config_name from profiles/pmc_latest.json
+    (tools/pmc_traffic.py), or None."""
+    if not path or not os.path.exists(path):
+        return None
+    with open(path) as fh:
+        tj = json.load(fh)
+    return tj.get("configs", {}).get(config_name)
+
+
+def roofline(pmc, alg_bytes, ref_layout_bytes, l_seg, frame_ms, n_cu):
+    """The roofline object of the JSON line (module docstring): the vector
+    memory issue bound from PMC, with the HBM and algorithmic figures."""
+    t = frame_ms * 1e-3                                     # s per launch of the running loop
+    vmem = pmc.get("SQ_INSTS_VMEM_RD") if pmc else None
+    traffic = pmc.get("hbm_bytes_per_launch") if pmc else None
+    peak = n_cu / TA_NS_PER_VMEM                            # G wave-instructions / s
+    achieved = vmem / t / 1e9 if vmem else None
+    hbm = traffic / t / 1e9 if traffic else None
+    alg = alg_bytes / t / 1e9
+    return {
+        "bound": "vmem_issue",
+        "achieved": round(achieved, 3) if achieved else None,
+        "peak": round(peak, 3),
+        "unit": "G wave-level vector-memory instructions/s",
+        "frac": round(achieved / peak, 4) if achieved else None,
+        "traffic": traffic,
+        "basis": f"achieved = SQ_INSTS_VMEM_RD per launch ({vmem}, PMC) / frame_ms_device; peak = {n_cu} CUs / "
+                 f"{TA_NS_PER_VMEM} ns per wave-level global_load_dwordx4 per CU ({TA_NS_SOURCE}); traffic = PMC "
+                 f"HBM bytes per launch (FETCH_SIZE x 1024 x 2). null without a PMC record of this config "
+                 f"(profiles/pmc_latest.json) or for N > 1 shares",
+        "pmc_source": pmc.get("source") if pmc else None,
+        "vmem_rd_per_launch": vmem,
+        "vmem_rd_per_segment": round(vmem / l_seg, 3) if vmem else None,
+        "hbm": {"achieved": round(hbm, 1) if hbm else None, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(hbm / HBM_PEAK_GBS, 4) if hbm else None},
+        "algorithmic": {"bytes_per_launch": int(alg_bytes), "bytes_per_segment": round(alg_bytes / l_seg, 1),
+                        "achieved": round(alg, 1), "unit": "GB/s",
+                        "alg_throughput_frac": round(alg / HBM_PEAK_GBS, 4),
+                        "reference_layout_frac": round(ref_layout_bytes / t / 1e9 / HBM_PEAK_GBS, 4),
+                        "note": "the reference's visit counts x record sizes (SURVEY.md §8d) over the launch time; "
+                                "mostly L2/MALL hits, so it can exceed the HBM peak"},
+    }
+
+
+def host_cpu():
+    """CPU model, the host's logical CPUs and the ones this process may use."""
+    model = None
+    try:
+        with open("/proc/cpuinfo") as fh:
+            model = next((ln.split(":", 1)[1].strip() for ln in fh if ln.startswith("model name")), None)
+    except OSError:
+        pass
+    try:
+        usable = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        usable = os.cpu_count() or 1
+    return model, os.cpu_count() or 1, usable
+
+
 def cpu_baseline(built, cam, W, H, B, frame_segments, target_s):
     """The oracle on every k-th row of the same frame, all host threads we may use."""
     from oracle import oracle_lib
-    threads = max(1, min(16, int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)))
+    model, nproc, usable = host_cpu()
+    # A GPU box gives one GPU's job a share of 16 of the host's CPUs (the pool's
+    # rule; os.cpu_count() reports the whole host), and sets OMP_NUM_THREADS to it
+    share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or 16
+    threads = max(1, min(share, usable))
     args = (built.model_vertex_data, built.model_material_data, built.flat_bvh_data, cam.ubo_bytes(), W, H, B)
     # probe on every 64th row, then size the sample to ~target_s: every k-th
     # row if the frame takes longer than that, else the whole frame repeated.
@@ -634,6 +686,14 @@ def cpu_baseline(built, cam, W, H, B, frame_segments, target_s):
         "cores": threads,
         "kind": "port",
         "sample": f"{what} ({px} px, {segs} segments, {dt:.2f} s, OpenMP threads {threads})",
+        "cpu_model": model,
+        "nproc": nproc,
+        "cpus_usable": usable,
+        "threads_why": f"the job's CPU share: OMP_NUM_THREADS / 16 per GPU on the GPU pool (of {nproc} logical "
+                       f"CPUs on the host, {usable} in this process's affinity mask)",
+        "what": "oracle/rt_oracle.c (a line-by-line C restatement of compute_dynamic_ray.comp, the parity "
+                "checker) with OpenMP over rows: the reference has no CPU render path (BVHNode.hit throws "
+                "UnsupportedOperationException, BVHNode.java:35-41), so no 'reference' CPU baseline exists",
     }
 
 

@@ -159,7 +159,9 @@ int rt_band_rows(int height, int band_h, int band_stride, int band_off);
  * bar counts the slots as concurrent launches.  Concurrent streams need a
  * hardware queue each, and HIP's default is 4 per process, fixed when the HIP
  * runtime loads: start the host process with GPU_MAX_HW_QUEUES=16 (JVM:
- * `GPU_MAX_HW_QUEUES=16 java ...`; the Python package sets it on import).
+ * `GPU_MAX_HW_QUEUES=16 java ...`; the Python package sets it on import if
+ * HIP is not initialised yet); rt_get_option "queues_short" says 1 when the
+ * slots cannot each have a queue.
  * out_rgba must stay valid until its ticket completes; it should come from
  * rt_host_alloc (pinned, portable), since a copy into pageable memory cannot run
  * asynchronously.  A Java host wraps rt_host_alloc memory with JNI
@@ -172,32 +174,25 @@ int rt_render_wait(rt_ctx* ctx, uint64_t ticket);
 
 /* Schedule options (no effect on results, which are identical for every
  * setting):
- *   "kernel"        0 = one lane per pixel (the reference's dispatch shape;
- *                       default),
- *                   1 = persistent waves with a tile queue,
- *                   2 = split: kernel 0 for the first seg_limit segments of
- *                       every path, then the surviving paths, compacted, on
- *                       persistent waves,
- *                   3 = tiered: kernel 0 with a per-path visit budget; walks
- *                       over budget finish one wave per ray (cooperative walk)
- *   "walk"          kernel 0: 0 = one node per step, 1 = child-pair
- *                   records + per-lane stack of right-child entry distances,
- *                   2 = one node per step, software-pipelined: the next
- *                   node's box is requested before this node's triangle test
- *                   and the loop control (default); 5 = walk 2 with scalar
- *                   loads when every walking lane moves to one node; 13 = walk
- *                   2 with the top tree's records in each workgroup's LDS;
- *                   14 = walk 2 with LDS-DMA fetches of a uniform step's
- *                   records (5, 13, 14: measured slower)
- *   "coop_lanes"    kernel 0: once at most this many lanes of a wave are still
- *                   walking, the whole wave finishes their walks one ray at a
- *                   time (0..64, default 1; 0 = off)
- *   "coop_walk"     cooperative walks (coop tail, tiered second pass):
- *                   0 = 64-node preorder windows (default), 1 = preorder
- *                   frontier (up to 64 live subtrees expanded per round trip)
- *   "block_waves"   kernel 0: waves per workgroup, 1 (default: a finished
- *                   wave frees its slot at once) or 4
- *   "heavy_first"   kernel 0 with block_waves 1: 1 (default) = the first
+ *   "kernel"        0 only: the one kernel, one lane per pixel (the
+ *                   reference's dispatch shape).  The persistent, split and
+ *                   tiered kernels (1-3) and the options that tuned them
+ *                   (shade_min, blocks_per_cu, seg_limit, heavy_budget,
+ *                   prio_after) measured slower and were archived in round 3
+ *                   (profiles/r03/archive); setting them is an error.
+ *   "walk"          0 = one node per step, 2 = one node per step,
+ *                   software-pipelined over compact records: the next node's
+ *                   box is requested before this node's triangle test and the
+ *                   loop control (default).  Walks 1, 5, 13, 14 are archived.
+ *   "coop_lanes"    once at most this many lanes of a wave are still walking,
+ *                   the whole wave finishes their walks one ray at a time
+ *                   (0..64, default 1; 0 = off)
+ *   "coop_walk"     cooperative walks (the coop tail): 0 = 64-node preorder
+ *                   windows (default), 1 = preorder frontier (up to 64 live
+ *                   subtrees expanded per round trip)
+ *   "block_waves"   waves per workgroup, 1 (default: a finished wave frees its
+ *                   slot at once) or 4
+ *   "heavy_first"   with block_waves 1: 1 (default) = the first
  *                   plain (non-stats) launch of a frame geometry + camera +
  *                   scene runs the diagnostic build, records every wave's
  *                   duration and walk length, and ends with a stream
@@ -212,7 +207,10 @@ int rt_render_wait(rt_ctx* ctx, uint64_t ticket);
  *                   "heavy_factor" percent (default 130) of the bulk estimate,
  *                   at most "heavy_cap" percent of one generation of
  *                   one-pixel waves (CUs x 24 / 64 tiles: 96 on MI355X, so 72
- *                   by default), shared by the concurrent launches
+ *                   by default), shared by the concurrent launches.  Heavy
+ *                   tiles and pixels need coop_lanes > 0 and no extensions
+ *                   (and walk 2 for heavy_stream 2); otherwise a launch uses
+ *                   the learned order alone
  *   "concurrent_launches" the number of launches of similar work the caller
  *                   keeps in flight on a device at once (1..64, default 1): a
  *                   render loop with two frames in flight says 2, a batch of N
@@ -237,26 +235,25 @@ int rt_render_wait(rt_ctx* ctx, uint64_t ticket);
  *                   heavy pixels; 0 = whole heavy tiles
  *   "heavy_pixel_factor" see heavy_pixels (1..100000, default 50)
  *   "reuse_order"   heavy_first: 1 (default) = a camera that has just moved
- *                   (the launch key differs from the previous launch's only in
- *                   the camera) uses the newest order learned for the same
- *                   frame geometry and scene instead of learning (no learning
- *                   frame while the camera moves; the first repeat of a camera
- *                   learns); 0 = every new camera learns
+ *                   (differs from the camera of the last launch with the same
+ *                   frame geometry and scene) uses the newest order learned
+ *                   for that geometry and scene instead of learning (no
+ *                   learning frame while the camera moves; the first repeat of
+ *                   a camera learns); 0 = every new camera learns
  *   "heavy_pixels_used" (rt_get_option only) heavy pixels of the last launch
- *   "graph"         kernel 0, plain launches on a non-null stream: 1 (default)
- *                   = captured once per launch key (scene, camera, frame,
- *                   schedule, learned order, outputs, stream) into a HIP
- *                   graph and replayed; 0 = launched directly.  Counting and
- *                   learning launches are never captured.  Same results.
+ *   "graph"         plain launches on a non-null stream whose frame is two
+ *                   launches (heavy_stream 1): 1 (default) = captured once per
+ *                   launch key into a HIP graph and replayed; 0 = launched
+ *                   directly.  Counting and learning launches are never
+ *                   captured.  Same results.
  *   "learn_cost"    heavy_first order by 1 = wave duration (default) or 0 =
  *                   walk length
  *   "heavy_tiles_used" (rt_get_option only) heavy tiles of the last launch
- *   "wave_tile"     kernel 0: pixels per wave (8<<s) x (8>>s), s = 0..3
+ *   "wave_tile"     pixels per wave (8<<s) x (8>>s), s = 0..3
  *                   (default 0: 8x8, the shader's local_size; with frames in
  *                   flight it beats 32x2 by 6%, profiles/r02/tiles)
  *   "extensions"    NON-REFERENCE features, bits (default 0 = the reference's
- *                   shader exactly).  Any bit set
- *                   runs kernel 0:
+ *                   shader exactly):
  *                   1 = honour sky_enabled (@68): a miss is black when it is 0
  *                   2 = a type-3 ("Emissive (Light)") hit ends the path with
  *                       attenuation * albedo (the reference renders it black)
@@ -264,23 +261,26 @@ int rt_render_wait(rt_ctx* ctx, uint64_t ticket);
  *                       (frame 0 is the reference's frame), a per-device buffer
  *                       keeps the running sum of the linear colour (frame_count
  *                       0 overwrites it; a new frame partition starts from
- *                       zero) and the output is sqrt(sum / (frame_count+1))
+ *                       zero) and the output is sqrt(sum / (frame_count+1)).
+ *                       The sums are per device, so frames must reach the
+ *                       device in frame_count order: rt_render_async
+ *                       serialises its slots' traces then; a caller tracing on
+ *                       several streams of its own must do the same
  *                   8 = spheres (rt_upload_spheres) after the BVH walk
- *   "prio_after"    kernel 0: raise a wave's priority after this many walk
- *                   steps (0 = never, default)
- *   "seg_limit"     split: segments traced in the first pass (default 2)
- *   "heavy_budget"  tiered: walk steps per path in the first pass (default 256)
- *   "shade_min"     persistent: shade once this many lanes of a wave are
- *                   ready (1..64, default 16)
- *   "blocks_per_cu" persistent: resident 256-thread blocks per CU (0 = from
- *                   the occupancy query)
- * Defaults can also be set with the environment variables
- * RTAMD_KERNEL=simple|persistent|split|tiered, RTAMD_WALK, RTAMD_COOP_LANES,
- * RTAMD_COOP_WALK, RTAMD_BLOCK_WAVES, RTAMD_HEAVY_FIRST, RTAMD_HEAVY_TILES,
- * RTAMD_HEAVY_FACTOR, RTAMD_HEAVY_STREAM (0 / 1 / 2), RTAMD_HEAVY_PIXELS, RTAMD_LEARN_COST,
- * RTAMD_SEG_LIMIT, RTAMD_SHADE_MIN and RTAMD_BLOCKS_PER_CU. */
+ *   "async_slots"   rt_render_async frames in flight per device (1..8, default 4)
+ *   "copy_streams"  rt_render_async readback copy streams (1 or 2, default 1)
+ *   "hw_queues"     (rt_get_option only) GPU_MAX_HW_QUEUES as seen by rt_create
+ *                   (4, HIP's default, when unset)
+ *   "queues_short"  (rt_get_option only) 1 when async_slots + 2 > hw_queues:
+ *                   the slots' traces then share hardware queues and run one
+ *                   after another (set GPU_MAX_HW_QUEUES before the process
+ *                   initialises HIP)
+ * Defaults can also be set with the environment variables RTAMD_WALK,
+ * RTAMD_COOP_LANES, RTAMD_COOP_WALK, RTAMD_BLOCK_WAVES, RTAMD_HEAVY_FIRST,
+ * RTAMD_HEAVY_TILES, RTAMD_HEAVY_FACTOR, RTAMD_HEAVY_STREAM (0 / 1 / 2),
+ * RTAMD_HEAVY_PIXELS, RTAMD_LEARN_COST and RTAMD_GRAPH. */
 int rt_set_option(rt_ctx* ctx, const char* name, int64_t value);
-/* Diagnostics: with option "diag" = 1, kernel 0 records per wave
+/* Diagnostics: with option "diag" = 1, the kernel records per wave
  * 8 words: {start, end} (s_memrealtime, 100 MHz), {XCC id << 32 | HW_ID},
  * {block << 8 | wave}, {lockstep walk iterations}, {cooperative windows},
  * {ticks spent in the cooperative tail}, {0} into a device buffer;
@@ -336,9 +336,11 @@ int rt_camera_from_lookat(const double origin[3], const double lookat[3],
                           const double vup[3], double vfov_deg, double aspect,
                           rt_camera_ubo* out);
 
-/* OBJ mesh (SceneBuilder.loadModel, SceneBuilder.java:129-191).  Faces with
- * more than 3 vertices are fan-triangulated from vertex 0 (the convex case of
- * Assimp's aiProcess_Triangulate; parity vs Assimp unpinned). */
+/* OBJ mesh (SceneBuilder.loadModel, SceneBuilder.java:129-191).  A quad is
+ * split along the diagonal from its concave corner, or from vertex 0 when it
+ * is convex (Assimp's aiProcess_Triangulate rule for quads); faces with more
+ * than 4 vertices are fanned from vertex 0 (Assimp ear-clips them).  Parity
+ * vs Assimp is unpinned. */
 typedef struct rt_mesh rt_mesh;
 int    rt_mesh_load_obj(const char* path, rt_mesh** out);
 size_t rt_mesh_tri_count(const rt_mesh* mesh);

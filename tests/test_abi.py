@@ -35,7 +35,8 @@ def test_library_exports_every_header_symbol():
 def test_library_is_gfx950_code_object():
     from rtamd import LIB_PATH
     data = open(LIB_PATH, "rb").read()
-    assert b"gfx950" in data and b"trace_simple" in data and b"trace_coop" in data
+    assert b"gfx950" in data and b"trace_simple" in data
+    assert b"trace_persistent" not in data and b"trace_coop" not in data   # archived in round 3
 
 
 def test_structs_match_reference_bytes():

@@ -14,8 +14,7 @@ from raw_bvh import raw_bvh_scene
 pytestmark = pytest.mark.gpu
 
 COUNTERS = ("segments", "node_visits", "tri_tests", "mat_reads")
-DEFAULT_OPTS = {"kernel": 0, "shade_min": 16, "blocks_per_cu": 0, "wave_tile": 0, "seg_limit": 2,
-                "heavy_budget": 256, "prio_after": 0, "coop_lanes": 1, "walk": 2, "coop_walk": 0,
+DEFAULT_OPTS = {"wave_tile": 0, "coop_lanes": 1, "walk": 2, "coop_walk": 0,
                 "block_waves": 1, "heavy_first": 1, "heavy_tiles": -1, "heavy_stream": 2,
                 "learn_cost": 1, "heavy_factor": 130, "graph": 1, "concurrent_launches": 1, "heavy_cap": 75,
                 "heavy_pixels": 1, "heavy_pixel_factor": 50, "reuse_order": 1}
@@ -115,53 +114,26 @@ def test_config5_1m_row_subset(renderer):
 
 @pytest.mark.parametrize("opts", [
     {"kernel": 0},
-    {"kernel": 0, "coop_lanes": 0},
-    {"kernel": 0, "walk": 1},
-    {"kernel": 0, "walk": 1, "coop_lanes": 0},
-    {"kernel": 3, "walk": 1, "heavy_budget": 40},
-    {"kernel": 1, "shade_min": 1},
-    {"kernel": 1, "shade_min": 16},
-    {"kernel": 1, "shade_min": 64},
-    {"kernel": 1, "shade_min": 24, "blocks_per_cu": 1},
-    {"kernel": 0, "wave_tile": 3},
-    {"kernel": 0, "wave_tile": 2, "coop_lanes": 2},
-    {"kernel": 0, "wave_tile": 1},
-    {"kernel": 2, "seg_limit": 1},
-    {"kernel": 2, "seg_limit": 2},
-    {"kernel": 2, "seg_limit": 3, "shade_min": 1},
-    {"kernel": 3, "heavy_budget": 1},
-    {"kernel": 3, "heavy_budget": 40},
-    {"kernel": 3, "heavy_budget": 256},
-    {"kernel": 0, "coop_lanes": 1},
-    {"kernel": 0, "coop_lanes": 8},
-    {"kernel": 0, "coop_lanes": 64},
-    {"kernel": 0, "coop_lanes": 4, "wave_tile": 0, "prio_after": 64},
-    {"kernel": 0, "coop_walk": 1},
-    {"kernel": 0, "block_waves": 4},
-    {"kernel": 0, "heavy_first": 0},
-    {"kernel": 0, "graph": 0},
-    {"kernel": 0, "graph": 0, "heavy_stream": 0},
-    {"kernel": 0, "walk": 0},
-    {"kernel": 0, "walk": 0, "coop_lanes": 8},
-    {"kernel": 0, "block_waves": 1, "wave_tile": 0, "coop_lanes": 0},
-    {"kernel": 0, "coop_walk": 1, "coop_lanes": 8},
-    {"kernel": 0, "coop_walk": 1, "coop_lanes": 64},
-    {"kernel": 0, "coop_walk": 1, "coop_lanes": 64, "walk": 1},
-    {"kernel": 3, "coop_walk": 1, "heavy_budget": 1},
-    {"kernel": 3, "coop_walk": 1, "heavy_budget": 40},
-    {"kernel": 0, "walk": 13},
-    {"kernel": 0, "walk": 13, "block_waves": 8},
-    {"kernel": 0, "walk": 13, "coop_lanes": 0},
-    {"kernel": 0, "walk": 13, "heavy_first": 0},
-    {"kernel": 0, "walk": 13, "wave_tile": 2, "coop_lanes": 4},
-    {"kernel": 0, "walk": 5},
-    {"kernel": 0, "walk": 5, "coop_lanes": 0},
-    {"kernel": 0, "walk": 5, "heavy_first": 0},
-    {"kernel": 0, "walk": 5, "wave_tile": 3, "coop_lanes": 8},
-    {"kernel": 0, "walk": 14},
-    {"kernel": 0, "walk": 14, "coop_lanes": 0},
-    {"kernel": 0, "walk": 14, "heavy_first": 0},
-    {"kernel": 0, "walk": 14, "wave_tile": 3, "coop_lanes": 8},
+    {"coop_lanes": 0},
+    {"wave_tile": 3},
+    {"wave_tile": 2, "coop_lanes": 2},
+    {"wave_tile": 1},
+    {"coop_lanes": 1},
+    {"coop_lanes": 8},
+    {"coop_lanes": 64},
+    {"coop_walk": 1},
+    {"block_waves": 4},
+    {"heavy_first": 0},
+    {"graph": 0},
+    {"graph": 0, "heavy_stream": 0},
+    {"walk": 0},
+    {"walk": 0, "coop_lanes": 8},
+    {"walk": 0, "coop_lanes": 0},
+    {"walk": 0, "heavy_stream": 1},
+    {"block_waves": 1, "wave_tile": 0, "coop_lanes": 0},
+    {"coop_walk": 1, "coop_lanes": 8},
+    {"coop_walk": 1, "coop_lanes": 64},
+    {"coop_walk": 1, "coop_lanes": 64, "walk": 0},
 ])
 def test_schedules_identical(renderer, opts):
     """Every schedule gives the oracle's frame and counters (config 2 at the
@@ -285,7 +257,7 @@ def test_heavy_pixels(renderer, cfg_k, factor):
             renderer.set_option(k, v)
 
 
-@pytest.mark.parametrize("cfg_k,walk", [(3, 2), (4, 2), (5, 2), (3, 5), (5, 5), (3, 14), (6, 14), (5, 14)])
+@pytest.mark.parametrize("cfg_k,walk", [(3, 2), (4, 2), (5, 2), (6, 2), (3, 0)])
 def test_bench_setting_whole_frame(renderer, cfg_k, walk):
     """BASELINE configs 3, 4 and 5 as whole frames (config 5: 1M triangles,
     3840x2160, 8 bounces) under bench.py's N = 1 setting: the default
@@ -307,49 +279,6 @@ def test_bench_setting_whole_frame(renderer, cfg_k, walk):
                                           stats=stats)
             _assert_same(rgba, rad, st if stats else None, *ref)
         assert st["pixels"] == cfg.width * cfg.height
-    finally:
-        for k, v in DEFAULT_OPTS.items():
-            renderer.set_option(k, v)
-
-
-@pytest.mark.parametrize("cfg_k,bw", [(3, 16), (6, 8), (4, 16)])
-def test_top_tree_walk_whole_frame(renderer, cfg_k, bw):
-    """Walk 13 (the top tree's records in each workgroup's LDS, 8- or
-    16-wave workgroups taking consecutive tiles of the learned order): the
-    learning launch, a counting launch and a plain launch in the learned
-    order give the oracle's whole frame and counters."""
-    from rtamd import configs
-    try:
-        renderer.set_option("walk", 13)
-        renderer.set_option("block_waves", bw)
-        cfg = configs.get(cfg_k)
-        built = cfg.build()
-        cam = cfg.camera()
-        renderer.upload_scene(built)
-        ref = _oracle(built, cam.ubo_bytes(), cfg.width, cfg.height, cfg.max_bounces)
-        for stats in (False, True, False):
-            rgba, rad, st = _bands_device(renderer, cam, cfg.width, cfg.height, cfg.max_bounces, cfg.height, 1, 0,
-                                          stats=stats)
-            _assert_same(rgba, rad, st if stats else None, *ref)
-    finally:
-        for k, v in DEFAULT_OPTS.items():
-            renderer.set_option(k, v)
-
-
-def test_top_tree_walk_1m(renderer):
-    """Walk 13 on config 5 (2^20 triangles, the most its 20-bit leaf field
-    holds): every 64th row of the 4K frame."""
-    from rtamd import configs
-    try:
-        renderer.set_option("walk", 13)
-        cfg = configs.config5()
-        built = cfg.build()
-        cam = cfg.camera()
-        renderer.upload_scene(built)
-        rgba, rad, st = _bands_device(renderer, cam, cfg.width, cfg.height, cfg.max_bounces, 1, 64, 3)
-        ref = _oracle(built, cam.ubo_bytes(), cfg.width, cfg.height, cfg.max_bounces,
-                      tile=(0, 3, cfg.width, cfg.height - 3), row_step=64)
-        _assert_same(rgba, rad, st, *ref)
     finally:
         for k, v in DEFAULT_OPTS.items():
             renderer.set_option(k, v)
@@ -598,7 +527,7 @@ def test_golden_frames_on_gpu(renderer):
 
 
 @pytest.mark.parametrize("shape,n", [("left", 50), ("right", 200), ("random", 300)])
-@pytest.mark.parametrize("walk", [0, 1, 2, 5, 13, 14, "frontier"])
+@pytest.mark.parametrize("walk", [0, 2, "frontier"])
 def test_unbalanced_bvh(renderer, shape, n, walk):
     from rtamd import configs
     built = raw_bvh_scene(n, shape, seed=n)
@@ -634,13 +563,11 @@ def test_extensions_bit_exact(renderer, ext, sky):
     cam = configs.Camera.default(w, h)
     cam.ubo.sky_enabled = sky
     try:
-        renderer.set_option("kernel", 2)            # extensions force kernel 0
         renderer.set_option("extensions", ext)
         rgba, rad, st = renderer.render(cam, w, h, b, radiance=True, stats=True)
         _assert_same(rgba, rad, st, *_oracle(built, cam.ubo_bytes(), w, h, b, ext=ext))
     finally:
         renderer.set_option("extensions", 0)
-        renderer.set_option("kernel", 0)
     rgba, rad, st = renderer.render(cam, w, h, b, radiance=True, stats=True)
     _assert_same(rgba, rad, st, *_oracle(built, cam.ubo_bytes(), w, h, b))
 
@@ -669,7 +596,7 @@ def test_accumulation_bit_exact(devices):
         r.close()
 
 
-@pytest.mark.parametrize("ext,sky,walk", [(8, 1, 2), (10, 1, 2), (9, 0, 2), (11, 0, 0), (10, 1, 1), (10, 1, 13)])
+@pytest.mark.parametrize("ext,sky,walk", [(8, 1, 2), (10, 1, 2), (9, 0, 2), (11, 0, 0), (10, 1, 0)])
 def test_spheres_bit_exact(renderer, ext, sky, walk):
     """Extension bit 8 (spheres after the BVH walk; no reference counterpart)
     matches the oracle's ORC_EXT_SPHERES bit for bit, with counters, in every

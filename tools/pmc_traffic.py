@@ -1,7 +1,12 @@
 #!/usr/bin/env python3
 """HBM traffic per launch of one kernel from tools/pmc.sh passes.
 
-Usage: python tools/pmc_traffic.py gpurun_out/<TAG> "<kernel substring>[|<kernel substring>...]" [--out ...]
+Usage: python tools/pmc_traffic.py gpurun_out/<TAG> "<kernel substring>[|<kernel substring>...]"
+           [--config NAME] [--out FILE] [--merge profiles/pmc_latest.json]
+
+--merge adds (or replaces) the config's record in a multi-config file
+{"configs": {NAME: {...}}}, which bench.py reads for its roofline
+(SQ_INSTS_VMEM_RD and HBM bytes per launch).
 
 FETCH_SIZE (pass C) is in KiB and, on gfx950, counts 64-B halves of 128-B
 requests, so bytes = FETCH_SIZE x 1024 x 2 (MI355X_MICROARCH.md, HBM /
@@ -23,6 +28,7 @@ def main():
     ap.add_argument("--config", default="cfg3_50k_1920x1080_b4")
     ap.add_argument("--out", default="")
     ap.add_argument("--source", default="")
+    ap.add_argument("--merge", default="", help="multi-config JSON to add this config's record to")
     args = ap.parse_args()
     # A frame may be several launches (heavy tiles + the other tiles): the
     # kernel argument is a "|"-separated list, and per-launch means are summed.
@@ -50,7 +56,8 @@ def main():
             out["sq_wait_any_frac"] = s["SQ_WAIT_ANY"] / s["SQ_WAVE_CYCLES"]
         if "SQ_ACTIVE_INST_ANY" in s:
             out["sq_active_frac"] = s["SQ_ACTIVE_INST_ANY"] / s["SQ_WAVE_CYCLES"]
-    for k in ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_VMEM_RD", "SQ_INSTS_LDS", "TA_BUSY_avr"):
+    for k in ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_VMEM_RD", "SQ_INSTS_LDS", "TA_BUSY_avr", "SQ_WAVES",
+              "SQ_BUSY_CYCLES", "GRBM_GUI_ACTIVE", "SQ_INSTS_VMEM", "SQ_INSTS_SMEM", "SQ_BUSY_CU_CYCLES"):
         if k in s:
             out[k] = s[k]
     text = json.dumps(out, indent=1)
@@ -58,6 +65,14 @@ def main():
     if args.out:
         with open(args.out, "w") as f:
             f.write(text + "\n")
+    if args.merge:
+        allj = {"configs": {}}
+        if os.path.exists(args.merge):
+            with open(args.merge) as f:
+                allj = json.load(f)
+        allj.setdefault("configs", {})[args.config] = out
+        with open(args.merge, "w") as f:
+            f.write(json.dumps(allj, indent=1) + "\n")
 
 
 if __name__ == "__main__":

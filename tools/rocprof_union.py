@@ -1,0 +1,90 @@
+#!/usr/bin/env python3
+"""Device time per frame from a rocprofv3 kernel trace of bench.py.
+
+With D frames in flight the trace launches overlap, so no single kernel's
+duration is the frame time.  This takes the timed region's launches (the
+last K plain launches of trace_simple: bench.py's K timed steps are its last
+plain launches at N = 1; counting launches are trace_simple<true, ...> and
+learning launches trace_simple<false, true, ...>), and reports:
+
+  union_ms      the union of their [start, end) intervals: time the device
+                spent with at least one frame launch running
+  span_ms       first start to last end
+  per frame     both divided by K
+  launches      mean duration (what --stats averages) and the mean number
+                running at once (sum of durations / union)
+
+With --bench, the bench.py JSON line of the same run is read and its
+ms_per_step (host wall clock per step) is compared with union_ms / K.
+
+Usage: python tools/rocprof_union.py <kernel_trace.csv> --steps K [--bench bench.json] [--out out.json]
+"""
+import argparse
+import csv
+import json
+import statistics
+
+
+def union_length(intervals):
+    total, cur_s, cur_e = 0, None, None
+    for s, e in sorted(intervals):
+        if cur_e is None or s > cur_e:
+            if cur_e is not None:
+                total += cur_e - cur_s
+            cur_s, cur_e = s, e
+        else:
+            cur_e = max(cur_e, e)
+    if cur_e is not None:
+        total += cur_e - cur_s
+    return total
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("trace")
+    ap.add_argument("--steps", type=int, required=True, help="timed steps (frames) of the bench run")
+    ap.add_argument("--launches-per-step", type=int, default=1)
+    ap.add_argument("--bench", default="", help="the run's bench.py JSON line (file)")
+    ap.add_argument("--out", default="")
+    args = ap.parse_args()
+    rows = [r for r in csv.DictReader(open(args.trace)) if "trace_simple<false, false" in r["Kernel_Name"]]
+    rows.sort(key=lambda r: int(r["Dispatch_Id"]))
+    n = args.steps * args.launches_per_step
+    if len(rows) < n:
+        raise SystemExit(f"{len(rows)} plain trace launches in the trace, need {n}")
+    timed = rows[-n:]
+    iv = [(int(r["Start_Timestamp"]), int(r["End_Timestamp"])) for r in timed]
+    durs = [(e - s) / 1e6 for s, e in iv]
+    union = union_length(iv) / 1e6
+    span = (max(e for _, e in iv) - min(s for s, _ in iv)) / 1e6
+    names = sorted({r["Kernel_Name"][r["Kernel_Name"].index("trace_simple"):].split(">(")[0] + ">" for r in timed})
+    out = {
+        "trace": args.trace,
+        "kernels": names,
+        "frames": args.steps,
+        "launches": n,
+        "union_ms": round(union, 4),
+        "span_ms": round(span, 4),
+        "union_ms_per_frame": round(union / args.steps, 4),
+        "span_ms_per_frame": round(span / args.steps, 4),
+        "launch_ms_mean": round(statistics.mean(durs), 4),
+        "launch_ms_min": round(min(durs), 4),
+        "launch_ms_max": round(max(durs), 4),
+        "launches_in_flight_mean": round(sum(durs) / union, 3),
+    }
+    if args.bench:
+        line = next(ln for ln in open(args.bench) if ln.lstrip().startswith("{"))
+        b = json.loads(line)
+        out["bench_ms_per_step"] = b["ms_per_step"]
+        out["bench_frame_ms_device"] = b.get("roofline", {}).get("frame_ms_device")
+        out["bench_kernel_ms"] = b.get("roofline", {}).get("kernel_ms")
+        out["union_vs_ms_per_step"] = round(out["union_ms_per_frame"] / b["ms_per_step"], 4)
+    text = json.dumps(out, indent=1)
+    print(text)
+    if args.out:
+        with open(args.out, "w") as fh:
+            fh.write(text + "\n")
+
+
+if __name__ == "__main__":
+    main()

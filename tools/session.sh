@@ -1,0 +1,80 @@
+#!/bin/bash
+# One GPU session on a gpurun box (replaces round 2's per-session scripts).
+# Every GPU step runs under its own time limit; a fault, abort or timeout
+# (exit status other than 0 / 1) ends the session, so nothing else touches the
+# GPU after it.  Usage: tools/session.sh TAG step [step ...]
+#
+#   test      pytest -m gpu (every GPU parity test)
+#   smoke     __graft_entry__.smoke()
+#   bench     bench.py at the driver's 20 steps / 5 warmup (config 3)
+#   bench200  bench.py with its default 200 steps
+#   prof3     rocprofv3 --kernel-trace --stats of bench.py --steps 20, then
+#             tools/rocprof_union.py (device union per frame vs ms_per_step)
+#   prof5     the same for config 5 (--steps 10)
+#   pmc3      PMC passes A (SQ instruction counts) and C (FETCH_SIZE) of
+#             config 3, merged into gpurun_out/TAG/pmc_latest.json
+#   pmc5      the same for config 5
+#   cfgs      bench.py on configs 4, 5, 6
+#   share     tools/share_inflight_bench.py (one rank's share, frames in flight)
+#   rank0     tools/rank0_exchange_bench.py (rank 0 of N with its exchange)
+#   pipeline  tools/pipeline_bench.py (PCIe-inclusive rates)
+#   cmd       the command in $CMD (600 s)
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+TAG=${1:?tag}; shift
+OUT=gpurun_out/$TAG
+mkdir -p "$OUT"
+status() { echo "$(date +%T) $*" >> "$OUT/status.txt"; }
+run() {  # run NAME SECONDS CMD...
+  local name=$1 secs=$2; shift 2
+  status "start $name"
+  timeout -k 10 "$secs" "$@"
+  local rc=$?
+  status "end $name rc=$rc"
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then status "abort session (rc=$rc)"; exit $rc; fi
+  return 0
+}
+prof() {  # prof CONFIG STEPS
+  local c=$1 k=$2 d="$OUT/prof$1"
+  run "prof$c" 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$d" -o run -- \
+      python3 bench.py --config "$c" --steps "$k" --warmup 5 --no-cpu-baseline > "$OUT/prof$c.json" 2> "$OUT/prof$c.err"
+  local tr
+  tr=$(find "$d" -name "run_kernel_trace.csv" | head -n 1)
+  python3 tools/rocprof_union.py "$tr" --steps "$k" --bench "$OUT/prof$c.json" --out "$OUT/union_cfg$c.json" \
+      > /dev/null 2>> "$OUT/status.txt" || status "rocprof_union cfg$c failed"
+  cp "$(find "$d" -name "run_kernel_stats.csv" | head -n 1)" "$OUT/kernel_stats_cfg$c.csv" 2>/dev/null || true
+}
+pmc() {  # pmc CONFIG NAME
+  local c=$1 name=$2
+  PMC_PASSES="A C" BENCH_ARGS="--config $c" bash tools/pmc.sh "${TAG}_pmc$c" || exit $?
+  cp -r "gpurun_out/${TAG}_pmc$c" "$OUT/pmc$c"
+  python3 tools/pmc_traffic.py "gpurun_out/${TAG}_pmc$c" "trace_simple<false, false" --config "$name" \
+      --source "profiles/r03/$TAG/pmc$c (tools/pmc.sh passes A and C, bench.py --config $c)" \
+      --merge "$OUT/pmc_latest.json" > "$OUT/pmc$c.json" 2>> "$OUT/status.txt" || status "pmc_traffic cfg$c failed"
+}
+rocminfo 2>/dev/null | grep -m1 -E "gfx950" > "$OUT/rocminfo.txt"
+for s in "$@"; do
+  case $s in
+    test)     run pytest 1200 python -u -m pytest tests -m gpu -q -rA --timeout 120 --timeout-method thread \
+                  > "$OUT/pytest_gpu.log" 2>&1 ;;
+    smoke)    run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 ;;
+    bench)    run bench 600 python bench.py --steps 20 --warmup 5 > "$OUT/bench.json" 2> "$OUT/bench.err" ;;
+    bench200) run bench200 600 python bench.py > "$OUT/bench200.json" 2> "$OUT/bench200.err" ;;
+    prof3)    prof 3 20 ;;
+    prof5)    prof 5 10 ;;
+    pmc3)     pmc 3 cfg3_50k_1920x1080_b4 ;;
+    pmc5)     pmc 5 cfg5_1M_3840x2160_b8 ;;
+    cfgs)     for a in "4 50" "5 10" "6 200"; do
+                set -- $a
+                run "cfg$1" 300 python bench.py --config "$1" --steps "$2" --warmup 3 --no-cpu-baseline \
+                    > "$OUT/bench_cfg$1.json" 2> "$OUT/bench_cfg$1.err"
+              done ;;
+    share)    run share 600 python tools/share_inflight_bench.py ${SHARE_ARGS:-} > "$OUT/share.jsonl" 2> "$OUT/share.err" ;;
+    rank0)    run rank0 600 python tools/rank0_exchange_bench.py ${RANK0_ARGS:-} > "$OUT/rank0.jsonl" 2> "$OUT/rank0.err" ;;
+    pipeline) run pipeline 300 python tools/pipeline_bench.py ${PIPE_ARGS:-} > "$OUT/pipeline.jsonl" 2> "$OUT/pipeline.err" ;;
+    cmd)      run cmd 600 bash -c "$CMD" > "$OUT/cmd.log" 2>&1 ;;
+    *)        status "unknown step $s" ;;
+  esac
+done
+status "session done"
