@@ -93,18 +93,25 @@ constexpr int kExtEmissive = 2;     // a type-3 hit ends the path with attenuati
 constexpr int kExtAccumulate = 4;   // seed += frame_count*W*H; output sqrt(mean of linear colour)
 constexpr int kExtSpheres = 8;      // spheres (rt_upload_spheres) after the BVH walk, in index order
 
+constexpr int kMaxBatch = 16;  // frames per launch (rt_render_batch_device)
+
 struct TraceArgs {
     DevScene scene;
-    CamF     cam;
+    CamF     cams[kMaxBatch];   // frame f of the batch is seen through cams[f]
+    int      n_frames;          // frames in the launch (1..kMaxBatch): the same rows of each
+    int      tiles_y;           // wave-tile rows per frame (launcher-internal: ceil(th / tile height))
     int      width, height;     // full frame
     int      max_bounces;
-    int      x0, y0, tw, th;    // columns [x0, x0+tw); th local rows
+    int      x0, y0, tw, th;    // columns [x0, x0+tw); th local rows per frame
     // Local row ly is frame row y0 + ((ly / band_h) * band_stride + band_off) * band_h + ly % band_h:
     // a plain tile is band_h = th, band_stride = 1, band_off = 0; rank r of N
     // interleaved 16-row bands is band_h = 16, band_stride = N, band_off = r.
+    // With band_list (device, nullable) it is band_list[ly / band_h] * band_h + ly % band_h.
     int      band_h, band_stride, band_off;
-    uchar4*  out_rgba;          // tw*th, nullable
-    float*   out_rad;           // tw*th*3, nullable
+    const int* band_list;
+    // Outputs: n_frames x th x tw pixels, frame f's local row ly at row f * th + ly
+    uchar4*  out_rgba;          // nullable
+    float*   out_rad;           // 3 floats per pixel, nullable
     Counters* counters;         // nullable
     int      wave_tile;         // wave tile (8<<s) x (8>>s), s in 0..3
     unsigned long long* diag;   // diagnostics: 8 words per wave, or null

@@ -269,6 +269,8 @@ struct PerDevice {
     // option graph: plain launches captured once per launch key into a HIP
     // graph and replayed (the heavy-tile fork / join becomes graph edges)
     struct Graph { std::vector<uint64_t> key; hipGraphExec_t exec; };
+    struct BandList { std::vector<int> bands; int* d; };
+    std::vector<BandList> band_lists;   // rt_render_batch_device's band lists on this device
     std::vector<Graph> graphs;
     unsigned     graph_next = 0;
 };
@@ -359,7 +361,8 @@ static int concurrency(const rt_ctx* ctx) { return std::max(ctx->concurrent_laun
 // order, so the waves that set the frame time start first.  Results do not
 // change (a tile's pixels and seeds are the same whichever workgroup traces
 // it); the learning launch ends with a stream synchronisation.
-static int plan_order(const rt_ctx* ctx, PerDevice& p, TraceArgs& a, const rt_camera_ubo* cam) {
+static int plan_order(const rt_ctx* ctx, PerDevice& p, TraceArgs& a, const rt_camera_ubo* cams,
+                      const std::vector<int>* bands) {
     a.tile_order = nullptr;
     a.tiles_x = 0;
     a.split_n = 0;
@@ -375,14 +378,20 @@ static int plan_order(const rt_ctx* ctx, PerDevice& p, TraceArgs& a, const rt_ca
     p.last_heavy_px = 0;
     if (!ctx->heavy_first || a.block_waves != 1) return RT_OK;
     const int tw_w = 8 << a.wave_tile, th_w = 8 >> a.wave_tile, bw = a.block_waves;
-    const size_t n = (size_t)((a.tw + bw * tw_w - 1) / (bw * tw_w)) * bw * (size_t)((a.th + th_w - 1) / th_w);
-    const int geo[] = {a.width, a.height, a.max_bounces, a.x0, a.y0, a.tw, a.th, a.band_h, a.band_stride,
-                       a.band_off, a.wave_tile, a.ext, a.coop_lanes, a.walk, ctx->learn_cost, ctx->heavy_factor,
-                       concurrency(ctx), ctx->heavy_cap, ctx->heavy_pixel_factor};
-    std::vector<uint8_t> key(sizeof(geo) + sizeof(rt_camera_ubo) + sizeof(uint64_t));
-    std::memcpy(key.data(), geo, sizeof(geo));
-    std::memcpy(key.data() + sizeof(geo), cam, sizeof(rt_camera_ubo));
-    std::memcpy(key.data() + sizeof(geo) + sizeof(rt_camera_ubo), &ctx->scene_gen, sizeof(uint64_t));
+    // every frame of a batch has the same tiles; the order covers all of them
+    const size_t n = (size_t)((a.tw + bw * tw_w - 1) / (bw * tw_w)) * bw * (size_t)((a.th + th_w - 1) / th_w) *
+                     (size_t)a.n_frames;
+    // key = geometry (+ the band list) | the cameras | the scene
+    std::vector<int> geo = {a.width, a.height, a.max_bounces, a.x0, a.y0, a.tw, a.th, a.band_h, a.band_stride,
+                            a.band_off, a.wave_tile, a.ext, a.coop_lanes, a.walk, ctx->learn_cost,
+                            ctx->heavy_factor, concurrency(ctx), ctx->heavy_cap, ctx->heavy_pixel_factor,
+                            a.n_frames, bands ? (int)bands->size() : -1};
+    if (bands) geo.insert(geo.end(), bands->begin(), bands->end());
+    const size_t g = geo.size() * sizeof(int), c = (size_t)a.n_frames * sizeof(rt_camera_ubo);
+    std::vector<uint8_t> key(g + c + sizeof(uint64_t));
+    std::memcpy(key.data(), geo.data(), g);
+    std::memcpy(key.data() + g, cams, c);
+    std::memcpy(key.data() + g + c, &ctx->scene_gen, sizeof(uint64_t));
     // Use a learned order: the exact key's; or, when only the camera differs
     // from a learned key and the camera has just moved (option reuse_order),
     // the newest order of the same frame geometry and scene.  The order and the
@@ -433,7 +442,6 @@ static int plan_order(const rt_ctx* ctx, PerDevice& p, TraceArgs& a, const rt_ca
     // Has the camera stopped?  Compared with the last launch of the same
     // frame geometry and scene, not with the device's last launch: several
     // geometries interleave on one device (band offsets, callers' streams).
-    const size_t g = sizeof(geo), c = sizeof(rt_camera_ubo);
     bool repeat = false;
     {
         std::vector<uint8_t> geo_scene(key.begin(), key.begin() + g);
@@ -454,7 +462,7 @@ static int plan_order(const rt_ctx* ctx, PerDevice& p, TraceArgs& a, const rt_ca
         if (o.n == n && o.key == key) return use(o);
     if (ctx->reuse_order && !repeat) {
         for (auto it = p.orders.rbegin(); it != p.orders.rend(); ++it)
-            if (it->n == n && std::memcmp(it->key.data(), key.data(), g) == 0 &&
+            if (it->n == n && it->key.size() == key.size() && std::memcmp(it->key.data(), key.data(), g) == 0 &&
                 std::memcmp(it->key.data() + g + c, key.data() + g + c, sizeof(uint64_t)) == 0)
                 return use(*it);
     }
@@ -570,7 +578,8 @@ static int learn_order(const rt_ctx* ctx, PerDevice& p, const TraceArgs& a, hipS
     return RT_OK;
 }
 
-static int set_schedule(const rt_ctx* ctx, PerDevice& p, TraceArgs& a, const rt_camera_ubo* cam) {
+static int set_schedule(const rt_ctx* ctx, PerDevice& p, TraceArgs& a, const rt_camera_ubo* cam,
+                        const std::vector<int>* bands = nullptr) {
     a.wave_tile = ctx->wave_tile;
     a.coop_lanes = ctx->coop_lanes;
     a.walk = ctx->walk;
@@ -583,6 +592,10 @@ static int set_schedule(const rt_ctx* ctx, PerDevice& p, TraceArgs& a, const rt_
     a.frame_count = cam->frame_count;
     a.accum = nullptr;
     if (a.ext & kExtAccumulate) {
+        if (a.n_frames != 1) {
+            set_error("the accumulation extension renders one frame per launch (its sums are per pixel)");
+            return RT_ERR_INVALID_ARG;
+        }
         const size_t need = (size_t)a.tw * (size_t)a.th * 3;
         if (need != p.accum_n) {                 // a new frame partition starts from zero sums
             if (p.d_accum) (void)hipFree(p.d_accum);
@@ -599,7 +612,8 @@ static int set_schedule(const rt_ctx* ctx, PerDevice& p, TraceArgs& a, const rt_
         // 8 words per wave (+ 63 per heavy tile traced one pixel per wave)
         const int tw_w = 8 << a.wave_tile, th_w = 8 >> a.wave_tile;
         const int gw = std::max(4, a.block_waves);   // columns are rounded up to whole workgroups
-        const size_t waves = (size_t)((a.tw + gw * tw_w - 1) / (gw * tw_w)) * ((a.th + th_w - 1) / th_w) * gw;
+        const size_t waves = (size_t)((a.tw + gw * tw_w - 1) / (gw * tw_w)) * ((a.th + th_w - 1) / th_w) * gw *
+                             (size_t)a.n_frames;
         const size_t split = ctx->heavy_first ? (size_t)(ctx->heavy_tiles < 0 ? kMaxHeavy : ctx->heavy_tiles) * 63 : 0;
         const size_t words = (waves + split) * 8;
         if (words > p.diag_cap) {
@@ -612,7 +626,7 @@ static int set_schedule(const rt_ctx* ctx, PerDevice& p, TraceArgs& a, const rt_
         p.diag_used = words;
         a.diag = p.d_diag;
     }
-    return plan_order(ctx, p, a, cam);
+    return plan_order(ctx, p, a, cam, bands);
 }
 
 // Option graph: a plain kernel-0 launch (no counters, no diagnostics) is
@@ -626,12 +640,10 @@ static std::vector<uint64_t> launch_key(const TraceArgs& a, hipStream_t s) {
     auto P = [](const void* q) { return (uint64_t)(uintptr_t)q; };
     auto F = [](float f) { uint32_t u; std::memcpy(&u, &f, 4); return (uint64_t)u; };
     const DevScene& sc = a.scene;
-    const CamF& c = a.cam;
-    return {P(s), P(sc.nodes), P(sc.leafs), P(sc.pairs), P(sc.nodes2), P(sc.leafs2), P(sc.norms), P(sc.mats), P(sc.spheres),
+    std::vector<uint64_t> k = {P(s), P(sc.nodes), P(sc.leafs), P(sc.pairs), P(sc.nodes2), P(sc.leafs2), P(sc.norms), P(sc.mats), P(sc.spheres),
             (uint64_t)sc.n_spheres, (uint64_t)sc.n_nodes, (uint64_t)sc.end, (uint64_t)sc.n_tris,
             (uint64_t)sc.root_leaf, F(sc.root_box[0]), F(sc.root_box[1]), F(sc.root_box[2]), F(sc.root_box[3]),
-            F(sc.root_box[4]), F(sc.root_box[5]),
-            F(c.ox), F(c.oy), F(c.oz), F(c.lx), F(c.ly), F(c.lz), F(c.hx), F(c.hy), F(c.hz), F(c.vx), F(c.vy), F(c.vz),
+            F(sc.root_box[4]), F(sc.root_box[5]), (uint64_t)a.n_frames, P(a.band_list),
             (uint64_t)a.width, (uint64_t)a.height, (uint64_t)a.max_bounces, (uint64_t)a.x0, (uint64_t)a.y0,
             (uint64_t)a.tw, (uint64_t)a.th, (uint64_t)a.band_h, (uint64_t)a.band_stride, (uint64_t)a.band_off,
             P(a.out_rgba), P(a.out_rad), (uint64_t)a.wave_tile,
@@ -639,6 +651,11 @@ static std::vector<uint64_t> launch_key(const TraceArgs& a, hipStream_t s) {
             (uint64_t)a.frame_count, P(a.accum), (uint64_t)a.walk, (uint64_t)a.block_waves, P(a.tile_order),
             (uint64_t)a.heavy_tiles, (uint64_t)(a.aux_stream != nullptr), (uint64_t)a.heavy_fused, P(a.heavy_px),
             (uint64_t)a.n_heavy_px, P(a.tile_mask), (uint64_t)a.coop_walk};
+    for (int f = 0; f < a.n_frames; ++f) {
+        const CamF& c = a.cams[f];
+        for (float v : {c.ox, c.oy, c.oz, c.lx, c.ly, c.lz, c.hx, c.hy, c.hz, c.vx, c.vy, c.vz}) k.push_back(F(v));
+    }
+    return k;
 }
 
 static int launch(const rt_ctx* ctx, PerDevice& p, const TraceArgs& a, hipStream_t s) {
@@ -791,6 +808,8 @@ int rt_destroy(rt_ctx* ctx) {
         if (p.d_learn_lane) (void)hipFree(p.d_learn_lane);
         free_orders(p);
         free_graphs(p);
+        for (auto& l : p.band_lists) (void)hipFree(l.d);
+        p.band_lists.clear();
         for (int k = 0; k < 4; ++k) {
             if (p.aux[k]) (void)hipStreamDestroy(p.aux[k]);
             if (p.aux_fork[k]) (void)hipEventDestroy(p.aux_fork[k]);
@@ -997,10 +1016,12 @@ int rt_render_tile_device(rt_ctx* ctx, const rt_camera_ubo* cam, int width, int 
     hipStream_t s = static_cast<hipStream_t>(stream);   // NULL = the null stream
     TraceArgs a;
     a.scene = p.scene;
-    a.cam = cam_from_ubo(cam);
+    a.cams[0] = cam_from_ubo(cam);
+    a.n_frames = 1;
     a.width = width; a.height = height; a.max_bounces = max_bounces;
     a.x0 = x0; a.y0 = y0; a.tw = tile_w; a.th = tile_h;
     a.band_h = tile_h; a.band_stride = 1; a.band_off = 0;
+    a.band_list = nullptr;
     a.out_rgba = static_cast<uchar4*>(d_out_rgba);
     a.out_rad = static_cast<float*>(d_out_radiance);
     // counters before set_schedule: a counting launch must not become the
@@ -1031,19 +1052,54 @@ int rt_band_rows(int height, int band_h, int band_stride, int band_off) {
     return rows;
 }
 
-static int render_bands_on(const rt_ctx* ctx, PerDevice& p, const rt_camera_ubo* cam, int width, int height, int max_bounces,
-                           int band_h, int band_stride, int band_off, int rows,
-                           uchar4* d_rgba, float* d_rad, hipStream_t s, bool count) {
+// A band list on the device (rt_render_batch_device), uploaded once per
+// distinct list and kept for the context's lifetime (a launch in flight may
+// still read it); past kMaxBandLists the device is drained and they are
+// dropped.
+static constexpr size_t kMaxBandLists = 256;
+
+static int device_band_list(PerDevice& p, const std::vector<int>& bands, const int** out) {
+    for (const auto& l : p.band_lists)
+        if (l.bands == bands) { *out = l.d; return RT_OK; }
+    if (p.band_lists.size() >= kMaxBandLists) {
+        RT_HIP_CHECK(hipDeviceSynchronize());
+        for (auto& l : p.band_lists) (void)hipFree(l.d);
+        p.band_lists.clear();
+    }
+    int* d = nullptr;
+    RT_HIP_CHECK(hipMalloc(&d, std::max<size_t>(1, bands.size()) * sizeof(int)));
+    const hipError_t e = hipMemcpy(d, bands.data(), bands.size() * sizeof(int), hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+        (void)hipFree(d);
+        RT_HIP_CHECK(e);
+    }
+    p.band_lists.push_back(PerDevice::BandList{bands, d});
+    *out = d;
+    return RT_OK;
+}
+
+// One launch over the same rows of n_frames frames (camera cams[f] each):
+// the band_h-row bands b with b mod band_stride == band_off, or, with
+// `bands`, the listed bands; rows per frame = rows.  Outputs hold the frames
+// one after another (n_frames x rows x width).
+static int render_rows_on(const rt_ctx* ctx, PerDevice& p, const rt_camera_ubo* cams, int n_frames, int width,
+                          int height, int max_bounces, int band_h, int band_stride, int band_off,
+                          const std::vector<int>* bands, int rows, uchar4* d_rgba, float* d_rad, hipStream_t s,
+                          bool count) {
     TraceArgs a;
     a.scene = p.scene;
-    a.cam = cam_from_ubo(cam);
+    for (int f = 0; f < n_frames; ++f) a.cams[f] = cam_from_ubo(cams + f);
+    a.n_frames = n_frames;
     a.width = width; a.height = height; a.max_bounces = max_bounces;
     a.x0 = 0; a.y0 = 0; a.tw = width; a.th = rows;
     a.band_h = band_h; a.band_stride = band_stride; a.band_off = band_off;
+    a.band_list = nullptr;
+    if (bands)
+        if (int rb = device_band_list(p, *bands, &a.band_list)) return rb;
     a.out_rgba = d_rgba;
     a.out_rad = d_rad;
     a.counters = count ? p.d_counters : nullptr;
-    if (int rs = set_schedule(ctx, p, a, cam)) return rs;
+    if (int rs = set_schedule(ctx, p, a, cams, bands)) return rs;
     if (count) {
         RT_HIP_CHECK(hipMemsetAsync(p.d_counters, 0, sizeof(Counters), s));
         RT_HIP_CHECK(hipEventRecord(p.ev0, s));   // the timing events exist for stats only
@@ -1052,6 +1108,13 @@ static int render_bands_on(const rt_ctx* ctx, PerDevice& p, const rt_camera_ubo*
     if (int ro = learn_order(ctx, p, a, s)) return ro;
     if (count) RT_HIP_CHECK(hipEventRecord(p.ev1, s));
     return RT_OK;
+}
+
+static int render_bands_on(const rt_ctx* ctx, PerDevice& p, const rt_camera_ubo* cam, int width, int height,
+                           int max_bounces, int band_h, int band_stride, int band_off, int rows,
+                           uchar4* d_rgba, float* d_rad, hipStream_t s, bool count) {
+    return render_rows_on(ctx, p, cam, 1, width, height, max_bounces, band_h, band_stride, band_off, nullptr, rows,
+                          d_rgba, d_rad, s, count);
 }
 
 static int collect_stats(const rt_ctx* ctx, PerDevice& p, uint64_t pixels, rt_stats* stats, bool accumulate) {
@@ -1095,6 +1158,58 @@ int rt_render_bands_device(rt_ctx* ctx, const rt_camera_ubo* cam, int width, int
     if (stats) {
         RT_HIP_CHECK(hipEventSynchronize(p.ev1));
         return collect_stats(ctx, p, (uint64_t)rows * width, stats, false);
+    }
+    return RT_OK;
+}
+
+int rt_band_list_rows(int height, int band_h, const int32_t* bands, int n_bands) {
+    if (height < 1 || band_h < 1 || n_bands < 0 || (n_bands > 0 && !bands)) return -1;
+    const int n_all = (height + band_h - 1) / band_h;
+    int rows = 0;
+    for (int k = 0; k < n_bands; ++k) {
+        if (bands[k] < 0 || bands[k] >= n_all || (k > 0 && bands[k] <= bands[k - 1])) return -1;
+        rows += std::min(band_h, height - bands[k] * band_h);
+    }
+    return rows;
+}
+
+int rt_render_batch_device(rt_ctx* ctx, const rt_camera_ubo* cams, int n_frames, int width, int height,
+                           int max_bounces, int band_h, const int32_t* bands, int n_bands,
+                           void* d_out_rgba, void* d_out_radiance, void* stream, rt_stats* stats) {
+    int rc = check_render_args(ctx, cams, width, height, max_bounces, "rt_render_batch_device");
+    if (rc) return rc;
+    if (n_frames < 1 || n_frames > kMaxBatch) {
+        set_error("rt_render_batch_device: n_frames must be in [1, %d], got %d", kMaxBatch, n_frames);
+        return RT_ERR_INVALID_ARG;
+    }
+    int rows;
+    std::vector<int> list;
+    if (bands) {
+        rows = rt_band_list_rows(height, band_h, bands, n_bands);
+        if (rows < 0) {
+            set_error("rt_render_batch_device: bad band list (band_h %d, %d bands: indices must increase and lie "
+                      "below ceil(height / band_h))", band_h, n_bands);
+            return RT_ERR_INVALID_ARG;
+        }
+        list.assign(bands, bands + n_bands);
+    } else {
+        band_h = height;                     // the whole frame
+        rows = height;
+    }
+    if (rows == 0) {
+        if (stats) std::memset(stats, 0, sizeof *stats);
+        return RT_OK;
+    }
+    PerDevice& p = ctx->dev[0];
+    RT_HIP_CHECK(hipSetDevice(p.device));
+    hipStream_t s = static_cast<hipStream_t>(stream);   // NULL = the null stream
+    rc = render_rows_on(ctx, p, cams, n_frames, width, height, max_bounces, band_h, 1, 0, bands ? &list : nullptr,
+                        rows, static_cast<uchar4*>(d_out_rgba), static_cast<float*>(d_out_radiance), s,
+                        stats != nullptr);
+    if (rc) return rc;
+    if (stats) {
+        RT_HIP_CHECK(hipEventSynchronize(p.ev1));
+        return collect_stats(ctx, p, (uint64_t)rows * width * n_frames, stats, false);
     }
     return RT_OK;
 }

@@ -88,24 +88,28 @@ __device__ __forceinline__ uint8_t unorm8(float c) {
 
 // Frame row of local row ly (rt_internal.h, TraceArgs band mapping).
 __device__ __forceinline__ int frame_row(const TraceArgs& a, int ly) {
+    if (a.band_list) return a.y0 + a.band_list[ly / a.band_h] * a.band_h + ly % a.band_h;
     return a.y0 + ((ly / a.band_h) * a.band_stride + a.band_off) * a.band_h + ly % a.band_h;
 }
 
-// Seed, AA jitter and primary ray (:164-173).
-__device__ __forceinline__ void primary_ray_seeded(const TraceArgs& a, int x, int y, uint32_t& seed, V3& o, V3& d);
-__device__ __forceinline__ void primary_ray(const TraceArgs& a, int x, int y, uint32_t& seed, V3& o, V3& d) {
+// Seed, AA jitter and primary ray (:164-173) of frame f of the launch.
+__device__ __forceinline__ void primary_ray_seeded(const TraceArgs& a, int f, int x, int y, uint32_t& seed, V3& o,
+                                                   V3& d);
+__device__ __forceinline__ void primary_ray(const TraceArgs& a, int f, int x, int y, uint32_t& seed, V3& o, V3& d) {
     seed = (uint32_t)(y * a.width + x);
-    primary_ray_seeded(a, x, y, seed, o, d);
+    primary_ray_seeded(a, f, x, y, seed, o, d);
 }
 
 // primary_ray with a caller-chosen initial seed (the accumulation extension).
-__device__ __forceinline__ void primary_ray_seeded(const TraceArgs& a, int x, int y, uint32_t& seed, V3& o, V3& d) {
+__device__ __forceinline__ void primary_ray_seeded(const TraceArgs& a, int f, int x, int y, uint32_t& seed, V3& o,
+                                                   V3& d) {
     const float u = ((float)x + rnd(seed)) / (float)a.width;
     const float v = ((float)(a.height - 1 - y) + rnd(seed)) / (float)a.height;
-    const V3 cam_o = {a.cam.ox, a.cam.oy, a.cam.oz};
-    const V3 cam_l = {a.cam.lx, a.cam.ly, a.cam.lz};
-    const V3 cam_h = {a.cam.hx, a.cam.hy, a.cam.hz};
-    const V3 cam_v = {a.cam.vx, a.cam.vy, a.cam.vz};
+    const CamF& c = a.cams[f];                 // f is wave-uniform: scalar loads of the kernel argument
+    const V3 cam_o = {c.ox, c.oy, c.oz};
+    const V3 cam_l = {c.lx, c.ly, c.lz};
+    const V3 cam_h = {c.hx, c.hy, c.hz};
+    const V3 cam_v = {c.vx, c.vy, c.vz};
     o = cam_o;
     d = vnormalize(vsub(vadd(vadd(cam_l, vscale(cam_h, u)), vscale(cam_v, v)), cam_o));
 }
@@ -619,14 +623,14 @@ constexpr int kFeatFused = 64;    // heavy tiles in the same launch: workgroups 
 // tile path's registers are not live in it and the launch keeps the tile
 // path's 73 VGPRs (out of line it would need 119 and spill the arguments).
 template <bool COUNT>
-__device__ __forceinline__ void heavy_pixel(const TraceArgs& a, int lx, int ly, uint4* F) {
+__device__ __forceinline__ void heavy_pixel(const TraceArgs& a, int f, int lx, int ly, int lyo, uint4* F) {
     const int lane = threadIdx.x & 63;
     const int end = a.scene.end;
     unsigned long long c_seg = 0, c_node = 0, c_tri = 0, c_mat = 0;
     if (lx < a.tw && ly < a.th) {
         uint32_t seed;
         V3 o, d;
-        primary_ray(a, a.x0 + lx, frame_row(a, ly), seed, o, d);
+        primary_ray(a, f, a.x0 + lx, frame_row(a, ly), seed, o, d);
         V3 att = {1.0f, 1.0f, 1.0f};
         V3 fin = {0.0f, 0.0f, 0.0f};
         int rounds = 0;
@@ -661,7 +665,7 @@ __device__ __forceinline__ void heavy_pixel(const TraceArgs& a, int lx, int ly, 
             d = nd;
             // b == max_bounces - 1 leaves fin black (:229-231)
         }
-        if (lane == 0) write_pixel(a, lx, ly, fin);
+        if (lane == 0) write_pixel(a, lx, lyo, fin);
     }
     if (COUNT) {
         if (lane != 0) c_seg = c_node = c_tri = c_mat = 0;                  // wave-uniform: counted once
@@ -725,7 +729,9 @@ void trace_simple(TraceArgs a) {
         bx = t % a.tiles_x;
         by = t / a.tiles_x;
         if ((FEAT & kFeatFused) && sub >= 0) {           // a heavy tile's pixel, dispatched first
-            heavy_pixel<COUNT>(a, bx * tw_w + (sub & (tw_w - 1)), by * th_w + (sub >> (3 + s)), fr);
+            const int hf = by / a.tiles_y;               // its frame of the batch
+            const int hy = (by - hf * a.tiles_y) * th_w + (sub >> (3 + s));
+            heavy_pixel<COUNT>(a, hf, bx * tw_w + (sub & (tw_w - 1)), hy, hf * a.th + hy, fr);
             if (DIAG) {
                 diag_stamp(drec, 1);
                 if (lane == 0) {
@@ -740,8 +746,11 @@ void trace_simple(TraceArgs a) {
     }
     const int tl = sub >= 0 ? sub : lane;                // the tile pixel this lane traces
     const int col = bx * a.block_waves + wave;           // wave-tile column
+    const int fr_i = by / a.tiles_y;                     // the wave's frame of the batch (tile rows of frame
+    by -= fr_i * a.tiles_y;                              //   f follow those of frame f - 1)
     const int lx = col * tw_w + (tl & (tw_w - 1));
-    const int ly = by * th_w + (tl >> (3 + s));
+    const int ly = by * th_w + (tl >> (3 + s));          // row within the frame's rows
+    const int lyo = fr_i * a.th + ly;                    // output row
     const bool pixel = lx < a.tw && ly < a.th && (sub < 0 || lane == 0) && !((skip_lanes >> lane) & 1ull);
     const int coop_lanes = sub >= 0 ? 64 : a.coop_lanes;
     const float4* __restrict__ nodes = a.scene.nodes;
@@ -759,9 +768,9 @@ void trace_simple(TraceArgs a) {
         if ((FEAT & kFeatExt) && (a.ext & kExtAccumulate)) {
             // extension: a new sample per frame; frame 0 is the reference's seed (:164)
             seed = (uint32_t)(y * a.width + x) + (uint32_t)a.frame_count * (uint32_t)(a.width * a.height);
-            primary_ray_seeded(a, x, y, seed, o, d);
+            primary_ray_seeded(a, fr_i, x, y, seed, o, d);
         } else {
-            primary_ray(a, x, y, seed, o, d);
+            primary_ray(a, fr_i, x, y, seed, o, d);
         }
     }
     V3 att = {1.0f, 1.0f, 1.0f};
@@ -915,11 +924,11 @@ void trace_simple(TraceArgs a) {
                     fin = vmul(att, sky_color(d));                        // (extension: sky off is black)
                 alive = false;
             }
-            if (!alive) finish_pixel<FEAT>(a, lx, ly, fin);
+            if (!alive) finish_pixel<FEAT>(a, lx, lyo, fin);
         }
     }
     // A path still alive here ran no bounce at all (max_bounces 0): black.
-    if (alive) finish_pixel<FEAT>(a, lx, ly, V3{0.0f, 0.0f, 0.0f});
+    if (alive) finish_pixel<FEAT>(a, lx, lyo, V3{0.0f, 0.0f, 0.0f});
     if (COUNT) flush_counters(a.counters, c_seg, c_node, c_tri, c_mat);
     if (DIAG) {
         diag_stamp(drec, 1);
@@ -946,11 +955,13 @@ void trace_simple(TraceArgs a) {
 
 hipError_t launch_trace(const TraceArgs& a, hipStream_t stream) {
     const int tw_w = 8 << a.wave_tile, th_w = 8 >> a.wave_tile, bw = a.block_waves;
-    dim3 grid((a.tw + bw * tw_w - 1) / (bw * tw_w), (a.th + th_w - 1) / th_w);
+    const int tiles_y = (a.th + th_w - 1) / th_w;       // wave-tile rows of one frame
+    dim3 grid((a.tw + bw * tw_w - 1) / (bw * tw_w), a.n_frames * tiles_y);
     const dim3 block(64 * bw);
     const int feat = (a.coop_lanes > 0 ? kFeatCoopTail : 0) | (a.ext != 0 ? kFeatExt : 0) |
                      (a.coop_lanes > 0 && a.coop_walk ? kFeatFrontier : 0);
     TraceArgs ao = a;
+    ao.tiles_y = tiles_y;
     bool join = false;
     if (a.tile_order) {      // heavy-first: a 1-D grid over the ordered tiles
         ao.tiles_x = (int)grid.x;

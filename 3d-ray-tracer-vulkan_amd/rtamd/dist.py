@@ -1,20 +1,33 @@
 """Multi-GPU frame tiling: one process per GPU (torch.distributed; backend
 "nccl" = RCCL over xGMI on MI355X, "gloo" for CPU tests).
 
-Two strong-scaling partitions of a frame, and a weak-scaling batch:
+Partitions of a frame over the N ranks:
 
-* rotating row pieces (bench.py's N > 1 default; block_layout,
-  exchange_blocks): one contiguous run of rows per rank, laid out in an order
-  that rotates every frame; rank 0 traces its piece in place and receives the
-  others straight into the frame (RCCL point-to-point in one group);
-* interleaved row bands (gather_frame, gather_frames): rank r of N traces the
-  band_h-row bands r, r+N, r+2N, ...; one gather of the packed bands to rank
-  0, which assembles the frame with one index_select;
-* frame batches (BatchPlan, gather_batch): N frames per step, bands rotated.
+* weighted interleaved row bands (bench.py's N > 1 default; band_owners,
+  SharePlan, gather_shares): the band_h-row bands are dealt out by a smooth
+  weighted round robin, rank 0 with weight root_weight (it also receives and
+  assembles every frame) and the others with weight 1, so every rank's bands
+  are spread over the frame; a rank traces its bands of a batch of frames in
+  one launch (rt_render_batch_device), one gather per batch brings the
+  packed bands to rank 0, which assembles the frames with one index_select.
+  root_weight 1 is the plain interleave: rank r gets the bands b = r mod N
+  (band_rows, gather_frame, gather_frames);
+* a tile grid (tile_grid, tile_rects, TilePlan, gather_tiles): N = gx x gy
+  rectangles, e.g. BASELINE config 4's 2 x 2 over 4 GPUs; one gather of the
+  (padded) tiles and one index_select;
+* rotating row pieces (block_layout, exchange_blocks; an option, measured
+  slower on the sending ranks): one contiguous run of rows per rank, laid out
+  in an order that rotates every frame; rank 0 receives the others straight
+  into the frame (RCCL point-to-point in one group);
+* frame batches (BatchPlan, gather_batch; weak scaling): N frames per step,
+  bands rotated.
 
-The scene is replicated on every rank (uploaded once per rank); pixels are
-independent and seeded by their global (x, y) (compute_dynamic_ray.comp:164),
-so every partition's frame equals the one-GPU frame bit for bit.
+Every gather can carry the RGBA8 frame and, beside it, the float radiance
+(the sqrt'd colour before quantisation, 3 floats per pixel), which the north
+star's "RCCL gather of per-tile radiance buffers" names.  The scene is
+replicated on every rank (uploaded once per rank); pixels are independent and
+seeded by their global (x, y) (compute_dynamic_ray.comp:164), so every
+partition's frame equals the one-GPU frame bit for bit.
 """
 from __future__ import annotations
 
@@ -74,7 +87,217 @@ def gather_frames(local, height: int, band_h: int, group=None):
     return gather_batch(local, plan, group, src_index=src_index)
 
 
-# --- rotating row blocks (strong scaling, bench.py's N > 1 default) ----------
+# --- weighted interleaved bands, batched (bench.py's N > 1 default) --------
+
+
+def band_owners(height: int, band_h: int, world: int, root_weight: float = 1.0) -> np.ndarray:
+    """Owner rank of every band_h-row band of the frame: a smooth weighted
+    round robin (each band goes to the rank with the largest running credit;
+    credits grow by the rank's weight and the winner pays the total), rank 0
+    weighted root_weight and the others 1, ties to the lower rank.  Every
+    rank's bands are spread over the whole frame, in proportion to its weight;
+    root_weight 1 gives band b to rank b mod world."""
+    n = (height + band_h - 1) // band_h
+    w = np.ones(world, np.float64)
+    w[0] = max(0.0, float(root_weight))
+    total = w.sum()
+    credit = np.zeros(world, np.float64)
+    owner = np.empty(n, np.int64)
+    for b in range(n):
+        credit += w
+        r = int(np.argmax(credit))          # first maximum: the lower rank wins ties
+        owner[b] = r
+        credit[r] -= total
+    return owner
+
+
+def band_list(height: int, band_h: int, world: int, rank: int, root_weight: float = 1.0) -> np.ndarray:
+    """rank's band indices, increasing (rt_render_batch_device's list)."""
+    return np.flatnonzero(band_owners(height, band_h, world, root_weight) == rank).astype(np.int32)
+
+
+def list_rows(height: int, band_h: int, bands) -> np.ndarray:
+    """Frame rows of a band list, in the packed order the kernel writes them."""
+    bands = np.asarray(bands, np.int64)
+    if len(bands) == 0:
+        return np.zeros(0, np.int64)
+    rows = (bands[:, None] * band_h + np.arange(band_h)[None, :]).reshape(-1)
+    return rows[rows < height]
+
+
+class SharePlan:
+    """Row bookkeeping of a batch of n_frames frames over world ranks in
+    weighted bands.  Rank r's exchange buffer holds its shares of the batch's
+    frames back to back (frame f's rows at [off[r][f], off[r][f] + R), as
+    rt_render_batch_device writes a batch of frames), padded to per_rank rows
+    so that every rank sends the same size.
+
+    rotate=False: rank r has the same bands in every frame (strong scaling,
+    bench.py --partition bands).  rotate=True (weights 1 only): in frame f,
+    rank r traces the bands of position (r + f) mod world, so over world
+    frames every rank traces every band once (weak scaling, --partition
+    frames)."""
+
+    def __init__(self, height: int, band_h: int, world: int, n_frames: int, root_weight: float = 1.0,
+                 rotate: bool = False):
+        if rotate and root_weight != 1.0:
+            raise ValueError("rotating bands take equal weights")
+        self.height, self.band_h, self.world, self.n_frames = height, band_h, world, n_frames
+        self.root_weight, self.rotate = root_weight, rotate
+        owner = band_owners(height, band_h, world, root_weight)
+        self.pos_bands = [np.flatnonzero(owner == r).astype(np.int32) for r in range(world)]
+        self.pos_rows = [list_rows(height, band_h, b) for b in self.pos_bands]
+        self.bands = self.pos_bands                    # rank r's bands (rotate=False)
+        self.rows = self.pos_rows
+        self.counts = [len(x) for x in self.pos_rows]
+        self.max_rows = max(self.counts)
+        self.off = [[0] * n_frames for _ in range(world)]
+        self.per_rank = 0
+        for r in range(world):
+            o = 0
+            for f in range(n_frames):
+                self.off[r][f] = o
+                o += len(self.frame_rows(r, f))
+            self.per_rank = max(self.per_rank, o)
+        src = np.empty(n_frames * height, np.int64)
+        for r in range(world):
+            for f in range(n_frames):
+                rows = self.frame_rows(r, f)
+                src[f * height + rows] = r * self.per_rank + self.off[r][f] + np.arange(len(rows))
+        self.src = src
+
+    def position(self, rank: int, frame: int) -> int:
+        return (rank + frame) % self.world if self.rotate else rank
+
+    def frame_bands(self, rank: int, frame: int) -> np.ndarray:
+        return self.pos_bands[self.position(rank, frame)]
+
+    def frame_rows(self, rank: int, frame: int) -> np.ndarray:
+        return self.pos_rows[self.position(rank, frame)]
+
+
+_SHARE_PLANS: dict = {}
+
+
+def cached_share_plan(height: int, band_h: int, world: int, n_frames: int, root_weight: float, device,
+                      rotate: bool = False):
+    """SharePlan and its source-row index on `device`, built once per layout."""
+    import torch
+    key = (height, band_h, world, n_frames, float(root_weight), str(device), rotate)
+    hit = _SHARE_PLANS.get(key)
+    if hit is None:
+        plan = SharePlan(height, band_h, world, n_frames, root_weight, rotate)
+        hit = (plan, torch.as_tensor(plan.src, device=device))
+        _SHARE_PLANS[key] = hit
+    return hit
+
+
+def gather_shares(local, plan: SharePlan, group=None, src_index=None, n_frames: int = None):
+    """local: this rank's [per_rank, W, C] exchange buffer (its packed shares
+    of the batch's frames, then padding).  One gather into a [world, ...]
+    stack on rank 0 and one index_select; returns the [n_frames, height, W, C]
+    frames on rank 0 (the first n_frames of the batch, default all), None
+    elsewhere."""
+    import torch
+    import torch.distributed as dist
+    if local.shape[0] != plan.per_rank:
+        raise ValueError(f"gather_shares: {local.shape[0]} rows, the plan sends {plan.per_rank}")
+    rank = dist.get_rank(group)
+    stack = gl = None
+    if rank == 0:
+        stack = torch.empty((plan.world,) + tuple(local.shape), dtype=local.dtype, device=local.device)
+        gl = list(stack.unbind(0))
+    if dist.get_backend(group) == "gloo" and local.is_cuda:       # gloo moves host memory
+        host = local.cpu()
+        hl = [torch.empty_like(host) for _ in range(plan.world)] if rank == 0 else None
+        dist.gather(host, hl, dst=0, group=group)
+        if rank == 0:
+            for d, h in zip(gl, hl):
+                d.copy_(h)
+    else:
+        dist.gather(local, gl, dst=0, group=group)
+    if rank != 0:
+        return None
+    if src_index is None:
+        src_index = torch.as_tensor(plan.src, device=local.device)
+    n = plan.n_frames if n_frames is None else n_frames
+    out = torch.index_select(stack.reshape(plan.world * plan.per_rank, -1), 0, src_index[: n * plan.height])
+    return out.reshape((n, plan.height) + tuple(local.shape[1:]))
+
+
+# --- a tile grid (BASELINE config 4: the screen tiled 2 x 2 over 4 GPUs) ----
+
+
+def tile_grid(world: int):
+    """(gx, gy) with gx * gy == world, as square as possible, gx >= gy
+    (1 -> 1 x 1, 2 -> 2 x 1, 4 -> 2 x 2, 8 -> 4 x 2)."""
+    gy = int(np.floor(np.sqrt(world)))
+    while world % gy:
+        gy -= 1
+    return world // gy, gy
+
+
+def tile_rects(width: int, height: int, gx: int, gy: int):
+    """Rank r's rectangle (x0, y0, w, h), row-major over the grid; the
+    remainder pixels go to the last column / row."""
+    xs = [width * i // gx for i in range(gx + 1)]
+    ys = [height * j // gy for j in range(gy + 1)]
+    return [(xs[i], ys[j], xs[i + 1] - xs[i], ys[j + 1] - ys[j]) for j in range(gy) for i in range(gx)]
+
+
+class TilePlan:
+    """Pixel bookkeeping of n_frames frames over a tile grid: rank r sends
+    [n_frames, hmax * wmax] pixels, frame f's tile packed at the start of its
+    row (h x w, row pitch w: rt_render_tile_device's layout); src maps every
+    frame pixel to its row in the gathered [world * n_frames * hmax * wmax]
+    stack."""
+
+    def __init__(self, width: int, height: int, world: int, n_frames: int = 1):
+        self.width, self.height, self.world, self.n_frames = width, height, world, n_frames
+        self.gx, self.gy = tile_grid(world)
+        self.rects = tile_rects(width, height, self.gx, self.gy)
+        self.hmax = max(r[3] for r in self.rects)
+        self.wmax = max(r[2] for r in self.rects)
+        self.tile_px = self.hmax * self.wmax
+        per = n_frames * self.tile_px
+        src = np.empty((n_frames, height, width), np.int64)
+        for r, (x0, y0, w, h) in enumerate(self.rects):
+            yy, xx = np.meshgrid(np.arange(h), np.arange(w), indexing="ij")
+            for f in range(n_frames):
+                src[f, y0:y0 + h, x0:x0 + w] = r * per + f * self.tile_px + yy * w + xx
+        self.src = src.reshape(-1)
+
+
+def gather_tiles(local, plan: TilePlan, group=None, src_index=None):
+    """local: this rank's [n_frames, hmax * wmax, C] tiles (each packed at the
+    start of its row).  Returns the [n_frames, height, width, C] frames on
+    rank 0, None elsewhere."""
+    import torch
+    import torch.distributed as dist
+    rank = dist.get_rank(group)
+    stack = gl = None
+    if rank == 0:
+        stack = torch.empty((plan.world,) + tuple(local.shape), dtype=local.dtype, device=local.device)
+        gl = list(stack.unbind(0))
+    if dist.get_backend(group) == "gloo" and local.is_cuda:
+        host = local.cpu()
+        hl = [torch.empty_like(host) for _ in range(plan.world)] if rank == 0 else None
+        dist.gather(host, hl, dst=0, group=group)
+        if rank == 0:
+            for d, h in zip(gl, hl):
+                d.copy_(h)
+    else:
+        dist.gather(local, gl, dst=0, group=group)
+    if rank != 0:
+        return None
+    if src_index is None:
+        src_index = torch.as_tensor(plan.src, device=local.device)
+    c = local.shape[-1]
+    out = torch.index_select(stack.reshape(-1, c), 0, src_index)
+    return out.reshape(plan.n_frames, plan.height, plan.width, c)
+
+
+# --- rotating row blocks (strong scaling, an option) -------------------------
 #
 # Each frame is cut into N contiguous row pieces, one per rank: rank 0's piece
 # has h0 = root_share x H / N rows and the other N - 1 pieces split the rest

@@ -4,28 +4,41 @@
 Workload (N = 1): BASELINE config 3 — the 50k-triangle synthetic scene at
 1920x1080, 4 bounces, default camera.  One step = one whole
 frame traced on the GPU: every pixel's full path, RGBA8 written to HBM.  The
-render loop keeps D frames in flight (step k on stream k mod D, each stream
-its own hardware queue), as a renderer does to hide each frame's serial tail;
-the timed region still covers exactly K frames, synchronised on both sides.
-With N > 1 ranks (one process per GPU, torch.distributed over RCCL), default
---partition bands: a step is still ONE frame, tiled over the ranks in
-interleaved 16-row bands (rank r traces the bands b with b mod N = r); every
-D steps the D frames traced since the last exchange are gathered to rank 0
-over xGMI (one dist.gather) and assembled there (one index_select), all
-inside the timed region (strong scaling: the work per step is fixed).  The
-collective's and the assembly's streams run at high priority
-(--exchange-priority), so the traces in flight do not starve them of CU slots.
---partition blocks: one contiguous row piece per rank, the pieces' order
-rotated every frame, received by rank 0 straight into the frame (RCCL
-send/recv, no assembly); rank 0's piece sized by --root-share.
---partition frames: a step is N frames of the render loop, each frame's bands
-rotated over the ranks, so every rank traces one frame's worth of pixels per
-step (weak scaling).  Rank 0 checks the assembled frames against a one-GPU
-frame afterwards (config.frames_verified) and times the same frames on its
-GPU alone (speedup_vs_1gpu).
+render loop keeps D launches in flight (launch j on stream j mod D, each
+stream its own hardware queue), as a renderer does to hide each frame's
+serial tail; a launch traces F frames (rt_render_batch_device; F = 1 at
+N = 1).  The timed region covers exactly K frames, synchronised on both
+sides.
 
-value = segments of a step x steps / wall time of the timed steps (max over
-ranks), in millions.  A segment is one executed bounce-loop iteration
+With N > 1 ranks (one process per GPU, torch.distributed over RCCL):
+--partition bands (default): a step is still ONE frame (strong scaling),
+  tiled over the ranks in interleaved band_h-row bands dealt out by a
+  weighted round robin (rank 0 weighted --root-weight: it also receives and
+  assembles every frame; rtamd.dist.band_owners).  A rank traces its bands of
+  F frames per launch, D launches in flight; every G frames the batch is
+  gathered to rank 0 over xGMI (one dist.gather) and assembled there (one
+  index_select), all inside the timed region.  The collective's and the
+  assembly's streams run at high priority (--exchange-priority).
+--partition tiles: the screen tiled gx x gy over the ranks (2 x 2 at N = 4,
+  BASELINE config 4), one tile per rank, gathered and assembled likewise.
+--partition frames: a step is N frames, each frame's bands rotated over the
+  ranks, so every rank traces one frame's worth of pixels per step (weak).
+--gather radiance: the float radiance (the sqrt'd colour before
+  quantisation) is gathered beside the RGBA8 frame.
+Afterwards rank 0 checks the assembled frames (and radiance) against the
+same frames traced on its GPU alone (config.frames_verified) and times those
+(single_gpu, speedup_vs_1gpu); every rank reports its trace and exchange
+device time (per_rank).
+
+--camera-path orbit: every frame has its own camera (the default camera's
+origin orbiting the look-at point, 0.5 degrees per frame, as the app's
+camera moves between frames, VulkanApp.java:726-770); segments are counted
+per camera.  After the timed frames the camera stops and the first frames
+at rest (the learning frame of the heavy-first order among them) are timed
+one by one (camera_stop).
+
+value = segments of the K timed frames / wall time of the timed steps (max
+over ranks), in millions.  A segment is one executed bounce-loop iteration
 (compute_dynamic_ray.comp:179-232); its count per frame is deterministic and is
 taken from a counting pass outside the timed region.
 
@@ -45,16 +58,21 @@ time against 8 TB/s, and "algorithmic" = the contract's algorithmic bytes
 4 B per pixel) over that time against 8 TB/s, which can exceed 1 because
 those bytes are cache hits.  kernel_ms is the mean duration of one launch
 (HIP events on its own stream; what rocprofv3 reports per kernel); with D
-frames in flight launches overlap, and kernel_ms / frame_ms_device is the
+launches in flight they overlap, and kernel_ms / frame_ms_device is the
 average number running at once.
 cpu_baseline: the CPU oracle (oracle/rt_oracle.c, OpenMP) on a bounded row
 sample of the same frame, rank 0 at N = 1 only (the reference has no CPU
 render path: BVHNode.hit throws, BVHNode.java:35-41).
+pcie (N = 1): rt_render_async with 4 frames in flight into pinned host
+frames, every frame read back over PCIe (the rate a host that displays the
+frames sees; never `value`).
 """
 from __future__ import annotations
 
 import argparse
+import ctypes as C
 import json
+import math
 import os
 import sys
 import time
@@ -77,35 +95,64 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-# Frames in flight need one hardware queue per stream to run concurrently; the
-# HIP default (4 queues per process) puts several streams on one queue and
+# Launches in flight need one hardware queue per stream to run concurrently;
+# the HIP default (4 queues per process) puts several streams on one queue and
 # serialises their launches (config 3, a rank's 1/8 share with 8 frames in
 # flight: 0.118 ms per frame on 4 queues, 0.057 on 16; profiles/r02/inflight16).
 # Read by the HIP runtime at initialisation, so set before torch touches the GPU.
-if int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < 16:
-    os.environ["GPU_MAX_HW_QUEUES"] = "16"
+def _queues() -> None:
+    raw = os.environ.get("GPU_MAX_HW_QUEUES", "")
+    try:
+        have = int(raw) if raw.strip() else 4
+    except ValueError:
+        have = 4
+    if have < 16:
+        os.environ["GPU_MAX_HW_QUEUES"] = "16"
+
+
+_queues()
 
 
 def default_inflight(world: int) -> int:
-    """Frames in flight per rank (bands partition), measured best for config 3
-    (tools/share_inflight_bench.py on one MI355X, 16 queues, the default
-    schedule; profiles/r02/inflight16/share4_q16.jsonl): N = 1: 4 (0.338 ms
-    per frame); N = 2: 8 (0.175 ms per half frame); N = 4, 8: 12 (0.092 /
-    0.050 ms per share vs 0.104 / 0.077 at 4).  At most 12: with the main
-    stream, the collective's and the runtime's own, 16 queues stay one per
-    stream."""
-    return 4 if world == 1 else (8 if world == 2 else 12)
+    """Launches in flight per rank.  N = 1: 4 whole frames (0.338 ms per
+    frame vs 0.343 at 6-12, profiles/r02/inflight16/share4_q16.jsonl).  N > 1:
+    4 batched launches (default_batch frames each): a rank's share of one
+    frame is too small a launch to fill the GPU past its own tail (DESIGN.md
+    §6)."""
+    return 4
 
 
-def default_root_share(world: int) -> float:
-    """blocks partition: rank 0's piece in units of H / N rows.  Rank 0 also
-    receives the other N - 1 pieces of every frame into place, which costs it
-    device time the other ranks do not spend; balancing trace + exchange time
-    per frame, rank 0's share is 1 - X (N - 1) / T (X: its exchange time per
-    frame, T: N x a share's trace time).  The one-GPU emulation of rank 0
-    (tools/rank0_exchange_bench.py, profiles/r02/rccl/) puts X at ~0.019 ms
-    per frame at N = 8 and ~0.01 at N = 4 for config 3."""
-    return 1.0 if world <= 2 else (0.9 if world <= 4 else 0.6)
+def default_batch(world: int) -> int:
+    """Frames per launch: 1 at N = 1; at N > 1 about half a frame of work per
+    launch (N / 2 shares, at most 16): a 1/8 share alone runs at 0.050 ms per
+    frame with 12 launches in flight against 0.0438 ms per 1/8 of a frame for
+    half-frame launches (profiles/r02/inflight16/share4_q16.jsonl, N = 2 vs
+    N = 8)."""
+    return 1 if world == 1 else max(1, min(16, world // 2))
+
+
+def default_root_weight(world: int) -> float:
+    """bands: rank 0's weight in the band deal (the others weigh 1).  Rank 0
+    also receives the other ranks' shares of every frame and assembles the
+    frame, device work the other ranks do not do."""
+    return 1.0 if world <= 2 else (0.85 if world <= 4 else 0.7)
+
+
+def camera_path(cfg, kind: str, n: int, first: int = 0):
+    """The cameras of frames first .. first + n - 1."""
+    from rtamd import configs
+    if kind == "static":
+        cam = cfg.camera()
+        return [cam] * n
+    out = []
+    ox, oy, oz = -25.0, 30.0, 140.0                 # VulkanApp.java:132-138
+    rad = math.hypot(ox, oz)
+    a0 = math.atan2(oz, ox)
+    for k in range(first, first + n):
+        a = a0 + math.radians(0.5) * k
+        out.append(configs.Camera((rad * math.cos(a), oy, rad * math.sin(a)), (0.0, 0.0, 0.0), (0.0, 1.0, 0.0),
+                                  20.0, cfg.width / cfg.height))
+    return out
 
 
 def file_sha16(path: str) -> str:
@@ -117,39 +164,35 @@ def file_sha16(path: str) -> str:
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    # 200 frames of config 3 are ~70 ms: with 4-12 frames in flight, 20 steps
-    # would spend a fifth of the timed region filling and draining the pipeline.
+    # 200 frames of config 3 are ~60 ms: with 4 launches in flight, 20 steps
+    # spend a fifth of the timed region filling and draining the pipeline.
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", type=int, default=3, help="BASELINE config index (3 = headline)")
-    ap.add_argument("--band", type=int, default=16, help="band height for N > 1")
-    ap.add_argument("--partition", choices=("bands", "blocks", "frames"), default="bands",
-                    help="N > 1: bands = one frame per step in interleaved --band-row bands, gathered and "
-                         "assembled on rank 0 (strong scaling, default); blocks = one frame per step in N "
-                         "contiguous row pieces laid out in an order rotated every frame, received by rank 0 "
-                         "straight into the frame (strong; emulated slower on the sending ranks, "
-                         "profiles/r02/rccl/README.md); frames = N frames per step, bands rotated over ranks (weak)")
-    ap.add_argument("--inflight", type=int, default=0,
-                    help="frames in flight per rank (bands partition): each step's trace goes on the next of this "
-                         "many streams, so frames overlap each other's serial tails and the gathers "
-                         "(0 = auto, default_inflight(): 4 at N = 1, 8 at N = 2, 12 at N > 2)")
-    ap.add_argument("--drain", type=int, default=0,
-                    help="1: the last frames of a run of steps plan their heavy pixels for the frames still in "
-                         "flight beside them (concurrent_launches min(D, frames left)); 0 (default): every frame "
-                         "for D.  Measured slower at 20 steps (0.329-0.332 vs 0.309-0.312 ms/frame, "
-                         "profiles/r02/drain)")
-    ap.add_argument("--set", default="", help="schedule options name=value,... (rt_set_option) before timing")
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-single", action="store_true", help="N > 1: skip rank 0's one-GPU timing")
+    ap.add_argument("--partition", choices=("bands", "tiles", "frames"), default="bands",
+                    help="N > 1: bands = one frame per step in weighted interleaved bands (strong scaling, "
+                         "default); tiles = one frame per step tiled gx x gy (2 x 2 at N = 4; strong); frames = "
+                         "N frames per step, bands rotated over the ranks (weak)")
+    ap.add_argument("--band", type=int, default=8, help="band height (rows) for N > 1 (8 = one wave-tile row)")
+    ap.add_argument("--root-weight", type=float, default=-1.0,
+                    help="bands: rank 0's weight in the band deal, the others weigh 1 (-1 = default_root_weight)")
+    ap.add_argument("--inflight", type=int, default=0, help="launches in flight per rank (0 = default_inflight)")
+    ap.add_argument("--batch", type=int, default=0, help="frames per launch (whole / bands; 0 = default_batch)")
+    ap.add_argument("--exchange-every", type=int, default=0,
+                    help="N > 1: frames per exchange batch (a multiple of --batch; 0 = launches in flight x batch)")
     ap.add_argument("--ring", type=int, default=2,
-                    help="N > 1 (blocks, bands): batches of frame slots in the ring (>= 2); the traces of a batch "
-                         "wait for the exchange of the batch that used its slots, ring - 1 batches back")
-    ap.add_argument("--root-share", type=float, default=-1.0,
-                    help="blocks: rank 0's piece in units of H / N rows (it also receives every other piece); "
-                         "-1 = default_root_share(N)")
+                    help="N > 1: exchange batches of slots in the ring (>= 2); a batch's slots are retraced only "
+                         "after the exchange ring - 1 batches back")
+    ap.add_argument("--gather", choices=("rgba", "radiance"), default="rgba",
+                    help="N > 1: radiance = gather the float radiance beside the RGBA8 frame")
+    ap.add_argument("--camera-path", choices=("static", "orbit"), default="static")
     ap.add_argument("--exchange-priority", type=int, default=1,
                     help="N > 1: 1 = the collective's stream and the assembly stream at high priority, so the "
                          "exchange is not starved of workgroup slots by the traces in flight")
+    ap.add_argument("--set", default="", help="schedule options name=value,... (rt_set_option) before timing")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-single", action="store_true", help="N > 1: skip rank 0's one-GPU timing")
+    ap.add_argument("--no-pcie", action="store_true", help="N = 1: skip the PCIe-inclusive rt_render_async rate")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU baseline sample time")
     ap.add_argument("--settle-s", type=float, default=0.2,
                     help="untimed frames before the warmup steps: this many seconds of counting-pass time "
@@ -164,6 +207,8 @@ def main() -> None:
     import torch.distributed as dist
     import rtamd
     from rtamd import configs
+    from rtamd._lib import CameraUBO, Stats, check
+    from rtamd.dist import SharePlan, TilePlan, gather_shares, gather_tiles
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -171,19 +216,18 @@ def main() -> None:
     if world != args.gpus:
         log(f"note: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE")
     # BENCH_FORCE_DIST=1 (rehearsal only): the N > 1 code path at any world size,
-    # so one GPU runs the bands partition, its RCCL gather and the rank-0 checks.
+    # so one GPU runs the partition, its RCCL gather and the rank-0 checks.
     dist_on = world > 1 or os.environ.get("BENCH_FORCE_DIST") == "1"
     # BENCH_SHARE_GPU=1 (rehearsal only): ranks share the visible GPUs round-robin.
     dev_index = local_rank % torch.cuda.device_count() if os.environ.get("BENCH_SHARE_GPU") else local_rank
     torch.cuda.set_device(dev_index)
     dev = torch.device("cuda", dev_index)
-    local_rank = dev_index
     backend = None
     if dist_on:
         backend = os.environ.get("BENCH_DIST_BACKEND", "nccl")     # nccl = RCCL over xGMI
         pg_options = None
         if backend == "nccl" and args.exchange_priority:
-            # RCCL's internal stream at high priority: with D traces in flight
+            # RCCL's internal stream at high priority: with traces in flight
             # every CU slot is taken, and a normal-priority collective gets
             # slots only as trace waves end
             from torch.distributed import ProcessGroupNCCL
@@ -194,313 +238,368 @@ def main() -> None:
     cfg = configs.get(args.config)
     t0 = time.time()
     built = cfg.build()
-    cam = cfg.camera()
     log(f"[rank {rank}] built {cfg.name}: {built.triangle_count} flat tris, {built.n_nodes} nodes "
         f"in {time.time() - t0:.2f}s")
     W, H, B = cfg.width, cfg.height, cfg.max_bounces
 
-    renderer = rtamd.Renderer((local_rank,))
+    renderer = rtamd.Renderer((dev_index,))
     renderer.upload_scene(built)
     for kv in filter(None, args.set.split(",")):
         k, v = kv.split("=")
         renderer.set_option(k.strip(), int(v))
     L = rtamd.lib()
-    from rtamd.dist import (BatchPlan, batch_band_offset, block_layout, block_sizes, exchange_blocks, gather_batch,
-                            gather_frames)
+    ctx = renderer._ctx
 
-    # Partition.  bands (default): one frame per step tiled over the ranks in
-    # interleaved band_h-row bands (strong scaling; a frame lasts as long as
-    # its slowest wave).  frames: a step renders N frames of the
-    # render loop (the reference re-renders the current camera every loop
-    # iteration, VulkanEngine.java:240-276), each tiled over all ranks in
-    # rotating bands, so every rank traces one frame's worth of pixels per
-    # step (weak scaling).  At N = 1 both are one whole frame per step.
-    frames_mode = args.partition == "frames" and world > 1
-    blocks_mode = args.partition == "blocks" and dist_on
-    F = world if frames_mode else 1
-    band_h = H if (not dist_on or blocks_mode) else args.band
-    offsets = [batch_band_offset(f, world, rank) if frames_mode else rank for f in range(F)]
-    plan = BatchPlan(H, band_h, world, F) if frames_mode else None
-    rows_f = [L.rt_band_rows(H, band_h, world, off) for off in offsets]
-    max_rows = plan.max_rows if plan else max(L.rt_band_rows(H, band_h, world, r) for r in range(world))
-    # blocks: rank 0's piece is root_share x H / N rows (it also receives the
-    # other pieces of every frame), the other ranks split the rest
-    share = (args.root_share if args.root_share >= 0 else default_root_share(world)) if blocks_mode else 1.0
-    if blocks_mode:
-        max_rows = max(block_sizes(H, world, share))
-    # Frames in flight (bands partition): step k traces on stream k mod D.  A
-    # frame's own time is bounded by its slowest pixel's dependent chain
-    # (DESIGN.md §7), so the render loop keeps D frames on the device at once
-    # (each stream its own hardware queue, GPU_MAX_HW_QUEUES above) and a
-    # rank's 1/N share of a frame fills the GPU only with several in flight
-    # (tools/share_inflight_bench.py, profiles/r02/inflight16/).
-    D = 1 if frames_mode else (args.inflight if args.inflight > 0 else default_inflight(world))
-    # The heavy-pixel bar counts every launch of similar work on the device at
-    # once (option concurrent_launches): a frame batch's F launches, or the D
-    # frames in flight.
-    renderer.set_option("concurrent_launches", F * D)
-    # Exchange (N > 1, blocks / bands): every G = D steps the G frames traced
-    # since the last exchange go to rank 0 in one RCCL group (blocks: sends /
-    # receives straight into rank 0's frames; bands: one gather and one
-    # index_select, dist.gather_frames), so the host cost of the exchange is
-    # paid once per G frames.  R x G frame slots: batches are traced while
-    # earlier ones are exchanged; a slot is retraced only after the exchange
-    # that used it.  N = 1: one slot per stream.  frames partition: one gather
-    # per step of F frames, D + 1 buffers.
-    G = D if (dist_on and not frames_mode) else 1
-    # R batches of slots in the ring: a batch's slots are retraced only after
-    # the exchange R - 1 batches back has finished.  The exchange kernels get
-    # workgroup slots only as trace waves end, so a deep ring keeps a late
-    # exchange from stalling the traces.
-    R = max(2, args.ring)
-    if frames_mode:
-        n_slots = D + 1
-    elif dist_on:
-        n_slots = R * G
+    # ---- partition -------------------------------------------------------
+    mode = args.partition if dist_on else "whole"
+    if mode == "frames" and args.camera_path != "static":
+        raise SystemExit("--partition frames takes the static camera")
+    D = args.inflight if args.inflight > 0 else default_inflight(world)
+    F = (args.batch if args.batch > 0 else default_batch(world)) if mode in ("whole", "bands") else 1
+    F = min(F, 16)
+    step_frames = world if mode == "frames" else 1           # frames per step (weak scaling: N)
+    if mode == "bands":
+        G = args.exchange_every if args.exchange_every > 0 else D * F
+        G = max(F, (G + F - 1) // F * F)                       # whole launches per exchange batch
+    elif mode == "frames":
+        G = world                                              # one exchange per step
+    elif mode == "tiles":
+        G = args.exchange_every if args.exchange_every > 0 else D
     else:
-        n_slots = D
-    d_bufs = [torch.empty((F, max_rows, W, 4), dtype=torch.uint8, device=dev) for _ in range(n_slots)] \
-        if frames_mode else None
-    slots = torch.empty((n_slots, max_rows, W, 4), dtype=torch.uint8, device=dev) if not frames_mode else None
-    # blocks: rank 0 traces its block of frame k in place in fring[k mod n_slots]
-    # and receives the other blocks there
-    fring = torch.empty((n_slots, H, W, 4), dtype=torch.uint8, device=dev) if (blocks_mode and rank == 0) else None
-    gathered = [None] * (n_slots if frames_mode else R)   # event: the last exchange that used a buffer / batch slot
-    # One stream per launch in flight (launches and their events on the same
-    # queue); the gathers run on main_stream.
-    streams = [torch.cuda.Stream(dev) for _ in range(min(F * D, 12))]
-    hi = -1 if (dist_on and args.exchange_priority) else 0   # the assembly (index_select) at high priority
-    main_stream = torch.cuda.Stream(dev, priority=hi) if (dist_on or len(streams) > 1) else streams[0]
+        G = D * F                                              # N = 1: the slot ring
+    R = max(2, args.ring)
+    rad_on = dist_on and args.gather == "radiance"
+    band_h = args.band
+    plan = tplan = None
+    src_index = None
+    my_bands = None
+    if mode in ("bands", "frames"):
+        rw = 1.0 if mode == "frames" else (args.root_weight if args.root_weight >= 0 else default_root_weight(world))
+        plan = SharePlan(H, band_h, world, G, rw, rotate=(mode == "frames"))
+        src_index = torch.as_tensor(plan.src, device=dev)
+        my_bands = [np.ascontiguousarray(plan.frame_bands(rank, f)) for f in range(G)]
+        rgba_slots = torch.empty((R, plan.per_rank, W, 4), dtype=torch.uint8, device=dev)
+        rad_slots = torch.empty((R, plan.per_rank, W, 3), dtype=torch.float32, device=dev) if rad_on else None
+        px_per_frame = plan.counts[rank] * W
+    elif mode == "tiles":
+        tplan = TilePlan(W, H, world, G)
+        src_index = torch.as_tensor(tplan.src, device=dev)
+        rect = tplan.rects[rank]
+        rgba_slots = torch.empty((R, G, tplan.tile_px, 4), dtype=torch.uint8, device=dev)
+        rad_slots = torch.empty((R, G, tplan.tile_px, 3), dtype=torch.float32, device=dev) if rad_on else None
+        px_per_frame = rect[2] * rect[3]
+    else:
+        rgba_slots = torch.empty((D, F * H, W, 4), dtype=torch.uint8, device=dev)
+        rad_slots = None
+        px_per_frame = W * H
+    streams = [torch.cuda.Stream(dev) for _ in range(D)]
+    hi = -1 if (dist_on and args.exchange_priority) else 0    # the assembly (index_select) at high priority
+    main_stream = torch.cuda.Stream(dev, priority=hi)
     torch.cuda.set_stream(main_stream)
-    src_index = torch.as_tensor(plan.src, device=dev) if (plan and dist_on) else None
+    # The heavy-pixel bar counts the launches of similar work on the device at
+    # once: the D launches in flight.
+    renderer.set_option("concurrent_launches", D)
 
-    import ctypes as C
-    from rtamd._lib import Stats, check
+    cam_cache = {}
 
-    def trace(f, stats: bool = False, ev=None, out=None, si=0, rect=None):
-        s = streams[si % len(streams)]
-        st = Stats()
-        if ev is not None:          # recorded after the stream's wait for the gather: the trace only
-            ev[0].record(s)
-        if rect is not None:        # blocks: frame rows [y0, y1), packed into out
-            if rect[1] > rect[0]:
-                check(L.rt_render_tile_device(renderer._ctx, C.byref(cam.ubo), W, H, B, 0, rect[0], W,
-                                              rect[1] - rect[0], out.data_ptr(), None, s.cuda_stream,
-                                              C.byref(st) if stats else None))
+    def cam_of(k):
+        if args.camera_path == "static":
+            k = 0
+        c = cam_cache.get(k)
+        if c is None:
+            c = cam_cache[k] = camera_path(cfg, args.camera_path, 1, k)[0]
+        return c
+
+    def i32p(a):
+        return a.ctypes.data_as(C.POINTER(C.c_int32)) if a is not None else None
+
+    def trace(k0, n, s, rgba_ptr, rad_ptr, stats=False):
+        """Frames k0 .. k0 + n - 1 (one exchange batch) in one launch on stream s."""
+        st = Stats() if stats else None
+        stp = C.byref(st) if stats else None
+        if mode == "tiles":
+            x0, y0, w, h = rect
+            check(L.rt_render_tile_device(ctx, C.byref(cam_of(k0).ubo), W, H, B, x0, y0, w, h, rgba_ptr, rad_ptr,
+                                          s.cuda_stream, stp))
         else:
-            check(L.rt_render_bands_device(renderer._ctx, C.byref(cam.ubo), W, H, B, band_h, world, offsets[f],
-                                           out.data_ptr(), None, s.cuda_stream, C.byref(st) if stats else None))
-        if ev is not None:
-            ev[1].record(s)
+            cams = (CameraUBO * n)(*[cam_of(k).ubo for k in range(k0, k0 + n)])
+            bl = my_bands[k0 % G] if my_bands is not None else None
+            check(L.rt_render_batch_device(ctx, cams, n, W, H, B, band_h if bl is not None else 0, i32p(bl),
+                                           len(bl) if bl is not None else 0, rgba_ptr, rad_ptr, s.cuda_stream, stp))
         return st.as_dict() if stats else None
 
-    k_step = [0]
-    last = [None]
+    def out_ptrs(k0, j):
+        """Where launch j (frames k0 ...) writes: its slot of the ring."""
+        if mode == "whole":
+            return rgba_slots[j % D].data_ptr(), None
+        h = (k0 // G) % R
+        if mode == "tiles":
+            f = k0 % G
+            return (rgba_slots[h, f].data_ptr(), rad_slots[h, f].data_ptr() if rad_on else None)
+        off = plan.off[rank][k0 % G]
+        return (rgba_slots[h, off].data_ptr() if off < plan.per_rank else rgba_slots[h].data_ptr(),
+                (rad_slots[h, off].data_ptr() if off < plan.per_rank else rad_slots[h].data_ptr()) if rad_on else None)
 
-    def flush():
-        """Bands, N > 1: gather the frames of the current batch traced so far
-        (a whole batch from step(), the rest at the end of a phase)."""
-        k = k_step[0]
+    st = {"k": 0, "j": 0}
+    gathered = [None] * R
+    last = {"rgba": None, "rad": None, "frames": []}
+    ex_evs = []            # (start, end) events of the timed region's exchanges
+
+    def flush(timed=False):
+        """Exchange the frames of the current batch traced so far (N > 1)."""
+        k = st["k"]
         n = k % G if k % G else (G if k else 0)
-        if n == 0:
-            return None
-        half = ((k - 1) // G) % R
+        if not dist_on or n == 0:
+            return
+        h = ((k - 1) // G) % R
         for s in streams:
             main_stream.wait_stream(s)
-        if blocks_mode:         # RCCL sends / receives straight into rank 0's frames
-            base = half * G
-            exchange_blocks(fring[base: base + n] if rank == 0 else None, slots[base: base + n],
-                            list(range(k - n, k)), H, share)
-            out = fring[base: base + n] if rank == 0 else None
+        e0 = e1 = None
+        if timed:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(main_stream)
+        if mode == "tiles":
+            out = gather_tiles(rgba_slots[h], tplan, src_index=src_index)
+            rad = gather_tiles(rad_slots[h], tplan, src_index=src_index) if rad_on else None
+            if out is not None:
+                out, rad = out[:n], (rad[:n] if rad is not None else None)
         else:
-            out = gather_frames(slots[half * G: half * G + n], H, band_h)   # RCCL gather + rank-0 assembly
-        gathered[half] = torch.cuda.Event()
-        gathered[half].record(main_stream)
-        k_step[0] = ((k + G - 1) // G) * G       # the next phase starts a fresh batch
-        last[0] = out
-        return out
+            out = gather_shares(rgba_slots[h], plan, src_index=src_index, n_frames=n)
+            rad = gather_shares(rad_slots[h], plan, src_index=src_index, n_frames=n) if rad_on else None
+        if timed:
+            e1.record(main_stream)
+            ex_evs.append((e0, e1))
+        ev = torch.cuda.Event()
+        ev.record(main_stream)
+        gathered[h] = ev
+        last["rgba"], last["rad"] = out, rad
+        last["frames"] = list(range(k - n, k))
+        st["k"] = ((k + G - 1) // G) * G            # the next phase starts a fresh batch
 
-    def step(evs=None):
-        k = k_step[0]
-        k_step[0] += 1
-        if frames_mode:
-            b = k % n_slots
-            mine = [streams[(k * F + f) % len(streams)] for f in range(F)]
-            for s in mine:                             # the gather that last read this buffer is done
-                if gathered[b] is not None:
-                    s.wait_event(gathered[b])
-            for f in range(F):
-                trace(f, ev=evs[f] if evs is not None else None, out=d_bufs[b][f], si=k * F + f)
-            for s in mine:
-                if s is not main_stream:
-                    main_stream.wait_stream(s)
-            last[0] = gather_batch(d_bufs[b], plan, src_index=src_index)
-            gathered[b] = torch.cuda.Event()
-            gathered[b].record(main_stream)
-            return
-        s = streams[k % len(streams)]
-        if blocks_mode:
-            half = (k // G) % R
-            if k % G == 0 and gathered[half] is not None:
-                for t in streams:                      # the exchange that last used this half is done
-                    t.wait_event(gathered[half])
-            y0, y1 = block_layout(H, world, k, share)[rank]
-            out = fring[k % n_slots, y0:y1] if rank == 0 else slots[k % n_slots, : y1 - y0]
-            trace(0, ev=evs[0] if evs is not None else None, out=out, si=k, rect=(y0, y1))
-            if k % G == G - 1:
-                flush()
-        elif dist_on:
-            half = (k // G) % R
-            if k % G == 0 and gathered[half] is not None:
-                for t in streams:                      # the gather that last read this half is done
-                    t.wait_event(gathered[half])
-            trace(0, ev=evs[0] if evs is not None else None, out=slots[k % n_slots, :rows_f[0]], si=k)
-            if k % G == G - 1:
-                flush()
-        else:
-            trace(0, ev=evs[0] if evs is not None else None, out=slots[k % n_slots, :rows_f[0]], si=k)
+    def phase(n_frames, evs=None):
+        """n_frames frames: launches of up to F frames, never across an exchange batch."""
+        end = st["k"] + n_frames
+        while st["k"] < end:
+            k0 = st["k"]
+            n = min(F, end - k0, G - k0 % G)
+            j = st["j"]
+            s = streams[j % D]
+            if dist_on and k0 % G == 0 and gathered[(k0 // G) % R] is not None:
+                for t in streams:                      # the exchange that last read these slots is done
+                    t.wait_event(gathered[(k0 // G) % R])
+            rp, dp = out_ptrs(k0, j)
+            if evs is not None:
+                e = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                e[0].record(s)
+            trace(k0, n, s, rp, dp)
+            if evs is not None:
+                e[1].record(s)
+                evs.append((e, n))
+            st["k"] = k0 + n
+            st["j"] = j + 1
+            if dist_on and st["k"] % G == 0:
+                flush(timed=evs is not None)
+        if dist_on:
+            flush(timed=evs is not None)
 
-    # Counting pass (untimed): this rank's work, then the job totals.
-    count_out = torch.empty((max_rows, W, 4), dtype=torch.uint8, device=dev)
-    per = [trace(f, stats=True, out=count_out, rect=block_layout(H, world, 0, share)[rank] if blocks_mode else None)
-           for f in range(F)]
-    torch.cuda.synchronize(dev)
-    counts = torch.tensor([sum(p[k] for p in per) for k in ("pixels", "segments", "node_visits", "tri_tests",
-                                                             "mat_reads")], dtype=torch.float64, device=dev)
-    local = counts.clone()
-    if dist_on:
-        dist.all_reduce(counts)
-    pixels, segments, node_visits, tri_tests, mat_reads = [float(x) for x in counts.tolist()]
-    # per launch (blocks: the mean over the ranks' blocks, which differ in cost)
-    per_launch = (counts / world) if blocks_mode else local
-    l_pix, l_seg, l_nodes, l_tris, l_mats = [float(x) / F for x in per_launch.tolist()]
-    log(f"[rank {rank}] step: {F} frame(s), {segments:.0f} segments ({segments / pixels:.3f}/px), "
-        f"{node_visits / segments:.2f} node visits/seg, {tri_tests / segments:.3f} tri tests/seg; "
-        f"{D} frame(s) in flight, exchange every {G} step(s)")
+    # ---- frame indices of the phases (fixed up front, so the counting pass
+    # counts exactly the timed frames' cameras): a phase of n frames from
+    # frame k ends at k + n, rounded up to a whole exchange batch at N > 1
+    def after(k, n):
+        k += n
+        return ((k + G - 1) // G) * G if dist_on else k
 
-    # Drain (option --drain, off by default: measured slower): a launch's heavy-pixel bar counts
-    # the launches that will run beside it, and at the end of a run of frames
-    # fewer do: step j of n has min(D, n - j) frames in flight from its launch
-    # on, so the last frames split their slowest pixels into one-pixel waves
-    # as a lone frame does, instead of leaving the run's end to one frame's
-    # serial tail.  Pixels and results do not change (DESIGN.md §4).
-    conc_now = [F * D]
+    # ---- counting pass (untimed): the timed frames' work ------------------
+    K = args.steps * step_frames                       # timed frames
+    W_fr = args.warmup * step_frames
+    count_rgba = torch.empty((max(rgba_slots[0].numel() // 4, 1), 4), dtype=torch.uint8, device=dev)
 
-    def set_conc(c):
-        if c != conc_now[0]:
-            renderer.set_option("concurrent_launches", c)
-            conc_now[0] = c
+    def count_frames(ks):
+        """This rank's work in frames ks (counting launches, one frame each)."""
+        tot = {k2: 0.0 for k2 in ("pixels", "segments", "node_visits", "tri_tests", "mat_reads")}
+        ms = []
+        for k in ks:
+            d = trace(k, 1, main_stream, count_rgba.data_ptr(), None, stats=True)
+            for k2 in tot:
+                tot[k2] += d[k2]
+            ms.append(d["ms"])
+        return tot, ms
 
-    def phase(n, evs=None):
-        for j in range(n):
-            if args.drain:
-                set_conc(F * min(D, n - j))
-            step(evs[j] if evs is not None else None)
-        set_conc(F * D)
-        if dist_on and not frames_mode:
-            flush()
-
-    # Settle (untimed): 5-100 frames, about settle_s / (the counting pass's
-    # device time; a counting launch runs ~4x a plain one), so the timed steps
-    # see the steady state of a running render loop (the first frames after
-    # start-up run 3-4% slower: profiles/r02/warmup), then the W warmup steps
-    # of the contract.
-    # The count is fixed up front (from the counting pass's device time) and
-    # agreed over the ranks, so every rank runs the same collectives.
-    est_ms = max(0.05, float(per[0].get("ms", 1.0)))
-    # at least 2D: the drain's launch keys (concurrency 1..D) learn their
-    # orders here, not in the timed region
+    # settle: 5-100 launches, about settle_s / (the counting launch's device
+    # time; a counting launch runs ~4x a plain one), so the timed steps see the
+    # steady state of a running render loop (the first frames after start-up
+    # run 3-4% slower: profiles/r02/warmup), then the W warmup steps.  Agreed
+    # over the ranks, so every rank runs the same collectives.
+    step0, ms0 = count_frames(range(step_frames))          # one step (frames: this rank's N positions)
+    est_ms = max(0.05, float(sum(ms0)) / F)
     n_settle = torch.tensor([max(5, 2 * D, min(100, int(args.settle_s * 1e3 / est_ms)))], dtype=torch.int64,
                             device=dev)
     if dist_on:
         dist.all_reduce(n_settle, op=dist.ReduceOp.MIN)
-    phase(int(n_settle.item()))
+    n_settle = int(n_settle.item()) * F * step_frames
+    k_t0 = after(after(0, n_settle), W_fr)
+    if mode == "frames" or args.camera_path == "static":
+        one = step0 if mode == "frames" else count_frames([k_t0])[0]
+        loc = {k2: v * args.steps for k2, v in one.items()}
+    else:
+        loc, _ = count_frames(range(k_t0, k_t0 + K))
     torch.cuda.synchronize(dev)
-    phase(args.warmup)
+    counts = torch.tensor([loc[k2] for k2 in ("pixels", "segments", "node_visits", "tri_tests", "mat_reads")],
+                          dtype=torch.float64, device=dev)
+    local = counts.clone()
+    if dist_on:
+        dist.all_reduce(counts)
+    pixels, segments, node_visits, tri_tests, mat_reads = [float(x) for x in counts.tolist()]
+    log(f"[rank {rank}] {mode}: {K} timed frames, {segments / K:.0f} segments per frame ({segments / pixels:.3f}/px), "
+        f"{node_visits / segments:.2f} node visits/seg; {D} launches in flight x {F} frames, exchange every "
+        f"{G if dist_on else '-'} frames")
+
+    # ---- settle, warmup, timed ---------------------------------------------
+    phase(n_settle)
     torch.cuda.synchronize(dev)
+    phase(W_fr)
+    torch.cuda.synchronize(dev)
+    assert st["k"] == k_t0, (st["k"], k_t0)
     if dist_on:
         dist.barrier()
     torch.cuda.synchronize(dev)
-
-    # HIP events: around every launch on its own stream (the launch's device
-    # duration; with D in flight the launches overlap), and around the whole
-    # timed region on main_stream after joining every stream (the device time
-    # per frame of the running loop).
-    evs = [[(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(F)]
-           for _ in range(args.steps)]
+    evs = []
     reg = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
     t_start = time.perf_counter()
     reg[0].record(main_stream)
     for s in streams:
-        if s is not main_stream:
-            s.wait_stream(main_stream)
-    phase(args.steps, evs)
+        s.wait_stream(main_stream)
+    phase(K, evs)
     for s in streams:
-        if s is not main_stream:
-            main_stream.wait_stream(s)
+        main_stream.wait_stream(s)
     reg[1].record(main_stream)
     torch.cuda.synchronize(dev)
     if dist_on:
         dist.barrier()
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t_start
-    launch_ms = float(np.mean([a.elapsed_time(b) for e in evs for a, b in e]))
+    n_launch = len(evs)
+    launch_ms = float(np.mean([a.elapsed_time(b) for (a, b), _ in evs]))
     region_ms = reg[0].elapsed_time(reg[1])
-    frame_ms = region_ms / (args.steps * F)            # device time per launch of the running loop
-    out = last[0]
+    frame_ms = region_ms / n_launch                    # device time per launch of the running loop
+    ivs = sorted((reg[0].elapsed_time(a), reg[0].elapsed_time(b)) for (a, b), _ in evs)
+    busy, cs, ce = 0.0, None, None
+    for a0, b0 in ivs:                                 # union of the launches' intervals
+        if ce is None or a0 > ce:
+            busy += (ce - cs) if ce is not None else 0.0
+            cs, ce = a0, b0
+        else:
+            ce = max(ce, b0)
+    busy += (ce - cs) if ce is not None else 0.0
+    exchange_ms = float(sum(a.elapsed_time(b) for a, b in ex_evs))
+    mine = torch.tensor([rank, px_per_frame, launch_ms, region_ms / K, busy / K, exchange_ms / K],
+                        dtype=torch.float64, device=dev)
+    if dist_on:
+        allr = [torch.empty_like(mine) for _ in range(world)]
+        dist.all_gather(allr, mine)
+    else:
+        allr = [mine]
+    per_rank = [{"rank": int(x[0]), "pixels_per_frame": int(x[1]), "kernel_ms": round(float(x[2]), 4),
+                 "device_ms_per_frame": round(float(x[3]), 4), "trace_busy_ms_per_frame": round(float(x[4]), 4),
+                 "exchange_ms_per_frame": round(float(x[5]), 4)} for x in (t.tolist() for t in allr)]
 
     heavy_used = renderer.get_option("heavy_tiles_used")   # of the last timed launch
+    heavy_px_used = renderer.get_option("heavy_pixels_used")
     verified = None
     single = None
-    if dist_on and rank == 0:
-        # the assembled frames equal the 1-GPU frame
+    if dist_on and rank == 0 and last["rgba"] is not None:
+        # the assembled frames (and radiance) equal the frames traced whole on one GPU
+        ok = True
         full = torch.empty((H, W, 4), dtype=torch.uint8, device=dev)
-        check(L.rt_render_bands_device(renderer._ctx, C.byref(cam.ubo), W, H, B, H, 1, 0, full.data_ptr(), None,
-                                       main_stream.cuda_stream, None))
-        torch.cuda.synchronize(dev)
-        frames = out if out.dim() == 4 else out[None]
-        verified = bool(all(torch.equal(frames[f], full) for f in range(frames.shape[0])))
+        fullr = torch.empty((H, W, 3), dtype=torch.float32, device=dev) if rad_on else None
+        for i, k in enumerate(last["frames"]):
+            c = cam_of(k)
+            check(L.rt_render_tile_device(ctx, C.byref(c.ubo), W, H, B, 0, 0, W, H, full.data_ptr(),
+                                          fullr.data_ptr() if rad_on else None, main_stream.cuda_stream, None))
+            torch.cuda.synchronize(dev)
+            ok = ok and torch.equal(last["rgba"][i], full)
+            if rad_on:
+                ok = ok and torch.equal(last["rad"][i].view(torch.int32), fullr.view(torch.int32))
+        verified = bool(ok)
         if not args.no_single:
             # The same frames on this GPU alone: whole frames, one per launch,
-            # with the one-GPU default frames in flight, for the speedup of
+            # with the one-GPU default launches in flight, for the speedup of
             # this partition.
             D1 = default_inflight(1)
             renderer.set_option("concurrent_launches", D1)
-            fulls = [full] + [torch.empty_like(full) for _ in range(D1 - 1)]
-            sstreams = streams[:D1] + [torch.cuda.Stream(dev) for _ in range(D1 - len(streams))]
+            fulls = [torch.empty((H, W, 4), dtype=torch.uint8, device=dev) for _ in range(D1)]
 
-            def one(j):
-                check(L.rt_render_bands_device(renderer._ctx, C.byref(cam.ubo), W, H, B, H, 1, 0,
-                                               fulls[j % D1].data_ptr(), None, sstreams[j % D1].cuda_stream, None))
-            one(0)                                    # learns the whole-frame order
+            def one(j, k):
+                check(L.rt_render_tile_device(ctx, C.byref(cam_of(k).ubo), W, H, B, 0, 0, W, H,
+                                              fulls[j % D1].data_ptr(), None, streams[j % D].cuda_stream, None))
+            one(0, k_t0)                              # learns the whole-frame order
             torch.cuda.synchronize(dev)
             for j in range(4 * D1):
-                one(j)
+                one(j, k_t0 + j % K)
             torch.cuda.synchronize(dev)
             t1 = time.perf_counter()
-            for j in range(args.steps * F):
-                one(j)
+            for j in range(K):
+                one(j, k_t0 + j)
             torch.cuda.synchronize(dev)
             single = time.perf_counter() - t1
+            renderer.set_option("concurrent_launches", D)
+
+    # the camera stops (orbit): the first frames at rest, timed one by one (the
+    # first repeat of a camera learns its own heavy-first order)
+    stop = None
+    if args.camera_path != "static" and mode != "frames":
+        k_last = k_t0 + K - 1
+        ms = []
+        for i in range(8):
+            torch.cuda.synchronize(dev)
+            t1 = time.perf_counter()
+            rp, dp = out_ptrs(k_last, 0) if mode != "whole" else (rgba_slots[0].data_ptr(), None)
+            trace(k_last, 1, streams[0], rp, dp)
+            torch.cuda.synchronize(dev)
+            ms.append(round((time.perf_counter() - t1) * 1e3, 4))
+        stop = {"ms_per_frame": ms,
+                "what": "the camera of the last timed frame traced 8 more times one at a time (launch to "
+                        "completion, host clock): the first repeat of a camera runs the learning launch "
+                        "(diagnostic build + stream synchronisation), later ones the learned order"}
 
     t = torch.tensor([elapsed, launch_ms, frame_ms], dtype=torch.float64, device=dev)
     if dist_on:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed, launch_ms_max, frame_ms_max = float(t[0]), float(t[1]), float(t[2])
 
-    value = segments * args.steps / elapsed / 1e6
+    value = segments / elapsed / 1e6
+    # this rank's work per launch of the timed region
+    l_seg, l_nodes, l_tris, l_mats, l_pix = [float(x) / n_launch for x in
+                                            (local[1], local[2], local[3], local[4], local[0])]
     alg_bytes = 32.0 * l_nodes + 36.0 * l_tris + 16.0 * l_mats + 4.0 * l_pix
     ref_layout_bytes = 48.0 * l_nodes + 48.0 * l_tris + 16.0 * l_mats + 4.0 * l_pix
     n_cu = torch.cuda.get_device_properties(dev).multi_processor_count
-    pmc = load_pmc(args.pmc_json, cfg.name) if (world == 1 and F == 1) else None
+    pmc = load_pmc(args.pmc_json, cfg.name) if (mode == "whole" and F == 1) else None
     roof = roofline(pmc, alg_bytes, ref_layout_bytes, l_seg, frame_ms, n_cu)
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(built, cam, W, H, B, segments, args.cpu_seconds)
+        cpu = cpu_baseline(built, cam_of(k_t0), W, H, B, segments / K, args.cpu_seconds)
+    pcie = None
+    if rank == 0 and mode == "whole" and args.camera_path == "static" and not args.no_pcie:
+        pcie = pcie_rate(renderer, cam_of(0), W, H, B, segments / K)
 
     if rank == 0:
         gather_kind = "RCCL" if backend == "nccl" else (backend or "none")
         shared = " (ranks share one GPU: rehearsal)" if os.environ.get("BENCH_SHARE_GPU") else ""
+        if mode == "whole":
+            part = f"one whole frame per step, {D} launches in flight, {F} frame(s) per launch"
+        elif mode == "bands":
+            part = (f"one frame per step in {band_h}-row bands dealt to {world} ranks by a weighted round robin "
+                    f"(rank 0 weight {plan.root_weight}, rows per rank {plan.counts}), {D} launches in flight x "
+                    f"{F} frames per launch, {gather_kind} gather of every {G} frames + rank-0 assembly{shared}")
+        elif mode == "tiles":
+            part = (f"one frame per step tiled {tplan.gx} x {tplan.gy} over {world} ranks (tiles "
+                    f"{tplan.rects}), {D} frames in flight, {gather_kind} gather of every {G} frames + rank-0 "
+                    f"assembly{shared}")
+        else:
+            part = (f"{world} frames per step, {band_h}-row bands rotated over {world} ranks, {gather_kind} gather "
+                    f"+ rank-0 assembly{shared}")
         out = {
             "metric": BASELINE["metric"],
             "value": round(value, 2),
@@ -510,79 +609,104 @@ def main() -> None:
             "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 4),
             "higher_is_better": True,
-            "scaling": "weak" if frames_mode else "strong",
+            "scaling": "weak" if mode == "frames" else "strong",
             "vs_baseline": None,
             "dtype": "f32",
             "data": f"{'reference asset' if args.config == 6 else 'synthetic'} "
-                    f"({cfg.note}; default camera)",
+                    f"({cfg.note}; {'default camera' if args.camera_path == 'static' else 'orbiting camera'})",
             "config": {
                 "workload": cfg.name,
                 "width": W, "height": H, "max_bounces": B,
                 "triangles_flat": built.triangle_count, "bvh_nodes": built.n_nodes,
-                "segments_per_frame": int(segments / F),
+                "segments_per_frame": int(round(segments / K)),
                 "node_visits_per_segment": round(node_visits / segments, 3),
                 "tri_tests_per_segment": round(tri_tests / segments, 4),
-                "partition": f"one whole frame per step, {D} frames in flight" if not dist_on else
-                             (f"{F} frames per step, {band_h}-row bands rotated over {world} ranks "
-                              f"(rank r traces bands (r+f) mod {world} of frame f), {gather_kind} gather + rank-0 "
-                              f"assembly{shared}"
-                              if frames_mode else
-                              f"one frame per step in {world} contiguous row pieces (rows per rank "
-                              f"{block_sizes(H, world, share)}, root_share {share}) laid out in an order rotated "
-                              f"every frame, {D} frames in flight per rank, {gather_kind} sends / receives of every "
-                              f"{G} frames straight into rank 0's frames{shared}"
-                              if blocks_mode else
-                              f"one frame per step, interleaved {band_h}-row bands over {world} ranks, "
-                              f"{D} frames in flight per rank, {gather_kind} gather of every {G} frames + rank-0 "
-                              f"assembly{shared}"),
-                "frames_per_step": F,
-                "frames_in_flight": D,
+                "camera_path": args.camera_path,
+                "partition": part,
+                "frames_per_step": step_frames,
+                "frames_per_launch": F,
+                "launches_in_flight": D,
+                "exchange_every_frames": G if dist_on else None,
+                "band_h": band_h if mode in ("bands", "frames") else None,
+                "root_weight": plan.root_weight if plan is not None else None,
+                "gather": ("rgba8 + float radiance" if rad_on else "rgba8") if dist_on else None,
                 "frames_verified": verified,
-                "parallelism": f"tile{world}",
-                "schedule": {**{k: renderer.get_option(k) for k in ("kernel", "walk", "wave_tile", "coop_lanes",
+                "parallelism": f"{mode}{world}",
+                "schedule": {**{k: renderer.get_option(k) for k in ("walk", "wave_tile", "coop_lanes",
                                                                       "heavy_first", "heavy_tiles", "heavy_factor",
                                                                       "heavy_stream", "heavy_pixels",
-                                                                      "heavy_pixel_factor", "heavy_cap", "graph")},
+                                                                      "heavy_pixel_factor", "heavy_cap", "graph",
+                                                                      "reuse_order", "hw_queues")},
                              "concurrent_launches": renderer.get_option("concurrent_launches"),
-                             "drain": args.drain,
                              "heavy_tiles_used": heavy_used,
-                             "heavy_pixels_used": renderer.get_option("heavy_pixels_used")},
-                "launches_per_step": F * (2 if heavy_used > 0 and renderer.get_option("heavy_stream") != 2 else 1),
+                             "heavy_pixels_used": heavy_px_used},
             },
             "roofline": {
                 **roof,
-                "kernel": ("trace_simple" if renderer.get_option("kernel") == 0 else "trace_*") + (
-                    f" (one launch per frame: the {renderer.get_option('heavy_pixels_used')} heaviest pixels one per "
-                    f"wave first, then every {8 << renderer.get_option('wave_tile')}x"
-                    f"{8 >> renderer.get_option('wave_tile')} tile without them)"
-                    if renderer.get_option("heavy_pixels_used") > 0
-                    else f" (one launch per frame: the {heavy_used} heaviest tiles one pixel per wave first)"
-                    if heavy_used > 0 and renderer.get_option("heavy_stream") == 2
-                    else f" (frame = the {heavy_used} heaviest tiles' one-pixel-wave launch concurrent with the "
-                         f"other tiles' launch; kernel_ms spans both)" if heavy_used > 0 else ""),
+                "kernel": "trace_simple" + (
+                    f" (one launch per {F} frame(s): the {heavy_px_used} heaviest pixels one per wave first, then "
+                    f"every {8 << renderer.get_option('wave_tile')}x{8 >> renderer.get_option('wave_tile')} tile "
+                    f"without them)" if heavy_px_used > 0 else
+                    f" (one launch per {F} frame(s): the {heavy_used} heaviest tiles one pixel per wave first)"
+                    if heavy_used > 0 else f" (one launch per {F} frame(s), tiles in the learned order)"),
                 "kernel_ms": round(launch_ms, 4),
                 "kernel_ms_max_over_ranks": round(launch_ms_max, 4) if dist_on else None,
                 "frame_ms_device": round(frame_ms, 4),
                 "frame_ms_device_max_over_ranks": round(frame_ms_max, 4) if dist_on else None,
                 "launches_in_flight_avg": round(launch_ms / frame_ms, 2),
                 "events": "kernel_ms: each launch's own stream, around every launch (after its wait for the "
-                          "gather); frame_ms_device: main stream around the timed region after joining every "
+                          "exchange); frame_ms_device: main stream around the timed region after joining every "
                           "launch stream, / launches",
             },
-            "primary_mrays_s": round(pixels * args.steps / elapsed / 1e6, 2),
+            "per_rank": per_rank,
+            "primary_mrays_s": round(pixels / elapsed / 1e6, 2),
             "cpu_baseline": cpu,
+            "pcie": pcie,
+            "camera_stop": stop,
             "bench_sha16": file_sha16(os.path.abspath(__file__)),
         }
         if single is not None:
-            sv = segments * args.steps / single / 1e6
-            out["single_gpu"] = {"value": round(sv, 2), "ms_per_frame": round(single / (args.steps * F) * 1e3, 4),
+            sv = segments / single / 1e6
+            out["single_gpu"] = {"value": round(sv, 2), "ms_per_frame": round(single / K * 1e3, 4),
                                  "what": f"the same frames traced whole on rank 0's GPU alone, one per launch, "
-                                         f"{D} in flight"}
+                                         f"{default_inflight(1)} in flight"}
             out["speedup_vs_1gpu"] = round(value / sv, 3)
         print(json.dumps(out), flush=True)
     renderer.close()
     if dist_on:
         dist.destroy_process_group()
+
+
+def pcie_rate(renderer, cam, W, H, B, frame_segments, n=100):
+    """rt_render_async: 4 frames in flight into pinned host frames, every frame
+    read back over PCIe (tools/pipeline_bench.py's async mode)."""
+    from rtamd.engine import PinnedFrame
+    S = 4
+    renderer.set_option("async_slots", S)
+    frames = [PinnedFrame(H, W) for _ in range(S)]
+    try:
+        pend = []
+        for j in range(2 * S):                       # learns / warms up
+            pend.append(renderer.render_async(cam, W, H, B, frames[j % S]))
+            if len(pend) == S:
+                renderer.wait(pend.pop(0))
+        while pend:
+            renderer.wait(pend.pop(0))
+        t0 = time.perf_counter()
+        for j in range(n):
+            pend.append(renderer.render_async(cam, W, H, B, frames[j % S]))
+            if len(pend) == S:
+                renderer.wait(pend.pop(0))
+        while pend:
+            renderer.wait(pend.pop(0))
+        dt = time.perf_counter() - t0
+    finally:
+        for f in frames:
+            f.close()
+    return {"value": round(frame_segments * n / dt / 1e6, 2), "unit": "Mrays/s",
+            "ms_per_frame": round(dt / n * 1e3, 4), "frames": n,
+            "what": f"rt_render_async, {S} frames in flight, every frame's RGBA8 read back into pinned host memory "
+                    f"(readback overlapped with later traces); the rate a host displaying the frames sees"}
 
 
 def load_pmc(path, config_name):
@@ -695,6 +819,7 @@ def cpu_baseline(built, cam, W, H, B, frame_segments, target_s):
                 "checker) with OpenMP over rows: the reference has no CPU render path (BVHNode.hit throws "
                 "UnsupportedOperationException, BVHNode.java:35-41), so no 'reference' CPU baseline exists",
     }
+
 
 
 if __name__ == "__main__":

@@ -142,6 +142,33 @@ int rt_render_bands_device(rt_ctx* ctx, const rt_camera_ubo* cam,
 /* Row count of such a band set (-1 for bad arguments).  Pure host code. */
 int rt_band_rows(int height, int band_h, int band_stride, int band_off);
 
+/* Batched frames over listed row bands, for the multi-GPU frame partitions
+ *  and a render loop's frames in flight: ONE launch traces,
+ * for each of the n_frames cameras cams[f] (1..16 frames), the frame rows of
+ * the band_h-row bands listed in `bands` (n_bands strictly increasing band
+ * indices below ceil(height / band_h); a rank's share of a weighted band
+ * partition), or the whole frame when bands is NULL.  Frame f's rows are
+ * packed in increasing y at rows [f * R, (f + 1) * R) of the DEVICE buffers
+ * d_out_rgba (R * width * 4 B per frame, may be null) and d_out_radiance
+ * (R * width * 3 floats per frame, may be null), R =
+ * rt_band_list_rows(height, band_h, bands, n_bands).  Every pixel is traced
+ * exactly as one frame per launch traces it (seed = its global pixel index,
+ * compute_dynamic_ray.comp:164); one launch of several frames replaces
+ * several small launches, whose per-launch tails and queue slots a rank's
+ * share of a frame cannot fill.  The band list is copied to
+ * the device once per distinct list.  The accumulation extension takes one
+ * frame per launch.  Same stream / stats semantics as rt_render_tile_device
+ * (stats: the totals over the frames). */
+int rt_render_batch_device(rt_ctx* ctx, const rt_camera_ubo* cams, int n_frames,
+                           int width, int height, int max_bounces,
+                           int band_h, const int32_t* bands, int n_bands,
+                           void* d_out_rgba, void* d_out_radiance,
+                           void* stream, rt_stats* stats);
+
+/* Row count of a band list (-1 if the list is not strictly increasing or
+ * reaches past the frame).  Pure host code. */
+int rt_band_list_rows(int height, int band_h, const int32_t* bands, int n_bands);
+
 /* Pipelined frames (overlap the readback with the next
  * frame; the reference waits on a fence after every frame,
  * VulkanEngine.java:410-429).

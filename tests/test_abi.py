@@ -124,3 +124,39 @@ def test_unbalanced_bvh_validates():
         assert nn == 2 * n - 1
         if depth is not None:
             assert md == depth
+
+
+def test_band_list_rows_and_weighted_deal():
+    """rt_band_list_rows (the C ABI's row count of a band list) against the
+    Python deal (rtamd.dist.band_owners): every band has exactly one owner,
+    the counts follow the weights, weight 1 is the plain interleave."""
+    import ctypes as C
+    from rtamd import lib
+    from rtamd.dist import SharePlan, band_owners, list_rows
+    L = lib()
+
+    def rows(h, bh, bands):
+        arr = (C.c_int32 * max(1, len(bands)))(*bands)
+        return L.rt_band_list_rows(h, bh, arr, len(bands))
+    for h, bh, world, rw in [(1080, 8, 8, 0.7), (1080, 16, 8, 0.6), (2160, 8, 4, 0.85), (53, 4, 3, 0.5),
+                             (720, 8, 2, 1.0), (7, 8, 4, 1.0)]:
+        own = band_owners(h, bh, world, rw)
+        assert len(own) == (h + bh - 1) // bh
+        total = 0
+        for r in range(world):
+            b = np.flatnonzero(own == r).astype(np.int32)
+            n = rows(h, bh, list(b))
+            assert n == len(list_rows(h, bh, b))
+            total += n
+        assert total == h
+        if rw == 1.0:
+            assert (own == np.arange(len(own)) % world).all()
+        else:
+            c = np.bincount(own, minlength=world)
+            assert c[0] <= c[1:].min() and abs(c[0] / c[1:].mean() - rw) < 0.2
+        plan = SharePlan(h, bh, world, 2, rw)
+        assert sorted(plan.src.tolist()) == sorted(set(plan.src.tolist()))     # every row from one place
+    assert rows(10, 4, [1, 0]) == -1          # not increasing
+    assert rows(10, 4, [3]) == -1             # past the frame
+    assert rows(10, 4, []) == 0
+    assert rows(10, 4, [2]) == 2              # the partial last band

@@ -672,3 +672,92 @@ def test_spheres_upload_validation(renderer):
     with pytest.raises(RtError, match="INVALID_ARG"):
         renderer.upload_spheres(np.zeros((65537, 8), np.float32) + np.float32(1.0))
     renderer.upload_spheres(np.zeros((0, 8), np.float32))
+
+
+def _batch_device(renderer, cams, w, h, b, band_h=0, bands=None, radiance=True, stats=True):
+    import ctypes as C
+    import torch
+    from rtamd import lib, CameraUBO
+    from rtamd._lib import Stats, check
+    L = lib()
+    n = len(cams)
+    arr = (C.c_int32 * max(1, len(bands)))(*bands) if bands is not None else None
+    rows = L.rt_band_list_rows(h, band_h, arr, len(bands)) if bands is not None else h
+    d_rgba = torch.empty((n, rows, w, 4), dtype=torch.uint8, device="cuda:0")
+    d_rad = torch.empty((n, rows, w, 3), dtype=torch.float32, device="cuda:0") if radiance else None
+    ubos = (CameraUBO * n)(*[c.ubo for c in cams])
+    s = Stats()
+    check(L.rt_render_batch_device(renderer._ctx, ubos, n, w, h, b, band_h, arr, len(bands) if bands is not None else 0,
+                                   d_rgba.data_ptr(), d_rad.data_ptr() if radiance else None,
+                                   torch.cuda.current_stream().cuda_stream, C.byref(s) if stats else None))
+    torch.cuda.synchronize()
+    return d_rgba.cpu().numpy(), (d_rad.cpu().numpy() if radiance else None), s.as_dict()
+
+
+@pytest.mark.parametrize("cfg_k,band_h,world,rw,rank", [(3, 8, 8, 0.7, 0), (3, 8, 8, 0.7, 5), (2, 16, 4, 1.0, 3),
+                                                       (6, 8, 4, 0.85, 1)])
+def test_batch_band_list_bit_exact(renderer, cfg_k, band_h, world, rw, rank):
+    """rt_render_batch_device: one launch traces a rank's weighted band share
+    (rtamd.dist.band_owners) of 3 frames with 3 different cameras; the
+    learning launch, a counting launch and a plain launch in the learned
+    order each give every frame's rows of the oracle's frame, bit for bit,
+    and the counts of those rows."""
+    from rtamd import configs
+    from rtamd.dist import band_list, list_rows
+    cfg = configs.get(cfg_k)
+    built = cfg.build()
+    renderer.upload_scene(built)
+    W, H, B = cfg.width, cfg.height, cfg.max_bounces
+    cams = [configs.Camera((-25.0 + 3 * f, 30.0, 140.0 - 4 * f), (0.0, 0.0, 0.0), (0.0, 1.0, 0.0), 20.0, W / H)
+            for f in range(3)]
+    bands = [int(x) for x in band_list(H, band_h, world, rank, rw)]
+    rows = list_rows(H, band_h, bands)
+    refs = []
+    tot = {k: 0 for k in COUNTERS}
+    for c in cams:
+        rgba, rad, cnt = _oracle(built, c.ubo_bytes(), W, H, B)
+        refs.append((rgba[rows], rad[rows]))
+        # the rows' own counts: the oracle on each band as a tile
+        for bnd in bands:
+            y0 = bnd * band_h
+            _, _, cb = _oracle(built, c.ubo_bytes(), W, H, B, tile=(0, y0, W, min(band_h, H - y0)), radiance=False)
+            for k in COUNTERS:
+                tot[k] += cb[k]
+    try:
+        renderer.set_option("concurrent_launches", 4)
+        for stats in (False, True, False):
+            rgba, rad, st = _batch_device(renderer, cams, W, H, B, band_h, bands, stats=stats)
+            for f in range(3):
+                _assert_same(rgba[f], rad[f], None, refs[f][0], refs[f][1], None)
+            if stats:
+                for k in COUNTERS:
+                    assert st[k] == tot[k], (k, st[k], tot[k])
+                assert st["pixels"] == 3 * len(rows) * W
+    finally:
+        for k, v in DEFAULT_OPTS.items():
+            renderer.set_option(k, v)
+
+
+def test_batch_whole_frames_and_errors(renderer):
+    """rt_render_batch_device with no band list: whole frames of a batch of 4
+    (two cameras, each twice) equal the oracle's; bad lists and batch sizes
+    are rejected with RT_ERR_INVALID_ARG."""
+    import ctypes as C
+    from rtamd import RtError, configs, lib
+    cfg = configs.config2()
+    built = cfg.build()
+    renderer.upload_scene(built)
+    w, h, b = 320, 180, 4
+    c0 = configs.Camera.default(w, h)
+    c1 = configs.Camera((10.0, 20.0, 90.0), (0.0, 0.0, 0.0), (0.0, 1.0, 0.0), 25.0, w / h)
+    cams = [c0, c1, c1, c0]
+    for _ in range(2):
+        rgba, rad, st = _batch_device(renderer, cams, w, h, b)
+        for f, c in enumerate(cams):
+            ref = _oracle(built, c.ubo_bytes(), w, h, b)
+            _assert_same(rgba[f], rad[f], None, *ref)
+    with pytest.raises(RtError, match="INVALID_ARG"):
+        _batch_device(renderer, [c0], w, h, b, 16, [3, 2])
+    with pytest.raises(RtError, match="INVALID_ARG"):
+        _batch_device(renderer, [c0] * 17, w, h, b)
+    assert lib().rt_band_list_rows(h, 16, (C.c_int32 * 1)(11), 1) == h - 11 * 16     # the partial last band
