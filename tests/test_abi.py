@@ -160,3 +160,21 @@ def test_band_list_rows_and_weighted_deal():
     assert rows(10, 4, [3]) == -1             # past the frame
     assert rows(10, 4, []) == 0
     assert rows(10, 4, [2]) == 2              # the partial last band
+
+
+def test_jni_shim_matches_java_and_header():
+    """jni/: every native method HipNative.java declares has its
+    Java_dev_demir_vulkan_engine_HipNative_* function in HipNative.c and back,
+    and every rt_* call in the shim is declared in include/rtamd.h (the shim
+    cannot be compiled here: no JDK / jni.h)."""
+    import re
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    c_src = open(os.path.join(root, "jni", "HipNative.c")).read()
+    j_src = open(os.path.join(root, "jni", "dev", "demir", "vulkan", "engine", "HipNative.java")).read()
+    hdr = open(os.path.join(root, "include", "rtamd.h")).read()
+    natives = set(re.findall(r"static native \w+ (\w+)\(", j_src))
+    jni_fns = set(re.findall(r"Java_dev_demir_vulkan_engine_HipNative_(\w+)\(", c_src))
+    assert natives and natives == jni_fns
+    calls = set(re.findall(r"\b(rt_\w+)\(", c_src))
+    declared = set(re.findall(r"\b(rt_\w+)\(", hdr))
+    assert calls <= declared, calls - declared

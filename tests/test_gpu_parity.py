@@ -756,8 +756,14 @@ def test_batch_whole_frames_and_errors(renderer):
         for f, c in enumerate(cams):
             ref = _oracle(built, c.ubo_bytes(), w, h, b)
             _assert_same(rgba[f], rad[f], None, *ref)
-    with pytest.raises(RtError, match="INVALID_ARG"):
-        _batch_device(renderer, [c0], w, h, b, 16, [3, 2])
-    with pytest.raises(RtError, match="INVALID_ARG"):
-        _batch_device(renderer, [c0] * 17, w, h, b)
+    import torch
+    from rtamd import CameraUBO
+    from rtamd._lib import check
+    buf = torch.empty((17 * h * w * 4,), dtype=torch.uint8, device="cuda:0")
+    for n, bands in ((1, [3, 2]), (1, [12]), (17, None), (0, None)):
+        ubos = (CameraUBO * max(1, n))(*([c0.ubo] * max(1, n)))
+        arr = (C.c_int32 * len(bands))(*bands) if bands else None
+        with pytest.raises(RtError, match="INVALID_ARG"):
+            check(lib().rt_render_batch_device(renderer._ctx, ubos, n, w, h, b, 16 if bands else 0, arr,
+                                               len(bands) if bands else 0, buf.data_ptr(), None, None, None))
     assert lib().rt_band_list_rows(h, 16, (C.c_int32 * 1)(11), 1) == h - 11 * 16     # the partial last band

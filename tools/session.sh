@@ -38,7 +38,7 @@ run() {  # run NAME SECONDS CMD...
 prof() {  # prof CONFIG STEPS
   local c=$1 k=$2 d="$OUT/prof$1"
   run "prof$c" 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$d" -o run -- \
-      python3 bench.py --config "$c" --steps "$k" --warmup 5 --no-cpu-baseline > "$OUT/prof$c.json" 2> "$OUT/prof$c.err"
+      python3 bench.py --config "$c" --steps "$k" --warmup 5 --no-cpu-baseline --no-pcie > "$OUT/prof$c.json" 2> "$OUT/prof$c.err"
   local tr
   tr=$(find "$d" -name "run_kernel_trace.csv" | head -n 1)
   python3 tools/rocprof_union.py "$tr" --steps "$k" --bench "$OUT/prof$c.json" --out "$OUT/union_cfg$c.json" \
