@@ -767,3 +767,48 @@ def test_batch_whole_frames_and_errors(renderer):
             check(lib().rt_render_batch_device(renderer._ctx, ubos, n, w, h, b, 16 if bands else 0, arr,
                                                len(bands) if bands else 0, buf.data_ptr(), None, None, None))
     assert lib().rt_band_list_rows(h, 16, (C.c_int32 * 1)(11), 1) == h - 11 * 16     # the partial last band
+
+
+@pytest.mark.parametrize("slots,toggle", [(4, False), (3, True)])
+def test_render_async_accumulation_and_copy_toggle(slots, toggle):
+    """rt_render_async with the accumulation extension (per-device running
+    sums that every frame reads and writes): with `slots` frames in flight the
+    frames still reach the sums in frame_count order (the runtime serialises
+    the slots' traces then), so every frame equals the oracle's accumulated
+    frame.  toggle: copy_streams flips between 1 and 2 from frame to frame and
+    every wait still returns a complete frame (copied2 is recorded for every
+    frame)."""
+    if not has_gpu():
+        pytest.skip("no GPU")
+    import rtamd
+    from test_oracle_kat import _ext_scene
+    from rtamd import configs
+    from rtamd.engine import PinnedFrame
+    built = _ext_scene()
+    w, h, b = 150, 97, 4
+    n = 2 * slots + 1
+    r = rtamd.Renderer((0,))
+    frames = [PinnedFrame(h, w) for _ in range(n)]
+    try:
+        r.upload_scene(built)
+        r.set_option("extensions", 7)
+        r.set_option("async_slots", slots)
+        cam = configs.Camera.default(w, h)
+        acc = np.zeros((h, w, 3), np.float32)
+        refs = []
+        for f in range(n):
+            cam.ubo.frame_count = f
+            refs.append(_oracle(built, cam.ubo_bytes(), w, h, b, ext=7, accum=acc)[0])
+        tickets = []
+        for f in range(n):
+            if toggle:
+                r.set_option("copy_streams", 2 if f % 2 else 1)
+            cam.ubo.frame_count = f
+            tickets.append(r.render_async(cam, w, h, b, frames[f]))
+        for f in reversed(range(n)):          # the newest first: each wait must cover its own frame
+            r.wait(tickets[f])
+            assert np.array_equal(frames[f].array, refs[f]), f"frame {f}"
+    finally:
+        r.close()
+        for fr in frames:
+            fr.close()

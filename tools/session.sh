@@ -16,7 +16,7 @@
 #   pmc5      the same for config 5
 #   cfgs      bench.py on configs 4, 5, 6
 #   share     tools/share_inflight_bench.py (one rank's share, frames in flight)
-#   rank0     tools/rank0_exchange_bench.py (rank 0 of N with its exchange)
+#   emu       tools/rank_emulator.py (one rank of N with its exchange; $EMU_ARGS)
 #   pipeline  tools/pipeline_bench.py (PCIe-inclusive rates)
 #   cmd       the command in $CMD (600 s)
 set -u
@@ -71,7 +71,7 @@ for s in "$@"; do
                     > "$OUT/bench_cfg$1.json" 2> "$OUT/bench_cfg$1.err"
               done ;;
     share)    run share 600 python tools/share_inflight_bench.py ${SHARE_ARGS:-} > "$OUT/share.jsonl" 2> "$OUT/share.err" ;;
-    rank0)    run rank0 600 python tools/rank0_exchange_bench.py ${RANK0_ARGS:-} > "$OUT/rank0.jsonl" 2> "$OUT/rank0.err" ;;
+    emu)      run emu 900 python tools/rank_emulator.py ${EMU_ARGS:-} > "$OUT/emu.jsonl" 2> "$OUT/emu.err" ;;
     pipeline) run pipeline 300 python tools/pipeline_bench.py ${PIPE_ARGS:-} > "$OUT/pipeline.jsonl" 2> "$OUT/pipeline.err" ;;
     cmd)      run cmd 600 bash -c "$CMD" > "$OUT/cmd.log" 2>&1 ;;
     *)        status "unknown step $s" ;;
