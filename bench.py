@@ -217,7 +217,14 @@ def main() -> None:
         log(f"note: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE")
     # BENCH_FORCE_DIST=1 (rehearsal only): the N > 1 code path at any world size,
     # so one GPU runs the partition, its RCCL gather and the rank-0 checks.
-    dist_on = world > 1 or os.environ.get("BENCH_FORCE_DIST") == "1"
+    # BENCH_EMULATE=N:r (analysis only, run under torchrun at world size 1):
+    # rank r of an N-rank run on this one GPU, its share and its exchange
+    # volume (rank 0: the whole batch into a stack + the assembly; rank r > 0:
+    # its own rows), the collective an RCCL gather at world size 1 (a device
+    # copy).  Frames are not checked; value is the job's rate if every rank
+    # ran at this rank's pace.
+    emu = os.environ.get("BENCH_EMULATE", "")
+    dist_on = world > 1 or os.environ.get("BENCH_FORCE_DIST") == "1" or bool(emu)
     # BENCH_SHARE_GPU=1 (rehearsal only): ranks share the visible GPUs round-robin.
     dev_index = local_rank % torch.cuda.device_count() if os.environ.get("BENCH_SHARE_GPU") else local_rank
     torch.cuda.set_device(dev_index)
@@ -235,6 +242,8 @@ def main() -> None:
             pg_options.is_high_priority_stream = True
         dist.init_process_group(backend, device_id=dev if backend == "nccl" else None, pg_options=pg_options)
 
+    if emu:
+        world, rank = (int(x) for x in emu.split(":"))
     cfg = configs.get(args.config)
     t0 = time.time()
     built = cfg.build()
@@ -292,6 +301,11 @@ def main() -> None:
         rgba_slots = torch.empty((D, F * H, W, 4), dtype=torch.uint8, device=dev)
         rad_slots = None
         px_per_frame = W * H
+    if emu:
+        if mode != "bands":
+            raise SystemExit("BENCH_EMULATE emulates --partition bands")
+        emu_buf = torch.zeros((world * plan.per_rank, W, 4) if rank == 0 else (1,), dtype=torch.uint8, device=dev)
+        emu_land = torch.empty_like(emu_buf if rank == 0 else rgba_slots[0])
     streams = [torch.cuda.Stream(dev) for _ in range(D)]
     hi = -1 if (dist_on and args.exchange_priority) else 0    # the assembly (index_select) at high priority
     main_stream = torch.cuda.Stream(dev, priority=hi)
@@ -358,7 +372,16 @@ def main() -> None:
         if timed:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(main_stream)
-        if mode == "tiles":
+        if emu and mode == "bands":
+            # the exchange volume of rank `rank` of `world`, through a world-size-1 gather
+            if rank == 0:
+                dist.gather(emu_buf, [emu_land])
+                out = torch.index_select(emu_land.reshape(world * plan.per_rank, -1), 0, src_index[: n * H])
+            else:
+                dist.gather(rgba_slots[h], [emu_land])
+                out = None
+            rad = None
+        elif mode == "tiles":
             out = gather_tiles(rgba_slots[h], tplan, src_index=src_index)
             rad = gather_tiles(rad_slots[h], tplan, src_index=src_index) if rad_on else None
             if out is not None:
@@ -447,7 +470,19 @@ def main() -> None:
     counts = torch.tensor([loc[k2] for k2 in ("pixels", "segments", "node_visits", "tri_tests", "mat_reads")],
                           dtype=torch.float64, device=dev)
     local = counts.clone()
-    if dist_on:
+    if emu:
+        # the job's work: whole frames of the timed frames' cameras
+        tot = {k2: 0.0 for k2 in ("pixels", "segments", "node_visits", "tri_tests", "mat_reads")}
+        whole = torch.empty((H, W, 4), dtype=torch.uint8, device=dev)
+        for k in ([k_t0] if args.camera_path == "static" else range(k_t0, k_t0 + K)):
+            sw = Stats()
+            check(L.rt_render_tile_device(ctx, C.byref(cam_of(k).ubo), W, H, B, 0, 0, W, H, whole.data_ptr(), None,
+                                          main_stream.cuda_stream, C.byref(sw)))
+            for k2 in tot:
+                tot[k2] += getattr(sw, k2) * (K if args.camera_path == "static" else 1)
+        counts = torch.tensor([tot[k2] for k2 in ("pixels", "segments", "node_visits", "tri_tests", "mat_reads")],
+                              dtype=torch.float64, device=dev)
+    elif dist_on:
         dist.all_reduce(counts)
     pixels, segments, node_visits, tri_tests, mat_reads = [float(x) for x in counts.tolist()]
     log(f"[rank {rank}] {mode}: {K} timed frames, {segments / K:.0f} segments per frame ({segments / pixels:.3f}/px), "
@@ -494,7 +529,7 @@ def main() -> None:
     exchange_ms = float(sum(a.elapsed_time(b) for a, b in ex_evs))
     mine = torch.tensor([rank, px_per_frame, launch_ms, region_ms / K, busy / K, exchange_ms / K],
                         dtype=torch.float64, device=dev)
-    if dist_on:
+    if dist_on and not emu:
         allr = [torch.empty_like(mine) for _ in range(world)]
         dist.all_gather(allr, mine)
     else:
@@ -507,7 +542,7 @@ def main() -> None:
     heavy_px_used = renderer.get_option("heavy_pixels_used")
     verified = None
     single = None
-    if dist_on and rank == 0 and last["rgba"] is not None:
+    if dist_on and not emu and rank == 0 and last["rgba"] is not None:
         # the assembled frames (and radiance) equal the frames traced whole on one GPU
         ok = True
         full = torch.empty((H, W, 4), dtype=torch.uint8, device=dev)
@@ -563,7 +598,7 @@ def main() -> None:
                         "(diagnostic build + stream synchronisation), later ones the learned order"}
 
     t = torch.tensor([elapsed, launch_ms, frame_ms], dtype=torch.float64, device=dev)
-    if dist_on:
+    if dist_on and not emu:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed, launch_ms_max, frame_ms_max = float(t[0]), float(t[1]), float(t[2])
 
@@ -584,7 +619,7 @@ def main() -> None:
     if rank == 0 and mode == "whole" and args.camera_path == "static" and not args.no_pcie:
         pcie = pcie_rate(renderer, cam_of(0), W, H, B, segments / K)
 
-    if rank == 0:
+    if rank == 0 or emu:
         gather_kind = "RCCL" if backend == "nccl" else (backend or "none")
         shared = " (ranks share one GPU: rehearsal)" if os.environ.get("BENCH_SHARE_GPU") else ""
         if mode == "whole":
@@ -665,6 +700,11 @@ def main() -> None:
             "camera_stop": stop,
             "bench_sha16": file_sha16(os.path.abspath(__file__)),
         }
+        if emu:
+            out["emulated"] = {"world": world, "rank": rank,
+                               "what": "EMULATION on one GPU (BENCH_EMULATE): this rank's share and exchange volume "
+                                       "only; value = the job's rate if every rank ran at this rank's pace; not a "
+                                       "measurement of N GPUs"}
         if single is not None:
             sv = segments / single / 1e6
             out["single_gpu"] = {"value": round(sv, 2), "ms_per_frame": round(single / K * 1e3, 4),
