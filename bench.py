@@ -10,25 +10,27 @@ serial tail; a launch traces F frames (rt_render_batch_device; F = 1 at
 N = 1).  The timed region covers exactly K frames, synchronised on both
 sides.
 
-With N > 1 ranks (one process per GPU, torch.distributed over RCCL):
---partition bands (default): a step is still ONE frame (strong scaling),
-  tiled over the ranks in interleaved band_h-row bands dealt out by a
+With N > 1 ranks (one process per GPU, torch.distributed over RCCL), every
+frame is tiled over ALL ranks and gathered to rank 0 over xGMI (one
+dist.gather per exchange batch) and assembled there (one index_select), all
+inside the timed region; the collective's and the assembly's streams run at
+high priority (--exchange-priority).
+--scaling weak (default): a step is N frames of the render loop (every rank
+  traces one frame's worth of pixels per step, the per-GPU work of N = 1),
+  exchanged every step.  --scaling strong: a step is ONE frame.
+--partition bands (default): interleaved band_h-row bands dealt out by a
   weighted round robin (rank 0 weighted --root-weight: it also receives and
   assembles every frame; rtamd.dist.band_owners).  A rank traces its bands of
-  F frames per launch, D launches in flight; every G frames the batch is
-  gathered to rank 0 over xGMI (one dist.gather) and assembled there (one
-  index_select), all inside the timed region.  The collective's and the
-  assembly's streams run at high priority (--exchange-priority).
+  F frames per launch (rt_render_batch_device; weak: F = N, the step), D
+  launches in flight.
 --partition tiles: the screen tiled gx x gy over the ranks (2 x 2 at N = 4,
   BASELINE config 4), one tile per rank, gathered and assembled likewise.
---partition frames: a step is N frames, each frame's bands rotated over the
-  ranks, so every rank traces one frame's worth of pixels per step (weak).
 --gather radiance: the float radiance (the sqrt'd colour before
   quantisation) is gathered beside the RGBA8 frame.
-Afterwards rank 0 checks the assembled frames (and radiance) against the
-same frames traced on its GPU alone (config.frames_verified) and times those
-(single_gpu, speedup_vs_1gpu); every rank reports its trace and exchange
-device time (per_rank).
+Afterwards rank 0 checks the last assembled frames (and radiance) against
+the same frames traced on its GPU alone (config.frames_verified) and times
+those (single_gpu, speedup_vs_1gpu); every rank reports its trace and
+exchange device time (per_rank).
 
 --camera-path orbit: every frame has its own camera (the default camera's
 origin orbiting the look-at point, 0.5 degrees per frame, as the app's
@@ -122,13 +124,17 @@ def default_inflight(world: int) -> int:
     return 4
 
 
-def default_batch(world: int) -> int:
-    """Frames per launch: 1 at N = 1; at N > 1 about half a frame of work per
-    launch (N / 2 shares, at most 16): a 1/8 share alone runs at 0.050 ms per
-    frame with 12 launches in flight against 0.0438 ms per 1/8 of a frame for
-    half-frame launches (profiles/r02/inflight16/share4_q16.jsonl, N = 2 vs
-    N = 8)."""
-    return 1 if world == 1 else max(1, min(16, world // 2))
+def default_batch(world: int, weak: bool = False) -> int:
+    """Frames per launch.  N = 1: 1.  N > 1, weak scaling: N (a launch is a
+    step, this rank's share of the step's N frames: one frame of work, the
+    shape of an N = 1 launch).  N > 1, strong scaling: N / 2 (about half a
+    frame of work per launch): a rank's 1/8 share of one frame is too small
+    a launch to run past its own tail (rank emulation at N = 8, 200 steps:
+    profiles/r03/evidence_r3c/emu.jsonl, 3.9x with 1 frame per launch against
+    6.3-7.7x with 4).  At most 16."""
+    if world == 1:
+        return 1
+    return max(1, min(16, world if weak else world // 2))
 
 
 def default_root_weight(world: int) -> float:
@@ -169,10 +175,13 @@ def main() -> None:
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", type=int, default=3, help="BASELINE config index (3 = headline)")
-    ap.add_argument("--partition", choices=("bands", "tiles", "frames"), default="bands",
-                    help="N > 1: bands = one frame per step in weighted interleaved bands (strong scaling, "
-                         "default); tiles = one frame per step tiled gx x gy (2 x 2 at N = 4; strong); frames = "
-                         "N frames per step, bands rotated over the ranks (weak)")
+    ap.add_argument("--partition", choices=("bands", "tiles"), default="bands",
+                    help="N > 1: how a frame is tiled over the ranks: bands = weighted interleaved row bands "
+                         "(default); tiles = gx x gy rectangles (2 x 2 at N = 4)")
+    ap.add_argument("--scaling", choices=("weak", "strong"), default="weak",
+                    help="N > 1: weak = a step is N frames of the render loop, each tiled over all ranks and "
+                         "gathered (every rank traces one frame's worth per step; default); strong = a step is "
+                         "one frame tiled over all ranks")
     ap.add_argument("--band", type=int, default=8, help="band height (rows) for N > 1 (8 = one wave-tile row)")
     ap.add_argument("--root-weight", type=float, default=-1.0,
                     help="bands: rank 0's weight in the band deal, the others weigh 1 (-1 = default_root_weight)")
@@ -261,30 +270,30 @@ def main() -> None:
 
     # ---- partition -------------------------------------------------------
     mode = args.partition if dist_on else "whole"
-    if mode == "frames" and args.camera_path != "static":
-        raise SystemExit("--partition frames takes the static camera")
+    weak = dist_on and args.scaling == "weak"
+    step_frames = world if weak else 1                         # frames per step (weak scaling: N)
     D = args.inflight if args.inflight > 0 else default_inflight(world)
-    F = (args.batch if args.batch > 0 else default_batch(world)) if mode in ("whole", "bands") else 1
+    F = (args.batch if args.batch > 0 else default_batch(world, weak)) if mode in ("whole", "bands") else 1
     F = min(F, 16)
-    step_frames = world if mode == "frames" else 1           # frames per step (weak scaling: N)
     if mode == "bands":
-        G = args.exchange_every if args.exchange_every > 0 else D * F
+        # weak: one exchange per launch (a step's frames); strong: per D launches
+        G = args.exchange_every if args.exchange_every > 0 else (F if weak else D * F)
         G = max(F, (G + F - 1) // F * F)                       # whole launches per exchange batch
-    elif mode == "frames":
-        G = world                                              # one exchange per step
     elif mode == "tiles":
         G = args.exchange_every if args.exchange_every > 0 else D
     else:
         G = D * F                                              # N = 1: the slot ring
-    R = max(2, args.ring)
+    # ring of exchange batches: enough for the D launches in flight plus the
+    # batch being exchanged
+    R = max(2, args.ring, -(-D * F // G) + 1)
     rad_on = dist_on and args.gather == "radiance"
     band_h = args.band
     plan = tplan = None
     src_index = None
     my_bands = None
-    if mode in ("bands", "frames"):
-        rw = 1.0 if mode == "frames" else (args.root_weight if args.root_weight >= 0 else default_root_weight(world))
-        plan = SharePlan(H, band_h, world, G, rw, rotate=(mode == "frames"))
+    if mode == "bands":
+        rw = args.root_weight if args.root_weight >= 0 else default_root_weight(world)
+        plan = SharePlan(H, band_h, world, G, rw)
         src_index = torch.as_tensor(plan.src, device=dev)
         my_bands = [np.ascontiguousarray(plan.frame_bands(rank, f)) for f in range(G)]
         rgba_slots = torch.empty((R, plan.per_rank, W, 4), dtype=torch.uint8, device=dev)
@@ -453,17 +462,17 @@ def main() -> None:
     # steady state of a running render loop (the first frames after start-up
     # run 3-4% slower: profiles/r02/warmup), then the W warmup steps.  Agreed
     # over the ranks, so every rank runs the same collectives.
-    step0, ms0 = count_frames(range(step_frames))          # one step (frames: this rank's N positions)
-    est_ms = max(0.05, float(sum(ms0)) / F)
+    _, ms0 = count_frames([0])
+    est_ms = max(0.05, float(ms0[0]) * F)                  # a launch's counting time
     n_settle = torch.tensor([max(5, 2 * D, min(100, int(args.settle_s * 1e3 / est_ms)))], dtype=torch.int64,
                             device=dev)
     if dist_on:
         dist.all_reduce(n_settle, op=dist.ReduceOp.MIN)
-    n_settle = int(n_settle.item()) * F * step_frames
+    n_settle = int(n_settle.item()) * F
     k_t0 = after(after(0, n_settle), W_fr)
-    if mode == "frames" or args.camera_path == "static":
-        one = step0 if mode == "frames" else count_frames([k_t0])[0]
-        loc = {k2: v * args.steps for k2, v in one.items()}
+    if args.camera_path == "static":
+        one = count_frames([k_t0])[0]
+        loc = {k2: v * K for k2, v in one.items()}
     else:
         loc, _ = count_frames(range(k_t0, k_t0 + K))
     torch.cuda.synchronize(dev)
@@ -582,7 +591,7 @@ def main() -> None:
     # the camera stops (orbit): the first frames at rest, timed one by one (the
     # first repeat of a camera learns its own heavy-first order)
     stop = None
-    if args.camera_path != "static" and mode != "frames":
+    if args.camera_path != "static":
         k_last = k_t0 + K - 1
         ms = []
         for i in range(8):
@@ -632,9 +641,6 @@ def main() -> None:
             part = (f"one frame per step tiled {tplan.gx} x {tplan.gy} over {world} ranks (tiles "
                     f"{tplan.rects}), {D} frames in flight, {gather_kind} gather of every {G} frames + rank-0 "
                     f"assembly{shared}")
-        else:
-            part = (f"{world} frames per step, {band_h}-row bands rotated over {world} ranks, {gather_kind} gather "
-                    f"+ rank-0 assembly{shared}")
         out = {
             "metric": BASELINE["metric"],
             "value": round(value, 2),
@@ -644,7 +650,7 @@ def main() -> None:
             "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 4),
             "higher_is_better": True,
-            "scaling": "weak" if mode == "frames" else "strong",
+            "scaling": "weak" if weak else "strong",
             "vs_baseline": None,
             "dtype": "f32",
             "data": f"{'reference asset' if args.config == 6 else 'synthetic'} "
@@ -662,7 +668,7 @@ def main() -> None:
                 "frames_per_launch": F,
                 "launches_in_flight": D,
                 "exchange_every_frames": G if dist_on else None,
-                "band_h": band_h if mode in ("bands", "frames") else None,
+                "band_h": band_h if mode == "bands" else None,
                 "root_weight": plan.root_weight if plan is not None else None,
                 "gather": ("rgba8 + float radiance" if rad_on else "rgba8") if dist_on else None,
                 "frames_verified": verified,
