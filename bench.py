@@ -383,7 +383,10 @@ def main() -> None:
             e0.record(main_stream)
         if emu and mode == "bands":
             # the exchange volume of rank `rank` of `world`, through a world-size-1 gather
-            if rank == 0:
+            # (BENCH_EMULATE_NOX=1: no exchange at all, the traces alone)
+            if os.environ.get("BENCH_EMULATE_NOX") == "1":
+                out = None
+            elif rank == 0:
                 dist.gather(emu_buf, [emu_land])
                 out = torch.index_select(emu_land.reshape(world * plan.per_rank, -1), 0, src_index[: n * H])
             else:
