@@ -324,6 +324,7 @@ def main() -> None:
     renderer.set_option("concurrent_launches", D)
 
     cam_cache = {}
+    cam_arrays = {}
 
     def cam_of(k):
         if args.camera_path == "static":
@@ -345,7 +346,10 @@ def main() -> None:
             check(L.rt_render_tile_device(ctx, C.byref(cam_of(k0).ubo), W, H, B, x0, y0, w, h, rgba_ptr, rad_ptr,
                                           s.cuda_stream, stp))
         else:
-            cams = (CameraUBO * n)(*[cam_of(k).ubo for k in range(k0, k0 + n)])
+            ck = (0, n) if args.camera_path == "static" else (k0, n)
+            cams = cam_arrays.get(ck)
+            if cams is None:                          # built once per (frames, count): no host work per launch
+                cams = cam_arrays[ck] = (CameraUBO * n)(*[cam_of(k).ubo for k in range(k0, k0 + n)])
             bl = my_bands[k0 % G] if my_bands is not None else None
             check(L.rt_render_batch_device(ctx, cams, n, W, H, B, band_h if bl is not None else 0, i32p(bl),
                                            len(bl) if bl is not None else 0, rgba_ptr, rad_ptr, s.cuda_stream, stp))
@@ -364,6 +368,7 @@ def main() -> None:
                 (rad_slots[h, off].data_ptr() if off < plan.per_rank else rad_slots[h].data_ptr()) if rad_on else None)
 
     st = {"k": 0, "j": 0}
+    batch_streams = []     # streams that traced part of the current exchange batch
     gathered = [None] * R
     last = {"rgba": None, "rad": None, "frames": []}
     ex_evs = []            # (start, end) events of the timed region's exchanges
@@ -375,8 +380,9 @@ def main() -> None:
         if not dist_on or n == 0:
             return
         h = ((k - 1) // G) % R
-        for s in streams:
+        for s in batch_streams:                       # only the streams that traced this batch
             main_stream.wait_stream(s)
+        batch_streams.clear()
         e0 = e1 = None
         if timed:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -419,9 +425,10 @@ def main() -> None:
             n = min(F, end - k0, G - k0 % G)
             j = st["j"]
             s = streams[j % D]
-            if dist_on and k0 % G == 0 and gathered[(k0 // G) % R] is not None:
-                for t in streams:                      # the exchange that last read these slots is done
-                    t.wait_event(gathered[(k0 // G) % R])
+            if dist_on and gathered[(k0 // G) % R] is not None:
+                s.wait_event(gathered[(k0 // G) % R])  # the exchange that last read this batch's slots is done
+            if dist_on and s not in batch_streams:
+                batch_streams.append(s)
             rp, dp = out_ptrs(k0, j)
             if evs is not None:
                 e = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
