@@ -276,8 +276,11 @@ def main() -> None:
     F = (args.batch if args.batch > 0 else default_batch(world, weak)) if mode in ("whole", "bands") else 1
     F = min(F, 16)
     if mode == "bands":
-        # weak: one exchange per launch (a step's frames); strong: per D launches
-        G = args.exchange_every if args.exchange_every > 0 else (F if weak else D * F)
+        # one exchange per D launches: every exchange costs the host a
+        # collective and an assembly and the streams a join, so fewer, larger
+        # ones (one per launch measured 0.426 vs 0.348 ms per step at N = 8,
+        # emulated: profiles/r03/evidence_r3h)
+        G = args.exchange_every if args.exchange_every > 0 else D * F
         G = max(F, (G + F - 1) // F * F)                       # whole launches per exchange batch
     elif mode == "tiles":
         G = args.exchange_every if args.exchange_every > 0 else D
