@@ -22,6 +22,7 @@
 #include <limits>
 #include <new>
 #include <string>
+#include <strings.h>
 #include <thread>
 #include <vector>
 
@@ -285,13 +286,213 @@ int rt_camera_from_lookat(const double origin[3], const double lookat[3], const 
 }
 
 // -------------------------------------------------------------------- OBJ --
+//
+// SceneBuilder.loadModel (SceneBuilder.java:144) reads OBJ files through
+// Assimp (LWJGL-assimp 3.3.6, Assimp 5.x):
+// aiImportFile(path, aiProcess_Triangulate | aiProcess_JoinIdenticalVertices),
+// then keeps the 3-index faces mesh by mesh, face by face.  Restated here from
+// Assimp's published sources (parity vs a real Assimp run is unpinned: the
+// library is not in this image):
+//  * numbers: fast_atoreal_move<float> (fast_atof.h), NOT a correctly rounded
+//    strtof: the integer digits become a float, the fraction digits (at most
+//    15) a double times 10^-digits, cast to float and added in float (4.9% of
+//    FinalBaseMesh's coordinates differ from strtof by one ulp);
+//  * 'v' lines: 3 components, 4 (x/w, y/w, z/w) or 6 (xyz + a colour);
+//  * faces of 1-2 indices are points / lines (the Java loop skips them);
+//  * aiProcess_Triangulate (TriangulateProcess.cpp): a quad is fanned from its
+//    concave corner (angle sum > pi), else from corner 0; a larger polygon is
+//    projected along its Newell normal's largest axis and ear-clipped; when no
+//    ear is found twice round, the rest of the polygon is dropped (Assimp logs
+//    "Failed to triangulate polygon (no ear found)" and keeps the ears so far).
+// Triangles come out in file order (Assimp splits meshes at material changes
+// but keeps their order of appearance).
 
 struct rt_mesh {
     std::vector<float> v;            // xyz per vertex (as parsed, float like aiVector3D)
     std::vector<uint32_t> tri;       // 3 vertex indices per triangle
 };
 
-static bool parse_index(const char* tok, size_t nverts, uint32_t* out) {
+namespace {
+
+// strtoul10_64 (fast_atof.h): decimal digits into a uint64; with max_digits,
+// stops after that many digits and skips the rest.  Overflow returns 0 and
+// leaves the cursor where it was.
+uint64_t ai_strtoul10_64(const char* in, const char** out, unsigned* max_inout) {
+    unsigned cur = 0;
+    uint64_t value = 0;
+    const char* p = in;
+    while (*p >= '0' && *p <= '9') {
+        const uint64_t nv = value * 10 + (uint64_t)(*p - '0');
+        if (nv < value) { if (out) *out = in; return 0; }
+        value = nv;
+        ++p;
+        ++cur;
+        if (max_inout && *max_inout == cur) {
+            while (*p >= '0' && *p <= '9') ++p;
+            if (out) *out = p;
+            return value;
+        }
+    }
+    if (out) *out = p;
+    if (max_inout) *max_inout = cur;
+    return value;
+}
+
+// fast_atoreal_move<float> (fast_atof.h).  false = Assimp throws (the import
+// fails and SceneBuilder skips the model).
+bool ai_fast_atof(const char* c, float* out) {
+    static const double kTable[16] = {0.0, 0.1, 0.01, 0.001, 0.0001, 0.00001, 0.000001, 0.0000001,
+                                      0.00000001, 0.000000001, 0.0000000001, 0.00000000001,
+                                      0.000000000001, 0.0000000000001, 0.00000000000001,
+                                      0.000000000000001};
+    float f = 0.f;
+    const bool inv = (*c == '-');
+    if (inv || *c == '+') ++c;
+    if ((c[0] == 'N' || c[0] == 'n') && strncasecmp(c, "nan", 3) == 0) {
+        *out = std::numeric_limits<float>::quiet_NaN();
+        return true;
+    }
+    if ((c[0] == 'I' || c[0] == 'i') && strncasecmp(c, "inf", 3) == 0) {
+        *out = inv ? -std::numeric_limits<float>::infinity() : std::numeric_limits<float>::infinity();
+        return true;
+    }
+    const bool comma = true;
+    if (!(c[0] >= '0' && c[0] <= '9') && !((c[0] == '.' || (comma && c[0] == ',')) && c[1] >= '0' && c[1] <= '9'))
+        return false;
+    if (*c != '.' && (!comma || c[0] != ',')) f = (float)ai_strtoul10_64(c, &c, nullptr);
+    if ((*c == '.' || (comma && c[0] == ',')) && c[1] >= '0' && c[1] <= '9') {
+        ++c;
+        unsigned diff = 15;                         // AI_FAST_ATOF_RELAVANT_DECIMALS
+        double pl = (double)ai_strtoul10_64(c, &c, &diff);
+        pl *= kTable[diff];
+        f += (float)pl;
+    } else if (*c == '.') {
+        ++c;
+    }
+    if (*c == 'e' || *c == 'E') {
+        ++c;
+        const bool einv = (*c == '-');
+        if (einv || *c == '+') ++c;
+        float e = (float)ai_strtoul10_64(c, &c, nullptr);
+        if (einv) e = -e;
+        f *= std::pow(10.0f, e);
+    }
+    if (inv) f = -f;
+    *out = f;
+    return true;
+}
+
+struct V3 { float x, y, z; };
+struct V2 { float x, y; };
+
+// aiVector3t::Normalize: *this /= Length(), operator/= multiplies by the
+// float reciprocal and leaves a zero vector alone.
+V3 ai_normalize(V3 a) {
+    const float len = std::sqrt(a.x * a.x + a.y * a.y + a.z * a.z);
+    if (len == 0.f) return a;
+    const float inv = 1.0f / len;
+    return {a.x * inv, a.y * inv, a.z * inv};
+}
+
+// PolyTools.h
+double ai_area2d(const V2& v1, const V2& v2, const V2& v3) {
+    return 0.5 * (v1.x * ((double)v3.y - v2.y) + v2.x * ((double)v1.y - v3.y) + v3.x * ((double)v2.y - v1.y));
+}
+bool ai_on_left_side(const V2& p0, const V2& p1, const V2& p2) { return ai_area2d(p0, p2, p1) > 0; }
+bool ai_point_in_triangle(const V2& p0, const V2& p1, const V2& p2, const V2& pp) {
+    const V2 v0 = {p1.x - p0.x, p1.y - p0.y}, v1 = {p2.x - p0.x, p2.y - p0.y}, v2 = {pp.x - p0.x, pp.y - p0.y};
+    double dot00 = v0.x * v0.x + v0.y * v0.y;       // aiVector2D dot products are float
+    double dot11 = v1.x * v1.x + v1.y * v1.y;
+    const double dot01 = v0.x * v1.x + v0.y * v1.y;
+    const double dot02 = v0.x * v2.x + v0.y * v2.y;
+    const double dot12 = v1.x * v2.x + v1.y * v2.y;
+    const double denom = dot00 * dot11 - dot01 * dot01;
+    if (denom == 0.0) return false;
+    const double inv = 1.0 / denom;
+    dot11 = (dot11 * dot02 - dot01 * dot12) * inv;
+    dot00 = (dot00 * dot12 - dot01 * dot02) * inv;
+    return (dot11 > 0) && (dot00 > 0) && (dot11 + dot00 < 1);
+}
+
+// TriangulateProcess::TriangulateMesh for one face of >= 3 indices: appends
+// its triangles (vertex indices) to tri.
+void ai_triangulate(const std::vector<float>& verts, const std::vector<uint32_t>& idx, std::vector<uint32_t>& tri) {
+    auto P = [&](uint32_t i) { return V3{verts[3 * i], verts[3 * i + 1], verts[3 * i + 2]}; };
+    const int max = (int)idx.size();
+    if (max == 3) { tri.insert(tri.end(), idx.begin(), idx.end()); return; }
+    if (max == 4) {
+        // quads have at most one concave corner: fan from it
+        unsigned start = 0;
+        for (unsigned i = 0; i < 4; ++i) {
+            const V3 v0 = P(idx[(i + 3) % 4]), v1 = P(idx[(i + 2) % 4]), v2 = P(idx[(i + 1) % 4]), v = P(idx[i]);
+            const V3 left = ai_normalize({v0.x - v.x, v0.y - v.y, v0.z - v.z});
+            const V3 diag = ai_normalize({v1.x - v.x, v1.y - v.y, v1.z - v.z});
+            const V3 right = ai_normalize({v2.x - v.x, v2.y - v.y, v2.z - v.z});
+            const float angle = std::acos(left.x * diag.x + left.y * diag.y + left.z * diag.z) +
+                                std::acos(right.x * diag.x + right.y * diag.y + right.z * diag.z);
+            if (angle > 3.14159265358979323846f) { start = i; break; }   // AI_MATH_PI_F
+        }
+        const uint32_t t[6] = {idx[start], idx[(start + 1) % 4], idx[(start + 2) % 4],
+                               idx[start], idx[(start + 2) % 4], idx[(start + 3) % 4]};
+        tri.insert(tri.end(), t, t + 6);
+        return;
+    }
+    // Newell normal (NewellNormal<3,3,3>, float sums)
+    float sxy = 0.f, syz = 0.f, szx = 0.f;
+    for (int k = 0; k < max; ++k) {
+        const V3 a = P(idx[k]), b = P(idx[(k + 1) % max]), c = P(idx[(k + 2) % max]);
+        sxy += b.x * (c.y - a.y);
+        syz += b.y * (c.z - a.z);
+        szx += b.z * (c.x - a.x);
+    }
+    const float nx = syz, ny = szx, nz = sxy;
+    const float ax = nx > 0 ? nx : -nx, ay = ny > 0 ? ny : -ny, az = nz > 0 ? nz : -nz;
+    int ac = 0, bc = 1;                              // drop z: project to xy
+    float inv = nz;
+    if (ax > ay) {
+        if (ax > az) { ac = 1; bc = 2; inv = nx; }   // drop x
+    } else if (ay > az) {
+        ac = 2; bc = 0; inv = ny;                    // drop y
+    }
+    if (inv < 0.f) std::swap(ac, bc);
+    std::vector<V2> tv(max);
+    std::vector<char> done(max, 0);
+    for (int k = 0; k < max; ++k) tv[k] = {verts[3 * idx[k] + ac], verts[3 * idx[k] + bc]};
+    std::vector<int> out;                            // polygon-local corners, 3 per triangle
+    int num = max, ear = 0, prev = max - 1, next = 0, tmp;
+    while (num > 3) {
+        int found = 0;
+        for (ear = next;; prev = ear, ear = next) {
+            for (next = ear + 1; done[(next >= max ? next = 0 : next)]; ++next) {}
+            if (next < ear && ++found == 2) break;
+            const V2 &p1 = tv[ear], &p0 = tv[prev], &p2 = tv[next];
+            if (ai_on_left_side(p0, p2, p1)) continue;          // must be convex
+            for (tmp = 0; tmp < max; ++tmp) {                   // and hold no other corner
+                const V2& q = tv[tmp];
+                const bool same1 = q.x == p1.x && q.y == p1.y, same2 = q.x == p2.x && q.y == p2.y,
+                           same0 = q.x == p0.x && q.y == p0.y;
+                if (!same1 && !same2 && !same0 && ai_point_in_triangle(p0, p1, p2, q)) break;
+            }
+            if (tmp != max) continue;
+            break;                                              // an ear
+        }
+        if (found == 2) { num = 0; break; }                     // no ear: the rest is dropped
+        out.push_back(prev); out.push_back(ear); out.push_back(next);
+        done[ear] = 1;
+        --num;
+    }
+    if (num > 0) {                                              // the last three corners
+        for (tmp = 0; done[tmp]; ++tmp) {}
+        out.push_back(tmp);
+        for (++tmp; done[tmp]; ++tmp) {}
+        out.push_back(tmp);
+        for (++tmp; done[tmp]; ++tmp) {}
+        out.push_back(tmp);
+    }
+    for (int k : out) tri.push_back(idx[k]);
+}
+
+bool parse_index(const char* tok, size_t nverts, uint32_t* out) {
     char* endp = nullptr;
     long k = std::strtol(tok, &endp, 10);
     if (endp == tok) return false;
@@ -300,6 +501,8 @@ static bool parse_index(const char* tok, size_t nverts, uint32_t* out) {
     *out = (uint32_t)(k - 1);
     return true;
 }
+
+}  // namespace
 
 int rt_mesh_load_obj(const char* path, rt_mesh** out) {
     if (!path || !out) { set_error("rt_mesh_load_obj: null pointer"); return RT_ERR_INVALID_ARG; }
@@ -310,69 +513,49 @@ int rt_mesh_load_obj(const char* path, rt_mesh** out) {
     if (!m) { std::fclose(f); set_error("rt_mesh_load_obj: out of memory"); return RT_ERR_OOM; }
     std::vector<char> line(1 << 16);
     std::vector<uint32_t> face;
+    std::vector<std::string> tok;
     size_t lineno = 0;
     int rc = RT_OK;
+    auto is_ws = [](char ch) { return ch == ' ' || ch == '\t' || ch == '\r' || ch == '\n'; };
     while (std::fgets(line.data(), (int)line.size(), f)) {
         ++lineno;
         const char* s = line.data();
         while (*s == ' ' || *s == '\t') ++s;
         if (s[0] == 'v' && (s[1] == ' ' || s[1] == '\t')) {
-            float xyz[3];
-            const char* p = s + 2;
-            for (int k = 0; k < 3; ++k) {
-                char* e = nullptr;
-                xyz[k] = std::strtof(p, &e);
-                if (e == p) { rc = RT_ERR_IO; break; }
+            tok.clear();
+            for (const char* p = s + 2; *p;) {
+                while (is_ws(*p)) ++p;
+                if (!*p) break;
+                const char* e = p;
+                while (*e && !is_ws(*e)) ++e;
+                tok.emplace_back(p, e);
                 p = e;
             }
-            if (rc) { set_error("rt_mesh_load_obj: %s:%zu: bad vertex", path, lineno); break; }
-            m->v.insert(m->v.end(), xyz, xyz + 3);
+            float c[4] = {0.f, 0.f, 0.f, 1.f};
+            const size_t n = tok.size();
+            bool ok = n == 3 || n == 4 || n == 6;
+            for (size_t k = 0; ok && k < (n == 4 ? 4u : 3u); ++k) ok = ai_fast_atof(tok[k].c_str(), &c[k]);
+            if (ok && n == 4) {
+                if (c[3] == 0.f) ok = false;                    // Assimp: division by zero
+                else { c[0] /= c[3]; c[1] /= c[3]; c[2] /= c[3]; }
+            }
+            if (!ok) { rc = RT_ERR_IO; set_error("rt_mesh_load_obj: %s:%zu: bad vertex", path, lineno); break; }
+            m->v.insert(m->v.end(), c, c + 3);
         } else if (s[0] == 'f' && (s[1] == ' ' || s[1] == '\t')) {
             face.clear();
             const char* p = s + 2;
             const size_t nv = m->v.size() / 3;
             while (*p) {
-                while (*p == ' ' || *p == '\t' || *p == '\r' || *p == '\n') ++p;
+                while (is_ws(*p)) ++p;
                 if (!*p) break;
                 uint32_t idx;
                 if (!parse_index(p, nv, &idx)) { rc = RT_ERR_IO; break; }
                 face.push_back(idx);
-                while (*p && *p != ' ' && *p != '\t' && *p != '\r' && *p != '\n') ++p;
+                while (*p && !is_ws(*p)) ++p;
             }
             if (rc) { set_error("rt_mesh_load_obj: %s:%zu: bad face", path, lineno); break; }
             if (face.size() < 3) continue;                 // points / lines are not triangles
-            if (face.size() == 4) {
-                // Assimp TriangulateProcess quad rule: start at a concave
-                // corner if there is one (angle sum > pi), else at corner 0.
-                unsigned start = 0;
-                for (unsigned i = 0; i < 4; ++i) {
-                    const float* v0 = &m->v[3 * face[(i + 3) % 4]];
-                    const float* v1 = &m->v[3 * face[(i + 2) % 4]];
-                    const float* v2 = &m->v[3 * face[(i + 1) % 4]];
-                    const float* vv = &m->v[3 * face[i]];
-                    float l[3], d[3], r[3];
-                    for (int k = 0; k < 3; ++k) { l[k] = v0[k] - vv[k]; d[k] = v1[k] - vv[k]; r[k] = v2[k] - vv[k]; }
-                    auto nrm = [](float* a) {
-                        const float len = std::sqrt(a[0] * a[0] + a[1] * a[1] + a[2] * a[2]);
-                        if (len > 0.f) { a[0] /= len; a[1] /= len; a[2] /= len; }
-                    };
-                    nrm(l); nrm(d); nrm(r);
-                    const float angle = std::acos(l[0] * d[0] + l[1] * d[1] + l[2] * d[2]) +
-                                        std::acos(r[0] * d[0] + r[1] * d[1] + r[2] * d[2]);
-                    if (angle > 3.14159265358979323846f) { start = i; break; }
-                }
-                const uint32_t q[4] = {face[0], face[1], face[2], face[3]};
-                const uint32_t t0[3] = {q[start], q[(start + 1) % 4], q[(start + 2) % 4]};
-                const uint32_t t1[3] = {q[start], q[(start + 2) % 4], q[(start + 3) % 4]};
-                m->tri.insert(m->tri.end(), t0, t0 + 3);
-                m->tri.insert(m->tri.end(), t1, t1 + 3);
-            } else {
-                for (size_t k = 1; k + 1 < face.size(); ++k) {
-                    m->tri.push_back(face[0]);
-                    m->tri.push_back(face[k]);
-                    m->tri.push_back(face[k + 1]);
-                }
-            }
+            ai_triangulate(m->v, face, m->tri);
         }
     }
     std::fclose(f);

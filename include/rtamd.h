@@ -363,11 +363,16 @@ int rt_camera_from_lookat(const double origin[3], const double lookat[3],
                           const double vup[3], double vfov_deg, double aspect,
                           rt_camera_ubo* out);
 
-/* OBJ mesh (SceneBuilder.loadModel, SceneBuilder.java:129-191).  A quad is
- * split along the diagonal from its concave corner, or from vertex 0 when it
- * is convex (Assimp's aiProcess_Triangulate rule for quads); faces with more
- * than 4 vertices are fanned from vertex 0 (Assimp ear-clips them).  Parity
- * vs Assimp is unpinned. */
+/* OBJ mesh (SceneBuilder.loadModel, SceneBuilder.java:129-191), read the way
+ * the reference's Assimp call (aiImportFile(path, aiProcess_Triangulate |
+ * aiProcess_JoinIdenticalVertices), :144) reads it: numbers by Assimp's
+ * fast_atof (not a correctly rounded strtof), 'v' lines of 3, 4 (/w) or 6
+ * components; a quad is split along the diagonal from its concave corner, or
+ * from corner 0 when convex; a larger polygon is projected along its Newell
+ * normal and ear-clipped (TriangulateProcess).  Faces of 1-2 indices are
+ * skipped, as the Java loop skips them.  Triangles in file order.  Restated
+ * from Assimp's published sources (csrc/scene_build.cpp, independently in
+ * oracle/obj_oracle.py); parity vs a real Assimp run is unpinned. */
 typedef struct rt_mesh rt_mesh;
 int    rt_mesh_load_obj(const char* path, rt_mesh** out);
 size_t rt_mesh_tri_count(const rt_mesh* mesh);

@@ -222,3 +222,119 @@ def test_final_base_mesh_fixture():
     if os.path.exists(src):                     # the fixture is the reference's file, unchanged
         from rtamd import Mesh
         assert np.array_equal(Mesh.load_obj(src).tris, m.tris)
+
+
+def _obj_text(rng, n_polys=60):
+    """Random OBJ: star-shaped and comb-shaped (concave) polygons of 3-14
+    corners in random planes, coordinates written with 1-18 fraction digits,
+    exponents, '+' signs and leading dots, plus one self-intersecting face."""
+    lines, nv = [], 0
+
+    def num(x):
+        k = int(rng.integers(0, 6))
+        if k == 0:
+            return f"{x:.{int(rng.integers(1, 19))}f}"
+        if k == 1:
+            return f"{x:.{int(rng.integers(1, 9))}e}"
+        if k == 2:
+            return ("+" if x >= 0 else "") + f"{x:.6f}"
+        if k == 3 and abs(x) < 1:
+            return ("-" if x < 0 else "") + f"{abs(x):.7f}"[1:]       # ".1234567"
+        return repr(float(np.float32(x)))
+
+    for pi in range(n_polys):
+        n = int(rng.integers(3, 15))
+        ang = np.sort(rng.uniform(0, 2 * np.pi, n))
+        if pi % 3 == 0:                                          # comb: alternating radii
+            rad = np.where(np.arange(n) % 2 == 0, 1.0, rng.uniform(0.05, 0.5, n))
+        else:
+            rad = rng.uniform(0.2, 1.5, n)
+        if pi % 5 == 4:
+            ang = ang[::-1]                                      # clockwise winding
+        pts2 = np.stack([rad * np.cos(ang), rad * np.sin(ang)], 1)
+        u, v = rng.normal(size=3), rng.normal(size=3)
+        if pi % 4 == 1:                                          # axis-aligned planes, both signs
+            ax = int(rng.integers(0, 3))
+            u = np.eye(3)[(ax + 1) % 3] * rng.choice([-1, 1])
+            v = np.eye(3)[(ax + 2) % 3]
+        o = rng.normal(size=3) * 5
+        for p in pts2:
+            x = o + p[0] * u + p[1] * v
+            lines.append("v " + " ".join(num(c) for c in x))
+        lines.append("f " + " ".join(str(nv + k + 1) for k in range(n)))
+        nv += n
+    # a self-intersecting hexagon (figure eight): no ear is found twice round
+    for x, y in ((0, 0), (2, 2), (4, 0), (4, 2), (2, 0), (0, 2)):
+        lines.append(f"v {x} {y} 0")
+    lines.append("f " + " ".join(str(nv + k + 1) for k in range(6)))
+    return "\n".join(lines) + "\n"
+
+
+def test_obj_loader_matches_assimp_restatement(tmp_path):
+    """rt_mesh_load_obj vs oracle/obj_oracle.py (an independent restatement of
+    Assimp's fast_atof, OBJ 'v' lines and aiProcess_Triangulate): bit-exact
+    triangles, in order, on random concave / convex / clockwise polygons of
+    3-14 corners in random and axis-aligned planes, numbers written in many
+    forms.  Parity vs a real Assimp run is unpinned."""
+    from oracle import obj_oracle as oo
+    from rtamd import Mesh
+    for seed in range(6):
+        p = tmp_path / f"poly{seed}.obj"
+        p.write_text(_obj_text(np.random.default_rng(seed)))
+        got = Mesh.load_obj(str(p)).tris
+        want = oo.load_obj(str(p)) + np.float32(0)       # the loader's x*1 + 0 turns -0 into +0
+        assert got.shape == want.shape, (seed, got.shape, want.shape)
+        assert np.array_equal(got.view(np.uint32), want.view(np.uint32)), seed
+
+
+def test_obj_ear_clipping_properties(tmp_path):
+    """Every simple polygon of n corners gives n - 2 triangles covering its
+    area, each wound like the polygon (ear clipping, not a fan: a fan from
+    corner 0 of a comb polygon leaves it and overlaps itself)."""
+    from rtamd import Mesh
+    rng = np.random.default_rng(7)
+    for trial in range(40):
+        n = int(rng.integers(5, 16))
+        ang = (np.arange(n) + rng.uniform(0.1, 0.9, n)) * (2 * np.pi / n)   # star-shaped around 0: simple
+        rad = np.where(np.arange(n) % 2 == 0, 1.0, rng.uniform(0.05, 0.6, n))
+        pts = np.stack([rad * np.cos(ang), rad * np.sin(ang)], 1).astype(np.float32)
+        p = tmp_path / f"comb{trial}.obj"
+        p.write_text("".join(f"v {float(x)!r} {float(y)!r} 0\n" for x, y in pts)
+                     + "f " + " ".join(str(k + 1) for k in range(n)) + "\n")
+        t = Mesh.load_obj(str(p)).tris.astype(np.float64)[:, :, :2]
+        assert len(t) == n - 2
+        area = 0.5 * ((t[:, 1, 0] - t[:, 0, 0]) * (t[:, 2, 1] - t[:, 0, 1])
+                      - (t[:, 2, 0] - t[:, 0, 0]) * (t[:, 1, 1] - t[:, 0, 1]))
+        x, y = pts[:, 0].astype(np.float64), pts[:, 1].astype(np.float64)
+        poly = 0.5 * np.sum(x * np.roll(y, -1) - np.roll(x, -1) * y)
+        assert (area > -1e-9).all(), trial                # every triangle counter-clockwise like the polygon
+        assert abs(area.sum() - poly) < 1e-5 * max(1.0, abs(poly)), (trial, area.sum(), poly)
+
+
+def test_obj_numbers_are_assimp_fast_atof(tmp_path):
+    """Assimp parses OBJ numbers with fast_atof, not a correctly rounded
+    strtof: FinalBaseMesh's coordinates (4 decimals) differ from strtof in
+    about 5% of cases, and the loader follows Assimp."""
+    import gzip
+    from oracle import obj_oracle as oo
+    vals = []
+    with gzip.open(os.path.join(os.path.dirname(__file__), "golden", "FinalBaseMesh.obj.gz"), "rt") as fh:
+        for ln in fh:
+            if ln.startswith("v "):
+                vals.extend(ln.split()[1:4])
+    vals = vals[:6000]
+    fa = np.array([oo.fast_atof(t) for t in vals], dtype=np.float32)
+    st = np.array([float(t) for t in vals], dtype=np.float32)
+    assert 0.01 < np.mean(fa != st) < 0.2
+    assert np.all(np.abs(fa.astype(np.float64) - st) <= np.spacing(np.abs(st)))   # one ulp at most
+    p = tmp_path / "nums.obj"
+    toks = ["1.5", "-0.25", "+3", ".5", "-.75", "1e3", "2.5E-2", "7.", "1,5", "123456789012.123456789012345678",
+            "0.1234567890123456789", "-1.000000000000000001"]
+    body = "".join(f"v {toks[k]} {toks[(k + 1) % len(toks)]} {toks[(k + 2) % len(toks)]}\n" for k in range(len(toks)))
+    body += "".join(f"f {k + 1} {(k + 1) % len(toks) + 1} {(k + 2) % len(toks) + 1}\n" for k in range(len(toks)))
+    p.write_text(body)
+    from rtamd import Mesh
+    got = Mesh.load_obj(str(p)).tris
+    want = oo.load_obj(str(p)) + np.float32(0)
+    assert np.array_equal(got.view(np.uint32), want.view(np.uint32))
+    assert got[0, 0].tolist() == [1.5, -0.25, 3.0]
