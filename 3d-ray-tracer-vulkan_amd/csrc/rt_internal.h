@@ -106,7 +106,9 @@ struct TraceArgs {
     // Local row ly is frame row y0 + ((ly / band_h) * band_stride + band_off) * band_h + ly % band_h:
     // a plain tile is band_h = th, band_stride = 1, band_off = 0; rank r of N
     // interleaved 16-row bands is band_h = 16, band_stride = N, band_off = r.
-    // With band_list (device, nullable) it is band_list[ly / band_h] * band_h + ly % band_h.
+    // With band_list (device, nullable) it is band_list[ly / band_h] * band_h + ly % band_h; with
+    // list_stride > 0 frame f reads its own list at band_list + f * list_stride, whose -1 entries
+    // (trailing padding) and rows past the frame are not traced.
     int      band_h, band_stride, band_off;
     const int* band_list;
     // Outputs: n_frames x th x tw pixels, frame f's local row ly at row f * th + ly
@@ -140,6 +142,8 @@ struct TraceArgs {
     hipEvent_t ev_fork, ev_join;
     int      coop_walk;         // cooperative tail: 0 = 64-node preorder windows (coop_walk),
                                 //   1 = preorder frontier (frontier_walk)
+    int      list_stride;       // band_list per frame: frame f's at band_list + f * list_stride
+                                //   (0 = one list for every frame of the launch)
 };
 
 // Host-side compact-scene build from the reference records; validates the

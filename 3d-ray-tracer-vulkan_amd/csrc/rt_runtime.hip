@@ -385,7 +385,7 @@ static int plan_order(const rt_ctx* ctx, PerDevice& p, TraceArgs& a, const rt_ca
     std::vector<int> geo = {a.width, a.height, a.max_bounces, a.x0, a.y0, a.tw, a.th, a.band_h, a.band_stride,
                             a.band_off, a.wave_tile, a.ext, a.coop_lanes, a.walk, ctx->learn_cost,
                             ctx->heavy_factor, concurrency(ctx), ctx->heavy_cap, ctx->heavy_pixel_factor,
-                            a.n_frames, bands ? (int)bands->size() : -1};
+                            a.n_frames, bands ? (int)bands->size() : -1, a.list_stride};
     if (bands) geo.insert(geo.end(), bands->begin(), bands->end());
     const size_t g = geo.size() * sizeof(int), c = (size_t)a.n_frames * sizeof(rt_camera_ubo);
     std::vector<uint8_t> key(g + c + sizeof(uint64_t));
@@ -643,7 +643,7 @@ static std::vector<uint64_t> launch_key(const TraceArgs& a, hipStream_t s) {
     std::vector<uint64_t> k = {P(s), P(sc.nodes), P(sc.leafs), P(sc.pairs), P(sc.nodes2), P(sc.leafs2), P(sc.norms), P(sc.mats), P(sc.spheres),
             (uint64_t)sc.n_spheres, (uint64_t)sc.n_nodes, (uint64_t)sc.end, (uint64_t)sc.n_tris,
             (uint64_t)sc.root_leaf, F(sc.root_box[0]), F(sc.root_box[1]), F(sc.root_box[2]), F(sc.root_box[3]),
-            F(sc.root_box[4]), F(sc.root_box[5]), (uint64_t)a.n_frames, P(a.band_list),
+            F(sc.root_box[4]), F(sc.root_box[5]), (uint64_t)a.n_frames, P(a.band_list), (uint64_t)a.list_stride,
             (uint64_t)a.width, (uint64_t)a.height, (uint64_t)a.max_bounces, (uint64_t)a.x0, (uint64_t)a.y0,
             (uint64_t)a.tw, (uint64_t)a.th, (uint64_t)a.band_h, (uint64_t)a.band_stride, (uint64_t)a.band_off,
             P(a.out_rgba), P(a.out_rad), (uint64_t)a.wave_tile,
@@ -1022,6 +1022,7 @@ int rt_render_tile_device(rt_ctx* ctx, const rt_camera_ubo* cam, int width, int 
     a.x0 = x0; a.y0 = y0; a.tw = tile_w; a.th = tile_h;
     a.band_h = tile_h; a.band_stride = 1; a.band_off = 0;
     a.band_list = nullptr;
+    a.list_stride = 0;
     a.out_rgba = static_cast<uchar4*>(d_out_rgba);
     a.out_rad = static_cast<float*>(d_out_radiance);
     // counters before set_schedule: a counting launch must not become the
@@ -1085,7 +1086,7 @@ static int device_band_list(PerDevice& p, const std::vector<int>& bands, const i
 static int render_rows_on(const rt_ctx* ctx, PerDevice& p, const rt_camera_ubo* cams, int n_frames, int width,
                           int height, int max_bounces, int band_h, int band_stride, int band_off,
                           const std::vector<int>* bands, int rows, uchar4* d_rgba, float* d_rad, hipStream_t s,
-                          bool count) {
+                          bool count, int list_stride = 0) {
     TraceArgs a;
     a.scene = p.scene;
     for (int f = 0; f < n_frames; ++f) a.cams[f] = cam_from_ubo(cams + f);
@@ -1094,6 +1095,7 @@ static int render_rows_on(const rt_ctx* ctx, PerDevice& p, const rt_camera_ubo* 
     a.x0 = 0; a.y0 = 0; a.tw = width; a.th = rows;
     a.band_h = band_h; a.band_stride = band_stride; a.band_off = band_off;
     a.band_list = nullptr;
+    a.list_stride = bands ? list_stride : 0;
     if (bands)
         if (int rb = device_band_list(p, *bands, &a.band_list)) return rb;
     a.out_rgba = d_rgba;
@@ -1210,6 +1212,61 @@ int rt_render_batch_device(rt_ctx* ctx, const rt_camera_ubo* cams, int n_frames,
     if (stats) {
         RT_HIP_CHECK(hipEventSynchronize(p.ev1));
         return collect_stats(ctx, p, (uint64_t)rows * width * n_frames, stats, false);
+    }
+    return RT_OK;
+}
+
+int rt_band_lists_rows(int height, int band_h, const int32_t* bands, int n_frames, int n_per) {
+    if (height < 1 || band_h < 1 || height % band_h != 0 || n_frames < 1 || n_per < 1 || !bands) return -1;
+    for (int f = 0; f < n_frames; ++f) {
+        const int32_t* l = bands + (size_t)f * n_per;
+        int k = 0;
+        while (k < n_per && l[k] >= 0) ++k;                 // the list, then -1 padding only
+        for (int j = k; j < n_per; ++j)
+            if (l[j] != -1) return -1;
+        if (rt_band_list_rows(height, band_h, l, k) < 0) return -1;
+    }
+    return n_per * band_h;                                  // every band is whole: the frame stride
+}
+
+int rt_render_batch_lists_device(rt_ctx* ctx, const rt_camera_ubo* cams, int n_frames, int width, int height,
+                                 int max_bounces, int band_h, const int32_t* bands, int n_per,
+                                 void* d_out_rgba, void* d_out_radiance, void* stream, rt_stats* stats) {
+    int rc = check_render_args(ctx, cams, width, height, max_bounces, "rt_render_batch_lists_device");
+    if (rc) return rc;
+    if (n_frames < 1 || n_frames > kMaxBatch) {
+        set_error("rt_render_batch_lists_device: n_frames must be in [1, %d], got %d", kMaxBatch, n_frames);
+        return RT_ERR_INVALID_ARG;
+    }
+    const int rows = rt_band_lists_rows(height, band_h, bands, n_frames, n_per);
+    if (rows < 0) {
+        set_error("rt_render_batch_lists_device: bad band lists (height %d, band_h %d, %d per frame: band_h must "
+                  "divide height; each frame's indices must increase and lie below height / band_h, then -1 "
+                  "padding only)", height, band_h, n_per);
+        return RT_ERR_INVALID_ARG;
+    }
+    uint64_t pixels = 0;
+    for (int f = 0; f < n_frames; ++f) {
+        const int32_t* l = bands + (size_t)f * n_per;
+        int k = 0;
+        while (k < n_per && l[k] >= 0) ++k;
+        pixels += (uint64_t)rt_band_list_rows(height, band_h, l, k) * (uint64_t)width;
+    }
+    if (rows == 0) {
+        if (stats) std::memset(stats, 0, sizeof *stats);
+        return RT_OK;
+    }
+    PerDevice& p = ctx->dev[0];
+    RT_HIP_CHECK(hipSetDevice(p.device));
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    const std::vector<int> list(bands, bands + (size_t)n_frames * n_per);
+    rc = render_rows_on(ctx, p, cams, n_frames, width, height, max_bounces, band_h, 1, 0, &list, rows,
+                        static_cast<uchar4*>(d_out_rgba), static_cast<float*>(d_out_radiance), s,
+                        stats != nullptr, n_per);
+    if (rc) return rc;
+    if (stats) {
+        RT_HIP_CHECK(hipEventSynchronize(p.ev1));
+        return collect_stats(ctx, p, pixels, stats, false);
     }
     return RT_OK;
 }

@@ -86,9 +86,10 @@ __device__ __forceinline__ uint8_t unorm8(float c) {
     return c > 0.0f ? (c < 1.0f ? (uint8_t)__builtin_rintf(c * 255.0f) : (uint8_t)255) : (uint8_t)0;
 }
 
-// Frame row of local row ly (rt_internal.h, TraceArgs band mapping).
-__device__ __forceinline__ int frame_row(const TraceArgs& a, int ly) {
-    if (a.band_list) return a.y0 + a.band_list[ly / a.band_h] * a.band_h + ly % a.band_h;
+// Frame row of local row ly of frame f of the launch (rt_internal.h, TraceArgs
+// band mapping; the caller skips a per-frame list's -1 padding entries).
+__device__ __forceinline__ int frame_row(const TraceArgs& a, int f, int ly) {
+    if (a.band_list) return a.y0 + a.band_list[f * a.list_stride + ly / a.band_h] * a.band_h + ly % a.band_h;
     return a.y0 + ((ly / a.band_h) * a.band_stride + a.band_off) * a.band_h + ly % a.band_h;
 }
 
@@ -627,10 +628,10 @@ __device__ __forceinline__ void heavy_pixel(const TraceArgs& a, int f, int lx, i
     const int lane = threadIdx.x & 63;
     const int end = a.scene.end;
     unsigned long long c_seg = 0, c_node = 0, c_tri = 0, c_mat = 0;
-    if (lx < a.tw && ly < a.th) {
+    if (lx < a.tw && ly < a.th && (a.list_stride == 0 || a.band_list[f * a.list_stride + ly / a.band_h] >= 0)) {
         uint32_t seed;
         V3 o, d;
-        primary_ray(a, f, a.x0 + lx, frame_row(a, ly), seed, o, d);
+        primary_ray(a, f, a.x0 + lx, frame_row(a, f, ly), seed, o, d);
         V3 att = {1.0f, 1.0f, 1.0f};
         V3 fin = {0.0f, 0.0f, 0.0f};
         int rounds = 0;
@@ -751,7 +752,9 @@ void trace_simple(TraceArgs a) {
     const int lx = col * tw_w + (tl & (tw_w - 1));
     const int ly = by * th_w + (tl >> (3 + s));          // row within the frame's rows
     const int lyo = fr_i * a.th + ly;                    // output row
-    const bool pixel = lx < a.tw && ly < a.th && (sub < 0 || lane == 0) && !((skip_lanes >> lane) & 1ull);
+    // (a per-frame band list's -1 entries are padding rows: no pixel)
+    const bool pixel = lx < a.tw && ly < a.th && (sub < 0 || lane == 0) && !((skip_lanes >> lane) & 1ull) &&
+                       (a.list_stride == 0 || a.band_list[fr_i * a.list_stride + ly / a.band_h] >= 0);
     const int coop_lanes = sub >= 0 ? 64 : a.coop_lanes;
     const float4* __restrict__ nodes = a.scene.nodes;
     const float4* __restrict__ leafs = a.scene.leafs;
@@ -764,7 +767,7 @@ void trace_simple(TraceArgs a) {
     uint32_t seed = 0;
     V3 o = {0.f, 0.f, 0.f}, d = {0.f, 0.f, 1.f};
     if (pixel) {
-        const int x = a.x0 + lx, y = frame_row(a, ly);
+        const int x = a.x0 + lx, y = frame_row(a, fr_i, ly);
         if ((FEAT & kFeatExt) && (a.ext & kExtAccumulate)) {
             // extension: a new sample per frame; frame 0 is the reference's seed (:164)
             seed = (uint32_t)(y * a.width + x) + (uint32_t)a.frame_count * (uint32_t)(a.width * a.height);

@@ -33,7 +33,7 @@ EXPORTED = (
     "rt_mesh_free", "rt_mesh_procedural", "rt_render_bands_device", "rt_band_rows",
     "rt_scene_validate", "rt_set_option", "rt_get_option", "rt_diag_copy",
     "rt_host_alloc", "rt_host_free", "rt_render_async", "rt_render_wait", "rt_upload_spheres",
-    "rt_render_batch_device", "rt_band_list_rows",
+    "rt_render_batch_device", "rt_band_list_rows", "rt_render_batch_lists_device", "rt_band_lists_rows",
 )
 
 
@@ -119,6 +119,9 @@ def lib() -> C.CDLL:
                 "rt_render_batch_device": (i32, [vp, C.POINTER(CameraUBO), i32, i32, i32, i32, i32,
                                                  C.POINTER(C.c_int32), i32, vp, vp, vp, C.POINTER(Stats)]),
                 "rt_band_list_rows": (i32, [i32, i32, C.POINTER(C.c_int32), i32]),
+                "rt_render_batch_lists_device": (i32, [vp, C.POINTER(CameraUBO), i32, i32, i32, i32, i32,
+                                                       C.POINTER(C.c_int32), i32, vp, vp, vp, C.POINTER(Stats)]),
+                "rt_band_lists_rows": (i32, [i32, i32, C.POINTER(C.c_int32), i32, i32]),
                 "rt_scene_validate": (i32, [vp, sz, vp, sz, vp, sz, C.POINTER(sz), C.POINTER(i32)]),
                 "rt_set_option": (i32, [vp, C.c_char_p, C.c_int64]),
                 "rt_get_option": (i32, [vp, C.c_char_p, C.POINTER(C.c_int64)]),

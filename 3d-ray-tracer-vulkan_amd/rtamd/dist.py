@@ -12,6 +12,13 @@ Partitions of a frame over the N ranks:
   packed bands to rank 0, which assembles the frames with one index_select.
   root_weight 1 is the plain interleave: rank r gets the bands b = r mod N
   (band_rows, gather_frame, gather_frames);
+* rotating contiguous pieces (SharePlan layout "pieces"; bench.py's weak
+  scaling default): the frame cut into N contiguous pieces of whole bands; in
+  frame f rank r traces piece (r + f) mod N, and a launch of N consecutive
+  frames (rt_render_batch_lists_device, one band list per frame) holds every
+  piece once, each of a different frame, so every rank traces one whole
+  frame's rows per step with a whole frame's spatial coherence; gathered and
+  assembled like the bands;
 * a tile grid (tile_grid, tile_rects, TilePlan, gather_tiles): N = gx x gy
   rectangles, e.g. BASELINE config 4's 2 x 2 over 4 GPUs; one gather of the
   (padded) tiles and one index_select;
@@ -125,6 +132,14 @@ def list_rows(height: int, band_h: int, bands) -> np.ndarray:
     return rows[rows < height]
 
 
+def piece_owners(height: int, band_h: int, world: int) -> np.ndarray:
+    """Owner position of every band_h-row band when the frame is cut into
+    world contiguous pieces of whole bands (sizes differ by at most one band):
+    piece p holds the bands [floor(p * n / world), floor((p + 1) * n / world))."""
+    n = (height + band_h - 1) // band_h
+    return (np.arange(n) * world) // n if n else np.zeros(0, np.int64)
+
+
 class SharePlan:
     """Row bookkeeping of a batch of n_frames frames over world ranks in
     weighted bands.  Rank r's exchange buffer holds its shares of the batch's
@@ -135,29 +150,42 @@ class SharePlan:
     rotate=False: rank r has the same bands in every frame (strong scaling,
     bench.py --partition bands).  rotate=True (weights 1 only): in frame f,
     rank r traces the bands of position (r + f) mod world, so over world
-    frames every rank traces every band once (weak scaling, --partition
-    frames)."""
+    frames every rank traces every band once.
+
+    layout="pieces" (weak scaling, bench.py --partition pieces; rotates, weights
+    1): the positions are world contiguous pieces of the frame (piece_owners),
+    so a launch of world consecutive frames holds every piece once, each of a
+    different frame: one whole frame's rows with a whole frame's spatial
+    coherence.  Frames sit at a fixed stride of max_rows rows (off[r][f] =
+    f * max_rows), as rt_render_batch_lists_device writes per-frame lists
+    padded to the longest piece; launch_lists gives those lists."""
 
     def __init__(self, height: int, band_h: int, world: int, n_frames: int, root_weight: float = 1.0,
-                 rotate: bool = False):
+                 rotate: bool = False, layout: str = "interleave"):
+        if layout == "pieces":
+            rotate = True
         if rotate and root_weight != 1.0:
             raise ValueError("rotating bands take equal weights")
+        if layout not in ("interleave", "pieces"):
+            raise ValueError(f"unknown layout {layout!r}")
         self.height, self.band_h, self.world, self.n_frames = height, band_h, world, n_frames
-        self.root_weight, self.rotate = root_weight, rotate
-        owner = band_owners(height, band_h, world, root_weight)
+        self.root_weight, self.rotate, self.layout = root_weight, rotate, layout
+        owner = piece_owners(height, band_h, world) if layout == "pieces" else \
+            band_owners(height, band_h, world, root_weight)
         self.pos_bands = [np.flatnonzero(owner == r).astype(np.int32) for r in range(world)]
         self.pos_rows = [list_rows(height, band_h, b) for b in self.pos_bands]
         self.bands = self.pos_bands                    # rank r's bands (rotate=False)
         self.rows = self.pos_rows
         self.counts = [len(x) for x in self.pos_rows]
         self.max_rows = max(self.counts)
+        self.n_per = max(len(b) for b in self.pos_bands)   # list length of a piece launch
         self.off = [[0] * n_frames for _ in range(world)]
         self.per_rank = 0
         for r in range(world):
             o = 0
             for f in range(n_frames):
                 self.off[r][f] = o
-                o += len(self.frame_rows(r, f))
+                o += self.max_rows if layout == "pieces" else len(self.frame_rows(r, f))
             self.per_rank = max(self.per_rank, o)
         src = np.empty(n_frames * height, np.int64)
         for r in range(world):
@@ -175,18 +203,27 @@ class SharePlan:
     def frame_rows(self, rank: int, frame: int) -> np.ndarray:
         return self.pos_rows[self.position(rank, frame)]
 
+    def launch_lists(self, rank: int, frame0: int, n: int) -> np.ndarray:
+        """rt_render_batch_lists_device's bands for frames frame0 .. frame0 + n - 1
+        of the batch: n lists of n_per entries, -1 padded."""
+        out = np.full((n, self.n_per), -1, np.int32)
+        for f in range(n):
+            b = self.frame_bands(rank, frame0 + f)
+            out[f, :len(b)] = b
+        return out
+
 
 _SHARE_PLANS: dict = {}
 
 
 def cached_share_plan(height: int, band_h: int, world: int, n_frames: int, root_weight: float, device,
-                      rotate: bool = False):
+                      rotate: bool = False, layout: str = "interleave"):
     """SharePlan and its source-row index on `device`, built once per layout."""
     import torch
-    key = (height, band_h, world, n_frames, float(root_weight), str(device), rotate)
+    key = (height, band_h, world, n_frames, float(root_weight), str(device), rotate, layout)
     hit = _SHARE_PLANS.get(key)
     if hit is None:
-        plan = SharePlan(height, band_h, world, n_frames, root_weight, rotate)
+        plan = SharePlan(height, band_h, world, n_frames, root_weight, rotate, layout)
         hit = (plan, torch.as_tensor(plan.src, device=device))
         _SHARE_PLANS[key] = hit
     return hit

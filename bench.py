@@ -175,9 +175,10 @@ def main() -> None:
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", type=int, default=3, help="BASELINE config index (3 = headline)")
-    ap.add_argument("--partition", choices=("bands", "tiles"), default="bands",
+    ap.add_argument("--partition", choices=("bands", "tiles", "pieces"), default="bands",
                     help="N > 1: how a frame is tiled over the ranks: bands = weighted interleaved row bands "
-                         "(default); tiles = gx x gy rectangles (2 x 2 at N = 4)")
+                         "(default); tiles = gx x gy rectangles (2 x 2 at N = 4); pieces = N contiguous row "
+                         "pieces rotated frame by frame (a launch of N frames holds every piece once)")
     ap.add_argument("--scaling", choices=("weak", "strong"), default="weak",
                     help="N > 1: weak = a step is N frames of the render loop, each tiled over all ranks and "
                          "gathered (every rank traces one frame's worth per step; default); strong = a step is "
@@ -273,9 +274,9 @@ def main() -> None:
     weak = dist_on and args.scaling == "weak"
     step_frames = world if weak else 1                         # frames per step (weak scaling: N)
     D = args.inflight if args.inflight > 0 else default_inflight(world)
-    F = (args.batch if args.batch > 0 else default_batch(world, weak)) if mode in ("whole", "bands") else 1
+    F = (args.batch if args.batch > 0 else default_batch(world, weak)) if mode in ("whole", "bands", "pieces") else 1
     F = min(F, 16)
-    if mode == "bands":
+    if mode in ("bands", "pieces"):
         # one exchange per D launches: every exchange costs the host a
         # collective and an assembly and the streams a join, so fewer, larger
         # ones (one per launch measured 0.426 vs 0.348 ms per step at N = 8,
@@ -294,9 +295,10 @@ def main() -> None:
     plan = tplan = None
     src_index = None
     my_bands = None
-    if mode == "bands":
+    if mode in ("bands", "pieces"):
         rw = args.root_weight if args.root_weight >= 0 else default_root_weight(world)
-        plan = SharePlan(H, band_h, world, G, rw)
+        plan = SharePlan(H, band_h, world, G, rw) if mode == "bands" else \
+            SharePlan(H, band_h, world, G, 1.0, layout="pieces")
         src_index = torch.as_tensor(plan.src, device=dev)
         my_bands = [np.ascontiguousarray(plan.frame_bands(rank, f)) for f in range(G)]
         rgba_slots = torch.empty((R, plan.per_rank, W, 4), dtype=torch.uint8, device=dev)
@@ -314,8 +316,8 @@ def main() -> None:
         rad_slots = None
         px_per_frame = W * H
     if emu:
-        if mode != "bands":
-            raise SystemExit("BENCH_EMULATE emulates --partition bands")
+        if mode not in ("bands", "pieces"):
+            raise SystemExit("BENCH_EMULATE emulates --partition bands / pieces")
         emu_buf = torch.zeros((world * plan.per_rank, W, 4) if rank == 0 else (1,), dtype=torch.uint8, device=dev)
         emu_land = torch.empty_like(emu_buf if rank == 0 else rgba_slots[0])
     streams = [torch.cuda.Stream(dev) for _ in range(D)]
@@ -328,6 +330,7 @@ def main() -> None:
 
     cam_cache = {}
     cam_arrays = {}
+    piece_lists = {}
 
     def cam_of(k):
         if args.camera_path == "static":
@@ -353,9 +356,17 @@ def main() -> None:
             cams = cam_arrays.get(ck)
             if cams is None:                          # built once per (frames, count): no host work per launch
                 cams = cam_arrays[ck] = (CameraUBO * n)(*[cam_of(k).ubo for k in range(k0, k0 + n)])
-            bl = my_bands[k0 % G] if my_bands is not None else None
-            check(L.rt_render_batch_device(ctx, cams, n, W, H, B, band_h if bl is not None else 0, i32p(bl),
-                                           len(bl) if bl is not None else 0, rgba_ptr, rad_ptr, s.cuda_stream, stp))
+            if mode == "pieces":                      # one band list per frame, built once per (frame, count)
+                pl = piece_lists.get((k0 % G, n))
+                if pl is None:
+                    pl = piece_lists[(k0 % G, n)] = np.ascontiguousarray(plan.launch_lists(rank, k0 % G, n))
+                check(L.rt_render_batch_lists_device(ctx, cams, n, W, H, B, band_h, i32p(pl), plan.n_per, rgba_ptr,
+                                                     rad_ptr, s.cuda_stream, stp))
+            else:
+                bl = my_bands[k0 % G] if my_bands is not None else None
+                check(L.rt_render_batch_device(ctx, cams, n, W, H, B, band_h if bl is not None else 0, i32p(bl),
+                                               len(bl) if bl is not None else 0, rgba_ptr, rad_ptr, s.cuda_stream,
+                                               stp))
         return st.as_dict() if stats else None
 
     def out_ptrs(k0, j):
@@ -390,7 +401,7 @@ def main() -> None:
         if timed:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(main_stream)
-        if emu and mode == "bands":
+        if emu and mode in ("bands", "pieces"):
             # the exchange volume of rank `rank` of `world`, through a world-size-1 gather
             # (BENCH_EMULATE_NOX=1: no exchange at all, the traces alone)
             if os.environ.get("BENCH_EMULATE_NOX") == "1":
@@ -650,6 +661,11 @@ def main() -> None:
             part = (f"one frame per step in {band_h}-row bands dealt to {world} ranks by a weighted round robin "
                     f"(rank 0 weight {plan.root_weight}, rows per rank {plan.counts}), {D} launches in flight x "
                     f"{F} frames per launch, {gather_kind} gather of every {G} frames + rank-0 assembly{shared}")
+        elif mode == "pieces":
+            part = (f"every frame cut into {world} contiguous pieces of {band_h}-row bands (rows {plan.counts}), "
+                    f"rank r tracing piece (r + f) mod {world} of frame f, {D} launches in flight x {F} frames per "
+                    f"launch (one band list per frame), {gather_kind} gather of every {G} frames + rank-0 "
+                    f"assembly{shared}")
         elif mode == "tiles":
             part = (f"one frame per step tiled {tplan.gx} x {tplan.gy} over {world} ranks (tiles "
                     f"{tplan.rects}), {D} frames in flight, {gather_kind} gather of every {G} frames + rank-0 "
@@ -681,7 +697,7 @@ def main() -> None:
                 "frames_per_launch": F,
                 "launches_in_flight": D,
                 "exchange_every_frames": G if dist_on else None,
-                "band_h": band_h if mode == "bands" else None,
+                "band_h": band_h if mode in ("bands", "pieces") else None,
                 "root_weight": plan.root_weight if plan is not None else None,
                 "gather": ("rgba8 + float radiance" if rad_on else "rgba8") if dist_on else None,
                 "frames_verified": verified,

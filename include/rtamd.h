@@ -169,6 +169,25 @@ int rt_render_batch_device(rt_ctx* ctx, const rt_camera_ubo* cams, int n_frames,
  * reaches past the frame).  Pure host code. */
 int rt_band_list_rows(int height, int band_h, const int32_t* bands, int n_bands);
 
+/* Batched frames, each over its OWN band list, for the weak-scaling
+ * partition that rotates contiguous row pieces over the ranks frame by frame
+ * (every rank's launch then holds one whole frame's worth of rows, each piece
+ * of a different frame): frame f traces the band_h-row bands
+ * bands[f * n_per .. f * n_per + n_per), a strictly increasing list followed
+ * by -1 padding only; band_h must divide height.  List position k of frame f is written at rows
+ * [f * R + k * band_h, ...) of the DEVICE buffers, R = n_per * band_h =
+ * rt_band_lists_rows(height, band_h, bands, n_frames, n_per); padding rows
+ * are neither traced nor written.  Otherwise as
+ * rt_render_batch_device (stats: totals over the frames' listed rows). */
+int rt_render_batch_lists_device(rt_ctx* ctx, const rt_camera_ubo* cams, int n_frames,
+                                 int width, int height, int max_bounces,
+                                 int band_h, const int32_t* bands, int n_per,
+                                 void* d_out_rgba, void* d_out_radiance,
+                                 void* stream, rt_stats* stats);
+
+/* R of such lists, n_per * band_h (-1 if a list is bad).  Pure host code. */
+int rt_band_lists_rows(int height, int band_h, const int32_t* bands, int n_frames, int n_per);
+
 /* Pipelined frames (overlap the readback with the next
  * frame; the reference waits on a fence after every frame,
  * VulkanEngine.java:410-429).

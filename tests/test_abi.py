@@ -158,6 +158,22 @@ def test_band_list_rows_and_weighted_deal():
         assert sorted(plan.src.tolist()) == sorted(set(plan.src.tolist()))     # every row from one place
     assert rows(10, 4, [1, 0]) == -1          # not increasing
     assert rows(10, 4, [3]) == -1             # past the frame
+
+    def lrows(h, bh, lists):
+        flat = [b for lst in lists for b in lst]
+        arr = (C.c_int32 * len(flat))(*flat)
+        return L.rt_band_lists_rows(h, bh, arr, len(lists), len(lists[0]))
+    # rt_band_lists_rows: per-frame lists, -1 padding at the end only, band_h | height
+    assert lrows(48, 4, [[0, 1, 2], [3, 4, -1]]) == 12
+    assert lrows(48, 4, [[0, -1, 2]]) == -1
+    assert lrows(48, 4, [[2, 1, -1]]) == -1
+    assert lrows(48, 4, [[12, -1]]) == -1     # past the frame
+    assert lrows(50, 4, [[0, 1]]) == -1       # band_h must divide the height
+    for world in (2, 3, 8):
+        plan = SharePlan(1080, 8, world, world, layout="pieces")
+        lists = plan.launch_lists(1, 0, world)
+        assert lrows(1080, 8, lists.tolist()) == plan.max_rows == plan.n_per * 8
+        assert sorted(int(b) for b in lists.reshape(-1) if b >= 0) == list(range(135))   # every band once
     assert rows(10, 4, []) == 0
     assert rows(10, 4, [2]) == 2              # the partial last band
 

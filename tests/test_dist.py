@@ -283,6 +283,26 @@ def _share_worker(rank, world, port, q, kind, arg, n_frames, W, H, B):
                     traced += w * h
             out = gather_tiles(rgba, plan)
             outr = gather_tiles(rad, plan)
+        elif kind == "pieces":
+            # rt_render_batch_lists_device's packing: one launch of all the
+            # batch's frames, list position k of frame f at rows off + k * band_h
+            band_h = arg
+            plan = SharePlan(H, band_h, world, n_frames, layout="pieces")
+            rgba = torch.zeros((plan.per_rank, W, 4), dtype=torch.uint8)
+            rad = torch.zeros((plan.per_rank, W, 3), dtype=torch.float32)
+            lists = plan.launch_lists(rank, 0, n_frames)
+            for f in range(n_frames):
+                for k, b in enumerate(lists[f]):
+                    if b < 0:
+                        continue
+                    a, r, _ = oracle_lib.render(*args, cams[f].ubo_bytes(), W, H, B, tile=(0, int(b) * band_h, W, band_h),
+                                                n_threads=1)
+                    o = plan.off[rank][f] + k * band_h
+                    rgba[o: o + band_h] = torch.from_numpy(a)
+                    rad[o: o + band_h] = torch.from_numpy(r)
+                    traced += W * band_h
+            out = gather_shares(rgba, plan)
+            outr = gather_shares(rad, plan)
         else:
             band_h, rw, rotate = arg
             plan = SharePlan(H, band_h, world, n_frames, rw, rotate=rotate)
@@ -362,3 +382,18 @@ def test_rotating_bands_weak_scaling_8_ranks():
     worth of rows; the 8 frames reassemble."""
     traced = _run_share(8, "bands", (4, 1.0, True), n_frames=8, W=48, H=40, B=2)
     assert set(traced.values()) == {48 * 40}
+
+
+@pytest.mark.parametrize("world,n_frames,band_h", [(8, 8, 4), (3, 6, 4), (2, 2, 8)])
+def test_rotating_pieces_weak_scaling(world, n_frames, band_h):
+    """--partition pieces (bench.py's weak-scaling partition): every frame cut
+    into world contiguous pieces of whole bands (sizes differ by a band), rank
+    r tracing piece (r + f) mod world of frame f, all the batch's frames in
+    one launch with one band list per frame (-1 padded to the longest piece,
+    rt_render_batch_lists_device's packing); one gather and one index_select:
+    every frame and its radiance equal the oracle's, and over world frames
+    every rank traced exactly one frame's worth of rows."""
+    W, H = 48, 40
+    traced = _run_share(world, "pieces", band_h, n_frames=n_frames, W=W, H=H, B=2)
+    assert sum(traced.values()) == n_frames * W * H
+    assert set(traced.values()) == {n_frames // world * W * H}

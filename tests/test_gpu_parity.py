@@ -769,6 +769,83 @@ def test_batch_whole_frames_and_errors(renderer):
     assert lib().rt_band_list_rows(h, 16, (C.c_int32 * 1)(11), 1) == h - 11 * 16     # the partial last band
 
 
+@pytest.mark.parametrize("cfg_k,world,rank,n", [(3, 3, 1, 3), (2, 8, 0, 8), (6, 4, 3, 4)])
+def test_batch_lists_pieces_bit_exact(renderer, cfg_k, world, rank, n):
+    """rt_render_batch_lists_device (bench.py --partition pieces): one launch
+    traces, for each of n frames (cameras differ), the contiguous piece
+    (rank + f) mod world of that frame, one band list per frame padded with -1
+    to the longest piece.  The learning launch, a counting launch and a plain
+    launch in the learned order each give every frame's piece of the oracle's
+    frame, bit for bit, with the pieces' counts; padding rows are left
+    untouched; bad lists are rejected."""
+    import ctypes as C
+    import torch
+    from rtamd import CameraUBO, RtError, configs, lib
+    from rtamd._lib import Stats, check
+    from rtamd.dist import SharePlan, list_rows
+    cfg = configs.get(cfg_k)
+    built = cfg.build()
+    renderer.upload_scene(built)
+    W, H, B = cfg.width, cfg.height, cfg.max_bounces
+    band_h = 8
+    cams = [configs.Camera((-25.0 + 3 * (f % 3), 30.0, 140.0 - 4 * (f % 3)), (0.0, 0.0, 0.0), (0.0, 1.0, 0.0), 20.0,
+                           W / H) for f in range(n)]
+    plan = SharePlan(H, band_h, world, n, layout="pieces")
+    lists = np.ascontiguousarray(plan.launch_lists(rank, 0, n))
+    L = lib()
+    arr = lists.ctypes.data_as(C.POINTER(C.c_int32))
+    R = L.rt_band_lists_rows(H, band_h, arr, n, plan.n_per)
+    assert R == plan.max_rows
+    full = {}
+    for f in range(n):
+        key = f % 3
+        if key not in full:
+            full[key] = _oracle(built, cams[f].ubo_bytes(), W, H, B)
+    tot = {k: 0 for k in COUNTERS}
+    for f in range(n):
+        for b in lists[f]:
+            if b >= 0:
+                _, _, cb = _oracle(built, cams[f].ubo_bytes(), W, H, B, tile=(0, int(b) * band_h, W, band_h),
+                                   radiance=False)
+                for k in COUNTERS:
+                    tot[k] += cb[k]
+    ubos = (CameraUBO * n)(*[c.ubo for c in cams])
+    try:
+        renderer.set_option("concurrent_launches", 4)
+        for stats in (False, True, False):
+            d_rgba = torch.full((n, R, W, 4), 7, dtype=torch.uint8, device="cuda:0")
+            d_rad = torch.full((n, R, W, 3), -2.0, dtype=torch.float32, device="cuda:0")
+            st = Stats()
+            check(L.rt_render_batch_lists_device(renderer._ctx, ubos, n, W, H, B, band_h, arr, plan.n_per,
+                                                 d_rgba.data_ptr(), d_rad.data_ptr(),
+                                                 torch.cuda.current_stream().cuda_stream,
+                                                 C.byref(st) if stats else None))
+            torch.cuda.synchronize()
+            rgba, rad = d_rgba.cpu().numpy(), d_rad.cpu().numpy()
+            for f in range(n):
+                valid = [int(b) for b in lists[f] if b >= 0]
+                rows = list_rows(H, band_h, valid)
+                ref_rgba, ref_rad, _ = full[f % 3]
+                k = len(rows)
+                _assert_same(rgba[f, :k], rad[f, :k], None, ref_rgba[rows], ref_rad[rows], None)
+                assert (rgba[f, k:] == 7).all() and (rad[f, k:] == -2.0).all()     # padding rows untouched
+            if stats:
+                sd = st.as_dict()
+                for k in COUNTERS:
+                    assert sd[k] == tot[k], (k, sd[k], tot[k])
+                assert sd["pixels"] == W * sum(8 * int((lists[f] >= 0).sum()) for f in range(n))
+                if n == world:
+                    assert sd["pixels"] == H * W                    # every piece once: one frame's worth
+    finally:
+        for k, v in DEFAULT_OPTS.items():
+            renderer.set_option(k, v)
+    bad = np.array([[1, 0] + [-1] * (plan.n_per - 2)], np.int32)
+    with pytest.raises(RtError, match="INVALID_ARG"):
+        check(L.rt_render_batch_lists_device(renderer._ctx, ubos, 1, W, H, B, band_h,
+                                             bad.ctypes.data_as(C.POINTER(C.c_int32)), plan.n_per,
+                                             None, None, None, None))
+
+
 @pytest.mark.parametrize("slots,toggle", [(4, False), (3, True)])
 def test_render_async_accumulation_and_copy_toggle(slots, toggle):
     """rt_render_async with the accumulation extension (per-device running
