@@ -235,6 +235,9 @@ struct PerDevice {
     hipStream_t  slot_stream[kMaxSlots] = {};
     hipEvent_t   traced[kMaxSlots] = {}, copied[kMaxSlots] = {}, copied2[kMaxSlots] = {};
     uint64_t     slot_ticket[kMaxSlots] = {};
+    bool         slot_split[kMaxSlots] = {};   // the slot's newest frame split its readback (copy_stream2)
+    uint64_t     last_split_t = 0;             // newest split frame's ticket, its copied2 slot
+    int          last_split_slot = -1;
     float*       d_accum = nullptr;  // extension kExtAccumulate: running sums
     float4*      d_spheres = nullptr; // extension kExtSpheres: 2 float4 per sphere
     int          n_spheres = 0;
@@ -1376,9 +1379,10 @@ int rt_render_async(rt_ctx* ctx, const rt_camera_ubo* cam, int width, int height
         // GPU_MAX_HW_QUEUES >= slots + 2), so the frames in flight run at once.
         if (!p.slot_stream[slot]) RT_HIP_CHECK(hipStreamCreateWithFlags(&p.slot_stream[slot], hipStreamNonBlocking));
         const hipStream_t ts = p.slot_stream[slot];
-        // The slot's previous frame must be read back before it is overwritten.
+        // The slot's previous frame must be read back before it is overwritten
+        // (both halves, if it split its readback).
         RT_HIP_CHECK(hipStreamWaitEvent(ts, p.copied[slot], 0));
-        RT_HIP_CHECK(hipStreamWaitEvent(ts, p.copied2[slot], 0));
+        if (p.slot_split[slot]) RT_HIP_CHECK(hipStreamWaitEvent(ts, p.copied2[slot], 0));
         // A frame that reads and writes per-device state shared by the slots
         // (the accumulation extension's running sums; the diagnostic records)
         // must not overlap the previous frame: its trace waits for that one.
@@ -1393,12 +1397,13 @@ int rt_render_async(rt_ctx* ctx, const rt_camera_ubo* cam, int width, int height
         if (rc) return rc;
         RT_HIP_CHECK(hipEventRecord(p.traced[slot], ts));
         // Copies run in ticket order on the one copy stream, whatever order the
-        // traces finish in.
+        // traces finish in.  copy_stream2 (a split readback's second half) is
+        // touched only by the frames that split: a join on an idle stream per
+        // frame costs the pipelined loop time for nothing.
         RT_HIP_CHECK(hipStreamWaitEvent(p.copy_stream, p.traced[slot], 0));
-        // copy_stream2 joins every frame, copying or not, so copied2[slot]
-        // always belongs to this slot's newest ticket (rt_render_wait)
-        RT_HIP_CHECK(hipStreamWaitEvent(p.copy_stream2, p.traced[slot], 0));
-        if (nd == 1 && ctx->copy_streams == 2 && rows > 1) {
+        const bool split = nd == 1 && ctx->copy_streams == 2 && rows > 1;
+        if (split) RT_HIP_CHECK(hipStreamWaitEvent(p.copy_stream2, p.traced[slot], 0));
+        if (split) {
             // the frame's top and bottom halves on two copy streams, so two copy
             // engines read the frame back at once
             const size_t top = (size_t)width * (size_t)(rows / 2) * 4;
@@ -1424,7 +1429,12 @@ int rt_render_async(rt_ctx* ctx, const rt_camera_ubo* cam, int width, int height
                                             p.copy_stream));
         }
         RT_HIP_CHECK(hipEventRecord(p.copied[slot], p.copy_stream));
-        RT_HIP_CHECK(hipEventRecord(p.copied2[slot], p.copy_stream2));
+        if (split) {
+            RT_HIP_CHECK(hipEventRecord(p.copied2[slot], p.copy_stream2));
+            p.last_split_t = t;
+            p.last_split_slot = slot;
+        }
+        p.slot_split[slot] = split;
         p.slot_ticket[slot] = t;
     }
     ctx->issued = t;
@@ -1446,13 +1456,13 @@ int rt_render_wait(rt_ctx* ctx, uint64_t ticket) {
         int best = -1;
         for (int k2 = 0; k2 < kMaxSlots; ++k2)
             if (p.slot_ticket[k2] >= ticket && (best < 0 || p.slot_ticket[k2] < p.slot_ticket[best])) best = k2;
-        if (best >= 0) {
-            RT_HIP_CHECK(hipEventSynchronize(p.copied[best]));
-            RT_HIP_CHECK(hipEventSynchronize(p.copied2[best]));   // recorded for every frame (rt_render_async)
-        } else {
-            RT_HIP_CHECK(hipStreamSynchronize(p.copy_stream));   // a device with no rows of that frame
-            RT_HIP_CHECK(hipStreamSynchronize(p.copy_stream2));
-        }
+        if (best >= 0) RT_HIP_CHECK(hipEventSynchronize(p.copied[best]));
+        else RT_HIP_CHECK(hipStreamSynchronize(p.copy_stream));   // a device with no rows of that frame
+        // A split frame's second half is on copy_stream2, in ticket order: the
+        // newest split frame's event covers every split frame up to it (it may
+        // over-wait for a frame that did not split, never under-wait).
+        if (p.last_split_t >= ticket && p.last_split_slot >= 0)
+            RT_HIP_CHECK(hipEventSynchronize(p.copied2[p.last_split_slot]));
     }
     return RT_OK;
 }

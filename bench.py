@@ -268,6 +268,14 @@ def main() -> None:
         renderer.set_option(k.strip(), int(v))
     L = rtamd.lib()
     ctx = renderer._ctx
+    # The PCIe-inclusive rate first, before this process creates its own
+    # streams: HIP deals its hardware queues out to streams in creation order,
+    # and rt_render_async's slot streams must not share queues with bench's
+    # (in the middle of bench.py they did: 0.49 vs 0.36 ms per frame,
+    # profiles/r03/emulation/r3l pipeline.jsonl vs bench20_pcie.json).
+    pcie = None
+    if rank == 0 and not dist_on and args.camera_path == "static" and not args.no_pcie:
+        pcie = pcie_rate(renderer, cfg.camera(), W, H, B)
 
     # ---- partition -------------------------------------------------------
     mode = args.partition if dist_on else "whole"
@@ -648,9 +656,6 @@ def main() -> None:
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(built, cam_of(k_t0), W, H, B, segments / K, args.cpu_seconds)
-    pcie = None
-    if rank == 0 and mode == "whole" and args.camera_path == "static" and not args.no_pcie:
-        pcie = pcie_rate(renderer, cam_of(0), W, H, B, segments / K)
 
     if rank == 0 or emu:
         gather_kind = "RCCL" if backend == "nccl" else (backend or "none")
@@ -752,11 +757,12 @@ def main() -> None:
         dist.destroy_process_group()
 
 
-def pcie_rate(renderer, cam, W, H, B, frame_segments, n=100):
+def pcie_rate(renderer, cam, W, H, B, n=200):
     """rt_render_async: 4 frames in flight into pinned host frames, every frame
     read back over PCIe (tools/pipeline_bench.py's async mode)."""
     from rtamd.engine import PinnedFrame
     S = 4
+    frame_segments = renderer.render(cam, W, H, B, stats=True)[2]["segments"]
     renderer.set_option("async_slots", S)
     frames = [PinnedFrame(H, W) for _ in range(S)]
     try:

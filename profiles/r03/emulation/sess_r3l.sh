@@ -5,7 +5,9 @@ set -u
 O=gpurun_out/r3l
 mkdir -p $O
 timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py -q -rA --timeout 300 --timeout-method thread \
-  -k "pieces or batch" > $O/pytest_pieces.log 2>&1 || exit $?
+  -k "pieces or batch or async" > $O/pytest_pieces.log 2>&1 || exit $?
+timeout -k 10 300 python tools/pipeline_bench.py --slots 4 --frames 400 > $O/pipeline.jsonl 2> $O/pipeline.err || exit $?
+timeout -k 10 300 python bench.py --steps 20 --warmup 5 --no-cpu-baseline > $O/bench20_pcie.json 2> $O/bench20_pcie.err || exit $?
 timeout -k 10 300 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-pcie > $O/base20.json 2> $O/base20.err || exit $?
 timeout -k 10 300 python bench.py --no-cpu-baseline --no-pcie > $O/base200.json 2> $O/base200.err || exit $?
 e() { local tag=$1 n=$2 r=$3; shift 3; bash tools/emulate.sh $O/emu $tag $n "$r" --warmup 5 "$@" || exit $?; }

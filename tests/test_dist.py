@@ -212,8 +212,9 @@ def _blocks_worker(rank, world, port, q, first_frame, share):
 
 @pytest.mark.parametrize("world,first,share", [(2, 0, 1.0), (3, 5, 1.0), (4, 2, 0.6), (3, 1, 0.0)])
 def test_blocks_exchange_assembles_frames(world, first, share):
-    """Rotating row pieces (bench.py's N > 1 default): frame k lays the ranks'
-    pieces out in the rotated order k, k+1, ...; rank 0 traces its piece (of
+    """Rotating row blocks exchanged point to point (rtamd.dist.exchange_blocks,
+    an option of the library; bench.py's partitions gather instead): frame k
+    lays the ranks' pieces out in the rotated order k, k+1, ...; rank 0 traces its piece (of
     root_share x H / N rows, 0 to a full share) in place and receives every
     other rank's piece straight into the frame (one batch of point-to-point
     receives).  53 rows over 3 / 4 ranks leaves unequal pieces.  Every frame of
