@@ -326,6 +326,8 @@ struct rt_ctx {
     int  concurrent_launches = 1;  // launches of similar work the caller keeps in flight on a device at once
                                    //   (the heavy-tile bulk estimate counts this launch's work that many times)
     int  learn_cost = 1;           // heavy_first cost: 0 = lockstep steps + 2 x coop windows, 1 = wave duration
+    int  order_split = 0;          // heavy_first: only tiles costing >= this percent of the costliest go first
+                                   //   (in cost order); the rest keep their raster order (0 = all by cost)
     int  graph = 1;                // kernel 0 plain launches: replay a captured HIP graph per launch key
     int  heavy_stream = 2;         // heavy_tiles: 1 = their launch runs on an auxiliary stream, concurrent
                                    //   with the other tiles; 2 = their workgroups come first in the
@@ -386,7 +388,7 @@ static int plan_order(const rt_ctx* ctx, PerDevice& p, TraceArgs& a, const rt_ca
                      (size_t)a.n_frames;
     // key = geometry (+ the band list) | the cameras | the scene
     std::vector<int> geo = {a.width, a.height, a.max_bounces, a.x0, a.y0, a.tw, a.th, a.band_h, a.band_stride,
-                            a.band_off, a.wave_tile, a.ext, a.coop_lanes, a.walk, ctx->learn_cost,
+                            a.band_off, a.wave_tile, a.ext, a.coop_lanes, a.walk, ctx->learn_cost, ctx->order_split,
                             ctx->heavy_factor, concurrency(ctx), ctx->heavy_cap, ctx->heavy_pixel_factor,
                             a.n_frames, bands ? (int)bands->size() : -1, a.list_stride};
     if (bands) geo.insert(geo.end(), bands->begin(), bands->end());
@@ -515,7 +517,17 @@ static int learn_order(const rt_ctx* ctx, PerDevice& p, const TraceArgs& a, hipS
     }
     std::vector<int> order(n);
     for (size_t k = 0; k < n; ++k) order[k] = (int)k;
-    std::stable_sort(order.begin(), order.end(), [&](int x, int y) { return cost[x] > cost[y]; });
+    // Option order_split: the tiles that cost at least that percentage of the
+    // costliest tile go first, most expensive first (they would otherwise end
+    // the launch); the rest keep their raster order, so the waves running at
+    // once trace neighbouring tiles of one frame (one BVH neighbourhood in the
+    // caches) rather than tiles of like cost scattered over the launch's frames.
+    unsigned long long cmax = 0;
+    for (size_t k = 0; k < n; ++k) cmax = std::max(cmax, cost[k]);
+    const double split_at = (double)ctx->order_split / 100.0 * (double)cmax;
+    auto first = [&](int x) { return ctx->order_split == 0 || (double)cost[x] >= split_at; };
+    auto mid = std::stable_partition(order.begin(), order.end(), first);
+    std::stable_sort(order.begin(), mid, [&](int x, int y) { return cost[x] > cost[y]; });
     // Automatic heavy tiles: the tiles whose walk length exceeds heavy_factor
     // times the bulk estimate, the total walk length spread over the device's
     // resident waves (kResidentPerCu per CU, measured).  A 1080p frame of
@@ -739,6 +751,7 @@ int rt_create(const int* device_ids, int n_devices, rt_ctx** out) {
     if (const char* v = std::getenv("RTAMD_HEAVY_FIRST")) ctx->heavy_first = std::atoi(v) ? 1 : 0;
     if (const char* v = std::getenv("RTAMD_HEAVY_TILES")) ctx->heavy_tiles = std::max(-1, std::atoi(v));
     if (const char* v = std::getenv("RTAMD_LEARN_COST")) ctx->learn_cost = std::atoi(v) ? 1 : 0;
+    if (const char* v = std::getenv("RTAMD_ORDER_SPLIT")) ctx->order_split = std::max(0, std::min(100, std::atoi(v)));
     if (const char* v = std::getenv("RTAMD_HEAVY_FACTOR")) ctx->heavy_factor = std::max(10, std::atoi(v));
     if (const char* v = std::getenv("RTAMD_HEAVY_STREAM")) ctx->heavy_stream = std::max(0, std::min(2, std::atoi(v)));
     if (const char* v = std::getenv("RTAMD_HEAVY_PIXELS")) ctx->heavy_pixels = std::atoi(v) ? 1 : 0;
@@ -1509,6 +1522,8 @@ int rt_set_option(rt_ctx* ctx, const char* name, int64_t value) {
         ctx->concurrent_launches = (int)value;
     } else if (std::strcmp(name, "learn_cost") == 0 && (value == 0 || value == 1)) {
         ctx->learn_cost = (int)value;
+    } else if (std::strcmp(name, "order_split") == 0 && value >= 0 && value <= 100) {
+        ctx->order_split = (int)value;
     } else if (std::strcmp(name, "heavy_stream") == 0 && value >= 0 && value <= 2) {
         ctx->heavy_stream = (int)value;
     } else if (std::strcmp(name, "graph") == 0 && (value == 0 || value == 1)) {
@@ -1537,6 +1552,7 @@ int rt_get_option(rt_ctx* ctx, const char* name, int64_t* value) {
     else if (std::strcmp(name, "heavy_stream") == 0) *value = ctx->heavy_stream;
     else if (std::strcmp(name, "graph") == 0) *value = ctx->graph;
     else if (std::strcmp(name, "learn_cost") == 0) *value = ctx->learn_cost;
+    else if (std::strcmp(name, "order_split") == 0) *value = ctx->order_split;
     else if (std::strcmp(name, "heavy_factor") == 0) *value = ctx->heavy_factor;
     else if (std::strcmp(name, "concurrent_launches") == 0) *value = ctx->concurrent_launches;
     else if (std::strcmp(name, "async_slots") == 0) *value = ctx->async_slots;

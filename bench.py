@@ -465,13 +465,19 @@ def main() -> None:
                 flush(timed=evs is not None)
         if dist_on:
             flush(timed=evs is not None)
+        elif F > 1:
+            st["k"] = ((st["k"] + G - 1) // G) * G           # the next phase starts a whole slot ring
 
     # ---- frame indices of the phases (fixed up front, so the counting pass
     # counts exactly the timed frames' cameras): a phase of n frames from
     # frame k ends at k + n, rounded up to a whole exchange batch at N > 1
     def after(k, n):
+        # phases start on a whole exchange batch (N > 1) or a whole slot ring
+        # (N = 1 with several frames per launch), so every timed launch has
+        # the same frame count and launch key (a new key learns, with a
+        # stream synchronisation)
         k += n
-        return ((k + G - 1) // G) * G if dist_on else k
+        return ((k + G - 1) // G) * G if (dist_on or F > 1) else k
 
     # ---- counting pass (untimed): the timed frames' work ------------------
     K = args.steps * step_frames                       # timed frames
@@ -711,7 +717,7 @@ def main() -> None:
                                                                       "heavy_first", "heavy_tiles", "heavy_factor",
                                                                       "heavy_stream", "heavy_pixels",
                                                                       "heavy_pixel_factor", "heavy_cap", "graph",
-                                                                      "reuse_order", "hw_queues")},
+                                                                      "reuse_order", "order_split", "hw_queues")},
                              "concurrent_launches": renderer.get_option("concurrent_launches"),
                              "heavy_tiles_used": heavy_used,
                              "heavy_pixels_used": heavy_px_used},

@@ -294,6 +294,11 @@ int rt_render_wait(rt_ctx* ctx, uint64_t ticket);
  *                   captured.  Same results.
  *   "learn_cost"    heavy_first order by 1 = wave duration (default) or 0 =
  *                   walk length
+ *   "order_split"   heavy_first: 0 = every tile in cost order; p in 1..100 =
+ *                   only the tiles costing at least p percent of the
+ *                   costliest go first (in cost order), the rest keep their
+ *                   raster order (frame by frame), which keeps the waves
+ *                   running at once on neighbouring tiles
  *   "heavy_tiles_used" (rt_get_option only) heavy tiles of the last launch
  *   "wave_tile"     pixels per wave (8<<s) x (8>>s), s = 0..3
  *                   (default 0: 8x8, the shader's local_size; with frames in

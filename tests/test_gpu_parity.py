@@ -17,7 +17,7 @@ COUNTERS = ("segments", "node_visits", "tri_tests", "mat_reads")
 DEFAULT_OPTS = {"wave_tile": 0, "coop_lanes": 1, "walk": 2, "coop_walk": 0,
                 "block_waves": 1, "heavy_first": 1, "heavy_tiles": -1, "heavy_stream": 2,
                 "learn_cost": 1, "heavy_factor": 130, "graph": 1, "concurrent_launches": 1, "heavy_cap": 75,
-                "heavy_pixels": 1, "heavy_pixel_factor": 50, "reuse_order": 1}
+                "heavy_pixels": 1, "heavy_pixel_factor": 50, "reuse_order": 1, "order_split": 0}
 
 
 def _oracle(built, cam_bytes, w, h, b, **kw):
@@ -124,6 +124,8 @@ def test_config5_1m_row_subset(renderer):
     {"coop_walk": 1},
     {"block_waves": 4},
     {"heavy_first": 0},
+    {"order_split": 20},
+    {"order_split": 100, "concurrent_launches": 4},
     {"graph": 0},
     {"graph": 0, "heavy_stream": 0},
     {"walk": 0},
