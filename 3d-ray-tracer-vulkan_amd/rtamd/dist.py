@@ -140,6 +140,33 @@ def piece_owners(height: int, band_h: int, world: int) -> np.ndarray:
     return (np.arange(n) * world) // n if n else np.zeros(0, np.int64)
 
 
+def weighted_pieces(height: int, band_h: int, world: int, frame: int, root_weight: float):
+    """Frame `frame`'s contiguous pieces, rank by rank (band index arrays):
+    position p belongs to rank (p - frame) mod world; rank 0's piece has
+    round(root_weight x n / (world - 1 + root_weight)) of the n bands, the
+    other ranks share the rest as evenly as whole bands allow (the earlier
+    positions one band more)."""
+    n = (height + band_h - 1) // band_h
+    s0 = int(round(max(0.0, root_weight) * n / (world - 1 + max(0.0, root_weight)))) if world > 1 else n
+    s0 = min(s0, n)
+    rest = n - s0
+    sizes, k = [], 0
+    for p in range(world):
+        r = (p - frame) % world
+        if r == 0:
+            sizes.append(s0)
+        else:
+            sizes.append(rest // (world - 1) + (1 if k < rest % (world - 1) else 0))
+            k += 1
+    out = [None] * world
+    b = 0
+    for p in range(world):
+        r = (p - frame) % world
+        out[r] = np.arange(b, b + sizes[p], dtype=np.int32)
+        b += sizes[p]
+    return out
+
+
 class SharePlan:
     """Row bookkeeping of a batch of n_frames frames over world ranks in
     weighted bands.  Rank r's exchange buffer holds its shares of the batch's
@@ -152,19 +179,23 @@ class SharePlan:
     rank r traces the bands of position (r + f) mod world, so over world
     frames every rank traces every band once.
 
-    layout="pieces" (weak scaling, bench.py --partition pieces; rotates, weights
-    1): the positions are world contiguous pieces of the frame (piece_owners),
-    so a launch of world consecutive frames holds every piece once, each of a
-    different frame: one whole frame's rows with a whole frame's spatial
-    coherence.  Frames sit at a fixed stride of max_rows rows (off[r][f] =
-    f * max_rows), as rt_render_batch_lists_device writes per-frame lists
-    padded to the longest piece; launch_lists gives those lists."""
+    layout="pieces" (weak scaling, bench.py --partition pieces; rotates): the
+    positions are world contiguous pieces of the frame (piece_owners), rank r
+    tracing position (r + f) mod world in frame f, so a launch of world
+    consecutive frames holds every piece once, each of a different frame: one
+    whole frame's rows with a whole frame's spatial coherence.  With
+    root_weight w < 1 rank 0's piece is w times the others' (weighted_pieces):
+    the cut points then move with rank 0's piece from frame to frame, so over
+    world frames a rank r > 0 covers every position with pieces of one size.
+    Frames sit at a fixed stride of max_rows rows (off[r][f] = f * max_rows),
+    as rt_render_batch_lists_device writes per-frame lists padded to the
+    longest piece; launch_lists gives those lists."""
 
     def __init__(self, height: int, band_h: int, world: int, n_frames: int, root_weight: float = 1.0,
                  rotate: bool = False, layout: str = "interleave"):
         if layout == "pieces":
             rotate = True
-        if rotate and root_weight != 1.0:
+        elif rotate and root_weight != 1.0:
             raise ValueError("rotating bands take equal weights")
         if layout not in ("interleave", "pieces"):
             raise ValueError(f"unknown layout {layout!r}")
@@ -177,8 +208,13 @@ class SharePlan:
         self.bands = self.pos_bands                    # rank r's bands (rotate=False)
         self.rows = self.pos_rows
         self.counts = [len(x) for x in self.pos_rows]
-        self.max_rows = max(self.counts)
-        self.n_per = max(len(b) for b in self.pos_bands)   # list length of a piece launch
+        # weighted pieces: rank r's bands in frame f (mod world), a table
+        self.wtable = None
+        if layout == "pieces" and root_weight != 1.0:
+            self.wtable = [weighted_pieces(height, band_h, world, f, root_weight) for f in range(world)]
+            self.counts = [len(list_rows(height, band_h, self.wtable[0][r])) for r in range(world)]
+        self.max_rows = max(len(self.frame_rows(r, f)) for r in range(world) for f in range(min(world, n_frames)))
+        self.n_per = max(len(self.frame_bands(r, f)) for r in range(world) for f in range(min(world, n_frames)))
         self.off = [[0] * n_frames for _ in range(world)]
         self.per_rank = 0
         for r in range(world):
@@ -198,9 +234,13 @@ class SharePlan:
         return (rank + frame) % self.world if self.rotate else rank
 
     def frame_bands(self, rank: int, frame: int) -> np.ndarray:
+        if self.wtable is not None:
+            return self.wtable[frame % self.world][rank]
         return self.pos_bands[self.position(rank, frame)]
 
     def frame_rows(self, rank: int, frame: int) -> np.ndarray:
+        if self.wtable is not None:
+            return list_rows(self.height, self.band_h, self.wtable[frame % self.world][rank])
         return self.pos_rows[self.position(rank, frame)]
 
     def launch_lists(self, rank: int, frame0: int, n: int) -> np.ndarray:

@@ -144,6 +144,12 @@ def default_root_weight(world: int) -> float:
     return 1.0 if world <= 2 else (0.85 if world <= 4 else 0.7)
 
 
+def default_piece_weight(world: int) -> float:
+    """pieces: rank 0's piece relative to the others' (its receive and
+    assembly of every frame are work the other ranks do not do)."""
+    return 1.0
+
+
 def camera_path(cfg, kind: str, n: int, first: int = 0):
     """The cameras of frames first .. first + n - 1."""
     from rtamd import configs
@@ -306,7 +312,8 @@ def main() -> None:
     if mode in ("bands", "pieces"):
         rw = args.root_weight if args.root_weight >= 0 else default_root_weight(world)
         plan = SharePlan(H, band_h, world, G, rw) if mode == "bands" else \
-            SharePlan(H, band_h, world, G, 1.0, layout="pieces")
+            SharePlan(H, band_h, world, G, rw if args.root_weight >= 0 else default_piece_weight(world),
+                      layout="pieces")
         src_index = torch.as_tensor(plan.src, device=dev)
         my_bands = [np.ascontiguousarray(plan.frame_bands(rank, f)) for f in range(G)]
         rgba_slots = torch.empty((R, plan.per_rank, W, 4), dtype=torch.uint8, device=dev)
@@ -673,8 +680,9 @@ def main() -> None:
                     f"(rank 0 weight {plan.root_weight}, rows per rank {plan.counts}), {D} launches in flight x "
                     f"{F} frames per launch, {gather_kind} gather of every {G} frames + rank-0 assembly{shared}")
         elif mode == "pieces":
-            part = (f"every frame cut into {world} contiguous pieces of {band_h}-row bands (rows {plan.counts}), "
-                    f"rank r tracing piece (r + f) mod {world} of frame f, {D} launches in flight x {F} frames per "
+            part = (f"every frame cut into {world} contiguous pieces of {band_h}-row bands (rows {plan.counts}, "
+                    f"rank 0 weight {plan.root_weight}), rank r tracing position (r + f) mod {world} of frame f, {D} "
+                    f"launches in flight x {F} frames per "
                     f"launch (one band list per frame), {gather_kind} gather of every {G} frames + rank-0 "
                     f"assembly{shared}")
         elif mode == "tiles":

@@ -20,4 +20,10 @@ b() { local tag=$1; shift; timeout -k 10 300 python bench.py --no-cpu-baseline -
 b f8d2 --batch 8 --inflight 2
 b f8d4 --batch 8 --inflight 4
 b f8d2_nohf --batch 8 --inflight 2 --set heavy_first=0
-echo done > $O/done.txt
+
+# weighted pieces: rank 0's piece smaller (its receive + assembly)
+e pw9 8 "0 1" --partition pieces --root-weight 0.9
+e pw8 8 "0 1" --partition pieces --root-weight 0.8
+e pw8_20 8 "0 1" --partition pieces --root-weight 0.8 --steps 20
+e b_20 8 "0 1" --partition bands --steps 20
+echo done2 > $O/done2.txt

@@ -287,8 +287,8 @@ def _share_worker(rank, world, port, q, kind, arg, n_frames, W, H, B):
         elif kind == "pieces":
             # rt_render_batch_lists_device's packing: one launch of all the
             # batch's frames, list position k of frame f at rows off + k * band_h
-            band_h = arg
-            plan = SharePlan(H, band_h, world, n_frames, layout="pieces")
+            band_h, rw = arg
+            plan = SharePlan(H, band_h, world, n_frames, rw, layout="pieces")
             rgba = torch.zeros((plan.per_rank, W, 4), dtype=torch.uint8)
             rad = torch.zeros((plan.per_rank, W, 3), dtype=torch.float32)
             lists = plan.launch_lists(rank, 0, n_frames)
@@ -385,16 +385,22 @@ def test_rotating_bands_weak_scaling_8_ranks():
     assert set(traced.values()) == {48 * 40}
 
 
-@pytest.mark.parametrize("world,n_frames,band_h", [(8, 8, 4), (3, 6, 4), (2, 2, 8)])
-def test_rotating_pieces_weak_scaling(world, n_frames, band_h):
+@pytest.mark.parametrize("world,n_frames,band_h,rw", [(8, 8, 4, 1.0), (3, 6, 4, 1.0), (2, 2, 8, 1.0),
+                                                      (4, 8, 2, 0.7), (8, 8, 2, 0.85)])
+def test_rotating_pieces_weak_scaling(world, n_frames, band_h, rw):
     """--partition pieces (bench.py's weak-scaling partition): every frame cut
     into world contiguous pieces of whole bands (sizes differ by a band), rank
     r tracing piece (r + f) mod world of frame f, all the batch's frames in
     one launch with one band list per frame (-1 padded to the longest piece,
     rt_render_batch_lists_device's packing); one gather and one index_select:
     every frame and its radiance equal the oracle's, and over world frames
-    every rank traced exactly one frame's worth of rows."""
+    every rank traced exactly one frame's worth of rows; with a root weight
+    below 1 (rank 0's piece smaller, the cut points moving with it) rank 0
+    traced less than every other rank."""
     W, H = 48, 40
-    traced = _run_share(world, "pieces", band_h, n_frames=n_frames, W=W, H=H, B=2)
+    traced = _run_share(world, "pieces", (band_h, rw), n_frames=n_frames, W=W, H=H, B=2)
     assert sum(traced.values()) == n_frames * W * H
-    assert set(traced.values()) == {n_frames // world * W * H}
+    if rw == 1.0:
+        assert set(traced.values()) == {n_frames // world * W * H}
+    else:
+        assert traced[0] < min(traced[r] for r in range(1, world))
