@@ -326,6 +326,7 @@ struct rt_ctx {
     int  concurrent_launches = 1;  // launches of similar work the caller keeps in flight on a device at once
                                    //   (the heavy-tile bulk estimate counts this launch's work that many times)
     int  learn_cost = 1;           // heavy_first cost: 0 = lockstep steps + 2 x coop windows, 1 = wave duration
+    int  learn_alone = 0;          // heavy_first: a learning launch first waits for the device to drain
     int  order_split = 0;          // heavy_first: only tiles costing >= this percent of the costliest go first
                                    //   (in cost order); the rest keep their raster order (0 = all by cost)
     int  graph = 1;                // kernel 0 plain launches: replay a captured HIP graph per launch key
@@ -490,6 +491,10 @@ static int plan_order(const rt_ctx* ctx, PerDevice& p, TraceArgs& a, const rt_ca
     }
     p.learning_key = key;
     p.learning_n = n;
+    // Option learn_alone: the learning launch waits for the device to drain,
+    // so its wave durations (the order's cost) are not those of waves that
+    // shared the GPU with other launches in flight at that moment.
+    if (ctx->learn_alone) RT_HIP_CHECK(hipDeviceSynchronize());
     a.diag = p.d_learn;                // the diagnostic build counts each wave's lockstep steps
     a.diag_lane = p.d_learn_lane;      // and each pixel's own walk length
     return RT_OK;
@@ -1524,6 +1529,8 @@ int rt_set_option(rt_ctx* ctx, const char* name, int64_t value) {
         ctx->learn_cost = (int)value;
     } else if (std::strcmp(name, "order_split") == 0 && value >= 0 && value <= 100) {
         ctx->order_split = (int)value;
+    } else if (std::strcmp(name, "learn_alone") == 0 && (value == 0 || value == 1)) {
+        ctx->learn_alone = (int)value;
     } else if (std::strcmp(name, "heavy_stream") == 0 && value >= 0 && value <= 2) {
         ctx->heavy_stream = (int)value;
     } else if (std::strcmp(name, "graph") == 0 && (value == 0 || value == 1)) {
@@ -1553,6 +1560,7 @@ int rt_get_option(rt_ctx* ctx, const char* name, int64_t* value) {
     else if (std::strcmp(name, "graph") == 0) *value = ctx->graph;
     else if (std::strcmp(name, "learn_cost") == 0) *value = ctx->learn_cost;
     else if (std::strcmp(name, "order_split") == 0) *value = ctx->order_split;
+    else if (std::strcmp(name, "learn_alone") == 0) *value = ctx->learn_alone;
     else if (std::strcmp(name, "heavy_factor") == 0) *value = ctx->heavy_factor;
     else if (std::strcmp(name, "concurrent_launches") == 0) *value = ctx->concurrent_launches;
     else if (std::strcmp(name, "async_slots") == 0) *value = ctx->async_slots;

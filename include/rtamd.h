@@ -294,6 +294,9 @@ int rt_render_wait(rt_ctx* ctx, uint64_t ticket);
  *                   captured.  Same results.
  *   "learn_cost"    heavy_first order by 1 = wave duration (default) or 0 =
  *                   walk length
+ *   "learn_alone"   heavy_first: 1 = a learning launch first waits for the
+ *                   device to drain (its wave durations then are not inflated
+ *                   by other launches in flight); 0 (default) = it does not
  *   "order_split"   heavy_first: 0 = every tile in cost order; p in 1..100 =
  *                   only the tiles costing at least p percent of the
  *                   costliest go first (in cost order), the rest keep their
