@@ -275,6 +275,24 @@ def gather_shares(local, plan: SharePlan, group=None, src_index=None, n_frames: 
     stack on rank 0 and one index_select; returns the [n_frames, height, W, C]
     frames on rank 0 (the first n_frames of the batch, default all), None
     elsewhere."""
+    stack = gather_stack(local, plan, group)
+    return None if stack is None else assemble_shares(stack, plan, src_index, n_frames)
+
+
+def assemble_shares(stack, plan: SharePlan, src_index=None, n_frames: int = None):
+    """Rank 0's frames from the gathered [world, per_rank, W, C] stack: one
+    index_select (it may run on another stream than the gather)."""
+    import torch
+    if src_index is None:
+        src_index = torch.as_tensor(plan.src, device=stack.device)
+    n = plan.n_frames if n_frames is None else n_frames
+    out = torch.index_select(stack.reshape(plan.world * plan.per_rank, -1), 0, src_index[: n * plan.height])
+    return out.reshape((n, plan.height) + tuple(stack.shape[2:]))
+
+
+def gather_stack(local, plan: SharePlan, group=None):
+    """The gather half of gather_shares: every rank's buffer into one
+    [world, per_rank, W, C] stack on rank 0 (None elsewhere)."""
     import torch
     import torch.distributed as dist
     if local.shape[0] != plan.per_rank:
@@ -293,13 +311,7 @@ def gather_shares(local, plan: SharePlan, group=None, src_index=None, n_frames: 
                 d.copy_(h)
     else:
         dist.gather(local, gl, dst=0, group=group)
-    if rank != 0:
-        return None
-    if src_index is None:
-        src_index = torch.as_tensor(plan.src, device=local.device)
-    n = plan.n_frames if n_frames is None else n_frames
-    out = torch.index_select(stack.reshape(plan.world * plan.per_rank, -1), 0, src_index[: n * plan.height])
-    return out.reshape((n, plan.height) + tuple(local.shape[1:]))
+    return stack if rank == 0 else None
 
 
 # --- a tile grid (BASELINE config 4: the screen tiled 2 x 2 over 4 GPUs) ----

@@ -205,6 +205,10 @@ def main() -> None:
     ap.add_argument("--exchange-priority", type=int, default=1,
                     help="N > 1: 1 = the collective's stream and the assembly stream at high priority, so the "
                          "exchange is not starved of workgroup slots by the traces in flight")
+    ap.add_argument("--assembly-priority", choices=("high", "normal"), default="high",
+                    help="N > 1, bands / pieces: the rank-0 assembly (index_select) on the exchange stream at high "
+                         "priority, or on a normal-priority stream of its own that a ring slot's reuse does not wait "
+                         "for")
     ap.add_argument("--set", default="", help="schedule options name=value,... (rt_set_option) before timing")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-single", action="store_true", help="N > 1: skip rank 0's one-GPU timing")
@@ -224,7 +228,7 @@ def main() -> None:
     import rtamd
     from rtamd import configs
     from rtamd._lib import CameraUBO, Stats, check
-    from rtamd.dist import SharePlan, TilePlan, gather_shares, gather_tiles
+    from rtamd.dist import SharePlan, TilePlan, assemble_shares, gather_stack, gather_tiles
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -339,6 +343,7 @@ def main() -> None:
     hi = -1 if (dist_on and args.exchange_priority) else 0    # the assembly (index_select) at high priority
     main_stream = torch.cuda.Stream(dev, priority=hi)
     torch.cuda.set_stream(main_stream)
+    asm_stream = torch.cuda.Stream(dev) if args.assembly_priority == "normal" else main_stream
     # The heavy-pixel bar counts the launches of similar work on the device at
     # once: the D launches in flight.
     renderer.set_option("concurrent_launches", D)
@@ -402,6 +407,17 @@ def main() -> None:
     last = {"rgba": None, "rad": None, "frames": []}
     ex_evs = []            # (start, end) events of the timed region's exchanges
 
+    def assemble(stack, n):
+        """Rank 0's frames from a gathered stack, on the assembly stream."""
+        if stack is None:
+            return None
+        if asm_stream is main_stream:
+            return assemble_shares(stack, plan, src_index, n)
+        asm_stream.wait_stream(main_stream)
+        stack.record_stream(asm_stream)
+        with torch.cuda.stream(asm_stream):
+            return assemble_shares(stack, plan, src_index, n)
+
     def flush(timed=False):
         """Exchange the frames of the current batch traced so far (N > 1)."""
         k = st["k"]
@@ -423,7 +439,7 @@ def main() -> None:
                 out = None
             elif rank == 0:
                 dist.gather(emu_buf, [emu_land])
-                out = torch.index_select(emu_land.reshape(world * plan.per_rank, -1), 0, src_index[: n * H])
+                out = assemble(emu_land.reshape(world, plan.per_rank, -1), n)
             else:
                 dist.gather(rgba_slots[h], [emu_land])
                 out = None
@@ -434,13 +450,15 @@ def main() -> None:
             if out is not None:
                 out, rad = out[:n], (rad[:n] if rad is not None else None)
         else:
-            out = gather_shares(rgba_slots[h], plan, src_index=src_index, n_frames=n)
-            rad = gather_shares(rad_slots[h], plan, src_index=src_index, n_frames=n) if rad_on else None
+            stk = gather_stack(rgba_slots[h], plan)
+            stk_r = gather_stack(rad_slots[h], plan) if rad_on else None
+            out = assemble(stk, n)
+            rad = assemble(stk_r, n)
         if timed:
             e1.record(main_stream)
             ex_evs.append((e0, e1))
         ev = torch.cuda.Event()
-        ev.record(main_stream)
+        ev.record(main_stream)                        # the slots are free once the gather has read them
         gathered[h] = ev
         last["rgba"], last["rad"] = out, rad
         last["frames"] = list(range(k - n, k))
@@ -561,6 +579,8 @@ def main() -> None:
     phase(K, evs)
     for s in streams:
         main_stream.wait_stream(s)
+    if asm_stream is not main_stream:
+        main_stream.wait_stream(asm_stream)
     reg[1].record(main_stream)
     torch.cuda.synchronize(dev)
     if dist_on:

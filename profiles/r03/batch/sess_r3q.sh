@@ -23,4 +23,8 @@ e w90_20 2 "0 1" --steps 20 --root-weight 0.9 --set order_split=15
 e w100_20_alone 2 "0 1" --steps 20 --root-weight 1.0 --set order_split=15,learn_alone=1
 e w100_20_f4 2 "0 1" --steps 20 --root-weight 1.0 --set order_split=15 --batch 4
 e w100_200 2 "0 1" --steps 200 --root-weight 1.0 --set order_split=15
+e asmn_w65 8 "0" --steps 200 --root-weight 0.65 --set order_split=15 --assembly-priority normal
+e asmn_w65_20 8 "0" --steps 20 --root-weight 0.65 --set order_split=15 --assembly-priority normal
+e asmn_w80 8 "0" --steps 200 --root-weight 0.8 --set order_split=15 --assembly-priority normal
+bash tools/rehearse.sh $O/rehearse 8 pieces --steps 20 --warmup 5 --root-weight 0.65 --set order_split=15 --assembly-priority normal || exit $?
 echo done > $O/done.txt
