@@ -202,9 +202,10 @@ def main() -> None:
     ap.add_argument("--gather", choices=("rgba", "radiance"), default="rgba",
                     help="N > 1: radiance = gather the float radiance beside the RGBA8 frame")
     ap.add_argument("--camera-path", choices=("static", "orbit"), default="static")
-    ap.add_argument("--exchange-priority", type=int, default=1,
+    ap.add_argument("--exchange-priority", type=int, default=1, choices=(0, 1, 2),
                     help="N > 1: 1 = the collective's stream and the assembly stream at high priority, so the "
-                         "exchange is not starved of workgroup slots by the traces in flight")
+                         "exchange is not starved of workgroup slots by the traces in flight; 2 = on rank 0 only "
+                         "(the senders' copies wait for slots); 0 = normal priority")
     ap.add_argument("--assembly-priority", choices=("high", "normal"), default="high",
                     help="N > 1, bands / pieces: the rank-0 assembly (index_select) on the exchange stream at high "
                          "priority, or on a normal-priority stream of its own that a ring slot's reuse does not wait "
@@ -253,7 +254,8 @@ def main() -> None:
     if dist_on:
         backend = os.environ.get("BENCH_DIST_BACKEND", "nccl")     # nccl = RCCL over xGMI
         pg_options = None
-        if backend == "nccl" and args.exchange_priority:
+        prio_rank = int(emu.split(":")[1]) if emu else rank     # the (emulated) rank
+        if backend == "nccl" and (args.exchange_priority == 1 or (args.exchange_priority == 2 and prio_rank == 0)):
             # RCCL's internal stream at high priority: with traces in flight
             # every CU slot is taken, and a normal-priority collective gets
             # slots only as trace waves end
@@ -340,7 +342,8 @@ def main() -> None:
         emu_buf = torch.zeros((world * plan.per_rank, W, 4) if rank == 0 else (1,), dtype=torch.uint8, device=dev)
         emu_land = torch.empty_like(emu_buf if rank == 0 else rgba_slots[0])
     streams = [torch.cuda.Stream(dev) for _ in range(D)]
-    hi = -1 if (dist_on and args.exchange_priority) else 0    # the assembly (index_select) at high priority
+    # the exchange's own stream (and rank 0's assembly) at high priority
+    hi = -1 if (dist_on and (args.exchange_priority == 1 or (args.exchange_priority == 2 and rank == 0))) else 0
     main_stream = torch.cuda.Stream(dev, priority=hi)
     torch.cuda.set_stream(main_stream)
     asm_stream = torch.cuda.Stream(dev) if args.assembly_priority == "normal" else main_stream
@@ -406,6 +409,10 @@ def main() -> None:
     gathered = [None] * R
     last = {"rgba": None, "rad": None, "frames": []}
     ex_evs = []            # (start, end) events of the timed region's exchanges
+    ev_pool = []           # timing events created (and their HIP events made) before the timed region
+
+    def timing_event():
+        return ev_pool.pop() if ev_pool else torch.cuda.Event(enable_timing=True)
 
     def assemble(stack, n):
         """Rank 0's frames from a gathered stack, on the assembly stream."""
@@ -430,7 +437,7 @@ def main() -> None:
         batch_streams.clear()
         e0 = e1 = None
         if timed:
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0, e1 = timing_event(), timing_event()
             e0.record(main_stream)
         if emu and mode in ("bands", "pieces"):
             # the exchange volume of rank `rank` of `world`, through a world-size-1 gather
@@ -478,7 +485,7 @@ def main() -> None:
                 batch_streams.append(s)
             rp, dp = out_ptrs(k0, j)
             if evs is not None:
-                e = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                e = (timing_event(), timing_event())
                 e[0].record(s)
             trace(k0, n, s, rp, dp)
             if evs is not None:
@@ -567,11 +574,21 @@ def main() -> None:
     phase(W_fr)
     torch.cuda.synchronize(dev)
     assert st["k"] == k_t0, (st["k"], k_t0)
+    evs = []
+    # the timed launches' and exchanges' events, created and recorded once here:
+    # torch makes the HIP event at its first record, which would otherwise be
+    # host time between the timed region's first launches
+    for _ in range(2 * (K // F + 2) + (2 * (K // G + 2) if dist_on else 0)):
+        e = torch.cuda.Event(enable_timing=True)
+        e.record(main_stream)
+        ev_pool.append(e)
+    reg = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+    reg[0].record(main_stream)
+    reg[1].record(main_stream)
+    torch.cuda.synchronize(dev)
     if dist_on:
         dist.barrier()
     torch.cuda.synchronize(dev)
-    evs = []
-    reg = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
     t_start = time.perf_counter()
     reg[0].record(main_stream)
     for s in streams:
