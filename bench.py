@@ -140,8 +140,19 @@ def default_batch(world: int, weak: bool = False) -> int:
 def default_root_weight(world: int) -> float:
     """bands: rank 0's weight in the band deal (the others weigh 1).  Rank 0
     also receives the other ranks' shares of every frame and assembles the
-    frame, device work the other ranks do not do."""
-    return 1.0 if world <= 2 else (0.85 if world <= 4 else 0.7)
+    frame, device work the other ranks do not do (at the
+    driver's 20 steps rank 0 weighted 0.7 of 8 finished 10% before the
+    others, 1.0 of 2 5% after: profiles/r03/batch/r3s)."""
+    if world == 1:
+        return 1.0
+    return 0.9 if world == 2 else (0.85 if world <= 4 else 0.8)
+
+
+# N > 1: only the tiles costing at least this percentage of the costliest go
+# first in the heavy-first order, the rest keep their raster order (rt option
+# order_split; a rank's batched launch of band shares runs faster with the
+# waves at once on neighbouring tiles, DESIGN.md §4; neutral at N = 1)
+ORDER_SPLIT_N_GT_1 = 15
 
 
 def default_piece_weight(world: int) -> float:
@@ -275,6 +286,8 @@ def main() -> None:
 
     renderer = rtamd.Renderer((dev_index,))
     renderer.upload_scene(built)
+    if dist_on:
+        renderer.set_option("order_split", ORDER_SPLIT_N_GT_1)
     for kv in filter(None, args.set.split(",")):
         k, v = kv.split("=")
         renderer.set_option(k.strip(), int(v))
