@@ -12,8 +12,8 @@ Partitions of a frame over the N ranks:
   packed bands to rank 0, which assembles the frames with one index_select.
   root_weight 1 is the plain interleave: rank r gets the bands b = r mod N
   (band_rows, gather_frame, gather_frames);
-* rotating contiguous pieces (SharePlan layout "pieces"; bench.py's weak
-  scaling default): the frame cut into N contiguous pieces of whole bands; in
+* rotating contiguous pieces (SharePlan layout "pieces"; bench.py --partition
+  pieces, an option): the frame cut into N contiguous pieces of whole bands; in
   frame f rank r traces piece (r + f) mod N, and a launch of N consecutive
   frames (rt_render_batch_lists_device, one band list per frame) holds every
   piece once, each of a different frame, so every rank traces one whole

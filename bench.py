@@ -22,7 +22,10 @@ high priority (--exchange-priority).
   weighted round robin (rank 0 weighted --root-weight: it also receives and
   assembles every frame; rtamd.dist.band_owners).  A rank traces its bands of
   F frames per launch (rt_render_batch_device; weak: F = N, the step), D
-  launches in flight.
+  launches in flight; heavy-first order with option order_split 15.
+--partition pieces: N contiguous row pieces, rank r tracing position
+  (r + f) mod N of frame f, all N pieces of a launch from different frames
+  (rt_render_batch_lists_device).
 --partition tiles: the screen tiled gx x gy over the ranks (2 x 2 at N = 4,
   BASELINE config 4), one tile per rank, gathered and assembled likewise.
 --gather radiance: the float radiance (the sqrt'd colour before

@@ -388,7 +388,7 @@ def test_rotating_bands_weak_scaling_8_ranks():
 @pytest.mark.parametrize("world,n_frames,band_h,rw", [(8, 8, 4, 1.0), (3, 6, 4, 1.0), (2, 2, 8, 1.0),
                                                       (4, 8, 2, 0.7), (8, 8, 2, 0.85)])
 def test_rotating_pieces_weak_scaling(world, n_frames, band_h, rw):
-    """--partition pieces (bench.py's weak-scaling partition): every frame cut
+    """--partition pieces (bench.py's weak-scaling option): every frame cut
     into world contiguous pieces of whole bands (sizes differ by a band), rank
     r tracing piece (r + f) mod world of frame f, all the batch's frames in
     one launch with one band list per frame (-1 padded to the longest piece,
