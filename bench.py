@@ -52,8 +52,8 @@ instructions (the texture addresser / data path), not by HBM
 bandwidth (the 8-MB scene stays in L2 / MALL).  bound "vmem_issue":
 achieved = SQ_INSTS_VMEM_RD per launch (PMC, tools/pmc.sh, committed in
 profiles/pmc_latest.json for this config) / frame_ms_device, the device time
-per launch of the running loop (HIP events around the timed region on the
-main stream after joining every launch stream, divided by the launches); peak
+per launch of the running loop (HIP events from before the first launch to
+the last event of every stream, divided by the launches); peak
 = CUs / TA_NS_PER_VMEM, the measured floor of one wave-level
 global_load_dwordx4 per CU (tools/ubench/ta_cost.hip,
 profiles/r02/walks/ubench_ta_cost.txt:1); frac = achieved / peak.  Beside it:
@@ -76,6 +76,7 @@ from __future__ import annotations
 
 import argparse
 import ctypes as C
+import gc
 import json
 import math
 import os
@@ -224,6 +225,10 @@ def main() -> None:
                     help="N > 1, bands / pieces: the rank-0 assembly (index_select) on the exchange stream at high "
                          "priority, or on a normal-priority stream of its own that a ring slot's reuse does not wait "
                          "for")
+    ap.add_argument("--bracket", choices=("lean", "join"), default="lean",
+                    help="timed region: lean = the launch streams start right after the device synchronisation "
+                         "and the closing device synchronisation joins them; join = they also wait on / are joined "
+                         "into the main stream around the region (two cross-queue hops)")
     ap.add_argument("--set", default="", help="schedule options name=value,... (rt_set_option) before timing")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-single", action="store_true", help="N > 1: skip rank 0's one-GPU timing")
@@ -594,7 +599,7 @@ def main() -> None:
     # the timed launches' and exchanges' events, created and recorded once here:
     # torch makes the HIP event at its first record, which would otherwise be
     # host time between the timed region's first launches
-    for _ in range(2 * (K // F + 2) + (2 * (K // G + 2) if dist_on else 0)):
+    for _ in range(2 * (K // F + 2) + (2 * (K // G + 2) if dist_on else 0) + D + 2):
         e = torch.cuda.Event(enable_timing=True)
         e.record(main_stream)
         ev_pool.append(e)
@@ -605,24 +610,40 @@ def main() -> None:
     if dist_on:
         dist.barrier()
     torch.cuda.synchronize(dev)
+    lean = args.bracket == "lean"
+    gc.collect()
+    gc.disable()                                       # no collector pause between the timed launches
     t_start = time.perf_counter()
-    reg[0].record(main_stream)
-    for s in streams:
-        s.wait_stream(main_stream)
+    if lean:
+        # the device is idle: the first launch's stream starts the region, and
+        # every stream's last event (launches, exchanges, assembly) ends it
+        reg[0].record(streams[0])
+    else:
+        reg[0].record(main_stream)
+        for s in streams:
+            s.wait_stream(main_stream)
     phase(K, evs)
-    for s in streams:
-        main_stream.wait_stream(s)
-    if asm_stream is not main_stream:
-        main_stream.wait_stream(asm_stream)
-    reg[1].record(main_stream)
+    if lean:
+        ends = [timing_event() for _ in streams] + ([timing_event()] if asm_stream is not main_stream else [])
+        for e, s in zip(ends, streams + ([asm_stream] if asm_stream is not main_stream else [])):
+            e.record(s)
+        ends.append(timing_event())
+        ends[-1].record(main_stream)
+    else:
+        for s in streams:
+            main_stream.wait_stream(s)
+        if asm_stream is not main_stream:
+            main_stream.wait_stream(asm_stream)
+        reg[1].record(main_stream)
     torch.cuda.synchronize(dev)
     if dist_on:
         dist.barrier()
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t_start
+    gc.enable()
     n_launch = len(evs)
     launch_ms = float(np.mean([a.elapsed_time(b) for (a, b), _ in evs]))
-    region_ms = reg[0].elapsed_time(reg[1])
+    region_ms = (max(reg[0].elapsed_time(e) for e in ends) if lean else reg[0].elapsed_time(reg[1]))
     frame_ms = region_ms / n_launch                    # device time per launch of the running loop
     ivs = sorted((reg[0].elapsed_time(a), reg[0].elapsed_time(b)) for (a, b), _ in evs)
     busy, cs, ce = 0.0, None, None
@@ -797,8 +818,10 @@ def main() -> None:
                 "frame_ms_device_max_over_ranks": round(frame_ms_max, 4) if dist_on else None,
                 "launches_in_flight_avg": round(launch_ms / frame_ms, 2),
                 "events": "kernel_ms: each launch's own stream, around every launch (after its wait for the "
-                          "exchange); frame_ms_device: main stream around the timed region after joining every "
-                          "launch stream, / launches",
+                          "exchange); frame_ms_device: from an event before the first launch to the last event of "
+                          "every stream (bracket lean) or main stream around the region after joining every launch "
+                          "stream (bracket join), / launches",
+                "bracket": args.bracket,
             },
             "per_rank": per_rank,
             "primary_mrays_s": round(pixels / elapsed / 1e6, 2),
