@@ -234,6 +234,9 @@ def main() -> None:
     ap.add_argument("--no-single", action="store_true", help="N > 1: skip rank 0's one-GPU timing")
     ap.add_argument("--no-pcie", action="store_true", help="N = 1: skip the PCIe-inclusive rt_render_async rate")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU baseline sample time")
+    ap.add_argument("--settle-max", type=int, default=100, help="at most this many settle launches")
+    ap.add_argument("--pcie-warm", type=int, default=200,
+                    help="untimed frames before the PCIe-inclusive rate (8: 0.41 ms per frame, 200: 0.345; r3z)")
     ap.add_argument("--settle-s", type=float, default=0.2,
                     help="untimed frames before the warmup steps: this many seconds of counting-pass time "
                          "(5-100 frames; steady clocks and caches)")
@@ -308,7 +311,7 @@ def main() -> None:
     # profiles/r03/emulation/r3l pipeline.jsonl vs bench20_pcie.json).
     pcie = None
     if rank == 0 and not dist_on and args.camera_path == "static" and not args.no_pcie:
-        pcie = pcie_rate(renderer, cfg.camera(), W, H, B)
+        pcie = pcie_rate(renderer, cfg.camera(), W, H, B, warm=args.pcie_warm)
 
     # ---- partition -------------------------------------------------------
     mode = args.partition if dist_on else "whole"
@@ -555,7 +558,7 @@ def main() -> None:
     # over the ranks, so every rank runs the same collectives.
     _, ms0 = count_frames([0])
     est_ms = max(0.05, float(ms0[0]) * F)                  # a launch's counting time
-    n_settle = torch.tensor([max(5, 2 * D, min(100, int(args.settle_s * 1e3 / est_ms)))], dtype=torch.int64,
+    n_settle = torch.tensor([max(5, 2 * D, min(args.settle_max, int(args.settle_s * 1e3 / est_ms)))], dtype=torch.int64,
                             device=dev)
     if dist_on:
         dist.all_reduce(n_settle, op=dist.ReduceOp.MIN)
@@ -847,7 +850,7 @@ def main() -> None:
         dist.destroy_process_group()
 
 
-def pcie_rate(renderer, cam, W, H, B, n=200):
+def pcie_rate(renderer, cam, W, H, B, n=200, warm=8):
     """rt_render_async: 4 frames in flight into pinned host frames, every frame
     read back over PCIe (tools/pipeline_bench.py's async mode)."""
     from rtamd.engine import PinnedFrame
@@ -857,7 +860,7 @@ def pcie_rate(renderer, cam, W, H, B, n=200):
     frames = [PinnedFrame(H, W) for _ in range(S)]
     try:
         pend = []
-        for j in range(2 * S):                       # learns / warms up
+        for j in range(max(2 * S, warm)):            # learns / warms up
             pend.append(renderer.render_async(cam, W, H, B, frames[j % S]))
             if len(pend) == S:
                 renderer.wait(pend.pop(0))
