@@ -237,7 +237,7 @@ def main() -> None:
     ap.add_argument("--settle-max", type=int, default=100, help="at most this many settle launches")
     ap.add_argument("--pcie-warm", type=int, default=200,
                     help="untimed frames before the PCIe-inclusive rate (8: 0.41 ms per frame, 200: 0.345; r3z)")
-    ap.add_argument("--settle-s", type=float, default=0.2,
+    ap.add_argument("--settle-s", type=float, default=0.4,
                     help="untimed frames before the warmup steps: this many seconds of counting-pass time "
                          "(5-100 frames; steady clocks and caches)")
     ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_latest.json"),
@@ -593,12 +593,6 @@ def main() -> None:
         f"{G if dist_on else '-'} frames")
 
     # ---- settle, warmup, timed ---------------------------------------------
-    phase(n_settle)
-    torch.cuda.synchronize(dev)
-    phase(W_fr)
-    torch.cuda.synchronize(dev)
-    assert st["k"] == k_t0, (st["k"], k_t0)
-    evs = []
     # the timed launches' and exchanges' events, created and recorded once here:
     # torch makes the HIP event at its first record, which would otherwise be
     # host time between the timed region's first launches
@@ -609,12 +603,21 @@ def main() -> None:
     reg = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
     reg[0].record(main_stream)
     reg[1].record(main_stream)
+    # Settle, then warm up, then time with no host work in between: the GPU's
+    # launches slow down after it idles (a frame's kernel ran 1.35 ms at the
+    # start of the settle, 1.16-1.20 ms after ~50 launches, and 1.29-1.31 ms
+    # again after a 69 ms host pause before the timed region:
+    # profiles/r03/r3f/prof3, kernel trace)
+    phase(n_settle)
     torch.cuda.synchronize(dev)
+    phase(W_fr)
+    torch.cuda.synchronize(dev)
+    assert st["k"] == k_t0, (st["k"], k_t0)
+    evs = []
     if dist_on:
         dist.barrier()
     torch.cuda.synchronize(dev)
     lean = args.bracket == "lean"
-    gc.collect()
     gc.disable()                                       # no collector pause between the timed launches
     t_start = time.perf_counter()
     if lean:
