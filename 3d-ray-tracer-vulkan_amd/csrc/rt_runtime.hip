@@ -329,6 +329,8 @@ struct rt_ctx {
     int  learn_alone = 0;          // heavy_first: a learning launch first waits for the device to drain
     int  order_split = 0;          // heavy_first: only tiles costing >= this percent of the costliest go first
                                    //   (in cost order); the rest keep their raster order (0 = all by cost)
+    int  order_frames = 0;         // heavy_first, several frames per launch: the non-leading tiles row by row
+                                   //   across the frames (0 = frame by frame)
     int  graph = 1;                // kernel 0 plain launches: replay a captured HIP graph per launch key
     int  heavy_stream = 2;         // heavy_tiles: 1 = their launch runs on an auxiliary stream, concurrent
                                    //   with the other tiles; 2 = their workgroups come first in the
@@ -391,7 +393,7 @@ static int plan_order(const rt_ctx* ctx, PerDevice& p, TraceArgs& a, const rt_ca
     std::vector<int> geo = {a.width, a.height, a.max_bounces, a.x0, a.y0, a.tw, a.th, a.band_h, a.band_stride,
                             a.band_off, a.wave_tile, a.ext, a.coop_lanes, a.walk, ctx->learn_cost, ctx->order_split,
                             ctx->heavy_factor, concurrency(ctx), ctx->heavy_cap, ctx->heavy_pixel_factor,
-                            a.n_frames, bands ? (int)bands->size() : -1, a.list_stride};
+                            a.n_frames, bands ? (int)bands->size() : -1, a.list_stride, ctx->order_frames};
     if (bands) geo.insert(geo.end(), bands->begin(), bands->end());
     const size_t g = geo.size() * sizeof(int), c = (size_t)a.n_frames * sizeof(rt_camera_ubo);
     std::vector<uint8_t> key(g + c + sizeof(uint64_t));
@@ -533,6 +535,20 @@ static int learn_order(const rt_ctx* ctx, PerDevice& p, const TraceArgs& a, hipS
     auto first = [&](int x) { return ctx->order_split == 0 || (double)cost[x] >= split_at; };
     auto mid = std::stable_partition(order.begin(), order.end(), first);
     std::stable_sort(order.begin(), mid, [&](int x, int y) { return cost[x] > cost[y]; });
+    // Option order_frames (a launch of several frames): the rest go row by
+    // row across the launch's frames (tile row y of frame 0, of frame 1, ...,
+    // then row y + 1), so the waves running at once trace the same part of
+    // the image in every frame of the batch instead of the rows of one or two
+    // frames spread over a rank's band share.
+    if (ctx->order_frames && a.n_frames > 1) {
+        const int tw_w = 8 << a.wave_tile, th_w = 8 >> a.wave_tile;
+        const long tx = (a.tw + tw_w - 1) / tw_w, ty = (a.th + th_w - 1) / th_w;
+        auto key = [&](int k) {
+            const long by = k / tx, f = by / ty, row = by % ty;
+            return (row * a.n_frames + f) * tx + k % tx;
+        };
+        std::stable_sort(mid, order.end(), [&](int x, int y) { return key(x) < key(y); });
+    }
     // Automatic heavy tiles: the tiles whose walk length exceeds heavy_factor
     // times the bulk estimate, the total walk length spread over the device's
     // resident waves (kResidentPerCu per CU, measured).  A 1080p frame of
@@ -1527,6 +1543,8 @@ int rt_set_option(rt_ctx* ctx, const char* name, int64_t value) {
         ctx->concurrent_launches = (int)value;
     } else if (std::strcmp(name, "learn_cost") == 0 && (value == 0 || value == 1)) {
         ctx->learn_cost = (int)value;
+    } else if (std::strcmp(name, "order_frames") == 0 && (value == 0 || value == 1)) {
+        ctx->order_frames = (int)value;
     } else if (std::strcmp(name, "order_split") == 0 && value >= 0 && value <= 100) {
         ctx->order_split = (int)value;
     } else if (std::strcmp(name, "learn_alone") == 0 && (value == 0 || value == 1)) {
@@ -1573,6 +1591,7 @@ int rt_get_option(rt_ctx* ctx, const char* name, int64_t* value) {
     else if (std::strcmp(name, "heavy_tiles_used") == 0) *value = ctx->dev.empty() ? 0 : ctx->dev[0].last_heavy;
     else if (std::strcmp(name, "extensions") == 0) *value = ctx->ext;
     else if (std::strcmp(name, "hw_queues") == 0) *value = ctx->hw_queues;
+    else if (std::strcmp(name, "order_frames") == 0) *value = ctx->order_frames;
     // 1 when rt_render_async's slots cannot each have a hardware queue of their
     // own (async_slots + 2 > hw_queues: the slots' traces then share queues and
     // run one after another); start the host with GPU_MAX_HW_QUEUES >= slots + 2

@@ -302,6 +302,10 @@ int rt_render_wait(rt_ctx* ctx, uint64_t ticket);
  *                   costliest go first (in cost order), the rest keep their
  *                   raster order (frame by frame), which keeps the waves
  *                   running at once on neighbouring tiles
+ *   "order_frames"  heavy_first, launches of several frames (the batch entry
+ *                   points): 1 = the tiles after the leading ones go row by
+ *                   row across the launch's frames (the same image rows of
+ *                   every frame run at once); 0 (default) = frame by frame
  *   "heavy_tiles_used" (rt_get_option only) heavy tiles of the last launch
  *   "wave_tile"     pixels per wave (8<<s) x (8>>s), s = 0..3
  *                   (default 0: 8x8, the shader's local_size; with frames in

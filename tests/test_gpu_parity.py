@@ -17,7 +17,8 @@ COUNTERS = ("segments", "node_visits", "tri_tests", "mat_reads")
 DEFAULT_OPTS = {"wave_tile": 0, "coop_lanes": 1, "walk": 2, "coop_walk": 0,
                 "block_waves": 1, "heavy_first": 1, "heavy_tiles": -1, "heavy_stream": 2,
                 "learn_cost": 1, "heavy_factor": 130, "graph": 1, "concurrent_launches": 1, "heavy_cap": 75,
-                "heavy_pixels": 1, "heavy_pixel_factor": 50, "reuse_order": 1, "order_split": 0}
+                "heavy_pixels": 1, "heavy_pixel_factor": 50, "reuse_order": 1, "order_split": 0,
+                "order_frames": 0}
 
 
 def _oracle(built, cam_bytes, w, h, b, **kw):
@@ -696,14 +697,16 @@ def _batch_device(renderer, cams, w, h, b, band_h=0, bands=None, radiance=True, 
     return d_rgba.cpu().numpy(), (d_rad.cpu().numpy() if radiance else None), s.as_dict()
 
 
-@pytest.mark.parametrize("cfg_k,band_h,world,rw,rank", [(3, 8, 8, 0.7, 0), (3, 8, 8, 0.7, 5), (2, 16, 4, 1.0, 3),
-                                                       (6, 8, 4, 0.85, 1)])
-def test_batch_band_list_bit_exact(renderer, cfg_k, band_h, world, rw, rank):
+@pytest.mark.parametrize("cfg_k,band_h,world,rw,rank,opts", [
+    (3, 8, 8, 0.7, 0, {}), (3, 8, 8, 0.7, 5, {}), (2, 16, 4, 1.0, 3, {}), (6, 8, 4, 0.85, 1, {}),
+    (3, 8, 8, 0.8, 1, {"order_split": 15, "order_frames": 1}), (2, 16, 4, 1.0, 0, {"order_frames": 1})])
+def test_batch_band_list_bit_exact(renderer, cfg_k, band_h, world, rw, rank, opts):
     """rt_render_batch_device: one launch traces a rank's weighted band share
     (rtamd.dist.band_owners) of 3 frames with 3 different cameras; the
     learning launch, a counting launch and a plain launch in the learned
-    order each give every frame's rows of the oracle's frame, bit for bit,
-    and the counts of those rows."""
+    order (also with the order's rows interleaved across the frames,
+    order_frames) each give every frame's rows of the oracle's frame, bit
+    for bit, and the counts of those rows."""
     from rtamd import configs
     from rtamd.dist import band_list, list_rows
     cfg = configs.get(cfg_k)
@@ -727,6 +730,8 @@ def test_batch_band_list_bit_exact(renderer, cfg_k, band_h, world, rw, rank):
                 tot[k] += cb[k]
     try:
         renderer.set_option("concurrent_launches", 4)
+        for k, v in opts.items():
+            renderer.set_option(k, v)
         for stats in (False, True, False):
             rgba, rad, st = _batch_device(renderer, cams, W, H, B, band_h, bands, stats=stats)
             for f in range(3):
