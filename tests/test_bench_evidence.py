@@ -1,0 +1,87 @@
+"""CPU checks of bench.py's host-side arithmetic against the committed evidence.
+
+The roofline in a bench.py JSON line must follow from the files under
+profiles/: SQ_INSTS_VMEM_RD per launch (rocprofv3 --pmc, pass A) over the
+line's device time per launch against CUs / TA_NS_PER_VMEM, and the HBM bytes
+from FETCH_SIZE (pass C).  The rocprofv3 kernel trace's union of the timed
+launches must agree with ms_per_step.  No GPU: these read JSON and CSV files.
+"""
+import csv
+import json
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+EVID = os.path.join(ROOT, "profiles", "r03", "evidence_r3fin")
+sys.path.insert(0, ROOT)
+
+import bench  # noqa: E402  (module level: argparse-free helpers, no torch)
+
+
+def _line(name):
+    with open(os.path.join(EVID, name)) as fh:
+        return json.loads([x for x in fh if x.startswith("{")][-1])
+
+
+def _pmc_mean(path, counter, kernel="trace_simple<false, false, 72, 2>"):
+    vals = [float(r["Counter_Value"]) for r in csv.DictReader(open(path))
+            if r["Counter_Name"] == counter and kernel in r["Kernel_Name"]]
+    assert vals, (path, counter)
+    return sum(vals) / len(vals)
+
+
+@pytest.mark.parametrize("name", ["bench.json", "bench200.json", "prof3.json"])
+def test_roofline_reproduces_from_profiles(name):
+    d = _line(name)
+    r = d["roofline"]
+    # the PMC record the line was computed from (profiles/pmc_latest.json at the time)
+    src = os.path.join(ROOT, r["pmc_source"].split(" ")[0])
+    vmem = _pmc_mean(os.path.join(src, "A_counter_collection.csv"), "SQ_INSTS_VMEM_RD")
+    fetch = _pmc_mean(os.path.join(src, "C_counter_collection.csv"), "FETCH_SIZE")
+    # the same kernel and config measured again in the final session's passes
+    again = _pmc_mean(os.path.join(EVID, "pmc3", "A_counter_collection.csv"), "SQ_INSTS_VMEM_RD")
+    assert again == pytest.approx(vmem, rel=0.01)
+    assert r["vmem_rd_per_launch"] == pytest.approx(vmem, rel=1e-6)
+    t = r["frame_ms_device"] * 1e-3
+    peak = 256 / bench.TA_NS_PER_VMEM
+    assert r["bound"] == "vmem_issue"
+    assert r["peak"] == pytest.approx(peak, abs=1e-3)
+    assert r["frac"] == pytest.approx(vmem / t / 1e9 / peak, rel=2e-3)   # frame_ms_device is rounded to 4 digits
+    hbm = fetch * 1024 * 2                                          # gfx950: 64-B halves, KiB
+    assert r["traffic"] == pytest.approx(hbm, rel=1e-6)
+    assert r["hbm"]["frac"] == pytest.approx(hbm / t / 1e9 / bench.HBM_PEAK_GBS, rel=2e-3)
+    assert 0.0 < r["frac"] < 1.0 and 0.0 < r["hbm"]["frac"] < 1.0
+
+
+def test_value_is_segments_over_wall_time():
+    for name in ("bench.json", "bench200.json"):
+        d = _line(name)
+        seg = d["config"]["segments_per_frame"] * d["steps"]
+        assert d["value"] == pytest.approx(seg / (d["ms_per_step"] * d["steps"] * 1e-3) / 1e6, rel=2e-3)
+        assert d["metric"] == bench.BASELINE["metric"] and d["n_gpus"] == 1 and d["unit"] == "Mrays/s"
+        cpu = d["cpu_baseline"]
+        assert cpu["kind"] == "port" and cpu["cores"] >= 1 and cpu["value"] > 0
+
+
+@pytest.mark.parametrize("cfg", [3, 5])
+def test_rocprof_union_agrees_with_ms_per_step(cfg):
+    u = json.load(open(os.path.join(EVID, f"union_cfg{cfg}.json")))
+    assert u["launches"] == u["frames"]
+    assert u["union_ms_per_frame"] == pytest.approx(u["bench_ms_per_step"], rel=0.05)
+    # the mean launch agrees with the rocprofv3 stats of the same run
+    with open(os.path.join(EVID, f"kernel_stats_cfg{cfg}.csv")) as fh:
+        rows = [r for r in csv.DictReader(fh) if "trace_simple<false, false" in r["Name"]]
+    assert rows
+    avg_ms = float(rows[0]["AverageNs"]) / 1e6
+    assert avg_ms == pytest.approx(u["launch_ms_mean"], rel=0.05)
+
+
+def test_default_schedule_helpers():
+    assert bench.default_inflight(1) == 4
+    assert bench.default_batch(1) == 1
+    for n in (2, 4, 8):
+        assert bench.default_batch(n, weak=True) == n
+        assert 0.5 < bench.default_root_weight(n) < 1.0
+    assert bench.default_root_weight(1) == 1.0
