@@ -118,6 +118,33 @@ def band_owners(height: int, band_h: int, world: int, root_weight: float = 1.0) 
     return owner
 
 
+def dealt_bands(height: int, band_h: int, world: int, root_weight: float = 1.0) -> list:
+    """The weighted round robin of band_owners run on over world consecutive
+    frames (the credits carry from one frame into the next): table[f][r] is
+    rank r's bands of frame f mod world.  Within a frame a rank's count
+    differs from its weighted share by under a band, as with band_owners; over
+    the world frames every rank's total is within one band of
+    world x its share, so a launch of world frames (weak scaling) gives every
+    rank other than 0 the same work to a band, where a fixed deal gives some
+    of them a whole band per frame more (at 1080 rows, N = 8, root weight
+    0.8: 18 bands to ranks 1-2, 17 to ranks 3-7)."""
+    n = (height + band_h - 1) // band_h
+    w = np.ones(world, np.float64)
+    w[0] = max(0.0, float(root_weight))
+    total = w.sum()
+    credit = np.zeros(world, np.float64)
+    table = []
+    for _ in range(world):
+        owner = np.empty(n, np.int64)
+        for b in range(n):
+            credit += w
+            r = int(np.argmax(credit))
+            owner[b] = r
+            credit[r] -= total
+        table.append([np.flatnonzero(owner == r).astype(np.int32) for r in range(world)])
+    return table
+
+
 def band_list(height: int, band_h: int, world: int, rank: int, root_weight: float = 1.0) -> np.ndarray:
     """rank's band indices, increasing (rt_render_batch_device's list)."""
     return np.flatnonzero(band_owners(height, band_h, world, root_weight) == rank).astype(np.int32)
@@ -189,16 +216,22 @@ class SharePlan:
     world frames a rank r > 0 covers every position with pieces of one size.
     Frames sit at a fixed stride of max_rows rows (off[r][f] = f * max_rows),
     as rt_render_batch_lists_device writes per-frame lists padded to the
-    longest piece; launch_lists gives those lists."""
+    longest piece; launch_lists gives those lists.
+
+    layout="dealt" (weak scaling, bench.py --partition bands --deal rotate):
+    weighted interleaved bands dealt on over world frames (dealt_bands), one
+    band list per frame, packed like the pieces (lists, max_rows stride)."""
 
     def __init__(self, height: int, band_h: int, world: int, n_frames: int, root_weight: float = 1.0,
                  rotate: bool = False, layout: str = "interleave"):
-        if layout == "pieces":
+        if layout in ("pieces", "dealt"):
             rotate = True
         elif rotate and root_weight != 1.0:
             raise ValueError("rotating bands take equal weights")
-        if layout not in ("interleave", "pieces"):
+        if layout not in ("interleave", "pieces", "dealt"):
             raise ValueError(f"unknown layout {layout!r}")
+        # per-frame band lists (rt_render_batch_lists_device), frames at a max_rows stride
+        self.lists = layout in ("pieces", "dealt")
         self.height, self.band_h, self.world, self.n_frames = height, band_h, world, n_frames
         self.root_weight, self.rotate, self.layout = root_weight, rotate, layout
         owner = piece_owners(height, band_h, world) if layout == "pieces" else \
@@ -213,6 +246,11 @@ class SharePlan:
         if layout == "pieces" and root_weight != 1.0:
             self.wtable = [weighted_pieces(height, band_h, world, f, root_weight) for f in range(world)]
             self.counts = [len(list_rows(height, band_h, self.wtable[0][r])) for r in range(world)]
+        elif layout == "dealt":
+            self.wtable = dealt_bands(height, band_h, world, root_weight)
+            # rows per frame, averaged over the world frames of the deal
+            self.counts = [sum(len(list_rows(height, band_h, self.wtable[f][r])) for f in range(world)) // world
+                           for r in range(world)]
         self.max_rows = max(len(self.frame_rows(r, f)) for r in range(world) for f in range(min(world, n_frames)))
         self.n_per = max(len(self.frame_bands(r, f)) for r in range(world) for f in range(min(world, n_frames)))
         self.off = [[0] * n_frames for _ in range(world)]
@@ -221,7 +259,7 @@ class SharePlan:
             o = 0
             for f in range(n_frames):
                 self.off[r][f] = o
-                o += self.max_rows if layout == "pieces" else len(self.frame_rows(r, f))
+                o += self.max_rows if self.lists else len(self.frame_rows(r, f))
             self.per_rank = max(self.per_rank, o)
         src = np.empty(n_frames * height, np.int64)
         for r in range(world):

@@ -205,6 +205,10 @@ def main() -> None:
                          "gathered (every rank traces one frame's worth per step; default); strong = a step is "
                          "one frame tiled over all ranks")
     ap.add_argument("--band", type=int, default=8, help="band height (rows) for N > 1 (8 = one wave-tile row)")
+    ap.add_argument("--deal", choices=("rotate", "fixed"), default="fixed",
+                    help="bands: rotate = the weighted deal runs on over N frames (one band list per frame, "
+                         "rtamd.dist.dealt_bands), so a launch of N frames gives every rank other than 0 the "
+                         "same rows to a band; fixed = the same bands in every frame")
     ap.add_argument("--root-weight", type=float, default=-1.0,
                     help="bands: rank 0's weight in the band deal, the others weigh 1 (-1 = default_root_weight)")
     ap.add_argument("--inflight", type=int, default=0, help="launches in flight per rank (0 = default_inflight)")
@@ -341,7 +345,8 @@ def main() -> None:
     my_bands = None
     if mode in ("bands", "pieces"):
         rw = args.root_weight if args.root_weight >= 0 else default_root_weight(world)
-        plan = SharePlan(H, band_h, world, G, rw) if mode == "bands" else \
+        plan = SharePlan(H, band_h, world, G, rw, layout="dealt" if args.deal == "rotate" else "interleave") \
+            if mode == "bands" else \
             SharePlan(H, band_h, world, G, rw if args.root_weight >= 0 else default_piece_weight(world),
                       layout="pieces")
         src_index = torch.as_tensor(plan.src, device=dev)
@@ -403,7 +408,7 @@ def main() -> None:
             cams = cam_arrays.get(ck)
             if cams is None:                          # built once per (frames, count): no host work per launch
                 cams = cam_arrays[ck] = (CameraUBO * n)(*[cam_of(k).ubo for k in range(k0, k0 + n)])
-            if mode == "pieces":                      # one band list per frame, built once per (frame, count)
+            if plan is not None and plan.lists:       # one band list per frame, built once per (frame, count)
                 pl = piece_lists.get((k0 % G, n))
                 if pl is None:
                     pl = piece_lists[(k0 % G, n)] = np.ascontiguousarray(plan.launch_lists(rank, k0 % G, n))
@@ -757,6 +762,7 @@ def main() -> None:
             part = f"one whole frame per step, {D} launches in flight, {F} frame(s) per launch"
         elif mode == "bands":
             part = (f"one frame per step in {band_h}-row bands dealt to {world} ranks by a weighted round robin "
+                    f"{'run on over ' + str(world) + ' frames (one band list per frame) ' if plan.lists else ''}"
                     f"(rank 0 weight {plan.root_weight}, rows per rank {plan.counts}), {D} launches in flight x "
                     f"{F} frames per launch, {gather_kind} gather of every {G} frames + rank-0 assembly{shared}")
         elif mode == "pieces":
@@ -798,6 +804,7 @@ def main() -> None:
                 "exchange_every_frames": G if dist_on else None,
                 "band_h": band_h if mode in ("bands", "pieces") else None,
                 "root_weight": plan.root_weight if plan is not None else None,
+                "deal": (("rotate" if plan.lists else "fixed") if mode == "bands" else None),
                 "gather": ("rgba8 + float radiance" if rad_on else "rgba8") if dist_on else None,
                 "frames_verified": verified,
                 "parallelism": f"{mode}{world}",

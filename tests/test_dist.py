@@ -284,11 +284,11 @@ def _share_worker(rank, world, port, q, kind, arg, n_frames, W, H, B):
                     traced += w * h
             out = gather_tiles(rgba, plan)
             outr = gather_tiles(rad, plan)
-        elif kind == "pieces":
+        elif kind in ("pieces", "dealt"):
             # rt_render_batch_lists_device's packing: one launch of all the
             # batch's frames, list position k of frame f at rows off + k * band_h
             band_h, rw = arg
-            plan = SharePlan(H, band_h, world, n_frames, rw, layout="pieces")
+            plan = SharePlan(H, band_h, world, n_frames, rw, layout=kind)
             rgba = torch.zeros((plan.per_rank, W, 4), dtype=torch.uint8)
             rad = torch.zeros((plan.per_rank, W, 3), dtype=torch.float32)
             lists = plan.launch_lists(rank, 0, n_frames)
@@ -404,3 +404,35 @@ def test_rotating_pieces_weak_scaling(world, n_frames, band_h, rw):
         assert set(traced.values()) == {n_frames // world * W * H}
     else:
         assert traced[0] < min(traced[r] for r in range(1, world))
+
+
+@pytest.mark.parametrize("world,n_frames,band_h,rw", [(8, 8, 2, 0.8), (4, 8, 2, 0.85), (3, 3, 4, 1.0)])
+def test_dealt_bands_weak_scaling(world, n_frames, band_h, rw):
+    """bench.py --partition bands --deal rotate: the weighted band deal runs
+    on over world frames (rtamd.dist.dealt_bands), one band list per frame
+    packed as rt_render_batch_lists_device writes them; one gather and one
+    index_select give every frame and its radiance bit for bit, and over world
+    frames the ranks other than 0 traced the same rows to within one band."""
+    W, H = 48, 40
+    traced = _run_share(world, "dealt", (band_h, rw), n_frames=n_frames, W=W, H=H, B=2)
+    assert sum(traced.values()) == n_frames * W * H
+    others = [traced[r] for r in range(1, world)]
+    assert max(others) - min(others) <= band_h * W * (n_frames // world)
+    if rw < 1.0:
+        assert traced[0] < min(others)
+
+
+def test_dealt_bands_balance_1080p():
+    """At 1080 rows in 8-row bands, N = 8, root weight 0.8: a fixed deal gives
+    ranks 1-2 18 bands a frame and ranks 3-7 17; dealt over 8 frames every rank
+    other than 0 gets 138-139 bands per 8 frames, and each frame's bands are
+    every band exactly once."""
+    from rtamd.dist import SharePlan, band_list
+    fixed = [len(band_list(1080, 8, 8, r, 0.8)) for r in range(8)]
+    assert max(fixed[1:]) == 18 and min(fixed[1:]) == 17
+    plan = SharePlan(1080, 8, 8, 32, 0.8, layout="dealt")
+    tot = [sum(len(plan.frame_bands(r, f)) for f in range(8)) for r in range(8)]
+    assert max(tot[1:]) - min(tot[1:]) <= 1 and max(tot[1:]) <= 139
+    for f in range(8):
+        allb = np.sort(np.concatenate([plan.frame_bands(r, f) for r in range(8)]))
+        assert np.array_equal(allb, np.arange(135))
