@@ -248,7 +248,7 @@ def main() -> None:
                     help="untimed frames before the PCIe-inclusive rate (8: 0.41 ms per frame, 200: 0.345; r3z)")
     ap.add_argument("--settle-s", type=float, default=0.4,
                     help="untimed frames before the warmup steps: this many seconds of counting-pass time "
-                         "(5-100 frames; steady clocks and caches)")
+                         "(5 to --settle-max launches; a GPU that has idled runs its first launches slower)")
     ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_latest.json"),
                     help="PMC per launch of each config (tools/pmc_traffic.py: SQ_INSTS_VMEM_RD, HBM bytes) for "
                          "the roofline")
