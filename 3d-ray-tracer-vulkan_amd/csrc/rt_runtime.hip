@@ -595,6 +595,8 @@ static int learn_order(const rt_ctx* ctx, PerDevice& p, const TraceArgs& a, hipS
         std::fprintf(stderr, "\n");
     }
     if (p.orders.size() >= kMaxOrders) {
+        // the oldest order may still steer a launch in flight on another stream
+        RT_HIP_CHECK(hipDeviceSynchronize());
         free_order(p.orders.front());
         p.orders.erase(p.orders.begin());
     }
@@ -634,7 +636,10 @@ static int set_schedule(const rt_ctx* ctx, PerDevice& p, TraceArgs& a, const rt_
         }
         const size_t need = (size_t)a.tw * (size_t)a.th * 3;
         if (need != p.accum_n) {                 // a new frame partition starts from zero sums
-            if (p.d_accum) (void)hipFree(p.d_accum);
+            if (p.d_accum) {
+                RT_HIP_CHECK(hipDeviceSynchronize());   // earlier frames in flight still add to the old sums
+                (void)hipFree(p.d_accum);
+            }
             p.d_accum = nullptr;
             p.accum_n = 0;
             RT_HIP_CHECK(hipMalloc(&p.d_accum, need * sizeof(float)));
@@ -653,7 +658,10 @@ static int set_schedule(const rt_ctx* ctx, PerDevice& p, TraceArgs& a, const rt_
         const size_t split = ctx->heavy_first ? (size_t)(ctx->heavy_tiles < 0 ? kMaxHeavy : ctx->heavy_tiles) * 63 : 0;
         const size_t words = (waves + split) * 8;
         if (words > p.diag_cap) {
-            if (p.d_diag) (void)hipFree(p.d_diag);
+            if (p.d_diag) {
+                RT_HIP_CHECK(hipDeviceSynchronize());   // diagnostic launches in flight still write it
+                (void)hipFree(p.d_diag);
+            }
             p.d_diag = nullptr;
             p.diag_cap = 0;
             RT_HIP_CHECK(hipMalloc(&p.d_diag, words * sizeof(unsigned long long)));
@@ -910,7 +918,12 @@ int rt_upload_scene(rt_ctx* ctx, const void* vertices, size_t vertex_bytes,
     ctx->has_scene = false;
     for (PerDevice& p : ctx->dev) {
         RT_HIP_CHECK(hipSetDevice(p.device));
-        RT_HIP_CHECK(hipStreamSynchronize(p.stream));   // like vkDeviceWaitIdle, VulkanEngine.java:321
+        // Like vkDeviceWaitIdle (VulkanEngine.java:321): every launch and copy
+        // still in flight on this device (rt_render_async's slot and copy
+        // streams, a caller's streams of the *_device calls, the heavy-tile
+        // streams) may read the old scene, so the whole device drains before
+        // its buffers are freed.
+        RT_HIP_CHECK(hipDeviceSynchronize());
         free_scene(p);
         DevScene s;
         s.n_nodes = hs.n_nodes;
@@ -978,7 +991,7 @@ int rt_upload_spheres(rt_ctx* ctx, const float* spheres, int n_spheres) {
     }
     for (PerDevice& p : ctx->dev) {
         RT_HIP_CHECK(hipSetDevice(p.device));
-        RT_HIP_CHECK(hipStreamSynchronize(p.stream));
+        RT_HIP_CHECK(hipDeviceSynchronize());            // frames in flight may read the old spheres
         if (p.d_spheres) (void)hipFree(p.d_spheres);
         p.d_spheres = nullptr;
         p.n_spheres = 0;
@@ -1160,7 +1173,6 @@ static int collect_stats(const rt_ctx* ctx, PerDevice& p, uint64_t pixels, rt_st
     (void)ctx;
     Counters c;
     RT_HIP_CHECK(hipMemcpy(&c, p.d_counters, sizeof c, hipMemcpyDeviceToHost));
-    const unsigned handoffs = 0;   // the schedules with a second pass are archived (round 3)
     float ms = 0.f;
     RT_HIP_CHECK(hipEventElapsedTime(&ms, p.ev0, p.ev1));
     if (!accumulate) std::memset(stats, 0, sizeof *stats);
@@ -1169,7 +1181,6 @@ static int collect_stats(const rt_ctx* ctx, PerDevice& p, uint64_t pixels, rt_st
     stats->node_visits += c.node_visits;
     stats->tri_tests += c.tri_tests;
     stats->mat_reads += c.mat_reads;
-    stats->handoffs += handoffs;
     if (ms > stats->ms) stats->ms = ms;
     return RT_OK;
 }
@@ -1476,28 +1487,67 @@ int rt_render_async(rt_ctx* ctx, const rt_camera_ubo* cam, int width, int height
     return RT_OK;
 }
 
-int rt_render_wait(rt_ctx* ctx, uint64_t ticket) {
-    if (!ctx) { set_error("rt_render_wait: null context"); return RT_ERR_INVALID_ARG; }
+// The events that cover frame `ticket` on device p.  Copies complete in
+// ticket order on copy_stream, so the copy event of the slot with the smallest
+// ticket >= this one covers it (e1; null: the device has no rows of that
+// frame, and copy_stream itself is waited on).  A split frame's second half
+// runs in ticket order on copy_stream2, so the copied2 event of the slot with
+// the smallest SPLIT ticket >= this one covers it (e2; the requested frame's
+// own when its slot still holds it), not the newest split frame's, which
+// would wait for every later frame in flight.  If no slot holds a split frame
+// >= ticket any more but one was issued, the newest split event (kept until
+// it is re-recorded) covers it.
+static void cover_events(const PerDevice& p, uint64_t ticket, hipEvent_t* e1, hipEvent_t* e2) {
+    int best = -1, best2 = -1;
+    for (int k2 = 0; k2 < kMaxSlots; ++k2) {
+        if (p.slot_ticket[k2] < ticket) continue;
+        if (best < 0 || p.slot_ticket[k2] < p.slot_ticket[best]) best = k2;
+        if (p.slot_split[k2] && (best2 < 0 || p.slot_ticket[k2] < p.slot_ticket[best2])) best2 = k2;
+    }
+    *e1 = best >= 0 ? p.copied[best] : nullptr;
+    *e2 = best2 >= 0 ? p.copied2[best2]
+                     : (p.last_split_t >= ticket && p.last_split_slot >= 0 ? p.copied2[p.last_split_slot] : nullptr);
+}
+
+static int check_ticket(const rt_ctx* ctx, uint64_t ticket, const char* fn) {
     if (ticket == 0 || ticket > ctx->issued) {
-        set_error("rt_render_wait: ticket %llu was not issued (last %llu)", (unsigned long long)ticket,
+        set_error("%s: ticket %llu was not issued (last %llu)", fn, (unsigned long long)ticket,
                   (unsigned long long)ctx->issued);
         return RT_ERR_INVALID_ARG;
     }
-    // Copies complete in ticket order, so the copy event of any slot whose
-    // last ticket is >= this one covers it (the oldest such slot waits least).
+    return RT_OK;
+}
+
+int rt_render_wait(rt_ctx* ctx, uint64_t ticket) {
+    if (!ctx) { set_error("rt_render_wait: null context"); return RT_ERR_INVALID_ARG; }
+    if (int rc = check_ticket(ctx, ticket, "rt_render_wait")) return rc;
     for (PerDevice& p : ctx->dev) {
         RT_HIP_CHECK(hipSetDevice(p.device));
-        int best = -1;
-        for (int k2 = 0; k2 < kMaxSlots; ++k2)
-            if (p.slot_ticket[k2] >= ticket && (best < 0 || p.slot_ticket[k2] < p.slot_ticket[best])) best = k2;
-        if (best >= 0) RT_HIP_CHECK(hipEventSynchronize(p.copied[best]));
-        else RT_HIP_CHECK(hipStreamSynchronize(p.copy_stream));   // a device with no rows of that frame
-        // A split frame's second half is on copy_stream2, in ticket order: the
-        // newest split frame's event covers every split frame up to it (it may
-        // over-wait for a frame that did not split, never under-wait).
-        if (p.last_split_t >= ticket && p.last_split_slot >= 0)
-            RT_HIP_CHECK(hipEventSynchronize(p.copied2[p.last_split_slot]));
+        hipEvent_t e1, e2;
+        cover_events(p, ticket, &e1, &e2);
+        if (e1) RT_HIP_CHECK(hipEventSynchronize(e1));
+        else RT_HIP_CHECK(hipStreamSynchronize(p.copy_stream));
+        if (e2) RT_HIP_CHECK(hipEventSynchronize(e2));
     }
+    return RT_OK;
+}
+
+int rt_render_poll(rt_ctx* ctx, uint64_t ticket, int* done) {
+    if (!ctx || !done) { set_error("rt_render_poll: null argument"); return RT_ERR_INVALID_ARG; }
+    if (int rc = check_ticket(ctx, ticket, "rt_render_poll")) return rc;
+    *done = 0;
+    for (PerDevice& p : ctx->dev) {
+        RT_HIP_CHECK(hipSetDevice(p.device));
+        hipEvent_t e1, e2;
+        cover_events(p, ticket, &e1, &e2);
+        for (int k = 0; k < 2; ++k) {
+            const hipError_t q = k == 0 ? (e1 ? hipEventQuery(e1) : hipStreamQuery(p.copy_stream))
+                                        : (e2 ? hipEventQuery(e2) : hipSuccess);
+            if (q == hipErrorNotReady) return RT_OK;
+            RT_HIP_CHECK(q);
+        }
+    }
+    *done = 1;
     return RT_OK;
 }
 

@@ -315,12 +315,17 @@ struct rt_mesh {
 namespace {
 
 // strtoul10_64 (fast_atof.h): decimal digits into a uint64; with max_digits,
-// stops after that many digits and skips the rest.  Overflow returns 0 and
-// leaves the cursor where it was.
-uint64_t ai_strtoul10_64(const char* in, const char** out, unsigned* max_inout) {
+// stops after that many digits and skips the rest.  No digit at all: Assimp
+// throws (*bad = true here).  Overflow returns 0 and leaves the cursor where
+// it was (Assimp logs a warning and carries on).
+uint64_t ai_strtoul10_64(const char* in, const char** out, unsigned* max_inout, bool* bad = nullptr) {
     unsigned cur = 0;
     uint64_t value = 0;
     const char* p = in;
+    if (*p < '0' || *p > '9') {
+        if (bad) *bad = true;
+        return 0;
+    }
     while (*p >= '0' && *p <= '9') {
         const uint64_t nv = value * 10 + (uint64_t)(*p - '0');
         if (nv < value) { if (out) *out = in; return 0; }
@@ -373,7 +378,9 @@ bool ai_fast_atof(const char* c, float* out) {
         ++c;
         const bool einv = (*c == '-');
         if (einv || *c == '+') ++c;
-        float e = (float)ai_strtoul10_64(c, &c, nullptr);
+        bool bad = false;
+        float e = (float)ai_strtoul10_64(c, &c, nullptr, &bad);
+        if (bad) return false;                      // "1e": no exponent digits, Assimp throws
         if (einv) e = -e;
         f *= std::pow(10.0f, e);
     }
@@ -531,10 +538,23 @@ int rt_mesh_load_obj(const char* path, rt_mesh** out) {
                 tok.emplace_back(p, e);
                 p = e;
             }
-            float c[4] = {0.f, 0.f, 0.f, 1.f};
-            const size_t n = tok.size();
-            bool ok = n == 3 || n == 4 || n == 6;
-            for (size_t k = 0; ok && k < (n == 4 ? 4u : 3u); ++k) ok = ai_fast_atof(tok[k].c_str(), &c[k]);
+            // ObjFileParser::getNumComponentsInDataDefinition: only the tokens
+            // that start like a number count (ParsingUtils.h IsNumeric: a
+            // digit, '-' or '+'; or nan / inf), so a trailing comment does not;
+            // 3, 4 or 6 read that many words in order (getVector3 /
+            // getHomogeneousVector3 / getTwoVectors3, the colour parsed and
+            // dropped); any other count adds no vertex at all.
+            size_t n = 0;
+            for (const std::string& t : tok) {
+                const char* q = t.c_str();
+                if ((*q >= '0' && *q <= '9') || *q == '-' || *q == '+' || strncasecmp(q, "nan", 3) == 0 ||
+                    strncasecmp(q, "inf", 3) == 0)
+                    ++n;
+            }
+            if (n != 3 && n != 4 && n != 6) continue;
+            float c[6] = {0.f, 0.f, 0.f, 1.f, 0.f, 0.f};
+            bool ok = true;
+            for (size_t k = 0; ok && k < n; ++k) ok = ai_fast_atof(tok[k].c_str(), &c[k]);
             if (ok && n == 4) {
                 if (c[3] == 0.f) ok = false;                    // Assimp: division by zero
                 else { c[0] /= c[3]; c[1] /= c[3]; c[2] /= c[3]; }

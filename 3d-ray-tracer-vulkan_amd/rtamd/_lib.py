@@ -34,6 +34,7 @@ EXPORTED = (
     "rt_scene_validate", "rt_set_option", "rt_get_option", "rt_diag_copy",
     "rt_host_alloc", "rt_host_free", "rt_render_async", "rt_render_wait", "rt_upload_spheres",
     "rt_render_batch_device", "rt_band_list_rows", "rt_render_batch_lists_device", "rt_band_lists_rows",
+    "rt_render_poll",
 )
 
 
@@ -59,13 +60,12 @@ class CameraUBO(C.Structure):
 
 class Stats(C.Structure):
     _fields_ = [
-        ("pixels", C.c_uint64),
         ("segments", C.c_uint64),
         ("node_visits", C.c_uint64),
         ("tri_tests", C.c_uint64),
         ("mat_reads", C.c_uint64),
         ("ms", C.c_double),
-        ("handoffs", C.c_uint64),
+        ("pixels", C.c_uint64),
     ]
 
     def as_dict(self) -> dict:
@@ -130,6 +130,7 @@ def lib() -> C.CDLL:
                 "rt_host_free": (None, [vp]),
                 "rt_render_async": (i32, [vp, C.POINTER(CameraUBO), i32, i32, i32, vp, C.POINTER(u64)]),
                 "rt_render_wait": (i32, [vp, u64]),
+                "rt_render_poll": (i32, [vp, u64, C.POINTER(i32)]),
             }
             for name, (res, args) in sig.items():
                 f = getattr(L, name)

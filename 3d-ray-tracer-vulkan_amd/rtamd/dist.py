@@ -399,6 +399,13 @@ def gather_tiles(local, plan: TilePlan, group=None, src_index=None):
     """local: this rank's [n_frames, hmax * wmax, C] tiles (each packed at the
     start of its row).  Returns the [n_frames, height, width, C] frames on
     rank 0, None elsewhere."""
+    stack = gather_tile_stack(local, plan, group)
+    return None if stack is None else assemble_tiles(stack, plan, src_index)
+
+
+def gather_tile_stack(local, plan: TilePlan, group=None):
+    """The gather half of gather_tiles: every rank's tiles into one
+    [world, n_frames, hmax * wmax, C] stack on rank 0 (None elsewhere)."""
     import torch
     import torch.distributed as dist
     rank = dist.get_rank(group)
@@ -415,13 +422,88 @@ def gather_tiles(local, plan: TilePlan, group=None, src_index=None):
                 d.copy_(h)
     else:
         dist.gather(local, gl, dst=0, group=group)
-    if rank != 0:
-        return None
+    return stack if rank == 0 else None
+
+
+def assemble_tiles(stack, plan: TilePlan, src_index=None):
+    """Rank 0's [n_frames, height, width, C] frames from the gathered tile
+    stack: one index_select."""
+    import torch
     if src_index is None:
-        src_index = torch.as_tensor(plan.src, device=local.device)
-    c = local.shape[-1]
+        src_index = torch.as_tensor(plan.src, device=stack.device)
+    c = stack.shape[-1]
     out = torch.index_select(stack.reshape(-1, c), 0, src_index)
     return out.reshape(plan.n_frames, plan.height, plan.width, c)
+
+
+# --- one rank's launches (bench.py's trace) ----------------------------------
+
+
+class ShareTracer:
+    """The launches that trace one rank's share of frames, exactly as bench.py
+    issues them (and as tests/test_gpu_dist.py replays them):
+
+    * mode "whole": whole frames, n per launch (rt_render_batch_device, no list);
+    * mode "bands" / "pieces" with a SharePlan: the rank's band list of each
+      frame (one list for every frame of a launch, rt_render_batch_device; or
+      one list per frame when plan.lists, rt_render_batch_lists_device), packed
+      at plan.off[rank][f] of the rank's exchange buffer;
+    * mode "tiles" with a TilePlan: the rank's rectangle of one frame
+      (rt_render_tile_device).
+
+    Frame k of the run is frame k mod batch of the exchange batch (the plans'
+    frame index).  Band lists are built once per (frame, count), so a launch
+    does no host work beyond the ABI call."""
+
+    def __init__(self, ctx, width: int, height: int, max_bounces: int, mode: str, rank: int = 0,
+                 plan: Optional[SharePlan] = None, tplan: Optional[TilePlan] = None, band_h: int = 8,
+                 batch: int = 1):
+        if mode in ("bands", "pieces") and plan is None:
+            raise ValueError(f"mode {mode!r} needs a SharePlan")
+        if mode == "tiles" and tplan is None:
+            raise ValueError("mode 'tiles' needs a TilePlan")
+        if plan is not None and plan.lists and height % band_h:
+            # rt_render_batch_lists_device packs whole bands at a fixed stride
+            raise ValueError(f"per-frame band lists need band_h ({band_h}) to divide the height ({height})")
+        self.ctx, self.W, self.H, self.B = ctx, width, height, max_bounces
+        self.mode, self.rank, self.plan, self.tplan, self.band_h, self.G = mode, rank, plan, tplan, band_h, batch
+        self.my_bands = [np.ascontiguousarray(plan.frame_bands(rank, f), dtype=np.int32) for f in range(batch)] \
+            if plan is not None else None
+        self.rect = tplan.rects[rank] if tplan is not None else None
+        self._lists = {}
+
+    @staticmethod
+    def _i32p(a):
+        return a.ctypes.data_as(C.POINTER(C.c_int32)) if a is not None else None
+
+    def launch(self, cams, k0: int, n: int, stream: int, rgba_ptr, rad_ptr, stats=None) -> None:
+        """Frames k0 .. k0 + n - 1 (cams: a ctypes array of their n CameraUBO)
+        in one launch on `stream` (a HIP stream handle), into rgba_ptr /
+        rad_ptr (device pointers; rad_ptr may be None); stats: an rt_stats or
+        None."""
+        L = lib()
+        stp = C.byref(stats) if stats is not None else None
+        if self.mode == "tiles":
+            x0, y0, w, h = self.rect
+            check(L.rt_render_tile_device(self.ctx, C.byref(cams[0]), self.W, self.H, self.B, x0, y0, w, h,
+                                          rgba_ptr, rad_ptr, stream, stp))
+        elif self.plan is not None and self.plan.lists:
+            key = (k0 % self.G, n)
+            pl = self._lists.get(key)
+            if pl is None:
+                pl = self._lists[key] = np.ascontiguousarray(self.plan.launch_lists(self.rank, k0 % self.G, n))
+            check(L.rt_render_batch_lists_device(self.ctx, cams, n, self.W, self.H, self.B, self.band_h,
+                                                 self._i32p(pl), self.plan.n_per, rgba_ptr, rad_ptr, stream, stp))
+        else:
+            bl = self.my_bands[k0 % self.G] if self.my_bands is not None else None
+            check(L.rt_render_batch_device(self.ctx, cams, n, self.W, self.H, self.B,
+                                           self.band_h if bl is not None else 0, self._i32p(bl),
+                                           len(bl) if bl is not None else 0, rgba_ptr, rad_ptr, stream, stp))
+
+    def offset_rows(self, k0: int) -> int:
+        """Bands / pieces: the row of the rank's exchange buffer where frame
+        k0's share starts."""
+        return self.plan.off[self.rank][k0 % self.G]
 
 
 # --- rotating row blocks (strong scaling, an option) -------------------------

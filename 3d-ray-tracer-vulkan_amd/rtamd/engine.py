@@ -124,6 +124,12 @@ class Renderer:
     def wait(self, ticket: int) -> None:
         check(lib().rt_render_wait(self._ctx, ticket))
 
+    def poll(self, ticket: int) -> bool:
+        """True when the frame of `ticket` is complete (rt_render_poll; never blocks)."""
+        done = C.c_int32()
+        check(lib().rt_render_poll(self._ctx, ticket, C.byref(done)))
+        return bool(done.value)
+
     def render_tile_device(self, camera, width: int, height: int, max_bounces: int,
                            x0: int, y0: int, tile_w: int, tile_h: int,
                            d_rgba: Optional[int], d_radiance: Optional[int] = None,

@@ -191,6 +191,98 @@ def file_sha16(path: str) -> str:
         return hashlib.sha256(fh.read()).hexdigest()[:16]
 
 
+# ---- rank launcher -----------------------------------------------------------
+# `python bench.py --gpus N` with no launcher (WORLD_SIZE unset) starts its own
+# N ranks: N fresh child processes of this script, one per GPU, each with
+# RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR / MASTER_PORT set as
+# torch.distributed.run sets them.  The parent never touches the GPU (it does
+# not import torch): it only relays rank 0's stdout (the JSON line), passes
+# every rank's stderr through, and exits with the first failing rank's status,
+# ending the other ranks when one fails or the whole job outlives
+# --launch-timeout.  Under torch.distributed.run (WORLD_SIZE set) bench.py runs
+# as that rank directly.
+
+
+def free_port() -> int:
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def spawn_plan(argv, n: int, port: int, base_env=None, script: str = None):
+    """The N child processes of a self-launched run: (command, env) per rank."""
+    base = dict(os.environ if base_env is None else base_env)
+    cmd = [sys.executable, "-u", script or os.path.abspath(__file__)] + list(argv)
+    plan = []
+    for r in range(n):
+        env = dict(base)
+        env.update(RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), BENCH_LAUNCHED="1")
+        plan.append((cmd, env))
+    return plan
+
+
+def launch_ranks(plan, timeout_s: float, out=None, poll_s: float = 0.2) -> int:
+    """Run the ranks of `plan` (spawn_plan) to completion: rank 0's stdout is
+    relayed line by line to `out` (default sys.stdout), the other ranks' stdout
+    goes to stderr.  Returns 0 when every rank exits 0; otherwise the first
+    failing rank's exit status (124 on timeout), after ending the others."""
+    import signal
+    import subprocess
+    import threading
+    out = out or sys.stdout
+    procs = []
+    for r, (cmd, env) in enumerate(plan):
+        procs.append(subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE if r == 0 else sys.stderr,
+                                      start_new_session=True))
+
+    def relay():
+        for line in iter(procs[0].stdout.readline, b""):
+            out.write(line.decode(errors="replace"))
+            out.flush()
+
+    th = threading.Thread(target=relay, daemon=True)
+    th.start()
+    t_end = time.monotonic() + timeout_s
+    status = 0
+    while True:
+        codes = [p.poll() for p in procs]
+        bad = [(r, c) for r, c in enumerate(codes) if c not in (None, 0)]
+        if bad:
+            r, c = bad[0]
+            log(f"launcher: rank {r} exited with status {c}; ending the other ranks")
+            status = c if c > 0 else 128 - c           # a signal -s reads as 128 + s, like a shell
+            break
+        if all(c == 0 for c in codes):
+            break
+        if time.monotonic() > t_end:
+            log(f"launcher: ranks still running after {timeout_s:.0f} s; ending them")
+            status = 124
+            break
+        time.sleep(poll_s)
+    for p in procs:                                    # end what is left: SIGTERM, then SIGKILL
+        if p.poll() is None:
+            try:
+                os.killpg(p.pid, signal.SIGTERM)
+            except ProcessLookupError:
+                pass
+    deadline = time.monotonic() + 10.0
+    for p in procs:
+        try:
+            p.wait(timeout=max(0.1, deadline - time.monotonic()))
+        except subprocess.TimeoutExpired:
+            try:
+                os.killpg(p.pid, signal.SIGKILL)
+            except ProcessLookupError:
+                pass
+            p.wait()
+    th.join(timeout=5.0)
+    return status
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -252,7 +344,16 @@ def main() -> None:
     ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_latest.json"),
                     help="PMC per launch of each config (tools/pmc_traffic.py: SQ_INSTS_VMEM_RD, HBM bytes) for "
                          "the roofline")
+    ap.add_argument("--launch-timeout", type=float, default=1500.0,
+                    help="--gpus N > 1 without a launcher: the spawned ranks are ended after this many seconds")
     args = ap.parse_args()
+
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # no launcher: start the N ranks here, before anything touches the GPU
+        plan = spawn_plan(sys.argv[1:], args.gpus, free_port())
+        log(f"launcher: starting {args.gpus} ranks (one process per GPU, MASTER_ADDR 127.0.0.1 port "
+            f"{plan[0][1]['MASTER_PORT']})")
+        sys.exit(launch_ranks(plan, args.launch_timeout))
 
     import numpy as np
     import torch
@@ -260,13 +361,17 @@ def main() -> None:
     import rtamd
     from rtamd import configs
     from rtamd._lib import CameraUBO, Stats, check
-    from rtamd.dist import SharePlan, TilePlan, assemble_shares, band_list, gather_stack, gather_tiles
+    from rtamd.dist import SharePlan, ShareTracer, TilePlan, assemble_shares, band_list, gather_stack, gather_tiles
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         log(f"note: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE")
+    n_visible = torch.cuda.device_count()             # counts devices without initialising HIP
+    if not os.environ.get("BENCH_SHARE_GPU") and local_rank >= n_visible:
+        raise SystemExit(f"rank {rank}: LOCAL_RANK {local_rank} but only {n_visible} GPU(s) visible; one process "
+                         f"per GPU needs --gpus <= the GPUs of the node (BENCH_SHARE_GPU=1 shares them: rehearsal)")
     # BENCH_FORCE_DIST=1 (rehearsal only): the N > 1 code path at any world size,
     # so one GPU runs the partition, its RCCL gather and the rank-0 checks.
     # BENCH_EMULATE=N:r (analysis only, run under torchrun at world size 1):
@@ -347,19 +452,22 @@ def main() -> None:
     band_h = args.band
     plan = tplan = None
     src_index = None
-    my_bands = None
     if mode in ("bands", "pieces"):
         rw = args.root_weight if args.root_weight >= 0 else default_root_weight(world)
         deal = args.deal
         if deal == "auto":
+            # per-frame band lists (the rotating deal) pack whole bands: only
+            # where band_h divides the height
             fixed = [len(band_list(H, band_h, world, r, rw)) for r in range(1, world)]
-            deal = "rotate" if fixed and max(fixed) > min(fixed) else "fixed"
+            deal = "rotate" if fixed and max(fixed) > min(fixed) and H % band_h == 0 else "fixed"
+        if (mode == "pieces" or deal == "rotate") and H % band_h:
+            raise SystemExit(f"--partition {mode} --deal {deal}: per-frame band lists need --band ({band_h}) to "
+                             f"divide the height ({H})")
         plan = SharePlan(H, band_h, world, G, rw, layout="dealt" if deal == "rotate" else "interleave") \
             if mode == "bands" else \
             SharePlan(H, band_h, world, G, rw if args.root_weight >= 0 else default_piece_weight(world),
                       layout="pieces")
         src_index = torch.as_tensor(plan.src, device=dev)
-        my_bands = [np.ascontiguousarray(plan.frame_bands(rank, f)) for f in range(G)]
         rgba_slots = torch.empty((R, plan.per_rank, W, 4), dtype=torch.uint8, device=dev)
         rad_slots = torch.empty((R, plan.per_rank, W, 3), dtype=torch.float32, device=dev) if rad_on else None
         px_per_frame = plan.counts[rank] * W
@@ -391,7 +499,6 @@ def main() -> None:
 
     cam_cache = {}
     cam_arrays = {}
-    piece_lists = {}
 
     def cam_of(k):
         if args.camera_path == "static":
@@ -401,33 +508,17 @@ def main() -> None:
             c = cam_cache[k] = camera_path(cfg, args.camera_path, 1, k)[0]
         return c
 
-    def i32p(a):
-        return a.ctypes.data_as(C.POINTER(C.c_int32)) if a is not None else None
+    tracer = ShareTracer(ctx, W, H, B, mode, rank, plan=plan, tplan=tplan, band_h=band_h, batch=G)
 
     def trace(k0, n, s, rgba_ptr, rad_ptr, stats=False):
-        """Frames k0 .. k0 + n - 1 (one exchange batch) in one launch on stream s."""
+        """Frames k0 .. k0 + n - 1 (one exchange batch) in one launch on stream s
+        (rtamd.dist.ShareTracer: the tests replay the same launches)."""
         st = Stats() if stats else None
-        stp = C.byref(st) if stats else None
-        if mode == "tiles":
-            x0, y0, w, h = rect
-            check(L.rt_render_tile_device(ctx, C.byref(cam_of(k0).ubo), W, H, B, x0, y0, w, h, rgba_ptr, rad_ptr,
-                                          s.cuda_stream, stp))
-        else:
-            ck = (0, n) if args.camera_path == "static" else (k0, n)
-            cams = cam_arrays.get(ck)
-            if cams is None:                          # built once per (frames, count): no host work per launch
-                cams = cam_arrays[ck] = (CameraUBO * n)(*[cam_of(k).ubo for k in range(k0, k0 + n)])
-            if plan is not None and plan.lists:       # one band list per frame, built once per (frame, count)
-                pl = piece_lists.get((k0 % G, n))
-                if pl is None:
-                    pl = piece_lists[(k0 % G, n)] = np.ascontiguousarray(plan.launch_lists(rank, k0 % G, n))
-                check(L.rt_render_batch_lists_device(ctx, cams, n, W, H, B, band_h, i32p(pl), plan.n_per, rgba_ptr,
-                                                     rad_ptr, s.cuda_stream, stp))
-            else:
-                bl = my_bands[k0 % G] if my_bands is not None else None
-                check(L.rt_render_batch_device(ctx, cams, n, W, H, B, band_h if bl is not None else 0, i32p(bl),
-                                               len(bl) if bl is not None else 0, rgba_ptr, rad_ptr, s.cuda_stream,
-                                               stp))
+        ck = (0, n) if args.camera_path == "static" else (k0, n)
+        cams = cam_arrays.get(ck)
+        if cams is None:                              # built once per (frames, count): no host work per launch
+            cams = cam_arrays[ck] = (CameraUBO * n)(*[cam_of(k).ubo for k in range(k0, k0 + n)])
+        tracer.launch(cams, k0, n, s.cuda_stream, rgba_ptr, rad_ptr, st)
         return st.as_dict() if stats else None
 
     def out_ptrs(k0, j):
@@ -443,6 +534,7 @@ def main() -> None:
                 (rad_slots[h, off].data_ptr() if off < plan.per_rank else rad_slots[h].data_ptr()) if rad_on else None)
 
     st = {"k": 0, "j": 0}
+    slot_last = {}         # N = 1: slot -> (first frame, frames) of its last launch
     batch_streams = []     # streams that traced part of the current exchange batch
     gathered = [None] * R
     last = {"rgba": None, "rad": None, "frames": []}
@@ -529,6 +621,8 @@ def main() -> None:
             if evs is not None:
                 e[1].record(s)
                 evs.append((e, n))
+            if mode == "whole":
+                slot_last[j % D] = (k0, n)            # the frames slot j mod D now holds
             st["k"] = k0 + n
             st["j"] = j + 1
             if dist_on and st["k"] % G == 0:
@@ -727,6 +821,23 @@ def main() -> None:
             single = time.perf_counter() - t1
             renderer.set_option("concurrent_launches", D)
 
+    gpu_frame = None
+    if mode == "whole" and rank == 0:
+        # N = 1: the frames the timed loop left in its slots (the last launch of
+        # every stream) equal the same frames traced whole, one launch at a time
+        # on one stream (rt_render_tile_device)
+        ok = bool(slot_last)
+        full = torch.empty((H, W, 4), dtype=torch.uint8, device=dev)
+        for j_slot, (k0, n) in sorted(slot_last.items()):
+            for f in range(n):
+                check(L.rt_render_tile_device(ctx, C.byref(cam_of(k0 + f).ubo), W, H, B, 0, 0, W, H, full.data_ptr(),
+                                              None, main_stream.cuda_stream, None))
+                torch.cuda.synchronize(dev)
+                ok = ok and torch.equal(rgba_slots[j_slot][f * H:(f + 1) * H], full)
+        verified = bool(ok)
+        if args.camera_path == "static":
+            gpu_frame = full.cpu().numpy()
+
     # the camera stops (orbit): the first frames at rest, timed one by one (the
     # first repeat of a camera learns its own heavy-first order)
     stop = None
@@ -762,7 +873,7 @@ def main() -> None:
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(built, cam_of(k_t0), W, H, B, segments / K, args.cpu_seconds)
+        cpu = cpu_baseline(built, cam_of(k_t0), W, H, B, segments / K, args.cpu_seconds, gpu_frame)
 
     if rank == 0 or emu:
         gather_kind = "RCCL" if backend == "nccl" else (backend or "none")
@@ -962,8 +1073,11 @@ def host_cpu():
     return model, os.cpu_count() or 1, usable
 
 
-def cpu_baseline(built, cam, W, H, B, frame_segments, target_s):
-    """The oracle on every k-th row of the same frame, all host threads we may use."""
+def cpu_baseline(built, cam, W, H, B, frame_segments, target_s, gpu_frame=None):
+    """The oracle on every k-th row of the same frame, all host threads we may use.
+    gpu_frame (the timed loop's frame, host RGBA8): the oracle's rows of the
+    sample are compared with it (gpu_rows_match), the oracle as the checker."""
+    import numpy as np
     from oracle import oracle_lib
     model, nproc, usable = host_cpu()
     # A GPU box gives one GPU's job a share of 16 of the host's CPUs (the pool's
@@ -995,6 +1109,10 @@ def cpu_baseline(built, cam, W, H, B, frame_segments, target_s):
         px += c["pixels"]
         n += 1
     dt = time.perf_counter() - t0
+    match = None
+    if gpu_frame is not None:
+        rgba = oracle_lib.render(*args, row_step=step, radiance=False, n_threads=threads)[0]
+        match = bool(np.array_equal(rgba, gpu_frame[::step]))
     what = (f"every {step}th row of the frame" + (f" x {n}" if n > 1 else "")) if step > 1 \
         else f"the whole frame x {n}"
     return {
@@ -1003,6 +1121,9 @@ def cpu_baseline(built, cam, W, H, B, frame_segments, target_s):
         "cores": threads,
         "kind": "port",
         "sample": f"{what} ({px} px, {segs} segments, {dt:.2f} s, OpenMP threads {threads})",
+        "gpu_rows_match": match,
+        "gpu_rows_match_what": "the sample's oracle rows (RGBA8) equal the same rows of the timed loop's frame "
+                               "(checked outside the timed CPU sample)" if match is not None else None,
         "cpu_model": model,
         "nproc": nproc,
         "cpus_usable": usable,

@@ -57,19 +57,20 @@ typedef struct rt_camera_ubo {
     int32_t pad[2];
 } rt_camera_ubo;
 
-/* Work counters of one render call.  segments = executed iterations of the
- * bounce loop (compute_dynamic_ray.comp:179-232); node_visits = hit_aabb calls
- * (:193); tri_tests = hit_triangle calls (:201); mat_reads = scatter calls (:217).
+/* Work counters of one render call, in SURVEY.md §8(b)'s field order.
+ * segments = executed iterations of the bounce loop
+ * (compute_dynamic_ray.comp:179-232); node_visits = hit_aabb calls (:193);
+ * tri_tests = hit_triangle calls (:201); mat_reads = scatter calls (:217).
  * They are counted in the reference's visit order, so they are the same for
- * every implementation of the path. */
+ * every implementation of the path.  pixels (after §8(b)'s fields) = the
+ * pixels the call traced. */
 typedef struct rt_stats {
-    uint64_t pixels;
     uint64_t segments;
     uint64_t node_visits;
     uint64_t tri_tests;
     uint64_t mat_reads;
     double   ms;          /* device time of the trace kernel(s), HIP events */
-    uint64_t handoffs;    /* paths handed to a second pass (split / tiered schedules) */
+    uint64_t pixels;
 } rt_stats;
 
 /* ---------------------------------------------------------------- engine -- */
@@ -217,6 +218,11 @@ void  rt_host_free(void* p);
 int rt_render_async(rt_ctx* ctx, const rt_camera_ubo* cam, int width, int height, int max_bounces,
                     uint8_t* out_rgba, uint64_t* ticket);
 int rt_render_wait(rt_ctx* ctx, uint64_t ticket);
+/* Non-blocking form of rt_render_wait: *done = 1 when the frame of `ticket`
+ * is complete in its out_rgba (rt_render_wait would return at once), else 0.
+ * A UI timer (VulkanApp.updateUI, VulkanApp.java:194-235) can poll it instead
+ * of blocking its thread. */
+int rt_render_poll(rt_ctx* ctx, uint64_t ticket, int* done);
 
 /* Schedule options (no effect on results, which are identical for every
  * setting):

@@ -10,7 +10,11 @@ sources, not from this repo's C++ (csrc/scene_build.cpp):
   fast_atoreal_move<float>   code/Common/fast_atof.h (integer digits -> float;
                              up to 15 fraction digits -> double x 10^-n -> float;
                              the two added in float; 'e' exponent x powf(10, e))
-  ObjFileParser 'v' lines    3 components, 4 (divided by w), 6 (xyz + colour)
+  ObjFileParser 'v' lines    the components are the tokens that start like a
+                             number (ParsingUtils.h IsNumeric: digit, '-',
+                             '+'; or nan / inf): 3, 4 (divided by w) or 6
+                             (xyz + colour) read that many words in order;
+                             any other count adds no vertex
   TriangulateProcess         quads fanned from the concave corner (acos angle
                              sum > pi, vectors normalised by multiplying with
                              the float reciprocal of the length), else corner 0;
@@ -37,12 +41,16 @@ _TABLE = [0.0, 0.1, 0.01, 0.001, 0.0001, 0.00001, 0.000001, 0.0000001, 0.0000000
 
 
 def _digits(s: str, i: int, cap: int | None):
-    """strtoul10_64: (value, next index, digits counted); overflow -> (0, i, 0)."""
+    """strtoul10_64: (value, next index, digits counted); overflow -> (0, i, 0);
+    ValueError (Assimp throws) when no digit starts the string."""
+    if not s[i:i + 1].isdigit():
+        raise ValueError(f"no digits at {s[i:]!r}")
     j, v, n = i, 0, 0
     while j < len(s) and s[j] in "0123456789":
-        v = v * 10 + ord(s[j]) - 48
-        if v >= 1 << 64:
+        nv = (v * 10 + ord(s[j]) - 48) & ((1 << 64) - 1)    # uint64 arithmetic, as Assimp's
+        if nv < v:                                          # its overflow test: the value went down
             return 0, i, 0
+        v = nv
         j += 1
         n += 1
         if cap is not None and n == cap:
@@ -215,10 +223,11 @@ def load_obj(path: str) -> np.ndarray:
             s = ln.lstrip(" \t")
             if s[:2] in ("v ", "v\t"):
                 tok = s[2:].split()
-                if len(tok) not in (3, 4, 6):
-                    raise ValueError("bad vertex")
-                c = [fast_atof(t) for t in tok[:4 if len(tok) == 4 else 3]]
-                if len(tok) == 4:
+                n = sum(1 for t in tok if t[0] in "0123456789+-" or t[:3].lower() in ("nan", "inf"))
+                if n not in (3, 4, 6):
+                    continue                             # Assimp reads no vertex from such a line
+                c = [fast_atof(t) for t in tok[:n]]
+                if n == 4:
                     if c[3] == 0:
                         raise ValueError("w = 0")
                     c = [f32(c[0] / c[3]), f32(c[1] / c[3]), f32(c[2] / c[3])]

@@ -44,7 +44,9 @@ def test_structs_match_reference_bytes():
     assert C.sizeof(CameraUBO) == 80              # VulkanEngine.java createCameraUbo: 80 bytes
     assert CameraUBO.vertical.offset == 48 and CameraUBO.frame_count.offset == 64
     assert CameraUBO.sky_enabled.offset == 68
-    assert Stats.ms.offset == 40
+    # {segments, node_visits, tri_tests, mat_reads; double ms}, then pixels
+    assert [f for f, _ in Stats._fields_] == ["segments", "node_visits", "tri_tests", "mat_reads", "ms", "pixels"]
+    assert Stats.ms.offset == 32 and Stats.pixels.offset == 40 and C.sizeof(Stats) == 48
 
 
 @pytest.mark.skipif(has_gpu(), reason="only meaningful without a GPU")

@@ -1,11 +1,25 @@
-"""The exchange on the GPU over RCCL (backend "nccl"): one process, world size 1.
+"""bench.py's N > 1 exchange on the GPU, with device tensors.
 
-The multi-GPU runs are the driver's; this runs the same calls bench.py makes
-at N > 1 (rtamd/dist.py: gather_frames of a batch of frame slots, gather_frame,
-DistRenderer) through RCCL with device tensors, and checks that the assembled
-frames equal the whole frame traced on one GPU bit for bit.  The partition and
-assembly logic at world sizes 2 and 3 is covered on CPU (test_dist.py, gloo).
+A gpurun box has one GPU and RCCL refuses two ranks on one GPU, so:
+
+* every rank's share of an exchange batch is traced on this GPU with the
+  launches bench.py issues at N > 1 (rtamd.dist.ShareTracer: the band lists of
+  SharePlan's "interleave", "dealt" and "pieces" layouts, one list for every
+  frame of a launch or one per frame, F = N frames per launch; TilePlan's
+  rectangles), into the ranks' exchange buffers at the plan's offsets, RGBA8
+  and float radiance;
+* the ranks' buffers are stacked as the gather to rank 0 stacks them, and
+  rank 0's assembly (assemble_shares / assemble_tiles, one index_select) runs
+  on that stack;
+* the collective itself, gather_stack / gather_tile_stack, runs over RCCL
+  (backend "nccl") at world size 1 on the same buffers.
+
+Every assembled frame (RGBA8 and radiance bits) equals the frame traced whole
+on the GPU.  The multi-process collective at world sizes 2-8 runs over gloo on
+the CPU (test_dist.py) and in the self-launched one-GPU rehearsal
+(`BENCH_SHARE_GPU=1 BENCH_DIST_BACKEND=gloo python bench.py --gpus N`).
 """
+import ctypes as C
 import socket
 
 import pytest
@@ -33,9 +47,120 @@ def rccl_group():
         dist.destroy_process_group()
 
 
+def _orbit_cams(W, H, n):
+    import math
+    from rtamd import configs
+    ox, oy, oz = -25.0, 30.0, 140.0
+    rad, a0 = math.hypot(ox, oz), math.atan2(oz, ox)
+    return [configs.Camera((rad * math.cos(a0 + math.radians(3.0) * k), oy, rad * math.sin(a0 + math.radians(3.0) * k)),
+                           (0.0, 0.0, 0.0), (0.0, 1.0, 0.0), 20.0, W / H) for k in range(n)]
+
+
+def _whole(renderer, cams, W, H, B):
+    """Reference frames: each traced whole on the GPU (RGBA8, radiance)."""
+    import torch
+    from rtamd import lib
+    from rtamd._lib import check
+    s = torch.cuda.current_stream()
+    out = []
+    for c in cams:
+        rgba = torch.empty((H, W, 4), dtype=torch.uint8, device="cuda:0")
+        rad = torch.empty((H, W, 3), dtype=torch.float32, device="cuda:0")
+        check(lib().rt_render_tile_device(renderer._ctx, C.byref(c.ubo), W, H, B, 0, 0, W, H, rgba.data_ptr(),
+                                          rad.data_ptr(), s.cuda_stream, None))
+        out.append((rgba, rad))
+    torch.cuda.synchronize()
+    return out
+
+
+def _check(frames, rads, whole, what):
+    import torch
+    for f, (rgba, rad) in enumerate(whole):
+        assert torch.equal(frames[f], rgba), f"{what}: frame {f} RGBA8"
+        assert torch.equal(rads[f].view(torch.int32), rad.view(torch.int32)), f"{what}: frame {f} radiance"
+
+
+@pytest.mark.parametrize("layout,world,rw", [("interleave", 1, 1.0), ("interleave", 2, 0.9), ("interleave", 4, 0.85),
+                                             ("dealt", 8, 0.8), ("dealt", 4, 1.0), ("pieces", 4, 1.0),
+                                             ("pieces", 8, 0.7)])
+def test_share_exchange_bit_exact(renderer, rccl_group, layout, world, rw):
+    import torch
+    from rtamd import configs
+    from rtamd._lib import CameraUBO
+    from rtamd.dist import SharePlan, ShareTracer, assemble_shares, gather_stack
+    cfg = configs.config2()
+    renderer.upload_scene(cfg.build())
+    W, H, B, band_h = 320, 184, 3, 8          # 23 bands of 8 rows
+    F = world                                  # frames per launch (weak scaling: a launch is a step)
+    G = 2 * F                                  # frames per exchange batch
+    cams = _orbit_cams(W, H, G)
+    whole = _whole(renderer, cams, W, H, B)
+    plan = SharePlan(H, band_h, world, G, rw, layout=layout)
+    src = torch.as_tensor(plan.src, device="cuda:0")
+    streams = [torch.cuda.Stream() for _ in range(2)]
+    bufs, rbufs = [], []
+    for rank in range(world):
+        tracer = ShareTracer(renderer._ctx, W, H, B, "bands", rank, plan=plan, band_h=band_h, batch=G)
+        rgba = torch.full((plan.per_rank, W, 4), 7, dtype=torch.uint8, device="cuda:0")
+        rad = torch.zeros((plan.per_rank, W, 3), dtype=torch.float32, device="cuda:0")
+        for j, k0 in enumerate(range(0, G, F)):
+            off = tracer.offset_rows(k0)
+            rp = rgba[off].data_ptr() if off < plan.per_rank else rgba.data_ptr()
+            dp = rad[off].data_ptr() if off < plan.per_rank else rad.data_ptr()
+            ubos = (CameraUBO * F)(*[c.ubo for c in cams[k0:k0 + F]])
+            tracer.launch(ubos, k0, F, streams[j % 2].cuda_stream, rp, dp)
+        bufs.append(rgba)
+        rbufs.append(rad)
+    torch.cuda.synchronize()
+    frames = assemble_shares(torch.stack(bufs), plan, src)
+    rads = assemble_shares(torch.stack(rbufs), plan, src)
+    torch.cuda.synchronize()
+    _check(frames, rads, whole, f"{layout} N={world}")
+    if world == 1:
+        # the collective half over RCCL at world size 1, on the same buffers
+        stk = gather_stack(bufs[0], plan)
+        stk_r = gather_stack(rbufs[0], plan)
+        _check(assemble_shares(stk, plan, src), assemble_shares(stk_r, plan, src), whole, "RCCL gather_stack")
+
+
+@pytest.mark.parametrize("world", [1, 2, 4])
+def test_tile_exchange_bit_exact(renderer, rccl_group, world):
+    """BASELINE config 4's tile grid (2 x 2 at N = 4): every rank's rectangle
+    of every frame of a batch, stacked and assembled; at world size 1 the
+    gather runs over RCCL."""
+    import torch
+    from rtamd import configs
+    from rtamd._lib import CameraUBO
+    from rtamd.dist import ShareTracer, TilePlan, assemble_tiles, gather_tile_stack, gather_tiles
+    cfg = configs.config2()
+    renderer.upload_scene(cfg.build())
+    W, H, B, G = 322, 181, 3, 3               # odd sizes: uneven tiles, padded to the largest
+    cams = _orbit_cams(W, H, G)
+    whole = _whole(renderer, cams, W, H, B)
+    plan = TilePlan(W, H, world, G)
+    src = torch.as_tensor(plan.src, device="cuda:0")
+    s = torch.cuda.current_stream()
+    bufs, rbufs = [], []
+    for rank in range(world):
+        tracer = ShareTracer(renderer._ctx, W, H, B, "tiles", rank, tplan=plan, batch=G)
+        rgba = torch.zeros((G, plan.tile_px, 4), dtype=torch.uint8, device="cuda:0")
+        rad = torch.zeros((G, plan.tile_px, 3), dtype=torch.float32, device="cuda:0")
+        for f in range(G):
+            tracer.launch((CameraUBO * 1)(cams[f].ubo), f, 1, s.cuda_stream, rgba[f].data_ptr(), rad[f].data_ptr())
+        bufs.append(rgba)
+        rbufs.append(rad)
+    torch.cuda.synchronize()
+    _check(assemble_tiles(torch.stack(bufs), plan, src), assemble_tiles(torch.stack(rbufs), plan, src), whole,
+           f"tiles N={world}")
+    if world == 1:
+        _check(gather_tiles(bufs[0], plan, src_index=src), gather_tiles(rbufs[0], plan, src_index=src), whole,
+               "RCCL gather_tiles")
+        assert torch.equal(gather_tile_stack(bufs[0], plan)[0], bufs[0])
+
+
 @pytest.mark.parametrize("band_h,n_frames", [(16, 4), (7, 3)])
 def test_rccl_gather_frames_bit_exact(renderer, rccl_group, band_h, n_frames):
-    import ctypes as C
+    """gather_frames / DistRenderer (the plain interleave of rtamd.dist) over RCCL."""
     import torch
     from rtamd import configs, lib
     from rtamd._lib import check
@@ -48,7 +173,6 @@ def test_rccl_gather_frames_bit_exact(renderer, rccl_group, band_h, n_frames):
     s = torch.cuda.current_stream()
     check(lib().rt_render_bands_device(renderer._ctx, C.byref(cam.ubo), W, H, B, H, 1, 0, full.data_ptr(), None,
                                        s.cuda_stream, None))
-    # bench.py's N > 1 exchange: frame slots traced as bands, one gather per batch
     rows = band_row_count(H, band_h, 1, 0)
     slots = torch.zeros((2 * n_frames, rows, W, 4), dtype=torch.uint8, device="cuda:0")
     for k in range(n_frames):

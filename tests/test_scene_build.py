@@ -239,7 +239,7 @@ def _obj_text(rng, n_polys=60):
         if k == 2:
             return ("+" if x >= 0 else "") + f"{x:.6f}"
         if k == 3 and abs(x) < 1:
-            return ("-" if x < 0 else "") + f"{abs(x):.7f}"[1:]       # ".1234567"
+            return ("-" if x < 0 else "+") + f"{abs(x):.7f}"[1:]      # "+.1234567" (a bare "." does not count)
         return repr(float(np.float32(x)))
 
     for pi in range(n_polys):
@@ -328,7 +328,7 @@ def test_obj_numbers_are_assimp_fast_atof(tmp_path):
     assert 0.01 < np.mean(fa != st) < 0.2
     assert np.all(np.abs(fa.astype(np.float64) - st) <= np.spacing(np.abs(st)))   # one ulp at most
     p = tmp_path / "nums.obj"
-    toks = ["1.5", "-0.25", "+3", ".5", "-.75", "1e3", "2.5E-2", "7.", "1,5", "123456789012.123456789012345678",
+    toks = ["1.5", "-0.25", "+3", "+.5", "-.75", "1e3", "2.5E-2", "7.", "1,5", "123456789012.123456789012345678",
             "0.1234567890123456789", "-1.000000000000000001"]
     body = "".join(f"v {toks[k]} {toks[(k + 1) % len(toks)]} {toks[(k + 2) % len(toks)]}\n" for k in range(len(toks)))
     body += "".join(f"f {k + 1} {(k + 1) % len(toks) + 1} {(k + 2) % len(toks) + 1}\n" for k in range(len(toks)))
@@ -338,3 +338,34 @@ def test_obj_numbers_are_assimp_fast_atof(tmp_path):
     want = oo.load_obj(str(p)) + np.float32(0)
     assert np.array_equal(got.view(np.uint32), want.view(np.uint32))
     assert got[0, 0].tolist() == [1.5, -0.25, 3.0]
+
+
+def test_obj_vertex_component_rule(tmp_path):
+    """ObjFileParser counts a 'v' line's components as the tokens that start
+    like a number (a digit, '-', '+', nan / inf): a trailing comment does not
+    count; a count other than 3, 4 or 6 adds no vertex (later indices shift);
+    6 is xyz + a colour.  "1e" (no exponent digits) fails the import, as
+    Assimp's strtoul10_64 throws.  Both restatements agree."""
+    from oracle import obj_oracle as oo
+    from rtamd import Mesh, RtError
+    p = tmp_path / "rule.obj"
+    p.write_text("v 1 2 3 # a note\n"          # 3 components: (1, 2, 3)
+                 "v .5 1 2\n"                  # '.5' does not count: 2 -> no vertex
+                 "v 4 5 6 7 8\n"               # 5 -> no vertex
+                 "v 0 1 0 0.5 0.25 1\n"        # 6: xyz + colour
+                 "v 2 4 6 2\n"                 # 4: divided by w
+                 "v -1 -2 -3\n"
+                 "v 99999999999999999999 1 2\n"   # integer overflow: Assimp's 0, with a warning
+                 "f 1 2 3\nf 2 3 4\nf 1 4 5\n")
+    got = Mesh.load_obj(str(p)).tris
+    want = oo.load_obj(str(p)) + np.float32(0)
+    assert np.array_equal(got.view(np.uint32), want.view(np.uint32))
+    assert got[0].tolist() == [[1, 2, 3], [0, 1, 0], [1, 2, 3]]
+    assert got[1].tolist() == [[0, 1, 0], [1, 2, 3], [-1, -2, -3]]
+    assert got[2, 2, 0] == oo.fast_atof("99999999999999999999")
+    bad = tmp_path / "exp.obj"
+    bad.write_text("v 1e 2 3\nv 0 0 0\nv 1 0 0\nf 1 2 3\n")
+    with pytest.raises(RtError, match="IO"):
+        Mesh.load_obj(str(bad))
+    with pytest.raises(ValueError):
+        oo.load_obj(str(bad))

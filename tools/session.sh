@@ -18,6 +18,9 @@
 #   share     tools/share_inflight_bench.py (one rank's share, frames in flight)
 #   emu       tools/rank_emulator.py (one rank of N with its exchange; $EMU_ARGS)
 #   pipeline  tools/pipeline_bench.py (PCIe-inclusive rates)
+#   spawn2    bench.py --gpus 2 with no launcher (it starts its own ranks):
+#             BENCH_SHARE_GPU=1 BENCH_DIST_BACKEND=gloo, two gloo ranks on one GPU
+#   spawn4    the same with 4 ranks and the 2 x 2 tile grid + radiance gather
 #   cmd       the command in $CMD (600 s)
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -73,6 +76,10 @@ for s in "$@"; do
     share)    run share 600 python tools/share_inflight_bench.py ${SHARE_ARGS:-} > "$OUT/share.jsonl" 2> "$OUT/share.err" ;;
     emu)      run emu 900 python tools/rank_emulator.py ${EMU_ARGS:-} > "$OUT/emu.jsonl" 2> "$OUT/emu.err" ;;
     pipeline) run pipeline 300 python tools/pipeline_bench.py ${PIPE_ARGS:-} > "$OUT/pipeline.jsonl" 2> "$OUT/pipeline.err" ;;
+    spawn2)   BENCH_SHARE_GPU=1 BENCH_DIST_BACKEND=gloo run spawn2 600 python bench.py --gpus 2 --steps 20 \
+                  --warmup 5 > "$OUT/spawn2.json" 2> "$OUT/spawn2.err" ;;
+    spawn4)   BENCH_SHARE_GPU=1 BENCH_DIST_BACKEND=gloo run spawn4 600 python bench.py --gpus 4 --steps 10 \
+                  --warmup 3 --partition tiles --gather radiance > "$OUT/spawn4.json" 2> "$OUT/spawn4.err" ;;
     cmd)      run cmd 600 bash -c "$CMD" > "$OUT/cmd.log" 2>&1 ;;
     *)        status "unknown step $s" ;;
   esac
