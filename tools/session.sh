@@ -76,9 +76,9 @@ for s in "$@"; do
     share)    run share 600 python tools/share_inflight_bench.py ${SHARE_ARGS:-} > "$OUT/share.jsonl" 2> "$OUT/share.err" ;;
     emu)      run emu 900 python tools/rank_emulator.py ${EMU_ARGS:-} > "$OUT/emu.jsonl" 2> "$OUT/emu.err" ;;
     pipeline) run pipeline 300 python tools/pipeline_bench.py ${PIPE_ARGS:-} > "$OUT/pipeline.jsonl" 2> "$OUT/pipeline.err" ;;
-    spawn2)   BENCH_SHARE_GPU=1 BENCH_DIST_BACKEND=gloo run spawn2 600 python bench.py --gpus 2 --steps 20 \
+    spawn2)   run spawn2 600 env BENCH_SHARE_GPU=1 BENCH_DIST_BACKEND=gloo python bench.py --gpus 2 --steps 20 \
                   --warmup 5 > "$OUT/spawn2.json" 2> "$OUT/spawn2.err" ;;
-    spawn4)   BENCH_SHARE_GPU=1 BENCH_DIST_BACKEND=gloo run spawn4 600 python bench.py --gpus 4 --steps 10 \
+    spawn4)   run spawn4 600 env BENCH_SHARE_GPU=1 BENCH_DIST_BACKEND=gloo python bench.py --gpus 4 --steps 10 \
                   --warmup 3 --partition tiles --gather radiance > "$OUT/spawn4.json" 2> "$OUT/spawn4.err" ;;
     cmd)      run cmd 600 bash -c "$CMD" > "$OUT/cmd.log" 2>&1 ;;
     *)        status "unknown step $s" ;;
