@@ -226,9 +226,9 @@ def spawn_plan(argv, n: int, port: int, base_env=None, script: str = None):
 
 
 def launch_ranks(plan, timeout_s: float, out=None, poll_s: float = 0.2) -> int:
-    """Run the ranks of `plan` (spawn_plan) to completion: rank 0's stdout is
-    relayed line by line to `out` (default sys.stdout), the other ranks' stdout
-    goes to stderr.  Returns 0 when every rank exits 0; otherwise the first
+    """Run the ranks of `plan` (spawn_plan) to completion: rank 0's JSON line is
+    relayed to `out` (default sys.stdout); its other stdout lines and the other
+    ranks' stdout go to stderr.  Returns 0 when every rank exits 0; otherwise the first
     failing rank's exit status (124 on timeout), after ending the others."""
     import signal
     import subprocess
@@ -240,9 +240,13 @@ def launch_ranks(plan, timeout_s: float, out=None, poll_s: float = 0.2) -> int:
                                       start_new_session=True))
 
     def relay():
+        # rank 0's JSON line to stdout; anything else it prints there (gloo's
+        # connection notes) to stderr, so stdout holds the one JSON line
         for line in iter(procs[0].stdout.readline, b""):
-            out.write(line.decode(errors="replace"))
-            out.flush()
+            text = line.decode(errors="replace")
+            dst = out if text.lstrip().startswith("{") else sys.stderr
+            dst.write(text)
+            dst.flush()
 
     th = threading.Thread(target=relay, daemon=True)
     th.start()

@@ -9,6 +9,8 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB = os.path.join(HERE, "liboracle.so")
+ENV_LIB = os.path.join(HERE, "liboracle_env.so")     # rt_envelope.c: the Vulkan-envelope study
+ENV_FMA, ENV_RSQ, ENV_RCP, ENV_ULP = 1, 2, 4, 8          # rt_oracle.c ENV_* bits
 
 
 class Counts(C.Structure):
@@ -20,35 +22,49 @@ class Counts(C.Structure):
 
 
 _lib = None
+_env_lib = None
 
 
 def build() -> None:
     subprocess.run(["make", "-s", "-C", HERE], check=True)
 
 
-def lib() -> C.CDLL:
-    global _lib
+def lib(envelope: bool = False) -> C.CDLL:
+    """liboracle.so (the contract), or with envelope=True liboracle_env.so
+    (the same oracle with orc_env_set_variant)."""
+    global _lib, _env_lib
+    if envelope:
+        if _env_lib is None:
+            if not os.path.exists(ENV_LIB):
+                build()
+            _env_lib = _bind(C.CDLL(ENV_LIB))
+            _env_lib.orc_env_set_variant.restype = C.c_int
+            _env_lib.orc_env_set_variant.argtypes = [C.c_int]
+        return _env_lib
     if _lib is None:
         if not os.path.exists(LIB):
             build()
-        L = C.CDLL(LIB)
-        f3 = C.POINTER(C.c_float)
-        L.orc_pcg.restype = C.c_uint32
-        L.orc_pcg.argtypes = [C.c_uint32]
-        L.orc_random_float.restype = C.c_float
-        L.orc_random_float.argtypes = [C.POINTER(C.c_uint32)]
-        L.orc_random_in_unit_sphere.argtypes = [C.POINTER(C.c_uint32), f3]
-        L.orc_hit_aabb.argtypes = [f3, f3, f3, f3, C.c_float, C.c_float]
-        L.orc_hit_triangle.argtypes = [f3, f3, f3, f3, f3, f3, f3]
-        L.orc_hit_sphere.argtypes = [f3, f3, f3, f3, f3]
-        L.orc_scatter.argtypes = [f3, C.POINTER(C.c_uint32), f3, f3, f3, f3, f3]
-        L.orc_render.argtypes = [C.c_void_p, C.c_size_t, C.c_void_p, C.c_size_t, C.c_void_p, C.c_size_t,
-                                 C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
-                                 C.c_int, C.c_void_p, C.c_void_p, C.POINTER(Counts), C.c_int]
-        L.orc_render_ext.argtypes = L.orc_render.argtypes + [C.c_int, C.c_void_p]
-        L.orc_render_spheres.argtypes = L.orc_render_ext.argtypes + [C.c_void_p, C.c_int]
-        _lib = L
+        _lib = _bind(C.CDLL(LIB))
     return _lib
+
+
+def _bind(L: C.CDLL) -> C.CDLL:
+    f3 = C.POINTER(C.c_float)
+    L.orc_pcg.restype = C.c_uint32
+    L.orc_pcg.argtypes = [C.c_uint32]
+    L.orc_random_float.restype = C.c_float
+    L.orc_random_float.argtypes = [C.POINTER(C.c_uint32)]
+    L.orc_random_in_unit_sphere.argtypes = [C.POINTER(C.c_uint32), f3]
+    L.orc_hit_aabb.argtypes = [f3, f3, f3, f3, C.c_float, C.c_float]
+    L.orc_hit_triangle.argtypes = [f3, f3, f3, f3, f3, f3, f3]
+    L.orc_hit_sphere.argtypes = [f3, f3, f3, f3, f3]
+    L.orc_scatter.argtypes = [f3, C.POINTER(C.c_uint32), f3, f3, f3, f3, f3]
+    L.orc_render.argtypes = [C.c_void_p, C.c_size_t, C.c_void_p, C.c_size_t, C.c_void_p, C.c_size_t,
+                             C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
+                             C.c_int, C.c_void_p, C.c_void_p, C.POINTER(Counts), C.c_int]
+    L.orc_render_ext.argtypes = L.orc_render.argtypes + [C.c_int, C.c_void_p]
+    L.orc_render_spheres.argtypes = L.orc_render_ext.argtypes + [C.c_void_p, C.c_int]
+    return L
 
 
 def _buf(x):
@@ -61,11 +77,13 @@ EXT_SKY_TOGGLE, EXT_EMISSIVE, EXT_ACCUMULATE, EXT_SPHERES = 1, 2, 4, 8   # rt_or
 
 def render(vertices, materials, nodes, camera_ubo: bytes, width: int, height: int, max_bounces: int,
            tile=None, row_step: int = 1, radiance: bool = True, n_threads: int = 0, ext: int = 0,
-           accum: "np.ndarray | None" = None, spheres: "np.ndarray | None" = None):
+           accum: "np.ndarray | None" = None, spheres: "np.ndarray | None" = None, variant: "int | None" = None):
     """Returns (rgba[rows, w, 4], radiance[rows, w, 3] or None, counts dict).
     ext: ORC_EXT_* bits (non-reference extensions); accum: float32[rows, w, 3],
     updated in place, required with EXT_ACCUMULATE; spheres: float32[n, 8]
-    (centre.xyz, radius, albedo.rgb, type), tested with EXT_SPHERES."""
+    (centre.xyz, radius, albedo.rgb, type), tested with EXT_SPHERES.
+    variant: ENV_* bits: render with liboracle_env.so (the Vulkan-envelope
+    study) instead of the contract's liboracle.so."""
     x0, y0, tw, th = tile if tile is not None else (0, 0, width, height)
     rows = (th + row_step - 1) // row_step
     v, vp, vn = _buf(vertices)
@@ -79,7 +97,11 @@ def render(vertices, materials, nodes, camera_ubo: bytes, width: int, height: in
         assert accum.dtype == np.float32 and accum.shape == (rows, tw, 3) and accum.flags.c_contiguous
     sph = np.ascontiguousarray(spheres if spheres is not None else np.zeros((0, 8)), dtype=np.float32)
     assert sph.ndim == 2 and sph.shape[1] == 8
-    rc = lib().orc_render_spheres(vp, vn, mp, mn, bp, bn, cam.ctypes.data, width, height, max_bounces,
+    L = lib()
+    if variant is not None:                 # the envelope build, with these ENV_* bits
+        L = lib(envelope=True)
+        L.orc_env_set_variant(int(variant))
+    rc = L.orc_render_spheres(vp, vn, mp, mn, bp, bn, cam.ctypes.data, width, height, max_bounces,
                                   x0, y0, tw, th, row_step, rgba.ctypes.data,
                                   rad.ctypes.data if rad is not None else None, C.byref(c), n_threads,
                                   ext, accum.ctypes.data if accum is not None else None,

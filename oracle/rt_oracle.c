@@ -53,18 +53,65 @@ static void trace_rec(int32_t v) { if (g_trace && g_trace_n < g_trace_cap) g_tra
 
 typedef struct { float x, y, z; } vec3;
 
+/* Implementation-defined float behaviour.  The default build (liboracle.so)
+ * is the contract above: every helper below is the plain IEEE expression.
+ * The envelope build (rt_envelope.c, liboracle_env.so; tests/golden/
+ * make_envelope.py) switches, per orc_env_set_variant bit, to behaviour a
+ * Vulkan implementation is also allowed (GLSL 4.50 §4.7.1, SPIR-V without
+ * NoContraction decorations): FMA contraction of a*b+c, normalize through
+ * inversesqrt, division through a reciprocal, and approximate (1-ulp)
+ * reciprocal / inversesqrt.  It measures how far a real Vulkan frame may lie
+ * from the contract. */
+#ifdef ORC_ENVELOPE
+#define ENV_FMA 1        /* contract a*b+c / a*b-c / c-a*b at the sites LLVM's DAG combiner fuses */
+#define ENV_RSQ 2        /* normalize(v) = v * inversesqrt(dot(v,v)), inversesqrt correctly rounded */
+#define ENV_RCP 4        /* a / b = a * (1 / b), the reciprocal correctly rounded */
+#define ENV_ULP 8        /* reciprocals and inversesqrts off by up to one ulp (a hash of the input picks) */
+static int g_env = 0;
+static float env_ulp(float r, float x) {
+    if (!(g_env & ENV_ULP)) return r;
+    uint32_t b;
+    memcpy(&b, &x, 4);
+    const uint32_t h = orc_pcg(b ^ 0x9E3779B9u) & 3u;
+    return h == 1u ? nextafterf(r, INFINITY) : h == 2u ? nextafterf(r, -INFINITY) : r;
+}
+static float mad(float a, float b, float c) { return (g_env & ENV_FMA) ? fmaf(a, b, c) : a * b + c; }
+static float msb(float a, float b, float c) { return (g_env & ENV_FMA) ? fmaf(a, b, -c) : a * b - c; }
+static float rcp(float x) { return env_ulp(1.0f / x, x); }
+static float fdiv(float a, float b) { return (g_env & (ENV_RCP | ENV_ULP)) ? a * rcp(b) : a / b; }
+static float rsq(float x) { return env_ulp((float)(1.0 / sqrt((double)x)), x); }
+#else
+static float mad(float a, float b, float c) { return a * b + c; }
+static float msb(float a, float b, float c) { return a * b - c; }
+static float rcp(float x) { return 1.0f / x; }
+static float fdiv(float a, float b) { return a / b; }
+#endif
+
 static vec3 v3(float x, float y, float z) { vec3 r = {x, y, z}; return r; }
 static vec3 add3(vec3 a, vec3 b) { return v3(a.x + b.x, a.y + b.y, a.z + b.z); }
 static vec3 sub3(vec3 a, vec3 b) { return v3(a.x - b.x, a.y - b.y, a.z - b.z); }
 static vec3 mul3(vec3 a, vec3 b) { return v3(a.x * b.x, a.y * b.y, a.z * b.z); }
 static vec3 scale3(vec3 a, float s) { return v3(a.x * s, a.y * s, a.z * s); }
-static float dot3(vec3 a, vec3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+/* a + b * s (add3(a, scale3(b, s)), one contraction site per component) */
+static vec3 madd3(vec3 a, vec3 b, float s) { return v3(mad(b.x, s, a.x), mad(b.y, s, a.y), mad(b.z, s, a.z)); }
+/* (x*x' + y*y') + z*z'; contracted: fma(z, z', fma(x, x', y*y')) */
+static float dot3(vec3 a, vec3 b) { return mad(a.z, b.z, mad(a.x, b.x, a.y * b.y)); }
 static float length3(vec3 a) { return sqrtf(dot3(a, a)); }
-static vec3 normalize3(vec3 a) { float l = length3(a); return v3(a.x / l, a.y / l, a.z / l); }
-static vec3 cross3(vec3 a, vec3 b) {
-    return v3(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
+static vec3 normalize3(vec3 a) {
+#ifdef ORC_ENVELOPE
+    if (g_env & ENV_RSQ) { const float k = rsq(dot3(a, a)); return v3(a.x * k, a.y * k, a.z * k); }
+#endif
+    float l = length3(a);
+    return v3(fdiv(a.x, l), fdiv(a.y, l), fdiv(a.z, l));
 }
-static vec3 reflect3(vec3 i, vec3 n) { return sub3(i, scale3(n, 2.0f * dot3(n, i))); }
+static vec3 cross3(vec3 a, vec3 b) {
+    return v3(msb(a.y, b.z, a.z * b.y), msb(a.z, b.x, a.x * b.z), msb(a.x, b.y, a.y * b.x));
+}
+/* I - N * (2 dot(N, I)); contracted: fma(-N, k, I) */
+static vec3 reflect3(vec3 i, vec3 n) {
+    const float k = 2.0f * dot3(n, i);
+    return v3(mad(-n.x, k, i.x), mad(-n.y, k, i.y), mad(-n.z, k, i.z));
+}
 
 /* ------------------------------------------------------------------ RNG -- */
 
@@ -88,7 +135,7 @@ static vec3 random_in_unit_sphere(uint32_t* seed) {             /* :63-70 */
         float x = orc_random_float(seed);
         float y = orc_random_float(seed);
         float z = orc_random_float(seed);
-        vec3 p = v3(x * 2.0f - 1.0f, y * 2.0f - 1.0f, z * 2.0f - 1.0f);
+        vec3 p = v3(msb(x, 2.0f, 1.0f), msb(y, 2.0f, 1.0f), msb(z, 2.0f, 1.0f));
         if (dot3(p, p) < 1.0f) return p;
     }
     return v3(0.0f, 0.0f, 0.0f);
@@ -107,17 +154,17 @@ static vec3 random_unit_vector(uint32_t* seed) {                 /* :72-74 */
 
 typedef struct { vec3 origin, dir; } ray;
 
-static vec3 ray_at(ray r, float t) { return add3(r.origin, scale3(r.dir, t)); }   /* :77-79 */
+static vec3 ray_at(ray r, float t) { return madd3(r.origin, r.dir, t); }   /* :77-79 */
 
 static vec3 sky_color(ray r) {                                   /* :81-85 */
     vec3 u = normalize3(r.dir);
     float t = 0.5f * (u.y + 1.0f);
     vec3 one = v3(1.0f, 1.0f, 1.0f);
-    return add3(scale3(one, 1.0f - t), scale3(v3(0.5f, 0.7f, 1.0f), t));
+    return madd3(scale3(one, 1.0f - t), v3(0.5f, 0.7f, 1.0f), t);
 }
 
 static int hit_aabb(ray r, vec3 bmin, vec3 bmax, float t_min, float t_max) {    /* :88-103 */
-    vec3 inv = v3(1.0f / r.dir.x, 1.0f / r.dir.y, 1.0f / r.dir.z);
+    vec3 inv = v3(rcp(r.dir.x), rcp(r.dir.y), rcp(r.dir.z));
     vec3 t0s = mul3(sub3(bmin, r.origin), inv);
     vec3 t1s = mul3(sub3(bmax, r.origin), inv);
     vec3 tmin = v3(fminf(t0s.x, t1s.x), fminf(t0s.y, t1s.y), fminf(t0s.z, t1s.z));
@@ -136,7 +183,7 @@ static int hit_triangle(ray r, vec3 v0, vec3 v1, vec3 v2,        /* :105-129 */
     vec3 ray_cross_e2 = cross3(r.dir, edge2);
     float det = dot3(edge1, ray_cross_e2);
     if (det > -0.00001f && det < 0.00001f) return 0;
-    float inv_det = 1.0f / det;
+    float inv_det = rcp(det);
     vec3 s = sub3(r.origin, v0);
     float u = inv_det * dot3(s, ray_cross_e2);
     if (u < 0.0f || u > 1.0f) return 0;
@@ -214,7 +261,7 @@ static int scatter(const unsigned char* m, uint32_t* seed, ray r_in,   /* :132-1
         vec3 reflected = reflect3(normalize3(r_in.dir), hit_normal);
         vec3 p = random_in_unit_sphere(seed);
         scattered->origin = hit_pos;
-        scattered->dir = normalize3(add3(reflected, scale3(p, fuzz)));
+        scattered->dir = normalize3(madd3(reflected, p, fuzz));
         *attenuation = albedo;
         return dot3(scattered->dir, hit_normal) > 0.0f;
     }
@@ -233,15 +280,15 @@ static int shade_pixel(const scene* s, const orc_camera* cam, int W, int H, int 
     uint32_t seed = (uint32_t)(py * W + px);                                   /* :164 */
     if (ext & ORC_EXT_ACCUMULATE)              /* extension: a new sample per frame (frame 0 = :164) */
         seed += (uint32_t)cam->frame_count * (uint32_t)(W * H);
-    float u = ((float)px + orc_random_float(&seed)) / (float)W;                /* :167 */
-    float v = ((float)(H - 1 - py) + orc_random_float(&seed)) / (float)H;      /* :168 */
+    float u = fdiv((float)px + orc_random_float(&seed), (float)W);             /* :167 */
+    float v = fdiv((float)(H - 1 - py) + orc_random_float(&seed), (float)H);   /* :168 */
     vec3 o = v3(cam->origin[0], cam->origin[1], cam->origin[2]);
     vec3 llc = v3(cam->lower_left[0], cam->lower_left[1], cam->lower_left[2]);
     vec3 hor = v3(cam->horizontal[0], cam->horizontal[1], cam->horizontal[2]);
     vec3 ver = v3(cam->vertical[0], cam->vertical[1], cam->vertical[2]);
     ray r;
     r.origin = o;
-    r.dir = normalize3(sub3(add3(add3(llc, scale3(hor, u)), scale3(ver, v)), o));     /* :173 */
+    r.dir = normalize3(sub3(madd3(madd3(llc, hor, u), ver, v), o));                 /* :173 */
 
     vec3 final_color = v3(0.0f, 0.0f, 0.0f);
     vec3 attenuation = v3(1.0f, 1.0f, 1.0f);

@@ -1,0 +1,110 @@
+#!/usr/bin/env python3
+"""The Vulkan tolerance envelope around the oracle.
+
+The reference's frame comes from a Vulkan driver, which the GLSL and SPIR-V
+specifications let choose, where this repo's contract fixes IEEE binary32:
+
+* contraction of a*b+c into an FMA: the executed SPIR-V carries no
+  NoContraction decoration (tests/golden/spirv_facts.json
+  "no_contraction_decorations": 0), so a driver may fuse every multiply-add;
+* normalize() through inversesqrt, whose precision is implementation-defined
+  (GLSL 4.50 §4.7.1: 2 ULP);
+* x / y through a reciprocal (2.5 ULP allowed), at compute_dynamic_ray.comp
+  :89 (1.0 / dir), :112 (1.0 / det), :167-168 (the AA jitter divided by W, H)
+  and inside normalize().
+
+This script renders BASELINE configs 2 and 3 and config 6 (the reference's
+FinalBaseMesh) as whole frames with the oracle under each of those choices
+(oracle/rt_envelope.c, liboracle_env.so, ENV_* bits) and records, against the
+contract's frame (liboracle.so, which the GPU matches bit for bit): the
+fraction of pixels whose float radiance stays within 1e-4 on every channel,
+within 1 LSB and identical in RGBA8, and the largest deviations.  Writes
+vulkan_envelope.json beside this script; tests/test_envelope.py re-derives
+its row subsets on the CPU.
+
+Variants (ENV_* bits): fma 1, rsq 2, rcp 4, ulp 8 (reciprocals and
+inversesqrts off by up to one ulp, chosen by a hash of the input), llvm 7 (a
+compiler that fuses, uses rsq and rcp: what an LLVM-based driver does with
+fast-math-style float lowering), llvm_ulp 15 (the same with approximate 1-ulp
+hardware rcp / rsq, the spec's worst case short of 2-2.5 ulp).
+
+Usage: python tests/golden/make_envelope.py [--threads N]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path[:0] = [os.path.join(ROOT, "3d-ray-tracer-vulkan_amd"), ROOT]
+
+VARIANTS = {"fma": 1, "rsq": 2, "rcp": 4, "ulp": 8, "llvm": 7, "llvm_ulp": 15}
+CONFIGS = (2, 3, 6)
+SUBSET_STEP = {2: 16, 3: 32, 6: 32}      # the rows tests/test_envelope.py re-derives
+TOL = 1e-4
+
+
+def stats(rgba, rad, rgba0, rad0) -> dict:
+    d = np.abs(rad.astype(np.float64) - rad0.astype(np.float64)).max(axis=-1)
+    q = np.abs(rgba.astype(np.int32) - rgba0.astype(np.int32)).max(axis=-1)
+    n = int(d.size)
+    return {
+        "pixels": n,
+        "within_1e-4": round(float((d <= TOL).mean()), 8),
+        "pixels_over_1e-4": int((d > TOL).sum()),
+        "rgba8_within_1lsb": round(float((q <= 1).mean()), 8),
+        "pixels_over_1lsb": int((q > 1).sum()),
+        "rgba8_identical": round(float((q == 0).mean()), 8),
+        "max_abs_radiance": float(d.max()),
+        "max_abs_rgba8": int(q.max()),
+    }
+
+
+def render(cfg, built, variant=None, row_step=1, threads=0):
+    from oracle import oracle_lib
+    cam = cfg.camera()
+    rgba, rad, _ = oracle_lib.render(built.model_vertex_data, built.model_material_data, built.flat_bvh_data,
+                                     cam.ubo_bytes(), cfg.width, cfg.height, cfg.max_bounces, row_step=row_step,
+                                     n_threads=threads, variant=variant)
+    return rgba, rad
+
+
+def envelope(k: int, row_step: int = 1, threads: int = 0, variants=VARIANTS) -> dict:
+    from rtamd import configs
+    cfg = configs.get(k)
+    built = cfg.build()
+    rgba0, rad0 = render(cfg, built, None, row_step, threads)
+    out = {}
+    for name, bits in variants.items():
+        rgba, rad = render(cfg, built, bits, row_step, threads)
+        out[name] = stats(rgba, rad, rgba0, rad0)
+    return {"config": cfg.name, "width": cfg.width, "height": cfg.height, "max_bounces": cfg.max_bounces,
+            "row_step": row_step, "variants": out}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--threads", type=int, default=0)
+    args = ap.parse_args()
+    res = {"what": __doc__.split("\n\n")[0], "tolerance": TOL, "variant_bits": VARIANTS, "configs": {},
+           "subsets": {}}
+    for k in CONFIGS:
+        t0 = time.time()
+        res["configs"][str(k)] = envelope(k, 1, args.threads)
+        res["subsets"][str(k)] = envelope(k, SUBSET_STEP[k], args.threads)
+        print(f"config {k}: {time.time() - t0:.1f} s", file=sys.stderr)
+    worst = min(v["within_1e-4"] for c in res["configs"].values() for v in c["variants"].values())
+    worst_lsb = min(v["rgba8_within_1lsb"] for c in res["configs"].values() for v in c["variants"].values())
+    res["summary"] = {"min_within_1e-4": worst, "min_rgba8_within_1lsb": worst_lsb}
+    with open(os.path.join(HERE, "vulkan_envelope.json"), "w") as fh:
+        json.dump(res, fh, indent=1)
+        fh.write("\n")
+    print(json.dumps(res["summary"]))
+
+
+if __name__ == "__main__":
+    main()

@@ -19,6 +19,8 @@ OUT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "spirv_facts.json
 
 OP_NAME, OP_TYPE_INT, OP_TYPE_FLOAT, OP_CONSTANT, OP_FUNCTION, OP_FUNCTION_END, OP_FUNCTION_CALL = 5, 21, 22, 43, 54, 56, 57
 OP_EXT_INST = 12
+OP_DECORATE, OP_MEMBER_DECORATE, DEC_NO_CONTRACTION = 71, 72, 42
+OP_FADD, OP_FSUB, OP_FMUL, OP_FDIV = 129, 131, 133, 136
 
 
 def main(path=SPV):
@@ -28,6 +30,9 @@ def main(path=SPV):
     names, types, consts = {}, {}, []
     calls, cur = {}, None
     ext = []
+    no_contraction = 0
+    float_ops = {"OpFAdd": 0, "OpFSub": 0, "OpFMul": 0, "OpFDiv": 0}
+    op_names = {OP_FADD: "OpFAdd", OP_FSUB: "OpFSub", OP_FMUL: "OpFMul", OP_FDIV: "OpFDiv"}
     i = 5
     while i < len(words):
         wc, op = words[i] >> 16, words[i] & 0xFFFF
@@ -56,6 +61,12 @@ def main(path=SPV):
             cur = None
         elif op == OP_FUNCTION_CALL and cur is not None:
             calls[cur].append(names.get(ins[3], str(ins[3])).split("(")[0])
+        elif op == OP_DECORATE and wc >= 3 and ins[2] == DEC_NO_CONTRACTION:
+            no_contraction += 1
+        elif op == OP_MEMBER_DECORATE and wc >= 4 and ins[3] == DEC_NO_CONTRACTION:
+            no_contraction += 1
+        elif op in op_names and cur is not None:
+            float_ops[op_names[op]] += 1
         elif op == OP_EXT_INST and cur is not None:
             ext.append({"function": cur, "glsl_std_450": ins[4]})
         i += wc
@@ -66,6 +77,10 @@ def main(path=SPV):
         "constants": consts,
         "calls": calls,
         "glsl_std_450_ops": ext,
+        # GLSL `precise` becomes NoContraction; none means a driver may fuse
+        # every multiply-add into an FMA (tests/golden/make_envelope.py)
+        "no_contraction_decorations": no_contraction,
+        "float_arith_ops": float_ops,
     }
     json.dump(facts, open(OUT, "w"), indent=1)
     print(f"wrote {OUT}: {len(consts)} constants, {len(calls)} functions")

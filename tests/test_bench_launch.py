@@ -57,6 +57,7 @@ class _Out:
 def test_launch_relays_rank0_only(tmp_path):
     script = _child(tmp_path, """
         import json, os
+        print("[Gloo] Rank 0 is connected to 2 peer ranks", flush=True)    # not JSON: goes to stderr
         print(json.dumps({k: os.environ[k] for k in ("RANK", "WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT")}),
               flush=True)
     """)

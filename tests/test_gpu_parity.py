@@ -2,8 +2,13 @@
 
 Bar: bit-exact RGBA8 and bit-exact float radiance (the sqrt'd colour before
 quantisation), and identical work counters (segments, BVH node visits,
-triangle tests, material reads), on the same buffers and camera.  North-star
-tolerance (1e-4 per channel) is thereby met with zero deviation.
+triangle tests, material reads), on the same buffers and camera.  That is
+zero deviation from this repo's IEEE contract, not from a real
+Vulkan frame: a Vulkan driver may contract multiply-adds, normalize through
+inversesqrt and divide through a reciprocal, and the study of those choices
+(tests/golden/vulkan_envelope.json, tests/test_envelope.py) puts at least
+99.998 % of pixels within 1e-4 per channel of the contract's frame (configs
+2, 3 and 6), the rest being a few dozen chaotic path flips per frame.
 """
 import numpy as np
 import pytest
