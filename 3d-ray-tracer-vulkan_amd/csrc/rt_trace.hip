@@ -940,16 +940,20 @@ void trace_simple(TraceArgs a) {
         if (a.diag_lane)
             a.diag_lane[((size_t)(blockIdx.y * gridDim.x + blockIdx.x) * a.block_waves + wave) * 64 + lane] =
                 (unsigned)(d_iters + 2 * d_lane_windows);
+        // the lanes' own lockstep steps, summed (the useful lane-steps of
+        // the wave's lockstep walk: lane utilisation = sum / (64 x word 4))
+        unsigned long long d_sum = d_iters;
 #pragma unroll
-        for (int off = 32; off > 0; off >>= 1) {   // the wave's iterations = the longest lane's
-            const unsigned long long o2 = __shfl_xor(d_iters, off);
+        for (int off = 32; off > 0; off >>= 1) {
+            d_sum += __shfl_xor(d_sum, off);
+            const unsigned long long o2 = __shfl_xor(d_iters, off);   // the wave's iterations = the longest lane's
             d_iters = o2 > d_iters ? o2 : d_iters;
         }
         if (lane == 0) {
             drec[4] = d_iters;
             drec[5] = d_windows;
             drec[6] = d_coop_t;
-            drec[7] = 0;
+            drec[7] = d_sum;
         }
     }
 }

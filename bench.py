@@ -50,24 +50,23 @@ over ranks), in millions.  A segment is one executed bounce-loop iteration
 (compute_dynamic_ray.comp:179-232); its count per frame is deterministic and is
 taken from a counting pass outside the timed region.
 
-roofline: the walk is bound by the issue of its vector memory
-instructions (the texture addresser / data path), not by HBM
-bandwidth (the 8-MB scene stays in L2 / MALL).  bound "vmem_issue":
-achieved = SQ_INSTS_VMEM_RD per launch (PMC, tools/pmc.sh, committed in
-profiles/pmc_latest.json for this config) / frame_ms_device, the device time
-per launch of the running loop (HIP events from before the first launch to
-the last event of every stream, divided by the launches); peak
-= CUs / TA_NS_PER_VMEM, the measured floor of one wave-level
-global_load_dwordx4 per CU (tools/ubench/ta_cost.hip,
-profiles/r02/walks/ubench_ta_cost.txt:1); frac = achieved / peak.  Beside it:
-"hbm" = the PMC HBM bytes per launch (FETCH_SIZE, corrected) over the same
-time against 8 TB/s, and "algorithmic" = the contract's algorithmic bytes
-(32 B per BVH node visit + 36 B per triangle test + 16 B per material read +
-4 B per pixel) over that time against 8 TB/s, which can exceed 1 because
-those bytes are cache hits.  kernel_ms is the mean duration of one launch
-(HIP events on its own stream; what rocprofv3 reports per kernel); with D
-launches in flight they overlap, and kernel_ms / frame_ms_device is the
-average number running at once.
+roofline, the frame kernel trace_simple: bound "hbm",
+achieved = the algorithmic bytes of one launch (32 B per BVH
+node visit + 36 B per triangle test + 16 B per material read + 4 B per pixel,
+from the reference's own visit counts) / kernel_ms, the mean duration of one
+launch (HIP events around every timed launch on the stream it runs on; what
+rocprofv3 reports per kernel); peak = 8 TB/s; traffic = the PMC HBM bytes per
+launch (FETCH_SIZE x 1024 x 2, tools/pmc.sh, profiles/pmc_latest.json) when
+a PMC record of this config AND camera path exists, else null.  With D
+launches in flight the launches overlap (kernel_ms / frame_ms_device is the
+average number running at once), so "views" restates the same bytes over
+frame_ms_device, the device time per launch of the running loop, against the
+HBM and the L2 peaks (the scene stays in L2 / MALL: those bytes are mostly
+cache hits), the measured HBM rate (PMC bytes / frame_ms_device), the
+vector-memory issue rate (SQ_INSTS_VMEM_RD against a floor measured by
+tools/ubench/ta_cost.hip, a builder's microbenchmark, not a guide figure) and
+the lockstep walk's lane utilisation (a diagnostic launch outside the timed
+region: the lanes' own walk steps / (64 x the waves' lockstep steps)).
 cpu_baseline: the CPU oracle (oracle/rt_oracle.c, OpenMP) on a bounded row
 sample of the same frame, rank 0 at N = 1 only (the reference has no CPU
 render path: BVHNode.hit throws, BVHNode.java:35-41).
@@ -91,6 +90,7 @@ sys.path.insert(0, os.path.join(ROOT, "3d-ray-tracer-vulkan_amd"))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0      # MI355X HBM3E, MI355X_MICROARCH.md chip table
+L2_PEAK_GBS = 34500.0      # the 8 XCDs' L2 together, MI355X_MICROARCH.md § L2 (per XCD): ≈34.5 TB/s
 # ns of the vector memory pipeline per wave-level global_load_dwordx4 per CU
 # when every lane reads one address: the cheapest form a walk step's loads take
 # (tools/ubench/ta_cost.hip; profiles/r02/walks/ubench_ta_cost.txt:1, 7.39 ns
@@ -336,6 +336,7 @@ def main() -> None:
                          "into the main stream around the region (two cross-queue hops)")
     ap.add_argument("--set", default="", help="schedule options name=value,... (rt_set_option) before timing")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-lanes", action="store_true", help="skip the lane-utilisation diagnostic launch")
     ap.add_argument("--no-single", action="store_true", help="N > 1: skip rank 0's one-GPU timing")
     ap.add_argument("--no-pcie", action="store_true", help="N = 1: skip the PCIe-inclusive rt_render_async rate")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU baseline sample time")
@@ -786,6 +787,8 @@ def main() -> None:
 
     heavy_used = renderer.get_option("heavy_tiles_used")   # of the last timed launch
     heavy_px_used = renderer.get_option("heavy_pixels_used")
+    lanes = lane_utilisation(renderer, L, ctx, lambda: trace(k_t0, 1, main_stream, count_rgba.data_ptr(), None),
+                             dev) if not args.no_lanes else None
     verified = None
     single = None
     if dist_on and not emu and rank == 0 and last["rgba"] is not None:
@@ -872,8 +875,9 @@ def main() -> None:
     alg_bytes = 32.0 * l_nodes + 36.0 * l_tris + 16.0 * l_mats + 4.0 * l_pix
     ref_layout_bytes = 48.0 * l_nodes + 48.0 * l_tris + 16.0 * l_mats + 4.0 * l_pix
     n_cu = torch.cuda.get_device_properties(dev).multi_processor_count
-    pmc = load_pmc(args.pmc_json, cfg.name) if (mode == "whole" and F == 1) else None
-    roof = roofline(pmc, alg_bytes, ref_layout_bytes, l_seg, frame_ms, n_cu)
+    # PMC only from a record of this config and camera path (pmc_key)
+    pmc = load_pmc(args.pmc_json, pmc_key(cfg.name, args.camera_path)) if (mode == "whole" and F == 1) else None
+    roof = roofline(pmc, alg_bytes, ref_layout_bytes, l_seg, launch_ms, frame_ms, n_cu, lanes)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -1017,6 +1021,42 @@ def pcie_rate(renderer, cam, W, H, B, n=200, warm=8):
                     f"(readback overlapped with later traces); the rate a host displaying the frames sees"}
 
 
+def lane_utilisation(renderer, L, ctx, launch, dev):
+    """One diagnostic launch of the first timed frame (option diag; outside the
+    timed region): per wave, its lockstep steps (diag word 4), cooperative
+    windows (5) and its lanes' own steps summed (7).  Lane utilisation = lane
+    steps / (64 x wave steps), over the tile waves (the heavy pixels' one-pixel
+    waves record zeros)."""
+    import numpy as np
+    import torch
+    from rtamd._lib import check
+    renderer.set_option("diag", 1)
+    try:
+        launch()
+        torch.cuda.synchronize(dev)
+        n = C.c_size_t()
+        check(L.rt_diag_copy(ctx, None, 0, C.byref(n)))
+        buf = np.zeros(max(8, n.value), np.uint64)
+        check(L.rt_diag_copy(ctx, buf.ctypes.data, n.value, C.byref(n)))
+    finally:
+        renderer.set_option("diag", 0)
+    rec = buf[: n.value // 8 * 8].reshape(-1, 8).astype(np.float64)
+    steps, lane_steps, wins = rec[:, 4].sum(), rec[:, 7].sum(), rec[:, 5].sum()
+    tile = rec[:, 4] > 0
+    return {"lockstep_lane_utilisation": round(lane_steps / (64.0 * steps), 4) if steps else None,
+            "lane_steps": int(lane_steps), "wave_steps": int(steps), "coop_windows": int(wins),
+            "tile_waves_walking": int(tile.sum()),
+            "what": "a diagnostic launch of the first timed frame in the learned order (heavy pixels split out): "
+                    "the lanes' own lockstep walk steps / (64 x the waves' lockstep steps), tile waves only; "
+                    "coop_windows = 64-node windows of the cooperative tail"}
+
+
+def pmc_key(config_name: str, camera_path: str) -> str:
+    """The key of a PMC record in profiles/pmc_latest.json: the config, and
+    the camera path unless it is the static default camera."""
+    return config_name if camera_path == "static" else f"{config_name}@{camera_path}"
+
+
 def load_pmc(path, config_name):
     """PMC per launch for config_name from profiles/pmc_latest.json
     (tools/pmc_traffic.py), or None."""
@@ -1027,38 +1067,61 @@ def load_pmc(path, config_name):
     return tj.get("configs", {}).get(config_name)
 
 
-def roofline(pmc, alg_bytes, ref_layout_bytes, l_seg, frame_ms, n_cu):
-    """The roofline object of the JSON line (module docstring): the vector
-    memory issue bound from PMC, with the HBM and algorithmic figures."""
-    t = frame_ms * 1e-3                                     # s per launch of the running loop
+def roofline(pmc, alg_bytes, ref_layout_bytes, l_seg, kernel_ms, frame_ms, n_cu, lanes=None):
+    """The roofline object of the JSON line (module docstring): the contract's
+    HBM roofline of the frame kernel, then the same bytes and the counters in
+    other views."""
+    tk = kernel_ms * 1e-3                                   # s per launch (its own duration)
+    tf = frame_ms * 1e-3                                    # s per launch of the running loop
     vmem = pmc.get("SQ_INSTS_VMEM_RD") if pmc else None
     traffic = pmc.get("hbm_bytes_per_launch") if pmc else None
-    peak = n_cu / TA_NS_PER_VMEM                            # G wave-instructions / s
-    achieved = vmem / t / 1e9 if vmem else None
-    hbm = traffic / t / 1e9 if traffic else None
-    alg = alg_bytes / t / 1e9
+    achieved = alg_bytes / tk / 1e9
+    alg_dev = alg_bytes / tf / 1e9
+    issue_peak = n_cu / TA_NS_PER_VMEM                      # G wave-instructions / s
+    issue = vmem / tf / 1e9 if vmem else None
     return {
-        "bound": "vmem_issue",
-        "achieved": round(achieved, 3) if achieved else None,
-        "peak": round(peak, 3),
-        "unit": "G wave-level vector-memory instructions/s",
-        "frac": round(achieved / peak, 4) if achieved else None,
+        "bound": "hbm",
+        "achieved": round(achieved, 1),
+        "peak": HBM_PEAK_GBS,
+        "unit": "GB/s",
+        "frac": round(achieved / HBM_PEAK_GBS, 4),
         "traffic": traffic,
-        "basis": f"achieved = SQ_INSTS_VMEM_RD per launch ({vmem}, PMC) / frame_ms_device; peak = {n_cu} CUs / "
-                 f"{TA_NS_PER_VMEM} ns per wave-level global_load_dwordx4 per CU ({TA_NS_SOURCE}); traffic = PMC "
-                 f"HBM bytes per launch (FETCH_SIZE x 1024 x 2). null without a PMC record of this config "
-                 f"(profiles/pmc_latest.json) or for N > 1 shares",
+        "basis": "achieved = algorithmic bytes per launch (SURVEY.md §8d: 32 B per BVH node visit + 36 B per "
+                 "triangle test + 16 B per material read + 4 B per pixel, the reference's visit counts) / kernel_ms "
+                 "(the mean launch duration, HIP events on each launch's own stream over the timed region); peak = "
+                 "8 TB/s HBM (MI355X_MICROARCH.md); traffic = PMC HBM bytes per launch (FETCH_SIZE x 1024 x 2, "
+                 "tools/pmc.sh) of this config and camera path, null without such a record",
         "pmc_source": pmc.get("source") if pmc else None,
-        "vmem_rd_per_launch": vmem,
-        "vmem_rd_per_segment": round(vmem / l_seg, 3) if vmem else None,
-        "hbm": {"achieved": round(hbm, 1) if hbm else None, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(hbm / HBM_PEAK_GBS, 4) if hbm else None},
-        "algorithmic": {"bytes_per_launch": int(alg_bytes), "bytes_per_segment": round(alg_bytes / l_seg, 1),
-                        "achieved": round(alg, 1), "unit": "GB/s",
-                        "alg_throughput_frac": round(alg / HBM_PEAK_GBS, 4),
-                        "reference_layout_frac": round(ref_layout_bytes / t / 1e9 / HBM_PEAK_GBS, 4),
-                        "note": "the reference's visit counts x record sizes (SURVEY.md §8d) over the launch time; "
-                                "mostly L2/MALL hits, so it can exceed the HBM peak"},
+        "alg_bytes_per_launch": int(alg_bytes),
+        "alg_bytes_per_segment": round(alg_bytes / l_seg, 1),
+        "reference_layout_bytes_per_launch": int(ref_layout_bytes),
+        "traffic_over_alg": round(traffic / alg_bytes, 4) if traffic else None,
+        "views": {
+            "device_time": {
+                "what": "the same algorithmic bytes over frame_ms_device (the device time per launch of the running "
+                        "loop, launches overlapping): mostly L2 / MALL hits, so against the L2 peak too",
+                "achieved": round(alg_dev, 1), "unit": "GB/s",
+                "hbm_frac": round(alg_dev / HBM_PEAK_GBS, 4),
+                "l2_peak": L2_PEAK_GBS, "l2_frac": round(alg_dev / L2_PEAK_GBS, 4),
+                "reference_layout_hbm_frac": round(ref_layout_bytes / tf / 1e9 / HBM_PEAK_GBS, 4),
+            },
+            "hbm_measured": {
+                "what": "PMC HBM bytes per launch over frame_ms_device: the HBM rate the running loop draws",
+                "achieved": round(traffic / tf / 1e9, 1) if traffic else None, "unit": "GB/s",
+                "frac": round(traffic / tf / 1e9 / HBM_PEAK_GBS, 4) if traffic else None,
+            },
+            "vmem_issue": {
+                "what": f"SQ_INSTS_VMEM_RD per launch (PMC) over frame_ms_device against {n_cu} CUs / "
+                        f"{TA_NS_PER_VMEM} ns per wave-level global_load_dwordx4 per CU (a builder-measured floor, "
+                        f"{TA_NS_SOURCE}; not a guide figure)",
+                "achieved": round(issue, 3) if issue else None, "peak": round(issue_peak, 3),
+                "unit": "G wave-level vector-memory instructions/s",
+                "frac": round(issue / issue_peak, 4) if issue else None,
+                "vmem_rd_per_launch": vmem,
+                "vmem_rd_per_segment": round(vmem / l_seg, 3) if vmem else None,
+            },
+            "lane_utilisation": lanes,
+        },
     }
 
 

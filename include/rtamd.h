@@ -347,7 +347,10 @@ int rt_set_option(rt_ctx* ctx, const char* name, int64_t value);
 /* Diagnostics: with option "diag" = 1, the kernel records per wave
  * 8 words: {start, end} (s_memrealtime, 100 MHz), {XCC id << 32 | HW_ID},
  * {block << 8 | wave}, {lockstep walk iterations}, {cooperative windows},
- * {ticks spent in the cooperative tail}, {0} into a device buffer;
+ * {ticks spent in the cooperative tail}, {the lanes' own lockstep steps,
+ * summed over the wave} into a device buffer (a heavy pixel's one-pixel wave
+ * leaves words 4-7 zero; lane utilisation of the lockstep walk = sum of word 7
+ * / (64 x sum of word 4));
  * rt_diag_copy copies up to cap_words 64-bit words of the last launch
  * (n_words = words recorded).  Not for timing runs. */
 int rt_diag_copy(rt_ctx* ctx, void* dst, size_t cap_words, size_t* n_words);

@@ -74,6 +74,13 @@ JNIEXPORT void JNICALL Java_dev_demir_vulkan_engine_HipNative_waitFrame(JNIEnv* 
     int rc = rt_render_wait((rt_ctx*)(intptr_t)ctx, (uint64_t)t);
     if (rc) throw_rt(env, rc);
 }
+/* boolean pollFrame(long ctx, long ticket): true when the frame is complete (never blocks) */
+JNIEXPORT jboolean JNICALL Java_dev_demir_vulkan_engine_HipNative_pollFrame(JNIEnv* env, jclass c, jlong ctx, jlong t) {
+    int done = 0;
+    int rc = rt_render_poll((rt_ctx*)(intptr_t)ctx, (uint64_t)t, &done);
+    if (rc) { throw_rt(env, rc); return JNI_FALSE; }
+    return done ? JNI_TRUE : JNI_FALSE;
+}
 
 /* Extension: void uploadSpheres(long ctx, float[] spheres8n) — centre.xyz, radius, albedo.rgb, type per sphere.
  * Then setOption(ctx, "extensions", 8) turns them on. */

@@ -14,6 +14,7 @@ final class HipNative {
     static native void freeFrame(ByteBuffer frame);
     static native long renderAsync(long ctx, ByteBuffer ubo80, int w, int h, int maxBounces, ByteBuffer pinnedOut);
     static native void waitFrame(long ctx, long ticket);
+    static native boolean pollFrame(long ctx, long ticket);       // rt_render_poll: never blocks
     static native void uploadSpheres(long ctx, float[] spheres8n);   // extension (option "extensions" bit 8)
     static native void setOption(long ctx, String name, long value);
     static native long getOption(long ctx, String name);

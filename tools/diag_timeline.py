@@ -97,10 +97,10 @@ def main():
         print(f"  slow wave block {blk[k]}: {dur[k] / 100:.0f} us, {iters[k]} lockstep iters "
               f"({lock_t / 100 / max(1, iters[k]) * 1000:.0f} ns each incl. shading), "
               f"{wins[k]} coop windows in {coop_t[k] / 100:.0f} us")
-    ho = rec[:, 7].astype(np.int64)
-    if (ho > 0).any():
-        hot = (ho[ho > 0] - base) / 100
-        print(f"tile waves that handed on: {(ho > 0).sum()}, at us p0 {hot.min():.0f} p50 {np.median(hot):.0f} max {hot.max():.0f}")
+    lane_steps = rec[:, 7].astype(np.int64)          # word 7: the lanes' own lockstep steps, summed
+    if iters.sum() > 0:
+        print(f"lockstep lane utilisation: {lane_steps.sum() / (64.0 * iters.sum()):.3f} "
+              f"({lane_steps.sum()} lane-steps over {iters.sum()} wave-steps)")
     if len(help_rec):
         hs, he = (help_rec[:, 0].astype(np.int64) - base) / 100, (help_rec[:, 1].astype(np.int64) - base) / 100
         rays = help_rec[:, 4].astype(np.int64)
