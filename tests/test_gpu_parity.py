@@ -865,8 +865,11 @@ def test_render_async_accumulation_and_copy_toggle(slots, toggle):
     frames still reach the sums in frame_count order (the runtime serialises
     the slots' traces then), so every frame equals the oracle's accumulated
     frame.  toggle: copy_streams flips between 1 and 2 from frame to frame and
-    every wait still returns a complete frame (copied2 is recorded for every
-    frame)."""
+    every wait still returns a complete frame: copied2 is recorded only for
+    the frames whose readback splits, and a wait covers its own split frame's
+    second half through the oldest split frame at or after it
+    (test_gpu_pipeline.test_split_wait_covers_only_its_frame: it does not wait
+    for newer frames)."""
     if not has_gpu():
         pytest.skip("no GPU")
     import rtamd
