@@ -163,8 +163,9 @@ int build_host_scene(const void* vertices, size_t vertex_bytes,
                      HostScene* out, const char** err);
 void free_host_scene(HostScene* s);
 
-// Kernel launcher (rt_trace.hip).
-hipError_t launch_trace(const TraceArgs& a, hipStream_t stream);
+// Kernel launcher (rt_trace.hip).  *kernels (nullable) = the kernels it
+// enqueued (2 when the heavy tiles run as a launch of their own).
+hipError_t launch_trace(const TraceArgs& a, hipStream_t stream, int* kernels = nullptr);
 
 void set_error(const char* fmt, ...);
 

@@ -271,7 +271,8 @@ struct PerDevice {
     int          last_heavy_px = 0; // heavy pixels of the last launch (option "heavy_pixels_used", read only)
     // option graph: plain launches captured once per launch key into a HIP
     // graph and replayed (the heavy-tile fork / join becomes graph edges)
-    struct Graph { std::vector<uint64_t> key; hipGraphExec_t exec; };
+    struct Graph { std::vector<uint64_t> key; hipGraphExec_t exec; int kernels; };
+    uint64_t     plain_kernels = 0;  // production-build kernels enqueued (option "plain_kernels", read only)
     struct BandList { std::vector<int> bands; int* d; };
     std::vector<BandList> band_lists;   // rt_render_batch_device's band lists on this device
     std::vector<Graph> graphs;
@@ -707,19 +708,23 @@ static int launch(const rt_ctx* ctx, PerDevice& p, const TraceArgs& a, hipStream
     // heavy_stream 1) gains from a graph: its fork and join become edges.  A
     // single launch (the fused heavy tiles, or none) goes straight to the
     // stream: a graph launch adds ~9 us between frames (profiles/r02/graph).
+    const bool plain = !a.counters && !a.diag;          // the production build (option "plain_kernels")
+    int nk = 1;
     if (!ctx->graph || s == nullptr || a.counters || a.diag || !a.aux_stream) {
-        RT_HIP_CHECK(launch_trace(a, s));
+        RT_HIP_CHECK(launch_trace(a, s, &nk));
+        if (plain) p.plain_kernels += (uint64_t)nk;
         return RT_OK;
     }
     std::vector<uint64_t> key = launch_key(a, s);
     for (auto& g : p.graphs)
         if (g.key == key) {
             RT_HIP_CHECK(hipGraphLaunch(g.exec, s));
+            p.plain_kernels += g.kernels;
             return RT_OK;
         }
     hipGraph_t graph = nullptr;
     RT_HIP_CHECK(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
-    const hipError_t le = launch_trace(a, s);
+    const hipError_t le = launch_trace(a, s, &nk);
     const hipError_t ce = hipStreamEndCapture(s, &graph);
     if (le != hipSuccess || ce != hipSuccess) {
         if (graph) (void)hipGraphDestroy(graph);
@@ -733,11 +738,12 @@ static int launch(const rt_ctx* ctx, PerDevice& p, const TraceArgs& a, hipStream
     if (p.graphs.size() >= kMaxGraphs) {          // replace the oldest-inserted entry
         const size_t k = p.graph_next++ % kMaxGraphs;
         (void)hipGraphExecDestroy(p.graphs[k].exec);
-        p.graphs[k] = PerDevice::Graph{std::move(key), exec};
+        p.graphs[k] = PerDevice::Graph{std::move(key), exec, nk};
     } else {
-        p.graphs.push_back(PerDevice::Graph{std::move(key), exec});
+        p.graphs.push_back(PerDevice::Graph{std::move(key), exec, nk});
     }
     RT_HIP_CHECK(hipGraphLaunch(exec, s));
+    p.plain_kernels += (uint64_t)nk;
     return RT_OK;
 }
 
@@ -1639,6 +1645,7 @@ int rt_get_option(rt_ctx* ctx, const char* name, int64_t* value) {
     else if (std::strcmp(name, "heavy_pixel_factor") == 0) *value = ctx->heavy_pixel_factor;
     else if (std::strcmp(name, "heavy_pixels_used") == 0) *value = ctx->dev.empty() ? 0 : ctx->dev[0].last_heavy_px;
     else if (std::strcmp(name, "heavy_tiles_used") == 0) *value = ctx->dev.empty() ? 0 : ctx->dev[0].last_heavy;
+    else if (std::strcmp(name, "plain_kernels") == 0) *value = ctx->dev.empty() ? 0 : (int64_t)ctx->dev[0].plain_kernels;
     else if (std::strcmp(name, "extensions") == 0) *value = ctx->ext;
     else if (std::strcmp(name, "hw_queues") == 0) *value = ctx->hw_queues;
     else if (std::strcmp(name, "order_frames") == 0) *value = ctx->order_frames;

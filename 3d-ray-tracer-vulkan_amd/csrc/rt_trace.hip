@@ -960,7 +960,8 @@ void trace_simple(TraceArgs a) {
 
 }  // namespace
 
-hipError_t launch_trace(const TraceArgs& a, hipStream_t stream) {
+hipError_t launch_trace(const TraceArgs& a, hipStream_t stream, int* kernels) {
+    if (kernels) *kernels = 1;
     const int tw_w = 8 << a.wave_tile, th_w = 8 >> a.wave_tile, bw = a.block_waves;
     const int tiles_y = (a.th + th_w - 1) / th_w;       // wave-tile rows of one frame
     dim3 grid((a.tw + bw * tw_w - 1) / (bw * tw_w), a.n_frames * tiles_y);
@@ -1023,6 +1024,7 @@ hipError_t launch_trace(const TraceArgs& a, hipStream_t stream) {
             e = hipGetLastError();
             if (e == hipSuccess && a.aux_stream) e = hipEventRecord(a.ev_join, a.aux_stream);
             if (e != hipSuccess) return e;
+            if (kernels) *kernels = 2;
             ao.tile_order = a.tile_order + H;
             if (a.diag) ao.diag = a.diag + (size_t)kDiagWords * gh.x;
             grid = dim3(n_tiles - H);

@@ -731,6 +731,7 @@ def main() -> None:
         dist.barrier()
     torch.cuda.synchronize(dev)
     lean = args.bracket == "lean"
+    pk_start = renderer.get_option("plain_kernels")
     gc.disable()                                       # no collector pause between the timed launches
     t_start = time.perf_counter()
     if lean:
@@ -760,6 +761,7 @@ def main() -> None:
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t_start
     gc.enable()
+    pk_timed = renderer.get_option("plain_kernels")
     n_launch = len(evs)
     launch_ms = float(np.mean([a.elapsed_time(b) for (a, b), _ in evs]))
     region_ms = (max(reg[0].elapsed_time(e) for e in ends) if lean else reg[0].elapsed_time(reg[1]))
@@ -883,6 +885,9 @@ def main() -> None:
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(built, cam_of(k_t0), W, H, B, segments / K, args.cpu_seconds, gpu_frame)
 
+    # production kernels enqueued after the timed region (verification, camera
+    # stop): tools/rocprof_union.py cuts them off the end of a kernel trace
+    pk_after = renderer.get_option("plain_kernels") - pk_timed
     if rank == 0 or emu:
         gather_kind = "RCCL" if backend == "nccl" else (backend or "none")
         shared = " (ranks share one GPU: rehearsal)" if os.environ.get("BENCH_SHARE_GPU") else ""
@@ -963,6 +968,8 @@ def main() -> None:
                           "every stream (bracket lean) or main stream around the region after joining every launch "
                           "stream (bracket join), / launches",
                 "bracket": args.bracket,
+                "plain_kernels_timed": pk_timed - pk_start,
+                "plain_kernels_after_timed": pk_after,
             },
             "per_rank": per_rank,
             "primary_mrays_s": round(pixels / elapsed / 1e6, 2),

@@ -333,6 +333,10 @@ int rt_render_poll(rt_ctx* ctx, uint64_t ticket, int* done);
  *                   8 = spheres (rt_upload_spheres) after the BVH walk
  *   "async_slots"   rt_render_async frames in flight per device (1..8, default 4)
  *   "copy_streams"  rt_render_async readback copy streams (1 or 2, default 1)
+ *   "plain_kernels" (rt_get_option only) production-build trace kernels enqueued
+ *                   on device 0 so far (not counting, diagnostic or learning
+ *                   launches): lets a profiler's kernel trace be cut at a
+ *                   caller's region (bench.py, tools/rocprof_union.py)
  *   "hw_queues"     (rt_get_option only) GPU_MAX_HW_QUEUES as seen by rt_create
  *                   (4, HIP's default, when unset)
  *   "queues_short"  (rt_get_option only) 1 when async_slots + 2 > hw_queues:

@@ -3,8 +3,9 @@
 
 With D frames in flight the trace launches overlap, so no single kernel's
 duration is the frame time.  This takes the timed region's launches (the
-last K plain launches of trace_simple: bench.py's K timed steps are its last
-plain launches at N = 1; counting launches are trace_simple<true, ...> and
+last K plain launches of trace_simple before the bench line's
+roofline.plain_kernels_after_timed trailing ones (verification, camera stop;
+the library counts them, option plain_kernels); counting launches are trace_simple<true, ...> and
 learning launches trace_simple<false, true, ...>), and reports:
 
   union_ms      the union of their [start, end) intervals: time the device
@@ -46,13 +47,23 @@ def main():
     ap.add_argument("--launches-per-step", type=int, default=1)
     ap.add_argument("--bench", default="", help="the run's bench.py JSON line (file)")
     ap.add_argument("--out", default="")
+    ap.add_argument("--skip-last", type=int, default=-1,
+                    help="plain launches after the timed region (default: the bench line's "
+                         "roofline.plain_kernels_after_timed, else 0)")
     args = ap.parse_args()
     rows = [r for r in csv.DictReader(open(args.trace)) if "trace_simple<false, false" in r["Kernel_Name"]]
     rows.sort(key=lambda r: int(r["Dispatch_Id"]))
     n = args.steps * args.launches_per_step
     if len(rows) < n:
         raise SystemExit(f"{len(rows)} plain trace launches in the trace, need {n}")
-    timed = rows[-n:]
+    skip = args.skip_last
+    if args.bench and skip < 0:
+        line = [x for x in open(args.bench) if x.startswith("{")][-1]
+        skip = json.loads(line).get("roofline", {}).get("plain_kernels_after_timed", 0) or 0
+    skip = max(0, skip)
+    if len(rows) < n + skip:
+        raise SystemExit(f"{len(rows)} plain trace launches in the trace, need {n} + {skip} after them")
+    timed = rows[len(rows) - skip - n:len(rows) - skip]
     iv = [(int(r["Start_Timestamp"]), int(r["End_Timestamp"])) for r in timed]
     durs = [(e - s) / 1e6 for s, e in iv]
     union = union_length(iv) / 1e6

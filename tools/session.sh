@@ -14,6 +14,8 @@
 #   pmc3      PMC passes A (SQ instruction counts) and C (FETCH_SIZE) of
 #             config 3, merged into gpurun_out/TAG/pmc_latest.json
 #   pmc5      the same for config 5
+#   pmc3o     the same for config 3 with the orbiting camera (record key cfg3_...@orbit)
+#   orbit     bench.py --camera-path orbit at 20 steps
 #   cfgs      bench.py on configs 4, 5, 6
 #   share     tools/share_inflight_bench.py (one rank's share, frames in flight)
 #   emu       tools/rank_emulator.py (one rank of N with its exchange; $EMU_ARGS)
@@ -48,15 +50,20 @@ prof() {  # prof CONFIG STEPS
       > /dev/null 2>> "$OUT/status.txt" || status "rocprof_union cfg$c failed"
   cp "$(find "$d" -name "run_kernel_stats.csv" | head -n 1)" "$OUT/kernel_stats_cfg$c.csv" 2>/dev/null || true
 }
-pmc() {  # pmc CONFIG NAME
-  local c=$1 name=$2
-  PMC_PASSES="A C" BENCH_ARGS="--config $c" bash tools/pmc.sh "${TAG}_pmc$c" || exit $?
-  cp -r "gpurun_out/${TAG}_pmc$c" "$OUT/pmc$c"
-  python3 tools/pmc_traffic.py "gpurun_out/${TAG}_pmc$c" "trace_simple<false, false" --config "$name" \
-      --source "profiles/r03/$TAG/pmc$c (tools/pmc.sh passes A and C, bench.py --config $c)" \
-      --merge "$OUT/pmc_latest.json" > "$OUT/pmc$c.json" 2>> "$OUT/status.txt" || status "pmc_traffic cfg$c failed"
+pmc() {  # pmc CONFIG NAME [SUFFIX EXTRA_BENCH_ARGS]
+  local c=$1 name=$2 sfx=${3:-} extra=${4:-}
+  PMC_PASSES="A C" BENCH_ARGS="--config $c $extra" bash tools/pmc.sh "${TAG}_pmc$c$sfx" || exit $?
+  cp -r "gpurun_out/${TAG}_pmc$c$sfx" "$OUT/pmc$c$sfx"
+  python3 tools/pmc_traffic.py "gpurun_out/${TAG}_pmc$c$sfx" "trace_simple<false, false" --config "$name" \
+      --source "profiles/r04/$TAG/pmc$c$sfx (tools/pmc.sh passes A and C, bench.py --config $c $extra)" \
+      --merge "$OUT/pmc_latest.json" > "$OUT/pmc$c$sfx.json" 2>> "$OUT/status.txt" || status "pmc_traffic cfg$c$sfx failed"
+  cp "$OUT/pmc_latest.json" profiles/pmc_latest.json
 }
 rocminfo 2>/dev/null | grep -m1 -E "gfx950" > "$OUT/rocminfo.txt"
+# PMC records accumulate onto the committed ones; after a pmc step the box's
+# profiles/pmc_latest.json is the merged file, so later bench steps of the
+# session attach the fresh records (copy gpurun_out/TAG/pmc_latest.json back)
+[ -f "$OUT/pmc_latest.json" ] || cp profiles/pmc_latest.json "$OUT/pmc_latest.json"
 for s in "$@"; do
   case $s in
     test)     run pytest 1200 python -u -m pytest tests -m gpu -q -rA --timeout 120 --timeout-method thread \
@@ -68,6 +75,9 @@ for s in "$@"; do
     prof5)    prof 5 10 ;;
     pmc3)     pmc 3 cfg3_50k_1920x1080_b4 ;;
     pmc5)     pmc 5 cfg5_1M_3840x2160_b8 ;;
+    pmc3o)    pmc 3 cfg3_50k_1920x1080_b4@orbit o "--camera-path orbit" ;;
+    orbit)    run orbit 600 python bench.py --steps 20 --warmup 5 --camera-path orbit \
+                  > "$OUT/bench_orbit.json" 2> "$OUT/bench_orbit.err" ;;
     cfgs)     for a in "4 50" "5 10" "6 200"; do
                 set -- $a
                 run "cfg$1" 300 python bench.py --config "$1" --steps "$2" --warmup 3 --no-cpu-baseline \
