@@ -1,10 +1,15 @@
 """CPU checks of bench.py's host-side arithmetic against the committed evidence.
 
 The roofline in a bench.py JSON line must follow from the files under
-profiles/: SQ_INSTS_VMEM_RD per launch (rocprofv3 --pmc, pass A) over the
-line's device time per launch against CUs / TA_NS_PER_VMEM, and the HBM bytes
-from FETCH_SIZE (pass C).  The rocprofv3 kernel trace's union of the timed
-launches must agree with ms_per_step.  No GPU: these read JSON and CSV files.
+profiles/.  Round 4's lines (profiles/r04/): the contract's HBM roofline =
+algorithmic bytes per launch / kernel_ms against 8 TB/s, traffic = the PMC
+FETCH_SIZE bytes of the same config AND camera path, and every view
+(device time against HBM and L2, measured HBM, vector-memory issue, lane
+utilisation) recomputed from the line and the PMC CSVs it names.  Round 3's
+lines (profiles/r03/evidence_r3fin2, vmem-issue bound): SQ_INSTS_VMEM_RD per
+launch over the line's device time per launch against CUs / TA_NS_PER_VMEM.
+The rocprofv3 kernel trace's union of the timed launches must agree with
+ms_per_step.  No GPU: these read JSON and CSV files.
 """
 import csv
 import json
@@ -15,6 +20,8 @@ import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 EVID = os.path.join(ROOT, "profiles", "r03", "evidence_r3fin2")
+R04 = os.path.join(ROOT, "profiles", "r04")
+R04_LINES = [("r4b", "bench.json"), ("r4b", "bench_orbit.json"), ("r4b", "prof3.json")]
 sys.path.insert(0, ROOT)
 
 import bench  # noqa: E402  (module level: argparse-free helpers, no torch)
@@ -85,3 +92,67 @@ def test_default_schedule_helpers():
         assert bench.default_batch(n, weak=True) == n
         assert 0.5 < bench.default_root_weight(n) < 1.0
     assert bench.default_root_weight(1) == 1.0
+
+
+def _r04(session, name):
+    with open(os.path.join(R04, session, name)) as fh:
+        return json.loads([x for x in fh if x.startswith("{")][-1])
+
+
+def _pmc_file(src, pas):
+    d = os.path.join(src, pas)
+    return os.path.join(d, next(f for f in os.listdir(d) if f.endswith("counter_collection.csv")))
+
+
+@pytest.mark.parametrize("session,name", R04_LINES)
+def test_r04_roofline_reproduces(session, name):
+    d = _r04(session, name)
+    r = d["roofline"]
+    alg = r["alg_bytes_per_launch"]
+    # the contract's roofline: algorithmic bytes per launch / the mean launch duration, against 8 TB/s
+    assert r["bound"] == "hbm" and r["unit"] == "GB/s" and r["peak"] == bench.HBM_PEAK_GBS
+    assert r["achieved"] == pytest.approx(alg / (r["kernel_ms"] * 1e-3) / 1e9, rel=1e-3)
+    assert r["frac"] == pytest.approx(r["achieved"] / r["peak"], rel=1e-3)
+    # the algorithmic bytes are SURVEY §8d's sum over the line's own counts per launch
+    c = d["config"]
+    seg = c["segments_per_frame"]
+    assert alg / seg == pytest.approx(r["alg_bytes_per_segment"], rel=1e-3)
+    # 32 B per node visit + 36 B per triangle test, plus at most 16 B (one material read) + 4 B (one
+    # pixel) per segment
+    extra = alg / seg - (32 * c["node_visits_per_segment"] + 36 * c["tri_tests_per_segment"])
+    assert 0.0 < extra <= 20.0 + 0.1
+    # PMC: a record of this config AND camera path, from CSVs under profiles/
+    src = os.path.join(ROOT, r["pmc_source"].split(" ")[0])
+    assert ("--camera-path orbit" in r["pmc_source"]) == (c["camera_path"] == "orbit")
+    fetch = _pmc_mean(_pmc_file(src, "C"), "FETCH_SIZE", kernel="trace_simple<false, false")
+    vmem = _pmc_mean(_pmc_file(src, "A"), "SQ_INSTS_VMEM_RD", kernel="trace_simple<false, false")
+    assert r["traffic"] == pytest.approx(fetch * 1024 * 2, rel=1e-6)
+    assert r["traffic_over_alg"] == pytest.approx(r["traffic"] / alg, abs=5e-5)      # rounded to 4 digits
+    v = r["views"]
+    tf = r["frame_ms_device"] * 1e-3
+    assert v["device_time"]["achieved"] == pytest.approx(alg / tf / 1e9, rel=2e-3)
+    assert v["device_time"]["l2_frac"] == pytest.approx(alg / tf / 1e9 / bench.L2_PEAK_GBS, rel=2e-3)
+    assert v["device_time"]["hbm_frac"] == pytest.approx(alg / tf / 1e9 / bench.HBM_PEAK_GBS, rel=2e-3)
+    assert v["hbm_measured"]["frac"] == pytest.approx(r["traffic"] / tf / 1e9 / bench.HBM_PEAK_GBS, rel=2e-3)
+    vi = v["vmem_issue"]
+    assert vi["vmem_rd_per_launch"] == pytest.approx(vmem, rel=1e-6)
+    assert vi["frac"] == pytest.approx(vmem / tf / 1e9 / (256 / bench.TA_NS_PER_VMEM), rel=2e-3)
+    lu = v["lane_utilisation"]
+    assert lu["lockstep_lane_utilisation"] == pytest.approx(lu["lane_steps"] / (64 * lu["wave_steps"]), rel=1e-3)
+    assert 0.0 < lu["lockstep_lane_utilisation"] < 1.0
+    assert 0.0 < r["frac"] < 1.0
+    # timing fits the steps: value = segments x steps / wall time
+    assert d["value"] == pytest.approx(seg * d["steps"] / (d["ms_per_step"] * d["steps"] * 1e-3) / 1e6, rel=2e-3)
+    assert c["frames_verified"] is True
+
+
+def test_r04_rocprof_union():
+    u = json.load(open(os.path.join(R04, "r4b", "union_cfg3.json")))
+    p = _r04("r4b", "prof3.json")
+    assert u["launches"] == u["frames"] == p["steps"]
+    assert u["union_ms_per_frame"] == pytest.approx(p["ms_per_step"], rel=0.05)
+    with open(os.path.join(R04, "r4b", "kernel_stats_cfg3.csv")) as fh:
+        rows = [r for r in csv.DictReader(fh) if "trace_simple<false, false" in r["Name"]]
+    # rocprofv3's mean launch duration agrees with bench.py's kernel_ms (HIP events on the launch streams)
+    assert float(rows[0]["AverageNs"]) / 1e6 == pytest.approx(p["roofline"]["kernel_ms"], rel=0.05)
+    assert u["launch_ms_mean"] == pytest.approx(p["roofline"]["kernel_ms"], rel=0.05)
