@@ -163,6 +163,31 @@ int build_host_scene(const void* vertices, size_t vertex_bytes,
                      HostScene* out, const char** err);
 void free_host_scene(HostScene* s);
 
+// A learning launch's walk length of a pixel traced by a one-pixel heavy wave
+// (its lockstep length is unknown there): above any real length, so it stays
+// among the heavy pixels (rt_learn.hip).
+constexpr unsigned kLearnHeavyMark = 0x3FFFFFFFu;
+
+// Device-side heavy-first learning (rt_learn.hip): the order, heavy pixels and
+// tile masks from a learning launch's diagnostic records, computed on the
+// stream that ran it, with no host synchronisation.
+struct LearnParams {
+    int      n;              // tiles of the launch (records at rec_off + t, pixels at t * 64 + lane)
+    int      rec_off;        // heavy-pixel waves ahead of the tile records (a fused launch in an order)
+    int      learn_cost;     // 0 = lockstep steps + 2 x windows, 1 = wave duration
+    int      order_split;    // percent (0 = every tile by cost)
+    double   bar_scale;      // heavy-pixel bar = bar_scale x total steps
+    int      cap;            // at most this many heavy pixels
+};
+struct LearnScratch;         // device scratch (rt_learn.hip)
+size_t learn_scratch_bytes(int n);
+// Enqueues on stream s: writes d_order (n tile indices, most expensive first),
+// d_mask (n lane masks), d_hpix (<= cap heavy pixels, tile * 64 + lane, most
+// expensive first) and *d_nhpix (their count).  scratch: learn_scratch_bytes(n).
+hipError_t learn_on_device(const LearnParams& lp, const unsigned long long* rec, const unsigned* lane,
+                           void* scratch, int* d_order, unsigned long long* d_mask, int* d_hpix, int* d_nhpix,
+                           hipStream_t s);
+
 // Kernel launcher (rt_trace.hip).  *kernels (nullable) = the kernels it
 // enqueued (2 when the heavy tiles run as a launch of their own).
 hipError_t launch_trace(const TraceArgs& a, hipStream_t stream, int* kernels = nullptr);

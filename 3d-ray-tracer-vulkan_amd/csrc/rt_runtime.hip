@@ -253,7 +253,19 @@ struct PerDevice {
     // the heavy pixels (tile * 64 + lane, most expensive first) with every
     // tile's mask of them (option heavy_pixels)
     struct Order { std::vector<uint8_t> key; int* d_order; size_t n; int heavy;
-                   int* d_hpix; int n_hpix; unsigned long long* d_mask; };
+                   int* d_hpix; int n_hpix; unsigned long long* d_mask;
+                   bool pending = false;      // learned on the device, heavy-pixel count not read yet
+                   void* d_base = nullptr;    // one allocation holding d_order, d_mask, d_hpix, d_nhpix
+                   int* d_nhpix = nullptr; };
+    // device-side learning (rt_learn.hip): one at a time per device; its
+    // scratch, the pinned heavy-pixel count it reports and the event after it
+    void*        d_learn_scratch = nullptr;
+    size_t       learn_scratch_cap = 0;
+    int*         h_nhpix = nullptr;           // pinned
+    hipEvent_t   learn_ev = nullptr;
+    bool         learn_busy = false;          // a device learning is in flight (its order pending)
+    bool         learning_device = false;     // the learning launch being planned learns on the device
+    int          learning_rec_off = 0;        // its heavy-pixel waves ahead of the tile records
     // option heavy_tiles: auxiliary streams (round robin) for the concurrent heavy-tile launch
     hipStream_t  aux[4] = {nullptr, nullptr, nullptr, nullptr};
     hipEvent_t   aux_fork[4] = {nullptr, nullptr, nullptr, nullptr}, aux_join[4] = {nullptr, nullptr, nullptr, nullptr};
@@ -285,9 +297,26 @@ static constexpr int    kMaxHeavy = 256;
 static constexpr size_t kDiagWords = 8;   // per-wave diag record (rt_trace.hip, rtamd.h rt_diag_copy)
 
 static void free_order(PerDevice::Order& o) {
+    if (o.d_base) {                              // device-learned: one allocation
+        (void)hipFree(o.d_base);
+        return;
+    }
     (void)hipFree(o.d_order);
     if (o.d_hpix) (void)hipFree(o.d_hpix);
     if (o.d_mask) (void)hipFree(o.d_mask);
+}
+
+// A device learning in flight: once its event has fired, its order's
+// heavy-pixel count (copied to pinned memory by the same stream) is read and
+// the order becomes usable.  Never blocks.
+static void poll_learning(PerDevice& p) {
+    if (!p.learn_busy || hipEventQuery(p.learn_ev) != hipSuccess) return;
+    for (auto& o : p.orders)
+        if (o.pending) {
+            o.n_hpix = *p.h_nhpix;
+            o.pending = false;
+        }
+    p.learn_busy = false;
 }
 
 static void free_orders(PerDevice& p) {
@@ -467,23 +496,43 @@ static int plan_order(const rt_ctx* ctx, PerDevice& p, TraceArgs& a, const rt_ca
             p.last_cam.push_back(PerDevice::LastCam{std::move(geo_scene), std::move(camk)});
         }
     }
+    poll_learning(p);
+    const PerDevice::Order* exact = nullptr;
     for (const auto& o : p.orders)
-        if (o.n == n && o.key == key) return use(o);
-    if (ctx->reuse_order && !repeat) {
+        if (o.n == n && o.key == key) { exact = &o; break; }
+    if (exact && !exact->pending) return use(*exact);
+    const PerDevice::Order* reuse = nullptr;
+    if (ctx->reuse_order)
         for (auto it = p.orders.rbegin(); it != p.orders.rend(); ++it)
-            if (it->n == n && it->key.size() == key.size() && std::memcmp(it->key.data(), key.data(), g) == 0 &&
-                std::memcmp(it->key.data() + g + c, key.data() + g + c, sizeof(uint64_t)) == 0)
-                return use(*it);
-    }
+            if (!it->pending && it->n == n && it->key.size() == key.size() &&
+                std::memcmp(it->key.data(), key.data(), g) == 0 &&
+                std::memcmp(it->key.data() + g + c, key.data() + g + c, sizeof(uint64_t)) == 0) {
+                reuse = &*it;
+                break;
+            }
+    // A moving camera reuses the newest order of the frame geometry; so does
+    // any launch while this key's own order is still being learned.
+    if (reuse && (!repeat || exact)) return use(*reuse);
+    if (exact) return RT_OK;                  // learning in flight, nothing to reuse: raster order
     // Learn on a plain launch: a diagnostic launch keeps its own records, and a
     // counting launch (stats) runs the counting build, not the diagnostic one.
     if (a.diag || a.counters) return RT_OK;
-    if (n * kDiagWords > p.learn_cap) {
+    // Device learning (rt_learn.hip), for the default heavy-pixel schedule: the
+    // learning launch runs in the reused order if there is one (its heavy
+    // pixels one per wave, as production launches), and the order is computed
+    // on its stream afterwards with no synchronisation; one learning at a
+    // time per device.  Other schedules learn on the host (learn_order).
+    const bool device = ctx->heavy_stream == 2 && ctx->heavy_pixels && ctx->heavy_tiles < 0 && !ctx->order_frames;
+    if (p.learn_busy) return reuse ? use(*reuse) : RT_OK;   // the device learning in flight finishes first
+    // a fused launch's heavy-pixel waves record first: at most one per resident
+    // wave slot (the largest cap any concurrency gives)
+    const size_t recs = n + (device ? (size_t)p.n_cu * kResidentPerCu : 0);
+    if (recs * kDiagWords > p.learn_cap) {
         if (p.d_learn) (void)hipFree(p.d_learn);
         p.d_learn = nullptr;
         p.learn_cap = 0;
-        RT_HIP_CHECK(hipMalloc(&p.d_learn, n * kDiagWords * sizeof(unsigned long long)));
-        p.learn_cap = n * kDiagWords;
+        RT_HIP_CHECK(hipMalloc(&p.d_learn, recs * kDiagWords * sizeof(unsigned long long)));
+        p.learn_cap = recs * kDiagWords;
     }
     if (n * 64 > p.learn_lane_cap) {
         if (p.d_learn_lane) (void)hipFree(p.d_learn_lane);
@@ -494,12 +543,73 @@ static int plan_order(const rt_ctx* ctx, PerDevice& p, TraceArgs& a, const rt_ca
     }
     p.learning_key = key;
     p.learning_n = n;
+    p.learning_device = device;
+    p.learning_rec_off = 0;
     // Option learn_alone: the learning launch waits for the device to drain,
     // so its wave durations (the order's cost) are not those of waves that
     // shared the GPU with other launches in flight at that moment.
     if (ctx->learn_alone) RT_HIP_CHECK(hipDeviceSynchronize());
+    if (device && reuse) {
+        if (int rc = use(*reuse)) return rc;
+        if (a.heavy_fused) p.learning_rec_off = a.n_heavy_px;
+    }
     a.diag = p.d_learn;                // the diagnostic build counts each wave's lockstep steps
     a.diag_lane = p.d_learn_lane;      // and each pixel's own walk length
+    return RT_OK;
+}
+
+// The device path of learn_order: a pending order whose buffers the learning
+// kernels fill on stream s; the heavy-pixel count follows into pinned memory
+// and an event marks it ready (poll_learning).
+static int learn_order_device(const rt_ctx* ctx, PerDevice& p, hipStream_t s) {
+    const size_t n = p.learning_n;
+    const int conc = std::max(1, concurrency(ctx));
+    const int cap = std::max(1, p.n_cu * kResidentPerCu * ctx->heavy_cap / 100 / conc);
+    const size_t need = learn_scratch_bytes((int)n);
+    if (need > p.learn_scratch_cap) {
+        if (p.d_learn_scratch) (void)hipFree(p.d_learn_scratch);
+        p.d_learn_scratch = nullptr;
+        p.learn_scratch_cap = 0;
+        RT_HIP_CHECK(hipMalloc(&p.d_learn_scratch, need));
+        p.learn_scratch_cap = need;
+    }
+    if (!p.h_nhpix) RT_HIP_CHECK(hipHostMalloc(&p.h_nhpix, sizeof(int), hipHostMallocPortable));
+    if (!p.learn_ev) RT_HIP_CHECK(hipEventCreateWithFlags(&p.learn_ev, hipEventDisableTiming));
+    if (p.orders.size() >= kMaxOrders) {
+        RT_HIP_CHECK(hipDeviceSynchronize());  // the oldest order may still steer a launch in flight
+        free_order(p.orders.front());
+        p.orders.erase(p.orders.begin());
+    }
+    auto up = [](size_t b) { return (b + 255) / 256 * 256; };
+    const size_t b_order = up(n * sizeof(int)), b_mask = up(n * sizeof(unsigned long long));
+    const size_t b_hpix = up((size_t)cap * sizeof(int));
+    PerDevice::Order o{p.learning_key, nullptr, n, 0, nullptr, 0, nullptr};
+    RT_HIP_CHECK(hipMalloc(&o.d_base, b_order + b_mask + b_hpix + sizeof(int)));
+    char* base = static_cast<char*>(o.d_base);
+    o.d_order = reinterpret_cast<int*>(base);
+    o.d_mask = reinterpret_cast<unsigned long long*>(base + b_order);
+    o.d_hpix = reinterpret_cast<int*>(base + b_order + b_mask);
+    o.d_nhpix = reinterpret_cast<int*>(base + b_order + b_mask + b_hpix);
+    o.pending = true;
+    LearnParams lp;
+    lp.n = (int)n;
+    lp.rec_off = p.learning_rec_off;
+    lp.learn_cost = ctx->learn_cost;
+    lp.order_split = ctx->order_split;
+    // the host path's bar: heavy_pixel_factor% x (total steps x concurrent / resident waves)
+    lp.bar_scale = ctx->heavy_pixel_factor / 100.0 * (double)conc / (double)std::max(1, p.n_cu * kResidentPerCu);
+    lp.cap = cap;
+    hipError_t e = learn_on_device(lp, p.d_learn, p.d_learn_lane, p.d_learn_scratch, o.d_order, o.d_mask, o.d_hpix,
+                                   o.d_nhpix, s);
+    if (e == hipSuccess) e = hipMemcpyAsync(p.h_nhpix, o.d_nhpix, sizeof(int), hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipEventRecord(p.learn_ev, s);
+    if (e != hipSuccess) {
+        (void)hipStreamSynchronize(s);
+        free_order(o);
+        RT_HIP_CHECK(e);
+    }
+    p.orders.push_back(std::move(o));
+    p.learn_busy = true;
     return RT_OK;
 }
 
@@ -510,6 +620,7 @@ static int learn_order(const rt_ctx* ctx, PerDevice& p, const TraceArgs& a, hipS
     const int learn_cost = ctx->learn_cost, concurrent = concurrency(ctx);
     const double heavy_factor = ctx->heavy_factor / 100.0;
     if (!a.diag || a.diag != p.d_learn) return RT_OK;
+    if (p.learning_device) return learn_order_device(ctx, p, s);
     const size_t n = p.learning_n;
     RT_HIP_CHECK(hipStreamSynchronize(s));
     std::vector<unsigned long long> rec(n * kDiagWords);
@@ -598,6 +709,7 @@ static int learn_order(const rt_ctx* ctx, PerDevice& p, const TraceArgs& a, hipS
     if (p.orders.size() >= kMaxOrders) {
         // the oldest order may still steer a launch in flight on another stream
         RT_HIP_CHECK(hipDeviceSynchronize());
+        poll_learning(p);
         free_order(p.orders.front());
         p.orders.erase(p.orders.begin());
     }
@@ -857,6 +969,9 @@ int rt_destroy(rt_ctx* ctx) {
         if (p.d_diag) (void)hipFree(p.d_diag);
         if (p.d_learn) (void)hipFree(p.d_learn);
         if (p.d_learn_lane) (void)hipFree(p.d_learn_lane);
+        if (p.d_learn_scratch) (void)hipFree(p.d_learn_scratch);
+        if (p.h_nhpix) (void)hipHostFree(p.h_nhpix);
+        if (p.learn_ev) (void)hipEventDestroy(p.learn_ev);
         free_orders(p);
         free_graphs(p);
         for (auto& l : p.band_lists) (void)hipFree(l.d);

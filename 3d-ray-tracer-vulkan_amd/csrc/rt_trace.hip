@@ -613,6 +613,7 @@ constexpr int kFeatExt = kFeatExtBit;   // non-reference extensions (option "ext
 constexpr int kFeatFrontier = 32; // cooperative tail uses frontier_walk (option coop_walk = 1)
 
 constexpr int kFeatFused = 64;    // heavy tiles in the same launch: workgroups k < 64 * split_n run heavy_pixel
+constexpr unsigned kHeavyLaneMark = kLearnHeavyMark;   // rt_internal.h
 
 // One pixel of a heavy tile, the whole wave on it (option heavy_fused, the
 // workgroups in front of the tile workgroups of the same launch): every
@@ -692,11 +693,6 @@ __attribute__((amdgpu_waves_per_eu((FEAT & kFeatFrontier) ? 1 : RT_SIMPLE_WPE)))
 void trace_simple(TraceArgs a) {
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
-    unsigned long long* drec = nullptr;
-    if (DIAG) {
-        drec = a.diag + kDiagWords * (size_t)((blockIdx.y * gridDim.x + blockIdx.x) * a.block_waves + wave);
-        diag_stamp(drec, 0);
-    }
     // frontier_walk's per-wave frontiers (kFCap entries per wave; dynamic LDS,
     // sized by the launch for variants with kFeatFrontier or kFeatFused)
     extern __shared__ uint4 fr[];
@@ -713,37 +709,56 @@ void trace_simple(TraceArgs a) {
     // single live lane walks every segment cooperatively (frontier walk).
     int bx = blockIdx.x, by = blockIdx.y, sub = -1;
     unsigned long long skip_lanes = 0;                   // heavy pixels this tile wave leaves out
+    // Diagnostic record of this wave and the tile of its per-pixel walk
+    // lengths (diag builds): the wave's index in the grid, except in a fused
+    // launch in a tile order, where tile t's wave records at n_heavy_px + t and
+    // its pixels at t * 64 + lane (a learning launch in another camera's order
+    // still gives each tile its own record: rt_learn.hip reads them by tile).
+    const int k_wave = (blockIdx.y * gridDim.x + blockIdx.x) * a.block_waves + wave;
+    int rec_id = k_wave, tile_id = k_wave, hq = -1;
     if (a.tile_order) {                                  // 1-D grid over the ordered tiles
         const int k = blockIdx.x;
         int t;
         if ((FEAT & kFeatFused) && k < a.n_heavy_px) {   // a heavy pixel (tile * 64 + lane), dispatched first
-            const int q = a.heavy_px[k];
-            t = q >> 6;
-            sub = q & 63;
+            hq = a.heavy_px[k];
+            t = hq >> 6;
+            sub = hq & 63;
         } else if (k < 64 * a.split_n) {
             t = a.tile_order[k >> 6];
             sub = k & 63;
         } else {
             t = a.tile_order[k - 63 * a.split_n - ((FEAT & kFeatFused) ? a.n_heavy_px : 0)];
             if ((FEAT & kFeatFused) && a.tile_mask) skip_lanes = a.tile_mask[t];
+            if (FEAT & kFeatFused) {
+                rec_id = a.n_heavy_px + t;
+                tile_id = t;
+            }
         }
         bx = t % a.tiles_x;
         by = t / a.tiles_x;
-        if ((FEAT & kFeatFused) && sub >= 0) {           // a heavy tile's pixel, dispatched first
-            const int hf = by / a.tiles_y;               // its frame of the batch
-            const int hy = (by - hf * a.tiles_y) * th_w + (sub >> (3 + s));
-            heavy_pixel<COUNT>(a, hf, bx * tw_w + (sub & (tw_w - 1)), hy, hf * a.th + hy, fr);
-            if (DIAG) {
-                diag_stamp(drec, 1);
-                if (lane == 0) {
-                    drec[4] = 0;
-                    drec[5] = 0;
-                    drec[6] = 0;
-                    drec[7] = 0;
-                }
+    }
+    unsigned long long* drec = nullptr;
+    if (DIAG) {
+        drec = a.diag + kDiagWords * (size_t)rec_id;
+        diag_stamp(drec, 0);
+    }
+    if ((FEAT & kFeatFused) && sub >= 0) {               // a heavy tile's pixel, dispatched first
+        const int hf = by / a.tiles_y;                   // its frame of the batch
+        const int hy = (by - hf * a.tiles_y) * th_w + (sub >> (3 + s));
+        heavy_pixel<COUNT>(a, hf, bx * tw_w + (sub & (tw_w - 1)), hy, hf * a.th + hy, fr);
+        if (DIAG) {
+            diag_stamp(drec, 1);
+            if (lane == 0) {
+                drec[4] = 0;
+                drec[5] = 0;
+                drec[6] = 0;
+                drec[7] = 0;
+                // a learning launch: a pixel traced as heavy keeps its place
+                // among the heavy ones (its lockstep length is unknown here)
+                if (a.diag_lane && hq >= 0) a.diag_lane[hq] = kHeavyLaneMark;
             }
-            return;
         }
+        return;
     }
     const int tl = sub >= 0 ? sub : lane;                // the tile pixel this lane traces
     const int col = bx * a.block_waves + wave;           // wave-tile column
@@ -937,9 +952,9 @@ void trace_simple(TraceArgs a) {
         diag_stamp(drec, 1);
         // each pixel's own walk length: its lockstep steps (d_iters counts the
         // loop iterations this lane walked) + 2 x the windows spent on it
-        if (a.diag_lane)
-            a.diag_lane[((size_t)(blockIdx.y * gridDim.x + blockIdx.x) * a.block_waves + wave) * 64 + lane] =
-                (unsigned)(d_iters + 2 * d_lane_windows);
+        // (a lane whose heavy pixel a one-pixel wave traced leaves that wave's mark)
+        if (a.diag_lane && !((skip_lanes >> lane) & 1ull))
+            a.diag_lane[(size_t)tile_id * 64 + lane] = (unsigned)(d_iters + 2 * d_lane_windows);
         // the lanes' own lockstep steps, summed (the useful lane-steps of
         // the wave's lockstep walk: lane utilisation = sum / (64 x word 4))
         unsigned long long d_sum = d_iters;

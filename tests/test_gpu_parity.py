@@ -295,8 +295,8 @@ def test_bench_setting_whole_frame(renderer, cfg_k, walk):
 def test_moving_camera_reuses_order(renderer):
     """Option reuse_order: a camera that has just moved uses the order and
     heavy pixels learned at another camera (no learning frame), which only
-    changes the schedule; the first repeat of a camera learns its own.  Every
-    frame equals the oracle's."""
+    changes the schedule; the first repeat of a camera learns its own, in the
+    reused order.  Every frame equals the oracle's."""
     from rtamd import configs
     cfg = configs.get(3)
     built = cfg.build()
@@ -315,7 +315,10 @@ def test_moving_camera_reuses_order(renderer):
     assert used[0] == 0                           # the learning launch itself runs without an order
     assert used[1] > 0                            # camera 0's own order
     assert used[2] == used[1] and used[3] == used[1]   # moving: camera 0's order reused, no learning
-    assert used[4] == 0                           # camera 2 repeated: this launch learns
+    # camera 2 repeated: this launch learns, on the device (rt_learn.hip, no
+    # synchronisation), and runs in the reused order meanwhile, its heavy
+    # pixels one per wave as in the production launches
+    assert used[4] == used[1]
     assert used[5] > 0                            # camera 2's own order
 
 
