@@ -51,15 +51,24 @@ struct DevScene {
     float4*  nodes   = nullptr;
     float4*  leafs   = nullptr;
     float4*  pairs   = nullptr;
-    // Compact records (walk 2 and the cooperative tail): 2 x float4 per node
-    // index in nodes2 (an internal node's record as in nodes; a leaf's [1].w
-    // holds v0.x and its [0].w the triangle index | 1 << 30 | L(i+1) << 31,
-    // since a leaf's skip is always i+1, so bit 30 of [0].w is L(i) for every
-    // node) and 2 x float4 per node index in leafs2 (a leaf's v0.yz, e1, e2): a
-    // leaf visit loads 4 float4 instead of 5 and the walk carries 8 leaf
-    // registers instead of 12
-    float4*  nodes2  = nullptr;
-    float4*  leafs2  = nullptr;
+    // walk 2's records (the lockstep walk and the cooperative tail), 32-B
+    // slots: the reference's preorder with every leaf's triangle inlined after
+    // its box.  An internal node takes one slot, (min.xyz, skip slot |
+    // L(skip) << 31), (max.xyz, L(i+1) | L(i) << 1); a leaf two, (min.xyz,
+    // triangle index | 1 << 30 | L(i+1) << 31), (max.xyz, v0.x), then
+    // (v0.yz, e1.xy), (e1.z, e2.xyz).  slot(i) = i + the leaves before i, so
+    // an internal node's left child (i+1) is the next slot and a leaf's
+    // successor (its skip, i+1) the slot after its two: only the internal
+    // skip is stored.  A leaf visit reads its node and triangle from one
+    // 64-B run (they were two arrays), sibling leaves sit side by side, and
+    // the records take 32 B per node + 32 B per leaf instead of 64 B per node
+    // (config 5: 100 MB instead of 134 MB).  Bit 30 of word [0].w is L(i) for
+    // every node.  end2 = the slots; slot_node = the node index of a node's
+    // first slot (the frontier tail's hand-off), -1 on a leaf's second slot.
+    float4*  walk    = nullptr;
+    int*     slot_node = nullptr;
+    int*     node_slot = nullptr;   // slot(i) of node i (walk 0 hands its node index to the windows tail)
+    int      end2    = 0;
     // norms and mats interleave in one allocation (kShadeStride float4 per
     // triangle: normal, then albedo/type), so shading a hit touches one 32-B
     // record; norms points at the allocation, mats one float4 in

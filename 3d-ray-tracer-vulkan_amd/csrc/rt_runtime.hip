@@ -380,8 +380,9 @@ struct rt_ctx {
 static void free_scene(PerDevice& p) {
     if (p.scene.nodes) (void)hipFree(p.scene.nodes);
     if (p.scene.leafs) (void)hipFree(p.scene.leafs);
-    if (p.scene.nodes2) (void)hipFree(p.scene.nodes2);
-    if (p.scene.leafs2) (void)hipFree(p.scene.leafs2);
+    if (p.scene.walk) (void)hipFree(p.scene.walk);
+    if (p.scene.slot_node) (void)hipFree(p.scene.slot_node);
+    if (p.scene.node_slot) (void)hipFree(p.scene.node_slot);
     if (p.scene.pairs) (void)hipFree(p.scene.pairs);
     if (p.scene.norms) (void)hipFree(p.scene.norms);   // mats lives in the same allocation
     p.scene = DevScene{};
@@ -797,8 +798,8 @@ static std::vector<uint64_t> launch_key(const TraceArgs& a, hipStream_t s) {
     auto P = [](const void* q) { return (uint64_t)(uintptr_t)q; };
     auto F = [](float f) { uint32_t u; std::memcpy(&u, &f, 4); return (uint64_t)u; };
     const DevScene& sc = a.scene;
-    std::vector<uint64_t> k = {P(s), P(sc.nodes), P(sc.leafs), P(sc.pairs), P(sc.nodes2), P(sc.leafs2), P(sc.norms), P(sc.mats), P(sc.spheres),
-            (uint64_t)sc.n_spheres, (uint64_t)sc.n_nodes, (uint64_t)sc.end, (uint64_t)sc.n_tris,
+    std::vector<uint64_t> k = {P(s), P(sc.nodes), P(sc.leafs), P(sc.pairs), P(sc.walk), P(sc.slot_node), P(sc.node_slot), P(sc.norms), P(sc.mats), P(sc.spheres),
+            (uint64_t)sc.n_spheres, (uint64_t)sc.n_nodes, (uint64_t)sc.end, (uint64_t)sc.end2, (uint64_t)sc.n_tris,
             (uint64_t)sc.root_leaf, F(sc.root_box[0]), F(sc.root_box[1]), F(sc.root_box[2]), F(sc.root_box[3]),
             F(sc.root_box[4]), F(sc.root_box[5]), (uint64_t)a.n_frames, P(a.band_list), (uint64_t)a.list_stride,
             (uint64_t)a.width, (uint64_t)a.height, (uint64_t)a.max_bounces, (uint64_t)a.x0, (uint64_t)a.y0,
@@ -1002,26 +1003,45 @@ int rt_upload_scene(rt_ctx* ctx, const void* vertices, size_t vertex_bytes,
     int rc = build_host_scene(vertices, vertex_bytes, materials, material_bytes,
                               bvh_nodes, bvh_bytes, &hs, &err);
     if (rc != RT_OK) { set_error("rt_upload_scene: %s", err); return rc; }
-    // walk 2's compact records (DevScene::nodes2 / leafs2), built from the
-    // compact scene: a leaf's skip is always i+1 (preorder), so its link word
-    // carries the triangle index instead, and its flags word v0.x
+    // walk 2's records (DevScene::walk; rt_internal.h): the reference's
+    // preorder with every leaf's triangle inlined after its box, so an
+    // internal node takes one 32-B slot and a leaf two.  slot(i) = i + the
+    // leaves before i; an internal node's left child is the next slot, a
+    // leaf's successor (its skip, i+1) the slot after its two, and only the
+    // internal skip is stored, as a slot.  The visit sequence is the
+    // reference's, node for node.
     const size_t n2 = (size_t)hs.n_nodes;
-    std::vector<float4> nodes2(2 * n2 + 2, make_float4(0.f, 0.f, 0.f, 0.f)), leafs2(2 * n2 + 2, nodes2[0]);
+    std::vector<int> slot(n2 + 1);
+    size_t nslot = 0;
     for (size_t i = 0; i < n2; ++i) {
-        nodes2[2 * i] = hs.nodes[2 * i];
-        nodes2[2 * i + 1] = hs.nodes[2 * i + 1];
+        slot[i] = (int)nslot;
         uint32_t fl;
         std::memcpy(&fl, &hs.nodes[2 * i + 1].w, 4);
-        if (!(fl & 2u)) {                                   // internal node: skip < 2^30 keeps bit 30 clear
-            if (n2 >= (1u << 30)) {
-                free_host_scene(&hs);
-                set_error("rt_upload_scene: %zu nodes: at most 2^30 supported", n2);
-                return RT_ERR_BAD_SCENE;
-            }
+        nslot += (fl & 2u) ? 2 : 1;
+        if (nslot >= (1u << 30)) {
+            free_host_scene(&hs);
+            set_error("rt_upload_scene: %zu nodes: at most 2^30 walk slots supported", n2);
+            return RT_ERR_BAD_SCENE;
+        }
+    }
+    slot[n2] = (int)nslot;
+    std::vector<float4> walk(2 * nslot + 4, make_float4(0.f, 0.f, 0.f, 0.f));   // + padding read at the end
+    std::vector<int> slot_node(nslot + 1, -1);
+    for (size_t i = 0; i < n2; ++i) {
+        const size_t w = 2 * (size_t)slot[i];
+        slot_node[slot[i]] = (int)i;
+        walk[w] = hs.nodes[2 * i];
+        walk[w + 1] = hs.nodes[2 * i + 1];
+        uint32_t fl, link;
+        std::memcpy(&fl, &hs.nodes[2 * i + 1].w, 4);
+        std::memcpy(&link, &hs.nodes[2 * i].w, 4);
+        if (!(fl & 2u)) {                                   // internal: the skip as a slot (< 2^30: bit 30 clear)
+            const uint32_t sk = link & 0x7FFFFFFFu;
+            const uint32_t w0 = (uint32_t)slot[sk] | (link & 0x80000000u);
+            std::memcpy(&walk[w].w, &w0, 4);
             continue;
         }
-        uint32_t link, tri;
-        std::memcpy(&link, &hs.nodes[2 * i].w, 4);
+        uint32_t tri;
         std::memcpy(&tri, &hs.leafs[3 * i].w, 4);
         if ((link & 0x7FFFFFFFu) != i + 1 || tri >= (1u << 30)) {
             free_host_scene(&hs);
@@ -1030,11 +1050,11 @@ int rt_upload_scene(rt_ctx* ctx, const void* vertices, size_t vertex_bytes,
             return RT_ERR_BAD_SCENE;
         }
         const uint32_t w0 = tri | (1u << 30) | (link & 0x80000000u);
-        std::memcpy(&nodes2[2 * i].w, &w0, 4);
-        nodes2[2 * i + 1].w = hs.leafs[3 * i].x;                              // v0.x
+        std::memcpy(&walk[w].w, &w0, 4);
+        walk[w + 1].w = hs.leafs[3 * i].x;                                   // v0.x
         const float4 P0 = hs.leafs[3 * i], P1 = hs.leafs[3 * i + 1], P2 = hs.leafs[3 * i + 2];
-        leafs2[2 * i] = make_float4(P0.y, P0.z, P1.x, P1.y);                   // v0.yz, e1.xy
-        leafs2[2 * i + 1] = make_float4(P1.z, P2.x, P2.y, P2.z);               // e1.z, e2
+        walk[w + 2] = make_float4(P0.y, P0.z, P1.x, P1.y);                   // v0.yz, e1.xy
+        walk[w + 3] = make_float4(P1.z, P2.x, P2.y, P2.z);                   // e1.z, e2
     }
     ctx->has_scene = false;
     for (PerDevice& p : ctx->dev) {
@@ -1064,10 +1084,14 @@ int rt_upload_scene(rt_ctx* ctx, const void* vertices, size_t vertex_bytes,
         if (e == hipSuccess) e = hipMalloc(&s.pairs, pb);
         if (e == hipSuccess) e = hipMemset(s.nodes + 2 * nn, 0, 2 * sizeof(float4));
         if (e == hipSuccess) e = hipMemset(s.leafs + 3 * nn, 0, sizeof(float4));
-        if (e == hipSuccess) e = hipMalloc(&s.nodes2, nodes2.size() * sizeof(float4));
-        if (e == hipSuccess) e = hipMalloc(&s.leafs2, leafs2.size() * sizeof(float4));
-        if (e == hipSuccess) e = hipMemcpy(s.nodes2, nodes2.data(), nodes2.size() * sizeof(float4), hipMemcpyHostToDevice);
-        if (e == hipSuccess) e = hipMemcpy(s.leafs2, leafs2.data(), leafs2.size() * sizeof(float4), hipMemcpyHostToDevice);
+        s.end2 = (int)nslot;
+        if (e == hipSuccess) e = hipMalloc(&s.walk, walk.size() * sizeof(float4));
+        if (e == hipSuccess) e = hipMalloc(&s.slot_node, slot_node.size() * sizeof(int));
+        if (e == hipSuccess) e = hipMalloc(&s.node_slot, slot.size() * sizeof(int));
+        if (e == hipSuccess) e = hipMemcpy(s.node_slot, slot.data(), slot.size() * sizeof(int), hipMemcpyHostToDevice);
+        if (e == hipSuccess) e = hipMemcpy(s.walk, walk.data(), walk.size() * sizeof(float4), hipMemcpyHostToDevice);
+        if (e == hipSuccess)
+            e = hipMemcpy(s.slot_node, slot_node.data(), slot_node.size() * sizeof(int), hipMemcpyHostToDevice);
         if (e == hipSuccess) e = hipMalloc(&s.norms, kShadeStride * mb);
         if (e == hipSuccess) s.mats = s.norms + 1;
         if (e == hipSuccess && hs.n_nodes) e = hipMemcpy(s.nodes, hs.nodes, nb - 2 * sizeof(float4), hipMemcpyHostToDevice);

@@ -348,23 +348,25 @@ __device__ __forceinline__ float lane_f(float v, int k) {
 //
 // The whole wave walks ONE ray (arguments wave-uniform), replaying the
 // reference's visit sequence exactly:
-//   1. lane k loads node n+k of the window [n, n+64) and, in the same round
-//      trip, the leaf record indexed by that node (the compact records
-//      nodes2 / leafs2: 2 + 2 coalesced 16-B loads per lane; bit 30 of the
-//      link word says leaf); it runs the slab test and, for a leaf whose box is hit
-//      at the current closest_t, the triangle test up to "t < closest_t";
+//   1. lane k loads slot n+k of the window [n, n+64) of the walk records
+//      (DevScene::walk) and the slot after it: 4 coalesced 16-B loads per
+//      lane, a node's record and, for a leaf, its triangle (bit 30 of the link
+//      word says leaf; a leaf's second slot loads as a node nobody visits); it
+//      runs the slab test and, for a leaf whose box is hit at the current
+//      closest_t, the triangle test up to "t < closest_t";
 //   2. ballots make 64-bit masks: box hit at closest_t (H), triangle hit that
 //      improves closest_t (T), is a leaf (Lf);
-//   3. the scalar unit replays the walk through the window: node k is hit iff
-//      bit k of H; next = k+1 on a hit, skip(k) on a miss; a triangle hit
+//   3. the scalar unit replays the walk through the window: the node at slot
+//      k is hit iff bit k of H; next = k+1 (an internal node hit), k+2 (a
+//      leaf, hit or not), skip(k) (an internal node missed); a triangle hit
 //      updates closest_t / hit and re-ballots H and T (closest_t only shrinks,
 //      so a leaf not pre-tested at the old closest_t cannot hit at the new one).
 // The float operations are node_step's, so closest_t, the hit and the visit /
 // triangle-test counts equal the per-lane walk's.
 template <bool COUNT>
-__device__ __forceinline__ int coop_walk(const float4* __restrict__ nodes2, const float4* __restrict__ leafs2,
-                                         int end, int n, V3 o, V3 d, V3 inv, float& closest, int& hit,
-                                         unsigned long long& c_node, unsigned long long& c_tri) {
+__device__ __forceinline__ int coop_walk(const float4* __restrict__ walk, int end, int n, V3 o, V3 d, V3 inv,
+                                         float& closest, int& hit, unsigned long long& c_node,
+                                         unsigned long long& c_tri) {
     const int lane = threadIdx.x & 63;
     int windows = 0;
     while (n < end) {
@@ -374,14 +376,14 @@ __device__ __forceinline__ int coop_walk(const float4* __restrict__ nodes2, cons
         int sk = 0, tri = -1;
         bool ind = false, tv = false, lf = false;
         if (j < end) {
-            const float4 A = nodes2[2 * j];
-            const float4 B = nodes2[2 * j + 1];
-            const float4 Q0 = leafs2[2 * j + 0];
-            const float4 Q1 = leafs2[2 * j + 1];
+            const float4 A = walk[2 * j];
+            const float4 B = walk[2 * j + 1];
+            const float4 Q0 = walk[2 * j + 2];                       // a leaf's triangle (end is padded)
+            const float4 Q1 = walk[2 * j + 3];
             slab(A, B, o, inv, te, ind);
             const uint32_t aw = __float_as_uint(A.w);
             lf = ((aw >> 30) & 1u) != 0u;
-            sk = lf ? j + 1 : (int)(aw & 0x7FFFFFFFu);               // a leaf's skip is j+1
+            sk = lf ? j + 2 : (int)(aw & 0x7FFFFFFFu);               // a leaf's skip is its successor, two slots on
             tri = (int)(aw & 0x3FFFFFFFu);
             if (lf && ind && te < closest)
                 tv = tri_test(make_float4(B.w, Q0.x, Q0.y, 0.f), make_float4(Q0.z, Q0.w, Q1.x, 0.f),
@@ -404,7 +406,7 @@ __device__ __forceinline__ int coop_walk(const float4* __restrict__ nodes2, cons
                         T = __ballot(tv && tt < closest);
                     }
                 }
-                ++k;
+                k += ((Lf >> k) & 1ull) ? 2 : 1;
             } else {
                 k = lane_i(sk, k) - n;
             }
@@ -774,7 +776,8 @@ void trace_simple(TraceArgs a) {
     const float4* __restrict__ nodes = a.scene.nodes;
     const float4* __restrict__ leafs = a.scene.leafs;
     const float4* __restrict__ pairs = a.scene.pairs;
-    const int end = a.scene.end;
+    const int end = a.scene.end;                         // node index end (walk 0, the frontier tail)
+    const int wend = WALK == 2 ? a.scene.end2 : end;     // the lockstep walk's end: slots for walk 2
     unsigned long long c_seg = 0, c_node = 0, c_tri = 0, c_mat = 0;
     unsigned long long d_iters = 0, d_windows = 0, d_coop_t = 0;   // diag builds only
     unsigned long long d_lane_windows = 0;           // diag: cooperative windows spent on this lane's walks
@@ -802,7 +805,8 @@ void trace_simple(TraceArgs a) {
         float closest = kTMax;
         int hit = -1;
         const V3 inv = {1.0f / d.x, 1.0f / d.y, 1.0f / d.z};              // :89
-        // The walk's position: n = the next node the reference would visit.
+        // The walk's position: n = the next node the reference would visit
+        // (walk 2: its slot in DevScene::walk; walk 0: its node index).
         int n = 0;
         bool nleaf = a.scene.root_leaf != 0;
         bool walking = alive && end > 0;
@@ -815,18 +819,17 @@ void trace_simple(TraceArgs a) {
             // walk 2, software-pipelined: the next node's box is requested as soon as
             // this node's slab test has chosen it, before this node's triangle
             // test and the loop control, which then overlap the load.
-            // walk 2 reads the compact records (DevScene::nodes2 / leafs2): a
-            // leaf's node record carries its triangle index and v0.x, and Q0, Q1
-            // the rest of its triangle.
+            // walk 2 reads the walk records (DevScene::walk): a leaf's first
+            // slot carries its triangle index and v0.x, and the slot after it,
+            // Q0 and Q1, the rest of its triangle.
             float4 A, B, Q0, Q1;
-            const float4* __restrict__ nodes2 = a.scene.nodes2;
-            const float4* __restrict__ leafs2 = a.scene.leafs2;
+            const float4* __restrict__ wr = a.scene.walk;
             if (WALK == 2 && walking) {
-                A = nodes2[2 * n];
-                B = nodes2[2 * n + 1];
+                A = wr[2 * n];
+                B = wr[2 * n + 1];
                 if (nleaf) {
-                    Q0 = leafs2[2 * n + 0];
-                    Q1 = leafs2[2 * n + 1];
+                    Q0 = wr[2 * n + 2];
+                    Q1 = wr[2 * n + 3];
                 }
             }
             while (walking) {
@@ -839,13 +842,15 @@ void trace_simple(TraceArgs a) {
                     slab(A, B, o, inv, te, ind);
                     const bool hb = ind && te < closest;
                     const uint32_t aw = __float_as_uint(A.w), bw = __float_as_uint(B.w);
-                    // a leaf's next node is n+1 whether it is hit or not (its skip)
-                    const int nxt = (hb || nleaf) ? n + 1 : (int)(aw & kIdx);
+                    // a leaf's next node is its successor, two slots on, whether it
+                    // is hit or not (its skip); an internal node's left child is
+                    // the next slot
+                    const int nxt = nleaf ? n + 2 : (hb ? n + 1 : (int)(aw & kIdx));
                     const bool nl = (((hb && !nleaf) ? bw : (aw >> 31)) & 1u) != 0u;
                     const float v0x = B.w;                                   // a leaf's v0.x
                     if (COUNT && hb && !nleaf) c_node += 2;
-                    A = nodes2[2 * nxt];                                     // index end is padding
-                    B = nodes2[2 * nxt + 1];
+                    A = wr[2 * nxt];                                         // slot end is padding
+                    B = wr[2 * nxt + 1];
                     if (hb && nleaf) {                                       // hit_triangle (:196-200)
                         if (COUNT) ++c_tri;
                         float t;
@@ -855,14 +860,14 @@ void trace_simple(TraceArgs a) {
                             hit = (int)(aw & kTri);
                         }
                     }
-                    if (nl && nxt < end) {
-                        Q0 = leafs2[2 * nxt + 0];
-                        Q1 = leafs2[2 * nxt + 1];
+                    if (nl && nxt < wend) {
+                        Q0 = wr[2 * nxt + 2];
+                        Q1 = wr[2 * nxt + 3];
                     }
                     n = nxt;
                     nleaf = nl;
                 }
-                walking = n < end;
+                walking = n < wend;
                 if ((FEAT & kFeatCoopTail) && __popcll(__ballot(walking)) <= coop_lanes) break;
             }
         }
@@ -884,13 +889,17 @@ void trace_simple(TraceArgs a) {
                 const int start = n;
                 int nw = 0;
                 if ((FEAT & kFeatFrontier) && a.coop_walk) {
-                    int p = lane_i(start, L);
+                    // the frontier walk takes node indices: walk 2's slot -> node
+                    int p = WALK == 2 ? a.scene.slot_node[lane_i(start, L)] : lane_i(start, L);
                     bool pl = false;
                     if (!frontier_walk<COUNT>(nodes, leafs, pairs, end, p, pl, bo, bd, bi, bc, bh, cn, ct,
                                               fr + wave * kFCap, nw))
                         while (p < end) p = node_step<COUNT>(nodes, leafs, p, pl, bo, bd, bi, bc, bh, cn, ct);
                 } else {
-                    nw = coop_walk<COUNT>(a.scene.nodes2, a.scene.leafs2, end, lane_i(start, L), bo, bd, bi, bc, bh, cn, ct);
+                    // the windows walk slots of the walk-2 records (walk 0 hands over a
+                    // node index: its slot first)
+                    const int ws = WALK == 2 ? lane_i(start, L) : a.scene.node_slot[lane_i(start, L)];
+                    nw = coop_walk<COUNT>(a.scene.walk, a.scene.end2, ws, bo, bd, bi, bc, bh, cn, ct);
                 }
                 if (DIAG) {
                     d_windows += nw;
