@@ -862,8 +862,9 @@ def main() -> None:
             ms.append(round((time.perf_counter() - t1) * 1e3, 4))
         stop = {"ms_per_frame": ms,
                 "what": "the camera of the last timed frame traced 8 more times one at a time (launch to "
-                        "completion, host clock): the first repeat of a camera runs the learning launch "
-                        "(diagnostic build + stream synchronisation), later ones the learned order"}
+                        "completion, host clock): the first repeat of a camera is its learning launch (the "
+                        "diagnostic build in the reused order, the order then computed on the device with no "
+                        "synchronisation, rt_learn.hip), later ones run its own learned order"}
 
     t = torch.tensor([elapsed, launch_ms, frame_ms], dtype=torch.float64, device=dev)
     if dist_on and not emu:
