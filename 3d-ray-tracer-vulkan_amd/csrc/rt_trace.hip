@@ -326,6 +326,14 @@ __device__ __forceinline__ int lanes_below(uint64_t mask) {
 
 __device__ __forceinline__ int lane_i(int v, int k) { return __builtin_amdgcn_readlane(v, k); }
 
+// Lane k + 1's value in lane k (DPP wave_shl:1; lane 63 keeps its own).
+__device__ __forceinline__ float next_lane(float v) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(v), __float_as_int(v), 0x130, 0xf, 0xf, false));
+}
+__device__ __forceinline__ float4 next_lane(float4 v) {
+    return make_float4(next_lane(v.x), next_lane(v.y), next_lane(v.z), next_lane(v.w));
+}
+
 // Bits [0, n) of a wave mask (n in 0..64).
 __device__ __forceinline__ uint64_t lanes_lt(int n) { return n >= 64 ? ~0ull : ((1ull << n) - 1ull); }
 
@@ -349,11 +357,13 @@ __device__ __forceinline__ float lane_f(float v, int k) {
 // The whole wave walks ONE ray (arguments wave-uniform), replaying the
 // reference's visit sequence exactly:
 //   1. lane k loads slot n+k of the window [n, n+64) of the walk records
-//      (DevScene::walk) and the slot after it: 4 coalesced 16-B loads per
-//      lane, a node's record and, for a leaf, its triangle (bit 30 of the link
-//      word says leaf; a leaf's second slot loads as a node nobody visits); it
-//      runs the slab test and, for a leaf whose box is hit at the current
-//      closest_t, the triangle test up to "t < closest_t";
+//      (DevScene::walk): 2 coalesced 16-B loads per lane.  A leaf's triangle is
+//      the slot after its box, which lane k+1 loaded: it comes across by DPP
+//      (wave_shl:1), so a window costs 2 loads, not 4 (bit 30 of the link word
+//      says leaf; a leaf's second slot is loaded as a node nobody visits).  A
+//      leaf in slot 63, whose triangle lies past the window, starts the next
+//      window instead.  Each lane runs the slab test and, for a leaf whose box
+//      is hit at the current closest_t, the triangle test up to "t < closest_t";
 //   2. ballots make 64-bit masks: box hit at closest_t (H), triangle hit that
 //      improves closest_t (T), is a leaf (Lf);
 //   3. the scalar unit replays the walk through the window: the node at slot
@@ -375,24 +385,27 @@ __device__ __forceinline__ int coop_walk(const float4* __restrict__ walk, int en
         float te = 0.0f, tt = 0.0f;
         int sk = 0, tri = -1;
         bool ind = false, tv = false, lf = false;
+        float4 A = make_float4(0.f, 0.f, 0.f, 0.f), B = A;
         if (j < end) {
-            const float4 A = walk[2 * j];
-            const float4 B = walk[2 * j + 1];
-            const float4 Q0 = walk[2 * j + 2];                       // a leaf's triangle (end is padded)
-            const float4 Q1 = walk[2 * j + 3];
+            A = walk[2 * j];
+            B = walk[2 * j + 1];
+        }
+        const float4 Q0 = next_lane(A), Q1 = next_lane(B);          // the slot after this one (every lane active)
+        if (j < end) {
             slab(A, B, o, inv, te, ind);
             const uint32_t aw = __float_as_uint(A.w);
             lf = ((aw >> 30) & 1u) != 0u;
             sk = lf ? j + 2 : (int)(aw & 0x7FFFFFFFu);               // a leaf's skip is its successor, two slots on
             tri = (int)(aw & 0x3FFFFFFFu);
-            if (lf && ind && te < closest)
+            if (lf && ind && te < closest && lane < 63)
                 tv = tri_test(make_float4(B.w, Q0.x, Q0.y, 0.f), make_float4(Q0.z, Q0.w, Q1.x, 0.f),
                               make_float4(Q1.y, Q1.z, Q1.w, 0.f), o, d, tt);
         }
         uint64_t H = __ballot(ind && te < closest);
         uint64_t T = __ballot(tv && tt < closest);
         const uint64_t Lf = __ballot(lf);
-        const int lim = min(64, end - n);
+        int lim = min(64, end - n);
+        if (lim == 64 && (Lf >> 63)) lim = 63;                       // its triangle is past the window
         int k = 0;
         while (k < lim) {
             if ((H >> k) & 1ull) {
