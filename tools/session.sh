@@ -23,6 +23,8 @@
 #   spawn2    bench.py --gpus 2 with no launcher (it starts its own ranks):
 #             BENCH_SHARE_GPU=1 BENCH_DIST_BACKEND=gloo, two gloo ranks on one GPU
 #   spawn4    the same with 4 ranks and the 2 x 2 tile grid + radiance gather
+#   ab3 / ab5 bench.py interleaved against the tree in build_ab/old (tools/ab_old_new.sh),
+#             config 3 (3 rounds, 200 steps) / config 5 (2 rounds, 10 steps)
 #   cmd       the command in $CMD (600 s)
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -90,6 +92,8 @@ for s in "$@"; do
                   --warmup 5 > "$OUT/spawn2.json" 2> "$OUT/spawn2.err" ;;
     spawn4)   run spawn4 600 env BENCH_SHARE_GPU=1 BENCH_DIST_BACKEND=gloo python bench.py --gpus 4 --steps 10 \
                   --warmup 3 --partition tiles --gather radiance > "$OUT/spawn4.json" 2> "$OUT/spawn4.err" ;;
+    ab3)      run ab3 900 bash tools/ab_old_new.sh "$OUT/ab3" 3 --steps 200 --warmup 5 ;;
+    ab5)      run ab5 900 bash tools/ab_old_new.sh "$OUT/ab5" 2 --config 5 --steps 10 --warmup 3 ;;
     cmd)      run cmd 600 bash -c "$CMD" > "$OUT/cmd.log" 2>&1 ;;
     *)        status "unknown step $s" ;;
   esac
