@@ -25,6 +25,7 @@
 #   spawn4    the same with 4 ranks and the 2 x 2 tile grid + radiance gather
 #   ab3 / ab5 bench.py interleaved against the tree in build_ab/old (tools/ab_old_new.sh),
 #             config 3 (3 rounds, 200 steps) / config 5 (2 rounds, 10 steps)
+#   abargs    tools/ab_args.sh over the arms in $ARMS_FILE ($REPS rounds, $STEPS steps)
 #   cmd       the command in $CMD (600 s)
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -94,6 +95,8 @@ for s in "$@"; do
                   --warmup 3 --partition tiles --gather radiance > "$OUT/spawn4.json" 2> "$OUT/spawn4.err" ;;
     ab3)      run ab3 900 bash tools/ab_old_new.sh "$OUT/ab3" 3 --steps 200 --warmup 5 ;;
     ab5)      run ab5 900 bash tools/ab_old_new.sh "$OUT/ab5" 2 --config 5 --steps 10 --warmup 3 ;;
+    abargs)   run abargs 900 env ARMS_FILE="${ARMS_FILE:?}" REPS="${REPS:-3}" STEPS="${STEPS:-200}" \
+                  bash tools/ab_args.sh "$TAG/abargs_$(basename "$ARMS_FILE" .txt)" ;;
     cmd)      run cmd 600 bash -c "$CMD" > "$OUT/cmd.log" 2>&1 ;;
     *)        status "unknown step $s" ;;
   esac
