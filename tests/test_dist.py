@@ -436,3 +436,21 @@ def test_dealt_bands_balance_1080p():
     for f in range(8):
         allb = np.sort(np.concatenate([plan.frame_bands(r, f) for r in range(8)]))
         assert np.array_equal(allb, np.arange(135))
+
+
+def test_share_tracer_rejects_uneven_lists():
+    """Per-frame band lists (dealt / pieces, rt_render_batch_lists_device) pack
+    whole bands: a band height that does not divide the frame is refused up
+    front, as bench.py's --deal auto avoids choosing it."""
+    from rtamd.dist import SharePlan, ShareTracer, TilePlan
+    plan = SharePlan(1080, 16, 8, 8, 0.8, layout="dealt")
+    with pytest.raises(ValueError, match="divide the height"):
+        ShareTracer(None, 1920, 1080, 4, "bands", 1, plan=plan, band_h=16, batch=8)
+    ok = SharePlan(1080, 8, 8, 8, 0.8, layout="dealt")
+    t = ShareTracer(None, 1920, 1080, 4, "bands", 1, plan=ok, band_h=8, batch=8)
+    assert [len(b) for b in t.my_bands] == [len(ok.frame_bands(1, f)) for f in range(8)]
+    assert t.offset_rows(3) == ok.off[1][3]
+    with pytest.raises(ValueError):
+        ShareTracer(None, 1920, 1080, 4, "tiles", 0)
+    tt = ShareTracer(None, 1920, 1080, 4, "tiles", 3, tplan=TilePlan(1920, 1080, 4, 2), batch=2)
+    assert tt.rect == (960, 540, 960, 540)
