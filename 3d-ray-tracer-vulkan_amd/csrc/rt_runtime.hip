@@ -357,6 +357,7 @@ struct rt_ctx {
                                    //   (the heavy-tile bulk estimate counts this launch's work that many times)
     int  learn_cost = 1;           // heavy_first cost: 0 = lockstep steps + 2 x coop windows, 1 = wave duration
     int  learn_alone = 0;          // heavy_first: a learning launch first waits for the device to drain
+    int  learn_device = 1;         // heavy_first: learn the order on the device (rt_learn.hip; 0 = on the host)
     int  order_split = 0;          // heavy_first: only tiles costing >= this percent of the costliest go first
                                    //   (in cost order); the rest keep their raster order (0 = all by cost)
     int  order_frames = 0;         // heavy_first, several frames per launch: the non-leading tiles row by row
@@ -523,7 +524,8 @@ static int plan_order(const rt_ctx* ctx, PerDevice& p, TraceArgs& a, const rt_ca
     // pixels one per wave, as production launches), and the order is computed
     // on its stream afterwards with no synchronisation; one learning at a
     // time per device.  Other schedules learn on the host (learn_order).
-    const bool device = ctx->heavy_stream == 2 && ctx->heavy_pixels && ctx->heavy_tiles < 0 && !ctx->order_frames;
+    const bool device = ctx->learn_device && ctx->heavy_stream == 2 && ctx->heavy_pixels && ctx->heavy_tiles < 0 &&
+                        !ctx->order_frames;
     if (p.learn_busy) return reuse ? use(*reuse) : RT_OK;   // the device learning in flight finishes first
     // a fused launch's heavy-pixel waves record first: at most one per resident
     // wave slot (the largest cap any concurrency gives)
@@ -1747,6 +1749,8 @@ int rt_set_option(rt_ctx* ctx, const char* name, int64_t value) {
         ctx->order_split = (int)value;
     } else if (std::strcmp(name, "learn_alone") == 0 && (value == 0 || value == 1)) {
         ctx->learn_alone = (int)value;
+    } else if (std::strcmp(name, "learn_device") == 0 && (value == 0 || value == 1)) {
+        ctx->learn_device = (int)value;
     } else if (std::strcmp(name, "heavy_stream") == 0 && value >= 0 && value <= 2) {
         ctx->heavy_stream = (int)value;
     } else if (std::strcmp(name, "graph") == 0 && (value == 0 || value == 1)) {
@@ -1777,6 +1781,7 @@ int rt_get_option(rt_ctx* ctx, const char* name, int64_t* value) {
     else if (std::strcmp(name, "learn_cost") == 0) *value = ctx->learn_cost;
     else if (std::strcmp(name, "order_split") == 0) *value = ctx->order_split;
     else if (std::strcmp(name, "learn_alone") == 0) *value = ctx->learn_alone;
+    else if (std::strcmp(name, "learn_device") == 0) *value = ctx->learn_device;
     else if (std::strcmp(name, "heavy_factor") == 0) *value = ctx->heavy_factor;
     else if (std::strcmp(name, "concurrent_launches") == 0) *value = ctx->concurrent_launches;
     else if (std::strcmp(name, "async_slots") == 0) *value = ctx->async_slots;

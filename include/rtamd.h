@@ -336,6 +336,10 @@ int rt_render_poll(rt_ctx* ctx, uint64_t ticket, int* done);
  *                   8 = spheres (rt_upload_spheres) after the BVH walk
  *   "async_slots"   rt_render_async frames in flight per device (1..8, default 4)
  *   "copy_streams"  rt_render_async readback copy streams (1 or 2, default 1)
+ *   "learn_device"  heavy_first: 1 = learn the order on the device, on the
+ *                   learning launch's stream, with no synchronisation (default;
+ *                   the default heavy-pixel schedule only); 0 = copy the records
+ *                   back and learn on the host after a stream synchronisation
  *   "plain_kernels" (rt_get_option only) production-build trace kernels enqueued
  *                   on device 0 so far (not counting, diagnostic or learning
  *                   launches): lets a profiler's kernel trace be cut at a

@@ -212,3 +212,30 @@ def test_stats_struct_order(renderer):
     renderer.upload_scene(cfg.build())
     _, _, st = renderer.render(configs.Camera.default(64, 36), 64, 36, 2, stats=True)
     assert st["pixels"] == 64 * 36 and st["segments"] >= 64 * 36 and st["ms"] > 0
+
+
+@pytest.mark.parametrize("cfg_k", [3, 6])
+def test_device_learning_matches_host_learning(renderer, cfg_k):
+    """The order learned on the device (rt_learn.hip) picks the heavy pixels the
+    host path picks from the same kind of learning launch (learn_cost 0: the
+    lockstep steps, a deterministic cost), and every frame stays the oracle's."""
+    from rtamd import configs
+    cfg = configs.get(cfg_k)
+    built = cfg.build()
+    W, H, B = cfg.width, cfg.height, cfg.max_bounces
+    cam = configs.Camera((-25.0, 30.0, 141.5), (0.0, 0.0, 0.0), (0.0, 1.0, 0.0), 20.0, W / H)
+    ref = _oracle(built, cam.ubo_bytes(), W, H, B, row_step=9, radiance=False)[0]
+    used = {}
+    try:
+        renderer.set_option("learn_cost", 0)
+        for dev in (1, 0):
+            renderer.set_option("learn_device", dev)
+            renderer.upload_scene(built)                 # a new scene generation: nothing learned yet
+            for launch in range(3):                      # the learning launch, then the learned order
+                rgba = renderer.render(cam, W, H, B)[0]
+                assert np.array_equal(rgba[::9], ref), (dev, launch)
+            used[dev] = renderer.get_option("heavy_pixels_used")
+    finally:
+        renderer.set_option("learn_cost", 1)
+        renderer.set_option("learn_device", 1)
+    assert used[1] > 0 and used[1] == used[0], used
