@@ -10,7 +10,7 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB = os.path.join(HERE, "liboracle.so")
 ENV_LIB = os.path.join(HERE, "liboracle_env.so")     # rt_envelope.c: the Vulkan-envelope study
-ENV_FMA, ENV_RSQ, ENV_RCP, ENV_ULP = 1, 2, 4, 8          # rt_oracle.c ENV_* bits
+ENV_FMA, ENV_RSQ, ENV_RCP, ENV_ULP, ENV_FTZ = 1, 2, 4, 8, 16   # rt_oracle.c ENV_* bits
 
 
 class Counts(C.Structure):

@@ -67,7 +67,14 @@ typedef struct { float x, y, z; } vec3;
 #define ENV_RSQ 2        /* normalize(v) = v * inversesqrt(dot(v,v)), inversesqrt correctly rounded */
 #define ENV_RCP 4        /* a / b = a * (1 / b), the reciprocal correctly rounded */
 #define ENV_ULP 8        /* reciprocals and inversesqrts off by up to one ulp (a hash of the input picks) */
+#define ENV_FTZ 16       /* denormal inputs and results flushed to zero (shaderDenormPreserveFloat32 off) */
+#include <xmmintrin.h>
 static int g_env = 0;
+/* the calling thread's SSE control word for the selected variant (FTZ + DAZ or not) */
+static void env_fp_mode(void) {
+    const unsigned base = _mm_getcsr() & ~0x8040u;
+    _mm_setcsr(base | ((g_env & ENV_FTZ) ? 0x8040u : 0u));
+}
 static float env_ulp(float r, float x) {
     if (!(g_env & ENV_ULP)) return r;
     uint32_t b;
@@ -277,6 +284,9 @@ static unsigned char unorm8(float c) {
 static int shade_pixel(const scene* s, const orc_camera* cam, int W, int H, int max_bounces,
                        int px, int py, float out_rgb[3], orc_counts* cnt, uint32_t* prof, int ext,
                        float lin[3]) {
+#ifdef ORC_ENVELOPE
+    env_fp_mode();
+#endif
     uint32_t seed = (uint32_t)(py * W + px);                                   /* :164 */
     if (ext & ORC_EXT_ACCUMULATE)              /* extension: a new sample per frame (frame 0 = :164) */
         seed += (uint32_t)cam->frame_count * (uint32_t)(W * H);

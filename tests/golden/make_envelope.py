@@ -11,7 +11,9 @@ specifications let choose, where this repo's contract fixes IEEE binary32:
   (GLSL 4.50 §4.7.1: 2 ULP);
 * x / y through a reciprocal (2.5 ULP allowed), at compute_dynamic_ray.comp
   :89 (1.0 / dir), :112 (1.0 / det), :167-168 (the AA jitter divided by W, H)
-  and inside normalize().
+  and inside normalize();
+* denormals flushed to zero (Vulkan's shaderDenormPreserveFloat32 is an
+  optional feature the shader does not request).
 
 This script renders BASELINE configs 2 and 3 and config 6 (the reference's
 FinalBaseMesh) as whole frames with the oracle under each of those choices
@@ -23,10 +25,11 @@ vulkan_envelope.json beside this script; tests/test_envelope.py re-derives
 its row subsets on the CPU.
 
 Variants (ENV_* bits): fma 1, rsq 2, rcp 4, ulp 8 (reciprocals and
-inversesqrts off by up to one ulp, chosen by a hash of the input), llvm 7 (a
-compiler that fuses, uses rsq and rcp: what an LLVM-based driver does with
+inversesqrts off by up to one ulp, chosen by a hash of the input), ftz 16
+(denormal inputs and results flushed to zero), llvm 7 (a compiler that
+fuses, uses rsq and rcp: what an LLVM-based driver does with
 fast-math-style float lowering), llvm_ulp 15 (the same with approximate 1-ulp
-hardware rcp / rsq, the spec's worst case short of 2-2.5 ulp).
+hardware rcp / rsq, the spec's worst case short of 2-2.5 ulp), all 31.
 
 Usage: python tests/golden/make_envelope.py [--threads N]
 """
@@ -42,7 +45,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(os.path.dirname(HERE))
 sys.path[:0] = [os.path.join(ROOT, "3d-ray-tracer-vulkan_amd"), ROOT]
 
-VARIANTS = {"fma": 1, "rsq": 2, "rcp": 4, "ulp": 8, "llvm": 7, "llvm_ulp": 15}
+VARIANTS = {"fma": 1, "rsq": 2, "rcp": 4, "ulp": 8, "ftz": 16, "llvm": 7, "llvm_ulp": 15, "all": 31}
 CONFIGS = (2, 3, 6)
 SUBSET_STEP = {2: 16, 3: 32, 6: 32}      # the rows tests/test_envelope.py re-derives
 TOL = 1e-4
