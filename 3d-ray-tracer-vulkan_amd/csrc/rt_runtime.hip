@@ -444,7 +444,7 @@ static int plan_order(const rt_ctx* ctx, PerDevice& p, TraceArgs& a, const rt_ca
     // branch of the cooperative-tail kernel), and for the fused launch
     // (heavy_stream 2) the default walk 2, which that launch runs.  Otherwise
     // a launch uses the learned order alone (and reports no heavy work).
-    const bool splittable = a.coop_lanes > 0 && a.ext == 0 && (ctx->heavy_stream != 2 || a.walk >= 2);
+    const bool splittable = a.coop_lanes > 0 && a.ext == 0 && (ctx->heavy_stream != 2 || a.walk == 2);
     auto use = [&](const PerDevice::Order& o) -> int {
         a.tile_order = o.d_order;
         if (!splittable) return RT_OK;
@@ -890,7 +890,7 @@ int rt_create(const int* device_ids, int n_devices, rt_ctx** out) {
     if (!ctx) { set_error("rt_create: out of memory"); return RT_ERR_OOM; }
     if (const char* v = std::getenv("RTAMD_WALK")) {
         const int w = std::atoi(v);
-        ctx->walk = w == 0 ? 0 : (w == 3 ? 3 : 2);
+        ctx->walk = w == 0 ? 0 : 2;
     }
     // HIP reads GPU_MAX_HW_QUEUES once, when the runtime initialises (HIP's
     // default is 4 hardware queues per process); reported as option
@@ -1715,7 +1715,7 @@ int rt_set_option(rt_ctx* ctx, const char* name, int64_t value) {
         ctx->coop_lanes = (int)value;
     } else if (std::strcmp(name, "extensions") == 0 && value >= 0 && value <= 15) {
         ctx->ext = (int)value;
-    } else if (std::strcmp(name, "walk") == 0 && (value == 0 || value == 2 || value == 3)) {
+    } else if (std::strcmp(name, "walk") == 0 && (value == 0 || value == 2)) {
         ctx->walk = (int)value;
     } else if (std::strcmp(name, "coop_walk") == 0 && (value == 0 || value == 1)) {
         ctx->coop_walk = (int)value;

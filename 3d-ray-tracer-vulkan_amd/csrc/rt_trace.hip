@@ -790,7 +790,7 @@ void trace_simple(TraceArgs a) {
     const float4* __restrict__ leafs = a.scene.leafs;
     const float4* __restrict__ pairs = a.scene.pairs;
     const int end = a.scene.end;                         // node index end (walk 0, the frontier tail)
-    const int wend = WALK >= 2 ? a.scene.end2 : end;     // the lockstep walk's end: slots for walks 2 and 3
+    const int wend = WALK == 2 ? a.scene.end2 : end;     // the lockstep walk's end: slots for walk 2
     unsigned long long c_seg = 0, c_node = 0, c_tri = 0, c_mat = 0;
     unsigned long long d_iters = 0, d_windows = 0, d_coop_t = 0;   // diag builds only
     unsigned long long d_lane_windows = 0;           // diag: cooperative windows spent on this lane's walks
@@ -835,18 +835,12 @@ void trace_simple(TraceArgs a) {
             // walk 2 reads the walk records (DevScene::walk): a leaf's first
             // slot carries its triangle index and v0.x, and the slot after it,
             // Q0 and Q1, the rest of its triangle.
-            // walk 3 (option walk 3) visits a leaf in two steps: its box, and
-            // only if the box is hit, its triangle slot, loaded like a node's
-            // record, so every step of every lane reads one 32-B slot (2 loads
-            // per step, where walk 2 adds 2 for any lane bound for a leaf).
             float4 A, B, Q0, Q1;
-            uint32_t aws = 0;                  // walk 3: the leaf's link word while at its triangle slot (else 0)
-            float v0s = 0.f;                   // walk 3: that leaf's v0.x
             const float4* __restrict__ wr = a.scene.walk;
-            if (WALK >= 2 && walking) {
+            if (WALK == 2 && walking) {
                 A = wr[2 * n];
                 B = wr[2 * n + 1];
-                if (WALK == 2 && nleaf) {
+                if (nleaf) {
                     Q0 = wr[2 * n + 2];
                     Q1 = wr[2 * n + 3];
                 }
@@ -855,37 +849,6 @@ void trace_simple(TraceArgs a) {
                 if (DIAG) ++d_iters;
                 if (WALK == 0) {
                     n = node_step<COUNT>(nodes, leafs, n, nleaf, o, d, inv, closest, hit, c_node, c_tri);
-                } else if (WALK == 3) {
-                    const bool tslot = aws != 0u;                            // A, B = the leaf's (Q0, Q1)
-                    if (tslot) {                                             // hit_triangle (:196-200)
-                        float t;
-                        if (tri_test(make_float4(v0s, A.x, A.y, 0.f), make_float4(A.z, A.w, B.x, 0.f),
-                                     make_float4(B.y, B.z, B.w, 0.f), o, d, t) && t < closest) {
-                            closest = t;
-                            hit = (int)(aws & kTri);
-                        }
-                    }
-                    float te;
-                    bool ind;
-                    slab(A, B, o, inv, te, ind);
-                    const bool hb = !tslot && ind && te < closest;
-                    const uint32_t aw = __float_as_uint(A.w), bw = __float_as_uint(B.w);
-                    // next: a triangle slot -> the leaf's successor (the next slot);
-                    // a leaf box hit -> its triangle slot; missed -> its successor,
-                    // two slots on; an internal node hit -> its left child, the next
-                    // slot; missed -> its skip
-                    const int nxt = (tslot || hb) ? n + 1 : (nleaf ? n + 2 : (int)(aw & kIdx));
-                    const bool nl = tslot ? (aws >> 31) != 0u
-                                          : ((((hb && !nleaf) ? bw : (aw >> 31)) & 1u) != 0u);
-                    if (COUNT && hb && !nleaf) c_node += 2;
-                    if (COUNT && hb && nleaf) ++c_tri;
-                    const bool to_tri = hb && nleaf;
-                    if (to_tri) v0s = B.w;                                   // a leaf's v0.x
-                    aws = to_tri ? aw : 0u;
-                    A = wr[2 * nxt];                                         // slot end is padding
-                    B = wr[2 * nxt + 1];
-                    n = nxt;
-                    nleaf = to_tri ? nleaf : nl;                            // (unused at a triangle slot)
                 } else {
                     float te;
                     bool ind;
@@ -918,10 +881,7 @@ void trace_simple(TraceArgs a) {
                     nleaf = nl;
                 }
                 walking = n < wend;
-                // (walk 3 hands over only between visits: no lane at a triangle slot)
-                if ((FEAT & kFeatCoopTail) && __popcll(__ballot(walking)) <= coop_lanes &&
-                    (WALK != 3 || __ballot(aws != 0u) == 0))
-                    break;
+                if ((FEAT & kFeatCoopTail) && __popcll(__ballot(walking)) <= coop_lanes) break;
             }
         }
         if (FEAT & kFeatCoopTail) {
@@ -943,7 +903,7 @@ void trace_simple(TraceArgs a) {
                 int nw = 0;
                 if ((FEAT & kFeatFrontier) && a.coop_walk) {
                     // the frontier walk takes node indices: walk 2's slot -> node
-                    int p = WALK >= 2 ? a.scene.slot_node[lane_i(start, L)] : lane_i(start, L);
+                    int p = WALK == 2 ? a.scene.slot_node[lane_i(start, L)] : lane_i(start, L);
                     bool pl = false;
                     if (!frontier_walk<COUNT>(nodes, leafs, pairs, end, p, pl, bo, bd, bi, bc, bh, cn, ct,
                                               fr + wave * kFCap, nw))
@@ -951,7 +911,7 @@ void trace_simple(TraceArgs a) {
                 } else {
                     // the windows walk slots of the walk-2 records (walk 0 hands over a
                     // node index: its slot first)
-                    const int ws = WALK >= 2 ? lane_i(start, L) : a.scene.node_slot[lane_i(start, L)];
+                    const int ws = WALK == 2 ? lane_i(start, L) : a.scene.node_slot[lane_i(start, L)];
                     nw = coop_walk<COUNT>(a.scene.walk, a.scene.end2, ws, bo, bd, bi, bc, bh, cn, ct);
                 }
                 if (DIAG) {
@@ -1037,17 +997,11 @@ void trace_simple(TraceArgs a) {
 
 }  // namespace
 
-// The fused heavy-pixel launch, walk 2 or walk 3 (option walk).
+// The fused heavy-pixel launch (walk 2).
 #define RT_FUSED(G)                                                                                           \
-    if (a.walk == 3) {                                                                                        \
-        if (a.diag) hipLaunchKernelGGL((trace_simple<false, true, FF, 3>), G, block, shm, stream, ao);         \
-        else if (a.counters) hipLaunchKernelGGL((trace_simple<true, false, FF, 3>), G, block, shm, stream, ao); \
-        else hipLaunchKernelGGL((trace_simple<false, false, FF, 3>), G, block, shm, stream, ao);               \
-    } else {                                                                                                  \
-        if (a.diag) hipLaunchKernelGGL((trace_simple<false, true, FF, 2>), G, block, shm, stream, ao);         \
-        else if (a.counters) hipLaunchKernelGGL((trace_simple<true, false, FF, 2>), G, block, shm, stream, ao); \
-        else hipLaunchKernelGGL((trace_simple<false, false, FF, 2>), G, block, shm, stream, ao);               \
-    }
+    if (a.diag) hipLaunchKernelGGL((trace_simple<false, true, FF, 2>), G, block, shm, stream, ao);             \
+    else if (a.counters) hipLaunchKernelGGL((trace_simple<true, false, FF, 2>), G, block, shm, stream, ao);     \
+    else hipLaunchKernelGGL((trace_simple<false, false, FF, 2>), G, block, shm, stream, ao);
 
 hipError_t launch_trace(const TraceArgs& a, hipStream_t stream, int* kernels) {
     if (kernels) *kernels = 1;
@@ -1123,9 +1077,7 @@ hipError_t launch_trace(const TraceArgs& a, hipStream_t stream, int* kernels) {
     if (a.diag) hipLaunchKernelGGL((trace_simple<false, true, F, W>), grid, block, ((F) & kFeatFrontier) ? shm_f : 0, stream, ao);           \
     else if (a.counters) hipLaunchKernelGGL((trace_simple<true, false, F, W>), grid, block, ((F) & kFeatFrontier) ? shm_f : 0, stream, ao); \
     else hipLaunchKernelGGL((trace_simple<false, false, F, W>), grid, block, ((F) & kFeatFrontier) ? shm_f : 0, stream, ao);
-    if (a.walk == 3 && feat == kFeatCoopTail) {
-        RT_SIMPLE(kFeatCoopTail, 3)
-    } else if (a.walk >= 2) {
+    if (a.walk == 2) {
         switch (feat) {
             case kFeatCoopTail: RT_SIMPLE(kFeatCoopTail, 2) break;
             case 0: RT_SIMPLE(0, 2) break;

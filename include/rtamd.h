@@ -235,10 +235,8 @@ int rt_render_poll(rt_ctx* ctx, uint64_t ticket, int* done);
  *   "walk"          0 = one node per step, 2 = one node per step,
  *                   software-pipelined over compact records: the next node's
  *                   box is requested before this node's triangle test and the
- *                   loop control (default); 3 = the same, a leaf visited in two
- *                   steps (its box, then its triangle slot only if the box is
- *                   hit), so every step loads one 32-B slot per lane.  Walks 1,
- *                   5, 13, 14 are archived.
+ *                   loop control (default).  Walks 1, 3 (round 4: a leaf in
+ *                   two steps), 5, 13, 14 were measured slower and archived.
  *   "coop_lanes"    once at most this many lanes of a wave are still walking,
  *                   the whole wave finishes their walks one ray at a time
  *                   (0..64, default 1; 0 = off)

@@ -142,11 +142,6 @@ def test_config5_1m_row_subset(renderer):
     {"coop_walk": 1, "coop_lanes": 8},
     {"coop_walk": 1, "coop_lanes": 64},
     {"coop_walk": 1, "coop_lanes": 64, "walk": 0},
-    {"walk": 3},
-    {"walk": 3, "coop_lanes": 8},
-    {"walk": 3, "coop_lanes": 0},
-    {"walk": 3, "coop_walk": 1},
-    {"walk": 3, "heavy_first": 0},
 ])
 def test_schedules_identical(renderer, opts):
     """Every schedule gives the oracle's frame and counters (config 2 at the
@@ -270,7 +265,7 @@ def test_heavy_pixels(renderer, cfg_k, factor):
             renderer.set_option(k, v)
 
 
-@pytest.mark.parametrize("cfg_k,walk", [(3, 2), (4, 2), (5, 2), (6, 2), (3, 0), (3, 3), (5, 3), (6, 3)])
+@pytest.mark.parametrize("cfg_k,walk", [(3, 2), (4, 2), (5, 2), (6, 2), (3, 0)])
 def test_bench_setting_whole_frame(renderer, cfg_k, walk):
     """BASELINE configs 3, 4 and 5 as whole frames (config 5: 1M triangles,
     3840x2160, 8 bounces) under bench.py's N = 1 setting: the default
