@@ -353,6 +353,9 @@ __device__ __forceinline__ float lane_f(float v, int k) {
 }
 
 // ------------------------------------------------------------ cooperative walk --
+#ifndef RT_COOP_DPP
+#define RT_COOP_DPP 1      // a leaf's triangle from the next lane by DPP (0: loaded by the lane, A/B builds)
+#endif
 //
 // The whole wave walks ONE ray (arguments wave-uniform), replaying the
 // reference's visit sequence exactly:
@@ -386,18 +389,28 @@ __device__ __forceinline__ int coop_walk(const float4* __restrict__ walk, int en
         int sk = 0, tri = -1;
         bool ind = false, tv = false, lf = false;
         float4 A = make_float4(0.f, 0.f, 0.f, 0.f), B = A;
+#if RT_COOP_DPP
         if (j < end) {
             A = walk[2 * j];
             B = walk[2 * j + 1];
         }
         const float4 Q0 = next_lane(A), Q1 = next_lane(B);          // the slot after this one (every lane active)
+#else
+        float4 Q0 = A, Q1 = A;                                       // (A/B variant: the slot after, loaded)
+        if (j < end) {
+            A = walk[2 * j];
+            B = walk[2 * j + 1];
+            Q0 = walk[2 * j + 2];
+            Q1 = walk[2 * j + 3];
+        }
+#endif
         if (j < end) {
             slab(A, B, o, inv, te, ind);
             const uint32_t aw = __float_as_uint(A.w);
             lf = ((aw >> 30) & 1u) != 0u;
             sk = lf ? j + 2 : (int)(aw & 0x7FFFFFFFu);               // a leaf's skip is its successor, two slots on
             tri = (int)(aw & 0x3FFFFFFFu);
-            if (lf && ind && te < closest && lane < 63)
+            if (lf && ind && te < closest && (!RT_COOP_DPP || lane < 63))
                 tv = tri_test(make_float4(B.w, Q0.x, Q0.y, 0.f), make_float4(Q0.z, Q0.w, Q1.x, 0.f),
                               make_float4(Q1.y, Q1.z, Q1.w, 0.f), o, d, tt);
         }
@@ -405,7 +418,7 @@ __device__ __forceinline__ int coop_walk(const float4* __restrict__ walk, int en
         uint64_t T = __ballot(tv && tt < closest);
         const uint64_t Lf = __ballot(lf);
         int lim = min(64, end - n);
-        if (lim == 64 && (Lf >> 63)) lim = 63;                       // its triangle is past the window
+        if (RT_COOP_DPP && lim == 64 && (Lf >> 63)) lim = 63;        // its triangle is past the window
         int k = 0;
         while (k < lim) {
             if ((H >> k) & 1ull) {
