@@ -213,6 +213,9 @@ int build_host_scene(const void* vertices, size_t vertex_bytes,
 using namespace rtamd;
 
 static constexpr int kMaxSlots = 8;   // rt_render_async frame slots per device
+#ifndef RT_LEAF_ALIGN
+#define RT_LEAF_ALIGN 0
+#endif
 
 struct PerDevice {
     int          device = 0;
@@ -358,6 +361,7 @@ struct rt_ctx {
     int  learn_cost = 1;           // heavy_first cost: 0 = lockstep steps + 2 x coop windows, 1 = wave duration
     int  learn_alone = 0;          // heavy_first: a learning launch first waits for the device to drain
     int  learn_device = 1;         // heavy_first: learn the order on the device (rt_learn.hip; 0 = on the host)
+    int  leaf_align = RT_LEAF_ALIGN;   // walk records: no leaf straddles a 128-B line (a pad slot before it)
     int  order_split = 0;          // heavy_first: only tiles costing >= this percent of the costliest go first
                                    //   (in cost order); the rest keep their raster order (0 = all by cost)
     int  order_frames = 0;         // heavy_first, several frames per launch: the non-leading tiles row by row
@@ -1015,13 +1019,22 @@ int rt_upload_scene(rt_ctx* ctx, const void* vertices, size_t vertex_bytes,
     // leaf's successor (its skip, i+1) the slot after its two, and only the
     // internal skip is stored, as a slot.  The visit sequence is the
     // reference's, node for node.
+    // Option leaf_align: a leaf that would start in the last slot of a 128-B
+    // line (and straddle two) starts one slot later; its predecessor's pad bit
+    // (a leaf's bit 29 of word [0].w, an internal node's bit 2 of word [1].w)
+    // tells the walk to step over the pad slot.
     const size_t n2 = (size_t)hs.n_nodes;
     std::vector<int> slot(n2 + 1);
+    std::vector<uint8_t> padded(n2 + 1, 0);       // a pad slot precedes node i
     size_t nslot = 0;
     for (size_t i = 0; i < n2; ++i) {
-        slot[i] = (int)nslot;
         uint32_t fl;
         std::memcpy(&fl, &hs.nodes[2 * i + 1].w, 4);
+        if (ctx->leaf_align && (fl & 2u) && nslot % 4 == 3) {
+            padded[i] = 1;
+            ++nslot;
+        }
+        slot[i] = (int)nslot;
         nslot += (fl & 2u) ? 2 : 1;
         if (nslot >= (1u << 30)) {
             free_host_scene(&hs);
@@ -1044,17 +1057,23 @@ int rt_upload_scene(rt_ctx* ctx, const void* vertices, size_t vertex_bytes,
             const uint32_t sk = link & 0x7FFFFFFFu;
             const uint32_t w0 = (uint32_t)slot[sk] | (link & 0x80000000u);
             std::memcpy(&walk[w].w, &w0, 4);
+            if (padded[i + 1]) {                            // the left child (i+1) sits past a pad slot
+                uint32_t w1;
+                std::memcpy(&w1, &walk[w + 1].w, 4);
+                w1 |= 4u;
+                std::memcpy(&walk[w + 1].w, &w1, 4);
+            }
             continue;
         }
         uint32_t tri;
         std::memcpy(&tri, &hs.leafs[3 * i].w, 4);
-        if ((link & 0x7FFFFFFFu) != i + 1 || tri >= (1u << 30)) {
+        if ((link & 0x7FFFFFFFu) != i + 1 || tri >= (1u << 29)) {
             free_host_scene(&hs);
             set_error("rt_upload_scene: leaf %zu: skip %u is not i+1 or triangle index %u too large", i,
                       link & 0x7FFFFFFFu, tri);
             return RT_ERR_BAD_SCENE;
         }
-        const uint32_t w0 = tri | (1u << 30) | (link & 0x80000000u);
+        const uint32_t w0 = tri | (padded[i + 1] ? 1u << 29 : 0u) | (1u << 30) | (link & 0x80000000u);
         std::memcpy(&walk[w].w, &w0, 4);
         walk[w + 1].w = hs.leafs[3 * i].x;                                   // v0.x
         const float4 P0 = hs.leafs[3 * i], P1 = hs.leafs[3 * i + 1], P2 = hs.leafs[3 * i + 2];
@@ -1751,6 +1770,8 @@ int rt_set_option(rt_ctx* ctx, const char* name, int64_t value) {
         ctx->learn_alone = (int)value;
     } else if (std::strcmp(name, "learn_device") == 0 && (value == 0 || value == 1)) {
         ctx->learn_device = (int)value;
+    } else if (std::strcmp(name, "leaf_align") == 0 && (value == 0 || value == 1)) {
+        ctx->leaf_align = (int)value;                   // takes effect at the next rt_upload_scene
     } else if (std::strcmp(name, "heavy_stream") == 0 && value >= 0 && value <= 2) {
         ctx->heavy_stream = (int)value;
     } else if (std::strcmp(name, "graph") == 0 && (value == 0 || value == 1)) {
@@ -1782,6 +1803,7 @@ int rt_get_option(rt_ctx* ctx, const char* name, int64_t* value) {
     else if (std::strcmp(name, "order_split") == 0) *value = ctx->order_split;
     else if (std::strcmp(name, "learn_alone") == 0) *value = ctx->learn_alone;
     else if (std::strcmp(name, "learn_device") == 0) *value = ctx->learn_device;
+    else if (std::strcmp(name, "leaf_align") == 0) *value = ctx->leaf_align;
     else if (std::strcmp(name, "heavy_factor") == 0) *value = ctx->heavy_factor;
     else if (std::strcmp(name, "concurrent_launches") == 0) *value = ctx->concurrent_launches;
     else if (std::strcmp(name, "async_slots") == 0) *value = ctx->async_slots;

@@ -387,7 +387,7 @@ __device__ __forceinline__ int coop_walk(const float4* __restrict__ walk, int en
         const int j = n + lane;
         float te = 0.0f, tt = 0.0f;
         int sk = 0, tri = -1;
-        bool ind = false, tv = false, lf = false;
+        bool ind = false, tv = false, lf = false, pd = false;
         float4 A = make_float4(0.f, 0.f, 0.f, 0.f), B = A;
 #if RT_COOP_DPP
         if (j < end) {
@@ -408,8 +408,10 @@ __device__ __forceinline__ int coop_walk(const float4* __restrict__ walk, int en
             slab(A, B, o, inv, te, ind);
             const uint32_t aw = __float_as_uint(A.w);
             lf = ((aw >> 30) & 1u) != 0u;
-            sk = lf ? j + 2 : (int)(aw & 0x7FFFFFFFu);               // a leaf's skip is its successor, two slots on
-            tri = (int)(aw & 0x3FFFFFFFu);
+            // a leaf's skip is its successor, two slots on (three past a pad slot)
+            sk = lf ? j + 2 + (int)((aw >> 29) & 1u) : (int)(aw & 0x7FFFFFFFu);
+            tri = (int)(aw & 0x1FFFFFFFu);
+            pd = lf ? ((aw >> 29) & 1u) != 0u : ((__float_as_uint(B.w) >> 2) & 1u) != 0u;
             if (lf && ind && te < closest && (!RT_COOP_DPP || lane < 63))
                 tv = tri_test(make_float4(B.w, Q0.x, Q0.y, 0.f), make_float4(Q0.z, Q0.w, Q1.x, 0.f),
                               make_float4(Q1.y, Q1.z, Q1.w, 0.f), o, d, tt);
@@ -417,6 +419,7 @@ __device__ __forceinline__ int coop_walk(const float4* __restrict__ walk, int en
         uint64_t H = __ballot(ind && te < closest);
         uint64_t T = __ballot(tv && tt < closest);
         const uint64_t Lf = __ballot(lf);
+        const uint64_t Pd = __ballot(pd);                           // a pad slot follows (leaf alignment)
         int lim = min(64, end - n);
         if (RT_COOP_DPP && lim == 64 && (Lf >> 63)) lim = 63;        // its triangle is past the window
         int k = 0;
@@ -432,7 +435,7 @@ __device__ __forceinline__ int coop_walk(const float4* __restrict__ walk, int en
                         T = __ballot(tv && tt < closest);
                     }
                 }
-                k += ((Lf >> k) & 1ull) ? 2 : 1;
+                k += (((Lf >> k) & 1ull) ? 2 : 1) + (int)((Pd >> k) & 1ull);
             } else {
                 k = lane_i(sk, k) - n;
             }
@@ -475,7 +478,7 @@ __device__ __forceinline__ int coop_walk(const float4* __restrict__ walk, int en
 // 4x the reference's 64-entry stack), the walk stops with pos = the
 // reference's next node, to be finished by node_step.
 constexpr uint32_t kIdx = 0x7FFFFFFFu;      // node index bits of a link word
-constexpr uint32_t kTri = 0x3FFFFFFFu;      // triangle index bits of a compact leaf record's link word
+constexpr uint32_t kTri = 0x1FFFFFFFu;      // triangle index bits of a leaf's link word (bit 29: pad after it)
 constexpr int kFCap = 256;                   // frontier entries per wave (16 B each)
 constexpr int kFReserve = 80;                // slots speculation leaves to the front (> 64-deep descent)
 constexpr uint32_t kUnres = 0xFFFFFFFFu;
@@ -870,8 +873,10 @@ void trace_simple(TraceArgs a) {
                     const uint32_t aw = __float_as_uint(A.w), bw = __float_as_uint(B.w);
                     // a leaf's next node is its successor, two slots on, whether it
                     // is hit or not (its skip); an internal node's left child is
-                    // the next slot
-                    const int nxt = nleaf ? n + 2 : (hb ? n + 1 : (int)(aw & kIdx));
+                    // the next slot (one more past a pad slot: leaf bit 29 of word
+                    // [0].w, internal bit 2 of word [1].w)
+                    const int nxt = nleaf ? n + 2 + (int)((aw >> 29) & 1u)
+                                          : (hb ? n + 1 + (int)((bw >> 2) & 1u) : (int)(aw & kIdx));
                     const bool nl = (((hb && !nleaf) ? bw : (aw >> 31)) & 1u) != 0u;
                     const float v0x = B.w;                                   // a leaf's v0.x
                     if (COUNT && hb && !nleaf) c_node += 2;

@@ -239,3 +239,33 @@ def test_device_learning_matches_host_learning(renderer, cfg_k):
         renderer.set_option("learn_cost", 1)
         renderer.set_option("learn_device", 1)
     assert used[1] > 0 and used[1] == used[0], used
+
+
+@pytest.mark.parametrize("cfg_k", [3, 6, 2])
+def test_leaf_align_bit_exact(renderer, cfg_k):
+    """Option leaf_align (walk records with a pad slot before any leaf that
+    would straddle a 128-B line; the predecessor's pad bit steps over it):
+    frames and counters equal the oracle's, in the lockstep walk, the
+    cooperative windows (coop_lanes 64: every walk) and the learned order."""
+    from rtamd import configs
+    cfg = configs.get(cfg_k)
+    built = cfg.build()
+    W, H, B = cfg.width, cfg.height, cfg.max_bounces
+    cam = cfg.camera()
+    ref = _oracle(built, cam.ubo_bytes(), W, H, B, row_step=7)
+    try:
+        renderer.set_option("leaf_align", 1)
+        renderer.upload_scene(built)
+        for coop in (1, 64):
+            renderer.set_option("coop_lanes", coop)
+            for launch in range(2):
+                rgba, rad, st = renderer.render(cam, W, H, B, radiance=True, stats=launch == 1)
+                assert np.array_equal(rgba[::7], ref[0]), (coop, launch)
+                assert np.array_equal(rad[::7].view(np.uint32), ref[1].view(np.uint32)), (coop, launch)
+        full = _oracle(built, cam.ubo_bytes(), W, H, B, radiance=False)[2]
+        for k in ("segments", "node_visits", "tri_tests", "mat_reads"):
+            assert st[k] == full[k], k
+    finally:
+        renderer.set_option("leaf_align", 0)
+        renderer.set_option("coop_lanes", 1)
+        renderer.upload_scene(built)

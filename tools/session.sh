@@ -100,6 +100,10 @@ for s in "$@"; do
                   bash tools/ab_args.sh "$TAG/abargs_$(basename "$ARMS_FILE" .txt)" ;;
     abcoop)   run abcoop 900 env REPS=3 bash tools/ab_lib.sh "$OUT/abcoop" "--steps 200 --warmup 5" \
                   3d-ray-tracer-vulkan_amd/lib/librtamd.so 3d-ray-tracer-vulkan_amd/lib/variants/librtamd_coop4.so ;;
+    abalign)  run abalign 900 env REPS=2 bash tools/ab_lib.sh "$OUT/abalign5" "--config 5 --steps 10 --warmup 3" \
+                  3d-ray-tracer-vulkan_amd/lib/librtamd.so 3d-ray-tracer-vulkan_amd/lib/variants/librtamd_align.so && \
+              run abalign3 900 env REPS=3 bash tools/ab_lib.sh "$OUT/abalign3" "--steps 200 --warmup 5" \
+                  3d-ray-tracer-vulkan_amd/lib/librtamd.so 3d-ray-tracer-vulkan_amd/lib/variants/librtamd_align.so ;;
     cmd)      run cmd 600 bash -c "$CMD" > "$OUT/cmd.log" 2>&1 ;;
     *)        status "unknown step $s" ;;
   esac
