@@ -15,6 +15,7 @@
 #             config 3, merged into gpurun_out/TAG/pmc_latest.json
 #   pmc5      the same for config 5
 #   pmc5a     pmc5 on lib/variants/librtamd_align.so (leaf_align 1), record key ...@align
+#   fetch5    pmc5 with coop_lanes 0 (no cooperative tail) and with order_split 40
 #   pmc3o     the same for config 3 with the orbiting camera (record key cfg3_...@orbit)
 #   orbit     bench.py --camera-path orbit at 20 steps
 #   cfgs      bench.py on configs 4, 5, 6
@@ -81,6 +82,8 @@ for s in "$@"; do
     pmc3)     pmc 3 cfg3_50k_1920x1080_b4 ;;
     pmc5)     pmc 5 cfg5_1M_3840x2160_b8 ;;
     pmc5a)    RTAMD_LIB_PATH=3d-ray-tracer-vulkan_amd/lib/variants/librtamd_align.so pmc 5 cfg5_1M_3840x2160_b8@align a ;;
+    fetch5)   pmc 5 cfg5_1M_3840x2160_b8@nocoop n "--set coop_lanes=0" && \
+              pmc 5 cfg5_1M_3840x2160_b8@split40 s "--set order_split=40" ;;
     pmc3o)    pmc 3 cfg3_50k_1920x1080_b4@orbit o "--camera-path orbit" ;;
     orbit)    run orbit 600 python bench.py --steps 20 --warmup 5 --camera-path orbit \
                   > "$OUT/bench_orbit.json" 2> "$OUT/bench_orbit.err" ;;
