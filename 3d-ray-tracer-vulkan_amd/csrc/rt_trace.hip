@@ -356,6 +356,9 @@ __device__ __forceinline__ float lane_f(float v, int k) {
 #ifndef RT_COOP_DPP
 #define RT_COOP_DPP 1      // a leaf's triangle from the next lane by DPP (0: loaded by the lane, A/B builds)
 #endif
+#ifndef RT_COOP_WIN
+#define RT_COOP_WIN 64     // slots per window (lanes that load; 16 / 32: A/B builds)
+#endif
 //
 // The whole wave walks ONE ray (arguments wave-uniform), replaying the
 // reference's visit sequence exactly:
@@ -385,26 +388,27 @@ __device__ __forceinline__ int coop_walk(const float4* __restrict__ walk, int en
     while (n < end) {
         ++windows;
         const int j = n + lane;
+        const bool ld = j < end && lane < RT_COOP_WIN;
         float te = 0.0f, tt = 0.0f;
         int sk = 0, tri = -1;
         bool ind = false, tv = false, lf = false, pd = false;
         float4 A = make_float4(0.f, 0.f, 0.f, 0.f), B = A;
 #if RT_COOP_DPP
-        if (j < end) {
+        if (ld) {
             A = walk[2 * j];
             B = walk[2 * j + 1];
         }
         const float4 Q0 = next_lane(A), Q1 = next_lane(B);          // the slot after this one (every lane active)
 #else
         float4 Q0 = A, Q1 = A;                                       // (A/B variant: the slot after, loaded)
-        if (j < end) {
+        if (ld) {
             A = walk[2 * j];
             B = walk[2 * j + 1];
             Q0 = walk[2 * j + 2];
             Q1 = walk[2 * j + 3];
         }
 #endif
-        if (j < end) {
+        if (ld) {
             slab(A, B, o, inv, te, ind);
             const uint32_t aw = __float_as_uint(A.w);
             lf = ((aw >> 30) & 1u) != 0u;
@@ -412,7 +416,7 @@ __device__ __forceinline__ int coop_walk(const float4* __restrict__ walk, int en
             sk = lf ? j + 2 + (int)((aw >> 29) & 1u) : (int)(aw & 0x7FFFFFFFu);
             tri = (int)(aw & 0x1FFFFFFFu);
             pd = lf ? ((aw >> 29) & 1u) != 0u : ((__float_as_uint(B.w) >> 2) & 1u) != 0u;
-            if (lf && ind && te < closest && (!RT_COOP_DPP || lane < 63))
+            if (lf && ind && te < closest && (!RT_COOP_DPP || lane < RT_COOP_WIN - 1))
                 tv = tri_test(make_float4(B.w, Q0.x, Q0.y, 0.f), make_float4(Q0.z, Q0.w, Q1.x, 0.f),
                               make_float4(Q1.y, Q1.z, Q1.w, 0.f), o, d, tt);
         }
@@ -420,8 +424,9 @@ __device__ __forceinline__ int coop_walk(const float4* __restrict__ walk, int en
         uint64_t T = __ballot(tv && tt < closest);
         const uint64_t Lf = __ballot(lf);
         const uint64_t Pd = __ballot(pd);                           // a pad slot follows (leaf alignment)
-        int lim = min(64, end - n);
-        if (RT_COOP_DPP && lim == 64 && (Lf >> 63)) lim = 63;        // its triangle is past the window
+        int lim = min(RT_COOP_WIN, end - n);
+        if (RT_COOP_DPP && lim == RT_COOP_WIN && ((Lf >> (RT_COOP_WIN - 1)) & 1ull))
+            lim = RT_COOP_WIN - 1;                                   // its triangle is past the window
         int k = 0;
         while (k < lim) {
             if ((H >> k) & 1ull) {

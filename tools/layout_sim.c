@@ -37,8 +37,12 @@ static int cache_access(cache_t* c, int64_t line) {
     return 0;
 }
 
+/* A negative node entry -(x + 1) is a cooperative-tail window starting at
+ * node x: every node whose walk slot lies in [slot(x), slot(x) + window) is
+ * loaded (node_slot: the walk-slot number the window counts in). */
 int64_t layout_sim(int n_tiles, const int64_t* tile_ptr, const int64_t* step_ptr, const int32_t* nodes,
-                   const int64_t* node_lines, int resident, int sets, int ways, int64_t* out_accesses) {
+                   const int64_t* node_lines, const int64_t* node_slot, int64_t n_nodes, int window,
+                   int resident, int sets, int ways, int64_t* out_accesses) {
     cache_t c;
     c.sets = sets;
     c.ways = ways;
@@ -60,18 +64,28 @@ int64_t layout_sim(int n_tiles, const int64_t* tile_ptr, const int64_t* step_ptr
         }
     }
     int64_t acc = 0, miss = 0;
-    int64_t seen[96];
+    enum { kSeen = 512 };
+    int64_t seen[kSeen];
     while (live > 0) {
         for (int r = 0; r < resident; ++r) {
             if (cur[r] >= end[r]) continue;
             const int64_t st = cur[r]++;
             int ns = 0;
             for (int64_t k = step_ptr[st]; k < step_ptr[st + 1]; ++k) {
-                const int64_t* nl = node_lines + 3 * (size_t)nodes[k];
-                for (int j = 0; j < 3 && nl[j] >= 0; ++j) {
-                    int dup = 0;
-                    for (int q = 0; q < ns; ++q) if (seen[q] == nl[j]) { dup = 1; break; }
-                    if (!dup && ns < 96) seen[ns++] = nl[j];
+                int64_t x = nodes[k], last = x;
+                if (x < 0) {                                  /* a window */
+                    x = -x - 1;
+                    last = x;
+                    while (last + 1 < n_nodes && node_slot[last + 1] < node_slot[x] + window) ++last;
+                }
+                for (int64_t y = x; y <= last; ++y) {
+                    const int64_t* nl = node_lines + 3 * (size_t)y;
+                    for (int j = 0; j < 3 && nl[j] >= 0; ++j) {
+                        int dup = 0;
+                        for (int q = ns - 1; q >= 0 && q >= ns - 8; --q) if (seen[q] == nl[j]) { dup = 1; break; }
+                        if (!dup) for (int q = 0; q < ns - 8; ++q) if (seen[q] == nl[j]) { dup = 1; break; }
+                        if (!dup && ns < kSeen) seen[ns++] = nl[j];
+                    }
                 }
             }
             for (int q = 0; q < ns; ++q) {
