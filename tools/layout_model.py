@@ -19,7 +19,15 @@ Layouts (32-B slots, 4 per line):
   separate      round 3's records: a 32-B box per node, a 48-B triangle
                 record per leaf by leaf ordinal
 
-Usage: layout_model.py [--config 5] [--rows 64] [--row0 N] [--xcd 0] [--resident 1024] [--workers 8]
+The walk is replayed as the kernel runs it: bounce by bounce (the bounce loop
+is wave-uniform), lockstep while two or more lanes walk, then the cooperative
+tail (--coop 1, coop_lanes 1): the last lane's remaining visits in 64-slot
+windows.  Config 5 (rows 103-166, 3,840 tiles of XCD 0): 292,630 windows, i.e.
+9.9 M per frame (the GPU's diagnostic launch counts 9.48 M); the misses scale to
+~20 GB per frame (PMC FETCH 28.5 GB), two thirds of them the windows', which
+serve 4.2 visits each (median 2) and use 2.5 of their ~17 lines.
+
+Usage: layout_model.py [--config 5] [--rows 64] [--row0 N] [--xcd 0] [--resident 1024] [--workers 8] [--coop 1]
 """
 import argparse
 import ctypes as C
