@@ -151,6 +151,7 @@ struct TraceArgs {
     hipEvent_t ev_fork, ev_join;
     int      coop_walk;         // cooperative tail: 0 = 64-node preorder windows (coop_walk),
                                 //   1 = preorder frontier (frontier_walk)
+    int      coop_win = 64;     // coop_walk's window: 64 or 32 slots (option coop_window)
     int      list_stride;       // band_list per frame: frame f's at band_list + f * list_stride
                                 //   (0 = one list for every frame of the launch)
 };

@@ -297,6 +297,11 @@ struct PerDevice {
 static constexpr size_t kMaxOrders = 16;
 static constexpr int    kResidentPerCu = 24;    // resident trace waves per CU (diag timelines)
 static constexpr int    kMaxHeavy = 256;
+// coop_window 0: scenes whose walk records exceed the 8 XCDs' L2s together
+// (8 x 4 MB) take 32-slot windows: config 5 (100 MB) fetched 22.4 instead of
+// 28.5 GB per frame at the same frame time; config 3 (6.3 MB, L2-resident)
+// is 1.2% faster with 64 (profiles/r04/r4f).
+static constexpr size_t kWin32Bytes = 32ull << 20;
 static constexpr size_t kDiagWords = 8;   // per-wave diag record (rt_trace.hip, rtamd.h rt_diag_copy)
 
 static void free_order(PerDevice::Order& o) {
@@ -344,6 +349,8 @@ struct rt_ctx {
     int  walk = 2;                 // 0 = node per step, 2 = node per step, software-pipelined over the
                                    //   compact records (fastest measured)
     int  coop_walk = 0;            // cooperative walks: 0 = 64-node windows, 1 = preorder frontier
+    int  coop_window = 0;          // coop_walk's window: 64 or 32 slots; 0 = 32 when the walk records
+                                   //   exceed kWin32Bytes (they cannot stay in the L2s), else 64
     int  block_waves = 1;          // waves per workgroup (1: a finished wave frees its slot at once; or 4)
     int  heavy_first = 1;          // dispatch tiles in the cost order of a learning launch
     int  heavy_factor = 130;       // automatic heavy tiles: walk length above this percentage of the bulk estimate
@@ -736,12 +743,18 @@ static int learn_order(const rt_ctx* ctx, PerDevice& p, const TraceArgs& a, hipS
     return RT_OK;
 }
 
+static int coop_window_of(const rt_ctx* ctx, const PerDevice& p) {
+    if (ctx->coop_window) return ctx->coop_window;
+    return (size_t)p.scene.end2 * 32 > kWin32Bytes ? 32 : 64;
+}
+
 static int set_schedule(const rt_ctx* ctx, PerDevice& p, TraceArgs& a, const rt_camera_ubo* cam,
                         const std::vector<int>* bands = nullptr) {
     a.wave_tile = ctx->wave_tile;
     a.coop_lanes = ctx->coop_lanes;
     a.walk = ctx->walk;
     a.coop_walk = ctx->coop_walk;
+    a.coop_win = coop_window_of(ctx, p);
     a.block_waves = ctx->block_waves;
     a.ext = ctx->ext;
     a.scene.spheres = p.d_spheres;
@@ -814,7 +827,7 @@ static std::vector<uint64_t> launch_key(const TraceArgs& a, hipStream_t s) {
             (uint64_t)a.coop_lanes, (uint64_t)a.ext, (uint64_t)a.sky_enabled,
             (uint64_t)a.frame_count, P(a.accum), (uint64_t)a.walk, (uint64_t)a.block_waves, P(a.tile_order),
             (uint64_t)a.heavy_tiles, (uint64_t)(a.aux_stream != nullptr), (uint64_t)a.heavy_fused, P(a.heavy_px),
-            (uint64_t)a.n_heavy_px, P(a.tile_mask), (uint64_t)a.coop_walk};
+            (uint64_t)a.n_heavy_px, P(a.tile_mask), (uint64_t)a.coop_walk, (uint64_t)a.coop_win};
     for (int f = 0; f < a.n_frames; ++f) {
         const CamF& c = a.cams[f];
         for (float v : {c.ox, c.oy, c.oz, c.lx, c.ly, c.lz, c.hx, c.hy, c.hz, c.vx, c.vy, c.vz}) k.push_back(F(v));
@@ -1736,6 +1749,8 @@ int rt_set_option(rt_ctx* ctx, const char* name, int64_t value) {
         ctx->ext = (int)value;
     } else if (std::strcmp(name, "walk") == 0 && (value == 0 || value == 2)) {
         ctx->walk = (int)value;
+    } else if (std::strcmp(name, "coop_window") == 0 && (value == 0 || value == 32 || value == 64)) {
+        ctx->coop_window = (int)value;
     } else if (std::strcmp(name, "coop_walk") == 0 && (value == 0 || value == 1)) {
         ctx->coop_walk = (int)value;
     } else if (std::strcmp(name, "block_waves") == 0 && (value == 1 || value == 4)) {
@@ -1794,6 +1809,9 @@ int rt_get_option(rt_ctx* ctx, const char* name, int64_t* value) {
     else if (std::strcmp(name, "coop_lanes") == 0) *value = ctx->coop_lanes;
     else if (std::strcmp(name, "walk") == 0) *value = ctx->walk;
     else if (std::strcmp(name, "coop_walk") == 0) *value = ctx->coop_walk;
+    else if (std::strcmp(name, "coop_window") == 0) *value = ctx->coop_window;
+    else if (std::strcmp(name, "coop_window_used") == 0)
+        *value = ctx->dev.empty() ? 0 : coop_window_of(ctx, ctx->dev[0]);
     else if (std::strcmp(name, "block_waves") == 0) *value = ctx->block_waves;
     else if (std::strcmp(name, "heavy_first") == 0) *value = ctx->heavy_first;
     else if (std::strcmp(name, "heavy_tiles") == 0) *value = ctx->heavy_tiles;

@@ -356,13 +356,10 @@ __device__ __forceinline__ float lane_f(float v, int k) {
 #ifndef RT_COOP_DPP
 #define RT_COOP_DPP 1      // a leaf's triangle from the next lane by DPP (0: loaded by the lane, A/B builds)
 #endif
-#ifndef RT_COOP_WIN
-#define RT_COOP_WIN 64     // slots per window (lanes that load; 16 / 32: A/B builds)
-#endif
 //
 // The whole wave walks ONE ray (arguments wave-uniform), replaying the
 // reference's visit sequence exactly:
-//   1. lane k loads slot n+k of the window [n, n+64) of the walk records
+//   1. lane k < WIN loads slot n+k of the window [n, n+WIN) of the walk records
 //      (DevScene::walk): 2 coalesced 16-B loads per lane.  A leaf's triangle is
 //      the slot after its box, which lane k+1 loaded: it comes across by DPP
 //      (wave_shl:1), so a window costs 2 loads, not 4 (bit 30 of the link word
@@ -379,7 +376,11 @@ __device__ __forceinline__ float lane_f(float v, int k) {
 //      so a leaf not pre-tested at the old closest_t cannot hit at the new one).
 // The float operations are node_step's, so closest_t, the hit and the visit /
 // triangle-test counts equal the per-lane walk's.
-template <bool COUNT>
+// WIN = 64 slots, or 32 (option coop_window; kFeatWin32): a window serves 4.2
+// visits on average in config 5's tails (median 2) and uses 2.5 of its ~17
+// lines (tools/layout_model.py); half a window costs ~22% more windows there and
+// fetches ~35% fewer lines.
+template <bool COUNT, int WIN = 64>
 __device__ __forceinline__ int coop_walk(const float4* __restrict__ walk, int end, int n, V3 o, V3 d, V3 inv,
                                          float& closest, int& hit, unsigned long long& c_node,
                                          unsigned long long& c_tri) {
@@ -388,7 +389,7 @@ __device__ __forceinline__ int coop_walk(const float4* __restrict__ walk, int en
     while (n < end) {
         ++windows;
         const int j = n + lane;
-        const bool ld = j < end && lane < RT_COOP_WIN;
+        const bool ld = j < end && lane < WIN;
         float te = 0.0f, tt = 0.0f;
         int sk = 0, tri = -1;
         bool ind = false, tv = false, lf = false, pd = false;
@@ -416,7 +417,7 @@ __device__ __forceinline__ int coop_walk(const float4* __restrict__ walk, int en
             sk = lf ? j + 2 + (int)((aw >> 29) & 1u) : (int)(aw & 0x7FFFFFFFu);
             tri = (int)(aw & 0x1FFFFFFFu);
             pd = lf ? ((aw >> 29) & 1u) != 0u : ((__float_as_uint(B.w) >> 2) & 1u) != 0u;
-            if (lf && ind && te < closest && (!RT_COOP_DPP || lane < RT_COOP_WIN - 1))
+            if (lf && ind && te < closest && (!RT_COOP_DPP || lane < WIN - 1))
                 tv = tri_test(make_float4(B.w, Q0.x, Q0.y, 0.f), make_float4(Q0.z, Q0.w, Q1.x, 0.f),
                               make_float4(Q1.y, Q1.z, Q1.w, 0.f), o, d, tt);
         }
@@ -424,9 +425,9 @@ __device__ __forceinline__ int coop_walk(const float4* __restrict__ walk, int en
         uint64_t T = __ballot(tv && tt < closest);
         const uint64_t Lf = __ballot(lf);
         const uint64_t Pd = __ballot(pd);                           // a pad slot follows (leaf alignment)
-        int lim = min(RT_COOP_WIN, end - n);
-        if (RT_COOP_DPP && lim == RT_COOP_WIN && ((Lf >> (RT_COOP_WIN - 1)) & 1ull))
-            lim = RT_COOP_WIN - 1;                                   // its triangle is past the window
+        int lim = min(WIN, end - n);
+        if (RT_COOP_DPP && lim == WIN && ((Lf >> (WIN - 1)) & 1ull))
+            lim = WIN - 1;                                   // its triangle is past the window
         int k = 0;
         while (k < lim) {
             if ((H >> k) & 1ull) {
@@ -649,6 +650,7 @@ constexpr int kFeatExt = kFeatExtBit;   // non-reference extensions (option "ext
 constexpr int kFeatFrontier = 32; // cooperative tail uses frontier_walk (option coop_walk = 1)
 
 constexpr int kFeatFused = 64;    // heavy tiles in the same launch: workgroups k < 64 * split_n run heavy_pixel
+constexpr int kFeatWin32 = 128;   // cooperative windows of 32 slots (option coop_window), else 64
 constexpr unsigned kHeavyLaneMark = kLearnHeavyMark;   // rt_internal.h
 
 // One pixel of a heavy tile, the whole wave on it (option heavy_fused, the
@@ -935,7 +937,8 @@ void trace_simple(TraceArgs a) {
                     // the windows walk slots of the walk-2 records (walk 0 hands over a
                     // node index: its slot first)
                     const int ws = WALK == 2 ? lane_i(start, L) : a.scene.node_slot[lane_i(start, L)];
-                    nw = coop_walk<COUNT>(a.scene.walk, a.scene.end2, ws, bo, bd, bi, bc, bh, cn, ct);
+                    nw = coop_walk<COUNT, (FEAT & kFeatWin32) ? 32 : 64>(a.scene.walk, a.scene.end2, ws, bo, bd,
+                                                                             bi, bc, bh, cn, ct);
                 }
                 if (DIAG) {
                     d_windows += nw;
@@ -1034,6 +1037,8 @@ hipError_t launch_trace(const TraceArgs& a, hipStream_t stream, int* kernels) {
     const dim3 block(64 * bw);
     const int feat = (a.coop_lanes > 0 ? kFeatCoopTail : 0) | (a.ext != 0 ? kFeatExt : 0) |
                      (a.coop_lanes > 0 && a.coop_walk ? kFeatFrontier : 0);
+    // the production kernels (walk 2, coop tail, no extensions) come in both window sizes
+    const bool win32 = a.coop_win == 32 && a.walk == 2 && (feat & ~kFeatFrontier) == kFeatCoopTail;
     TraceArgs ao = a;
     ao.tiles_y = tiles_y;
     bool join = false;
@@ -1048,8 +1053,13 @@ hipError_t launch_trace(const TraceArgs& a, hipStream_t stream, int* kernels) {
             ao.split_n = 0;
             const dim3 gf(a.n_heavy_px + n_tiles);
             const size_t shm = kFCap * sizeof(uint4);
-            constexpr int FF = kFeatCoopTail | kFeatFused;
-            RT_FUSED(gf)
+            if (win32) {
+                constexpr int FF = kFeatCoopTail | kFeatFused | kFeatWin32;
+                RT_FUSED(gf)
+            } else {
+                constexpr int FF = kFeatCoopTail | kFeatFused;
+                RT_FUSED(gf)
+            }
             return hipGetLastError();
         }
         if (H > 0 && a.heavy_fused && bw == 1 && (feat & ~kFeatFrontier) == kFeatCoopTail) {
@@ -1059,8 +1069,13 @@ hipError_t launch_trace(const TraceArgs& a, hipStream_t stream, int* kernels) {
             ao.split_n = H;
             const dim3 gf(64 * H + (n_tiles - H));
             const size_t shm = kFCap * sizeof(uint4);
-            constexpr int FF = kFeatCoopTail | kFeatFused;
-            RT_FUSED(gf)
+            if (win32) {
+                constexpr int FF = kFeatCoopTail | kFeatFused | kFeatWin32;
+                RT_FUSED(gf)
+            } else {
+                constexpr int FF = kFeatCoopTail | kFeatFused;
+                RT_FUSED(gf)
+            }
             return hipGetLastError();
         }
         if (H > 0 && a.ev_fork && bw == 1 && (feat & ~kFeatFrontier) == kFeatCoopTail) {
@@ -1102,7 +1117,13 @@ hipError_t launch_trace(const TraceArgs& a, hipStream_t stream, int* kernels) {
     else hipLaunchKernelGGL((trace_simple<false, false, F, W>), grid, block, ((F) & kFeatFrontier) ? shm_f : 0, stream, ao);
     if (a.walk == 2) {
         switch (feat) {
-            case kFeatCoopTail: RT_SIMPLE(kFeatCoopTail, 2) break;
+            case kFeatCoopTail:
+                if (win32) {
+                    RT_SIMPLE(kFeatCoopTail | kFeatWin32, 2)
+                } else {
+                    RT_SIMPLE(kFeatCoopTail, 2)
+                }
+                break;
             case 0: RT_SIMPLE(0, 2) break;
             default: RT_SIMPLE(kFeatCoopTail | kFeatExt | kFeatFrontier, 2) break;
         }

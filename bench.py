@@ -946,7 +946,8 @@ def main() -> None:
                                                                       "heavy_first", "heavy_tiles", "heavy_factor",
                                                                       "heavy_stream", "heavy_pixels",
                                                                       "heavy_pixel_factor", "heavy_cap", "graph",
-                                                                      "reuse_order", "order_split", "hw_queues")},
+                                                                      "reuse_order", "order_split", "hw_queues",
+                                                                      "coop_window", "coop_window_used")},
                              "concurrent_launches": renderer.get_option("concurrent_launches"),
                              "heavy_tiles_used": heavy_used,
                              "heavy_pixels_used": heavy_px_used},

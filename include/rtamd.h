@@ -243,6 +243,11 @@ int rt_render_poll(rt_ctx* ctx, uint64_t ticket, int* done);
  *   "coop_walk"     cooperative walks (the coop tail): 0 = 64-node preorder
  *                   windows (default), 1 = preorder frontier (up to 64 live
  *                   subtrees expanded per round trip)
+ *   "coop_window"   the windows' size: 64 or 32 slots; 0 (default) = 32 when
+ *                   the scene's walk records exceed 32 MB (the L2s of the 8
+ *                   XCDs), else 64
+ *   "coop_window_used" (rt_get_option only) the window size the current scene
+ *                   gets on device 0
  *   "block_waves"   waves per workgroup, 1 (default: a finished wave frees its
  *                   slot at once) or 4
  *   "heavy_first"   with block_waves 1: 1 (default) = the first

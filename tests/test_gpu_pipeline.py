@@ -269,3 +269,34 @@ def test_leaf_align_bit_exact(renderer, cfg_k):
         renderer.set_option("leaf_align", 0)
         renderer.set_option("coop_lanes", 1)
         renderer.upload_scene(built)
+
+
+@pytest.mark.parametrize("win", [32, 64])
+@pytest.mark.parametrize("cfg_k", [3, 6])
+def test_coop_window_bit_exact(renderer, cfg_k, win):
+    """Option coop_window (the cooperative tail's window: 32 or 64 slots):
+    frames and counters equal the oracle's, in the learned order with heavy
+    pixels and with every walk cooperative (coop_lanes 64)."""
+    from rtamd import configs
+    cfg = configs.get(cfg_k)
+    built = cfg.build()
+    W, H, B = cfg.width, cfg.height, cfg.max_bounces
+    cam = cfg.camera()
+    ref = _oracle(built, cam.ubo_bytes(), W, H, B, row_step=11)
+    try:
+        renderer.upload_scene(built)
+        assert renderer.get_option("coop_window_used") == 64    # L2-sized scenes: 64-slot windows
+        renderer.set_option("coop_window", win)
+        assert renderer.get_option("coop_window") == win
+        for coop in (1, 64):
+            renderer.set_option("coop_lanes", coop)
+            for launch in range(3):
+                rgba, rad, st = renderer.render(cam, W, H, B, radiance=True, stats=launch == 2)
+                assert np.array_equal(rgba[::11], ref[0]), (coop, launch)
+                assert np.array_equal(rad[::11].view(np.uint32), ref[1].view(np.uint32)), (coop, launch)
+        full = _oracle(built, cam.ubo_bytes(), W, H, B, radiance=False)[2]
+        for k in ("segments", "node_visits", "tri_tests", "mat_reads"):
+            assert st[k] == full[k], k
+    finally:
+        renderer.set_option("coop_window", 0)
+        renderer.set_option("coop_lanes", 1)
