@@ -28,9 +28,6 @@
 #   ab3 / ab5 bench.py interleaved against the tree in build_ab/old (tools/ab_old_new.sh),
 #             config 3 (3 rounds, 200 steps) / config 5 (2 rounds, 10 steps)
 #   abargs    tools/ab_args.sh over the arms in $ARMS_FILE ($REPS rounds, $STEPS steps)
-#   abcoop    the default build against lib/variants/librtamd_coop4.so (coop windows loading 4 x 16 B)
-#   abwin     the default build against the coop-window variants win32 / win16 (configs 3 and 5)
-#   pmc5w     pmc5 on the win16 and win32 builds
 #   cmd       the command in $CMD (600 s)
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -105,20 +102,10 @@ for s in "$@"; do
     ab5)      run ab5 900 bash tools/ab_old_new.sh "$OUT/ab5" 2 --config 5 --steps 10 --warmup 3 ;;
     abargs)   run abargs 900 env ARMS_FILE="${ARMS_FILE:?}" REPS="${REPS:-3}" STEPS="${STEPS:-200}" \
                   bash tools/ab_args.sh "$TAG/abargs_$(basename "$ARMS_FILE" .txt)" ;;
-    abcoop)   run abcoop 900 env REPS=3 bash tools/ab_lib.sh "$OUT/abcoop" "--steps 200 --warmup 5" \
-                  3d-ray-tracer-vulkan_amd/lib/librtamd.so 3d-ray-tracer-vulkan_amd/lib/variants/librtamd_coop4.so ;;
     abalign)  run abalign 900 env REPS=2 bash tools/ab_lib.sh "$OUT/abalign5" "--config 5 --steps 10 --warmup 3" \
                   3d-ray-tracer-vulkan_amd/lib/librtamd.so 3d-ray-tracer-vulkan_amd/lib/variants/librtamd_align.so && \
               run abalign3 900 env REPS=3 bash tools/ab_lib.sh "$OUT/abalign3" "--steps 200 --warmup 5" \
                   3d-ray-tracer-vulkan_amd/lib/librtamd.so 3d-ray-tracer-vulkan_amd/lib/variants/librtamd_align.so ;;
-    abwin)    run abwin3 900 env REPS=3 bash tools/ab_lib.sh "$OUT/abwin3" "--steps 200 --warmup 5" \
-                  3d-ray-tracer-vulkan_amd/lib/librtamd.so 3d-ray-tracer-vulkan_amd/lib/variants/librtamd_win32.so \
-                  3d-ray-tracer-vulkan_amd/lib/variants/librtamd_win16.so && \
-              run abwin5 900 env REPS=2 bash tools/ab_lib.sh "$OUT/abwin5" "--config 5 --steps 10 --warmup 3" \
-                  3d-ray-tracer-vulkan_amd/lib/librtamd.so 3d-ray-tracer-vulkan_amd/lib/variants/librtamd_win32.so \
-                  3d-ray-tracer-vulkan_amd/lib/variants/librtamd_win16.so ;;
-    pmc5w)    RTAMD_LIB_PATH=3d-ray-tracer-vulkan_amd/lib/variants/librtamd_win16.so pmc 5 cfg5_1M_3840x2160_b8@win16 w16 && \
-              RTAMD_LIB_PATH=3d-ray-tracer-vulkan_amd/lib/variants/librtamd_win32.so pmc 5 cfg5_1M_3840x2160_b8@win32 w32 ;;
     cmd)      run cmd 600 bash -c "$CMD" > "$OUT/cmd.log" 2>&1 ;;
     *)        status "unknown step $s" ;;
   esac
