@@ -213,8 +213,11 @@ int build_host_scene(const void* vertices, size_t vertex_bytes,
 using namespace rtamd;
 
 static constexpr int kMaxSlots = 8;   // rt_render_async frame slots per device
+// Walk records with no leaf straddling a 128-B line (option leaf_align):
+// config 5 8.24 vs 8.39-8.46 ms and 21.3 vs 22.4 GB fetched per frame, config 3
+// 0.319-0.321 vs 0.322-0.323 ms (profiles/r04/r4g), for 11% more slots.
 #ifndef RT_LEAF_ALIGN
-#define RT_LEAF_ALIGN 0
+#define RT_LEAF_ALIGN 1
 #endif
 
 struct PerDevice {
@@ -777,6 +780,11 @@ static int set_schedule(const rt_ctx* ctx, PerDevice& p, TraceArgs& a, const rt_
             p.accum_n = 0;
             RT_HIP_CHECK(hipMalloc(&p.d_accum, need * sizeof(float)));
             RT_HIP_CHECK(hipMemset(p.d_accum, 0, need * sizeof(float)));
+            // hipMemset runs on the null stream, which the non-blocking launch
+            // streams do not wait for: without this the zeroing could land on
+            // sums frame 0 has already written (frames 1+ then differ, seen on a
+            // second device of one context: tools/dbg/accum3.py, profiles/r04/r4g)
+            RT_HIP_CHECK(hipDeviceSynchronize());
             p.accum_n = need;
         }
         a.accum = p.d_accum;
@@ -1140,6 +1148,9 @@ int rt_upload_scene(rt_ctx* ctx, const void* vertices, size_t vertex_bytes,
         if (e == hipSuccess && hs.n_tris)
             e = hipMemcpy2D(s.mats, kShadeStride * sizeof(float4), hs.mats, sizeof(float4), sizeof(float4),
                             (size_t)hs.n_tris, hipMemcpyHostToDevice);
+        // the padding memsets ran on the null stream: complete before any
+        // launch stream (non-blocking) reads the scene
+        if (e == hipSuccess) e = hipDeviceSynchronize();
         p.scene = s;
         if (e != hipSuccess) {
             set_error("rt_upload_scene: device %d: %s", p.device, hipGetErrorString(e));

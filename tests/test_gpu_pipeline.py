@@ -241,12 +241,14 @@ def test_device_learning_matches_host_learning(renderer, cfg_k):
     assert used[1] > 0 and used[1] == used[0], used
 
 
+@pytest.mark.parametrize("align", [0, 1])
 @pytest.mark.parametrize("cfg_k", [3, 6, 2])
-def test_leaf_align_bit_exact(renderer, cfg_k):
-    """Option leaf_align (walk records with a pad slot before any leaf that
-    would straddle a 128-B line; the predecessor's pad bit steps over it):
-    frames and counters equal the oracle's, in the lockstep walk, the
-    cooperative windows (coop_lanes 64: every walk) and the learned order."""
+def test_leaf_align_bit_exact(renderer, cfg_k, align):
+    """Option leaf_align both ways (1, the default: walk records with a pad
+    slot before any leaf that would straddle a 128-B line, the predecessor's
+    pad bit stepping over it; 0: packed): frames and counters equal the
+    oracle's, in the lockstep walk, the cooperative windows (coop_lanes 64:
+    every walk) and the learned order."""
     from rtamd import configs
     cfg = configs.get(cfg_k)
     built = cfg.build()
@@ -254,7 +256,7 @@ def test_leaf_align_bit_exact(renderer, cfg_k):
     cam = cfg.camera()
     ref = _oracle(built, cam.ubo_bytes(), W, H, B, row_step=7)
     try:
-        renderer.set_option("leaf_align", 1)
+        renderer.set_option("leaf_align", align)
         renderer.upload_scene(built)
         for coop in (1, 64):
             renderer.set_option("coop_lanes", coop)
@@ -266,7 +268,7 @@ def test_leaf_align_bit_exact(renderer, cfg_k):
         for k in ("segments", "node_visits", "tri_tests", "mat_reads"):
             assert st[k] == full[k], k
     finally:
-        renderer.set_option("leaf_align", 0)
+        renderer.set_option("leaf_align", 1)
         renderer.set_option("coop_lanes", 1)
         renderer.upload_scene(built)
 

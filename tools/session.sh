@@ -14,7 +14,6 @@
 #   pmc3      PMC passes A (SQ instruction counts) and C (FETCH_SIZE) of
 #             config 3, merged into gpurun_out/TAG/pmc_latest.json
 #   pmc5      the same for config 5
-#   pmc5a     pmc5 on lib/variants/librtamd_align.so (leaf_align 1), record key ...@align
 #   fetch5    pmc5 with coop_lanes 0 (no cooperative tail) and with order_split 40
 #   pmc3o     the same for config 3 with the orbiting camera (record key cfg3_...@orbit)
 #   orbit     bench.py --camera-path orbit at 20 steps
@@ -80,7 +79,6 @@ for s in "$@"; do
     prof5)    prof 5 10 ;;
     pmc3)     pmc 3 cfg3_50k_1920x1080_b4 ;;
     pmc5)     pmc 5 cfg5_1M_3840x2160_b8 ;;
-    pmc5a)    RTAMD_LIB_PATH=3d-ray-tracer-vulkan_amd/lib/variants/librtamd_align.so pmc 5 cfg5_1M_3840x2160_b8@align a ;;
     fetch5)   pmc 5 cfg5_1M_3840x2160_b8@nocoop n "--set coop_lanes=0" && \
               pmc 5 cfg5_1M_3840x2160_b8@split40 s "--set order_split=40" ;;
     pmc3o)    pmc 3 cfg3_50k_1920x1080_b4@orbit o "--camera-path orbit" ;;
@@ -102,10 +100,6 @@ for s in "$@"; do
     ab5)      run ab5 900 bash tools/ab_old_new.sh "$OUT/ab5" 2 --config 5 --steps 10 --warmup 3 ;;
     abargs)   run abargs 900 env ARMS_FILE="${ARMS_FILE:?}" REPS="${REPS:-3}" STEPS="${STEPS:-200}" \
                   bash tools/ab_args.sh "$TAG/abargs_$(basename "$ARMS_FILE" .txt)" ;;
-    abalign)  run abalign 900 env REPS=2 bash tools/ab_lib.sh "$OUT/abalign5" "--config 5 --steps 10 --warmup 3" \
-                  3d-ray-tracer-vulkan_amd/lib/librtamd.so 3d-ray-tracer-vulkan_amd/lib/variants/librtamd_align.so && \
-              run abalign3 900 env REPS=3 bash tools/ab_lib.sh "$OUT/abalign3" "--steps 200 --warmup 5" \
-                  3d-ray-tracer-vulkan_amd/lib/librtamd.so 3d-ray-tracer-vulkan_amd/lib/variants/librtamd_align.so ;;
     cmd)      run cmd 600 bash -c "$CMD" > "$OUT/cmd.log" 2>&1 ;;
     *)        status "unknown step $s" ;;
   esac
