@@ -21,7 +21,10 @@ import pytest
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 EVID = os.path.join(ROOT, "profiles", "r03", "evidence_r3fin2")
 R04 = os.path.join(ROOT, "profiles", "r04")
-R04_LINES = [("r4b", "bench.json"), ("r4b", "bench_orbit.json"), ("r4b", "prof3.json")]
+R04_LINES = [("r4b", "bench.json"), ("r4b", "bench_orbit.json"), ("r4b", "prof3.json"),
+             # the final layout (aligned leaf records, 32-slot windows for config 5), PMC of r4h
+             ("r4i", "bench.json"), ("r4i", "bench_orbit.json"), ("r4i", "prof3.json"), ("r4i", "prof5.json"),
+             ("r4h", "bench_cfg5.json")]
 sys.path.insert(0, ROOT)
 
 import bench  # noqa: E402  (module level: argparse-free helpers, no torch)
@@ -146,13 +149,26 @@ def test_r04_roofline_reproduces(session, name):
     assert c["frames_verified"] is True
 
 
-def test_r04_rocprof_union():
-    u = json.load(open(os.path.join(R04, "r4b", "union_cfg3.json")))
-    p = _r04("r4b", "prof3.json")
+@pytest.mark.parametrize("session,cfg", [("r4b", 3), ("r4i", 3), ("r4i", 5)])
+def test_r04_rocprof_union(session, cfg):
+    u = json.load(open(os.path.join(R04, session, f"union_cfg{cfg}.json")))
+    p = _r04(session, f"prof{cfg}.json")
     assert u["launches"] == u["frames"] == p["steps"]
     assert u["union_ms_per_frame"] == pytest.approx(p["ms_per_step"], rel=0.05)
-    with open(os.path.join(R04, "r4b", "kernel_stats_cfg3.csv")) as fh:
+    with open(os.path.join(R04, session, f"kernel_stats_cfg{cfg}.csv")) as fh:
         rows = [r for r in csv.DictReader(fh) if "trace_simple<false, false" in r["Name"]]
     # rocprofv3's mean launch duration agrees with bench.py's kernel_ms (HIP events on the launch streams)
     assert float(rows[0]["AverageNs"]) / 1e6 == pytest.approx(p["roofline"]["kernel_ms"], rel=0.05)
     assert u["launch_ms_mean"] == pytest.approx(p["roofline"]["kernel_ms"], rel=0.05)
+
+
+@pytest.mark.parametrize("session", ["r4i"])
+def test_r04_camera_stop_learning_frame(session):
+    """The frames after the camera stops (the first: its learning launch, the
+    order then learned on the device; the second: the launch behind those
+    learning kernels) cost at most 2x the steady lone frame (round 3's host
+    learning: 4.4 ms against ~0.65; r4b, an earlier build of this round:
+    4.16 ms for the second)."""
+    cs = _r04(session, "bench_orbit.json")["camera_stop"]["ms_per_frame"]
+    steady = sorted(cs[2:])[len(cs[2:]) // 2]
+    assert cs[0] <= 2.0 * steady and max(cs) <= 2.0 * steady, cs
