@@ -100,6 +100,8 @@ for s in "$@"; do
     ab5)      run ab5 900 bash tools/ab_old_new.sh "$OUT/ab5" 2 --config 5 --steps 10 --warmup 3 ;;
     abargs)   run abargs 900 env ARMS_FILE="${ARMS_FILE:?}" REPS="${REPS:-3}" STEPS="${STEPS:-200}" \
                   bash tools/ab_args.sh "$TAG/abargs_$(basename "$ARMS_FILE" .txt)" ;;
+    bisect)   run bisect 900 bash tools/ab_trees.sh "$OUT/bisect" 2 "--steps 200 --warmup 5" \
+                  build_ab/old build_ab/793740e build_ab/b88e2c4 build_ab/5b41a91 . ;;
     cmd)      run cmd 600 bash -c "$CMD" > "$OUT/cmd.log" 2>&1 ;;
     *)        status "unknown step $s" ;;
   esac
