@@ -196,3 +196,15 @@ def test_jni_shim_matches_java_and_header():
     calls = set(re.findall(r"\b(rt_\w+)\(", c_src))
     declared = set(re.findall(r"\b(rt_\w+)\(", hdr))
     assert calls <= declared, calls - declared
+
+
+def test_every_option_is_documented():
+    """Every option name rt_set_option / rt_get_option accepts
+    (csrc/rt_runtime.hip) is documented in include/rtamd.h."""
+    import re
+    src = open(os.path.join(ROOT, "3d-ray-tracer-vulkan_amd", "csrc", "rt_runtime.hip")).read()
+    hdr = open(os.path.join(ROOT, "include", "rtamd.h")).read()
+    names = set(re.findall(r'std::strcmp\(name, "([a-z0-9_]+)"\)', src))
+    assert len(names) > 20
+    missing = sorted(n for n in names if f'"{n}"' not in hdr)
+    assert not missing, missing
