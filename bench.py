@@ -415,12 +415,13 @@ def main() -> None:
     W, H, B = cfg.width, cfg.height, cfg.max_bounces
 
     renderer = rtamd.Renderer((dev_index,))
-    renderer.upload_scene(built)
     if dist_on:
         renderer.set_option("order_split", ORDER_SPLIT_N_GT_1)
+    # --set before the upload: some options shape the uploaded records (leaf_align)
     for kv in filter(None, args.set.split(",")):
         k, v = kv.split("=")
         renderer.set_option(k.strip(), int(v))
+    renderer.upload_scene(built)
     L = rtamd.lib()
     ctx = renderer._ctx
     # The PCIe-inclusive rate first, before this process creates its own
