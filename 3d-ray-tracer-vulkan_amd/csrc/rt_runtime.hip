@@ -219,6 +219,9 @@ static constexpr int kMaxSlots = 8;   // rt_render_async frame slots per device
 #ifndef RT_LEAF_ALIGN
 #define RT_LEAF_ALIGN 1
 #endif
+#ifndef RT_WALK_PAD
+#define RT_WALK_PAD 1     // (rt_trace.hip) 0: an A/B build whose walk ignores pad bits: records stay packed
+#endif
 
 struct PerDevice {
     int          device = 0;
@@ -1051,7 +1054,7 @@ int rt_upload_scene(rt_ctx* ctx, const void* vertices, size_t vertex_bytes,
     for (size_t i = 0; i < n2; ++i) {
         uint32_t fl;
         std::memcpy(&fl, &hs.nodes[2 * i + 1].w, 4);
-        if (ctx->leaf_align && (fl & 2u) && nslot % 4 == 3) {
+        if (RT_WALK_PAD && ctx->leaf_align && (fl & 2u) && nslot % 4 == 3) {
             padded[i] = 1;
             ++nslot;
         }

@@ -353,6 +353,9 @@ __device__ __forceinline__ float lane_f(float v, int k) {
 }
 
 // ------------------------------------------------------------ cooperative walk --
+#ifndef RT_WALK_PAD
+#define RT_WALK_PAD 1      // the lockstep walk reads pad bits (leaf_align); 0: packed records only (A/B builds)
+#endif
 #ifndef RT_COOP_DPP
 #define RT_COOP_DPP 1      // a leaf's triangle from the next lane by DPP (0: loaded by the lane, A/B builds)
 #endif
@@ -885,8 +888,12 @@ void trace_simple(TraceArgs a) {
                     // (selects by masks: written as ternaries, the compiler branched
                     // here, on the dependent chain to the next load: +7% per frame,
                     // profiles/r04/r4j)
+#if RT_WALK_PAD
                     const int n_leaf = n + 2 + (int)((aw >> 29) & 1u);
                     const int n_hit = n + 1 + (int)((bw >> 2) & 1u);
+#else
+                    const int n_leaf = n + 2, n_hit = n + 1;                 // (A/B build: packed records only)
+#endif
                     const int m_hit = -(int)hb, m_leaf = -(int)nleaf;
                     const int n_int = (n_hit & m_hit) | ((int)(aw & kIdx) & ~m_hit);
                     const int nxt = (n_leaf & m_leaf) | (n_int & ~m_leaf);
