@@ -416,10 +416,17 @@ __device__ __forceinline__ int coop_walk(const float4* __restrict__ walk, int en
             slab(A, B, o, inv, te, ind);
             const uint32_t aw = __float_as_uint(A.w);
             lf = ((aw >> 30) & 1u) != 0u;
-            // a leaf's skip is its successor, two slots on (three past a pad slot)
-            sk = lf ? j + 2 + (int)((aw >> 29) & 1u) : (int)(aw & 0x7FFFFFFFu);
+            // a leaf's skip is its successor, two slots on (three past a pad
+            // slot); selects by masks, not ternaries (which became branches)
+            const int m_lf = -(int)lf;
+#if RT_WALK_PAD
+            const int pl = (int)((aw >> 29) & 1u), pi = (int)((__float_as_uint(B.w) >> 2) & 1u);
+            pd = ((pl & m_lf) | (pi & ~m_lf)) != 0;
+#else
+            const int pl = 0;
+#endif
+            sk = ((j + 2 + pl) & m_lf) | ((int)(aw & 0x7FFFFFFFu) & ~m_lf);
             tri = (int)(aw & 0x1FFFFFFFu);
-            pd = lf ? ((aw >> 29) & 1u) != 0u : ((__float_as_uint(B.w) >> 2) & 1u) != 0u;
             if (lf && ind && te < closest && (!RT_COOP_DPP || lane < WIN - 1))
                 tv = tri_test(make_float4(B.w, Q0.x, Q0.y, 0.f), make_float4(Q0.z, Q0.w, Q1.x, 0.f),
                               make_float4(Q1.y, Q1.z, Q1.w, 0.f), o, d, tt);
@@ -427,7 +434,7 @@ __device__ __forceinline__ int coop_walk(const float4* __restrict__ walk, int en
         uint64_t H = __ballot(ind && te < closest);
         uint64_t T = __ballot(tv && tt < closest);
         const uint64_t Lf = __ballot(lf);
-        const uint64_t Pd = __ballot(pd);                           // a pad slot follows (leaf alignment)
+        const uint64_t Pd = RT_WALK_PAD ? __ballot(pd) : 0ull;      // a pad slot follows (leaf alignment)
         int lim = min(WIN, end - n);
         if (RT_COOP_DPP && lim == WIN && ((Lf >> (WIN - 1)) & 1ull))
             lim = WIN - 1;                                   // its triangle is past the window
@@ -444,7 +451,7 @@ __device__ __forceinline__ int coop_walk(const float4* __restrict__ walk, int en
                         T = __ballot(tv && tt < closest);
                     }
                 }
-                k += (((Lf >> k) & 1ull) ? 2 : 1) + (int)((Pd >> k) & 1ull);
+                k += 1 + (int)((Lf >> k) & 1ull) + (RT_WALK_PAD ? (int)((Pd >> k) & 1ull) : 0);
             } else {
                 k = lane_i(sk, k) - n;
             }
