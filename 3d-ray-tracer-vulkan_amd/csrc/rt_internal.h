@@ -69,6 +69,7 @@ struct DevScene {
     int*     slot_node = nullptr;
     int*     node_slot = nullptr;   // slot(i) of node i (walk 0 hands its node index to the windows tail)
     int      end2    = 0;
+    int      padded  = 0;   // 1: the walk records hold pad slots (leaf_align)
     // norms and mats interleave in one allocation (kShadeStride float4 per
     // triangle: normal, then albedo/type), so shading a hit touches one 32-B
     // record; norms points at the allocation, mats one float4 in

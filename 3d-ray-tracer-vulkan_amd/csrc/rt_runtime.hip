@@ -213,14 +213,14 @@ int build_host_scene(const void* vertices, size_t vertex_bytes,
 using namespace rtamd;
 
 static constexpr int kMaxSlots = 8;   // rt_render_async frame slots per device
-// Walk records with no leaf straddling a 128-B line (option leaf_align):
-// config 5 8.24 vs 8.39-8.46 ms and 21.3 vs 22.4 GB fetched per frame, config 3
-// 0.319-0.321 vs 0.322-0.323 ms (profiles/r04/r4g), for 11% more slots.
+// Walk records with no leaf straddling a 128-B line (option leaf_align; 2 =
+// auto: aligned when the packed records exceed kWin32Bytes, like the window
+// size): config 5 8.24 vs 8.39-8.46 ms and 21.3 vs 22.4 GB fetched per frame
+// (profiles/r04/r4g), for 11% more slots.  A scene whose records stay in L2
+// gains nothing from it, and its kernels then skip the pad-bit arithmetic
+// (kFeatPad off: config 3 0.303-0.304 vs 0.306-0.307 ms, profiles/r04/r4m).
 #ifndef RT_LEAF_ALIGN
-#define RT_LEAF_ALIGN 1
-#endif
-#ifndef RT_WALK_PAD
-#define RT_WALK_PAD 1     // (rt_trace.hip) 0: an A/B build whose walk ignores pad bits: records stay packed
+#define RT_LEAF_ALIGN 2
 #endif
 
 struct PerDevice {
@@ -1050,13 +1050,21 @@ int rt_upload_scene(rt_ctx* ctx, const void* vertices, size_t vertex_bytes,
     const size_t n2 = (size_t)hs.n_nodes;
     std::vector<int> slot(n2 + 1);
     std::vector<uint8_t> padded(n2 + 1, 0);       // a pad slot precedes node i
-    size_t nslot = 0;
+    size_t n_leaves = 0;
     for (size_t i = 0; i < n2; ++i) {
         uint32_t fl;
         std::memcpy(&fl, &hs.nodes[2 * i + 1].w, 4);
-        if (RT_WALK_PAD && ctx->leaf_align && (fl & 2u) && nslot % 4 == 3) {
+        n_leaves += (fl & 2u) ? 1 : 0;
+    }
+    const bool align = ctx->leaf_align == 1 || (ctx->leaf_align == 2 && (n2 + n_leaves) * 32 > kWin32Bytes);
+    size_t nslot = 0, n_pads = 0;
+    for (size_t i = 0; i < n2; ++i) {
+        uint32_t fl;
+        std::memcpy(&fl, &hs.nodes[2 * i + 1].w, 4);
+        if (align && (fl & 2u) && nslot % 4 == 3) {
             padded[i] = 1;
             ++nslot;
+            ++n_pads;
         }
         slot[i] = (int)nslot;
         nslot += (fl & 2u) ? 2 : 1;
@@ -1133,6 +1141,7 @@ int rt_upload_scene(rt_ctx* ctx, const void* vertices, size_t vertex_bytes,
         if (e == hipSuccess) e = hipMemset(s.nodes + 2 * nn, 0, 2 * sizeof(float4));
         if (e == hipSuccess) e = hipMemset(s.leafs + 3 * nn, 0, sizeof(float4));
         s.end2 = (int)nslot;
+        s.padded = n_pads > 0 ? 1 : 0;
         if (e == hipSuccess) e = hipMalloc(&s.walk, walk.size() * sizeof(float4));
         if (e == hipSuccess) e = hipMalloc(&s.slot_node, slot_node.size() * sizeof(int));
         if (e == hipSuccess) e = hipMalloc(&s.node_slot, slot.size() * sizeof(int));
@@ -1799,7 +1808,7 @@ int rt_set_option(rt_ctx* ctx, const char* name, int64_t value) {
         ctx->learn_alone = (int)value;
     } else if (std::strcmp(name, "learn_device") == 0 && (value == 0 || value == 1)) {
         ctx->learn_device = (int)value;
-    } else if (std::strcmp(name, "leaf_align") == 0 && (value == 0 || value == 1)) {
+    } else if (std::strcmp(name, "leaf_align") == 0 && value >= 0 && value <= 2) {
         ctx->leaf_align = (int)value;                   // takes effect at the next rt_upload_scene
     } else if (std::strcmp(name, "heavy_stream") == 0 && value >= 0 && value <= 2) {
         ctx->heavy_stream = (int)value;
@@ -1836,6 +1845,7 @@ int rt_get_option(rt_ctx* ctx, const char* name, int64_t* value) {
     else if (std::strcmp(name, "learn_alone") == 0) *value = ctx->learn_alone;
     else if (std::strcmp(name, "learn_device") == 0) *value = ctx->learn_device;
     else if (std::strcmp(name, "leaf_align") == 0) *value = ctx->leaf_align;
+    else if (std::strcmp(name, "leaf_align_used") == 0) *value = ctx->dev.empty() ? 0 : ctx->dev[0].scene.padded;
     else if (std::strcmp(name, "heavy_factor") == 0) *value = ctx->heavy_factor;
     else if (std::strcmp(name, "concurrent_launches") == 0) *value = ctx->concurrent_launches;
     else if (std::strcmp(name, "async_slots") == 0) *value = ctx->async_slots;

@@ -353,9 +353,6 @@ __device__ __forceinline__ float lane_f(float v, int k) {
 }
 
 // ------------------------------------------------------------ cooperative walk --
-#ifndef RT_WALK_PAD
-#define RT_WALK_PAD 1      // the lockstep walk reads pad bits (leaf_align); 0: packed records only (A/B builds)
-#endif
 #ifndef RT_COOP_DPP
 #define RT_COOP_DPP 1      // a leaf's triangle from the next lane by DPP (0: loaded by the lane, A/B builds)
 #endif
@@ -383,7 +380,8 @@ __device__ __forceinline__ float lane_f(float v, int k) {
 // visits on average in config 5's tails (median 2) and uses 2.5 of its ~17
 // lines (tools/layout_model.py); half a window costs ~22% more windows there and
 // fetches ~35% fewer lines.
-template <bool COUNT, int WIN = 64>
+// PAD: the records may hold pad slots (leaf_align; the kernel's kFeatPad).
+template <bool COUNT, int WIN = 64, bool PAD = true>
 __device__ __forceinline__ int coop_walk(const float4* __restrict__ walk, int end, int n, V3 o, V3 d, V3 inv,
                                          float& closest, int& hit, unsigned long long& c_node,
                                          unsigned long long& c_tri) {
@@ -416,16 +414,16 @@ __device__ __forceinline__ int coop_walk(const float4* __restrict__ walk, int en
             slab(A, B, o, inv, te, ind);
             const uint32_t aw = __float_as_uint(A.w);
             lf = ((aw >> 30) & 1u) != 0u;
-            // a leaf's skip is its successor, two slots on (three past a pad
-            // slot); selects by masks, not ternaries (which became branches)
-            const int m_lf = -(int)lf;
-#if RT_WALK_PAD
-            const int pl = (int)((aw >> 29) & 1u), pi = (int)((__float_as_uint(B.w) >> 2) & 1u);
-            pd = ((pl & m_lf) | (pi & ~m_lf)) != 0;
-#else
-            const int pl = 0;
-#endif
-            sk = ((j + 2 + pl) & m_lf) | ((int)(aw & 0x7FFFFFFFu) & ~m_lf);
+            // a leaf's skip is its successor, two slots on (three past a pad slot)
+            // (the code generated for these lines moves the frame time by
+            // several percent: written with masks the PAD form measured 2.7%
+            // slower on config 3, profiles/r04/r4n)
+            if (PAD) {
+                sk = lf ? j + 2 + (int)((aw >> 29) & 1u) : (int)(aw & 0x7FFFFFFFu);
+                pd = lf ? ((aw >> 29) & 1u) != 0u : ((__float_as_uint(B.w) >> 2) & 1u) != 0u;
+            } else {
+                sk = lf ? j + 2 : (int)(aw & 0x7FFFFFFFu);
+            }
             tri = (int)(aw & 0x1FFFFFFFu);
             if (lf && ind && te < closest && (!RT_COOP_DPP || lane < WIN - 1))
                 tv = tri_test(make_float4(B.w, Q0.x, Q0.y, 0.f), make_float4(Q0.z, Q0.w, Q1.x, 0.f),
@@ -434,7 +432,7 @@ __device__ __forceinline__ int coop_walk(const float4* __restrict__ walk, int en
         uint64_t H = __ballot(ind && te < closest);
         uint64_t T = __ballot(tv && tt < closest);
         const uint64_t Lf = __ballot(lf);
-        const uint64_t Pd = RT_WALK_PAD ? __ballot(pd) : 0ull;      // a pad slot follows (leaf alignment)
+        const uint64_t Pd = PAD ? __ballot(pd) : 0ull;              // a pad slot follows (leaf alignment)
         int lim = min(WIN, end - n);
         if (RT_COOP_DPP && lim == WIN && ((Lf >> (WIN - 1)) & 1ull))
             lim = WIN - 1;                                   // its triangle is past the window
@@ -451,7 +449,10 @@ __device__ __forceinline__ int coop_walk(const float4* __restrict__ walk, int en
                         T = __ballot(tv && tt < closest);
                     }
                 }
-                k += 1 + (int)((Lf >> k) & 1ull) + (RT_WALK_PAD ? (int)((Pd >> k) & 1ull) : 0);
+                if (PAD)
+                    k += (((Lf >> k) & 1ull) ? 2 : 1) + (int)((Pd >> k) & 1ull);
+                else
+                    k += ((Lf >> k) & 1ull) ? 2 : 1;
             } else {
                 k = lane_i(sk, k) - n;
             }
@@ -661,6 +662,8 @@ constexpr int kFeatFrontier = 32; // cooperative tail uses frontier_walk (option
 
 constexpr int kFeatFused = 64;    // heavy tiles in the same launch: workgroups k < 64 * split_n run heavy_pixel
 constexpr int kFeatWin32 = 128;   // cooperative windows of 32 slots (option coop_window), else 64
+constexpr int kFeatPad = 256;     // the production kernels (cooperative tail, no extensions) on records
+                                  //   with pad slots (leaf_align); every other variant always reads pad bits
 constexpr unsigned kHeavyLaneMark = kLearnHeavyMark;   // rt_internal.h
 
 // One pixel of a heavy tile, the whole wave on it (option heavy_fused, the
@@ -739,6 +742,11 @@ template <bool COUNT, bool DIAG = false, int FEAT = 0, int WALK = 2>
 __global__ __launch_bounds__(256)
 __attribute__((amdgpu_waves_per_eu((FEAT & kFeatFrontier) ? 1 : RT_SIMPLE_WPE)))
 void trace_simple(TraceArgs a) {
+    // Pad bits (leaf_align): the production kernels (cooperative tail, no
+    // extensions or frontier tail) read them only when built with kFeatPad, so
+    // scenes with packed records run the packed code; every other variant
+    // reads them always.
+    constexpr bool PAD = (FEAT & kFeatPad) || (FEAT & (kFeatExt | kFeatFrontier)) || !(FEAT & kFeatCoopTail);
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
     // frontier_walk's per-wave frontiers (kFCap entries per wave; dynamic LDS,
@@ -892,18 +900,20 @@ void trace_simple(TraceArgs a) {
                     // is hit or not (its skip); an internal node's left child is
                     // the next slot (one more past a pad slot: leaf bit 29 of word
                     // [0].w, internal bit 2 of word [1].w)
-                    // (selects by masks: written as ternaries, the compiler branched
-                    // here, on the dependent chain to the next load: +7% per frame,
-                    // profiles/r04/r4j)
-#if RT_WALK_PAD
-                    const int n_leaf = n + 2 + (int)((aw >> 29) & 1u);
-                    const int n_hit = n + 1 + (int)((bw >> 2) & 1u);
-#else
-                    const int n_leaf = n + 2, n_hit = n + 1;                 // (A/B build: packed records only)
-#endif
-                    const int m_hit = -(int)hb, m_leaf = -(int)nleaf;
-                    const int n_int = (n_hit & m_hit) | ((int)(aw & kIdx) & ~m_hit);
-                    const int nxt = (n_leaf & m_leaf) | (n_int & ~m_leaf);
+                    // Packed records (no kFeatPad) take the plain ternary; with pad
+                    // bits the selects are written by masks: as ternaries the
+                    // compiler branched there, on the dependent chain to the next
+                    // load (+7% per frame, profiles/r04/r4j-r4k).
+                    int nxt;
+                    if (PAD) {
+                        const int n_leaf = n + 2 + (int)((aw >> 29) & 1u);
+                        const int n_hit = n + 1 + (int)((bw >> 2) & 1u);
+                        const int m_hit = -(int)hb, m_leaf = -(int)nleaf;
+                        const int n_int = (n_hit & m_hit) | ((int)(aw & kIdx) & ~m_hit);
+                        nxt = (n_leaf & m_leaf) | (n_int & ~m_leaf);
+                    } else {
+                        nxt = nleaf ? n + 2 : (hb ? n + 1 : (int)(aw & kIdx));
+                    }
                     const bool nl = (((hb && !nleaf) ? bw : (aw >> 31)) & 1u) != 0u;
                     const float v0x = B.w;                                   // a leaf's v0.x
                     if (COUNT && hb && !nleaf) c_node += 2;
@@ -957,8 +967,8 @@ void trace_simple(TraceArgs a) {
                     // the windows walk slots of the walk-2 records (walk 0 hands over a
                     // node index: its slot first)
                     const int ws = WALK == 2 ? lane_i(start, L) : a.scene.node_slot[lane_i(start, L)];
-                    nw = coop_walk<COUNT, (FEAT & kFeatWin32) ? 32 : 64>(a.scene.walk, a.scene.end2, ws, bo, bd,
-                                                                             bi, bc, bh, cn, ct);
+                    nw = coop_walk<COUNT, (FEAT & kFeatWin32) ? 32 : 64, PAD>(a.scene.walk, a.scene.end2, ws, bo,
+                                                                                  bd, bi, bc, bh, cn, ct);
                 }
                 if (DIAG) {
                     d_windows += nw;
@@ -1043,11 +1053,22 @@ void trace_simple(TraceArgs a) {
 
 }  // namespace
 
-// The fused heavy-pixel launch (walk 2).
+// The fused heavy-pixel launch (walk 2), in the window size and record form
+// of the scene (big: kFeatWin32 | kFeatPad).
 #define RT_FUSED(G)                                                                                           \
     if (a.diag) hipLaunchKernelGGL((trace_simple<false, true, FF, 2>), G, block, shm, stream, ao);             \
     else if (a.counters) hipLaunchKernelGGL((trace_simple<true, false, FF, 2>), G, block, shm, stream, ao);     \
     else hipLaunchKernelGGL((trace_simple<false, false, FF, 2>), G, block, shm, stream, ao);
+#define RT_FUSED_BIG(G)                                                                                       \
+    switch (big) {                                                                                            \
+        case kFeatWin32: { constexpr int FF = kFeatCoopTail | kFeatFused | kFeatWin32; RT_FUSED(G) } break;   \
+        case kFeatPad: { constexpr int FF = kFeatCoopTail | kFeatFused | kFeatPad; RT_FUSED(G) } break;       \
+        case kFeatWin32 | kFeatPad: {                                                                         \
+            constexpr int FF = kFeatCoopTail | kFeatFused | kFeatWin32 | kFeatPad;                            \
+            RT_FUSED(G)                                                                                       \
+        } break;                                                                                              \
+        default: { constexpr int FF = kFeatCoopTail | kFeatFused; RT_FUSED(G) } break;                        \
+    }
 
 hipError_t launch_trace(const TraceArgs& a, hipStream_t stream, int* kernels) {
     if (kernels) *kernels = 1;
@@ -1057,8 +1078,10 @@ hipError_t launch_trace(const TraceArgs& a, hipStream_t stream, int* kernels) {
     const dim3 block(64 * bw);
     const int feat = (a.coop_lanes > 0 ? kFeatCoopTail : 0) | (a.ext != 0 ? kFeatExt : 0) |
                      (a.coop_lanes > 0 && a.coop_walk ? kFeatFrontier : 0);
-    // the production kernels (walk 2, coop tail, no extensions) come in both window sizes
-    const bool win32 = a.coop_win == 32 && a.walk == 2 && (feat & ~kFeatFrontier) == kFeatCoopTail;
+    // the production kernels (walk 2, coop tail, no extensions or frontier
+    // tail) come in both window sizes, for packed and for padded records
+    const bool prod = a.walk == 2 && (feat & ~kFeatFrontier) == kFeatCoopTail;
+    const int big = prod ? ((a.coop_win == 32 ? kFeatWin32 : 0) | (a.scene.padded ? kFeatPad : 0)) : 0;
     TraceArgs ao = a;
     ao.tiles_y = tiles_y;
     bool join = false;
@@ -1073,13 +1096,7 @@ hipError_t launch_trace(const TraceArgs& a, hipStream_t stream, int* kernels) {
             ao.split_n = 0;
             const dim3 gf(a.n_heavy_px + n_tiles);
             const size_t shm = kFCap * sizeof(uint4);
-            if (win32) {
-                constexpr int FF = kFeatCoopTail | kFeatFused | kFeatWin32;
-                RT_FUSED(gf)
-            } else {
-                constexpr int FF = kFeatCoopTail | kFeatFused;
-                RT_FUSED(gf)
-            }
+            RT_FUSED_BIG(gf)
             return hipGetLastError();
         }
         if (H > 0 && a.heavy_fused && bw == 1 && (feat & ~kFeatFrontier) == kFeatCoopTail) {
@@ -1089,13 +1106,7 @@ hipError_t launch_trace(const TraceArgs& a, hipStream_t stream, int* kernels) {
             ao.split_n = H;
             const dim3 gf(64 * H + (n_tiles - H));
             const size_t shm = kFCap * sizeof(uint4);
-            if (win32) {
-                constexpr int FF = kFeatCoopTail | kFeatFused | kFeatWin32;
-                RT_FUSED(gf)
-            } else {
-                constexpr int FF = kFeatCoopTail | kFeatFused;
-                RT_FUSED(gf)
-            }
+            RT_FUSED_BIG(gf)
             return hipGetLastError();
         }
         if (H > 0 && a.ev_fork && bw == 1 && (feat & ~kFeatFrontier) == kFeatCoopTail) {
@@ -1138,10 +1149,11 @@ hipError_t launch_trace(const TraceArgs& a, hipStream_t stream, int* kernels) {
     if (a.walk == 2) {
         switch (feat) {
             case kFeatCoopTail:
-                if (win32) {
-                    RT_SIMPLE(kFeatCoopTail | kFeatWin32, 2)
-                } else {
-                    RT_SIMPLE(kFeatCoopTail, 2)
+                switch (big) {
+                    case kFeatWin32: RT_SIMPLE(kFeatCoopTail | kFeatWin32, 2) break;
+                    case kFeatPad: RT_SIMPLE(kFeatCoopTail | kFeatPad, 2) break;
+                    case kFeatWin32 | kFeatPad: RT_SIMPLE(kFeatCoopTail | kFeatWin32 | kFeatPad, 2) break;
+                    default: RT_SIMPLE(kFeatCoopTail, 2) break;
                 }
                 break;
             case 0: RT_SIMPLE(0, 2) break;
@@ -1155,6 +1167,7 @@ hipError_t launch_trace(const TraceArgs& a, hipStream_t stream, int* kernels) {
         }
     }
 #undef RT_SIMPLE
+#undef RT_FUSED_BIG
 #undef RT_FUSED
     if (join) {
         hipError_t e = hipGetLastError();

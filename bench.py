@@ -948,7 +948,8 @@ def main() -> None:
                                                                       "heavy_stream", "heavy_pixels",
                                                                       "heavy_pixel_factor", "heavy_cap", "graph",
                                                                       "reuse_order", "order_split", "hw_queues",
-                                                                      "coop_window", "coop_window_used")},
+                                                                      "coop_window", "coop_window_used",
+                                                                      "leaf_align", "leaf_align_used")},
                              "concurrent_launches": renderer.get_option("concurrent_launches"),
                              "heavy_tiles_used": heavy_used,
                              "heavy_pixels_used": heavy_px_used},

@@ -343,9 +343,13 @@ int rt_render_poll(rt_ctx* ctx, uint64_t ticket, int* done);
  *                   learning launch's stream, with no synchronisation (default;
  *                   the default heavy-pixel schedule only); 0 = copy the records
  *                   back and learn on the host after a stream synchronisation
- *   "leaf_align"    1 (default) = at the next rt_upload_scene, lay the walk
- *                   records out so that no leaf's 64-B record straddles a
- *                   128-B line (a pad slot before such a leaf); 0 = packed
+ *   "leaf_align"    at the next rt_upload_scene: 1 = lay the walk records out
+ *                   so that no leaf's 64-B record straddles a 128-B line (a
+ *                   pad slot before such a leaf); 0 = packed; 2 (default) =
+ *                   aligned when the packed records exceed 32 MB (the L2s of
+ *                   the 8 XCDs), else packed
+ *   "leaf_align_used" (rt_get_option only) 1 if the current scene's records
+ *                   on device 0 hold pad slots
  *   "plain_kernels" (rt_get_option only) production-build trace kernels enqueued
  *                   on device 0 so far (not counting, diagnostic or learning
  *                   launches): lets a profiler's kernel trace be cut at a

@@ -113,6 +113,7 @@ def test_config5_1m_row_subset(renderer):
     info = renderer.scene_info()
     assert info["n_tris"] == built.triangle_count
     assert renderer.get_option("coop_window_used") == 32      # ~100 MB of walk records: 32-slot windows
+    assert renderer.get_option("leaf_align_used") == 1        # and aligned leaf records
     rgba, rad, st = _bands_device(renderer, cam, cfg.width, cfg.height, cfg.max_bounces, 1, 64, 5)
     ref = _oracle(built, cam.ubo_bytes(), cfg.width, cfg.height, cfg.max_bounces,
                   tile=(0, 5, cfg.width, cfg.height - 5), row_step=64)

@@ -244,10 +244,10 @@ def test_device_learning_matches_host_learning(renderer, cfg_k):
 @pytest.mark.parametrize("align", [0, 1])
 @pytest.mark.parametrize("cfg_k", [3, 6, 2])
 def test_leaf_align_bit_exact(renderer, cfg_k, align):
-    """Option leaf_align both ways (1, the default: walk records with a pad
-    slot before any leaf that would straddle a 128-B line, the predecessor's
-    pad bit stepping over it; 0: packed): frames and counters equal the
-    oracle's, in the lockstep walk, the cooperative windows (coop_lanes 64:
+    """Option leaf_align both ways (1: walk records with a pad slot before any
+    leaf that would straddle a 128-B line, the predecessor's pad bit stepping
+    over it, run by the kFeatPad kernels; 0: packed): frames and counters equal
+    the oracle's, in the lockstep walk, the cooperative windows (coop_lanes 64:
     every walk) and the learned order."""
     from rtamd import configs
     cfg = configs.get(cfg_k)
@@ -258,6 +258,7 @@ def test_leaf_align_bit_exact(renderer, cfg_k, align):
     try:
         renderer.set_option("leaf_align", align)
         renderer.upload_scene(built)
+        assert renderer.get_option("leaf_align_used") == align
         for coop in (1, 64):
             renderer.set_option("coop_lanes", coop)
             for launch in range(2):
@@ -268,7 +269,7 @@ def test_leaf_align_bit_exact(renderer, cfg_k, align):
         for k in ("segments", "node_visits", "tri_tests", "mat_reads"):
             assert st[k] == full[k], k
     finally:
-        renderer.set_option("leaf_align", 1)
+        renderer.set_option("leaf_align", 2)
         renderer.set_option("coop_lanes", 1)
         renderer.upload_scene(built)
 
@@ -288,6 +289,7 @@ def test_coop_window_bit_exact(renderer, cfg_k, win):
     try:
         renderer.upload_scene(built)
         assert renderer.get_option("coop_window_used") == 64    # L2-sized scenes: 64-slot windows
+        assert renderer.get_option("leaf_align_used") == 0      # and packed records
         renderer.set_option("coop_window", win)
         assert renderer.get_option("coop_window") == win
         for coop in (1, 64):
