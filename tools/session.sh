@@ -102,8 +102,6 @@ for s in "$@"; do
     ab5)      run ab5 900 bash tools/ab_old_new.sh "$OUT/ab5" 2 --config 5 --steps 10 --warmup 3 ;;
     abargs)   run abargs 900 env ARMS_FILE="${ARMS_FILE:?}" REPS="${REPS:-3}" STEPS="${STEPS:-200}" \
                   bash tools/ab_args.sh "$TAG/abargs_$(basename "$ARMS_FILE" .txt)" ;;
-    bisect)   run bisect 900 bash tools/ab_trees.sh "$OUT/bisect" 2 "--steps 200 --warmup 5" \
-                  build_ab/old build_ab/793740e build_ab/b88e2c4 build_ab/5b41a91 . ;;
     abchain)  run abchain3 900 env REPS=3 bash tools/ab_lib.sh "$OUT/abchain3" "--steps 200 --warmup 5" \
                   3d-ray-tracer-vulkan_amd/lib/librtamd.so 3d-ray-tracer-vulkan_amd/lib/variants/librtamd_chain.so \
                   3d-ray-tracer-vulkan_amd/lib/variants/librtamd_chain2.so && \
