@@ -24,7 +24,11 @@ R04 = os.path.join(ROOT, "profiles", "r04")
 R04_LINES = [("r4b", "bench.json"), ("r4b", "bench_orbit.json"), ("r4b", "prof3.json"),
              # the final layout (aligned leaf records, 32-slot windows for config 5), PMC of r4h
              ("r4i", "bench.json"), ("r4i", "bench_orbit.json"), ("r4i", "prof3.json"), ("r4i", "prof5.json"),
-             ("r4h", "bench_cfg5.json")]
+             ("r4h", "bench_cfg5.json"),
+             # the final tree (packed records and the r4d walk for config 3; aligned + 32-slot windows for
+             # config 5), PMC of the same session
+             ("r4s", "bench.json"), ("r4s", "bench_orbit.json"), ("r4s", "prof3.json"), ("r4s", "prof5.json"),
+             ("r4s", "bench_cfg5.json")]
 sys.path.insert(0, ROOT)
 
 import bench  # noqa: E402  (module level: argparse-free helpers, no torch)
@@ -149,7 +153,7 @@ def test_r04_roofline_reproduces(session, name):
     assert c["frames_verified"] is True
 
 
-@pytest.mark.parametrize("session,cfg", [("r4b", 3), ("r4i", 3), ("r4i", 5)])
+@pytest.mark.parametrize("session,cfg", [("r4b", 3), ("r4i", 3), ("r4i", 5), ("r4s", 3), ("r4s", 5)])
 def test_r04_rocprof_union(session, cfg):
     u = json.load(open(os.path.join(R04, session, f"union_cfg{cfg}.json")))
     p = _r04(session, f"prof{cfg}.json")
@@ -162,7 +166,7 @@ def test_r04_rocprof_union(session, cfg):
     assert u["launch_ms_mean"] == pytest.approx(p["roofline"]["kernel_ms"], rel=0.05)
 
 
-@pytest.mark.parametrize("session", ["r4i"])
+@pytest.mark.parametrize("session", ["r4i", "r4s"])
 def test_r04_camera_stop_learning_frame(session):
     """The frames after the camera stops (the first: its learning launch, the
     order then learned on the device; the second: the launch behind those
