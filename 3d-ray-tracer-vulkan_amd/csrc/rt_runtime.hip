@@ -308,6 +308,9 @@ static constexpr int    kMaxHeavy = 256;
 // 28.5 GB per frame at the same frame time; config 3 (6.3 MB, L2-resident)
 // is 1.2% faster with 64 (profiles/r04/r4f).
 static constexpr size_t kWin32Bytes = 32ull << 20;
+// The walk's buffer loads address the records with 32-bit byte offsets
+// (rt_trace.hip, RT_CHAIN 2): at most 2^27 - 4 slots of 32 B (~45M triangles).
+static constexpr unsigned kMaxWalkSlots = (1u << 27) - 4;
 static constexpr size_t kDiagWords = 8;   // per-wave diag record (rt_trace.hip, rtamd.h rt_diag_copy)
 
 static void free_order(PerDevice::Order& o) {
@@ -1068,9 +1071,10 @@ int rt_upload_scene(rt_ctx* ctx, const void* vertices, size_t vertex_bytes,
         }
         slot[i] = (int)nslot;
         nslot += (fl & 2u) ? 2 : 1;
-        if (nslot >= (1u << 30)) {
+        if (nslot >= kMaxWalkSlots) {
             free_host_scene(&hs);
-            set_error("rt_upload_scene: %zu nodes: at most 2^30 walk slots supported", n2);
+            set_error("rt_upload_scene: %zu nodes: at most %u walk slots (4 GB of walk records) supported", n2,
+                      kMaxWalkSlots);
             return RT_ERR_BAD_SCENE;
         }
     }

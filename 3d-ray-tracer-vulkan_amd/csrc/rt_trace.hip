@@ -354,7 +354,12 @@ __device__ __forceinline__ float lane_f(float v, int k) {
 
 // ------------------------------------------------------------ cooperative walk --
 #ifndef RT_CHAIN
-#define RT_CHAIN 0         // A/B: a shorter dependent chain from the slab test to the next load
+// The lockstep walk's next records: 2 = buffer loads whose address is one
+// shift of the slot index (config 3 0.2947-0.2960 vs 0.2965-0.2980 ms, config 5
+// 8.07-8.10 vs 8.10-8.11, profiles/r04/r4s abchain; records < 4 GB, checked at
+// upload); 1 = one select on the chain (slower: 0.298-0.300, 8.42-8.56); 0 =
+// global loads.
+#define RT_CHAIN 2
 #endif
 #if RT_CHAIN == 2
 __device__ __forceinline__ float4 wbuf(__amdgpu_buffer_rsrc_t r, int slot, int off) {
@@ -891,7 +896,7 @@ void trace_simple(TraceArgs a) {
             // a buffer resource over the records: the next slot's address is one
             // shift of its index (the offset field adds the 16-B halves)
             const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc(
-                const_cast<float4*>(wr), 0, (a.scene.end2 + 2) * 32, 0x00020000);
+                const_cast<float4*>(wr), 0, (int)((unsigned)(a.scene.end2 + 2) * 32u), 0x00020000);
 #endif
             if (WALK == 2 && walking) {
                 A = wr[2 * n];
