@@ -28,7 +28,10 @@ R04_LINES = [("r4b", "bench.json"), ("r4b", "bench_orbit.json"), ("r4b", "prof3.
              # the final tree (packed records and the r4d walk for config 3; aligned + 32-slot windows for
              # config 5), PMC of the same session
              ("r4s", "bench.json"), ("r4s", "bench_orbit.json"), ("r4s", "prof3.json"), ("r4s", "prof5.json"),
-             ("r4s", "bench_cfg5.json")]
+             ("r4s", "bench_cfg5.json"),
+             # + the walk's buffer loads (RT_CHAIN 2): the shipped build
+             ("r4u", "bench.json"), ("r4u", "bench_orbit.json"), ("r4u", "prof3.json"), ("r4u", "prof5.json"),
+             ("r4u", "bench_cfg5.json")]
 sys.path.insert(0, ROOT)
 
 import bench  # noqa: E402  (module level: argparse-free helpers, no torch)
@@ -153,7 +156,8 @@ def test_r04_roofline_reproduces(session, name):
     assert c["frames_verified"] is True
 
 
-@pytest.mark.parametrize("session,cfg", [("r4b", 3), ("r4i", 3), ("r4i", 5), ("r4s", 3), ("r4s", 5)])
+@pytest.mark.parametrize("session,cfg", [("r4b", 3), ("r4i", 3), ("r4i", 5), ("r4s", 3), ("r4s", 5),
+                                         ("r4u", 3), ("r4u", 5)])
 def test_r04_rocprof_union(session, cfg):
     u = json.load(open(os.path.join(R04, session, f"union_cfg{cfg}.json")))
     p = _r04(session, f"prof{cfg}.json")
@@ -166,7 +170,7 @@ def test_r04_rocprof_union(session, cfg):
     assert u["launch_ms_mean"] == pytest.approx(p["roofline"]["kernel_ms"], rel=0.05)
 
 
-@pytest.mark.parametrize("session", ["r4i", "r4s"])
+@pytest.mark.parametrize("session", ["r4i", "r4s", "r4u"])
 def test_r04_camera_stop_learning_frame(session):
     """The frames after the camera stops (the first: its learning launch, the
     order then learned on the device; the second: the launch behind those
