@@ -361,7 +361,7 @@ __device__ __forceinline__ float lane_f(float v, int k) {
 // global loads.
 #define RT_CHAIN 2
 #endif
-#if RT_CHAIN == 2
+#if RT_CHAIN >= 2
 __device__ __forceinline__ float4 wbuf(__amdgpu_buffer_rsrc_t r, int slot, int off) {
     const auto v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)((unsigned)slot << 5) + off, 0, 0);
     return make_float4(__uint_as_float(v[0]), __uint_as_float(v[1]), __uint_as_float(v[2]), __uint_as_float(v[3]));
@@ -892,7 +892,7 @@ void trace_simple(TraceArgs a) {
             // Q0 and Q1, the rest of its triangle.
             float4 A, B, Q0, Q1;
             const float4* __restrict__ wr = a.scene.walk;
-#if RT_CHAIN == 2
+#if RT_CHAIN >= 2
             // a buffer resource over the records: the next slot's address is one
             // shift of its index (the offset field adds the 16-B halves)
             const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc(
@@ -932,7 +932,7 @@ void trace_simple(TraceArgs a) {
                         const int n_int = (n_hit & m_hit) | ((int)(aw & kIdx) & ~m_hit);
                         nxt = (n_leaf & m_leaf) | (n_int & ~m_leaf);
                     } else {
-#if RT_CHAIN
+#if RT_CHAIN == 1 || RT_CHAIN == 2
                         const int t = nleaf ? n + 2 : n + 1;                 // known before the slab test ends
                         nxt = (hb || nleaf) ? t : (int)(aw & kIdx);
 #else
@@ -942,10 +942,10 @@ void trace_simple(TraceArgs a) {
                     const bool nl = (((hb && !nleaf) ? bw : (aw >> 31)) & 1u) != 0u;
                     const float v0x = B.w;                                   // a leaf's v0.x
                     if (COUNT && hb && !nleaf) c_node += 2;
-#if RT_CHAIN == 2
+#if RT_CHAIN >= 2
                     A = wbuf(wrs, nxt, 0);                                   // slot end is padding
                     B = wbuf(wrs, nxt, 16);
-#elif RT_CHAIN
+#elif RT_CHAIN == 1
                     {
                         const float4* p = reinterpret_cast<const float4*>(reinterpret_cast<const char*>(wr) +
                                                                           ((size_t)(unsigned)nxt << 5));
@@ -966,7 +966,7 @@ void trace_simple(TraceArgs a) {
                         }
                     }
                     if (nl && nxt < wend) {
-#if RT_CHAIN == 2
+#if RT_CHAIN >= 2
                         Q0 = wbuf(wrs, nxt, 32);
                         Q1 = wbuf(wrs, nxt, 48);
 #else
