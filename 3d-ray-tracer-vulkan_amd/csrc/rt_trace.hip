@@ -357,8 +357,9 @@ __device__ __forceinline__ float lane_f(float v, int k) {
 // The lockstep walk's next records: 2 = buffer loads whose address is one
 // shift of the slot index (config 3 0.2947-0.2960 vs 0.2965-0.2980 ms, config 5
 // 8.07-8.10 vs 8.10-8.11, profiles/r04/r4s abchain; records < 4 GB, checked at
-// upload); 1 = one select on the chain (slower: 0.298-0.300, 8.42-8.56); 0 =
-// global loads.
+// upload); 3 = the same with two selects (equal: 0.2957-0.2963 vs
+// 0.2955-0.2977, profiles/r04/r4v); 1 = one select on the chain with global
+// loads (slower: 0.298-0.300, 8.42-8.56); 0 = global loads.
 #define RT_CHAIN 2
 #endif
 #if RT_CHAIN >= 2

@@ -27,7 +27,6 @@
 #   ab3 / ab5 bench.py interleaved against the tree in build_ab/old (tools/ab_old_new.sh),
 #             config 3 (3 rounds, 200 steps) / config 5 (2 rounds, 10 steps)
 #   abargs    tools/ab_args.sh over the arms in $ARMS_FILE ($REPS rounds, $STEPS steps)
-#   abchain   the default build (RT_CHAIN 2) against lib/variants/librtamd_chain3.so (RT_CHAIN 3)
 #   cmd       the command in $CMD (600 s)
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -101,10 +100,6 @@ for s in "$@"; do
     ab5)      run ab5 900 bash tools/ab_old_new.sh "$OUT/ab5" 2 --config 5 --steps 10 --warmup 3 ;;
     abargs)   run abargs 900 env ARMS_FILE="${ARMS_FILE:?}" REPS="${REPS:-3}" STEPS="${STEPS:-200}" \
                   bash tools/ab_args.sh "$TAG/abargs_$(basename "$ARMS_FILE" .txt)" ;;
-    abchain)  run abchain3 900 env REPS=3 bash tools/ab_lib.sh "$OUT/abchain3" "--steps 200 --warmup 5" \
-                  3d-ray-tracer-vulkan_amd/lib/librtamd.so 3d-ray-tracer-vulkan_amd/lib/variants/librtamd_chain3.so && \
-              run abchain5 900 env REPS=2 bash tools/ab_lib.sh "$OUT/abchain5" "--config 5 --steps 10 --warmup 3" \
-                  3d-ray-tracer-vulkan_amd/lib/librtamd.so 3d-ray-tracer-vulkan_amd/lib/variants/librtamd_chain3.so ;;
     cmd)      run cmd 600 bash -c "$CMD" > "$OUT/cmd.log" 2>&1 ;;
     *)        status "unknown step $s" ;;
   esac
