@@ -88,7 +88,10 @@ int rt_create(const int* device_ids, int n_devices, rt_ctx** out);
  * Deep-copies; the caller may free the buffers on return (the Java host frees
  * them right after upload, VulkanEngine.java:343,351).  Sizes below one record
  * (the reference's 1-float / 1-byte dummies for an empty scene,
- * SceneBuilder.java:61-70) upload an empty scene, which renders sky only. */
+ * SceneBuilder.java:61-70) upload an empty scene, which renders sky only.
+ * Scenes whose walk records would exceed 4 GB (2^27 - 4 slots of 32 B: about
+ * 45M triangles) fail with RT_ERR_BAD_SCENE: the walk addresses its records
+ * with 32-bit buffer offsets. */
 int rt_upload_scene(rt_ctx* ctx,
                     const void* vertices,  size_t vertex_bytes,
                     const void* materials, size_t material_bytes,
