@@ -362,6 +362,15 @@ __device__ __forceinline__ float lane_f(float v, int k) {
 // loads (slower: 0.298-0.300, 8.42-8.56); 0 = global loads.
 #define RT_CHAIN 2
 #endif
+#ifndef RT_COOP_BUF
+#define RT_COOP_BUF 1      // cooperative windows through buffer loads (0: global loads, A/B builds)
+#endif
+#if RT_COOP_BUF
+__device__ __forceinline__ float4 wbuf_s(__amdgpu_buffer_rsrc_t r, int voff, unsigned soff) {
+    const auto v = __builtin_amdgcn_raw_buffer_load_b128(r, voff, (int)soff, 0);
+    return make_float4(__uint_as_float(v[0]), __uint_as_float(v[1]), __uint_as_float(v[2]), __uint_as_float(v[3]));
+}
+#endif
 #if RT_CHAIN >= 2
 __device__ __forceinline__ float4 wbuf(__amdgpu_buffer_rsrc_t r, int slot, int off) {
     const auto v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)((unsigned)slot << 5) + off, 0, 0);
@@ -402,6 +411,14 @@ __device__ __forceinline__ int coop_walk(const float4* __restrict__ walk, int en
                                          unsigned long long& c_tri) {
     const int lane = threadIdx.x & 63;
     int windows = 0;
+#if RT_COOP_BUF
+    // buffer loads: lane k's offset k x 32 B is fixed, the window start is the
+    // scalar offset, so no vector instruction sits between the replay's next n
+    // and the window's loads
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float4*>(walk), 0, (int)((unsigned)(end + 2) * 32u), 0x00020000);
+    const int voff = lane << 5;
+#endif
     while (n < end) {
         ++windows;
         const int j = n + lane;
@@ -411,10 +428,17 @@ __device__ __forceinline__ int coop_walk(const float4* __restrict__ walk, int en
         bool ind = false, tv = false, lf = false, pd = false;
         float4 A = make_float4(0.f, 0.f, 0.f, 0.f), B = A;
 #if RT_COOP_DPP
+#if RT_COOP_BUF
+        if (ld) {                                                   // window start in the scalar offset
+            A = wbuf_s(rs, voff, (unsigned)n << 5);
+            B = wbuf_s(rs, voff + 16, (unsigned)n << 5);
+        }
+#else
         if (ld) {
             A = walk[2 * j];
             B = walk[2 * j + 1];
         }
+#endif
         const float4 Q0 = next_lane(A), Q1 = next_lane(B);          // the slot after this one (every lane active)
 #else
         float4 Q0 = A, Q1 = A;                                       // (A/B variant: the slot after, loaded)
