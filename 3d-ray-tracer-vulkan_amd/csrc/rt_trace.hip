@@ -363,7 +363,9 @@ __device__ __forceinline__ float lane_f(float v, int k) {
 #define RT_CHAIN 2
 #endif
 #ifndef RT_COOP_BUF
-#define RT_COOP_BUF 1      // cooperative windows through buffer loads (0: global loads, A/B builds)
+// 1 = cooperative windows through buffer loads: slower (config 3 0.2969-0.2986 vs
+// 0.2946-0.2957 ms; 8 B more scratch per lane; profiles/r04/r4y), so 0
+#define RT_COOP_BUF 0
 #endif
 #if RT_COOP_BUF
 __device__ __forceinline__ float4 wbuf_s(__amdgpu_buffer_rsrc_t r, int voff, unsigned soff) {
