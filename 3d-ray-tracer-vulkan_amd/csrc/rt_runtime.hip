@@ -351,7 +351,8 @@ static constexpr size_t kMaxLastCams = 64;
 
 struct rt_ctx {
     std::vector<PerDevice> dev;
-    int  wave_tile = 0;            // 8x8 (default) / 16x4 / 32x2 / 64x1 pixels per wave
+    int  wave_tile = -1;           // 8x8 / 16x4 / 32x2 / 64x1 pixels per wave (0-3); -1 (default) = 16x4
+                                   //   when the walk records exceed kWin32Bytes, else 8x8
     int  diag = 0;                 // record per-wave timestamps
     int  coop_lanes = 1;           // cooperative tail once <= this many lanes walk (0 = off)
     int  ext = 0;                  // non-reference extensions (kExt* bits), off by default
@@ -752,6 +753,14 @@ static int learn_order(const rt_ctx* ctx, PerDevice& p, const TraceArgs& a, hipS
     return RT_OK;
 }
 
+// wave_tile -1: config 5 (112 MB of records, 4K) runs 16x4 tiles in 7.83-7.89
+// ms per frame against 8.07-8.10 for 8x8; config 3 (6 MB, 1080p) runs 8x8 in
+// 0.2942-0.2954 against 0.2965-0.2987 (profiles/r04/r4aa, r4ab).
+static int wave_tile_of(const rt_ctx* ctx, const PerDevice& p) {
+    if (ctx->wave_tile >= 0) return ctx->wave_tile;
+    return (size_t)p.scene.end2 * 32 > kWin32Bytes ? 1 : 0;
+}
+
 static int coop_window_of(const rt_ctx* ctx, const PerDevice& p) {
     if (ctx->coop_window) return ctx->coop_window;
     return (size_t)p.scene.end2 * 32 > kWin32Bytes ? 32 : 64;
@@ -759,7 +768,7 @@ static int coop_window_of(const rt_ctx* ctx, const PerDevice& p) {
 
 static int set_schedule(const rt_ctx* ctx, PerDevice& p, TraceArgs& a, const rt_camera_ubo* cam,
                         const std::vector<int>* bands = nullptr) {
-    a.wave_tile = ctx->wave_tile;
+    a.wave_tile = wave_tile_of(ctx, p);
     a.coop_lanes = ctx->coop_lanes;
     a.walk = ctx->walk;
     a.coop_walk = ctx->coop_walk;
@@ -1820,7 +1829,7 @@ int rt_set_option(rt_ctx* ctx, const char* name, int64_t value) {
         ctx->graph = (int)value;
     } else if (std::strcmp(name, "diag") == 0 && (value == 0 || value == 1)) {
         ctx->diag = (int)value;
-    } else if (std::strcmp(name, "wave_tile") == 0 && value >= 0 && value <= 3) {
+    } else if (std::strcmp(name, "wave_tile") == 0 && value >= -1 && value <= 3) {
         ctx->wave_tile = (int)value;
     } else {
         set_error("rt_set_option: unknown option or bad value: %s = %lld", name, (long long)value);
@@ -1833,6 +1842,8 @@ int rt_get_option(rt_ctx* ctx, const char* name, int64_t* value) {
     if (!ctx || !name || !value) { set_error("rt_get_option: null argument"); return RT_ERR_INVALID_ARG; }
     if (std::strcmp(name, "kernel") == 0) *value = 0;
     else if (std::strcmp(name, "wave_tile") == 0) *value = ctx->wave_tile;
+    else if (std::strcmp(name, "wave_tile_used") == 0)
+        *value = ctx->dev.empty() ? 0 : wave_tile_of(ctx, ctx->dev[0]);
     else if (std::strcmp(name, "coop_lanes") == 0) *value = ctx->coop_lanes;
     else if (std::strcmp(name, "walk") == 0) *value = ctx->walk;
     else if (std::strcmp(name, "coop_walk") == 0) *value = ctx->coop_walk;

@@ -949,7 +949,8 @@ def main() -> None:
                                                                       "heavy_pixel_factor", "heavy_cap", "graph",
                                                                       "reuse_order", "order_split", "hw_queues",
                                                                       "coop_window", "coop_window_used",
-                                                                      "leaf_align", "leaf_align_used")},
+                                                                      "leaf_align", "leaf_align_used",
+                                                                      "wave_tile_used")},
                              "concurrent_launches": renderer.get_option("concurrent_launches"),
                              "heavy_tiles_used": heavy_used,
                              "heavy_pixels_used": heavy_px_used},
@@ -958,7 +959,7 @@ def main() -> None:
                 **roof,
                 "kernel": "trace_simple" + (
                     f" (one launch per {F} frame(s): the {heavy_px_used} heaviest pixels one per wave first, then "
-                    f"every {8 << renderer.get_option('wave_tile')}x{8 >> renderer.get_option('wave_tile')} tile "
+                    f"every {8 << renderer.get_option('wave_tile_used')}x{8 >> renderer.get_option('wave_tile_used')} tile "
                     f"without them)" if heavy_px_used > 0 else
                     f" (one launch per {F} frame(s): the {heavy_used} heaviest tiles one pixel per wave first)"
                     if heavy_used > 0 else f" (one launch per {F} frame(s), tiles in the learned order)"),

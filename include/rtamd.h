@@ -322,9 +322,12 @@ int rt_render_poll(rt_ctx* ctx, uint64_t ticket, int* done);
  *                   row across the launch's frames (the same image rows of
  *                   every frame run at once); 0 (default) = frame by frame
  *   "heavy_tiles_used" (rt_get_option only) heavy tiles of the last launch
- *   "wave_tile"     pixels per wave (8<<s) x (8>>s), s = 0..3
- *                   (default 0: 8x8, the shader's local_size; with frames in
- *                   flight it beats 32x2 by 6%, profiles/r02/tiles)
+ *   "wave_tile"     pixels per wave (8<<s) x (8>>s), s = 0..3; -1 (default) =
+ *                   16x4 when the scene's walk records exceed 32 MB (config 5:
+ *                   3% faster), else 8x8 (the shader's local_size; config 3:
+ *                   0.8% faster than 16x4, 6% than 32x2, profiles/r02/tiles)
+ *   "wave_tile_used" (rt_get_option only) the tile shape s the current scene
+ *                   gets on device 0
  *   "extensions"    NON-REFERENCE features, bits (default 0 = the reference's
  *                   shader exactly):
  *                   1 = honour sky_enabled (@68): a miss is black when it is 0

@@ -19,7 +19,7 @@ from raw_bvh import raw_bvh_scene
 pytestmark = pytest.mark.gpu
 
 COUNTERS = ("segments", "node_visits", "tri_tests", "mat_reads")
-DEFAULT_OPTS = {"wave_tile": 0, "coop_lanes": 1, "walk": 2, "coop_walk": 0,
+DEFAULT_OPTS = {"wave_tile": -1, "coop_lanes": 1, "walk": 2, "coop_walk": 0,
                 "block_waves": 1, "heavy_first": 1, "heavy_tiles": -1, "heavy_stream": 2,
                 "learn_cost": 1, "heavy_factor": 130, "graph": 1, "concurrent_launches": 1, "heavy_cap": 75,
                 "heavy_pixels": 1, "heavy_pixel_factor": 50, "reuse_order": 1, "order_split": 0,
