@@ -31,7 +31,9 @@ R04_LINES = [("r4b", "bench.json"), ("r4b", "bench_orbit.json"), ("r4b", "prof3.
              ("r4s", "bench_cfg5.json"),
              # + the walk's buffer loads (RT_CHAIN 2): the shipped build
              ("r4u", "bench.json"), ("r4u", "bench_orbit.json"), ("r4u", "prof3.json"), ("r4u", "prof5.json"),
-             ("r4u", "bench_cfg5.json")]
+             ("r4u", "bench_cfg5.json"),
+             # + 16x4 tiles for scenes past 32 MB of records (config 5)
+             ("r4ad", "prof5.json"), ("r4ad", "bench_cfg5.json")]
 sys.path.insert(0, ROOT)
 
 import bench  # noqa: E402  (module level: argparse-free helpers, no torch)
@@ -157,7 +159,7 @@ def test_r04_roofline_reproduces(session, name):
 
 
 @pytest.mark.parametrize("session,cfg", [("r4b", 3), ("r4i", 3), ("r4i", 5), ("r4s", 3), ("r4s", 5),
-                                         ("r4u", 3), ("r4u", 5)])
+                                         ("r4u", 3), ("r4u", 5), ("r4ad", 5)])
 def test_r04_rocprof_union(session, cfg):
     u = json.load(open(os.path.join(R04, session, f"union_cfg{cfg}.json")))
     p = _r04(session, f"prof{cfg}.json")
