@@ -1,0 +1,65 @@
+// accel_build.h — the runtime-built acceleration structure of option "accel"
+// (pure host C++; no HIP types, so tools/accel_study builds it with g++).
+//
+// The reference's BVH is a median split on a random axis, visited left child
+// first (BVHBuilder.java:48-93, compute_dynamic_ray.comp:185-210).  Its tree
+// is random on every build (BVHBuilder.java:53, an unseeded ThreadLocalRandom),
+// so its frame is a function of the triangles, not of the tree, except on
+// floating-point ties.  Option accel traces the same triangles through a
+// binned-SAH tree built here from the uploaded buffers, visited near child
+// first, with the two rules that make the closest hit the reference's
+// (DESIGN.md §4a):
+//   * a box is entered when t_enter <= closest_t (the reference: <), so a
+//     triangle whose t equals closest_t is still tested;
+//   * a triangle hit is taken when t < closest_t, or t == closest_t and its
+//     flattened index is lower than the current hit's: the reference visits
+//     leaves in preorder, which is flattened-index order, and keeps the first
+//     hit found at a given t (:122, strict <).
+// Every leaf keeps its triangle's own box from the reference's leaf node (the
+// box the reference tests before the triangle), so a triangle is tested only
+// where the reference could test it.
+//
+// Records: the walk-2 slot format of rt_internal.h (DevScene::walk), packed
+// (no pad slots): an internal node one 32-B slot, a leaf two (box, then its
+// triangle v0 / e1 / e2).  n_layouts copies of the tree in preorder, each with
+// its own child order: layout o puts first, at a node split on axis a, the
+// child on the side a ray with sign bit ((o >> a) & 1) on axis a reaches first
+// (n_layouts 1: always the lower child).  A ray walks the layout of its
+// direction's octant (sign bits of d.x, d.y, d.z), so the stackless skip walk
+// is a near-first ordered traversal.
+#pragma once
+#include <cmath>
+#include <cstddef>
+#include <cstdint>
+#include <string>
+#include <vector>
+
+namespace rtamd {
+
+struct AccelHost {
+    std::vector<uint32_t> rec;      // 8 words per slot, n_layouts * slots slots, + 2 slots of zero padding
+    int n_layouts = 0;              // 1 or 8
+    int slots = 0;                  // slots per layout (0: empty scene)
+    int root_leaf = 0;              // the root is a leaf (a one-triangle scene)
+    int n_prims = 0;                // leaves: triangles after removing exact duplicates
+    int n_inputs = 0;               // leaves of the reference tree
+    int depth = 0;                  // deepest leaf (root = 0)
+    double sah = 0.0;               // SAH cost of the tree (internal 1, leaf 1, relative to the root box area)
+};
+
+// Builds the records from the reference's buffers (the rt_upload_scene
+// inputs: 48-B vertex records, 16-B materials, 48-B preorder nodes).  The
+// buffers must already have passed build_host_scene's validation.  Returns
+// 0, or -1 with *err set.  n_threads: 0 = hardware concurrency.
+int accel_build(const void* vertices, size_t vertex_bytes, const void* materials, size_t material_bytes,
+                const void* bvh_nodes, size_t bvh_bytes, int n_layouts, int n_threads, AccelHost* out,
+                std::string* err);
+
+// The layout a ray with direction d walks: its octant (sign bits) when
+// n_layouts is 8, else 0.
+inline int accel_layout(float dx, float dy, float dz, int n_layouts) {
+    if (n_layouts != 8) return 0;
+    return (std::signbit(dx) ? 1 : 0) | (std::signbit(dy) ? 2 : 0) | (std::signbit(dz) ? 4 : 0);
+}
+
+}  // namespace rtamd

@@ -70,6 +70,17 @@ struct DevScene {
     int*     node_slot = nullptr;   // slot(i) of node i (walk 0 hands its node index to the windows tail)
     int      end2    = 0;
     int      padded  = 0;   // 1: the walk records hold pad slots (leaf_align)
+    // Option accel (accel_build.h): walk = the accel records,
+    // n_layouts (1 or 8) layouts of layout_slots slots each (end2 = their
+    // total, end = layout_slots), and the reference's walk records beside
+    // them for the fallback (a segment whose hit lies before its own box's
+    // t_enter is walked again in the reference's order): walk_ref, end2_ref
+    // slots (pad slots as `ref_padded`).  n_layouts 0: no accel.
+    int      n_layouts = 0;
+    int      layout_slots = 0;
+    float4*  walk_ref = nullptr;
+    int      end2_ref = 0;
+    int      ref_padded = 0;
     // norms and mats interleave in one allocation (kShadeStride float4 per
     // triangle: normal, then albedo/type), so shading a hit touches one 32-B
     // record; norms points at the allocation, mats one float4 in

@@ -4,6 +4,7 @@
 // barriers, staging image) has no counterpart: device buffers + one HIP
 // stream per device.
 #include "rt_internal.h"
+#include "accel_build.h"
 
 #include <cmath>
 #include <cstdarg>
@@ -222,6 +223,10 @@ static constexpr int kMaxSlots = 8;   // rt_render_async frame slots per device
 #ifndef RT_LEAF_ALIGN
 #define RT_LEAF_ALIGN 2
 #endif
+// Option accel's default.
+#ifndef RT_ACCEL
+#define RT_ACCEL 0
+#endif
 
 struct PerDevice {
     int          device = 0;
@@ -379,6 +384,8 @@ struct rt_ctx {
     int  learn_alone = 0;          // heavy_first: a learning launch first waits for the device to drain
     int  learn_device = 1;         // heavy_first: learn the order on the device (rt_learn.hip; 0 = on the host)
     int  leaf_align = RT_LEAF_ALIGN;   // walk records: no leaf straddles a 128-B line (a pad slot before it)
+    int  accel = RT_ACCEL;         // at the next upload: 0 = the reference's tree and order; 1 / 8 = the
+                                   //   binned-SAH tree in 1 / 8 (octant) layouts (accel_build.h)
     int  order_split = 0;          // heavy_first: only tiles costing >= this percent of the costliest go first
                                    //   (in cost order); the rest keep their raster order (0 = all by cost)
     int  order_frames = 0;         // heavy_first, several frames per launch: the non-leading tiles row by row
@@ -403,6 +410,7 @@ static void free_scene(PerDevice& p) {
     if (p.scene.nodes) (void)hipFree(p.scene.nodes);
     if (p.scene.leafs) (void)hipFree(p.scene.leafs);
     if (p.scene.walk) (void)hipFree(p.scene.walk);
+    if (p.scene.walk_ref) (void)hipFree(p.scene.walk_ref);
     if (p.scene.slot_node) (void)hipFree(p.scene.slot_node);
     if (p.scene.node_slot) (void)hipFree(p.scene.node_slot);
     if (p.scene.pairs) (void)hipFree(p.scene.pairs);
@@ -465,7 +473,8 @@ static int plan_order(const rt_ctx* ctx, PerDevice& p, TraceArgs& a, const rt_ca
     // branch of the cooperative-tail kernel), and for the fused launch
     // (heavy_stream 2) the default walk 2, which that launch runs.  Otherwise
     // a launch uses the learned order alone (and reports no heavy work).
-    const bool splittable = a.coop_lanes > 0 && a.ext == 0 && (ctx->heavy_stream != 2 || a.walk == 2);
+    const bool splittable = a.coop_lanes > 0 && a.ext == 0 && (ctx->heavy_stream != 2 || a.walk == 2) &&
+                            a.scene.n_layouts == 0;   // accel: no frontier walk for heavy work
     auto use = [&](const PerDevice::Order& o) -> int {
         a.tile_order = o.d_order;
         if (!splittable) return RT_OK;
@@ -756,22 +765,27 @@ static int learn_order(const rt_ctx* ctx, PerDevice& p, const TraceArgs& a, hipS
 // wave_tile -1: config 5 (112 MB of records, 4K) runs 16x4 tiles in 7.83-7.89
 // ms per frame against 8.07-8.10 for 8x8; config 3 (6 MB, 1080p) runs 8x8 in
 // 0.2942-0.2954 against 0.2965-0.2987 (profiles/r04/r4aa, r4ab).
+// The records one ray walks: the reference's walk records, or one accel layout.
+static size_t walk_bytes(const PerDevice& p) {
+    return (size_t)(p.scene.n_layouts ? p.scene.layout_slots : p.scene.end2) * 32;
+}
+
 static int wave_tile_of(const rt_ctx* ctx, const PerDevice& p) {
     if (ctx->wave_tile >= 0) return ctx->wave_tile;
-    return (size_t)p.scene.end2 * 32 > kWin32Bytes ? 1 : 0;
+    return walk_bytes(p) > kWin32Bytes ? 1 : 0;
 }
 
 static int coop_window_of(const rt_ctx* ctx, const PerDevice& p) {
     if (ctx->coop_window) return ctx->coop_window;
-    return (size_t)p.scene.end2 * 32 > kWin32Bytes ? 32 : 64;
+    return walk_bytes(p) > kWin32Bytes ? 32 : 64;
 }
 
 static int set_schedule(const rt_ctx* ctx, PerDevice& p, TraceArgs& a, const rt_camera_ubo* cam,
                         const std::vector<int>* bands = nullptr) {
     a.wave_tile = wave_tile_of(ctx, p);
     a.coop_lanes = ctx->coop_lanes;
-    a.walk = ctx->walk;
-    a.coop_walk = ctx->coop_walk;
+    a.walk = p.scene.n_layouts ? 2 : ctx->walk;          // accel: the walk-2 records only
+    a.coop_walk = p.scene.n_layouts ? 0 : ctx->coop_walk;
     a.coop_win = coop_window_of(ctx, p);
     a.block_waves = ctx->block_waves;
     a.ext = ctx->ext;
@@ -941,6 +955,10 @@ int rt_create(const int* device_ids, int n_devices, rt_ctx** out) {
         if (q > 0) ctx->hw_queues = q;
     }
     if (const char* v = std::getenv("RTAMD_COOP_WALK")) ctx->coop_walk = std::atoi(v) ? 1 : 0;
+    if (const char* v = std::getenv("RTAMD_ACCEL")) {
+        const int k = std::atoi(v);
+        ctx->accel = k == 1 || k == 8 ? k : 0;
+    }
     if (const char* v = std::getenv("RTAMD_HEAVY_FIRST")) ctx->heavy_first = std::atoi(v) ? 1 : 0;
     if (const char* v = std::getenv("RTAMD_HEAVY_TILES")) ctx->heavy_tiles = std::max(-1, std::atoi(v));
     if (const char* v = std::getenv("RTAMD_LEARN_COST")) ctx->learn_cost = std::atoi(v) ? 1 : 0;
@@ -1125,6 +1143,21 @@ int rt_upload_scene(rt_ctx* ctx, const void* vertices, size_t vertex_bytes,
         walk[w + 2] = make_float4(P0.y, P0.z, P1.x, P1.y);                   // v0.yz, e1.xy
         walk[w + 3] = make_float4(P1.z, P2.x, P2.y, P2.z);                   // e1.z, e2
     }
+    // Option accel: the binned-SAH records (accel_build.h), built once for
+    // every device; the reference's walk records above stay beside them for
+    // the fallback, and the node-indexed arrays (walk 0, the frontier walk of
+    // heavy pixels) are not needed.
+    AccelHost ah;
+    if (ctx->accel) {
+        std::string msg;
+        if (accel_build(vertices, vertex_bytes, materials, material_bytes, bvh_nodes, bvh_bytes, ctx->accel, 0, &ah,
+                        &msg)) {
+            free_host_scene(&hs);
+            set_error("rt_upload_scene: %s", msg.c_str());
+            return RT_ERR_BAD_SCENE;
+        }
+    }
+    const bool acc = ctx->accel != 0;
     ctx->has_scene = false;
     for (PerDevice& p : ctx->dev) {
         RT_HIP_CHECK(hipSetDevice(p.device));
@@ -1148,25 +1181,45 @@ int rt_upload_scene(rt_ctx* ctx, const void* vertices, size_t vertex_bytes,
         const size_t lb = sizeof(float4) * (3 * nn + 1);
         const size_t pb = sizeof(float4) * 4 * (size_t)(hs.n_nodes ? hs.n_nodes : 1);
         const size_t mb = sizeof(float4) * (size_t)(hs.n_tris ? hs.n_tris : 1);
-        hipError_t e = hipMalloc(&s.nodes, nb);
-        if (e == hipSuccess) e = hipMalloc(&s.leafs, lb);
-        if (e == hipSuccess) e = hipMalloc(&s.pairs, pb);
-        if (e == hipSuccess) e = hipMemset(s.nodes + 2 * nn, 0, 2 * sizeof(float4));
-        if (e == hipSuccess) e = hipMemset(s.leafs + 3 * nn, 0, sizeof(float4));
-        s.end2 = (int)nslot;
-        s.padded = n_pads > 0 ? 1 : 0;
-        if (e == hipSuccess) e = hipMalloc(&s.walk, walk.size() * sizeof(float4));
-        if (e == hipSuccess) e = hipMalloc(&s.slot_node, slot_node.size() * sizeof(int));
-        if (e == hipSuccess) e = hipMalloc(&s.node_slot, slot.size() * sizeof(int));
-        if (e == hipSuccess) e = hipMemcpy(s.node_slot, slot.data(), slot.size() * sizeof(int), hipMemcpyHostToDevice);
-        if (e == hipSuccess) e = hipMemcpy(s.walk, walk.data(), walk.size() * sizeof(float4), hipMemcpyHostToDevice);
-        if (e == hipSuccess)
-            e = hipMemcpy(s.slot_node, slot_node.data(), slot_node.size() * sizeof(int), hipMemcpyHostToDevice);
+        hipError_t e = hipSuccess;
+        if (acc) {
+            s.n_layouts = ah.n_layouts;
+            s.layout_slots = ah.slots;
+            s.end = ah.slots;
+            s.end2 = ah.n_layouts * ah.slots;
+            s.root_leaf = ah.root_leaf;
+            s.end2_ref = (int)nslot;
+            s.ref_padded = n_pads > 0 ? 1 : 0;
+            e = hipMalloc(&s.walk, ah.rec.size() * sizeof(uint32_t));
+            if (e == hipSuccess) e = hipMalloc(&s.walk_ref, walk.size() * sizeof(float4));
+            if (e == hipSuccess)
+                e = hipMemcpy(s.walk, ah.rec.data(), ah.rec.size() * sizeof(uint32_t), hipMemcpyHostToDevice);
+            if (e == hipSuccess)
+                e = hipMemcpy(s.walk_ref, walk.data(), walk.size() * sizeof(float4), hipMemcpyHostToDevice);
+        } else {
+            e = hipMalloc(&s.nodes, nb);
+            if (e == hipSuccess) e = hipMalloc(&s.leafs, lb);
+            if (e == hipSuccess) e = hipMalloc(&s.pairs, pb);
+            if (e == hipSuccess) e = hipMemset(s.nodes + 2 * nn, 0, 2 * sizeof(float4));
+            if (e == hipSuccess) e = hipMemset(s.leafs + 3 * nn, 0, sizeof(float4));
+            s.end2 = (int)nslot;
+            s.padded = n_pads > 0 ? 1 : 0;
+            if (e == hipSuccess) e = hipMalloc(&s.walk, walk.size() * sizeof(float4));
+            if (e == hipSuccess) e = hipMalloc(&s.slot_node, slot_node.size() * sizeof(int));
+            if (e == hipSuccess) e = hipMalloc(&s.node_slot, slot.size() * sizeof(int));
+            if (e == hipSuccess)
+                e = hipMemcpy(s.node_slot, slot.data(), slot.size() * sizeof(int), hipMemcpyHostToDevice);
+            if (e == hipSuccess) e = hipMemcpy(s.walk, walk.data(), walk.size() * sizeof(float4), hipMemcpyHostToDevice);
+            if (e == hipSuccess)
+                e = hipMemcpy(s.slot_node, slot_node.data(), slot_node.size() * sizeof(int), hipMemcpyHostToDevice);
+            if (e == hipSuccess && hs.n_nodes)
+                e = hipMemcpy(s.nodes, hs.nodes, nb - 2 * sizeof(float4), hipMemcpyHostToDevice);
+            if (e == hipSuccess && hs.n_nodes)
+                e = hipMemcpy(s.leafs, hs.leafs, lb - sizeof(float4), hipMemcpyHostToDevice);
+            if (e == hipSuccess && hs.n_nodes) e = hipMemcpy(s.pairs, hs.pairs, pb, hipMemcpyHostToDevice);
+        }
         if (e == hipSuccess) e = hipMalloc(&s.norms, kShadeStride * mb);
         if (e == hipSuccess) s.mats = s.norms + 1;
-        if (e == hipSuccess && hs.n_nodes) e = hipMemcpy(s.nodes, hs.nodes, nb - 2 * sizeof(float4), hipMemcpyHostToDevice);
-        if (e == hipSuccess && hs.n_nodes) e = hipMemcpy(s.leafs, hs.leafs, lb - sizeof(float4), hipMemcpyHostToDevice);
-        if (e == hipSuccess && hs.n_nodes) e = hipMemcpy(s.pairs, hs.pairs, pb, hipMemcpyHostToDevice);
         if (e == hipSuccess && hs.n_tris)
             e = hipMemcpy2D(s.norms, kShadeStride * sizeof(float4), hs.norms, sizeof(float4), sizeof(float4),
                             (size_t)hs.n_tris, hipMemcpyHostToDevice);
@@ -1823,6 +1876,8 @@ int rt_set_option(rt_ctx* ctx, const char* name, int64_t value) {
         ctx->learn_device = (int)value;
     } else if (std::strcmp(name, "leaf_align") == 0 && value >= 0 && value <= 2) {
         ctx->leaf_align = (int)value;                   // takes effect at the next rt_upload_scene
+    } else if (std::strcmp(name, "accel") == 0 && (value == 0 || value == 1 || value == 8)) {
+        ctx->accel = (int)value;                        // takes effect at the next rt_upload_scene
     } else if (std::strcmp(name, "heavy_stream") == 0 && value >= 0 && value <= 2) {
         ctx->heavy_stream = (int)value;
     } else if (std::strcmp(name, "graph") == 0 && (value == 0 || value == 1)) {
@@ -1860,6 +1915,8 @@ int rt_get_option(rt_ctx* ctx, const char* name, int64_t* value) {
     else if (std::strcmp(name, "learn_alone") == 0) *value = ctx->learn_alone;
     else if (std::strcmp(name, "learn_device") == 0) *value = ctx->learn_device;
     else if (std::strcmp(name, "leaf_align") == 0) *value = ctx->leaf_align;
+    else if (std::strcmp(name, "accel") == 0) *value = ctx->accel;
+    else if (std::strcmp(name, "accel_used") == 0) *value = ctx->dev.empty() ? 0 : ctx->dev[0].scene.n_layouts;
     else if (std::strcmp(name, "leaf_align_used") == 0) *value = ctx->dev.empty() ? 0 : ctx->dev[0].scene.padded;
     else if (std::strcmp(name, "heavy_factor") == 0) *value = ctx->heavy_factor;
     else if (std::strcmp(name, "concurrent_launches") == 0) *value = ctx->concurrent_launches;
@@ -1892,6 +1949,30 @@ int rt_diag_copy(rt_ctx* ctx, void* dst, size_t cap_words, size_t* n_words) {
         RT_HIP_CHECK(hipDeviceSynchronize());
         RT_HIP_CHECK(hipMemcpy(dst, p.d_diag, std::min(cap_words, p.diag_used) * 8, hipMemcpyDeviceToHost));
     }
+    return RT_OK;
+}
+
+int rt_accel_records(const void* vertices, size_t vertex_bytes, const void* materials, size_t material_bytes,
+                     const void* bvh_nodes, size_t bvh_bytes, int n_layouts, uint32_t* out_words, size_t cap_words,
+                     size_t* n_words, int32_t info[6]) {
+    HostScene hs;
+    const char* err = nullptr;
+    int rc = build_host_scene(vertices, vertex_bytes, materials, material_bytes, bvh_nodes, bvh_bytes, &hs, &err);
+    if (rc != RT_OK) { set_error("rt_accel_records: %s", err); return rc; }
+    free_host_scene(&hs);
+    AccelHost ah;
+    std::string msg;
+    if (accel_build(vertices, vertex_bytes, materials, material_bytes, bvh_nodes, bvh_bytes, n_layouts, 0, &ah,
+                    &msg)) {
+        set_error("rt_accel_records: %s", msg.c_str());
+        return n_layouts == 1 || n_layouts == 8 ? RT_ERR_BAD_SCENE : RT_ERR_INVALID_ARG;
+    }
+    if (n_words) *n_words = ah.rec.size();
+    if (info) {
+        info[0] = ah.n_layouts; info[1] = ah.slots; info[2] = ah.root_leaf;
+        info[3] = ah.n_prims; info[4] = ah.n_inputs; info[5] = ah.depth;
+    }
+    if (out_words) std::memcpy(out_words, ah.rec.data(), std::min(cap_words, ah.rec.size()) * sizeof(uint32_t));
     return RT_OK;
 }
 

@@ -352,6 +352,20 @@ __device__ __forceinline__ float lane_f(float v, int k) {
     return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), k));
 }
 
+// Option accel's rules (accel_build.h).  A box is entered when
+// t_enter <= closest_t * (1 + 2^-10) + 2^-10: every box holding a triangle
+// that ties or beats closest_t is entered, even where rounding puts the
+// triangle's t a little before its box's t_enter.  A triangle is taken on
+// t < closest_t, or on a tie with a lower flattened index (the reference
+// visits leaves in flattened-index order and keeps the first hit at a given
+// t).  oracle/rt_accel_model.c states the same arithmetic.
+constexpr float kRelax = 1.0f + 1.0f / 1024.0f;
+constexpr float kRelaxAbs = 1.0f / 1024.0f;
+__device__ __forceinline__ bool accel_enter(float te, float closest) { return te <= closest * kRelax + kRelaxAbs; }
+__device__ __forceinline__ bool accel_take(float t, int tri, float closest, int hit) {
+    return t < closest || (t == closest && tri < hit);
+}
+
 // ------------------------------------------------------------ cooperative walk --
 #ifndef RT_CHAIN
 // The lockstep walk's next records: 2 = buffer loads whose address is one
@@ -407,10 +421,12 @@ __device__ __forceinline__ float4 wbuf(__amdgpu_buffer_rsrc_t r, int slot, int o
 // lines (tools/layout_model.py); half a window costs ~22% more windows there and
 // fetches ~35% fewer lines.
 // PAD: the records may hold pad slots (leaf_align; the kernel's kFeatPad).
-template <bool COUNT, int WIN = 64, bool PAD = true>
+// ACC: option accel's records and rules (accel_enter / accel_take); `incons`
+// tracks whether the hit lies before its own box's t_enter.
+template <bool COUNT, int WIN = 64, bool PAD = true, bool ACC = false>
 __device__ __forceinline__ int coop_walk(const float4* __restrict__ walk, int end, int n, V3 o, V3 d, V3 inv,
                                          float& closest, int& hit, unsigned long long& c_node,
-                                         unsigned long long& c_tri) {
+                                         unsigned long long& c_tri, bool& incons) {
     const int lane = threadIdx.x & 63;
     int windows = 0;
 #if RT_COOP_BUF
@@ -466,12 +482,12 @@ __device__ __forceinline__ int coop_walk(const float4* __restrict__ walk, int en
                 sk = lf ? j + 2 : (int)(aw & 0x7FFFFFFFu);
             }
             tri = (int)(aw & 0x1FFFFFFFu);
-            if (lf && ind && te < closest && (!RT_COOP_DPP || lane < WIN - 1))
+            if (lf && ind && (ACC ? accel_enter(te, closest) : te < closest) && (!RT_COOP_DPP || lane < WIN - 1))
                 tv = tri_test(make_float4(B.w, Q0.x, Q0.y, 0.f), make_float4(Q0.z, Q0.w, Q1.x, 0.f),
                               make_float4(Q1.y, Q1.z, Q1.w, 0.f), o, d, tt);
         }
-        uint64_t H = __ballot(ind && te < closest);
-        uint64_t T = __ballot(tv && tt < closest);
+        uint64_t H = __ballot(ind && (ACC ? accel_enter(te, closest) : te < closest));
+        uint64_t T = __ballot(tv && (ACC ? accel_take(tt, tri, closest, hit) : tt < closest));
         const uint64_t Lf = __ballot(lf);
         const uint64_t Pd = PAD ? __ballot(pd) : 0ull;              // a pad slot follows (leaf alignment)
         int lim = min(WIN, end - n);
@@ -486,8 +502,9 @@ __device__ __forceinline__ int coop_walk(const float4* __restrict__ walk, int en
                     if ((T >> k) & 1ull) {
                         closest = lane_f(tt, k);
                         hit = lane_i(tri, k);
-                        H = __ballot(ind && te < closest);
-                        T = __ballot(tv && tt < closest);
+                        if (ACC) incons = closest < lane_f(te, k);
+                        H = __ballot(ind && (ACC ? accel_enter(te, closest) : te < closest));
+                        T = __ballot(tv && (ACC ? accel_take(tt, tri, closest, hit) : tt < closest));
                     }
                 }
                 if (PAD)
@@ -705,6 +722,8 @@ constexpr int kFeatFused = 64;    // heavy tiles in the same launch: workgroups 
 constexpr int kFeatWin32 = 128;   // cooperative windows of 32 slots (option coop_window), else 64
 constexpr int kFeatPad = 256;     // the production kernels (cooperative tail, no extensions) on records
                                   //   with pad slots (leaf_align); every other variant always reads pad bits
+constexpr int kFeatAccel = 512;   // option accel: the accel records and rules, packed records, the
+                                  //   reference-order fallback
 constexpr unsigned kHeavyLaneMark = kLearnHeavyMark;   // rt_internal.h
 
 // One pixel of a heavy tile, the whole wave on it (option heavy_fused, the
@@ -787,7 +806,8 @@ void trace_simple(TraceArgs a) {
     // extensions or frontier tail) read them only when built with kFeatPad, so
     // scenes with packed records run the packed code; every other variant
     // reads them always.
-    constexpr bool PAD = (FEAT & kFeatPad) || (FEAT & (kFeatExt | kFeatFrontier)) || !(FEAT & kFeatCoopTail);
+    constexpr bool ACC = (FEAT & kFeatAccel) != 0;
+    constexpr bool PAD = !ACC && ((FEAT & kFeatPad) || (FEAT & (kFeatExt | kFeatFrontier)) || !(FEAT & kFeatCoopTail));
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
     // frontier_walk's per-wave frontiers (kFCap entries per wave; dynamic LDS,
@@ -828,6 +848,12 @@ void trace_simple(TraceArgs a) {
             if ((FEAT & kFeatFused) && a.tile_mask) skip_lanes = a.tile_mask[t];
             if (FEAT & kFeatFused) {
                 rec_id = a.n_heavy_px + t;
+                tile_id = t;
+            } else if (DIAG && a.diag_lane && a.split_n == 0) {
+                // a learning launch in a reused order without heavy pixels (a
+                // schedule that does not split them out): records by tile too,
+                // as rt_learn.hip reads them
+                rec_id = t;
                 tile_id = t;
             }
         }
@@ -903,6 +929,13 @@ void trace_simple(TraceArgs a) {
         // The walk's position: n = the next node the reference would visit
         // (walk 2: its slot in DevScene::walk; walk 0: its node index).
         int n = 0;
+        int lend = wend;                  // accel: the end of this ray's layout
+        bool incons = false;              // accel: the hit lies before its own box's t_enter
+        if (ACC && a.scene.n_layouts == 8) {
+            n = ((__float_as_uint(d.x) >> 31) | ((__float_as_uint(d.y) >> 31) << 1) |
+                 ((__float_as_uint(d.z) >> 31) << 2)) * a.scene.layout_slots;
+            lend = n + a.scene.layout_slots;
+        }
         bool nleaf = a.scene.root_leaf != 0;
         bool walking = alive && end > 0;
         if (COUNT && alive) {
@@ -941,7 +974,7 @@ void trace_simple(TraceArgs a) {
                     float te;
                     bool ind;
                     slab(A, B, o, inv, te, ind);
-                    const bool hb = ind && te < closest;
+                    const bool hb = ind && (ACC ? accel_enter(te, closest) : te < closest);
                     const uint32_t aw = __float_as_uint(A.w), bw = __float_as_uint(B.w);
                     // a leaf's next node is its successor, two slots on, whether it
                     // is hit or not (its skip); an internal node's left child is
@@ -987,12 +1020,14 @@ void trace_simple(TraceArgs a) {
                         if (COUNT) ++c_tri;
                         float t;
                         if (tri_test(make_float4(v0x, Q0.x, Q0.y, 0.f), make_float4(Q0.z, Q0.w, Q1.x, 0.f),
-                                     make_float4(Q1.y, Q1.z, Q1.w, 0.f), o, d, t) && t < closest) {
+                                     make_float4(Q1.y, Q1.z, Q1.w, 0.f), o, d, t) &&
+                            (ACC ? accel_take(t, (int)(aw & kTri), closest, hit) : t < closest)) {
                             closest = t;
                             hit = (int)(aw & kTri);
+                            if (ACC) incons = t < te;
                         }
                     }
-                    if (nl && nxt < wend) {
+                    if (nl && nxt < (ACC ? lend : wend)) {
 #if RT_CHAIN >= 2
                         Q0 = wbuf(wrs, nxt, 32);
                         Q1 = wbuf(wrs, nxt, 48);
@@ -1004,7 +1039,7 @@ void trace_simple(TraceArgs a) {
                     n = nxt;
                     nleaf = nl;
                 }
-                walking = n < wend;
+                walking = n < (ACC ? lend : wend);
                 if ((FEAT & kFeatCoopTail) && __popcll(__ballot(walking)) <= coop_lanes) break;
             }
         }
@@ -1022,6 +1057,7 @@ void trace_simple(TraceArgs a) {
                 const V3 bi = {lane_f(inv.x, L), lane_f(inv.y, L), lane_f(inv.z, L)};
                 float bc = lane_f(closest, L);
                 int bh = lane_i(hit, L);
+                bool bx = ACC && lane_i((int)incons, L) != 0;
                 unsigned long long cn = 0, ct = 0;   // wave-uniform: counted once, by lane L
                 const int start = n;
                 int nw = 0;
@@ -1036,13 +1072,43 @@ void trace_simple(TraceArgs a) {
                     // the windows walk slots of the walk-2 records (walk 0 hands over a
                     // node index: its slot first)
                     const int ws = WALK == 2 ? lane_i(start, L) : a.scene.node_slot[lane_i(start, L)];
-                    nw = coop_walk<COUNT, (FEAT & kFeatWin32) ? 32 : 64, PAD>(a.scene.walk, a.scene.end2, ws, bo,
-                                                                                  bd, bi, bc, bh, cn, ct);
+                    nw = coop_walk<COUNT, (FEAT & kFeatWin32) ? 32 : 64, PAD, ACC>(
+                        a.scene.walk, ACC ? lane_i(lend, L) : a.scene.end2, ws, bo, bd, bi, bc, bh, cn, ct, bx);
                 }
                 if (DIAG) {
                     d_windows += nw;
                     if (lane == L) d_lane_windows += nw;
                 }
+                if (lane == L) {
+                    closest = bc;
+                    hit = bh;
+                    if (ACC) incons = bx;
+                    if (COUNT) {
+                        c_node += cn;
+                        c_tri += ct;
+                    }
+                }
+            }
+            if (DIAG && tc0) d_coop_t += wall_clock64() - tc0;
+        }
+        if (ACC) {
+            // The fallback: a hit before its own box's t_enter
+            // is the one case where the reference's result depends on its
+            // visit order; such a segment is walked again, in the reference's
+            // order over the reference's records, by the whole wave.
+            uint64_t redo = __ballot(alive && hit >= 0 && incons);
+            while (redo != 0) {
+                const int L = __ffsll((long long)redo) - 1;
+                redo &= redo - 1;
+                const V3 bo = {lane_f(o.x, L), lane_f(o.y, L), lane_f(o.z, L)};
+                const V3 bd = {lane_f(d.x, L), lane_f(d.y, L), lane_f(d.z, L)};
+                const V3 bi = {lane_f(inv.x, L), lane_f(inv.y, L), lane_f(inv.z, L)};
+                float bc = kTMax;
+                int bh = -1;
+                bool bx = false;
+                unsigned long long cn = 1, ct = 0;   // the reference walk's root visit
+                coop_walk<COUNT, (FEAT & kFeatWin32) ? 32 : 64, true, false>(a.scene.walk_ref, a.scene.end2_ref, 0,
+                                                                             bo, bd, bi, bc, bh, cn, ct, bx);
                 if (lane == L) {
                     closest = bc;
                     hit = bh;
@@ -1052,7 +1118,6 @@ void trace_simple(TraceArgs a) {
                     }
                 }
             }
-            if (DIAG && tc0) d_coop_t += wall_clock64() - tc0;
         }
         if ((FEAT & kFeatExt) && alive && a.scene.n_spheres > 0)
             sphere_tests(a.scene.spheres, a.scene.n_spheres, o, d, closest, hit);   // extension: spheres
@@ -1154,6 +1219,10 @@ hipError_t launch_trace(const TraceArgs& a, hipStream_t stream, int* kernels) {
     TraceArgs ao = a;
     ao.tiles_y = tiles_y;
     bool join = false;
+    if (a.scene.n_layouts > 0 && (a.n_heavy_px > 0 || a.heavy_tiles > 0 || a.walk != 2)) {
+        set_error("accel launch with heavy tiles / pixels or walk %d", a.walk);   // plan_order never asks for it
+        return hipErrorInvalidValue;
+    }
     if (a.tile_order) {      // heavy-first: a 1-D grid over the ordered tiles
         ao.tiles_x = (int)grid.x;
         ao.split_n = 0;
@@ -1215,7 +1284,18 @@ hipError_t launch_trace(const TraceArgs& a, hipStream_t stream, int* kernels) {
     if (a.diag) hipLaunchKernelGGL((trace_simple<false, true, F, W>), grid, block, ((F) & kFeatFrontier) ? shm_f : 0, stream, ao);           \
     else if (a.counters) hipLaunchKernelGGL((trace_simple<true, false, F, W>), grid, block, ((F) & kFeatFrontier) ? shm_f : 0, stream, ao); \
     else hipLaunchKernelGGL((trace_simple<false, false, F, W>), grid, block, ((F) & kFeatFrontier) ? shm_f : 0, stream, ao);
-    if (a.walk == 2) {
+    if (a.scene.n_layouts > 0) {
+        // option accel (walk 2 records; the launcher never splits heavy tiles
+        // or pixels out of an accel launch, and there is no frontier tail)
+        switch (feat & ~kFeatFrontier) {
+            case kFeatCoopTail:
+                if (a.coop_win == 32) RT_SIMPLE(kFeatCoopTail | kFeatAccel | kFeatWin32, 2)
+                else RT_SIMPLE(kFeatCoopTail | kFeatAccel, 2)
+                break;
+            case 0: RT_SIMPLE(kFeatAccel, 2) break;
+            default: RT_SIMPLE(kFeatCoopTail | kFeatExt | kFeatAccel, 2) break;
+        }
+    } else if (a.walk == 2) {
         switch (feat) {
             case kFeatCoopTail:
                 switch (big) {

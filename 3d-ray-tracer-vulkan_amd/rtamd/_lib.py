@@ -131,6 +131,8 @@ def lib() -> C.CDLL:
                 "rt_render_async": (i32, [vp, C.POINTER(CameraUBO), i32, i32, i32, vp, C.POINTER(u64)]),
                 "rt_render_wait": (i32, [vp, u64]),
                 "rt_render_poll": (i32, [vp, u64, C.POINTER(i32)]),
+                "rt_accel_records": (i32, [vp, sz, vp, sz, vp, sz, i32, C.POINTER(C.c_uint32), sz, C.POINTER(sz),
+                                           C.POINTER(C.c_int32)]),
             }
             for name, (res, args) in sig.items():
                 f = getattr(L, name)
@@ -144,3 +146,23 @@ def check(rc: int) -> None:
     if rc != RT_OK:
         msg = lib().rt_last_error()
         raise RtError(rc, msg.decode() if msg else "")
+
+
+def accel_records(built, n_layouts: int = 8):
+    """Option accel's records for a BuiltCpuData (rt_accel_records): returns
+    (uint32[slots_total * 8], info dict).  Host-only; no device needed."""
+    import numpy as np
+    L = lib()
+    bufs = [np.ascontiguousarray(np.frombuffer(bytes(x), dtype=np.uint8)) if isinstance(x, (bytes, bytearray))
+            else np.ascontiguousarray(x) for x in (built.model_vertex_data, built.model_material_data,
+                                                   built.flat_bvh_data)]
+    args = []
+    for b in bufs:
+        args += [b.ctypes.data, b.nbytes]
+    n = C.c_size_t(0)
+    info = (C.c_int32 * 6)()
+    check(L.rt_accel_records(*args, n_layouts, None, 0, C.byref(n), info))
+    out = np.zeros(n.value, dtype=np.uint32)
+    check(L.rt_accel_records(*args, n_layouts, out.ctypes.data_as(C.POINTER(C.c_uint32)), out.size, C.byref(n), info))
+    keys = ("n_layouts", "slots", "root_leaf", "n_prims", "n_inputs", "depth")
+    return out, dict(zip(keys, list(info)))

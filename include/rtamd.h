@@ -402,6 +402,22 @@ int rt_scene_validate(const void* vertices, size_t vertex_bytes,
                       const void* bvh_nodes, size_t bvh_bytes,
                       size_t* n_nodes, int* max_depth);
 
+/* Option "accel"'s records, built on the host exactly as
+ * rt_upload_scene builds them for a context with accel on (pure host code, no
+ * device): the binned-SAH tree over the reference leaves' (triangle, box)
+ * pairs, n_layouts (1, or 8 = one per ray-direction octant) near-first
+ * preorder layouts in the walk-record format, 8 32-bit words per 32-B slot.
+ * Writes up to cap_words words (out_words may be NULL to size the call) and
+ * *n_words = the words of the records (n_layouts * slots + 2 padding slots);
+ * info (nullable) receives {n_layouts, slots per layout, root is a leaf,
+ * primitives after dropping byte-identical duplicates, reference leaves, tree
+ * depth}.  An analysis and test entry point (oracle/rt_accel_model.c walks
+ * these records on the CPU); a host embedding the backend never needs it. */
+int rt_accel_records(const void* vertices, size_t vertex_bytes,
+                     const void* materials, size_t material_bytes,
+                     const void* bvh_nodes, size_t bvh_bytes, int n_layouts,
+                     uint32_t* out_words, size_t cap_words, size_t* n_words, int32_t info[6]);
+
 /* ----------------------------------------------------------- scene build -- */
 /* Host-side producers of the three buffers, replacing the Java SceneBuilder
  * (SceneBuilder.java:38-118), BVHBuilder (BVHBuilder.java:48-108), BVHFlattener

@@ -10,6 +10,7 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB = os.path.join(HERE, "liboracle.so")
 ENV_LIB = os.path.join(HERE, "liboracle_env.so")     # rt_envelope.c: the Vulkan-envelope study
+ACCEL_LIB = os.path.join(HERE, "liboracle_accel.so") # rt_accel_model.c: option accel's walk on the CPU
 ENV_FMA, ENV_RSQ, ENV_RCP, ENV_ULP, ENV_FTZ = 1, 2, 4, 8, 16   # rt_oracle.c ENV_* bits
 
 
@@ -23,16 +24,28 @@ class Counts(C.Structure):
 
 _lib = None
 _env_lib = None
+_accel_lib = None
 
 
 def build() -> None:
     subprocess.run(["make", "-s", "-C", HERE], check=True)
 
 
-def lib(envelope: bool = False) -> C.CDLL:
+def lib(envelope: bool = False, accel: bool = False) -> C.CDLL:
     """liboracle.so (the contract), or with envelope=True liboracle_env.so
-    (the same oracle with orc_env_set_variant)."""
-    global _lib, _env_lib
+    (the same oracle with orc_env_set_variant), or with accel=True
+    liboracle_accel.so (the oracle walking option accel's records)."""
+    global _lib, _env_lib, _accel_lib
+    if accel:
+        if _accel_lib is None:
+            if not os.path.exists(ACCEL_LIB):
+                build()
+            _accel_lib = _bind(C.CDLL(ACCEL_LIB))
+            _accel_lib.orc_accel_set.restype = C.c_int
+            _accel_lib.orc_accel_set.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int]
+            _accel_lib.orc_accel_fallbacks.restype = C.c_uint64
+            _accel_lib.orc_accel_margin.argtypes = [C.c_float, C.c_float]
+        return _accel_lib
     if envelope:
         if _env_lib is None:
             if not os.path.exists(ENV_LIB):
@@ -63,6 +76,7 @@ def _bind(L: C.CDLL) -> C.CDLL:
                              C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
                              C.c_int, C.c_void_p, C.c_void_p, C.POINTER(Counts), C.c_int]
     L.orc_render_ext.argtypes = L.orc_render.argtypes + [C.c_int, C.c_void_p]
+    L.orc_render_profile.argtypes = L.orc_render.argtypes + [C.c_void_p]
     L.orc_render_spheres.argtypes = L.orc_render_ext.argtypes + [C.c_void_p, C.c_int]
     return L
 
@@ -109,3 +123,57 @@ def render(vertices, materials, nodes, camera_ubo: bytes, width: int, height: in
     if rc != 0:
         raise RuntimeError(f"orc_render failed ({rc})")
     return rgba, rad, c.as_dict()
+
+
+def render_accel(vertices, materials, nodes, camera_ubo: bytes, width: int, height: int, max_bounces: int,
+                 records: np.ndarray, info: dict, tile=None, row_step: int = 1, n_threads: int = 0,
+                 profile: bool = False):
+    """The same frame through option accel's walk (rt_accel_model.c) over
+    `records` / `info` (rtamd._lib.accel_records).  Returns (rgba, radiance,
+    counts[, profile uint32[rows, w, max_bounces]: node visits | tri tests << 20
+    per bounce])."""
+    x0, y0, tw, th = tile if tile is not None else (0, 0, width, height)
+    rows = (th + row_step - 1) // row_step
+    v, vp, vn = _buf(vertices)
+    m, mp, mn = _buf(materials)
+    b, bp, bn = _buf(nodes)
+    rec = np.ascontiguousarray(records, dtype=np.uint32)
+    cam = np.frombuffer(bytes(camera_ubo), dtype=np.uint8).copy()
+    rgba = np.empty((rows, tw, 4), dtype=np.uint8)
+    rad = np.empty((rows, tw, 3), dtype=np.float32)
+    prof = np.zeros((rows, tw, max_bounces), dtype=np.uint32) if profile else None
+    c = Counts()
+    L = lib(accel=True)
+    if L.orc_accel_set(rec.ctypes.data, int(info["n_layouts"]), int(info["slots"]), int(info["root_leaf"])) != 0:
+        raise RuntimeError("orc_accel_set failed")
+    rc = L.orc_render_profile(vp, vn, mp, mn, bp, bn, cam.ctypes.data, width, height, max_bounces,
+                              x0, y0, tw, th, row_step, rgba.ctypes.data, rad.ctypes.data, C.byref(c), n_threads,
+                              prof.ctypes.data if prof is not None else None)
+    if rc != 0:
+        raise RuntimeError(f"orc_render_profile (accel) failed ({rc})")
+    cd = c.as_dict()
+    cd["fallbacks"] = int(L.orc_accel_fallbacks())
+    if profile:
+        return rgba, rad, cd, prof
+    return rgba, rad, cd
+
+
+def render_profile(vertices, materials, nodes, camera_ubo: bytes, width: int, height: int, max_bounces: int,
+                   tile=None, row_step: int = 1, n_threads: int = 0):
+    """orc_render_profile of the contract oracle: (rgba, radiance, counts, profile)."""
+    x0, y0, tw, th = tile if tile is not None else (0, 0, width, height)
+    rows = (th + row_step - 1) // row_step
+    v, vp, vn = _buf(vertices)
+    m, mp, mn = _buf(materials)
+    b, bp, bn = _buf(nodes)
+    cam = np.frombuffer(bytes(camera_ubo), dtype=np.uint8).copy()
+    rgba = np.empty((rows, tw, 4), dtype=np.uint8)
+    rad = np.empty((rows, tw, 3), dtype=np.float32)
+    prof = np.zeros((rows, tw, max_bounces), dtype=np.uint32)
+    c = Counts()
+    rc = lib().orc_render_profile(vp, vn, mp, mn, bp, bn, cam.ctypes.data, width, height, max_bounces,
+                                  x0, y0, tw, th, row_step, rgba.ctypes.data, rad.ctypes.data, C.byref(c),
+                                  n_threads, prof.ctypes.data)
+    if rc != 0:
+        raise RuntimeError(f"orc_render_profile failed ({rc})")
+    return rgba, rad, c.as_dict(), prof

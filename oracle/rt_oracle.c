@@ -279,6 +279,55 @@ static unsigned char unorm8(float c) {
     return c > 0.0f ? (c < 1.0f ? (unsigned char)rintf(c * 255.0f) : 255) : 0;
 }
 
+/* The closest hit of one bounce (:181-210): the reference's DFS with an int
+ * stack[64], left child popped first.  Returns 0, or -1 on stack overflow or
+ * an out-of-range index (where the reference reads out of bounds). */
+static int reference_walk(const scene* s, ray r, float* closest, int* hit_index, vec3* hit_normal,
+                          orc_counts* cnt) {
+    float closest_t = *closest;
+    int hit_triangle_index = *hit_index;
+    int stack[STACK_SIZE];
+    int sp = 0;
+    if (s->n_nodes > 0) stack[sp++] = 0;          /* empty scene: no root to read */
+    while (sp > 0) {                                                       /* :189-210 */
+        int node_index = stack[--sp];
+        if (node_index < 0 || (size_t)node_index >= s->n_nodes) return -1;
+        const unsigned char* nd = s->nodes + (size_t)node_index * 48;
+        vec3 bmin = v3(f32_at(nd, 0), f32_at(nd, 4), f32_at(nd, 8));
+        vec3 bmax = v3(f32_at(nd, 16), f32_at(nd, 20), f32_at(nd, 24));
+        int32_t data = i32_at(nd, 32), count = i32_at(nd, 36);
+        cnt->node_visits++;
+        trace_rec(node_index);
+        if (hit_aabb(r, bmin, bmax, T_MIN, closest_t)) {
+            if (count < 0) {
+                int tri = -(data + 1);
+                if (tri < 0 || (size_t)tri >= s->n_tris || (size_t)tri >= s->n_mats) return -1;
+                vec3 v0 = vertex_pos(s, (size_t)tri * 3 + 0);
+                vec3 v1 = vertex_pos(s, (size_t)tri * 3 + 1);
+                vec3 v2 = vertex_pos(s, (size_t)tri * 3 + 2);
+                vec3 temp_normal;
+                cnt->tri_tests++;
+                if (hit_triangle(r, v0, v1, v2, &closest_t, &temp_normal)) {
+                    hit_triangle_index = tri;
+                    *hit_normal = temp_normal;
+                }
+            } else {
+                if (sp + 2 > STACK_SIZE) return -1;
+                stack[sp++] = count;   /* right */
+                stack[sp++] = data;    /* left  */
+            }
+        }
+    }
+    *closest = closest_t;
+    *hit_index = hit_triangle_index;
+    return 0;
+}
+
+#ifdef ORC_WALK_HOOK
+static int ORC_WALK_HOOK(const scene* s, ray r, float* closest_t, int* hit_index, vec3* hit_normal,
+                         orc_counts* cnt);
+#endif
+
 /* One invocation of main() (:158-237).  Returns 0, or -1 on stack overflow or
  * an out-of-range index (where the reference reads out of bounds). */
 static int shade_pixel(const scene* s, const orc_camera* cam, int W, int H, int max_bounces,
@@ -309,38 +358,12 @@ static int shade_pixel(const scene* s, const orc_camera* cam, int W, int H, int 
         float closest_t = T_MAX;
         int hit_triangle_index = -1;
         vec3 hit_normal = v3(0.0f, 0.0f, 0.0f);
-        int stack[STACK_SIZE];
-        int sp = 0;
-        if (s->n_nodes > 0) stack[sp++] = 0;          /* empty scene: no root to read */
-        while (sp > 0) {                                                       /* :189-210 */
-            int node_index = stack[--sp];
-            if (node_index < 0 || (size_t)node_index >= s->n_nodes) return -1;
-            const unsigned char* nd = s->nodes + (size_t)node_index * 48;
-            vec3 bmin = v3(f32_at(nd, 0), f32_at(nd, 4), f32_at(nd, 8));
-            vec3 bmax = v3(f32_at(nd, 16), f32_at(nd, 20), f32_at(nd, 24));
-            int32_t data = i32_at(nd, 32), count = i32_at(nd, 36);
-            cnt->node_visits++;
-            trace_rec(node_index);
-            if (hit_aabb(r, bmin, bmax, T_MIN, closest_t)) {
-                if (count < 0) {
-                    int tri = -(data + 1);
-                    if (tri < 0 || (size_t)tri >= s->n_tris || (size_t)tri >= s->n_mats) return -1;
-                    vec3 v0 = vertex_pos(s, (size_t)tri * 3 + 0);
-                    vec3 v1 = vertex_pos(s, (size_t)tri * 3 + 1);
-                    vec3 v2 = vertex_pos(s, (size_t)tri * 3 + 2);
-                    vec3 temp_normal;
-                    cnt->tri_tests++;
-                    if (hit_triangle(r, v0, v1, v2, &closest_t, &temp_normal)) {
-                        hit_triangle_index = tri;
-                        hit_normal = temp_normal;
-                    }
-                } else {
-                    if (sp + 2 > STACK_SIZE) return -1;
-                    stack[sp++] = count;   /* right */
-                    stack[sp++] = data;    /* left  */
-                }
-            }
-        }
+#ifdef ORC_WALK_HOOK
+        /* rt_accel_model.c: the accel option's walk instead of the reference's DFS */
+        if (ORC_WALK_HOOK(s, r, &closest_t, &hit_triangle_index, &hit_normal, cnt)) return -1;
+#else
+        if (reference_walk(s, r, &closest_t, &hit_triangle_index, &hit_normal, cnt)) return -1;
+#endif
         if (prof) prof[b] = (uint32_t)(cnt->node_visits - nv0) | ((uint32_t)(cnt->tri_tests - tt0) << 20);
         const unsigned char* hit_mat = hit_triangle_index != -1 ? s->mats + (size_t)hit_triangle_index * 16 : NULL;
         if (ext & ORC_EXT_SPHERES) {

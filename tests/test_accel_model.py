@@ -1,0 +1,178 @@
+"""Option accel on the CPU: the records rt_accel_records builds
+and the accel walk's CPU model (oracle/rt_accel_model.c) against the
+reference-order oracle (oracle/rt_oracle.c).
+
+The accel walk visits a binned-SAH tree near child first, enters a box when
+t_enter <= closest_t and takes a triangle on t < closest_t or on a tie with a
+lower flattened index.  The claim: its frames are the reference's, bit for
+bit, while its node visits differ by design.  tools/accel_study.py measured
+whole frames of configs 1-6 (tests/golden/accel_study.json); these tests
+re-check small cases, tie-heavy scenes and the record format."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def _records(built, n_layouts):
+    from rtamd import _lib
+    return _lib.accel_records(built, n_layouts)
+
+
+def _frames(built, cam, w, h, b, n_layouts, tile=None, row_step=1):
+    from oracle import oracle_lib as O
+    args = (built.model_vertex_data, built.model_material_data, built.flat_bvh_data, cam.ubo_bytes(), w, h, b)
+    ref = O.render(*args, tile=tile, row_step=row_step)
+    rec, info = _records(built, n_layouts)
+    acc = O.render_accel(*args, rec, info, tile=tile, row_step=row_step)
+    return ref, acc
+
+
+def _assert_frames_equal(ref, acc, what=""):
+    (r_rgba, r_rad, r_c), (a_rgba, a_rad, a_c) = ref, acc
+    bad = (r_rgba != a_rgba).any(-1) | (r_rad.view(np.uint32) != a_rad.view(np.uint32)).any(-1)
+    assert not bad.any(), f"{what}: {int(bad.sum())} pixels differ, first at {np.argwhere(bad)[0]}"
+    # the path of every pixel is the reference's: same segments and hits
+    assert a_c["segments"] == r_c["segments"] and a_c["mat_reads"] == r_c["mat_reads"], what
+
+
+def _walk_all(rec, info, o):
+    """Every slot of layout o in walk order with every box entered: the walk
+    must reach each leaf exactly once and end at the layout's end."""
+    s = info["slots"]
+    n, end, leaf = o * s, (o + 1) * s, bool(info["root_leaf"])
+    tris, steps = [], 0
+    while n < end:
+        aw, bw = int(rec[8 * n + 3]), int(rec[8 * n + 7])
+        assert bool((aw >> 30) & 1) == leaf, f"slot {n}: bit 30 disagrees with the L bit that led here"
+        if leaf:
+            tris.append(aw & 0x1FFFFFFF)
+            n, leaf = n + 2, bool(aw >> 31)
+        else:
+            skip = aw & 0x7FFFFFFF
+            assert n < skip <= end
+            n, leaf = n + 1, bool(bw & 1)
+        steps += 1
+        assert steps <= s
+    assert n == end
+    return tris
+
+
+@pytest.mark.parametrize("k", [1, 2, 3])
+def test_record_layouts(k):
+    from rtamd import configs
+    built = configs.get(k).build()
+    for nl in (1, 8):
+        rec, info = _records(built, nl)
+        assert rec.size == 8 * (nl * info["slots"] + 2)
+        assert info["slots"] == 3 * info["n_prims"] - 1
+        first = None
+        for o in range(nl):
+            tris = _walk_all(rec, info, o)
+            assert len(tris) == info["n_prims"] == len(set(tris))
+            if first is None:
+                first = sorted(tris)
+            assert sorted(tris) == first            # every layout holds the same triangles
+        # a flattened triangle dropped as a duplicate is byte-identical to a kept one
+        vb = built.model_vertex_data.view(np.uint8).reshape(-1, 48)
+        kept = {vb[t].tobytes() for t in first}
+        for t in range(built.triangle_count):
+            assert vb[t].tobytes() in kept
+
+
+def test_duplicates_dropped():
+    from rtamd import configs
+    built = configs.config3().build()
+    _, info = _records(built, 1)
+    # 50,000 triangles + plane (2) + cube (12); the reference's one-triangle
+    # nodes flatten to two copies (BVHBuilder.java:60-62): 65,536 leaves
+    assert info["n_inputs"] == 65536 and info["n_prims"] == 50014
+
+
+@pytest.mark.parametrize("nl", [1, 8])
+@pytest.mark.parametrize("k,b,tile,row_step", [(1, 1, None, 1), (2, 2, None, 2), (2, 10, (400, 200, 480, 320), 1),
+                                                 (3, 4, None, 24), (6, 4, None, 40)])
+def test_model_matches_oracle(k, b, tile, row_step, nl):
+    from rtamd import configs
+    cfg = configs.get(k)
+    built = cfg.build()
+    ref, acc = _frames(built, cfg.camera(), cfg.width, cfg.height, b, nl, tile=tile, row_step=row_step)
+    _assert_frames_equal(ref, acc, f"config {k}")
+    # far fewer box tests than the reference's walk (3: 36.8 vs 8.2 per segment)
+    if k >= 3:
+        assert acc[2]["node_visits"] < 0.4 * ref[2]["node_visits"]
+
+
+def _tie_scenes():
+    from rtamd import build_buffers, configs, triangles_of
+    verts, mats = triangles_of(configs.config2().scene)
+    rng = np.random.default_rng(7)
+    out = {}
+    # twins: every triangle twice, the copy in another colour: equal t on every
+    # hit, the lower flattened index must win (the reference's first found)
+    m2 = mats.copy()
+    m2[:, :3] = 1.0 - m2[:, :3]
+    out["twins"] = build_buffers(np.concatenate([verts, verts]), np.concatenate([mats, m2]), 1)
+    out["twins_rev"] = build_buffers(np.concatenate([verts, verts]), np.concatenate([m2, mats]), 3)
+    # an integer grid: coplanar, coincident and axis-aligned faces, shared edges
+    g = rng.integers(-3, 4, size=(300, 3, 3)).astype(np.float64) * 4.0
+    gm = np.concatenate([rng.random((300, 3)), rng.integers(0, 4, (300, 1))], 1).astype(np.float32)
+    out["grid"] = build_buffers(g.reshape(300, 9), gm, 5)
+    # the cube's faces also split along their other diagonal, in other
+    # colours: coincident triangles that cross, ties on half of each face
+    q = verts[2:].reshape(-1, 2, 3, 3)     # face k: triangles (a, b, c) and (a, c, d)
+    a, b, c, d = q[:, 0, 0], q[:, 0, 1], q[:, 0, 2], q[:, 1, 2]
+    other = np.stack([np.stack([a, b, d], 1), np.stack([b, c, d], 1)], 1).reshape(-1, 9)
+    out["cube_both_diagonals"] = build_buffers(np.concatenate([verts, other]),
+                                               np.concatenate([mats, m2[2:]]), 2)
+    return out
+
+
+@pytest.mark.parametrize("nl", [1, 8])
+def test_model_ties(nl):
+    from rtamd import configs
+    for name, built in _tie_scenes().items():
+        for (w, h, b) in [(160, 90, 3), (97, 61, 10)]:
+            cam = configs.Camera.default(w, h)
+            ref, acc = _frames(built, cam, w, h, b, nl)
+            _assert_frames_equal(ref, acc, f"{name} {w}x{h}x{b}")
+
+
+def test_model_tree_independent():
+    """The reference's frame does not depend on its random tree (SURVEY.md §0
+    fact 9), and the accel walk's does not depend on which reference tree its
+    primitives came from."""
+    from rtamd import configs
+    from oracle import oracle_lib as O
+    cfg = configs.config2()
+    cam = cfg.camera()
+    frames = []
+    for seed in (1, 2, 3):
+        built = cfg.build(axis_seed=seed)
+        ref, acc = _frames(built, cam, cfg.width, cfg.height, 2, 1, row_step=3)
+        _assert_frames_equal(ref, acc, f"seed {seed}")
+        frames.append(acc[0])
+    assert all(np.array_equal(frames[0], f) for f in frames[1:])
+
+
+def test_study_claims():
+    with open(os.path.join(HERE, "golden", "accel_study.json")) as f:
+        d = json.load(f)
+    names = {c["config"] for c in d["cases"]}
+    assert {"cfg2_cube_plane_1280x720_b2", "cfg3_50k_1920x1080_b4", "cfg6_fbm_1920x1080_b4",
+            "cfg5_1M_3840x2160_b8"} <= names
+    for c in d["cases"]:
+        for k, e in c["accel"].items():
+            assert e["rgba_px"] == 0 and e["radiance_px"] == 0, (c["config"], k)
+            if k in ("layouts1", "layouts8"):
+                assert e["segments_equal"] and e["mat_reads_equal"]
+                # rare: hits on a face that lies on its box's entry plane (the
+                # cube of configs 1-2 is a large share of those frames)
+                assert e["fallback_segments"] < (1e-2 if c["config"].startswith(("cfg1", "cfg2")) else 1e-3) * \
+                    e["segments"]
+        if c["config"].startswith(("cfg3", "cfg5", "cfg6")):
+            ref = c["reference_seed1"]["visits_per_segment"]
+            assert c["accel"]["layouts1"]["visits_per_segment"] < ref / 3.0

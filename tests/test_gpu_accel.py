@@ -1,0 +1,178 @@
+"""GPU parity of option accel: the binned-SAH tree walked near
+child first through the C ABI, against the reference-order CPU oracle
+(oracle/rt_oracle.c).
+
+Bar: bit-exact RGBA8 and float radiance, and the same segments and material
+reads as the oracle (every path is the reference's); node visits and
+triangle tests equal the accel walk's CPU model (oracle/rt_accel_model.c),
+which walks the same records with the same rules and fallback."""
+import numpy as np
+import pytest
+
+from conftest import has_gpu
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def acc():
+    if not has_gpu():
+        pytest.skip("no GPU")
+    import rtamd
+    r = rtamd.Renderer((0,))
+    yield r
+    r.close()
+
+
+def _oracle(built, cam, w, h, b, **kw):
+    from oracle import oracle_lib
+    return oracle_lib.render(built.model_vertex_data, built.model_material_data, built.flat_bvh_data,
+                             cam.ubo_bytes(), w, h, b, **kw)
+
+
+def _model(built, cam, w, h, b, nl, **kw):
+    from oracle import oracle_lib
+    from rtamd import _lib
+    rec, info = _lib.accel_records(built, nl)
+    return oracle_lib.render_accel(built.model_vertex_data, built.model_material_data, built.flat_bvh_data,
+                                   cam.ubo_bytes(), w, h, b, rec, info, **kw)
+
+
+def _check(rgba, rad, st, ref, model=None, what=""):
+    r_rgba, r_rad, r_c = ref
+    bad = (rgba != r_rgba).any(-1) | (rad.view(np.uint32) != r_rad.view(np.uint32)).any(-1)
+    assert not bad.any(), f"{what}: {int(bad.sum())} pixels differ from the oracle, first {np.argwhere(bad)[:4].tolist()}"
+    if st is not None:
+        assert st["segments"] == r_c["segments"] and st["mat_reads"] == r_c["mat_reads"], (what, st, r_c)
+        if model is not None:
+            m = model[2]
+            assert (st["node_visits"], st["tri_tests"]) == (m["node_visits"], m["tri_tests"]), (what, st, m)
+
+
+def _upload(r, built, nl):
+    r.set_option("accel", nl)
+    r.upload_scene(built)
+    assert r.get_option("accel_used") == nl
+
+
+@pytest.mark.parametrize("nl", [1, 8])
+@pytest.mark.parametrize("k,b", [(1, 1), (2, 2), (2, 10), (3, 4), (6, 4)])
+def test_accel_full_frame(acc, k, b, nl):
+    from rtamd import configs
+    cfg = configs.get(k)
+    built = cfg.build()
+    cam = cfg.camera()
+    _upload(acc, built, nl)
+    ref = _oracle(built, cam, cfg.width, cfg.height, b)
+    model = _model(built, cam, cfg.width, cfg.height, b, nl)
+    for stats in (False, True):                    # the production build, then the counting build
+        rgba, rad, st = acc.render(cam, cfg.width, cfg.height, b, radiance=True, stats=stats)
+        _check(rgba, rad, st, ref, model, f"config {k} b{b} layouts {nl}")
+
+
+@pytest.mark.parametrize("nl", [1, 8])
+def test_accel_config5_strips(acc, nl):
+    """Config 5 (1M triangles, 3840x2160, 8 bounces, all material types):
+    three 64-row strips through rt_render_tile_device."""
+    import torch
+    from rtamd import configs
+    cfg = configs.config5()
+    built = cfg.build()
+    cam = cfg.camera()
+    _upload(acc, built, nl)
+    W, H, B = cfg.width, cfg.height, cfg.max_bounces
+    for y0 in (0, 1000, 1800):
+        tile = (0, y0, W, 64)
+        d_rgba = torch.empty((64, W, 4), dtype=torch.uint8, device="cuda:0")
+        d_rad = torch.empty((64, W, 3), dtype=torch.float32, device="cuda:0")
+        st = acc.render_tile_device(cam, W, H, B, *tile, d_rgba.data_ptr(), d_rad.data_ptr(),
+                                    torch.cuda.current_stream().cuda_stream, stats=True)
+        torch.cuda.synchronize()
+        ref = _oracle(built, cam, W, H, B, tile=tile)
+        model = _model(built, cam, W, H, B, nl, tile=tile)
+        _check(d_rgba.cpu().numpy(), d_rad.cpu().numpy(), st, ref, model, f"config 5 rows {y0}+64")
+
+
+def _tie_scenes():
+    import test_accel_model as M
+    return M._tie_scenes()
+
+
+@pytest.mark.parametrize("nl", [1, 8])
+def test_accel_ties_and_fallback(acc, nl):
+    """Scenes built to tie: every triangle twice in two colours, an integer
+    grid of coplanar and coincident faces, the cube's faces split both ways.
+    Hits on a face whose box starts at the face (rounding puts t before the
+    box's t_enter) take the fallback to the reference's order."""
+    from rtamd import configs
+    for name, built in _tie_scenes().items():
+        _upload(acc, built, nl)
+        for (w, h, b) in [(160, 90, 3), (97, 61, 10)]:
+            cam = configs.Camera.default(w, h)
+            ref = _oracle(built, cam, w, h, b)
+            model = _model(built, cam, w, h, b, nl)
+            rgba, rad, st = acc.render(cam, w, h, b, radiance=True, stats=True)
+            _check(rgba, rad, st, ref, model, f"{name} {w}x{h}x{b}")
+
+
+@pytest.mark.parametrize("opts", [{"coop_lanes": 0}, {"coop_lanes": 8}, {"heavy_first": 0},
+                                  {"wave_tile": 1}, {"wave_tile": 3}, {"coop_window": 32},
+                                  {"block_waves": 4}])
+def test_accel_schedules(acc, opts):
+    """Schedule options change which wave traces a pixel and when, never what
+    it computes."""
+    from rtamd import configs
+    cfg = configs.config3()
+    built = cfg.build()
+    cam = cfg.camera()
+    _upload(acc, built, 1)
+    ref = _oracle(built, cam, cfg.width, cfg.height, cfg.max_bounces, row_step=8)
+    old = {k: acc.get_option(k) for k in opts}
+    try:
+        for k, v in opts.items():
+            acc.set_option(k, v)
+        for _ in range(2):                         # a learning launch, then the learned order
+            rgba, rad, _ = acc.render(cam, cfg.width, cfg.height, cfg.max_bounces, radiance=True)
+            _check(rgba[::8], rad[::8], None, ref, None, str(opts))
+    finally:
+        for k, v in old.items():
+            acc.set_option(k, v)
+
+
+def test_accel_empty_and_tiny_scenes(acc):
+    from rtamd import build_buffers, configs, triangles_of
+    verts, mats = triangles_of(configs.config2().scene)
+    for n in (0, 1, 2, 3):
+        built = build_buffers(verts[:n], mats[:n])
+        for nl in (1, 8):
+            _upload(acc, built, nl)
+            for (w, h, b) in [(37, 23, 3), (1, 1, 1)]:
+                cam = configs.Camera.default(w, h)
+                ref = _oracle(built, cam, w, h, b)
+                rgba, rad, st = acc.render(cam, w, h, b, radiance=True, stats=True)
+                _check(rgba, rad, st, ref, _model(built, cam, w, h, b, nl), f"{n} triangles")
+
+
+def test_accel_extensions(acc):
+    """The non-reference extensions run over the accel walk too (sky toggle,
+    emissive, spheres); frames equal the oracle's extension build."""
+    from oracle import oracle_lib
+    from rtamd import configs
+    cfg = configs.config3()
+    built = cfg.build()
+    _upload(acc, built, 1)
+    w, h, b = 320, 180, 4
+    cam = configs.Camera.default(w, h)
+    spheres = np.array([[0.0, 5.0, 20.0, 6.0, 0.9, 0.9, 0.9, 1.0],
+                        [-15.0, 2.0, 0.0, 4.0, 5.0, 5.0, 5.0, 3.0]], np.float32)
+    acc.upload_spheres(spheres)
+    ext = oracle_lib.EXT_SKY_TOGGLE | oracle_lib.EXT_EMISSIVE | oracle_lib.EXT_SPHERES
+    try:
+        acc.set_option("extensions", ext)
+        rgba, rad, _ = acc.render(cam, w, h, b, radiance=True)
+        ref = oracle_lib.render(built.model_vertex_data, built.model_material_data, built.flat_bvh_data,
+                                cam.ubo_bytes(), w, h, b, ext=ext, spheres=spheres)
+        _check(rgba, rad, None, ref, None, "extensions")
+    finally:
+        acc.set_option("extensions", 0)
+        acc.upload_spheres(np.zeros((0, 8), np.float32))
