@@ -223,9 +223,12 @@ static constexpr int kMaxSlots = 8;   // rt_render_async frame slots per device
 #ifndef RT_LEAF_ALIGN
 #define RT_LEAF_ALIGN 2
 #endif
-// Option accel's default.
+// Option accel's default: the binned-SAH tree in 8 octant
+// layouts.  Config 3 0.1279-0.1288 ms per frame against 0.2962-0.2964 for the
+// reference's tree and order, config 5 1.24-1.25 against 7.84 ms, config 6
+// 0.140 against 0.342 (profiles/r05/r5a, r5b); 1 layout: 0.1365, 1.40, 0.148.
 #ifndef RT_ACCEL
-#define RT_ACCEL 0
+#define RT_ACCEL 8
 #endif
 
 struct PerDevice {
@@ -359,7 +362,9 @@ struct rt_ctx {
     int  wave_tile = -1;           // 8x8 / 16x4 / 32x2 / 64x1 pixels per wave (0-3); -1 (default) = 16x4
                                    //   when the walk records exceed kWin32Bytes, else 8x8
     int  diag = 0;                 // record per-wave timestamps
-    int  coop_lanes = 1;           // cooperative tail once <= this many lanes walk (0 = off)
+    int  coop_lanes = -1;          // cooperative tail once <= this many lanes walk (0 = off); -1 (default) =
+                                   //   1 on the reference-order walk, 0 on the accel walk (its walks are
+                                   //   short: config 3 0.1253-0.1254 vs 0.1279-0.1288 ms, profiles/r05/r5b)
     int  ext = 0;                  // non-reference extensions (kExt* bits), off by default
     int  walk = 2;                 // 0 = node per step, 2 = node per step, software-pipelined over the
                                    //   compact records (fastest measured)
@@ -783,7 +788,7 @@ static int coop_window_of(const rt_ctx* ctx, const PerDevice& p) {
 static int set_schedule(const rt_ctx* ctx, PerDevice& p, TraceArgs& a, const rt_camera_ubo* cam,
                         const std::vector<int>* bands = nullptr) {
     a.wave_tile = wave_tile_of(ctx, p);
-    a.coop_lanes = ctx->coop_lanes;
+    a.coop_lanes = ctx->coop_lanes >= 0 ? ctx->coop_lanes : (p.scene.n_layouts ? 0 : 1);
     a.walk = p.scene.n_layouts ? 2 : ctx->walk;          // accel: the walk-2 records only
     a.coop_walk = p.scene.n_layouts ? 0 : ctx->coop_walk;
     a.coop_win = coop_window_of(ctx, p);
@@ -971,7 +976,24 @@ int rt_create(const int* device_ids, int n_devices, rt_ctx** out) {
         const int bw = std::atoi(v);
         ctx->block_waves = bw == 1 ? 1 : 4;
     }
-    if (const char* v = std::getenv("RTAMD_COOP_LANES")) ctx->coop_lanes = std::max(0, std::min(64, std::atoi(v)));
+    if (const char* v = std::getenv("RTAMD_COOP_LANES")) ctx->coop_lanes = std::max(-1, std::min(64, std::atoi(v)));
+    // RTAMD_OPTS="name=value,...": any rt_set_option defaults (A/B runs)
+    if (const char* v = std::getenv("RTAMD_OPTS")) {
+        std::string all(v);
+        size_t pos = 0;
+        while (pos < all.size()) {
+            size_t comma = all.find(',', pos);
+            if (comma == std::string::npos) comma = all.size();
+            const std::string item = all.substr(pos, comma - pos);
+            const size_t eq = item.find('=');
+            if (eq != std::string::npos &&
+                rt_set_option(ctx, item.substr(0, eq).c_str(), std::atoll(item.c_str() + eq + 1)) != RT_OK) {
+                rt_destroy(ctx);
+                return RT_ERR_INVALID_ARG;       // rt_set_option's message names the option
+            }
+            pos = comma + 1;
+        }
+    }
     for (int k = 0; k < n_devices; ++k) {
         const int d = device_ids[k];
         if (d < 0 || d >= count) {
@@ -1832,7 +1854,7 @@ int rt_set_option(rt_ctx* ctx, const char* name, int64_t value) {
         }
     if (std::strcmp(name, "kernel") == 0 && value == 0) {
         // the one kernel (kernels 1-3, persistent / split / tiered, are archived)
-    } else if (std::strcmp(name, "coop_lanes") == 0 && value >= 0 && value <= 64) {
+    } else if (std::strcmp(name, "coop_lanes") == 0 && value >= -1 && value <= 64) {
         ctx->coop_lanes = (int)value;
     } else if (std::strcmp(name, "extensions") == 0 && value >= 0 && value <= 15) {
         ctx->ext = (int)value;
@@ -1916,6 +1938,7 @@ int rt_get_option(rt_ctx* ctx, const char* name, int64_t* value) {
     else if (std::strcmp(name, "learn_device") == 0) *value = ctx->learn_device;
     else if (std::strcmp(name, "leaf_align") == 0) *value = ctx->leaf_align;
     else if (std::strcmp(name, "accel") == 0) *value = ctx->accel;
+    else if (std::strcmp(name, "walk_bytes") == 0) *value = ctx->dev.empty() ? 0 : (int64_t)walk_bytes(ctx->dev[0]);
     else if (std::strcmp(name, "accel_used") == 0) *value = ctx->dev.empty() ? 0 : ctx->dev[0].scene.n_layouts;
     else if (std::strcmp(name, "leaf_align_used") == 0) *value = ctx->dev.empty() ? 0 : ctx->dev[0].scene.padded;
     else if (std::strcmp(name, "heavy_factor") == 0) *value = ctx->heavy_factor;

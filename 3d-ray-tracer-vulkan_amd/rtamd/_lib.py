@@ -34,7 +34,7 @@ EXPORTED = (
     "rt_scene_validate", "rt_set_option", "rt_get_option", "rt_diag_copy",
     "rt_host_alloc", "rt_host_free", "rt_render_async", "rt_render_wait", "rt_upload_spheres",
     "rt_render_batch_device", "rt_band_list_rows", "rt_render_batch_lists_device", "rt_band_lists_rows",
-    "rt_render_poll",
+    "rt_render_poll", "rt_accel_records",
 )
 
 

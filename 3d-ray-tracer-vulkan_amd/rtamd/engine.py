@@ -75,6 +75,10 @@ class Renderer:
         check(lib().rt_get_option(self._ctx, name.encode(), C.byref(v)))
         return v.value
 
+    def walk_bytes(self) -> int:
+        """Bytes of the records one ray walks (option walk_bytes)."""
+        return self.get_option("walk_bytes")
+
     def upload_scene(self, data: BuiltCpuData) -> None:
         """internalSwapScene (VulkanEngine.java:318-373); deep copy."""
         v = np.ascontiguousarray(data.model_vertex_data, dtype=np.float32)

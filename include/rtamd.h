@@ -240,9 +240,31 @@ int rt_render_poll(rt_ctx* ctx, uint64_t ticket, int* done);
  *                   box is requested before this node's triangle test and the
  *                   loop control (default).  Walks 1, 3 (round 4: a leaf in
  *                   two steps), 5, 13, 14 were measured slower and archived.
+ *   "accel"         at the next rt_upload_scene: 8 (default) = trace the
+ *                   uploaded triangles through a binned-SAH tree built on the
+ *                   host (one primitive per reference leaf: the triangle and
+ *                   its own leaf box; byte-identical copies dropped), in 8
+ *                   preorder layouts, each putting the near child first for
+ *                   one octant of ray directions; 1 = one layout (lower child
+ *                   first); 0 = the reference's own tree in its DFS order.
+ *                   The walk enters a box when t_enter <= closest_t *
+ *                   (1 + 2^-10) + 2^-10 and takes a triangle on t < closest_t
+ *                   or on a tie with a lower flattened index (the reference's
+ *                   first-found); a segment whose hit lies before its own
+ *                   box's t_enter is walked again in the reference's order.
+ *                   Frames, segments and material reads are the reference
+ *                   order's; node visits and triangle tests are the accel
+ *                   walk's own.  Heavy tiles / pixels are not
+ *                   split out of accel launches (heavy_first still orders
+ *                   the tiles)
+ *   "accel_used"    (rt_get_option only) the current scene's layouts on device
+ *                   0 (0 = the reference's tree)
+ *   "walk_bytes"    (rt_get_option only) bytes of the records one ray walks on
+ *                   device 0 (the reference's walk records, or one accel layout)
  *   "coop_lanes"    once at most this many lanes of a wave are still walking,
  *                   the whole wave finishes their walks one ray at a time
- *                   (0..64, default 1; 0 = off)
+ *                   (0..64; 0 = off; -1, the default = 1 on the reference's
+ *                   tree, 0 on the accel tree)
  *   "coop_walk"     cooperative walks (the coop tail): 0 = 64-node preorder
  *                   windows (default), 1 = preorder frontier (up to 64 live
  *                   subtrees expanded per round trip)
@@ -366,8 +388,8 @@ int rt_render_poll(rt_ctx* ctx, uint64_t ticket, int* done);
  *                   the slots' traces then share hardware queues and run one
  *                   after another (set GPU_MAX_HW_QUEUES before the process
  *                   initialises HIP)
- * Defaults can also be set with the environment variables RTAMD_WALK,
- * RTAMD_COOP_LANES, RTAMD_COOP_WALK, RTAMD_BLOCK_WAVES, RTAMD_HEAVY_FIRST,
+ * Defaults can also be set with the environment variables RTAMD_ACCEL,
+ * RTAMD_OPTS ("name=value,..." of any option above), RTAMD_WALK, RTAMD_COOP_LANES, RTAMD_COOP_WALK, RTAMD_BLOCK_WAVES, RTAMD_HEAVY_FIRST,
  * RTAMD_HEAVY_TILES, RTAMD_HEAVY_FACTOR, RTAMD_HEAVY_STREAM (0 / 1 / 2),
  * RTAMD_HEAVY_PIXELS, RTAMD_LEARN_COST and RTAMD_GRAPH. */
 int rt_set_option(rt_ctx* ctx, const char* name, int64_t value);

@@ -11,6 +11,14 @@ for p in (PKG_DIR, ROOT):
 
 REFERENCE = "/root/reference"
 
+# The GPU suites test_gpu_parity / test_gpu_pipeline / test_gpu_dist / test_jni_shim
+# pin the reference-order walk (option accel 0), whose work counters are the
+# oracle's own, on every Renderer that does not choose otherwise (rt_create
+# reads RTAMD_ACCEL).  The default accel walk (binned-SAH tree, DESIGN.md
+# §4a) is tested by test_gpu_accel.py and by the tests below that set option
+# accel themselves, against the same oracle frames.
+os.environ["RTAMD_ACCEL"] = "0"
+
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (gfx950) GPU")

@@ -176,3 +176,47 @@ def test_accel_extensions(acc):
     finally:
         acc.set_option("extensions", 0)
         acc.upload_spheres(np.zeros((0, 8), np.float32))
+
+
+@pytest.mark.parametrize("cfg_k", [3, 4, 5, 6])
+def test_accel_bench_setting_whole_frame(acc, cfg_k):
+    """BASELINE configs 3, 4, 5 (1M triangles, 3840x2160, 8 bounces) and 6 as
+    whole frames under bench.py's N = 1 setting with the default options
+    (accel 8, 4 launches in flight counted): the learning launch, the
+    production kernel in the learned order, then a counting launch.  Frames
+    equal the oracle's; the counters equal the accel model's."""
+    from rtamd import configs
+    from test_gpu_parity import _bands_device
+    cfg = configs.get(cfg_k)
+    built = cfg.build()
+    cam = cfg.camera()
+    _upload(acc, built, 8)
+    W, H, B = cfg.width, cfg.height, cfg.max_bounces
+    ref = _oracle(built, cam, W, H, B)
+    model = _model(built, cam, W, H, B, 8)
+    try:
+        acc.set_option("concurrent_launches", 4)
+        for stats in (False, False, True):
+            rgba, rad, st = _bands_device(acc, cam, W, H, B, H, 1, 0, stats=stats)
+            _check(rgba, rad, st if stats else None, ref, model, f"config {cfg_k} whole frame")
+        assert st["pixels"] == W * H
+    finally:
+        acc.set_option("concurrent_launches", 1)
+
+
+def test_accel_is_the_default():
+    """A context that is not told otherwise walks the accel tree in 8 octant
+    layouts; RTAMD_ACCEL only overrides it (the legacy suites
+    pin 0, conftest.py)."""
+    import os
+    import rtamd
+    from rtamd import configs
+    old = os.environ.pop("RTAMD_ACCEL", None)
+    try:
+        with rtamd.Renderer((0,)) as r:
+            assert r.get_option("accel") == 8 and r.get_option("coop_lanes") == -1
+            r.upload_scene(configs.config2().build())
+            assert r.get_option("accel_used") == 8
+    finally:
+        if old is not None:
+            os.environ["RTAMD_ACCEL"] = old

@@ -83,13 +83,16 @@ def _check(frames, rads, whole, what):
 @pytest.mark.parametrize("layout,world,rw", [("interleave", 1, 1.0), ("interleave", 2, 0.9), ("interleave", 4, 0.85),
                                              ("dealt", 8, 0.8), ("dealt", 4, 1.0), ("pieces", 4, 1.0),
                                              ("pieces", 8, 0.7)])
-def test_share_exchange_bit_exact(renderer, rccl_group, layout, world, rw):
+@pytest.mark.parametrize("accel", [0, 8])
+def test_share_exchange_bit_exact(renderer, rccl_group, layout, world, rw, accel):
     import torch
     from rtamd import configs
     from rtamd._lib import CameraUBO
     from rtamd.dist import SharePlan, ShareTracer, assemble_shares, gather_stack
     cfg = configs.config2()
+    renderer.set_option("accel", accel)
     renderer.upload_scene(cfg.build())
+    renderer.set_option("accel", 0)
     W, H, B, band_h = 320, 184, 3, 8          # 23 bands of 8 rows
     F = world                                  # frames per launch (weak scaling: a launch is a step)
     G = 2 * F                                  # frames per exchange batch
@@ -123,8 +126,9 @@ def test_share_exchange_bit_exact(renderer, rccl_group, layout, world, rw):
         _check(assemble_shares(stk, plan, src), assemble_shares(stk_r, plan, src), whole, "RCCL gather_stack")
 
 
+@pytest.mark.parametrize("accel", [0, 8])
 @pytest.mark.parametrize("world", [1, 2, 4])
-def test_tile_exchange_bit_exact(renderer, rccl_group, world):
+def test_tile_exchange_bit_exact(renderer, rccl_group, world, accel):
     """BASELINE config 4's tile grid (2 x 2 at N = 4): every rank's rectangle
     of every frame of a batch, stacked and assembled; at world size 1 the
     gather runs over RCCL."""
@@ -133,7 +137,9 @@ def test_tile_exchange_bit_exact(renderer, rccl_group, world):
     from rtamd._lib import CameraUBO
     from rtamd.dist import ShareTracer, TilePlan, assemble_tiles, gather_tile_stack, gather_tiles
     cfg = configs.config2()
+    renderer.set_option("accel", accel)
     renderer.upload_scene(cfg.build())
+    renderer.set_option("accel", 0)
     W, H, B, G = 322, 181, 3, 3               # odd sizes: uneven tiles, padded to the largest
     cams = _orbit_cams(W, H, G)
     whole = _whole(renderer, cams, W, H, B)

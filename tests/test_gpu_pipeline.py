@@ -38,8 +38,9 @@ def _orbit(cfg, k):
                           cfg.width / cfg.height)
 
 
+@pytest.mark.parametrize("accel", [0, 8])
 @pytest.mark.parametrize("camera", ["static", "orbit"])
-def test_bench_trace_shape_frames(renderer, camera):
+def test_bench_trace_shape_frames(renderer, camera, accel):
     """Config 3 through bench.py's N = 1 launches: D = 4 launches in flight on
     4 streams (concurrent_launches 4), each one whole frame into its slot,
     three rounds (the learning launch, then the learned order with heavy
@@ -53,6 +54,7 @@ def test_bench_trace_shape_frames(renderer, camera):
     W, H, B = cfg.width, cfg.height, cfg.max_bounces
     D = 4
     try:
+        renderer.set_option("accel", accel)       # accel 8: the default walk
         renderer.upload_scene(built)
         renderer.set_option("concurrent_launches", D)
         cams = [cfg.camera() if camera == "static" else _orbit(cfg, k) for k in range(D)]
@@ -76,12 +78,14 @@ def test_bench_trace_shape_frames(renderer, camera):
                 if not np.array_equal(got[j], ref):
                     n = int(np.any(got[j] != ref, axis=-1).sum())
                     raise AssertionError(f"round {rnd}, stream {j}: {n} pixels differ")
-        assert renderer.get_option("heavy_pixels_used") > 0 or camera == "orbit"
+        assert renderer.get_option("heavy_pixels_used") > 0 or camera == "orbit" or accel
     finally:
         renderer.set_option("concurrent_launches", 1)
+        renderer.set_option("accel", 0)
 
 
-def test_scene_swap_with_frames_in_flight():
+@pytest.mark.parametrize("accel", [0, 8])
+def test_scene_swap_with_frames_in_flight(accel):
     """HipEngine.java's loop: 4 frames in flight through rt_render_async and a
     scene upload between two submits (the old scene's frames still tracing);
     then frames of the new scene.  Every frame equals the oracle frame of the
@@ -100,6 +104,7 @@ def test_scene_swap_with_frames_in_flight():
     frames = [PinnedFrame(h, w) for _ in range(S)]
     try:
         r.set_option("async_slots", S)
+        r.set_option("accel", accel)
         order = [0] * 6 + [1] * 6 + [2] * 6          # a swap after every 6 submits
         pending = []
         cur = None

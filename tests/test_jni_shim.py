@@ -147,7 +147,8 @@ def test_error_status_becomes_runtime_exception():
 
 
 @pytest.mark.gpu
-def test_shim_renders_config2_bit_exact():
+@pytest.mark.parametrize("accel", [0, 8])
+def test_shim_renders_config2_bit_exact(accel):
     if not has_gpu():
         pytest.skip("no GPU")
     from oracle import oracle_lib
@@ -165,6 +166,7 @@ def test_shim_renders_config2_bit_exact():
         v = np.ascontiguousarray(built.model_vertex_data, dtype=np.float32)
         m = np.ascontiguousarray(built.model_material_data, dtype=np.float32)
         b = np.ascontiguousarray(built.flat_bvh_data, dtype=np.uint8)
+        jvm.call("setOption", ctx, jvm.string("accel"), accel)   # at the upload below
         # byte counts as VulkanEngine.java:337,345,353 computes them (remaining() * 4 / remaining())
         jvm.call("uploadScene", ctx, jvm.direct(v), v.size * 4, jvm.direct(m), m.size * 4, jvm.direct(b), b.size)
         ubo = np.frombuffer(cam.ubo_bytes(), dtype=np.uint8).copy()
