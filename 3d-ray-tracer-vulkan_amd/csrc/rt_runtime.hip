@@ -534,10 +534,24 @@ static int plan_order(const rt_ctx* ctx, PerDevice& p, TraceArgs& a, const rt_ca
         }
     }
     poll_learning(p);
+    static const bool dbg = std::getenv("RTAMD_DEBUG_PLAN") != nullptr;
     const PerDevice::Order* exact = nullptr;
     for (const auto& o : p.orders)
         if (o.n == n && o.key == key) { exact = &o; break; }
-    if (exact && !exact->pending) return use(*exact);
+    if (dbg) {
+        size_t n_reuse = 0;
+        for (const auto& o : p.orders)
+            if (!o.pending && o.n == n && o.key.size() == key.size() && std::memcmp(o.key.data(), key.data(), g) == 0)
+                ++n_reuse;
+        std::fprintf(stderr, "plan_order: n %zu frames %d lists %d exact %d pending %d same-geo %zu repeat %d busy %d "
+                     "orders %zu diag %d counters %d\n", n, a.n_frames, bands ? (int)bands->size() : -1,
+                     exact != nullptr, exact ? (int)exact->pending : -1, n_reuse, (int)repeat, (int)p.learn_busy,
+                     p.orders.size(), a.diag != nullptr, a.counters != nullptr);
+    }
+    if (exact && !exact->pending) {
+        if (dbg) std::fprintf(stderr, "  -> exact order %p\n", (void*)exact->d_order);
+        return use(*exact);
+    }
     const PerDevice::Order* reuse = nullptr;
     if (ctx->reuse_order)
         for (auto it = p.orders.rbegin(); it != p.orders.rend(); ++it)
@@ -549,7 +563,10 @@ static int plan_order(const rt_ctx* ctx, PerDevice& p, TraceArgs& a, const rt_ca
             }
     // A moving camera reuses the newest order of the frame geometry; so does
     // any launch while this key's own order is still being learned.
-    if (reuse && (!repeat || exact)) return use(*reuse);
+    if (reuse && (!repeat || exact)) {
+        if (dbg) std::fprintf(stderr, "  -> reuse order %p\n", (void*)reuse->d_order);
+        return use(*reuse);
+    }
     if (exact) return RT_OK;                  // learning in flight, nothing to reuse: raster order
     // Learn on a plain launch: a diagnostic launch keeps its own records, and a
     // counting launch (stats) runs the counting build, not the diagnostic one.
@@ -593,6 +610,7 @@ static int plan_order(const rt_ctx* ctx, PerDevice& p, TraceArgs& a, const rt_ca
     }
     a.diag = p.d_learn;                // the diagnostic build counts each wave's lockstep steps
     a.diag_lane = p.d_learn_lane;      // and each pixel's own walk length
+    if (dbg) std::fprintf(stderr, "  -> learn (device %d, in order %p)\n", (int)device, (void*)a.tile_order);
     return RT_OK;
 }
 

@@ -76,7 +76,9 @@ def _whole(renderer, cams, W, H, B):
 def _check(frames, rads, whole, what):
     import torch
     for f, (rgba, rad) in enumerate(whole):
-        assert torch.equal(frames[f], rgba), f"{what}: frame {f} RGBA8"
+        if not torch.equal(frames[f], rgba):
+            bad = torch.nonzero((frames[f] != rgba).any(-1)).cpu().tolist()
+            raise AssertionError(f"{what}: frame {f} RGBA8: {len(bad)} pixels differ, first {bad[:8]}")
         assert torch.equal(rads[f].view(torch.int32), rad.view(torch.int32)), f"{what}: frame {f} radiance"
 
 
@@ -106,6 +108,10 @@ def test_share_exchange_bit_exact(renderer, rccl_group, layout, world, rw, accel
         tracer = ShareTracer(renderer._ctx, W, H, B, "bands", rank, plan=plan, band_h=band_h, batch=G)
         rgba = torch.full((plan.per_rank, W, 4), 7, dtype=torch.uint8, device="cuda:0")
         rad = torch.zeros((plan.per_rank, W, 3), dtype=torch.float32, device="cuda:0")
+        # the fills above run on the current stream: the launch streams wait
+        # for them (without this a fast trace can land before its buffer's fill)
+        for st in streams:
+            st.wait_stream(torch.cuda.current_stream())
         for j, k0 in enumerate(range(0, G, F)):
             off = tracer.offset_rows(k0)
             rp = rgba[off].data_ptr() if off < plan.per_rank else rgba.data_ptr()

@@ -59,7 +59,7 @@ pmc() {  # pmc CONFIG NAME [SUFFIX EXTRA_BENCH_ARGS]
   PMC_PASSES="A C" BENCH_ARGS="--config $c $extra" bash tools/pmc.sh "${TAG}_pmc$c$sfx" || exit $?
   cp -r "gpurun_out/${TAG}_pmc$c$sfx" "$OUT/pmc$c$sfx"
   python3 tools/pmc_traffic.py "gpurun_out/${TAG}_pmc$c$sfx" "trace_simple<false, false" --config "$name" \
-      --source "profiles/r04/$TAG/pmc$c$sfx (tools/pmc.sh passes A and C, bench.py --config $c $extra)" \
+      --source "profiles/r05/$TAG/pmc$c$sfx (tools/pmc.sh passes A and C, bench.py --config $c $extra)" \
       --merge "$OUT/pmc_latest.json" > "$OUT/pmc$c$sfx.json" 2>> "$OUT/status.txt" || status "pmc_traffic cfg$c$sfx failed"
   cp "$OUT/pmc_latest.json" profiles/pmc_latest.json
 }
@@ -77,11 +77,14 @@ for s in "$@"; do
     bench200) run bench200 600 python bench.py > "$OUT/bench200.json" 2> "$OUT/bench200.err" ;;
     prof3)    prof 3 20 ;;
     prof5)    prof 5 10 ;;
-    pmc3)     pmc 3 cfg3_50k_1920x1080_b4 ;;
-    pmc5)     pmc 5 cfg5_1M_3840x2160_b8 ;;
-    fetch5)   pmc 5 cfg5_1M_3840x2160_b8@nocoop n "--set coop_lanes=0" && \
-              pmc 5 cfg5_1M_3840x2160_b8@split40 s "--set order_split=40" ;;
-    pmc3o)    pmc 3 cfg3_50k_1920x1080_b4@orbit o "--camera-path orbit" ;;
+    # record keys: bench.py pmc_key (the default accel 8 walk: "@accel8")
+    pmc3)     pmc 3 cfg3_50k_1920x1080_b4@accel8 ;;
+    pmc5)     pmc 5 cfg5_1M_3840x2160_b8@accel8 ;;
+    pmc6)     pmc 6 cfg6_fbm_1920x1080_b4@accel8 ;;
+    pmc3r)    RTAMD_ACCEL=0 pmc 3 cfg3_50k_1920x1080_b4 r ;;
+    fetch5)   pmc 5 cfg5_1M_3840x2160_b8@nocoop@accel8 n "--set coop_lanes=0" && \
+              pmc 5 cfg5_1M_3840x2160_b8@split40@accel8 s "--set order_split=40" ;;
+    pmc3o)    pmc 3 cfg3_50k_1920x1080_b4@orbit@accel8 o "--camera-path orbit" ;;
     orbit)    run orbit 600 python bench.py --steps 20 --warmup 5 --camera-path orbit \
                   > "$OUT/bench_orbit.json" 2> "$OUT/bench_orbit.err" ;;
     cfgs)     for a in "4 50" "5 10" "6 200"; do
