@@ -952,6 +952,12 @@ extern "C" {
 
 const char* rt_last_error(void) { return g_err; }
 
+int rt_abi_version(size_t* stats_bytes, size_t* camera_bytes) {
+    if (stats_bytes) *stats_bytes = sizeof(rt_stats);
+    if (camera_bytes) *camera_bytes = sizeof(rt_camera_ubo);
+    return RT_ABI_VERSION;
+}
+
 int rt_create(const int* device_ids, int n_devices, rt_ctx** out) {
     if (!out || n_devices < 1 || !device_ids) {
         set_error("rt_create: need out != NULL and n_devices >= 1 (there is no CPU backend)");

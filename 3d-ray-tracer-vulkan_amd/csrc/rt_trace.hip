@@ -798,9 +798,19 @@ __device__ __forceinline__ void heavy_pixel(const TraceArgs& a, int f, int lx, i
 #ifndef RT_SIMPLE_WPE
 #define RT_SIMPLE_WPE 8
 #endif
+// option accel's kernels (A/B builds: make variant FLAGS=-DRT_ACCEL_WPE=7)
+#ifndef RT_ACCEL_WPE
+#define RT_ACCEL_WPE RT_SIMPLE_WPE
+#endif
+// 1 = an accel leaf's triangle is loaded only once its box is hit (a second
+// dependent round trip for the quarter of leaf visits that test it, two loads
+// fewer for the rest); 0 = with the leaf's box, as the reference-order walk
+#ifndef RT_ACC_LAZY
+#define RT_ACC_LAZY 0
+#endif
 template <bool COUNT, bool DIAG = false, int FEAT = 0, int WALK = 2>
 __global__ __launch_bounds__(256)
-__attribute__((amdgpu_waves_per_eu((FEAT & kFeatFrontier) ? 1 : RT_SIMPLE_WPE)))
+__attribute__((amdgpu_waves_per_eu((FEAT & kFeatFrontier) ? 1 : (FEAT & kFeatAccel) ? RT_ACCEL_WPE : RT_SIMPLE_WPE)))
 void trace_simple(TraceArgs a) {
     // Pad bits (leaf_align): the production kernels (cooperative tail, no
     // extensions or frontier tail) read them only when built with kFeatPad, so
@@ -1018,6 +1028,12 @@ void trace_simple(TraceArgs a) {
 #endif
                     if (hb && nleaf) {                                       // hit_triangle (:196-200)
                         if (COUNT) ++c_tri;
+#if RT_CHAIN >= 2
+                        if (ACC && RT_ACC_LAZY) {
+                            Q0 = wbuf(wrs, n, 32);
+                            Q1 = wbuf(wrs, n, 48);
+                        }
+#endif
                         float t;
                         if (tri_test(make_float4(v0x, Q0.x, Q0.y, 0.f), make_float4(Q0.z, Q0.w, Q1.x, 0.f),
                                      make_float4(Q1.y, Q1.z, Q1.w, 0.f), o, d, t) &&
@@ -1027,7 +1043,7 @@ void trace_simple(TraceArgs a) {
                             if (ACC) incons = t < te;
                         }
                     }
-                    if (nl && nxt < (ACC ? lend : wend)) {
+                    if (nl && nxt < (ACC ? lend : wend) && !(ACC && RT_ACC_LAZY)) {
 #if RT_CHAIN >= 2
                         Q0 = wbuf(wrs, nxt, 32);
                         Q1 = wbuf(wrs, nxt, 48);

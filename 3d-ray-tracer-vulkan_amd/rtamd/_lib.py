@@ -26,6 +26,8 @@ RT_ERR = {
 }
 
 # Every symbol include/rtamd.h declares (checked by tests/test_abi.py).
+ABI_VERSION = 5           # include/rtamd.h RT_ABI_VERSION
+
 EXPORTED = (
     "rt_create", "rt_upload_scene", "rt_render", "rt_render_tile_device", "rt_destroy",
     "rt_last_error", "rt_scene_info", "rt_bvh_layout_size", "rt_build_scene",
@@ -34,7 +36,7 @@ EXPORTED = (
     "rt_scene_validate", "rt_set_option", "rt_get_option", "rt_diag_copy",
     "rt_host_alloc", "rt_host_free", "rt_render_async", "rt_render_wait", "rt_upload_spheres",
     "rt_render_batch_device", "rt_band_list_rows", "rt_render_batch_lists_device", "rt_band_lists_rows",
-    "rt_render_poll", "rt_accel_records",
+    "rt_render_poll", "rt_accel_records", "rt_abi_version",
 )
 
 
@@ -133,11 +135,18 @@ def lib() -> C.CDLL:
                 "rt_render_poll": (i32, [vp, u64, C.POINTER(i32)]),
                 "rt_accel_records": (i32, [vp, sz, vp, sz, vp, sz, i32, C.POINTER(C.c_uint32), sz, C.POINTER(sz),
                                            C.POINTER(C.c_int32)]),
+                "rt_abi_version": (i32, [C.POINTER(sz), C.POINTER(sz)]),
             }
             for name, (res, args) in sig.items():
                 f = getattr(L, name)
                 f.restype = res
                 f.argtypes = args
+            # the structs this binding lays out must be the library's
+            sb, cb = C.c_size_t(), C.c_size_t()
+            ver = L.rt_abi_version(C.byref(sb), C.byref(cb))
+            if ver != ABI_VERSION or sb.value != C.sizeof(Stats) or cb.value != C.sizeof(CameraUBO):
+                raise RtError(-1, f"{LIB_PATH}: ABI version {ver} (rt_stats {sb.value} B, camera {cb.value} B); "
+                                  f"this binding expects {ABI_VERSION} ({C.sizeof(Stats)} B, {C.sizeof(CameraUBO)} B)")
             _lib = L
         return _lib
 

@@ -40,6 +40,11 @@ extern "C" {
 #define RT_NODE_RECORD_BYTES     48  /* LinearBVHNode, std430                              BVHFlattener.java:19    */
 #define RT_CAMERA_UBO_BYTES      80  /* CameraUBO + frameCount + isSkyEnabled              VulkanEngine.java:378-396 */
 #define RT_REFERENCE_MAX_BOUNCES 10  /* compute_dynamic_ray.comp:44 */
+/* Layout version of the structs below (rt_camera_ubo, rt_stats) and of the
+ * calls' argument lists: bumped whenever one changes (round 4 moved
+ * rt_stats.pixels to the end, SURVEY.md §8b's order).  A binding compiled
+ * against another version must refuse the library (rt_abi_version). */
+#define RT_ABI_VERSION 5
 
 typedef struct rt_ctx rt_ctx;
 
@@ -410,6 +415,10 @@ int rt_destroy(rt_ctx* ctx);
 
 /* Thread-local message for the last failing call on this thread. */
 const char* rt_last_error(void);
+
+/* RT_ABI_VERSION of the library, and sizeof(rt_stats) / sizeof(rt_camera_ubo)
+ * as it was compiled (nullable): a host checks them once after loading. */
+int rt_abi_version(size_t* stats_bytes, size_t* camera_bytes);
 
 /* Node / triangle counts and tree depth of the uploaded scene. */
 int rt_scene_info(rt_ctx* ctx, size_t* n_nodes, size_t* n_tris, int* max_depth);

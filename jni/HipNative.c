@@ -23,6 +23,13 @@ static void throw_rt(JNIEnv* env, int rc) {
 
 /* long create(int[] deviceIds) */
 JNIEXPORT jlong JNICALL Java_dev_demir_vulkan_engine_HipNative_create(JNIEnv* env, jclass c, jintArray ids) {
+    /* the library must have this shim's struct layouts (rtamd.h RT_ABI_VERSION) */
+    size_t sb = 0, cb = 0;
+    if (rt_abi_version(&sb, &cb) != RT_ABI_VERSION || sb != sizeof(rt_stats) || cb != sizeof(rt_camera_ubo)) {
+        jclass ex = (*env)->FindClass(env, "java/lang/RuntimeException");
+        if (ex) (*env)->ThrowNew(env, ex, "librtamd ABI version differs from the shim's (include/rtamd.h)");
+        return 0;
+    }
     jsize n = (*env)->GetArrayLength(env, ids);
     jint* p = (*env)->GetIntArrayElements(env, ids, NULL);
     rt_ctx* ctx = NULL;
