@@ -51,9 +51,13 @@ def main():
                     help="plain launches after the timed region (default: the bench line's "
                          "roofline.plain_kernels_after_timed, else 0)")
     args = ap.parse_args()
-    rows = [r for r in csv.DictReader(open(args.trace)) if "trace_simple<false, false" in r["Kernel_Name"]]
+    # plain launches: trace_simple<false, false, ...>, and with option
+    # split_bounce each frame's second kernel trace_queue<false, ...>
+    rows = [r for r in csv.DictReader(open(args.trace))
+            if "trace_simple<false, false" in r["Kernel_Name"] or "trace_queue<false" in r["Kernel_Name"]]
     rows.sort(key=lambda r: int(r["Dispatch_Id"]))
-    n = args.steps * args.launches_per_step
+    per = 2 if any("trace_queue" in r["Kernel_Name"] for r in rows) else 1
+    n = args.steps * args.launches_per_step * per
     if len(rows) < n:
         raise SystemExit(f"{len(rows)} plain trace launches in the trace, need {n}")
     skip = args.skip_last
@@ -68,10 +72,17 @@ def main():
     durs = [(e - s) / 1e6 for s, e in iv]
     union = union_length(iv) / 1e6
     span = (max(e for _, e in iv) - min(s for s, _ in iv)) / 1e6
-    names = sorted({r["Kernel_Name"][r["Kernel_Name"].index("trace_simple"):].split(">(")[0] + ">" for r in timed})
+    def short(k):
+        i = k.index("trace_simple") if "trace_simple" in k else k.index("trace_queue")
+        return k[i:].split(">(")[0] + ">"
+    names = sorted({short(r["Kernel_Name"]) for r in timed})
+    by_kernel = {nm: round(statistics.mean((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6
+                                           for r in timed if short(r["Kernel_Name"]) == nm), 4) for nm in names}
     out = {
         "trace": args.trace,
         "kernels": names,
+        "kernels_per_frame": per,
+        "mean_ms_by_kernel": by_kernel,
         "frames": args.steps,
         "launches": n,
         "union_ms": round(union, 4),
