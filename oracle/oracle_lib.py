@@ -12,6 +12,7 @@ LIB = os.path.join(HERE, "liboracle.so")
 ENV_LIB = os.path.join(HERE, "liboracle_env.so")     # rt_envelope.c: the Vulkan-envelope study
 ACCEL_LIB = os.path.join(HERE, "liboracle_accel.so") # rt_accel_model.c: option accel's walk on the CPU
 ENV_FMA, ENV_RSQ, ENV_RCP, ENV_ULP, ENV_FTZ = 1, 2, 4, 8, 16   # rt_oracle.c ENV_* bits
+ENV_ULP2, ENV_SQRT_RCP, ENV_SQRT_MUL = 32, 64, 128
 
 
 class Counts(C.Structure):

@@ -14,6 +14,6 @@
  * a render in progress).  Returns the previous bits. */
 int orc_env_set_variant(int bits) {
     const int old = g_env;
-    g_env = bits & (ENV_FMA | ENV_RSQ | ENV_RCP | ENV_ULP | ENV_FTZ);
+    g_env = bits & (ENV_FMA | ENV_RSQ | ENV_RCP | ENV_ULP | ENV_FTZ | ENV_ULP2 | ENV_SQRT_RCP | ENV_SQRT_MUL);
     return old;
 }

@@ -68,6 +68,11 @@ typedef struct { float x, y, z; } vec3;
 #define ENV_RCP 4        /* a / b = a * (1 / b), the reciprocal correctly rounded */
 #define ENV_ULP 8        /* reciprocals and inversesqrts off by up to one ulp (a hash of the input picks) */
 #define ENV_FTZ 16       /* denormal inputs and results flushed to zero (shaderDenormPreserveFloat32 off) */
+#define ENV_ULP2 32      /* reciprocals and inversesqrts off by up to two ulps: with ENV_RCP a division is
+                          * within the 2.5 ulps GLSL 4.50 allows, and inversesqrt at its 2-ulp bound */
+#define ENV_SQRT_RCP 64  /* sqrt(x) = 1 / inversesqrt(x) (GLSL 4.50 defines sqrt's precision so), at length()
+                          * (:139), normalize and the gamma sqrt (:235) */
+#define ENV_SQRT_MUL 128 /* sqrt(x) = x * inversesqrt(x) (0 for x = 0), at the same sites */
 #include <xmmintrin.h>
 static int g_env = 0;
 /* the calling thread's SSE control word for the selected variant (FTZ + DAZ or not) */
@@ -76,22 +81,35 @@ static void env_fp_mode(void) {
     _mm_setcsr(base | ((g_env & ENV_FTZ) ? 0x8040u : 0u));
 }
 static float env_ulp(float r, float x) {
-    if (!(g_env & ENV_ULP)) return r;
+    if (!(g_env & (ENV_ULP | ENV_ULP2))) return r;
     uint32_t b;
     memcpy(&b, &x, 4);
-    const uint32_t h = orc_pcg(b ^ 0x9E3779B9u) & 3u;
-    return h == 1u ? nextafterf(r, INFINITY) : h == 2u ? nextafterf(r, -INFINITY) : r;
+    const uint32_t h = orc_pcg(b ^ 0x9E3779B9u);
+    if (g_env & ENV_ULP2) {                    /* -2 .. +2 ulps, a hash of the input picks */
+        const int k = (int)(h % 5u) - 2;
+        for (int i = 0; i < k; ++i) r = nextafterf(r, INFINITY);
+        for (int i = 0; i < -k; ++i) r = nextafterf(r, -INFINITY);
+        return r;
+    }
+    const uint32_t h3 = h & 3u;
+    return h3 == 1u ? nextafterf(r, INFINITY) : h3 == 2u ? nextafterf(r, -INFINITY) : r;
 }
 static float mad(float a, float b, float c) { return (g_env & ENV_FMA) ? fmaf(a, b, c) : a * b + c; }
 static float msb(float a, float b, float c) { return (g_env & ENV_FMA) ? fmaf(a, b, -c) : a * b - c; }
 static float rcp(float x) { return env_ulp(1.0f / x, x); }
-static float fdiv(float a, float b) { return (g_env & (ENV_RCP | ENV_ULP)) ? a * rcp(b) : a / b; }
+static float fdiv(float a, float b) { return (g_env & (ENV_RCP | ENV_ULP | ENV_ULP2)) ? a * rcp(b) : a / b; }
 static float rsq(float x) { return env_ulp((float)(1.0 / sqrt((double)x)), x); }
+static float fsqrt(float x) {
+    if (g_env & ENV_SQRT_RCP) return 1.0f / rsq(x);
+    if (g_env & ENV_SQRT_MUL) return x == 0.0f ? 0.0f : x * rsq(x);
+    return sqrtf(x);
+}
 #else
 static float mad(float a, float b, float c) { return a * b + c; }
 static float msb(float a, float b, float c) { return a * b - c; }
 static float rcp(float x) { return 1.0f / x; }
 static float fdiv(float a, float b) { return a / b; }
+static float fsqrt(float x) { return sqrtf(x); }
 #endif
 
 static vec3 v3(float x, float y, float z) { vec3 r = {x, y, z}; return r; }
@@ -103,7 +121,7 @@ static vec3 scale3(vec3 a, float s) { return v3(a.x * s, a.y * s, a.z * s); }
 static vec3 madd3(vec3 a, vec3 b, float s) { return v3(mad(b.x, s, a.x), mad(b.y, s, a.y), mad(b.z, s, a.z)); }
 /* (x*x' + y*y') + z*z'; contracted: fma(z, z', fma(x, x', y*y')) */
 static float dot3(vec3 a, vec3 b) { return mad(a.z, b.z, mad(a.x, b.x, a.y * b.y)); }
-static float length3(vec3 a) { return sqrtf(dot3(a, a)); }
+static float length3(vec3 a) { return fsqrt(dot3(a, a)); }
 static vec3 normalize3(vec3 a) {
 #ifdef ORC_ENVELOPE
     if (g_env & ENV_RSQ) { const float k = rsq(dot3(a, a)); return v3(a.x * k, a.y * k, a.z * k); }
@@ -408,9 +426,9 @@ static int shade_pixel(const scene* s, const orc_camera* cam, int W, int H, int 
         lin[1] = final_color.y;
         lin[2] = final_color.z;
     }
-    out_rgb[0] = sqrtf(final_color.x);                                         /* :235 */
-    out_rgb[1] = sqrtf(final_color.y);
-    out_rgb[2] = sqrtf(final_color.z);
+    out_rgb[0] = fsqrt(final_color.x);                                         /* :235 */
+    out_rgb[1] = fsqrt(final_color.y);
+    out_rgb[2] = fsqrt(final_color.z);
     return 0;
 }
 

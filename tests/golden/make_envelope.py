@@ -29,7 +29,13 @@ inversesqrts off by up to one ulp, chosen by a hash of the input), ftz 16
 (denormal inputs and results flushed to zero), llvm 7 (a compiler that
 fuses, uses rsq and rcp: what an LLVM-based driver does with
 fast-math-style float lowering), llvm_ulp 15 (the same with approximate 1-ulp
-hardware rcp / rsq, the spec's worst case short of 2-2.5 ulp), all 31.
+hardware rcp / rsq), all 31.  Round 5 adds the specification's own bounds:
+ulp2 32 (reciprocals and inversesqrts off by up to two ulps, so a division
+through the reciprocal stays within GLSL's 2.5 ulps and inversesqrt at its 2
+ulps), sqrt_rcp 64 (sqrt(x) = 1 / inversesqrt(x), the form GLSL 4.50 defines
+sqrt's precision by) and sqrt_mul 128 (sqrt(x) = x * inversesqrt(x)), both at
+length() (:139), normalize and the gamma sqrt (:235); llvm_ulp2 39,
+llvm_ulp2_sqrt_rcp 103, llvm_ulp2_sqrt_mul 167 and all2 127 combine them.
 
 Usage: python tests/golden/make_envelope.py [--threads N]
 """
@@ -45,7 +51,10 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(os.path.dirname(HERE))
 sys.path[:0] = [os.path.join(ROOT, "3d-ray-tracer-vulkan_amd"), ROOT]
 
-VARIANTS = {"fma": 1, "rsq": 2, "rcp": 4, "ulp": 8, "ftz": 16, "llvm": 7, "llvm_ulp": 15, "all": 31}
+VARIANTS = {"fma": 1, "rsq": 2, "rcp": 4, "ulp": 8, "ftz": 16, "llvm": 7, "llvm_ulp": 15, "all": 31,
+            # round 5: the GLSL 4.50 bounds themselves
+            "ulp2": 32, "sqrt_rcp": 64, "sqrt_mul": 128, "llvm_ulp2": 39, "llvm_ulp2_sqrt_rcp": 103,
+            "llvm_ulp2_sqrt_mul": 167, "all2": 127}
 CONFIGS = (2, 3, 6)
 SUBSET_STEP = {2: 16, 3: 32, 6: 32}      # the rows tests/test_envelope.py re-derives
 TOL = 1e-4

@@ -182,3 +182,48 @@ def test_r04_camera_stop_learning_frame(session):
     cs = _r04(session, "bench_orbit.json")["camera_stop"]["ms_per_frame"]
     steady = sorted(cs[2:])[len(cs[2:]) // 2]
     assert cs[0] <= 2.0 * steady and max(cs) <= 2.0 * steady, cs
+
+
+# ---- round 5: the headline over the device time per frame
+R05 = os.path.join(ROOT, "profiles", "r05")
+
+
+# (session, file) of the round-5 lines this round's evidence rests on (r5c's
+# lines predate the PMC records keyed by accel: their traffic came from the
+# reference walk's round-4 record, so they are not listed)
+R05_LINES = []
+
+
+def _r05_lines():
+    return [x for x in R05_LINES if os.path.exists(os.path.join(R05, *x))]
+
+
+@pytest.mark.parametrize("session,name", _r05_lines())
+def test_r05_roofline_reproduces(session, name):
+    with open(os.path.join(R05, session, name)) as fh:
+        d = json.loads([x for x in fh if x.startswith("{")][-1])
+    r = d["roofline"]
+    alg = r["alg_bytes_per_launch"]
+    tf = r["frame_ms_device"] * 1e-3
+    tk = r["kernel_ms"] * 1e-3
+    assert r["views"]["device_time"]["l2_frac"] == pytest.approx(alg / tf / 1e9 / bench.L2_PEAK_GBS, rel=2e-3)
+    assert r["views"]["per_launch"]["frac"] == pytest.approx(alg / tk / 1e9 / bench.HBM_PEAK_GBS, rel=2e-3)
+    if r["bound"] == "l2":
+        assert r["peak"] == bench.L2_PEAK_GBS
+        assert r["frac"] == pytest.approx(alg / tf / 1e9 / bench.L2_PEAK_GBS, rel=2e-3)
+    else:
+        assert r["bound"] == "hbm" and r["peak"] == bench.HBM_PEAK_GBS
+        num = r["traffic"] if r["traffic"] else alg
+        assert r["frac"] == pytest.approx(num / tf / 1e9 / bench.HBM_PEAK_GBS, rel=2e-3)
+    if r["traffic"]:
+        # the PMC record it names: FETCH_SIZE (KiB of 64-B halves) x 1024 x 2
+        src = os.path.join(ROOT, r["pmc_source"].split(" ")[0])
+        fetch = _pmc_mean(os.path.join(src, "C_counter_collection.csv"), "FETCH_SIZE",
+                          kernel="trace_simple<false, false")
+        assert r["traffic"] == pytest.approx(fetch * 1024 * 2, rel=1e-6)
+        assert r["bound"] == ("hbm" if r["traffic"] / tf / 1e9 / bench.HBM_PEAK_GBS >
+                              alg / tf / 1e9 / bench.L2_PEAK_GBS else "l2")
+    # throughput: segments of the timed frames over the wall time
+    seg = d["config"]["segments_per_frame"] * d["steps"] * d["config"]["frames_per_step"]
+    assert d["value"] == pytest.approx(seg / (d["ms_per_step"] * 1e-3 * d["steps"]) / 1e6, rel=2e-3)
+    assert 0.0 < r["frac"] < 1.0
