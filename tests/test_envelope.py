@@ -10,8 +10,10 @@ CPU checks:
   the driver's choice) and five OpFDiv;
 * the committed row subsets re-derive exactly (the study is reproducible);
 * the committed whole-frame results state the band DESIGN.md §2 quotes: every
-  variant keeps at least 99.99 % of pixels within 1e-4 per channel and within
-  1 LSB of RGBA8, with a few chaotic outliers (a 1-ulp change flips a path).
+  variant (round 5: up to the specification's 2.5-ulp division, 2-ulp
+  inversesqrt and sqrt through inversesqrt) keeps at least 99.99 % of pixels
+  within 1e-4 per channel and within 1 LSB of RGBA8, with a few chaotic
+  outliers (an ulp or two flips a path).
 """
 import json
 import os
@@ -70,6 +72,15 @@ def test_envelope_band():
             assert s["pixels"] == c["width"] * c["height"]
             assert s["within_1e-4"] >= 0.9999, (k, v)
             assert s["rgba8_within_1lsb"] >= 0.9999, (k, v)
-            assert s["pixels_over_1e-4"] <= 64, (k, v)
+            assert s["pixels_over_1e-4"] <= 100, (k, v)
     # the outliers are chaotic path flips, not drift: some move by most of the range
     assert max(s["max_abs_rgba8"] for c in env["configs"].values() for s in c["variants"].values()) > 100
+
+
+def test_round5_variants_present():
+    """the spec's own bounds are in the study."""
+    env = _load()
+    for k, c in env["configs"].items():
+        for v in ("ulp2", "sqrt_rcp", "sqrt_mul", "llvm_ulp2", "llvm_ulp2_sqrt_rcp", "llvm_ulp2_sqrt_mul", "all2"):
+            assert v in c["variants"], (k, v)
+    assert env["summary"]["min_within_1e-4"] >= 0.99996
