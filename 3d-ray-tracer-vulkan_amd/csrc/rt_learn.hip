@@ -144,13 +144,17 @@ __global__ __launch_bounds__(1024) void learn_top(const unsigned long long* __re
             __syncthreads();
         }
     }
-    const int nout = m < cap ? m : cap;
+    // More candidates than the sort holds: which ones arrived first is a race,
+    // so the choice would be neither the costliest nor deterministic.  Such an
+    // order takes no heavy pixels (exact, only less balanced); the count
+    // reports the overflow as -1 (rt_runtime.hip poll_learning).
+    const int nout = nc > (unsigned)kCand ? 0 : (m < cap ? m : cap);
     for (int i = tid; i < nout; i += 1024) {
         const int q = (int)(0xFFFFFFFFu - (unsigned)(sk[i] & 0xFFFFFFFFull));
         hpix[i] = q;
         atomicOr(&mask[q >> 6], 1ull << (q & 63));
     }
-    if (tid == 0) *nhpix = nout;
+    if (tid == 0) *nhpix = nc > (unsigned)kCand ? -1 : nout;
 }
 
 }  // namespace

@@ -286,6 +286,7 @@ struct PerDevice {
     hipEvent_t   learn_ev = nullptr;
     bool         learn_busy = false;          // a device learning is in flight (its order pending)
     bool         learning_device = false;     // the learning launch being planned learns on the device
+    int          learn_overflows = 0;         // device learnings with more heavy-pixel candidates than sorted
     int          learning_rec_off = 0;        // its heavy-pixel waves ahead of the tile records
     // option heavy_tiles: auxiliary streams (round robin) for the concurrent heavy-tile launch
     hipStream_t  aux[4] = {nullptr, nullptr, nullptr, nullptr};
@@ -346,7 +347,9 @@ static void poll_learning(PerDevice& p) {
     if (!p.learn_busy || hipEventQuery(p.learn_ev) != hipSuccess) return;
     for (auto& o : p.orders)
         if (o.pending) {
-            o.n_hpix = *p.h_nhpix;
+            // -1: more candidates than learn_top sorts (rt_learn.hip): no heavy pixels
+            o.n_hpix = std::max(0, *p.h_nhpix);
+            if (*p.h_nhpix < 0) ++p.learn_overflows;
             o.pending = false;
         }
     p.learn_busy = false;
@@ -467,10 +470,13 @@ static int plan_order(const rt_ctx* ctx, PerDevice& p, TraceArgs& a, const rt_ca
     const size_t n = (size_t)((a.tw + bw * tw_w - 1) / (bw * tw_w)) * bw * (size_t)((a.th + th_w - 1) / th_w) *
                      (size_t)a.n_frames;
     // key = geometry (+ the band list) | the cameras | the scene
+    // (the heavy-split options are part of the key: an order learned on the
+    // device has no heavy tiles, one learned on the host does)
     std::vector<int> geo = {a.width, a.height, a.max_bounces, a.x0, a.y0, a.tw, a.th, a.band_h, a.band_stride,
                             a.band_off, a.wave_tile, a.ext, a.coop_lanes, a.walk, ctx->learn_cost, ctx->order_split,
                             ctx->heavy_factor, concurrency(ctx), ctx->heavy_cap, ctx->heavy_pixel_factor,
-                            a.n_frames, bands ? (int)bands->size() : -1, a.list_stride, ctx->order_frames};
+                            a.n_frames, bands ? (int)bands->size() : -1, a.list_stride, ctx->order_frames,
+                            ctx->heavy_stream, ctx->heavy_pixels, ctx->heavy_tiles, ctx->learn_device};
     if (bands) geo.insert(geo.end(), bands->begin(), bands->end());
     const size_t g = geo.size() * sizeof(int), c = (size_t)a.n_frames * sizeof(rt_camera_ubo);
     std::vector<uint8_t> key(g + c + sizeof(uint64_t));
@@ -2030,6 +2036,7 @@ int rt_get_option(rt_ctx* ctx, const char* name, int64_t* value) {
     else if (std::strcmp(name, "reuse_order") == 0) *value = ctx->reuse_order;
     else if (std::strcmp(name, "heavy_pixels") == 0) *value = ctx->heavy_pixels;
     else if (std::strcmp(name, "heavy_pixel_factor") == 0) *value = ctx->heavy_pixel_factor;
+    else if (std::strcmp(name, "learn_overflows") == 0) *value = ctx->dev.empty() ? 0 : ctx->dev[0].learn_overflows;
     else if (std::strcmp(name, "heavy_pixels_used") == 0) *value = ctx->dev.empty() ? 0 : ctx->dev[0].last_heavy_px;
     else if (std::strcmp(name, "heavy_tiles_used") == 0) *value = ctx->dev.empty() ? 0 : ctx->dev[0].last_heavy;
     else if (std::strcmp(name, "plain_kernels") == 0) *value = ctx->dev.empty() ? 0 : (int64_t)ctx->dev[0].plain_kernels;

@@ -28,6 +28,7 @@
 static const uint32_t* g_rec = NULL;   /* 8 words per slot */
 static int g_layouts = 1, g_slots = 0, g_root_leaf = 0;
 static uint64_t g_fallbacks = 0;       /* segments re-walked in the reference's order */
+static uint64_t g_leaf_visits = 0;     /* analysis: leaf slots walked (the rest are internal nodes) */
 /* The walk's box margin: a box is entered when t_enter <= closest_t * RELAX +
  * RELAX_ABS (accel_build.h).  orc_accel_margin changes them for studies. */
 static float g_relax = 1.0f + 1.0f / 1024.0f, g_relax_abs = 1.0f / 1024.0f;
@@ -45,6 +46,13 @@ uint64_t orc_accel_fallbacks(void) {
     return f;
 }
 
+/* Leaf slots walked since the last call (resets); an analysis aid. */
+uint64_t orc_accel_leaf_visits(void) {
+    const uint64_t f = g_leaf_visits;
+    g_leaf_visits = 0;
+    return f;
+}
+
 /* Sets the records the following renders walk (the caller keeps them alive). */
 int orc_accel_set(const uint32_t* rec, int n_layouts, int slots, int root_leaf) {
     if ((n_layouts != 1 && n_layouts != 8) || slots < 0 || (slots > 0 && !rec)) return -2;
@@ -56,6 +64,22 @@ int orc_accel_set(const uint32_t* rec, int n_layouts, int slots, int root_leaf) 
 }
 
 static float rec_f(size_t slot, int w) { float f; memcpy(&f, &g_rec[8 * slot + (size_t)w], 4); return f; }
+
+/* Analysis (orc_accel_quant): internal boxes widened to what a compressed
+ * record could hold, to count the visits that would cost; leaves stay exact.
+ * 1 = IEEE half precision of each coordinate, rounded outward. */
+static int g_quant = 0;
+int orc_accel_quant(int mode) { const int o = g_quant; g_quant = mode; return o; }
+static float half_down(float x) {           /* the largest half-precision value <= x, as float */
+    if (x == 0.0f || !isfinite(x)) return x;
+    int E;
+    (void)frexpf(x, &E);                     /* |x| in [2^(E-1), 2^E) */
+    const int e = E - 1 < -14 ? -14 : E - 1;
+    const float ulp = ldexpf(1.0f, e - 10);
+    const float r = floorf(x / ulp) * ulp;
+    return r > 65504.0f ? 65504.0f : (r < -65504.0f ? -INFINITY : r);
+}
+static float half_up(float x) { return -half_down(-x); }
 
 static int accel_walk(const scene* s, ray r, float* closest_t, int* hit_index, vec3* hit_normal,
                       orc_counts* cnt) {
@@ -70,16 +94,23 @@ static int accel_walk(const scene* s, ray r, float* closest_t, int* hit_index, v
     float thr = c * g_relax + g_relax_abs;
     float hit_te = 0.0f;                      /* t_enter of the hit triangle's own box */
     int hit = -1;
+    uint64_t leaf_visits = 0;
     while (n < end) {
         const uint32_t aw = g_rec[8 * n + 3], bw = g_rec[8 * n + 7];
         cnt->node_visits++;
         trace_rec((int32_t)n);
         /* the slab test of hit_aabb (:88-103), t_enter <= closest_t */
-        const vec3 t0s = mul3(sub3(v3(rec_f(n, 0), rec_f(n, 1), rec_f(n, 2)), r.origin), inv);
-        const vec3 t1s = mul3(sub3(v3(rec_f(n, 4), rec_f(n, 5), rec_f(n, 6)), r.origin), inv);
+        vec3 blo = v3(rec_f(n, 0), rec_f(n, 1), rec_f(n, 2)), bhi = v3(rec_f(n, 4), rec_f(n, 5), rec_f(n, 6));
+        if (g_quant == 1 && !leaf) {
+            blo = v3(half_down(blo.x), half_down(blo.y), half_down(blo.z));
+            bhi = v3(half_up(bhi.x), half_up(bhi.y), half_up(bhi.z));
+        }
+        const vec3 t0s = mul3(sub3(blo, r.origin), inv);
+        const vec3 t1s = mul3(sub3(bhi, r.origin), inv);
         const float te = fmaxf(fmaxf(fminf(t0s.x, t1s.x), fminf(t0s.y, t1s.y)), fminf(t0s.z, t1s.z));
         const float tx = fminf(fminf(fmaxf(t0s.x, t1s.x), fmaxf(t0s.y, t1s.y)), fmaxf(t0s.z, t1s.z));
         const int hb = tx > te && tx > T_MIN && te <= thr;
+        leaf_visits += (uint64_t)leaf;
         if (hb && leaf) {
             const int tri = (int)(aw & 0x1FFFFFFFu);
             cnt->tri_tests++;
@@ -113,6 +144,10 @@ static int accel_walk(const scene* s, ray r, float* closest_t, int* hit_index, v
         n = nxt;
         leaf = nl;
     }
+#ifdef _OPENMP
+#pragma omp atomic
+#endif
+    g_leaf_visits += leaf_visits;
     if (hit >= 0 && c < hit_te) {
         /* The hit lies before its own box's t_enter (float rounding on the
          * box face): the one case where the reference's result depends on
