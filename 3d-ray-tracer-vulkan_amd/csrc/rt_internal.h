@@ -166,18 +166,7 @@ struct TraceArgs {
     int      coop_win = 64;     // coop_walk's window: 64 or 32 slots (option coop_window)
     int      list_stride;       // band_list per frame: frame f's at band_list + f * list_stride
                                 //   (0 = one list for every frame of the launch)
-    // Split launch (option split_bounce, accel walk): the paths still alive at
-    // bounce split_bounce leave trace_simple for the launch stream's ray queue
-    // (queue_count at the base, 3 float4 per ray after it), and trace_queue
-    // (queue_waves one-wave workgroups) finishes them, 64 paths per wave.
-    int      split_bounce = 0;  // 0 = off
-    unsigned* queue_count = nullptr;   // [0] = rays queued, [1] = trace_queue waves done
-    float4*  queue = nullptr;
-    int      queue_waves = 0;
 };
-
-constexpr size_t kQueueHeader = 256;   // bytes before a ray queue's records
-constexpr size_t kQueueRayBytes = 48;  // 3 float4: (o, d.x), (d.yz, att.xy), (att.z, seed, pixel, 0)
 
 // Host-side compact-scene build from the reference records; validates the
 // buffers.  Returns RT_OK or RT_ERR_BAD_SCENE with a message in *err.

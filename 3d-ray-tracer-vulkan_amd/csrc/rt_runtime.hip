@@ -223,10 +223,6 @@ static constexpr int kMaxSlots = 8;   // rt_render_async frame slots per device
 #ifndef RT_LEAF_ALIGN
 #define RT_LEAF_ALIGN 2
 #endif
-// Option split_bounce's default.
-#ifndef RT_SPLIT_BOUNCE
-#define RT_SPLIT_BOUNCE 0
-#endif
 // Option accel's default: the binned-SAH tree in 8 octant
 // layouts.  Config 3 0.1279-0.1288 ms per frame against 0.2962-0.2964 for the
 // reference's tree and order, config 5 1.24-1.25 against 7.84 ms, config 6
@@ -311,10 +307,6 @@ struct PerDevice {
     std::vector<BandList> band_lists;   // rt_render_batch_device's band lists on this device
     std::vector<Graph> graphs;
     unsigned     graph_next = 0;
-    // option split_bounce: one ray queue per launch stream (rt_internal.h
-    // TraceArgs::queue), grown to the largest launch seen on that stream
-    struct Queue { hipStream_t s; char* base; size_t cap; };
-    std::vector<Queue> queues;
 };
 
 static constexpr size_t kMaxOrders = 16;
@@ -402,9 +394,6 @@ struct rt_ctx {
     int  leaf_align = RT_LEAF_ALIGN;   // walk records: no leaf straddles a 128-B line (a pad slot before it)
     int  accel = RT_ACCEL;         // at the next upload: 0 = the reference's tree and order; 1 / 8 = the
                                    //   SAH tree in 1 / 8 (octant) layouts (accel_build.h)
-    int  split_bounce = RT_SPLIT_BOUNCE;   // accel walk: paths alive at this bounce finish in a second kernel
-                                   //   (trace_queue), 64 per wave (0 = one kernel)
-    int  queue_waves = 8;          // trace_queue's one-wave workgroups per CU
     int  order_split = 0;          // heavy_first: only tiles costing >= this percent of the costliest go first
                                    //   (in cost order); the rest keep their raster order (0 = all by cost)
     int  order_frames = 0;         // heavy_first, several frames per launch: the non-leading tiles row by row
@@ -904,8 +893,7 @@ static std::vector<uint64_t> launch_key(const TraceArgs& a, hipStream_t s) {
             (uint64_t)a.coop_lanes, (uint64_t)a.ext, (uint64_t)a.sky_enabled,
             (uint64_t)a.frame_count, P(a.accum), (uint64_t)a.walk, (uint64_t)a.block_waves, P(a.tile_order),
             (uint64_t)a.heavy_tiles, (uint64_t)(a.aux_stream != nullptr), (uint64_t)a.heavy_fused, P(a.heavy_px),
-            (uint64_t)a.n_heavy_px, P(a.tile_mask), (uint64_t)a.coop_walk, (uint64_t)a.coop_win,
-            (uint64_t)a.split_bounce, P(a.queue_count), (uint64_t)a.queue_waves};
+            (uint64_t)a.n_heavy_px, P(a.tile_mask), (uint64_t)a.coop_walk, (uint64_t)a.coop_win};
     for (int f = 0; f < a.n_frames; ++f) {
         const CamF& c = a.cams[f];
         for (float v : {c.ox, c.oy, c.oz, c.lx, c.ly, c.lz, c.hx, c.hy, c.hz, c.vx, c.vy, c.vz}) k.push_back(F(v));
@@ -913,44 +901,7 @@ static std::vector<uint64_t> launch_key(const TraceArgs& a, hipStream_t s) {
     return k;
 }
 
-// Option split_bounce (accel walk, no extensions): the stream's ray queue for
-// a launch of tw x th x n_frames pixels.  A queue that must grow waits for
-// the launches already on its stream, which may still use it.
-static int attach_queue(const rt_ctx* ctx, PerDevice& p, TraceArgs& a, hipStream_t s) {
-    a.split_bounce = 0;
-    a.queue_count = nullptr;
-    a.queue = nullptr;
-    if (!p.scene.n_layouts || ctx->split_bounce <= 0 || a.ext || ctx->split_bounce >= a.max_bounces) return RT_OK;
-    const size_t rays = (size_t)a.tw * (size_t)a.th * (size_t)a.n_frames;
-    PerDevice::Queue* q = nullptr;
-    for (auto& x : p.queues)
-        if (x.s == s) { q = &x; break; }
-    if (!q || q->cap < rays) {
-        if (q) {
-            RT_HIP_CHECK(hipStreamSynchronize(s));
-            (void)hipFree(q->base);
-            q->base = nullptr;
-            q->cap = 0;
-        } else {
-            p.queues.push_back(PerDevice::Queue{s, nullptr, 0});
-            q = &p.queues.back();
-        }
-        void* base = nullptr;
-        RT_HIP_CHECK(hipMalloc(&base, kQueueHeader + rays * kQueueRayBytes));
-        RT_HIP_CHECK(hipMemsetAsync(base, 0, kQueueHeader, s));      // stream-ordered before the launch
-        q->base = static_cast<char*>(base);
-        q->cap = rays;
-    }
-    a.split_bounce = ctx->split_bounce;
-    a.queue_count = reinterpret_cast<unsigned*>(q->base);
-    a.queue = reinterpret_cast<float4*>(q->base + kQueueHeader);
-    a.queue_waves = std::max(1, p.n_cu * ctx->queue_waves);
-    return RT_OK;
-}
-
-static int launch(const rt_ctx* ctx, PerDevice& p, const TraceArgs& a_in, hipStream_t s) {
-    TraceArgs a = a_in;
-    if (int rq = attach_queue(ctx, p, a, s)) return rq;
+static int launch(const rt_ctx* ctx, PerDevice& p, const TraceArgs& a, hipStream_t s) {
     // Only a frame of two launches (heavy tiles on an auxiliary stream,
     // heavy_stream 1) gains from a graph: its fork and join become edges.  A
     // single launch (the fused heavy tiles, or none) goes straight to the
@@ -1148,8 +1099,6 @@ int rt_destroy(rt_ctx* ctx) {
         }
         if (p.d_accum) (void)hipFree(p.d_accum);
         if (p.d_spheres) (void)hipFree(p.d_spheres);
-        for (auto& q : p.queues) (void)hipFree(q.base);
-        p.queues.clear();
         if (p.d_rgba) (void)hipFree(p.d_rgba);
         if (p.d_rad) (void)hipFree(p.d_rad);
         if (p.ev0) (void)hipEventDestroy(p.ev0);
@@ -1979,10 +1928,6 @@ int rt_set_option(rt_ctx* ctx, const char* name, int64_t value) {
         ctx->learn_device = (int)value;
     } else if (std::strcmp(name, "leaf_align") == 0 && value >= 0 && value <= 2) {
         ctx->leaf_align = (int)value;                   // takes effect at the next rt_upload_scene
-    } else if (std::strcmp(name, "split_bounce") == 0 && value >= 0 && value <= 64) {
-        ctx->split_bounce = (int)value;
-    } else if (std::strcmp(name, "queue_waves") == 0 && value >= 1 && value <= 64) {
-        ctx->queue_waves = (int)value;
     } else if (std::strcmp(name, "accel") == 0 && (value == 0 || value == 1 || value == 8)) {
         ctx->accel = (int)value;                        // takes effect at the next rt_upload_scene
     } else if (std::strcmp(name, "heavy_stream") == 0 && value >= 0 && value <= 2) {
@@ -2023,8 +1968,6 @@ int rt_get_option(rt_ctx* ctx, const char* name, int64_t* value) {
     else if (std::strcmp(name, "learn_device") == 0) *value = ctx->learn_device;
     else if (std::strcmp(name, "leaf_align") == 0) *value = ctx->leaf_align;
     else if (std::strcmp(name, "accel") == 0) *value = ctx->accel;
-    else if (std::strcmp(name, "split_bounce") == 0) *value = ctx->split_bounce;
-    else if (std::strcmp(name, "queue_waves") == 0) *value = ctx->queue_waves;
     else if (std::strcmp(name, "walk_bytes") == 0) *value = ctx->dev.empty() ? 0 : (int64_t)walk_bytes(ctx->dev[0]);
     else if (std::strcmp(name, "accel_used") == 0) *value = ctx->dev.empty() ? 0 : ctx->dev[0].scene.n_layouts;
     else if (std::strcmp(name, "leaf_align_used") == 0) *value = ctx->dev.empty() ? 0 : ctx->dev[0].scene.padded;

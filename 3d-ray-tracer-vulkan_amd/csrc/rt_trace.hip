@@ -366,21 +366,6 @@ __device__ __forceinline__ bool accel_take(float t, int tri, float closest, int 
     return t < closest || (t == closest && tri < hit);
 }
 
-// Occupancy floors (waves per SIMD): trace_simple's, see below.
-#ifndef RT_SIMPLE_WPE
-#define RT_SIMPLE_WPE 8
-#endif
-// option accel's kernels (A/B builds: make variant FLAGS=-DRT_ACCEL_WPE=7)
-#ifndef RT_ACCEL_WPE
-#define RT_ACCEL_WPE RT_SIMPLE_WPE
-#endif
-// 1 = an accel leaf's triangle is loaded only once its box is hit (a second
-// dependent round trip for the quarter of leaf visits that test it, two loads
-// fewer for the rest); 0 = with the leaf's box, as the reference-order walk
-#ifndef RT_ACC_LAZY
-#define RT_ACC_LAZY 0
-#endif
-
 // ------------------------------------------------------------ cooperative walk --
 #ifndef RT_CHAIN
 // The lockstep walk's next records: 2 = buffer loads whose address is one
@@ -739,27 +724,6 @@ constexpr int kFeatPad = 256;     // the production kernels (cooperative tail, n
                                   //   with pad slots (leaf_align); every other variant always reads pad bits
 constexpr int kFeatAccel = 512;   // option accel: the accel records and rules, packed records, the
                                   //   reference-order fallback
-constexpr int kFeatQueue = 1024;  // split launch: paths alive at bounce split_bounce go to the ray queue
-
-// A split launch's hand-over (kFeatQueue): the lanes whose paths are still
-// alive append their state to the launch stream's ray queue, one atomic per
-// wave, in lane order (so a wave's survivors stay together).
-__device__ __forceinline__ void enqueue(const TraceArgs& a, bool alive, V3 o, V3 d, V3 att, uint32_t seed, int lx,
-                                        int lyo) {
-    const uint64_t m = __ballot(alive);
-    if (m == 0) return;
-    const int lane = threadIdx.x & 63;
-    const int first = __ffsll((long long)m) - 1;
-    unsigned base = 0;
-    if (lane == first) base = atomicAdd(&a.queue_count[0], (unsigned)__popcll(m));
-    base = (unsigned)__builtin_amdgcn_readlane((int)base, first);
-    if (alive) {
-        float4* r = a.queue + 3 * (size_t)(base + (unsigned)lanes_below(m));
-        r[0] = make_float4(o.x, o.y, o.z, d.x);
-        r[1] = make_float4(d.y, d.z, att.x, att.y);
-        r[2] = make_float4(att.z, __uint_as_float(seed), __int_as_float(lyo * a.tw + lx), 0.0f);
-    }
-}
 constexpr unsigned kHeavyLaneMark = kLearnHeavyMark;   // rt_internal.h
 
 // One pixel of a heavy tile, the whole wave on it (option heavy_fused, the
@@ -822,40 +786,153 @@ __device__ __forceinline__ void heavy_pixel(const TraceArgs& a, int f, int lx, i
     }
 }
 
-// The bounce loop of one lane's path (compute_dynamic_ray.comp:179-236) from
-// bounce b0, with its pixel's final store.  Shared by trace_simple (b0 = 0,
-// after the primary ray) and trace_queue (the queued paths of a split
-// launch, from bounce split_bounce).  Wave-uniform control: every lane of the
-// wave calls it.
-template <bool COUNT, bool DIAG, int FEAT, int WALK>
-__device__ __forceinline__ void trace_path(const TraceArgs& a, int b0, V3 o, V3 d, V3 att, uint32_t seed, bool alive,
-                                           int lx, int lyo, int coop_lanes, uint4* fr,
-                                           unsigned long long& c_seg, unsigned long long& c_node,
-                                           unsigned long long& c_tri, unsigned long long& c_mat,
-                                           unsigned long long& d_iters, unsigned long long& d_windows,
-                                           unsigned long long& d_coop_t, unsigned long long& d_lane_windows) {
+// Occupancy floor for trace_simple (waves per SIMD).  Unconstrained, the
+// walk-2 build takes ~70 VGPRs (7 waves).  One frame at a time more waves did
+// not pay (round 1); with frames in flight the device is throughput-bound and
+// they do: at 7 (round 2, before the compact records) config 3 0.328-0.330 vs
+// 0.344-0.346 ms (profiles/r02/occupancy/wpe7); with the compact records, 8
+// waves (64 VGPRs, ~20 B per lane of per-segment spills) beat 7 on config 3
+// (0.298-0.299 vs 0.301-0.302 ms) and config 6 (0.343-0.344 vs 0.364-0.365),
+// config 5 even (profiles/r02/occupancy/wpe8).  The frontier (heavy-tile)
+// instantiations keep their registers.
+#ifndef RT_SIMPLE_WPE
+#define RT_SIMPLE_WPE 8
+#endif
+// option accel's kernels (A/B builds: make variant FLAGS=-DRT_ACCEL_WPE=7)
+#ifndef RT_ACCEL_WPE
+#define RT_ACCEL_WPE RT_SIMPLE_WPE
+#endif
+// 1 = an accel leaf's triangle is loaded only once its box is hit (a second
+// dependent round trip for the quarter of leaf visits that test it, two loads
+// fewer for the rest); 0 = with the leaf's box, as the reference-order walk
+#ifndef RT_ACC_LAZY
+#define RT_ACC_LAZY 0
+#endif
+template <bool COUNT, bool DIAG = false, int FEAT = 0, int WALK = 2>
+__global__ __launch_bounds__(256)
+__attribute__((amdgpu_waves_per_eu((FEAT & kFeatFrontier) ? 1 : (FEAT & kFeatAccel) ? RT_ACCEL_WPE : RT_SIMPLE_WPE)))
+void trace_simple(TraceArgs a) {
+    // Pad bits (leaf_align): the production kernels (cooperative tail, no
+    // extensions or frontier tail) read them only when built with kFeatPad, so
+    // scenes with packed records run the packed code; every other variant
+    // reads them always.
     constexpr bool ACC = (FEAT & kFeatAccel) != 0;
     constexpr bool PAD = !ACC && ((FEAT & kFeatPad) || (FEAT & (kFeatExt | kFeatFrontier)) || !(FEAT & kFeatCoopTail));
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
+    // frontier_walk's per-wave frontiers (kFCap entries per wave; dynamic LDS,
+    // sized by the launch for variants with kFeatFrontier or kFeatFused)
+    extern __shared__ uint4 fr[];
+    // One wave = one tile of 64 pixels, (8 << s) x (8 >> s) with s = a.wave_tile
+    // (s = 0: 8x8, the reference's local_size 8x8x1, compute_dynamic_ray.comp:157);
+    // a workgroup = block_waves (4 or 1) such tiles side by side.
+    const int s = a.wave_tile;
+    const int tw_w = 8 << s, th_w = 8 >> s;
+    // Heavy-first order (option heavy_first): workgroup k takes the k-th most
+    // expensive tile of an earlier launch of the same frame, so the frame's
+    // longest waves start first.  Only the tile each wave traces changes.
+    // With split_n > 0 (the heavy-tile launch) the first split_n tiles of the
+    // order are traced one pixel per wave (64 workgroups per tile): the wave's
+    // single live lane walks every segment cooperatively (frontier walk).
+    int bx = blockIdx.x, by = blockIdx.y, sub = -1;
+    unsigned long long skip_lanes = 0;                   // heavy pixels this tile wave leaves out
+    // Diagnostic record of this wave and the tile of its per-pixel walk
+    // lengths (diag builds): the wave's index in the grid, except in a fused
+    // launch in a tile order, where tile t's wave records at n_heavy_px + t and
+    // its pixels at t * 64 + lane (a learning launch in another camera's order
+    // still gives each tile its own record: rt_learn.hip reads them by tile).
+    const int k_wave = (blockIdx.y * gridDim.x + blockIdx.x) * a.block_waves + wave;
+    int rec_id = k_wave, tile_id = k_wave, hq = -1;
+    if (a.tile_order) {                                  // 1-D grid over the ordered tiles
+        const int k = blockIdx.x;
+        int t;
+        if ((FEAT & kFeatFused) && k < a.n_heavy_px) {   // a heavy pixel (tile * 64 + lane), dispatched first
+            hq = a.heavy_px[k];
+            t = hq >> 6;
+            sub = hq & 63;
+        } else if (k < 64 * a.split_n) {
+            t = a.tile_order[k >> 6];
+            sub = k & 63;
+        } else {
+            t = a.tile_order[k - 63 * a.split_n - ((FEAT & kFeatFused) ? a.n_heavy_px : 0)];
+            if ((FEAT & kFeatFused) && a.tile_mask) skip_lanes = a.tile_mask[t];
+            if (FEAT & kFeatFused) {
+                rec_id = a.n_heavy_px + t;
+                tile_id = t;
+            } else if (DIAG && a.diag_lane && a.split_n == 0) {
+                // a learning launch in a reused order without heavy pixels (a
+                // schedule that does not split them out): records by tile too,
+                // as rt_learn.hip reads them
+                rec_id = t;
+                tile_id = t;
+            }
+        }
+        bx = t % a.tiles_x;
+        by = t / a.tiles_x;
+    }
+    unsigned long long* drec = nullptr;
+    if (DIAG) {
+        drec = a.diag + kDiagWords * (size_t)rec_id;
+        diag_stamp(drec, 0);
+    }
+    if ((FEAT & kFeatFused) && sub >= 0) {               // a heavy tile's pixel, dispatched first
+        const int hf = by / a.tiles_y;                   // its frame of the batch
+        const int hy = (by - hf * a.tiles_y) * th_w + (sub >> (3 + s));
+        heavy_pixel<COUNT>(a, hf, bx * tw_w + (sub & (tw_w - 1)), hy, hf * a.th + hy, fr);
+        if (DIAG) {
+            diag_stamp(drec, 1);
+            if (lane == 0) {
+                drec[4] = 0;
+                drec[5] = 0;
+                drec[6] = 0;
+                drec[7] = 0;
+                // a learning launch: a pixel traced as heavy keeps its place
+                // among the heavy ones (its lockstep length is unknown here)
+                if (a.diag_lane && hq >= 0) a.diag_lane[hq] = kHeavyLaneMark;
+            }
+        }
+        return;
+    }
+    const int tl = sub >= 0 ? sub : lane;                // the tile pixel this lane traces
+    const int col = bx * a.block_waves + wave;           // wave-tile column
+    const int fr_i = by / a.tiles_y;                     // the wave's frame of the batch (tile rows of frame
+    by -= fr_i * a.tiles_y;                              //   f follow those of frame f - 1)
+    const int lx = col * tw_w + (tl & (tw_w - 1));
+    const int ly = by * th_w + (tl >> (3 + s));          // row within the frame's rows
+    const int lyo = fr_i * a.th + ly;                    // output row
+    // (a per-frame band list's -1 entries are padding rows: no pixel)
+    const bool pixel = lx < a.tw && ly < a.th && (sub < 0 || lane == 0) && !((skip_lanes >> lane) & 1ull) &&
+                       (a.list_stride == 0 || a.band_list[fr_i * a.list_stride + ly / a.band_h] >= 0);
+    const int coop_lanes = sub >= 0 ? 64 : a.coop_lanes;
     const float4* __restrict__ nodes = a.scene.nodes;
     const float4* __restrict__ leafs = a.scene.leafs;
     const float4* __restrict__ pairs = a.scene.pairs;
     const int end = a.scene.end;                         // node index end (walk 0, the frontier tail)
     const int wend = WALK == 2 ? a.scene.end2 : end;     // the lockstep walk's end: slots for walk 2
+    unsigned long long c_seg = 0, c_node = 0, c_tri = 0, c_mat = 0;
+    unsigned long long d_iters = 0, d_windows = 0, d_coop_t = 0;   // diag builds only
+    unsigned long long d_lane_windows = 0;           // diag: cooperative windows spent on this lane's walks
+
+    uint32_t seed = 0;
+    V3 o = {0.f, 0.f, 0.f}, d = {0.f, 0.f, 1.f};
+    if (pixel) {
+        const int x = a.x0 + lx, y = frame_row(a, fr_i, ly);
+        if ((FEAT & kFeatExt) && (a.ext & kExtAccumulate)) {
+            // extension: a new sample per frame; frame 0 is the reference's seed (:164)
+            seed = (uint32_t)(y * a.width + x) + (uint32_t)a.frame_count * (uint32_t)(a.width * a.height);
+            primary_ray_seeded(a, fr_i, x, y, seed, o, d);
+        } else {
+            primary_ray(a, fr_i, x, y, seed, o, d);
+        }
+    }
+    V3 att = {1.0f, 1.0f, 1.0f};
+    bool alive = pixel;
+
     // The bounce loop (:179) is wave-uniform: a lane whose path has ended
     // stays in it with alive = false, so the cooperative tail below can use
     // every lane of the wave.
-    for (int b = b0; b < a.max_bounces; ++b) {
+    for (int b = 0; b < a.max_bounces; ++b) {
         if (__ballot(alive) == 0) break;
-        if ((FEAT & kFeatQueue) && b == a.split_bounce) {
-            // kernel 1 of a split launch: the paths still alive go to the
-            // launch's ray queue (one atomic per wave), and trace_queue
-            // finishes them in dense waves
-            enqueue(a, alive, o, d, att, seed, lx, lyo);
-            alive = false;
-            break;
-        }
         float closest = kTMax;
         int hit = -1;
         const V3 inv = {1.0f / d.x, 1.0f / d.y, 1.0f / d.z};              // :89
@@ -1098,129 +1175,6 @@ __device__ __forceinline__ void trace_path(const TraceArgs& a, int b0, V3 o, V3 
     }
     // A path still alive here ran no bounce at all (max_bounces 0): black.
     if (alive) finish_pixel<FEAT>(a, lx, lyo, V3{0.0f, 0.0f, 0.0f});
-}
-
-// Occupancy floor for trace_simple (waves per SIMD).  Unconstrained, the
-// walk-2 build takes ~70 VGPRs (7 waves).  One frame at a time more waves did
-// not pay (round 1); with frames in flight the device is throughput-bound and
-// they do: at 7 (round 2, before the compact records) config 3 0.328-0.330 vs
-// 0.344-0.346 ms (profiles/r02/occupancy/wpe7); with the compact records, 8
-// waves (64 VGPRs, ~20 B per lane of per-segment spills) beat 7 on config 3
-// (0.298-0.299 vs 0.301-0.302 ms) and config 6 (0.343-0.344 vs 0.364-0.365),
-// config 5 even (profiles/r02/occupancy/wpe8).  The frontier (heavy-tile)
-// instantiations keep their registers.
-template <bool COUNT, bool DIAG = false, int FEAT = 0, int WALK = 2>
-__global__ __launch_bounds__(256)
-__attribute__((amdgpu_waves_per_eu((FEAT & kFeatFrontier) ? 1 : (FEAT & kFeatAccel) ? RT_ACCEL_WPE : RT_SIMPLE_WPE)))
-void trace_simple(TraceArgs a) {
-    // Pad bits (leaf_align): the production kernels (cooperative tail, no
-    // extensions or frontier tail) read them only when built with kFeatPad, so
-    // scenes with packed records run the packed code; every other variant
-    // reads them always.
-    const int lane = threadIdx.x & 63;
-    const int wave = threadIdx.x >> 6;
-    // frontier_walk's per-wave frontiers (kFCap entries per wave; dynamic LDS,
-    // sized by the launch for variants with kFeatFrontier or kFeatFused)
-    extern __shared__ uint4 fr[];
-    // One wave = one tile of 64 pixels, (8 << s) x (8 >> s) with s = a.wave_tile
-    // (s = 0: 8x8, the reference's local_size 8x8x1, compute_dynamic_ray.comp:157);
-    // a workgroup = block_waves (4 or 1) such tiles side by side.
-    const int s = a.wave_tile;
-    const int tw_w = 8 << s, th_w = 8 >> s;
-    // Heavy-first order (option heavy_first): workgroup k takes the k-th most
-    // expensive tile of an earlier launch of the same frame, so the frame's
-    // longest waves start first.  Only the tile each wave traces changes.
-    // With split_n > 0 (the heavy-tile launch) the first split_n tiles of the
-    // order are traced one pixel per wave (64 workgroups per tile): the wave's
-    // single live lane walks every segment cooperatively (frontier walk).
-    int bx = blockIdx.x, by = blockIdx.y, sub = -1;
-    unsigned long long skip_lanes = 0;                   // heavy pixels this tile wave leaves out
-    // Diagnostic record of this wave and the tile of its per-pixel walk
-    // lengths (diag builds): the wave's index in the grid, except in a fused
-    // launch in a tile order, where tile t's wave records at n_heavy_px + t and
-    // its pixels at t * 64 + lane (a learning launch in another camera's order
-    // still gives each tile its own record: rt_learn.hip reads them by tile).
-    const int k_wave = (blockIdx.y * gridDim.x + blockIdx.x) * a.block_waves + wave;
-    int rec_id = k_wave, tile_id = k_wave, hq = -1;
-    if (a.tile_order) {                                  // 1-D grid over the ordered tiles
-        const int k = blockIdx.x;
-        int t;
-        if ((FEAT & kFeatFused) && k < a.n_heavy_px) {   // a heavy pixel (tile * 64 + lane), dispatched first
-            hq = a.heavy_px[k];
-            t = hq >> 6;
-            sub = hq & 63;
-        } else if (k < 64 * a.split_n) {
-            t = a.tile_order[k >> 6];
-            sub = k & 63;
-        } else {
-            t = a.tile_order[k - 63 * a.split_n - ((FEAT & kFeatFused) ? a.n_heavy_px : 0)];
-            if ((FEAT & kFeatFused) && a.tile_mask) skip_lanes = a.tile_mask[t];
-            if (FEAT & kFeatFused) {
-                rec_id = a.n_heavy_px + t;
-                tile_id = t;
-            } else if (DIAG && a.diag_lane && a.split_n == 0) {
-                // a learning launch in a reused order without heavy pixels (a
-                // schedule that does not split them out): records by tile too,
-                // as rt_learn.hip reads them
-                rec_id = t;
-                tile_id = t;
-            }
-        }
-        bx = t % a.tiles_x;
-        by = t / a.tiles_x;
-    }
-    unsigned long long* drec = nullptr;
-    if (DIAG) {
-        drec = a.diag + kDiagWords * (size_t)rec_id;
-        diag_stamp(drec, 0);
-    }
-    if ((FEAT & kFeatFused) && sub >= 0) {               // a heavy tile's pixel, dispatched first
-        const int hf = by / a.tiles_y;                   // its frame of the batch
-        const int hy = (by - hf * a.tiles_y) * th_w + (sub >> (3 + s));
-        heavy_pixel<COUNT>(a, hf, bx * tw_w + (sub & (tw_w - 1)), hy, hf * a.th + hy, fr);
-        if (DIAG) {
-            diag_stamp(drec, 1);
-            if (lane == 0) {
-                drec[4] = 0;
-                drec[5] = 0;
-                drec[6] = 0;
-                drec[7] = 0;
-                // a learning launch: a pixel traced as heavy keeps its place
-                // among the heavy ones (its lockstep length is unknown here)
-                if (a.diag_lane && hq >= 0) a.diag_lane[hq] = kHeavyLaneMark;
-            }
-        }
-        return;
-    }
-    const int tl = sub >= 0 ? sub : lane;                // the tile pixel this lane traces
-    const int col = bx * a.block_waves + wave;           // wave-tile column
-    const int fr_i = by / a.tiles_y;                     // the wave's frame of the batch (tile rows of frame
-    by -= fr_i * a.tiles_y;                              //   f follow those of frame f - 1)
-    const int lx = col * tw_w + (tl & (tw_w - 1));
-    const int ly = by * th_w + (tl >> (3 + s));          // row within the frame's rows
-    const int lyo = fr_i * a.th + ly;                    // output row
-    // (a per-frame band list's -1 entries are padding rows: no pixel)
-    const bool pixel = lx < a.tw && ly < a.th && (sub < 0 || lane == 0) && !((skip_lanes >> lane) & 1ull) &&
-                       (a.list_stride == 0 || a.band_list[fr_i * a.list_stride + ly / a.band_h] >= 0);
-    const int coop_lanes = sub >= 0 ? 64 : a.coop_lanes;
-    unsigned long long c_seg = 0, c_node = 0, c_tri = 0, c_mat = 0;
-    unsigned long long d_iters = 0, d_windows = 0, d_coop_t = 0;   // diag builds only
-    unsigned long long d_lane_windows = 0;           // diag: cooperative windows spent on this lane's walks
-
-    uint32_t seed = 0;
-    V3 o = {0.f, 0.f, 0.f}, d = {0.f, 0.f, 1.f};
-    if (pixel) {
-        const int x = a.x0 + lx, y = frame_row(a, fr_i, ly);
-        if ((FEAT & kFeatExt) && (a.ext & kExtAccumulate)) {
-            // extension: a new sample per frame; frame 0 is the reference's seed (:164)
-            seed = (uint32_t)(y * a.width + x) + (uint32_t)a.frame_count * (uint32_t)(a.width * a.height);
-            primary_ray_seeded(a, fr_i, x, y, seed, o, d);
-        } else {
-            primary_ray(a, fr_i, x, y, seed, o, d);
-        }
-    }
-    trace_path<COUNT, DIAG, FEAT, WALK>(a, 0, o, d, V3{1.0f, 1.0f, 1.0f}, seed, pixel, lx, lyo, coop_lanes, fr,
-                                        c_seg, c_node, c_tri, c_mat, d_iters, d_windows, d_coop_t, d_lane_windows);
     if (COUNT) flush_counters(a.counters, c_seg, c_node, c_tri, c_mat);
     if (DIAG) {
         diag_stamp(drec, 1);
@@ -1244,44 +1198,6 @@ void trace_simple(TraceArgs a) {
             drec[6] = d_coop_t;
             drec[7] = d_sum;
         }
-    }
-}
-
-// Kernel 2 of a split launch: the paths trace_simple queued at bounce
-// split_bounce, 64 per wave in queue order, through the same bounce loop
-// (trace_path).  A fixed grid of one-wave workgroups loops over the queue; the
-// last wave out resets the queue for the stream's next launch.
-template <bool COUNT, int FEAT>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RT_ACCEL_WPE)))
-void trace_queue(TraceArgs a) {
-    const int lane = threadIdx.x & 63;
-    const unsigned count = __builtin_nontemporal_load(&a.queue_count[0]);
-    unsigned long long c_seg = 0, c_node = 0, c_tri = 0, c_mat = 0;
-    unsigned long long d_iters = 0, d_windows = 0, d_coop_t = 0, d_lane_windows = 0;
-    for (unsigned pk = blockIdx.x; pk * 64u < count; pk += gridDim.x) {
-        const unsigned i = pk * 64u + (unsigned)lane;
-        const bool valid = i < count;
-        V3 o = {0.f, 0.f, 0.f}, d = {0.f, 0.f, 1.f}, att = {1.f, 1.f, 1.f};
-        uint32_t seed = 0;
-        int lx = 0, lyo = 0;
-        if (valid) {
-            const float4* r = a.queue + 3 * (size_t)i;
-            const float4 r0 = r[0], r1 = r[1], r2 = r[2];
-            o = {r0.x, r0.y, r0.z};
-            d = {r0.w, r1.x, r1.y};
-            att = {r1.z, r1.w, r2.x};
-            seed = __float_as_uint(r2.y);
-            const int p = __float_as_int(r2.z);
-            lyo = p / a.tw;
-            lx = p - lyo * a.tw;
-        }
-        trace_path<COUNT, false, FEAT, 2>(a, a.split_bounce, o, d, att, seed, valid, lx, lyo, a.coop_lanes, nullptr,
-                                          c_seg, c_node, c_tri, c_mat, d_iters, d_windows, d_coop_t, d_lane_windows);
-    }
-    if (COUNT) flush_counters(a.counters, c_seg, c_node, c_tri, c_mat);
-    if (lane == 0 && atomicAdd(&a.queue_count[1], 1u) == gridDim.x - 1) {
-        a.queue_count[0] = 0;   // every wave has read the count: the queue is empty for the next launch
-        a.queue_count[1] = 0;
     }
 }
 
@@ -1386,37 +1302,15 @@ hipError_t launch_trace(const TraceArgs& a, hipStream_t stream, int* kernels) {
     else hipLaunchKernelGGL((trace_simple<false, false, F, W>), grid, block, ((F) & kFeatFrontier) ? shm_f : 0, stream, ao);
     if (a.scene.n_layouts > 0) {
         // option accel (walk 2 records; the launcher never splits heavy tiles
-        // or pixels out of an accel launch, and there is no frontier tail).
-        // A split launch (split_bounce, no extensions): trace_simple hands the
-        // paths alive at split_bounce to the stream's ray queue, trace_queue
-        // finishes them.
-        const bool split = a.split_bounce > 0 && a.split_bounce < a.max_bounces && a.queue_count &&
-                           !(feat & kFeatExt);
-#define RT_QUEUE(F)                                                                                             \
-    if (a.counters) hipLaunchKernelGGL((trace_queue<true, F>), dim3(a.queue_waves), dim3(64), 0, stream, ao);    \
-    else hipLaunchKernelGGL((trace_queue<false, F>), dim3(a.queue_waves), dim3(64), 0, stream, ao);
-        if (split) {
-            if (feat & kFeatCoopTail) {
-                RT_SIMPLE(kFeatCoopTail | kFeatAccel | kFeatQueue, 2)
-                if (hipGetLastError() != hipSuccess) return hipErrorLaunchFailure;
-                RT_QUEUE(kFeatCoopTail | kFeatAccel)
-            } else {
-                RT_SIMPLE(kFeatAccel | kFeatQueue, 2)
-                if (hipGetLastError() != hipSuccess) return hipErrorLaunchFailure;
-                RT_QUEUE(kFeatAccel)
-            }
-            if (kernels) *kernels = 2;
-        } else {
-            switch (feat & ~kFeatFrontier) {
-                case kFeatCoopTail:
-                    if (a.coop_win == 32) RT_SIMPLE(kFeatCoopTail | kFeatAccel | kFeatWin32, 2)
-                    else RT_SIMPLE(kFeatCoopTail | kFeatAccel, 2)
-                    break;
-                case 0: RT_SIMPLE(kFeatAccel, 2) break;
-                default: RT_SIMPLE(kFeatCoopTail | kFeatExt | kFeatAccel, 2) break;
-            }
+        // or pixels out of an accel launch, and there is no frontier tail)
+        switch (feat & ~kFeatFrontier) {
+            case kFeatCoopTail:
+                if (a.coop_win == 32) RT_SIMPLE(kFeatCoopTail | kFeatAccel | kFeatWin32, 2)
+                else RT_SIMPLE(kFeatCoopTail | kFeatAccel, 2)
+                break;
+            case 0: RT_SIMPLE(kFeatAccel, 2) break;
+            default: RT_SIMPLE(kFeatCoopTail | kFeatExt | kFeatAccel, 2) break;
         }
-#undef RT_QUEUE
     } else if (a.walk == 2) {
         switch (feat) {
             case kFeatCoopTail:

@@ -952,7 +952,7 @@ def main() -> None:
                                                                       "reuse_order", "order_split", "hw_queues",
                                                                       "coop_window", "coop_window_used",
                                                                       "leaf_align", "leaf_align_used",
-                                                                      "accel", "accel_used", "split_bounce",
+                                                                      "accel", "accel_used",
                                                                       "wave_tile_used")},
                              "concurrent_launches": renderer.get_option("concurrent_launches"),
                              "heavy_tiles_used": heavy_used,

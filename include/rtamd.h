@@ -262,14 +262,6 @@ int rt_render_poll(rt_ctx* ctx, uint64_t ticket, int* done);
  *                   walk's own.  Heavy tiles / pixels are not
  *                   split out of accel launches (heavy_first still orders
  *                   the tiles)
- *   "split_bounce"  accel walk, no extensions: b in 1..max_bounces-1 = the
- *                   paths still alive at bounce b leave the frame's kernel for
- *                   a ray queue of the launch's stream and a second kernel
- *                   (trace_queue) finishes them 64 per wave, so the few long
- *                   late-bounce paths of a tile no longer hold a whole wave
- *                   (DESIGN.md §4b); 0 = one kernel.  Same pixels and counters
- *   "queue_waves"   split launches: trace_queue's one-wave workgroups per CU
- *                   (1..64, default 8)
  *   "accel_used"    (rt_get_option only) the current scene's layouts on device
  *                   0 (0 = the reference's tree)
  *   "walk_bytes"    (rt_get_option only) bytes of the records one ray walks on

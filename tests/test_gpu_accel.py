@@ -55,12 +55,11 @@ def _upload(r, built, nl):
     assert r.get_option("accel_used") == nl
 
 
-@pytest.mark.parametrize("split", [0, 1, 2])
 @pytest.mark.parametrize("nl", [1, 8])
 @pytest.mark.parametrize("k,b", [(1, 1), (2, 2), (2, 10), (3, 4), (6, 4)])
-def test_accel_full_frame(acc, k, b, nl, split):
-    """split: option split_bounce (the paths alive at that bounce finish in
-    trace_queue, 64 per wave): same frames, same counters."""
+def test_accel_full_frame(acc, k, b, nl):
+    """Whole frames of configs 1, 2, 3 and 6: frames equal the oracle's, the
+    counters the accel model's."""
     from rtamd import configs
     cfg = configs.get(k)
     built = cfg.build()
@@ -68,14 +67,9 @@ def test_accel_full_frame(acc, k, b, nl, split):
     _upload(acc, built, nl)
     ref = _oracle(built, cam, cfg.width, cfg.height, b)
     model = _model(built, cam, cfg.width, cfg.height, b, nl)
-    old = acc.get_option("split_bounce")
-    try:
-        acc.set_option("split_bounce", split)
-        for stats in (False, True, False):         # learning, counting, then the production build
-            rgba, rad, st = acc.render(cam, cfg.width, cfg.height, b, radiance=True, stats=stats)
-            _check(rgba, rad, st, ref, model, f"config {k} b{b} layouts {nl} split {split}")
-    finally:
-        acc.set_option("split_bounce", old)
+    for stats in (False, True, False):         # learning, counting, then the production build
+        rgba, rad, st = acc.render(cam, cfg.width, cfg.height, b, radiance=True, stats=stats)
+        _check(rgba, rad, st, ref, model, f"config {k} b{b} layouts {nl}")
 
 
 @pytest.mark.parametrize("nl", [1, 8])
@@ -186,9 +180,8 @@ def test_accel_extensions(acc):
         acc.upload_spheres(np.zeros((0, 8), np.float32))
 
 
-@pytest.mark.parametrize("split", [0, 2])
 @pytest.mark.parametrize("cfg_k", [3, 4, 5, 6])
-def test_accel_bench_setting_whole_frame(acc, cfg_k, split):
+def test_accel_bench_setting_whole_frame(acc, cfg_k):
     """BASELINE configs 3, 4, 5 (1M triangles, 3840x2160, 8 bounces) and 6 as
     whole frames under bench.py's N = 1 setting with the default options
     (accel 8, 4 launches in flight counted): the learning launch, the
@@ -203,17 +196,14 @@ def test_accel_bench_setting_whole_frame(acc, cfg_k, split):
     W, H, B = cfg.width, cfg.height, cfg.max_bounces
     ref = _oracle(built, cam, W, H, B)
     model = _model(built, cam, W, H, B, 8)
-    old = acc.get_option("split_bounce")
     try:
         acc.set_option("concurrent_launches", 4)
-        acc.set_option("split_bounce", split)
         for stats in (False, False, True):
             rgba, rad, st = _bands_device(acc, cam, W, H, B, H, 1, 0, stats=stats)
-            _check(rgba, rad, st if stats else None, ref, model, f"config {cfg_k} whole frame split {split}")
+            _check(rgba, rad, st if stats else None, ref, model, f"config {cfg_k} whole frame")
         assert st["pixels"] == W * H
     finally:
         acc.set_option("concurrent_launches", 1)
-        acc.set_option("split_bounce", old)
 
 
 def test_accel_is_the_default():

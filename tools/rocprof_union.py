@@ -51,13 +51,10 @@ def main():
                     help="plain launches after the timed region (default: the bench line's "
                          "roofline.plain_kernels_after_timed, else 0)")
     args = ap.parse_args()
-    # plain launches: trace_simple<false, false, ...>, and with option
-    # split_bounce each frame's second kernel trace_queue<false, ...>
-    rows = [r for r in csv.DictReader(open(args.trace))
-            if "trace_simple<false, false" in r["Kernel_Name"] or "trace_queue<false" in r["Kernel_Name"]]
+    # plain launches: trace_simple<false, false, ...>
+    rows = [r for r in csv.DictReader(open(args.trace)) if "trace_simple<false, false" in r["Kernel_Name"]]
     rows.sort(key=lambda r: int(r["Dispatch_Id"]))
-    per = 2 if any("trace_queue" in r["Kernel_Name"] for r in rows) else 1
-    n = args.steps * args.launches_per_step * per
+    n = args.steps * args.launches_per_step
     if len(rows) < n:
         raise SystemExit(f"{len(rows)} plain trace launches in the trace, need {n}")
     skip = args.skip_last
