@@ -506,6 +506,116 @@ class ShareTracer:
         return self.plan.off[self.rank][k0 % self.G]
 
 
+# --- contiguous spans of a batch (weak scaling; bench.py --partition spans) ---
+#
+# A batch of G frames is one column of G x H rows (frame f's rows at
+# [f * H, (f + 1) * H)).  Rank r traces one contiguous span of it, cut at
+# whole bands, rank 0's span root_weight times the others': whole frames where
+# the span covers them, a run of bands of one frame at either end.  Whole
+# frames are the kernel's most efficient launch (a band share of every frame
+# traces ~20% slower per pixel, profiles/r05/r5k/emu), and the spans tile the
+# batch column in rank order, so rank 0 receives every other span straight into
+# the batch's frames (RCCL point-to-point in one group) and traces its own span
+# in place: there is no stack and no assembly pass.
+
+
+class SpanPlan:
+    """Rank r's span of a batch of n_frames frames: bands [cuts[r],
+    cuts[r + 1]) of the batch's n_frames * (height / band_h) bands, i.e. rows
+    [row0[r], row0[r] + rows[r]) of the batch column.  launches[r] lists its
+    launches: (frame, band_lo, band_hi, out_row), one frame each, the whole
+    frame when (band_lo, band_hi) == (0, height / band_h), written at row
+    out_row of the rank's span buffer (rank 0: the batch column from row0[0])."""
+
+    def __init__(self, height: int, band_h: int, world: int, n_frames: int, root_weight: float = 1.0):
+        if height % band_h:
+            raise ValueError(f"spans: band_h ({band_h}) must divide the height ({height})")
+        if not root_weight >= 0:
+            raise ValueError("spans: root_weight must be >= 0")
+        self.height, self.band_h, self.world, self.n_frames = height, band_h, world, n_frames
+        self.root_weight = root_weight
+        self.bpf = height // band_h
+        total = n_frames * self.bpf
+        w = np.array([root_weight] + [1.0] * (world - 1))
+        cum = np.concatenate([[0.0], np.cumsum(w)])
+        self.cuts = [int(round(total * c / cum[-1])) for c in cum]
+        self.cuts[-1] = total
+        self.row0 = [c * band_h for c in self.cuts[:-1]]
+        self.rows = [(self.cuts[r + 1] - self.cuts[r]) * band_h for r in range(world)]
+        self.per_rank = max(self.rows)
+        self.counts = [r // n_frames for r in self.rows]      # rows per frame, on average
+        self.launches = []
+        for r in range(world):
+            out, b, out_row = [], self.cuts[r], 0
+            while b < self.cuts[r + 1]:
+                f = b // self.bpf
+                lo = b - f * self.bpf
+                hi = min(self.bpf, self.cuts[r + 1] - f * self.bpf)
+                out.append((f, lo, hi, out_row))
+                out_row += (hi - lo) * band_h
+                b = f * self.bpf + hi
+            self.launches.append(out)
+
+    def recv_slices(self):
+        """(rank, row0, rows) of every span rank 0 receives."""
+        return [(r, self.row0[r], self.rows[r]) for r in range(1, self.world) if self.rows[r] > 0]
+
+
+class SpanTracer:
+    """The launches of one rank's span of a batch (bench.py's trace for
+    --partition spans; tests/test_gpu_dist.py replays them): launch j of
+    plan.launches[rank] traces one frame's bands band_lo .. band_hi - 1
+    (rt_render_batch_device with that band list; no list for a whole frame),
+    packed at row out_row of the span buffer."""
+
+    def __init__(self, ctx, width: int, height: int, max_bounces: int, plan: SpanPlan, rank: int = 0):
+        self.ctx, self.W, self.H, self.B, self.plan, self.rank = ctx, width, height, max_bounces, plan, rank
+        self.launches = plan.launches[rank]
+        self._lists = [None if (lo, hi) == (0, plan.bpf) else np.arange(lo, hi, dtype=np.int32)
+                       for (_, lo, hi, _) in self.launches]
+
+    def launch(self, cam, j: int, stream: int, rgba_ptr, rad_ptr, stats=None) -> None:
+        """Launch j of the rank's span (cam: the CameraUBO of its frame) on
+        `stream` into rgba_ptr / rad_ptr, the span buffer's row out_row
+        (device pointers; rad_ptr may be None)."""
+        L = lib()
+        bl = self._lists[j]
+        check(L.rt_render_batch_device(self.ctx, C.byref(cam), 1, self.W, self.H, self.B,
+                                       self.plan.band_h if bl is not None else 0,
+                                       bl.ctypes.data_as(C.POINTER(C.c_int32)) if bl is not None else None,
+                                       len(bl) if bl is not None else 0, rgba_ptr, rad_ptr, stream,
+                                       C.byref(stats) if stats is not None else None))
+
+
+def exchange_spans(column, span, plan: SpanPlan, group=None) -> None:
+    """One batch of the spans partition.  Rank 0: column is the batch's
+    [n_frames * height, W, C] frames, its own span traced in place; every
+    other span is received straight into its rows.  Rank r > 0: span is its
+    [>= rows[r], W, C] span buffer, sent to rank 0.  One batch_isend_irecv
+    (one RCCL group); on return the current stream is ordered after it."""
+    import torch.distributed as dist
+    rank = dist.get_rank(group)
+    buf = column if rank == 0 else span
+    staged = dist.get_backend(group) == "gloo" and buf is not None and buf.is_cuda   # gloo moves host memory
+    glob = (lambda r: dist.get_global_rank(group, r)) if group is not None else (lambda r: r)
+    ops, landings = [], []
+    if rank == 0:
+        for r, y0, n in plan.recv_slices():
+            dst = column[y0:y0 + n]
+            if staged:
+                landings.append((dst, dst.cpu()))
+                dst = landings[-1][1]
+            ops.append(dist.P2POp(dist.irecv, dst, glob(r), group))
+    elif plan.rows[rank] > 0:
+        src = span[: plan.rows[rank]]
+        ops.append(dist.P2POp(dist.isend, src.cpu() if staged else src, glob(0), group))
+    if ops:
+        for w in dist.batch_isend_irecv(ops):
+            w.wait()
+    for dst, host in landings:
+        dst.copy_(host)
+
+
 # --- rotating row blocks (strong scaling, an option) -------------------------
 #
 # Each frame is cut into N contiguous row pieces, one per rank: rank 0's piece

@@ -11,24 +11,32 @@ N = 1).  The timed region covers exactly K frames, synchronised on both
 sides.
 
 With N > 1 ranks (one process per GPU, torch.distributed over RCCL), every
-frame is tiled over ALL ranks and gathered to rank 0 over xGMI (one
-dist.gather per exchange batch) and assembled there (one index_select), all
-inside the timed region; the collective's and the assembly's streams run at
-high priority (--exchange-priority).
+frame is tiled over ALL ranks and its rows sent to rank 0 over xGMI inside
+the timed region.
 --scaling weak (default): a step is N frames of the render loop (every rank
-  traces one frame's worth of pixels per step, the per-GPU work of N = 1),
-  exchanged every step.  --scaling strong: a step is ONE frame.
---partition bands (default): interleaved band_h-row bands dealt out by a
-  weighted round robin (rank 0 weighted --root-weight: it also receives and
-  assembles every frame; rtamd.dist.band_owners).  A rank traces its bands of
-  F frames per launch (rt_render_batch_device; weak: F = N, the step), D
-  launches in flight; heavy-first order with option order_split 15.  Where
-  that deal gives the other ranks unequal bands (N = 8), the deal runs on over
-  the N frames of a launch instead (--deal, rtamd.dist.dealt_bands; one band
-  list per frame, rt_render_batch_lists_device).
+  traces one frame's worth of pixels per step, the per-GPU work of N = 1).
+  --scaling strong: a step is ONE frame.
+--partition spans (default): an exchange batch of G frames is one column of
+  G x H rows cut into N contiguous spans of band_h-row bands, rank 0's
+  --root-weight times the others' (it also receives every span).  A rank
+  traces its span one frame per launch (whole frames, a band run at either
+  end; rtamd.dist.SpanPlan / SpanTracer), D launches in flight; rank 0 traces
+  its span in place in the batch's frames and receives the others' straight
+  into them (one group of RCCL point-to-point receives per batch), so there
+  is no assembly pass.  The exchange is ordered by the host, one batch
+  behind, and the launch streams never wait on a device event.
+--partition bands: interleaved band_h-row bands dealt out by a weighted round
+  robin (rank 0 weighted --root-weight: it also receives and assembles every
+  frame; rtamd.dist.band_owners).  A rank traces its bands of F frames per
+  launch (rt_render_batch_device; weak: F = N, the step), D launches in
+  flight; heavy-first order with option order_split 15; one dist.gather per
+  exchange batch and one index_select assembly on rank 0.  Where that deal
+  gives the other ranks unequal bands (N = 8), the deal runs on over the N
+  frames of a launch instead (--deal, rtamd.dist.dealt_bands; one band list
+  per frame, rt_render_batch_lists_device).
 --partition pieces: N contiguous row pieces, rank r tracing position
   (r + f) mod N of frame f, all N pieces of a launch from different frames
-  (rt_render_batch_lists_device).
+  (rt_render_batch_lists_device); gathered and assembled as the bands.
 --partition tiles: the screen tiled gx x gy over the ranks (2 x 2 at N = 4,
   BASELINE config 4), one tile per rank, gathered and assembled likewise.
 --gather radiance: the float radiance (the sqrt'd colour before
@@ -160,6 +168,24 @@ def default_root_weight(world: int) -> float:
 # order_split; a rank's batched launch of band shares runs faster with the
 # waves at once on neighbouring tiles; neutral at N = 1)
 ORDER_SPLIT_N_GT_1 = 15
+
+
+def default_span_weight(world: int) -> float:
+    """spans: rank 0's span relative to the others' (it also receives every
+    other span of the batch).  Emulated at the driver's 20 steps
+    (profiles/r05/r5v, r5w): N = 2 1.0 (0.1437 ms per step, both ranks even;
+    0.9 leaves rank 1 the slower), N = 4 0.9 (0.162 vs 0.171 at 1.0), N = 8
+    0.8 (0.163 vs 0.171 at 0.9)."""
+    return 1.0 if world <= 2 else (0.9 if world <= 4 else 0.8)
+
+
+def default_span_batch(world: int) -> int:
+    """spans: frames per exchange batch (bench.py fits it to divide the timed
+    frames).  Fewer, larger batches cost the launch streams less host order
+    (N = 8 at 200 steps: 64 frames 0.143 ms per step, 32 0.146; r5v), but the
+    batch exchanged after the last trace is exposed: 32 at N = 2 and 8, 16 at
+    N = 4 (0.162 vs 0.170 ms per step at 20 steps, r5w)."""
+    return 16 if world == 4 else 32
 
 
 def default_piece_weight(world: int) -> float:
@@ -295,10 +321,11 @@ def main() -> None:
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", type=int, default=3, help="BASELINE config index (3 = headline)")
-    ap.add_argument("--partition", choices=("bands", "tiles", "pieces"), default="bands",
-                    help="N > 1: how a frame is tiled over the ranks: bands = weighted interleaved row bands "
-                         "(default); tiles = gx x gy rectangles (2 x 2 at N = 4); pieces = N contiguous row "
-                         "pieces rotated frame by frame (a launch of N frames holds every piece once)")
+    ap.add_argument("--partition", choices=("bands", "tiles", "pieces", "spans"), default="spans",
+                    help="N > 1: how a frame is tiled over the ranks: bands = weighted interleaved row bands; tiles = gx x gy rectangles (2 x 2 at N = 4); pieces = N contiguous row "
+                         "pieces rotated frame by frame (a launch of N frames holds every piece once); spans = "
+                         "one contiguous span of each exchange batch's rows per rank (whole frames, a run of "
+                         "bands at its ends), received by rank 0 straight into the frames (no assembly; the default)")
     ap.add_argument("--scaling", choices=("weak", "strong"), default="weak",
                     help="N > 1: weak = a step is N frames of the render loop, each tiled over all ranks and "
                          "gathered (every rank traces one frame's worth per step; default); strong = a step is "
@@ -315,7 +342,8 @@ def main() -> None:
     ap.add_argument("--inflight", type=int, default=0, help="launches in flight per rank (0 = default_inflight)")
     ap.add_argument("--batch", type=int, default=0, help="frames per launch (whole / bands; 0 = default_batch)")
     ap.add_argument("--exchange-every", type=int, default=0,
-                    help="N > 1: frames per exchange batch (a multiple of --batch; 0 = launches in flight x batch)")
+                    help="N > 1: frames per exchange batch (a multiple of --batch; 0 = default_span_batch for "
+                         "spans, launches in flight x batch otherwise; spans fit it to divide the timed frames)")
     ap.add_argument("--ring", type=int, default=2,
                     help="N > 1: exchange batches of slots in the ring (>= 2); a batch's slots are retraced only "
                          "after the exchange ring - 1 batches back")
@@ -366,7 +394,8 @@ def main() -> None:
     import rtamd
     from rtamd import configs
     from rtamd._lib import CameraUBO, Stats, check
-    from rtamd.dist import SharePlan, ShareTracer, TilePlan, assemble_shares, band_list, gather_stack, gather_tiles
+    from rtamd.dist import (SharePlan, ShareTracer, SpanPlan, SpanTracer, TilePlan, assemble_shares, band_list,
+                            exchange_spans, gather_stack, gather_tiles)
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -438,22 +467,28 @@ def main() -> None:
     weak = dist_on and args.scaling == "weak"
     step_frames = world if weak else 1                         # frames per step (weak scaling: N)
     D = args.inflight if args.inflight > 0 else default_inflight(world)
-    F = (args.batch if args.batch > 0 else default_batch(world, weak)) if mode in ("whole", "bands", "pieces") else 1
+    F = (args.batch if args.batch > 0 else default_batch(world, weak)) \
+        if mode in ("whole", "bands", "pieces", "spans") else 1
     F = min(F, 16)
-    if mode in ("bands", "pieces"):
+    if mode in ("bands", "pieces", "spans"):
         # one exchange per D launches: every exchange costs the host a
         # collective and an assembly and the streams a join, so fewer, larger
         # ones (one per launch measured 0.426 vs 0.348 ms per step at N = 8,
         # emulated: profiles/r03/evidence_r3h)
-        G = args.exchange_every if args.exchange_every > 0 else D * F
+        G = args.exchange_every if args.exchange_every > 0 else \
+            (default_span_batch(world) if mode == "spans" else D * F)
         G = max(F, (G + F - 1) // F * F)                       # whole launches per exchange batch
+        if mode == "spans":
+            # a span covers a whole batch: the timed frames are whole batches
+            while G > F and (args.steps * step_frames) % G:
+                G -= F
     elif mode == "tiles":
         G = args.exchange_every if args.exchange_every > 0 else D
     else:
         G = D * F                                              # N = 1: the slot ring
     # ring of exchange batches: enough for the D launches in flight plus the
     # batch being exchanged
-    R = max(2, args.ring, -(-D * F // G) + 1)
+    R = max(3 if mode == "spans" else 2, args.ring, -(-D * F // G) + 1)
     rad_on = dist_on and args.gather == "radiance"
     band_h = args.band
     plan = tplan = None
@@ -477,6 +512,16 @@ def main() -> None:
         rgba_slots = torch.empty((R, plan.per_rank, W, 4), dtype=torch.uint8, device=dev)
         rad_slots = torch.empty((R, plan.per_rank, W, 3), dtype=torch.float32, device=dev) if rad_on else None
         px_per_frame = plan.counts[rank] * W
+    elif mode == "spans":
+        if H % band_h:
+            raise SystemExit(f"--partition spans: --band ({band_h}) must divide the height ({H})")
+        plan = SpanPlan(H, band_h, world, G, args.root_weight if args.root_weight >= 0 else default_span_weight(world))
+        # rank 0: the batch's frames (its own span traced in place, the others
+        # received into them); rank r: its span
+        rows = G * H if rank == 0 else plan.per_rank
+        rgba_slots = torch.empty((R, rows, W, 4), dtype=torch.uint8, device=dev)
+        rad_slots = torch.empty((R, rows, W, 3), dtype=torch.float32, device=dev) if rad_on else None
+        px_per_frame = plan.rows[rank] * W // G
     elif mode == "tiles":
         tplan = TilePlan(W, H, world, G)
         src_index = torch.as_tensor(tplan.src, device=dev)
@@ -488,9 +533,14 @@ def main() -> None:
         rgba_slots = torch.empty((D, F * H, W, 4), dtype=torch.uint8, device=dev)
         rad_slots = None
         px_per_frame = W * H
-    if emu:
+    if emu and mode == "spans":
+        # rank 0: the others' spans land in its frames (a device copy per span,
+        # the bytes RCCL's receives write); rank r: its span read once (the send)
+        emu_buf = torch.zeros((plan.per_rank, W, 4), dtype=torch.uint8, device=dev)
+        emu_land = torch.empty_like(emu_buf)
+    elif emu:
         if mode not in ("bands", "pieces"):
-            raise SystemExit("BENCH_EMULATE emulates --partition bands / pieces")
+            raise SystemExit("BENCH_EMULATE emulates --partition bands / pieces / spans")
         emu_buf = torch.zeros((world * plan.per_rank, W, 4) if rank == 0 else (1,), dtype=torch.uint8, device=dev)
         emu_land = torch.empty_like(emu_buf if rank == 0 else rgba_slots[0])
     streams = [torch.cuda.Stream(dev) for _ in range(D)]
@@ -514,7 +564,8 @@ def main() -> None:
             c = cam_cache[k] = camera_path(cfg, args.camera_path, 1, k)[0]
         return c
 
-    tracer = ShareTracer(ctx, W, H, B, mode, rank, plan=plan, tplan=tplan, band_h=band_h, batch=G)
+    tracer = SpanTracer(ctx, W, H, B, plan, rank) if mode == "spans" else \
+        ShareTracer(ctx, W, H, B, mode, rank, plan=plan, tplan=tplan, band_h=band_h, batch=G)
 
     def trace(k0, n, s, rgba_ptr, rad_ptr, stats=False):
         """Frames k0 .. k0 + n - 1 (one exchange batch) in one launch on stream s
@@ -526,6 +577,24 @@ def main() -> None:
             cams = cam_arrays[ck] = (CameraUBO * n)(*[cam_of(k).ubo for k in range(k0, k0 + n)])
         tracer.launch(cams, k0, n, s.cuda_stream, rgba_ptr, rad_ptr, st)
         return st.as_dict() if stats else None
+
+    def trace_span(k0, jl, s, rgba_ptr, rad_ptr, stats=False):
+        """Launch jl of this rank's span of the batch that starts at frame k0
+        (rtamd.dist.SpanTracer)."""
+        st_ = Stats() if stats else None
+        tracer.launch(cam_of(k0 + tracer.launches[jl][0]).ubo, jl, s.cuda_stream, rgba_ptr, rad_ptr, st_)
+        return st_.as_dict() if stats else None
+
+    def span_ptrs(h, out_row):
+        """Where a span launch writes: row out_row of the span (rank 0: of its
+        span inside the batch's frames) in ring slot h."""
+        y = out_row + (plan.row0[0] if rank == 0 else 0)
+        return rgba_slots[h, y].data_ptr(), (rad_slots[h, y].data_ptr() if rad_on else None)
+
+    # spans: every launch's pointers per ring slot, made once (no tensor
+    # indexing on the host between launches)
+    span_tab = [[span_ptrs(h, orow) for (_, _, _, orow) in tracer.launches] for h in range(R)] \
+        if mode == "spans" else None
 
     def out_ptrs(k0, j):
         """Where launch j (frames k0 ...) writes: its slot of the ring."""
@@ -607,8 +676,159 @@ def main() -> None:
         last["frames"] = list(range(k - n, k))
         st["k"] = ((k + G - 1) // G) * G            # the next phase starts a fresh batch
 
+    # ---- spans: the exchange in host order ------------------------------------
+    # A wait packet in a launch stream's queue (hipStreamWaitEvent) slows every
+    # trace in flight: the dist path at world size 1 ran 0.145 ms per frame with
+    # the slot ring's device-side waits against 0.126 host-ordered and 0.124 for
+    # N = 1 (profiles/r05/r5q, r5r).  So the launch streams never wait: the host
+    # orders the exchange.  A rank r > 0 sends its span of batch b (one
+    # batch_isend_irecv, one RCCL group) once the host has seen batch b's
+    # launches end, which it checks after queueing batch b + 1 (one batch
+    # behind: the GPU always has a batch of traces queued).  Rank 0 posts batch
+    # b's receives (one per rank, straight into the batch's frames) before it
+    # traces its own span of batch b.  A ring slot is traced into again only
+    # after the host has seen its last exchange complete (ring R >= 3 leaves a
+    # batch of slack).  Sending each launch's rows as it ended instead (smaller
+    # last exchange) ran the senders 25% slower in the emulation (r5t, r5u).
+    span_sent = [None] * R     # r > 0: event after the last send out of slot h
+    span_recv = [None] * R     # rank 0: (works, landings, k_end, e0) of slot h's pending receive group
+    send_q = []                # r > 0: (launch end events, slot, out_row, rows) of traced batches not yet sent
+    staged = backend == "gloo"  # gloo moves host memory: device rows staged through the host
+
+    def span_send(timed):
+        e_ends, h, orow, nr = send_q.pop(0)
+        for e_end in e_ends:
+            e_end.synchronize()                        # host: the batch's launches have ended
+        e0 = e1 = None
+        if timed:
+            e0, e1 = timing_event(), timing_event()
+            e0.record(main_stream)
+        src = rgba_slots[h][orow:orow + nr]
+        if emu:
+            if os.environ.get("BENCH_EMULATE_NOX") != "1":
+                emu_land[:nr].copy_(src)               # the send's read of the rows
+        else:
+            ops = [dist.P2POp(dist.isend, src.cpu() if staged else src, 0)]
+            if rad_on:
+                rs = rad_slots[h][orow:orow + nr]
+                ops.append(dist.P2POp(dist.isend, rs.cpu() if staged else rs, 0))
+            for w in dist.batch_isend_irecv(ops):
+                w.wait()                               # NCCL: main_stream waits for the send (host free)
+        if timed:
+            e1.record(main_stream)
+            ex_evs.append((e0, e1))
+        ev = torch.cuda.Event()
+        ev.record(main_stream)
+        span_sent[h] = ev
+
+    def span_post_recvs(k0, h, timed):
+        """Rank 0: batch k0's receives of every other span, into slot h's frames."""
+        e0 = None
+        if timed:
+            e0 = timing_event()
+            e0.record(main_stream)
+        col = rgba_slots[h]
+        works, landings = [], []
+        if emu:
+            if os.environ.get("BENCH_EMULATE_NOX") != "1":
+                for r_, jl_list in recv_plan:          # the bytes the receives write
+                    for y0, nr in jl_list:
+                        col[y0:y0 + nr].copy_(emu_buf[:nr])
+        else:
+            ops = []
+            for r_, jl_list in recv_plan:
+                for y0, nr in jl_list:
+                    for buf in ((col, rad_slots[h]) if rad_on else (col,)):
+                        dst = buf[y0:y0 + nr]
+                        if staged:
+                            landings.append((dst, torch.empty(dst.shape, dtype=dst.dtype)))
+                            dst = landings[-1][1]
+                        ops.append(dist.P2POp(dist.irecv, dst, r_))
+            if ops:
+                works = dist.batch_isend_irecv(ops)
+        span_recv[h] = (works, landings, k0 + G, e0)
+
+    def span_complete_recvs(h, timed):
+        works, landings, k_end, e0 = span_recv[h]
+        span_recv[h] = None
+        for w in works:
+            w.wait()                                   # NCCL: main_stream waits (gloo: the host)
+        for dst, host in landings:
+            dst.copy_(host)
+        if timed and e0 is not None:
+            e1 = timing_event()
+            e1.record(main_stream)
+            ex_evs.append((e0, e1))
+        ev = torch.cuda.Event()
+        ev.record(main_stream)
+        gathered[h] = ev
+        if not emu:
+            last["rgba"] = rgba_slots[h][:G * H].view(G, H, W, 4)
+            last["rad"] = rad_slots[h][:G * H].view(G, H, W, 3) if rad_on else None
+            last["frames"] = list(range(k_end - G, k_end))
+
+    # rank 0's receives per batch: for every rank r > 0, its launches' rows of
+    # the batch column in launch order (the order rank r sends them)
+    recv_plan = [(r_, [(plan.row0[r_], plan.rows[r_])]) for r_ in range(1, world) if plan.rows[r_]] \
+        if mode == "spans" else []
+
+    def phase_spans(n_frames, evs=None):
+        """n_frames frames in whole exchange batches: per batch this rank's
+        span launches, round robin over the D streams, the exchange streamed
+        behind them in host order (above)."""
+        timed = evs is not None
+        end = st["k"] + n_frames
+        while st["k"] < end:
+            k0 = st["k"]
+            h = (k0 // G) % R
+            if rank == 0:
+                if span_recv[h] is not None:           # the slot's last batch: its receives complete
+                    span_complete_recvs(h, timed)
+                if gathered[h] is not None:
+                    gathered[h].synchronize()
+                span_post_recvs(k0, h, timed)
+            else:
+                while any(q[1] == h for q in send_q):  # the slot's last batch: every launch sent
+                    span_send(timed)
+                if span_sent[h] is not None:
+                    span_sent[h].synchronize()
+            used = []
+            for jl in range(len(tracer.launches)):
+                j = st["j"]
+                s = streams[j % D]
+                rp, dp = span_tab[h][jl]
+                if timed:
+                    e = (timing_event(), timing_event())
+                    e[0].record(s)
+                trace_span(k0, jl, s, rp, dp)
+                if timed:
+                    e[1].record(s)
+                    evs.append((e, 1))
+                if s not in used:
+                    used.append(s)
+                st["j"] = j + 1
+            st["k"] = k0 + G
+            if rank and plan.rows[rank]:
+                ends = []
+                for s in used:
+                    ev = torch.cuda.Event()
+                    ev.record(s)
+                    ends.append(ev)
+                send_q.append((ends, h, 0, plan.rows[rank]))
+                while len(send_q) > 1:                 # the batch before: sent once its launches end
+                    span_send(timed)
+        # the phase's exchanges complete before it ends
+        while send_q:
+            span_send(timed)
+        if rank == 0:
+            k_ends = sorted((span_recv[h][2], h) for h in range(R) if span_recv[h] is not None)
+            for _, h in k_ends:
+                span_complete_recvs(h, timed)
+
     def phase(n_frames, evs=None):
         """n_frames frames: launches of up to F frames, never across an exchange batch."""
+        if mode == "spans":
+            return phase_spans(n_frames, evs)
         end = st["k"] + n_frames
         while st["k"] < end:
             k0 = st["k"]
@@ -655,9 +875,18 @@ def main() -> None:
     count_rgba = torch.empty((max(rgba_slots[0].numel() // 4, 1), 4), dtype=torch.uint8, device=dev)
 
     def count_frames(ks):
-        """This rank's work in frames ks (counting launches, one frame each)."""
+        """This rank's work in frames ks (counting launches, one frame each);
+        spans: in the batches that start at frames ks, one span launch each."""
         tot = {k2: 0.0 for k2 in ("pixels", "segments", "node_visits", "tri_tests", "mat_reads")}
         ms = []
+        if mode == "spans":
+            for k in ks:
+                for jl, (_, _, _, orow) in enumerate(tracer.launches):
+                    d = trace_span(k, jl, main_stream, count_rgba[orow * W].data_ptr(), None, stats=True)
+                    for k2 in tot:
+                        tot[k2] += d[k2]
+                    ms.append(d["ms"])
+            return tot, ms
         for k in ks:
             d = trace(k, 1, main_stream, count_rgba.data_ptr(), None, stats=True)
             for k2 in tot:
@@ -678,7 +907,13 @@ def main() -> None:
         dist.all_reduce(n_settle, op=dist.ReduceOp.MIN)
     n_settle = int(n_settle.item()) * F
     k_t0 = after(after(0, n_settle), W_fr)
-    if args.camera_path == "static":
+    if mode == "spans":
+        if args.camera_path == "static":
+            one = count_frames([k_t0])[0]
+            loc = {k2: v * (K // G) for k2, v in one.items()}
+        else:
+            loc, _ = count_frames(range(k_t0, k_t0 + K, G))
+    elif args.camera_path == "static":
         one = count_frames([k_t0])[0]
         loc = {k2: v * K for k2, v in one.items()}
     else:
@@ -744,6 +979,7 @@ def main() -> None:
         for s in streams:
             s.wait_stream(main_stream)
     phase(K, evs)
+    host_ms = (time.perf_counter() - t_start) * 1e3      # the host's enqueue time of the timed launches
     if lean:
         ends = [timing_event() for _ in streams] + ([timing_event()] if asm_stream is not main_stream else [])
         for e, s in zip(ends, streams + ([asm_stream] if asm_stream is not main_stream else [])):
@@ -777,7 +1013,7 @@ def main() -> None:
             ce = max(ce, b0)
     busy += (ce - cs) if ce is not None else 0.0
     exchange_ms = float(sum(a.elapsed_time(b) for a, b in ex_evs))
-    mine = torch.tensor([rank, px_per_frame, launch_ms, region_ms / K, busy / K, exchange_ms / K],
+    mine = torch.tensor([rank, px_per_frame, launch_ms, region_ms / K, busy / K, exchange_ms / K, host_ms / K],
                         dtype=torch.float64, device=dev)
     if dist_on and not emu:
         allr = [torch.empty_like(mine) for _ in range(world)]
@@ -786,12 +1022,13 @@ def main() -> None:
         allr = [mine]
     per_rank = [{"rank": int(x[0]), "pixels_per_frame": int(x[1]), "kernel_ms": round(float(x[2]), 4),
                  "device_ms_per_frame": round(float(x[3]), 4), "trace_busy_ms_per_frame": round(float(x[4]), 4),
-                 "exchange_ms_per_frame": round(float(x[5]), 4)} for x in (t.tolist() for t in allr)]
+                 "exchange_ms_per_frame": round(float(x[5]), 4),
+                 "host_enqueue_ms_per_frame": round(float(x[6]), 4)} for x in (t.tolist() for t in allr)]
 
     heavy_used = renderer.get_option("heavy_tiles_used")   # of the last timed launch
     heavy_px_used = renderer.get_option("heavy_pixels_used")
     lanes = lane_utilisation(renderer, L, ctx, lambda: trace(k_t0, 1, main_stream, count_rgba.data_ptr(), None),
-                             dev) if not args.no_lanes else None
+                             dev) if not (args.no_lanes or mode == "spans") else None
     verified = None
     single = None
     if dist_on and not emu and rank == 0 and last["rgba"] is not None:
@@ -851,7 +1088,7 @@ def main() -> None:
     # the camera stops (orbit): the first frames at rest, timed one by one (the
     # first repeat of a camera learns its own heavy-first order)
     stop = None
-    if args.camera_path != "static":
+    if args.camera_path != "static" and mode != "spans":
         k_last = k_t0 + K - 1
         ms = []
         for i in range(8):
@@ -908,6 +1145,11 @@ def main() -> None:
                     f"launches in flight x {F} frames per "
                     f"launch (one band list per frame), {gather_kind} gather of every {G} frames + rank-0 "
                     f"assembly{shared}")
+        elif mode == "spans":
+            part = (f"every batch of {G} frames cut into {world} contiguous spans of {band_h}-row bands (rank 0 "
+                    f"weight {plan.root_weight}, rows per rank {plan.rows}), one launch per frame of a span (whole "
+                    f"frames, a band run at either end), {D} launches in flight, {gather_kind} point-to-point "
+                    f"receives of every span straight into rank 0's frames (no assembly){shared}")
         elif mode == "tiles":
             part = (f"one frame per step tiled {tplan.gx} x {tplan.gy} over {world} ranks (tiles "
                     f"{tplan.rects}), {D} frames in flight, {gather_kind} gather of every {G} frames + rank-0 "
@@ -939,7 +1181,7 @@ def main() -> None:
                 "frames_per_launch": F,
                 "launches_in_flight": D,
                 "exchange_every_frames": G if dist_on else None,
-                "band_h": band_h if mode in ("bands", "pieces") else None,
+                "band_h": band_h if mode in ("bands", "pieces", "spans") else None,
                 "root_weight": plan.root_weight if plan is not None else None,
                 "deal": (("rotate" if plan.lists else "fixed") if mode == "bands" else None),
                 "gather": ("rgba8 + float radiance" if rad_on else "rgba8") if dist_on else None,

@@ -263,7 +263,7 @@ def _share_worker(rank, world, port, q, kind, arg, n_frames, W, H, B):
     import torch.distributed as dist
     from oracle import oracle_lib
     from rtamd import configs
-    from rtamd.dist import SharePlan, TilePlan, gather_shares, gather_tiles
+    from rtamd.dist import SharePlan, SpanPlan, TilePlan, exchange_spans, gather_shares, gather_tiles
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
@@ -271,7 +271,30 @@ def _share_worker(rank, world, port, q, kind, arg, n_frames, W, H, B):
         args = (built.model_vertex_data, built.model_material_data, built.flat_bvh_data)
         cams = _cams(n_frames, W, H)
         traced = 0
-        if kind == "tiles":
+        if kind == "spans":
+            # bench.py --partition spans: rank 0 traces its span in place in
+            # the batch's frames, the others into a span buffer; one group of
+            # point-to-point receives lands every span in rank 0's frames
+            band_h, rw = arg
+            plan = SpanPlan(H, band_h, world, n_frames, rw)
+            col = torch.zeros((n_frames * H, W, 4), dtype=torch.uint8) if rank == 0 else None
+            colr = torch.zeros((n_frames * H, W, 3), dtype=torch.float32) if rank == 0 else None
+            span = torch.zeros((plan.per_rank, W, 4), dtype=torch.uint8) if rank else None
+            spanr = torch.zeros((plan.per_rank, W, 3), dtype=torch.float32) if rank else None
+            base = plan.row0[0] if rank == 0 else 0
+            for f, lo, hi, orow in plan.launches[rank]:
+                a, r, _ = oracle_lib.render(*args, cams[f].ubo_bytes(), W, H, B,
+                                            tile=(0, lo * band_h, W, (hi - lo) * band_h), n_threads=1)
+                o = base + orow
+                n = (hi - lo) * band_h
+                (col if rank == 0 else span)[o:o + n] = torch.from_numpy(a)
+                (colr if rank == 0 else spanr)[o:o + n] = torch.from_numpy(r)
+                traced += W * n
+            exchange_spans(col, span, plan)
+            exchange_spans(colr, spanr, plan)
+            out = col.view(n_frames, H, W, 4) if rank == 0 else None
+            outr = colr.view(n_frames, H, W, 3) if rank == 0 else None
+        elif kind == "tiles":
             plan = TilePlan(W, H, world, n_frames)
             x0, y0, w, h = plan.rects[rank]
             rgba = torch.zeros((n_frames, plan.tile_px, 4), dtype=torch.uint8)
@@ -454,3 +477,45 @@ def test_share_tracer_rejects_uneven_lists():
         ShareTracer(None, 1920, 1080, 4, "tiles", 0)
     tt = ShareTracer(None, 1920, 1080, 4, "tiles", 3, tplan=TilePlan(1920, 1080, 4, 2), batch=2)
     assert tt.rect == (960, 540, 960, 540)
+
+
+@pytest.mark.parametrize("world,n_frames,band_h,rw", [(2, 3, 4, 1.0), (4, 4, 4, 0.6), (8, 8, 2, 0.8), (3, 2, 8, 0.0)])
+def test_spans_weak_scaling(world, n_frames, band_h, rw):
+    """bench.py --partition spans: each rank traces one contiguous span of the
+    batch's rows (whole frames, a run of bands at either end; rank 0's span
+    rw times the others'), rank 0 in place in the batch's frames, and one
+    group of point-to-point receives lands every other span straight in them:
+    every frame and its radiance equal the oracle's, bit for bit."""
+    W, H = 48, 40
+    traced = _run_share(world, "spans", (band_h, rw), n_frames=n_frames, W=W, H=H, B=2)
+    assert sum(traced.values()) == n_frames * W * H
+    if 0 < rw < 1.0:
+        assert traced[0] < min(traced[r] for r in range(1, world))
+    if rw == 0.0:
+        assert traced[0] == 0
+
+
+def test_span_plan_1080p():
+    """The N = 8 batch of bench.py (32 frames of 1080 rows in 8-row bands,
+    rank 0 weight 0.8): the spans tile the batch column in rank order, the
+    ranks other than 0 get the same rows to within one band, every launch is
+    one frame's band run (a whole frame or an end piece), and the launches of
+    a span pack its rows back to back."""
+    from rtamd.dist import SpanPlan, SpanTracer
+    plan = SpanPlan(1080, 8, 8, 32, 0.8)
+    assert plan.row0[0] == 0 and plan.row0[1:] == [plan.row0[r] + plan.rows[r] for r in range(7)]
+    assert plan.row0[7] + plan.rows[7] == 32 * 1080
+    others = plan.rows[1:]
+    assert max(others) - min(others) <= 8 and plan.rows[0] < min(others)
+    for r in range(8):
+        out_row = 0
+        for f, lo, hi, orow in plan.launches[r]:
+            assert 0 <= lo < hi <= 135 and orow == out_row
+            assert plan.row0[r] + orow == f * 1080 + lo * 8           # the span is the batch column
+            out_row += (hi - lo) * 8
+        assert out_row == plan.rows[r]
+        t = SpanTracer(None, 1920, 1080, 4, plan, r)
+        assert sum(1 for b in t._lists if b is None) >= 2             # mostly whole frames
+    assert plan.recv_slices() == [(r, plan.row0[r], plan.rows[r]) for r in range(1, 8)]
+    with pytest.raises(ValueError, match="divide the height"):
+        SpanPlan(1080, 16, 8, 32, 0.8)

@@ -132,6 +132,56 @@ def test_share_exchange_bit_exact(renderer, rccl_group, layout, world, rw, accel
         _check(assemble_shares(stk, plan, src), assemble_shares(stk_r, plan, src), whole, "RCCL gather_stack")
 
 
+@pytest.mark.parametrize("world,rw", [(1, 1.0), (2, 0.9), (4, 0.8), (8, 0.55), (8, 1.0)])
+@pytest.mark.parametrize("accel", [0, 8])
+def test_span_exchange_bit_exact(renderer, world, rw, accel):
+    """bench.py --partition spans: every rank's span of an exchange batch
+    traced with SpanTracer's launches (one frame's band run each) on 4 streams,
+    rank 0's in place in the batch's frames, the others' into span buffers
+    that land in rank 0's frames at the plan's rows (what the point-to-point
+    receives write; exchange_spans itself runs over gloo in test_dist.py).
+    Every frame and its radiance equal the frame traced whole."""
+    import torch
+    from rtamd import configs
+    from rtamd.dist import SpanPlan, SpanTracer
+    cfg = configs.config2()
+    renderer.set_option("accel", accel)
+    renderer.upload_scene(cfg.build())
+    renderer.set_option("accel", 0)
+    W, H, B, band_h = 320, 184, 3, 8          # 23 bands of 8 rows
+    G = 4 * world if world > 1 else 4
+    cams = _orbit_cams(W, H, G)
+    whole = _whole(renderer, cams, W, H, B)
+    plan = SpanPlan(H, band_h, world, G, rw)
+    col = torch.full((G * H, W, 4), 7, dtype=torch.uint8, device="cuda:0")
+    colr = torch.zeros((G * H, W, 3), dtype=torch.float32, device="cuda:0")
+    streams = [torch.cuda.Stream() for _ in range(4)]
+    spans = []
+    j = 0
+    for rank in range(world):
+        tracer = SpanTracer(renderer._ctx, W, H, B, plan, rank)
+        if rank == 0:
+            buf, rbuf, base = col, colr, plan.row0[0]
+        else:
+            buf = torch.full((plan.per_rank, W, 4), 7, dtype=torch.uint8, device="cuda:0")
+            rbuf = torch.zeros((plan.per_rank, W, 3), dtype=torch.float32, device="cuda:0")
+            base = 0
+            spans.append((rank, buf, rbuf))
+        for st in streams:
+            st.wait_stream(torch.cuda.current_stream())
+        for jl, (f, lo, hi, orow) in enumerate(tracer.launches):
+            tracer.launch(cams[f].ubo, jl, streams[j % 4].cuda_stream, buf[base + orow].data_ptr(),
+                          rbuf[base + orow].data_ptr())
+            j += 1
+    torch.cuda.synchronize()
+    for rank, buf, rbuf in spans:
+        y0, n = plan.row0[rank], plan.rows[rank]
+        col[y0:y0 + n].copy_(buf[:n])
+        colr[y0:y0 + n].copy_(rbuf[:n])
+    torch.cuda.synchronize()
+    _check(col.view(G, H, W, 4), colr.view(G, H, W, 3), whole, f"spans N={world} rw={rw}")
+
+
 @pytest.mark.parametrize("accel", [0, 8])
 @pytest.mark.parametrize("world", [1, 2, 4])
 def test_tile_exchange_bit_exact(renderer, rccl_group, world, accel):
