@@ -158,10 +158,40 @@ void put_f(uint32_t* w, float f) { std::memcpy(w, &f, 4); }
 
 }  // namespace
 
+uint16_t half_bits_down(float x) {
+    if (std::isnan(x)) return 0x7E00u;
+    const uint16_t sign = std::signbit(x) ? 0x8000u : 0u;
+    if (x == 0.0f) return sign;
+    if (std::isinf(x)) return (uint16_t)(sign | 0x7C00u);
+    int E;
+    (void)std::frexp(x, &E);                          // |x| in [2^(E-1), 2^E)
+    const int e = std::max(E - 1, -14);               // the half exponent (subnormals: -14)
+    const float ulp = std::ldexp(1.0f, e - 10);
+    float r = std::floor(x / ulp) * ulp;              // exact: x / ulp is a power-of-2 scaling
+    if (r > 65504.0f) r = 65504.0f;
+    if (r < -65504.0f) return 0xFC00u;                // -inf
+    if (r == 0.0f) return sign;                       // (only for x >= 0: floor of a negative is < 0)
+    const uint16_t rs = std::signbit(r) ? 0x8000u : 0u;
+    const float a = std::fabs(r);
+    int Ea;
+    (void)std::frexp(a, &Ea);
+    const int ea = Ea - 1;
+    if (ea >= -14)                                    // normal: a = (1 + m / 1024) * 2^ea
+        return (uint16_t)(rs | ((ea + 15) << 10) | ((uint32_t)std::ldexp(a, 10 - ea) - 1024u));
+    return (uint16_t)(rs | (uint32_t)std::ldexp(a, 24));   // subnormal: a = m * 2^-24
+}
+
 int accel_build(const void* vertices, size_t vertex_bytes, const void* materials, size_t material_bytes,
                 const void* bvh_nodes, size_t bvh_bytes, int n_layouts, int n_threads, AccelHost* out,
-                std::string* err) {
+                std::string* err, int format) {
     *out = AccelHost{};
+    if (format != 0 && format != 1) {
+        *err = "accel: format must be 0 or 1";
+        return -1;
+    }
+    out->format = format;
+    const int W = format ? 4 : 8;                     // words per slot
+    const int64_t LS = format ? 4 : 2;                // slots per leaf
 #ifdef ACCEL_TIMING
     const auto t_start = std::chrono::steady_clock::now();
 #endif
@@ -175,7 +205,7 @@ int accel_build(const void* vertices, size_t vertex_bytes, const void* materials
     const unsigned char* vb = static_cast<const unsigned char*>(vertices);
     const unsigned char* mb = static_cast<const unsigned char*>(materials);
     if (n_nodes == 0) {           // empty scene: no slots (two of padding), every ray misses
-        out->rec.assign(16, 0u);
+        out->rec.assign(16, 0u);                      // 64 B of padding
         return 0;
     }
 
@@ -239,9 +269,12 @@ int accel_build(const void* vertices, size_t vertex_bytes, const void* materials
     const int m = (int)B.prims.size();
     out->n_prims = m;
     ACCEL_T("duplicates dropped");
-    const int64_t slots = 3 * (int64_t)m - 1;
-    if (slots * n_layouts + 2 > (int64_t)((1u << 27) - 4)) {
-        *err = "accel: " + std::to_string(m) + " triangles: the layouts exceed 2^27 slots (4 GB)";
+    // a subtree of k triangles: k - 1 internal nodes (1 slot) and k leaves
+    const auto span = [LS](int64_t k) { return (LS + 1) * k - 1; };
+    const int64_t slots = span(m);
+    const int64_t cap = format ? (int64_t)(1u << 30) - 8 : (int64_t)(1u << 27) - 4;   // link bits; 4 GB
+    if (slots * n_layouts + 8 > cap) {
+        *err = "accel: " + std::to_string(m) + " triangles: the layouts exceed " + std::to_string(cap) + " slots";
         return -1;
     }
 
@@ -277,7 +310,7 @@ int accel_build(const void* vertices, size_t vertex_bytes, const void* materials
     out->slots = (int)slots;
     out->root_leaf = B.nodes[0].prim >= 0 ? 1 : 0;
     const size_t total = (size_t)slots * (size_t)n_layouts;
-    out->rec.assign(8 * (total + 2), 0u);
+    out->rec.assign((size_t)W * total + 16, 0u);
     std::vector<uint8_t> leaf_at(total + 1, 0);
     auto emit = [&](int o) {
         const size_t base = (size_t)o * (size_t)slots;
@@ -288,10 +321,16 @@ int accel_build(const void* vertices, size_t vertex_bytes, const void* materials
             const Item it = st.back();
             st.pop_back();
             const BNode& nd = B.nodes[it.node];
-            uint32_t* w = &out->rec[8 * it.pos];
-            for (int q = 0; q < 3; ++q) {
-                put_f(&w[q], nd.lo[q]);
-                put_f(&w[4 + q], nd.hi[q]);
+            uint32_t* w = &out->rec[(size_t)W * it.pos];
+            if (nd.prim >= 0 || format == 0) {
+                for (int q = 0; q < 3; ++q) {
+                    put_f(&w[q], nd.lo[q]);
+                    put_f(&w[4 + q], nd.hi[q]);
+                }
+            } else {
+                w[0] = half_bits_down(nd.lo[0]) | (uint32_t)half_bits_down(nd.lo[1]) << 16;
+                w[1] = half_bits_down(nd.lo[2]) | (uint32_t)half_bits_up(nd.hi[0]) << 16;
+                w[2] = half_bits_up(nd.hi[1]) | (uint32_t)half_bits_up(nd.hi[2]) << 16;
             }
             if (nd.prim >= 0) {
                 leaf_at[it.pos] = 1;
@@ -316,9 +355,9 @@ int accel_build(const void* vertices, size_t vertex_bytes, const void* materials
             }
             const bool neg = n_layouts == 8 && ((o >> nd.axis) & 1);
             const int first = neg ? nd.right : nd.left, second = neg ? nd.left : nd.right;
-            const size_t skip = it.pos + 3 * (size_t)nd.m - 1;
+            const size_t skip = it.pos + (size_t)span(nd.m);
             w[3] = (uint32_t)skip;                                 // | L(skip) << 31, below
-            const size_t pos2 = it.pos + 1 + 3 * (size_t)B.nodes[first].m - 1;
+            const size_t pos2 = it.pos + 1 + (size_t)span(B.nodes[first].m);
             st.push_back({second, pos2});
             st.push_back({first, it.pos + 1});
         }
@@ -326,13 +365,16 @@ int accel_build(const void* vertices, size_t vertex_bytes, const void* materials
         const size_t end = base + (size_t)slots;
         auto L = [&](size_t s) -> uint32_t { return s < end && leaf_at[s] ? 1u : 0u; };
         for (size_t s = base; s < end;) {
-            uint32_t* w = &out->rec[8 * s];
+            uint32_t* w = &out->rec[(size_t)W * s];
             if (leaf_at[s]) {
-                w[3] |= L(s + 2) << 31;
-                s += 2;
-            } else {
+                w[3] |= L(s + (size_t)LS) << 31;
+                s += (size_t)LS;
+            } else if (format == 0) {
                 w[3] |= L(w[3]) << 31;
                 w[7] = L(s + 1);
+                s += 1;
+            } else {
+                w[3] |= L(w[3]) << 31 | L(s + 1) << 30;
                 s += 1;
             }
         }

@@ -27,6 +27,15 @@
 // (n_layouts 1: always the lower child).  A ray walks the layout of its
 // direction's octant (sign bits of d.x, d.y, d.z), so the stackless skip walk
 // is a near-first ordered traversal.
+//
+// Format 1 ("half", option accel_half): 16-B slots.  An internal node is one
+// slot: its box in IEEE half precision rounded outward (lo down, hi up; words
+// 0-2 = lo.x | lo.y << 16, lo.z | hi.x << 16, hi.y | hi.z << 16) and word 3 =
+// skip | L(first child) << 30 | L(skip) << 31.  A leaf is four slots, the same
+// 64 bytes as format 0's two (its exact fp32 box, triangle index, v0 / e1 /
+// e2).  A subtree of m triangles takes 5m - 1 slots; a walk step of internal
+// nodes loads 16 B instead of 32.  Widened internal boxes are only entered
+// more often: every leaf box and triangle test is format 0's.
 #pragma once
 #include <cmath>
 #include <cstddef>
@@ -37,7 +46,9 @@
 namespace rtamd {
 
 struct AccelHost {
-    std::vector<uint32_t> rec;      // 8 words per slot, n_layouts * slots slots, + 2 slots of zero padding
+    std::vector<uint32_t> rec;      // 8 words per slot (format 1: 4), n_layouts * slots slots, + 64 B of zero
+                                    //   padding
+    int format = 0;                 // 0: 32-B slots, fp32 boxes; 1: 16-B slots, half-precision internal boxes
     int n_layouts = 0;              // 1 or 8
     int slots = 0;                  // slots per layout (0: empty scene)
     int root_leaf = 0;              // the root is a leaf (a one-triangle scene)
@@ -50,10 +61,16 @@ struct AccelHost {
 // Builds the records from the reference's buffers (the rt_upload_scene
 // inputs: 48-B vertex records, 16-B materials, 48-B preorder nodes).  The
 // buffers must already have passed build_host_scene's validation.  Returns
-// 0, or -1 with *err set.  n_threads: 0 = hardware concurrency.
+// 0, or -1 with *err set.  n_threads: 0 = hardware concurrency.  format: 0 or
+// 1 (above).
 int accel_build(const void* vertices, size_t vertex_bytes, const void* materials, size_t material_bytes,
                 const void* bvh_nodes, size_t bvh_bytes, int n_layouts, int n_threads, AccelHost* out,
-                std::string* err);
+                std::string* err, int format = 0);
+
+// Half-precision bits of the largest half <= x (-inf below -65504), and of the
+// smallest half >= x: the outward rounding of format 1's internal boxes.
+uint16_t half_bits_down(float x);
+inline uint16_t half_bits_up(float x) { return (uint16_t)(half_bits_down(-x) ^ 0x8000u); }
 
 // The layout a ray with direction d walks: its octant (sign bits) when
 // n_layouts is 8, else 0.

@@ -78,6 +78,8 @@ struct DevScene {
     // slots (pad slots as `ref_padded`).  n_layouts 0: no accel.
     int      n_layouts = 0;
     int      layout_slots = 0;
+    int      half = 0;          // accel format 1: 16-B slots, half-precision internal boxes (accel_build.h);
+                                //   layout_slots and end2 then count 16-B slots
     float4*  walk_ref = nullptr;
     int      end2_ref = 0;
     int      ref_padded = 0;

@@ -230,6 +230,11 @@ static constexpr int kMaxSlots = 8;   // rt_render_async frame slots per device
 #ifndef RT_ACCEL
 #define RT_ACCEL 8
 #endif
+// Option accel_half's default: the accel records' internal boxes in half
+// precision (accel_build.h format 1).
+#ifndef RT_ACCEL_HALF
+#define RT_ACCEL_HALF 0
+#endif
 
 struct PerDevice {
     int          device = 0;
@@ -392,6 +397,7 @@ struct rt_ctx {
     int  learn_alone = 0;          // heavy_first: a learning launch first waits for the device to drain
     int  learn_device = 1;         // heavy_first: learn the order on the device (rt_learn.hip; 0 = on the host)
     int  leaf_align = RT_LEAF_ALIGN;   // walk records: no leaf straddles a 128-B line (a pad slot before it)
+    int  accel_half = RT_ACCEL_HALF;   // at the next upload: accel records in format 1 (accel_build.h)
     int  accel = RT_ACCEL;         // at the next upload: 0 = the reference's tree and order; 1 / 8 = the
                                    //   SAH tree in 1 / 8 (octant) layouts (accel_build.h)
     int  order_split = 0;          // heavy_first: only tiles costing >= this percent of the costliest go first
@@ -796,7 +802,7 @@ static int learn_order(const rt_ctx* ctx, PerDevice& p, const TraceArgs& a, hipS
 // 0.2942-0.2954 against 0.2965-0.2987 (profiles/r04/r4aa, r4ab).
 // The records one ray walks: the reference's walk records, or one accel layout.
 static size_t walk_bytes(const PerDevice& p) {
-    return (size_t)(p.scene.n_layouts ? p.scene.layout_slots : p.scene.end2) * 32;
+    return (size_t)(p.scene.n_layouts ? p.scene.layout_slots : p.scene.end2) * (p.scene.half ? 16 : 32);
 }
 
 static int wave_tile_of(const rt_ctx* ctx, const PerDevice& p) {
@@ -812,7 +818,8 @@ static int coop_window_of(const rt_ctx* ctx, const PerDevice& p) {
 static int set_schedule(const rt_ctx* ctx, PerDevice& p, TraceArgs& a, const rt_camera_ubo* cam,
                         const std::vector<int>* bands = nullptr) {
     a.wave_tile = wave_tile_of(ctx, p);
-    a.coop_lanes = ctx->coop_lanes >= 0 ? ctx->coop_lanes : (p.scene.n_layouts ? 0 : 1);
+    // (the cooperative tail walks 32-B slots: not over half-format accel records)
+    a.coop_lanes = p.scene.half ? 0 : ctx->coop_lanes >= 0 ? ctx->coop_lanes : (p.scene.n_layouts ? 0 : 1);
     a.walk = p.scene.n_layouts ? 2 : ctx->walk;          // accel: the walk-2 records only
     a.coop_walk = p.scene.n_layouts ? 0 : ctx->coop_walk;
     a.coop_win = coop_window_of(ctx, p);
@@ -994,6 +1001,7 @@ int rt_create(const int* device_ids, int n_devices, rt_ctx** out) {
         const int k = std::atoi(v);
         ctx->accel = k == 1 || k == 8 ? k : 0;
     }
+    if (const char* v = std::getenv("RTAMD_ACCEL_HALF")) ctx->accel_half = std::atoi(v) ? 1 : 0;
     if (const char* v = std::getenv("RTAMD_HEAVY_FIRST")) ctx->heavy_first = std::atoi(v) ? 1 : 0;
     if (const char* v = std::getenv("RTAMD_HEAVY_TILES")) ctx->heavy_tiles = std::max(-1, std::atoi(v));
     if (const char* v = std::getenv("RTAMD_LEARN_COST")) ctx->learn_cost = std::atoi(v) ? 1 : 0;
@@ -1203,7 +1211,7 @@ int rt_upload_scene(rt_ctx* ctx, const void* vertices, size_t vertex_bytes,
     if (ctx->accel) {
         std::string msg;
         if (accel_build(vertices, vertex_bytes, materials, material_bytes, bvh_nodes, bvh_bytes, ctx->accel, 0, &ah,
-                        &msg)) {
+                        &msg, ctx->accel_half ? 1 : 0)) {
             free_host_scene(&hs);
             set_error("rt_upload_scene: %s", msg.c_str());
             return RT_ERR_BAD_SCENE;
@@ -1237,6 +1245,7 @@ int rt_upload_scene(rt_ctx* ctx, const void* vertices, size_t vertex_bytes,
         if (acc) {
             s.n_layouts = ah.n_layouts;
             s.layout_slots = ah.slots;
+            s.half = ah.format;
             s.end = ah.slots;
             s.end2 = ah.n_layouts * ah.slots;
             s.root_leaf = ah.root_leaf;
@@ -1930,6 +1939,8 @@ int rt_set_option(rt_ctx* ctx, const char* name, int64_t value) {
         ctx->leaf_align = (int)value;                   // takes effect at the next rt_upload_scene
     } else if (std::strcmp(name, "accel") == 0 && (value == 0 || value == 1 || value == 8)) {
         ctx->accel = (int)value;                        // takes effect at the next rt_upload_scene
+    } else if (std::strcmp(name, "accel_half") == 0 && (value == 0 || value == 1)) {
+        ctx->accel_half = (int)value;                   // takes effect at the next rt_upload_scene
     } else if (std::strcmp(name, "heavy_stream") == 0 && value >= 0 && value <= 2) {
         ctx->heavy_stream = (int)value;
     } else if (std::strcmp(name, "graph") == 0 && (value == 0 || value == 1)) {
@@ -1968,6 +1979,8 @@ int rt_get_option(rt_ctx* ctx, const char* name, int64_t* value) {
     else if (std::strcmp(name, "learn_device") == 0) *value = ctx->learn_device;
     else if (std::strcmp(name, "leaf_align") == 0) *value = ctx->leaf_align;
     else if (std::strcmp(name, "accel") == 0) *value = ctx->accel;
+    else if (std::strcmp(name, "accel_half") == 0) *value = ctx->accel_half;
+    else if (std::strcmp(name, "accel_half_used") == 0) *value = ctx->dev.empty() ? 0 : ctx->dev[0].scene.half;
     else if (std::strcmp(name, "walk_bytes") == 0) *value = ctx->dev.empty() ? 0 : (int64_t)walk_bytes(ctx->dev[0]);
     else if (std::strcmp(name, "accel_used") == 0) *value = ctx->dev.empty() ? 0 : ctx->dev[0].scene.n_layouts;
     else if (std::strcmp(name, "leaf_align_used") == 0) *value = ctx->dev.empty() ? 0 : ctx->dev[0].scene.padded;
@@ -2016,10 +2029,11 @@ int rt_accel_records(const void* vertices, size_t vertex_bytes, const void* mate
     free_host_scene(&hs);
     AccelHost ah;
     std::string msg;
-    if (accel_build(vertices, vertex_bytes, materials, material_bytes, bvh_nodes, bvh_bytes, n_layouts, 0, &ah,
-                    &msg)) {
+    const int nl = n_layouts & ~RT_ACCEL_FORMAT_HALF;
+    if (accel_build(vertices, vertex_bytes, materials, material_bytes, bvh_nodes, bvh_bytes, nl, 0, &ah,
+                    &msg, (n_layouts & RT_ACCEL_FORMAT_HALF) ? 1 : 0)) {
         set_error("rt_accel_records: %s", msg.c_str());
-        return n_layouts == 1 || n_layouts == 8 ? RT_ERR_BAD_SCENE : RT_ERR_INVALID_ARG;
+        return nl == 1 || nl == 8 ? RT_ERR_BAD_SCENE : RT_ERR_INVALID_ARG;
     }
     if (n_words) *n_words = ah.rec.size();
     if (info) {

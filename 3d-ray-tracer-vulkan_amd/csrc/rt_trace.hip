@@ -393,6 +393,18 @@ __device__ __forceinline__ float4 wbuf(__amdgpu_buffer_rsrc_t r, int slot, int o
     return make_float4(__uint_as_float(v[0]), __uint_as_float(v[1]), __uint_as_float(v[2]), __uint_as_float(v[3]));
 }
 #endif
+// A half-format accel record's 16-B slot (accel_build.h format 1).
+__device__ __forceinline__ float4 hbuf(__amdgpu_buffer_rsrc_t r, int slot) {
+    const auto v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)((unsigned)slot << 4), 0, 0);
+    return make_float4(__uint_as_float(v[0]), __uint_as_float(v[1]), __uint_as_float(v[2]), __uint_as_float(v[3]));
+}
+// The low / high IEEE half of a word, as float (exact).
+__device__ __forceinline__ float half_lo(uint32_t w) {
+    return (float)__builtin_bit_cast(_Float16, (unsigned short)(w & 0xFFFFu));
+}
+__device__ __forceinline__ float half_hi(uint32_t w) {
+    return (float)__builtin_bit_cast(_Float16, (unsigned short)(w >> 16));
+}
 #ifndef RT_COOP_DPP
 #define RT_COOP_DPP 1      // a leaf's triangle from the next lane by DPP (0: loaded by the lane, A/B builds)
 #endif
@@ -722,6 +734,8 @@ constexpr int kFeatFused = 64;    // heavy tiles in the same launch: workgroups 
 constexpr int kFeatWin32 = 128;   // cooperative windows of 32 slots (option coop_window), else 64
 constexpr int kFeatPad = 256;     // the production kernels (cooperative tail, no extensions) on records
                                   //   with pad slots (leaf_align); every other variant always reads pad bits
+constexpr int kFeatHalf = 2048;   // option accel_half (with kFeatAccel): 16-B slots, half-precision internal
+                                  //   boxes (accel_build.h format 1)
 constexpr int kFeatAccel = 512;   // option accel: the accel records and rules, packed records, the
                                   //   reference-order fallback
 constexpr unsigned kHeavyLaneMark = kLearnHeavyMark;   // rt_internal.h
@@ -817,6 +831,7 @@ void trace_simple(TraceArgs a) {
     // scenes with packed records run the packed code; every other variant
     // reads them always.
     constexpr bool ACC = (FEAT & kFeatAccel) != 0;
+    constexpr bool HALF = ACC && (FEAT & kFeatHalf) != 0;
     constexpr bool PAD = !ACC && ((FEAT & kFeatPad) || (FEAT & (kFeatExt | kFeatFrontier)) || !(FEAT & kFeatCoopTail));
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
@@ -966,9 +981,18 @@ void trace_simple(TraceArgs a) {
             // a buffer resource over the records: the next slot's address is one
             // shift of its index (the offset field adds the 16-B halves)
             const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc(
-                const_cast<float4*>(wr), 0, (int)((unsigned)(a.scene.end2 + 2) * 32u), 0x00020000);
+                const_cast<float4*>(wr), 0,
+                HALF ? (int)((unsigned)(a.scene.end2 + 4) * 16u) : (int)((unsigned)(a.scene.end2 + 2) * 32u),
+                0x00020000);
 #endif
-            if (WALK == 2 && walking) {
+            if (HALF && walking) {
+                A = hbuf(wrs, n);
+                if (nleaf) {
+                    B = hbuf(wrs, n + 1);
+                    Q0 = hbuf(wrs, n + 2);
+                    Q1 = hbuf(wrs, n + 3);
+                }
+            } else if (WALK == 2 && walking) {
                 A = wr[2 * n];
                 B = wr[2 * n + 1];
                 if (nleaf) {
@@ -980,6 +1004,43 @@ void trace_simple(TraceArgs a) {
                 if (DIAG) ++d_iters;
                 if (WALK == 0) {
                     n = node_step<COUNT>(nodes, leafs, n, nleaf, o, d, inv, closest, hit, c_node, c_tri);
+                } else if (HALF) {
+                    // Format 1: an internal node is its 16-B slot A (half box,
+                    // skip | L(first) << 30 | L(skip) << 31); a leaf is A (lo,
+                    // triangle | L(next) << 31), B (hi, v0.x), Q0, Q1, exactly as
+                    // format 0's.  Only a step with a lane at a leaf loads more
+                    // than A.
+                    const uint32_t aw = __float_as_uint(A.w);
+                    const uint32_t h0 = __float_as_uint(A.x), h1 = __float_as_uint(A.y), h2 = __float_as_uint(A.z);
+                    const float4 lo = nleaf ? A : make_float4(half_lo(h0), half_hi(h0), half_lo(h1), 0.f);
+                    const float4 hi = nleaf ? B : make_float4(half_hi(h1), half_lo(h2), half_hi(h2), 0.f);
+                    float te;
+                    bool ind;
+                    slab(lo, hi, o, inv, te, ind);
+                    const bool hb = ind && accel_enter(te, closest);
+                    const int nxt = nleaf ? n + 4 : (hb ? n + 1 : (int)(aw & 0x3FFFFFFFu));
+                    const bool nl = ((nleaf || !hb) ? (aw >> 31) : (aw >> 30)) & 1u;
+                    const float v0x = B.w;                                   // a leaf's v0.x
+                    if (COUNT && hb && !nleaf) c_node += 2;
+                    A = hbuf(wrs, nxt);                                      // slot end is padding
+                    if (hb && nleaf) {                                       // hit_triangle (:196-200)
+                        if (COUNT) ++c_tri;
+                        float t;
+                        if (tri_test(make_float4(v0x, Q0.x, Q0.y, 0.f), make_float4(Q0.z, Q0.w, Q1.x, 0.f),
+                                     make_float4(Q1.y, Q1.z, Q1.w, 0.f), o, d, t) &&
+                            accel_take(t, (int)(aw & kTri), closest, hit)) {
+                            closest = t;
+                            hit = (int)(aw & kTri);
+                            incons = t < te;
+                        }
+                    }
+                    if (nl && nxt < lend) {
+                        B = hbuf(wrs, nxt + 1);
+                        Q0 = hbuf(wrs, nxt + 2);
+                        Q1 = hbuf(wrs, nxt + 3);
+                    }
+                    n = nxt;
+                    nleaf = nl;
                 } else {
                     float te;
                     bool ind;
@@ -1303,6 +1364,16 @@ hipError_t launch_trace(const TraceArgs& a, hipStream_t stream, int* kernels) {
     if (a.scene.n_layouts > 0) {
         // option accel (walk 2 records; the launcher never splits heavy tiles
         // or pixels out of an accel launch, and there is no frontier tail)
+        if (a.scene.half) {
+            // format 1 records: no cooperative tail (set_schedule: coop_lanes 0)
+            if (feat & kFeatCoopTail) {
+                set_error("accel_half launch with coop_lanes %d", a.coop_lanes);
+                return hipErrorInvalidValue;
+            }
+            if (feat & kFeatExt) RT_SIMPLE(kFeatExt | kFeatAccel | kFeatHalf, 2)
+            else RT_SIMPLE(kFeatAccel | kFeatHalf, 2)
+            return hipGetLastError();
+        }
         switch (feat & ~kFeatFrontier) {
             case kFeatCoopTail:
                 if (a.coop_win == 32) RT_SIMPLE(kFeatCoopTail | kFeatAccel | kFeatWin32, 2)

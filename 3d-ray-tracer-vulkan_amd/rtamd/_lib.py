@@ -157,9 +157,13 @@ def check(rc: int) -> None:
         raise RtError(rc, msg.decode() if msg else "")
 
 
-def accel_records(built, n_layouts: int = 8):
+RT_ACCEL_FORMAT_HALF = 0x100
+
+
+def accel_records(built, n_layouts: int = 8, half: bool = False):
     """Option accel's records for a BuiltCpuData (rt_accel_records): returns
-    (uint32[slots_total * 8], info dict).  Host-only; no device needed."""
+    (uint32[slots_total * 8] (half: * 4, option accel_half's format), info
+    dict).  Host-only; no device needed."""
     import numpy as np
     L = lib()
     bufs = [np.ascontiguousarray(np.frombuffer(bytes(x), dtype=np.uint8)) if isinstance(x, (bytes, bytearray))
@@ -170,8 +174,11 @@ def accel_records(built, n_layouts: int = 8):
         args += [b.ctypes.data, b.nbytes]
     n = C.c_size_t(0)
     info = (C.c_int32 * 6)()
-    check(L.rt_accel_records(*args, n_layouts, None, 0, C.byref(n), info))
+    nl = n_layouts | (RT_ACCEL_FORMAT_HALF if half else 0)
+    check(L.rt_accel_records(*args, nl, None, 0, C.byref(n), info))
     out = np.zeros(n.value, dtype=np.uint32)
-    check(L.rt_accel_records(*args, n_layouts, out.ctypes.data_as(C.POINTER(C.c_uint32)), out.size, C.byref(n), info))
+    check(L.rt_accel_records(*args, nl, out.ctypes.data_as(C.POINTER(C.c_uint32)), out.size, C.byref(n), info))
     keys = ("n_layouts", "slots", "root_leaf", "n_prims", "n_inputs", "depth")
-    return out, dict(zip(keys, list(info)))
+    d = dict(zip(keys, list(info)))
+    d["format"] = 1 if half else 0
+    return out, d

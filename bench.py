@@ -1117,7 +1117,8 @@ def main() -> None:
     ref_layout_bytes = 48.0 * l_nodes + 48.0 * l_tris + 16.0 * l_mats + 4.0 * l_pix
     n_cu = torch.cuda.get_device_properties(dev).multi_processor_count
     # PMC only from a record of this config and camera path (pmc_key)
-    pmc = load_pmc(args.pmc_json, pmc_key(cfg.name, args.camera_path, renderer.get_option("accel_used"))) \
+    pmc = load_pmc(args.pmc_json, pmc_key(cfg.name, args.camera_path, renderer.get_option("accel_used"),
+                                         renderer.get_option("accel_half_used"))) \
         if (mode == "whole" and F == 1) else None
     walk_mb = round(renderer.walk_bytes() / 2**20, 2)
     roof = roofline(pmc, alg_bytes, ref_layout_bytes, l_seg, launch_ms, frame_ms, n_cu, lanes, walk_mb)
@@ -1194,7 +1195,8 @@ def main() -> None:
                                                                       "reuse_order", "order_split", "hw_queues",
                                                                       "coop_window", "coop_window_used",
                                                                       "leaf_align", "leaf_align_used",
-                                                                      "accel", "accel_used",
+                                                                      "accel", "accel_used", "accel_half",
+                                                                      "accel_half_used",
                                                                       "wave_tile_used")},
                              "concurrent_launches": renderer.get_option("concurrent_launches"),
                              "heavy_tiles_used": heavy_used,
@@ -1308,13 +1310,13 @@ def lane_utilisation(renderer, L, ctx, launch, dev):
                     "coop_windows = 64-node windows of the cooperative tail"}
 
 
-def pmc_key(config_name: str, camera_path: str, accel: int = 0) -> str:
+def pmc_key(config_name: str, camera_path: str, accel: int = 0, half: int = 0) -> str:
     """The key of a PMC record in profiles/pmc_latest.json: the config, the
     camera path unless it is the static default camera, and the accel layouts
     unless the scene runs the reference's own tree (accel 0; round 4's
-    records)."""
+    records), with "h" for option accel_half's records."""
     k = config_name if camera_path == "static" else f"{config_name}@{camera_path}"
-    return f"{k}@accel{accel}" if accel else k
+    return f"{k}@accel{accel}{'h' if half else ''}" if accel else k
 
 
 def load_pmc(path, config_name):

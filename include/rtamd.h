@@ -262,6 +262,15 @@ int rt_render_poll(rt_ctx* ctx, uint64_t ticket, int* done);
  *                   walk's own.  Heavy tiles / pixels are not
  *                   split out of accel launches (heavy_first still orders
  *                   the tiles)
+ *   "accel_half"    at the next rt_upload_scene, accel records with the
+ *                   internal nodes' boxes in IEEE half precision rounded
+ *                   outward (16-B internal records instead of 32; leaves keep
+ *                   their exact fp32 boxes and triangles): a walk step of
+ *                   internal nodes loads half the bytes, widened boxes are only
+ *                   entered more often, so frames are unchanged (DESIGN.md
+ *                   §4a).  Forces coop_lanes 0.  0 / 1
+ *   "accel_half_used" (rt_get_option only) 1 when device 0's accel records
+ *                   are in that format
  *   "accel_used"    (rt_get_option only) the current scene's layouts on device
  *                   0 (0 = the reference's tree)
  *   "walk_bytes"    (rt_get_option only) bytes of the records one ray walks on
@@ -396,7 +405,7 @@ int rt_render_poll(rt_ctx* ctx, uint64_t ticket, int* done);
  *                   the slots' traces then share hardware queues and run one
  *                   after another (set GPU_MAX_HW_QUEUES before the process
  *                   initialises HIP)
- * Defaults can also be set with the environment variables RTAMD_ACCEL,
+ * Defaults can also be set with the environment variables RTAMD_ACCEL, RTAMD_ACCEL_HALF,
  * RTAMD_OPTS ("name=value,..." of any option above), RTAMD_WALK, RTAMD_COOP_LANES, RTAMD_COOP_WALK, RTAMD_BLOCK_WAVES, RTAMD_HEAVY_FIRST,
  * RTAMD_HEAVY_TILES, RTAMD_HEAVY_FACTOR, RTAMD_HEAVY_STREAM (0 / 1 / 2),
  * RTAMD_HEAVY_PIXELS, RTAMD_LEARN_COST and RTAMD_GRAPH. */
@@ -440,13 +449,16 @@ int rt_scene_validate(const void* vertices, size_t vertex_bytes,
  * rt_upload_scene builds them for a context with accel on (pure host code, no
  * device): the binned-SAH tree over the reference leaves' (triangle, box)
  * pairs, n_layouts (1, or 8 = one per ray-direction octant) near-first
- * preorder layouts in the walk-record format, 8 32-bit words per 32-B slot.
+ * preorder layouts in the walk-record format, 8 32-bit words per 32-B slot;
+ * n_layouts | RT_ACCEL_FORMAT_HALF: option accel_half's format, 4 words per
+ * 16-B slot, internal boxes in half precision rounded outward.
  * Writes up to cap_words words (out_words may be NULL to size the call) and
- * *n_words = the words of the records (n_layouts * slots + 2 padding slots);
+ * *n_words = the words of the records (n_layouts * slots, + 64 B of padding);
  * info (nullable) receives {n_layouts, slots per layout, root is a leaf,
  * primitives after dropping byte-identical duplicates, reference leaves, tree
  * depth}.  An analysis and test entry point (oracle/rt_accel_model.c walks
  * these records on the CPU); a host embedding the backend never needs it. */
+#define RT_ACCEL_FORMAT_HALF 0x100
 int rt_accel_records(const void* vertices, size_t vertex_bytes,
                      const void* materials, size_t material_bytes,
                      const void* bvh_nodes, size_t bvh_bytes, int n_layouts,

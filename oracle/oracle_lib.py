@@ -44,6 +44,7 @@ def lib(envelope: bool = False, accel: bool = False) -> C.CDLL:
             _accel_lib = _bind(C.CDLL(ACCEL_LIB))
             _accel_lib.orc_accel_set.restype = C.c_int
             _accel_lib.orc_accel_set.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int]
+            _accel_lib.orc_accel_format.argtypes = [C.c_int]
             _accel_lib.orc_accel_fallbacks.restype = C.c_uint64
             _accel_lib.orc_accel_margin.argtypes = [C.c_float, C.c_float]
         return _accel_lib
@@ -145,6 +146,8 @@ def render_accel(vertices, materials, nodes, camera_ubo: bytes, width: int, heig
     prof = np.zeros((rows, tw, max_bounces), dtype=np.uint32) if profile else None
     c = Counts()
     L = lib(accel=True)
+    if L.orc_accel_format(int(info.get("format", 0))) != 0:
+        raise RuntimeError("orc_accel_format failed")
     if L.orc_accel_set(rec.ctypes.data, int(info["n_layouts"]), int(info["slots"]), int(info["root_leaf"])) != 0:
         raise RuntimeError("orc_accel_set failed")
     rc = L.orc_render_profile(vp, vn, mp, mn, bp, bn, cam.ctypes.data, width, height, max_bounces,

@@ -21,11 +21,16 @@
  * sky, the counters' definitions) is the oracle's own code.  Node visits are
  * box tests (slots walked), as in the reference's counts: 1 + 2 x the internal
  * nodes whose box is entered.
+ *
+ * orc_accel_format(1): the records are accel_build.h's format 1 (option
+ * accel_half): 16-B slots, an internal node one slot with its box in IEEE half
+ * precision (decoded exactly, as the kernel's v_cvt_f32_f16), a leaf four.
  */
 #define ORC_WALK_HOOK accel_walk
 #include "rt_oracle.c"
 
-static const uint32_t* g_rec = NULL;   /* 8 words per slot */
+static const uint32_t* g_rec = NULL;   /* 8 words per slot (format 1: 4) */
+static int g_fmt = 0;
 static int g_layouts = 1, g_slots = 0, g_root_leaf = 0;
 static uint64_t g_fallbacks = 0;       /* segments re-walked in the reference's order */
 static uint64_t g_leaf_visits = 0;     /* analysis: leaf slots walked (the rest are internal nodes) */
@@ -53,6 +58,23 @@ uint64_t orc_accel_leaf_visits(void) {
     return f;
 }
 
+/* The format of the records the following renders walk: 0 or 1. */
+int orc_accel_format(int fmt) {
+    if (fmt != 0 && fmt != 1) return -2;
+    g_fmt = fmt;
+    return 0;
+}
+
+/* An IEEE half (bits h) as float, exactly. */
+static float half_to_float(uint32_t h) {
+    const uint32_t e = (h >> 10) & 31u, m = h & 1023u;
+    float v;
+    if (e == 0) v = ldexpf((float)m, -24);
+    else if (e == 31) v = m ? NAN : INFINITY;
+    else v = ldexpf((float)(1024u + m), (int)e - 25);
+    return (h & 0x8000u) ? -v : v;
+}
+
 /* Sets the records the following renders walk (the caller keeps them alive). */
 int orc_accel_set(const uint32_t* rec, int n_layouts, int slots, int root_leaf) {
     if ((n_layouts != 1 && n_layouts != 8) || slots < 0 || (slots > 0 && !rec)) return -2;
@@ -63,7 +85,11 @@ int orc_accel_set(const uint32_t* rec, int n_layouts, int slots, int root_leaf) 
     return 0;
 }
 
-static float rec_f(size_t slot, int w) { float f; memcpy(&f, &g_rec[8 * slot + (size_t)w], 4); return f; }
+static float rec_f(size_t slot, int w) {
+    float f;
+    memcpy(&f, &g_rec[(g_fmt ? 4 : 8) * slot + (size_t)w], 4);
+    return f;
+}
 
 /* Analysis (orc_accel_quant): internal boxes widened to what a compressed
  * record could hold, to count the visits that would cost; leaves stay exact.
@@ -95,12 +121,21 @@ static int accel_walk(const scene* s, ray r, float* closest_t, int* hit_index, v
     float hit_te = 0.0f;                      /* t_enter of the hit triangle's own box */
     int hit = -1;
     uint64_t leaf_visits = 0;
+    const size_t WS = g_fmt ? 4 : 8;
     while (n < end) {
-        const uint32_t aw = g_rec[8 * n + 3], bw = g_rec[8 * n + 7];
+        const uint32_t aw = g_rec[WS * n + 3], bw = g_fmt ? 0u : g_rec[8 * n + 7];
         cnt->node_visits++;
         trace_rec((int32_t)n);
         /* the slab test of hit_aabb (:88-103), t_enter <= closest_t */
-        vec3 blo = v3(rec_f(n, 0), rec_f(n, 1), rec_f(n, 2)), bhi = v3(rec_f(n, 4), rec_f(n, 5), rec_f(n, 6));
+        vec3 blo, bhi;
+        if (g_fmt && !leaf) {
+            const uint32_t* w = &g_rec[4 * n];
+            blo = v3(half_to_float(w[0] & 0xFFFFu), half_to_float(w[0] >> 16), half_to_float(w[1] & 0xFFFFu));
+            bhi = v3(half_to_float(w[1] >> 16), half_to_float(w[2] & 0xFFFFu), half_to_float(w[2] >> 16));
+        } else {
+            blo = v3(rec_f(n, 0), rec_f(n, 1), rec_f(n, 2));
+            bhi = v3(rec_f(n, 4), rec_f(n, 5), rec_f(n, 6));
+        }
         if (g_quant == 1 && !leaf) {
             blo = v3(half_down(blo.x), half_down(blo.y), half_down(blo.z));
             bhi = v3(half_up(bhi.x), half_up(bhi.y), half_up(bhi.z));
@@ -131,13 +166,13 @@ static int accel_walk(const scene* s, ray r, float* closest_t, int* hit_index, v
         size_t nxt;
         int nl;
         if (leaf) {
-            nxt = n + 2;
+            nxt = n + (g_fmt ? 4 : 2);
             nl = (int)(aw >> 31);
         } else if (hb) {
             nxt = n + 1;
-            nl = (int)(bw & 1u);
+            nl = g_fmt ? (int)((aw >> 30) & 1u) : (int)(bw & 1u);
         } else {
-            nxt = aw & 0x7FFFFFFFu;
+            nxt = aw & (g_fmt ? 0x3FFFFFFFu : 0x7FFFFFFFu);
             nl = (int)(aw >> 31);
         }
         if (nxt <= n && !hb) return -1;         /* a link that does not move forward: bad records */

@@ -17,16 +17,16 @@ import pytest
 HERE = os.path.dirname(os.path.abspath(__file__))
 
 
-def _records(built, n_layouts):
+def _records(built, n_layouts, half=False):
     from rtamd import _lib
-    return _lib.accel_records(built, n_layouts)
+    return _lib.accel_records(built, n_layouts, half)
 
 
-def _frames(built, cam, w, h, b, n_layouts, tile=None, row_step=1):
+def _frames(built, cam, w, h, b, n_layouts, tile=None, row_step=1, half=False):
     from oracle import oracle_lib as O
     args = (built.model_vertex_data, built.model_material_data, built.flat_bvh_data, cam.ubo_bytes(), w, h, b)
     ref = O.render(*args, tile=tile, row_step=row_step)
-    rec, info = _records(built, n_layouts)
+    rec, info = _records(built, n_layouts, half)
     acc = O.render_accel(*args, rec, info, tile=tile, row_step=row_step)
     return ref, acc
 
@@ -61,6 +61,70 @@ def _walk_all(rec, info, o):
     return tris
 
 
+def _walk_all_half(rec, info, o):
+    """_walk_all over format 1 (option accel_half): 16-B slots, a leaf four."""
+    s = info["slots"]
+    n, end, leaf = o * s, (o + 1) * s, bool(info["root_leaf"])
+    tris, steps = [], 0
+    while n < end:
+        aw = int(rec[4 * n + 3])
+        if leaf:
+            assert (aw >> 30) & 1, f"slot {n}: a leaf without its marker"
+            tris.append(aw & 0x1FFFFFFF)
+            n, leaf = n + 4, bool(aw >> 31)
+        else:
+            skip = aw & 0x3FFFFFFF
+            assert n < skip <= end
+            n, leaf = n + 1, bool((aw >> 30) & 1)
+        steps += 1
+        assert steps <= s
+    assert n == end
+    return tris
+
+
+def _half(bits):
+    return np.array(bits, dtype=np.uint16).view(np.float16).astype(np.float32)
+
+
+@pytest.mark.parametrize("k", [1, 2, 3])
+def test_record_layouts_half(k):
+    """Option accel_half's records: 5m - 1 16-B slots per layout, the same
+    triangles in the same walk order as format 0, every leaf's 64 bytes equal
+    to format 0's, and every internal box the format-0 box rounded outward to
+    the nearest halves (lo down, hi up)."""
+    from rtamd import configs
+    built = configs.get(k).build()
+    for nl in (1, 8):
+        r0, i0 = _records(built, nl)
+        r1, i1 = _records(built, nl, half=True)
+        m = i0["n_prims"]
+        assert i1["slots"] == 5 * m - 1 and r1.size == 4 * nl * i1["slots"] + 16
+        for o in range(nl):
+            assert _walk_all_half(r1, i1, o) == _walk_all(r0, i0, o)
+            # walk both layouts in step, every box entered: the same nodes
+            a, b = o * i0["slots"], o * i1["slots"]
+            leaf = bool(i0["root_leaf"])
+            while a < (o + 1) * i0["slots"]:
+                w0, w1 = r0[8 * a: 8 * a + 16], r1[4 * b: 4 * b + 16]
+                if leaf:
+                    assert np.array_equal(w0, w1)
+                    leaf = bool(int(w0[3]) >> 31)
+                    a, b = a + 2, b + 4
+                else:
+                    lo0, hi0 = w0[0:3].view(np.float32), w0[4:7].view(np.float32)
+                    h = w1[0:3].astype(np.uint32)
+                    lo1 = _half([h[0] & 0xFFFF, h[0] >> 16, h[1] & 0xFFFF])
+                    hi1 = _half([h[1] >> 16, h[2] & 0xFFFF, h[2] >> 16])
+                    assert (lo1 <= lo0).all() and (hi1 >= hi0).all()
+                    # the nearest halves outward: one step further in would cut the box
+                    lo_in = np.nextafter(lo1.astype(np.float16), np.float16(np.inf)).astype(np.float32)
+                    hi_in = np.nextafter(hi1.astype(np.float16), np.float16(-np.inf)).astype(np.float32)
+                    assert ((lo_in > lo0) | ~np.isfinite(lo1)).all() and ((hi_in < hi0) | ~np.isfinite(hi1)).all()
+                    leaf = bool(int(w0[7]) & 1)
+                    assert leaf == bool((int(w1[3]) >> 30) & 1)
+                    a, b = a + 1, b + 1
+
+
 @pytest.mark.parametrize("k", [1, 2, 3])
 def test_record_layouts(k):
     from rtamd import configs
@@ -92,15 +156,15 @@ def test_duplicates_dropped():
     assert info["n_inputs"] == 65536 and info["n_prims"] == 50014
 
 
-@pytest.mark.parametrize("nl", [1, 8])
+@pytest.mark.parametrize("nl,half", [(1, False), (8, False), (8, True)])
 @pytest.mark.parametrize("k,b,tile,row_step", [(1, 1, None, 1), (2, 2, None, 2), (2, 10, (400, 200, 480, 320), 1),
                                                  (3, 4, None, 24), (6, 4, None, 40)])
-def test_model_matches_oracle(k, b, tile, row_step, nl):
+def test_model_matches_oracle(k, b, tile, row_step, nl, half):
     from rtamd import configs
     cfg = configs.get(k)
     built = cfg.build()
-    ref, acc = _frames(built, cfg.camera(), cfg.width, cfg.height, b, nl, tile=tile, row_step=row_step)
-    _assert_frames_equal(ref, acc, f"config {k}")
+    ref, acc = _frames(built, cfg.camera(), cfg.width, cfg.height, b, nl, tile=tile, row_step=row_step, half=half)
+    _assert_frames_equal(ref, acc, f"config {k} half {half}")
     # far fewer box tests than the reference's walk (3: 36.8 vs 8.2 per segment)
     if k >= 3:
         assert acc[2]["node_visits"] < 0.4 * ref[2]["node_visits"]
@@ -131,14 +195,14 @@ def _tie_scenes():
     return out
 
 
-@pytest.mark.parametrize("nl", [1, 8])
-def test_model_ties(nl):
+@pytest.mark.parametrize("nl,half", [(1, False), (8, False), (8, True)])
+def test_model_ties(nl, half):
     from rtamd import configs
     for name, built in _tie_scenes().items():
         for (w, h, b) in [(160, 90, 3), (97, 61, 10)]:
             cam = configs.Camera.default(w, h)
-            ref, acc = _frames(built, cam, w, h, b, nl)
-            _assert_frames_equal(ref, acc, f"{name} {w}x{h}x{b}")
+            ref, acc = _frames(built, cam, w, h, b, nl, half=half)
+            _assert_frames_equal(ref, acc, f"{name} {w}x{h}x{b} half {half}")
 
 
 def test_model_tree_independent():
