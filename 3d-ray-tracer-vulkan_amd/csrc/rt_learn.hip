@@ -17,12 +17,15 @@
 //                  their raster order (cost key 0)
 //   radix sort     tiles by cost, descending and stable (rocPRIM), so equal
 //                  keys keep raster order, as the host's stable_sort did
-//   learn_cand     pixels whose walk length exceeds the heavy-pixel bar (the
-//                  bulk estimate: total steps x concurrent launches / resident
-//                  waves x heavy_pixel_factor), gathered with their lengths
-//   learn_top      one workgroup: the candidates sorted by length, descending,
-//                  ties by pixel index (an LDS bitonic sort), the first `cap`
-//                  become the heavy pixels and their tiles' lane masks
+//   learn_cand     every pixel's key: its walk length and pixel index if the
+//                  length exceeds the heavy-pixel bar (the bulk estimate: total
+//                  steps x concurrent launches / resident waves x
+//                  heavy_pixel_factor), else 0
+//   radix sort     the keys, descending (rocPRIM): length first, then the
+//                  lower pixel index, a total order, so the choice is the
+//                  host's whatever the candidate count
+//   learn_top      the first `cap` non-zero keys become the heavy pixels and
+//                  their tiles' lane masks
 //
 // The order only decides which wave traces a pixel and when, never what it
 // computes, so results are identical whatever these kernels choose.
@@ -35,19 +38,18 @@ namespace rtamd {
 struct LearnScratch {
     unsigned long long total;    // sum of the tiles' lockstep steps + 2 x windows
     unsigned long long cmax;     // the costliest tile's cost
-    unsigned ncand;              // heavy-pixel candidates found (may exceed kCand)
+    unsigned ncand;              // unused (round 5: every pixel has a key)
     unsigned pad[3];
 };
 
 namespace {
 
-constexpr int kCand = 8192;              // candidates the one-workgroup sort ranks (64 KB of LDS)
 constexpr size_t kAlign = 256;
 
 size_t up(size_t x) { return (x + kAlign - 1) / kAlign * kAlign; }
 
 struct Layout {
-    size_t hdr, key_in, key_out, val_in, cand, temp, temp_bytes, total;
+    size_t hdr, key_in, key_out, val_in, cand, cand_out, temp, temp_bytes, total;
 };
 
 Layout layout(int n) {
@@ -57,12 +59,16 @@ Layout layout(int n) {
     L.key_in = off;  off += up(sizeof(unsigned) * (size_t)n);
     L.key_out = off; off += up(sizeof(unsigned) * (size_t)n);
     L.val_in = off;  off += up(sizeof(int) * (size_t)n);
-    L.cand = off;    off += up(sizeof(unsigned long long) * kCand);
+    const size_t nl = (size_t)n * 64;
+    L.cand = off;    off += up(sizeof(unsigned long long) * nl);
+    L.cand_out = off; off += up(sizeof(unsigned long long) * nl);
     L.temp = off;
-    size_t tb = 0;
+    size_t tb = 0, tc = 0;
     (void)rocprim::radix_sort_pairs_desc(nullptr, tb, (const unsigned*)nullptr, (unsigned*)nullptr,
                                          (const int*)nullptr, (int*)nullptr, n, 0, 32);
-    L.temp_bytes = up(tb);
+    (void)rocprim::radix_sort_keys_desc(nullptr, tc, (const unsigned long long*)nullptr,
+                                        (unsigned long long*)nullptr, nl, 0, 64);
+    L.temp_bytes = up(tb > tc ? tb : tc);
     off += L.temp_bytes;
     L.total = off;
     return L;
@@ -106,55 +112,30 @@ __global__ __launch_bounds__(256) void learn_split(unsigned* __restrict__ key, i
 // index, so a descending sort puts longer walks first and, among equal ones,
 // the lower pixel index first (the host's stable_sort order).
 __global__ __launch_bounds__(256) void learn_cand(const unsigned* __restrict__ lane, size_t nl,
-                                                  LearnScratch* hdr, double bar_scale,
+                                                  const LearnScratch* hdr, double bar_scale,
                                                   unsigned long long* __restrict__ cand) {
     const size_t q = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (q >= nl) return;
     const unsigned len = lane[q];
     const double bar = bar_scale * (double)hdr->total;
-    if ((double)len > bar) {
-        const unsigned i = atomicAdd(&hdr->ncand, 1u);
-        if (i < (unsigned)kCand)
-            cand[i] = ((unsigned long long)len << 32) | (unsigned long long)(0xFFFFFFFFu - (unsigned)q);
-    }
+    cand[q] = (double)len > bar ? ((unsigned long long)len << 32) | (unsigned long long)(0xFFFFFFFFu - (unsigned)q)
+                                : 0ull;
 }
 
-__global__ __launch_bounds__(1024) void learn_top(const unsigned long long* __restrict__ cand,
-                                                  const LearnScratch* hdr, int cap, int* __restrict__ hpix,
-                                                  unsigned long long* __restrict__ mask, int* __restrict__ nhpix) {
-    __shared__ unsigned long long sk[kCand];
-    const int tid = threadIdx.x;
-    const unsigned nc = hdr->ncand;
-    const int m = nc < (unsigned)kCand ? (int)nc : kCand;
-    for (int i = tid; i < kCand; i += 1024) sk[i] = i < m ? cand[i] : 0ull;
-    __syncthreads();
-    for (int k = 2; k <= kCand; k <<= 1) {             // bitonic sort, descending
-        for (int j = k >> 1; j > 0; j >>= 1) {
-            for (int i = tid; i < kCand; i += 1024) {
-                const int ixj = i ^ j;
-                if (ixj > i) {
-                    const unsigned long long x = sk[i], y = sk[ixj];
-                    const bool desc = (i & k) == 0;
-                    if (desc ? x < y : x > y) {
-                        sk[i] = y;
-                        sk[ixj] = x;
-                    }
-                }
-            }
-            __syncthreads();
-        }
-    }
-    // More candidates than the sort holds: which ones arrived first is a race,
-    // so the choice would be neither the costliest nor deterministic.  Such an
-    // order takes no heavy pixels (exact, only less balanced); the count
-    // reports the overflow as -1 (rt_runtime.hip poll_learning).
-    const int nout = nc > (unsigned)kCand ? 0 : (m < cap ? m : cap);
-    for (int i = tid; i < nout; i += 1024) {
-        const int q = (int)(0xFFFFFFFFu - (unsigned)(sk[i] & 0xFFFFFFFFull));
-        hpix[i] = q;
-        atomicOr(&mask[q >> 6], 1ull << (q & 63));
-    }
-    if (tid == 0) *nhpix = nc > (unsigned)kCand ? -1 : nout;
+// sorted: every pixel's key, descending; the first cap non-zero ones are the
+// heavy pixels (a non-zero key's length is >= 1, so it sorts above every 0).
+__global__ __launch_bounds__(256) void learn_top(const unsigned long long* __restrict__ sorted, int cap,
+                                                 int* __restrict__ hpix, unsigned long long* __restrict__ mask,
+                                                 int* __restrict__ nhpix) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= cap) return;
+    const unsigned long long k = sorted[i];
+    if (i == 0 && k == 0ull) *nhpix = 0;
+    if (k == 0ull) return;
+    const int q = (int)(0xFFFFFFFFu - (unsigned)(k & 0xFFFFFFFFull));
+    hpix[i] = q;
+    atomicOr(&mask[q >> 6], 1ull << (q & 63));
+    if (i + 1 == cap || sorted[i + 1] == 0ull) *nhpix = i + 1;      // the last heavy pixel
 }
 
 }  // namespace
@@ -186,10 +167,16 @@ hipError_t learn_on_device(const LearnParams& lp, const unsigned long long* rec,
     e = rocprim::radix_sort_pairs_desc(base + L.temp, tb, key_in, key_out, val_in, d_order, lp.n, 0, 32, s);
     if (e != hipSuccess) return e;
     const size_t nl = (size_t)lp.n * 64;
+    unsigned long long* cand_out = reinterpret_cast<unsigned long long*>(base + L.cand_out);
     hipLaunchKernelGGL(learn_cand, dim3((unsigned)((nl + 255) / 256)), dim3(256), 0, s, lane, nl, hdr,
                        lp.bar_scale, cand);
     if ((e = hipGetLastError()) != hipSuccess) return e;
-    hipLaunchKernelGGL(learn_top, dim3(1), dim3(1024), 0, s, cand, hdr, lp.cap < kCand ? lp.cap : kCand, d_hpix,
+    tb = L.temp_bytes;
+    e = rocprim::radix_sort_keys_desc(base + L.temp, tb, cand, cand_out, nl, 0, 64, s);
+    if (e != hipSuccess) return e;
+    const int cap = (int)std::min<size_t>((size_t)std::max(lp.cap, 0), nl);
+    if (cap == 0) return hipMemsetAsync(d_nhpix, 0, sizeof(int), s);
+    hipLaunchKernelGGL(learn_top, dim3((unsigned)((cap + 255) / 256)), dim3(256), 0, s, cand_out, cap, d_hpix,
                        d_mask, d_nhpix);
     return hipGetLastError();
 }

@@ -287,7 +287,6 @@ struct PerDevice {
     hipEvent_t   learn_ev = nullptr;
     bool         learn_busy = false;          // a device learning is in flight (its order pending)
     bool         learning_device = false;     // the learning launch being planned learns on the device
-    int          learn_overflows = 0;         // device learnings with more heavy-pixel candidates than sorted
     int          learning_rec_off = 0;        // its heavy-pixel waves ahead of the tile records
     // option heavy_tiles: auxiliary streams (round robin) for the concurrent heavy-tile launch
     hipStream_t  aux[4] = {nullptr, nullptr, nullptr, nullptr};
@@ -344,9 +343,7 @@ static void poll_learning(PerDevice& p) {
     if (!p.learn_busy || hipEventQuery(p.learn_ev) != hipSuccess) return;
     for (auto& o : p.orders)
         if (o.pending) {
-            // -1: more candidates than learn_top sorts (rt_learn.hip): no heavy pixels
             o.n_hpix = std::max(0, *p.h_nhpix);
-            if (*p.h_nhpix < 0) ++p.learn_overflows;
             o.pending = false;
         }
     p.learn_busy = false;
@@ -1992,7 +1989,6 @@ int rt_get_option(rt_ctx* ctx, const char* name, int64_t* value) {
     else if (std::strcmp(name, "reuse_order") == 0) *value = ctx->reuse_order;
     else if (std::strcmp(name, "heavy_pixels") == 0) *value = ctx->heavy_pixels;
     else if (std::strcmp(name, "heavy_pixel_factor") == 0) *value = ctx->heavy_pixel_factor;
-    else if (std::strcmp(name, "learn_overflows") == 0) *value = ctx->dev.empty() ? 0 : ctx->dev[0].learn_overflows;
     else if (std::strcmp(name, "heavy_pixels_used") == 0) *value = ctx->dev.empty() ? 0 : ctx->dev[0].last_heavy_px;
     else if (std::strcmp(name, "heavy_tiles_used") == 0) *value = ctx->dev.empty() ? 0 : ctx->dev[0].last_heavy;
     else if (std::strcmp(name, "plain_kernels") == 0) *value = ctx->dev.empty() ? 0 : (int64_t)ctx->dev[0].plain_kernels;

@@ -338,9 +338,6 @@ int rt_render_poll(rt_ctx* ctx, uint64_t ticket, int* done);
  *                   learning frame while the camera moves; the first repeat of
  *                   a camera learns); 0 = every new camera learns
  *   "heavy_pixels_used" (rt_get_option only) heavy pixels of the last launch
- *   "learn_overflows" (rt_get_option only) device learnings on device 0 that
- *                   found more heavy-pixel candidates than the one-workgroup
- *                   sort holds (8192): their orders take no heavy pixels
  *   "graph"         plain launches on a non-null stream whose frame is two
  *                   launches (heavy_stream 1): 1 (default) = captured once per
  *                   launch key into a HIP graph and replayed; 0 = launched
