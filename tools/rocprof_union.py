@@ -78,7 +78,6 @@ def main():
     out = {
         "trace": args.trace,
         "kernels": names,
-        "kernels_per_frame": per,
         "mean_ms_by_kernel": by_kernel,
         "frames": args.steps,
         "launches": n,

@@ -18,7 +18,7 @@
 #   pmc3o     the same for config 3 with the orbiting camera (record key cfg3_...@orbit)
 #   orbit     bench.py --camera-path orbit at 20 steps
 #   cfgs      bench.py on configs 4, 5, 6
-#   inflight  bench.py at 1, 2 and 4 launches in flight (200 steps): the headline
+#   inflight  bench.py at 1, 2 and 4 ($INFLIGHT) launches in flight (200 steps): the headline
 #             frac must not move with them
 #   share     tools/share_inflight_bench.py (one rank's share, frames in flight)
 #   emu       tools/rank_emulator.py (one rank of N with its exchange; $EMU_ARGS)
@@ -94,7 +94,7 @@ for s in "$@"; do
                 run "cfg$1" 300 python bench.py --config "$1" --steps "$2" --warmup 3 --no-cpu-baseline \
                     > "$OUT/bench_cfg$1.json" 2> "$OUT/bench_cfg$1.err"
               done ;;
-    inflight) for k in 1 2 4; do
+    inflight) for k in ${INFLIGHT:-1 2 4}; do
                 run "inflight$k" 300 python bench.py --inflight "$k" --steps 200 --warmup 5 --no-cpu-baseline \
                     --no-pcie > "$OUT/bench_if$k.json" 2> "$OUT/bench_if$k.err"
               done ;;
