@@ -191,7 +191,9 @@ R05 = os.path.join(ROOT, "profiles", "r05")
 # (session, file) of the round-5 lines this round's evidence rests on (r5c's
 # lines predate the PMC records keyed by accel: their traffic came from the
 # reference walk's round-4 record, so they are not listed)
-R05_LINES = []
+R05_LINES = [("r5aa", "bench.json"), ("r5aa", "prof3.json"), ("r5aa", "prof5.json"), ("r5aa", "bench_cfg5.json"),
+             ("r5aa", "bench_cfg6.json"), ("r5aa", "bench_if4.json"), ("r5aa", "bench_if6.json"),
+             ("r5aa", "bench_if8.json")]
 
 
 def _r05_lines():
@@ -218,8 +220,7 @@ def test_r05_roofline_reproduces(session, name):
     if r["traffic"]:
         # the PMC record it names: FETCH_SIZE (KiB of 64-B halves) x 1024 x 2
         src = os.path.join(ROOT, r["pmc_source"].split(" ")[0])
-        fetch = _pmc_mean(os.path.join(src, "C_counter_collection.csv"), "FETCH_SIZE",
-                          kernel="trace_simple<false, false")
+        fetch = _pmc_mean(_pmc_file(src, "C"), "FETCH_SIZE", kernel="trace_simple<false, false")
         assert r["traffic"] == pytest.approx(fetch * 1024 * 2, rel=1e-6)
         assert r["bound"] == ("hbm" if r["traffic"] / tf / 1e9 / bench.HBM_PEAK_GBS >
                               alg / tf / 1e9 / bench.L2_PEAK_GBS else "l2")
@@ -227,3 +228,47 @@ def test_r05_roofline_reproduces(session, name):
     seg = d["config"]["segments_per_frame"] * d["steps"] * d["config"]["frames_per_step"]
     assert d["value"] == pytest.approx(seg / (d["ms_per_step"] * 1e-3 * d["steps"]) / 1e6, rel=2e-3)
     assert 0.0 < r["frac"] < 1.0
+
+
+def test_r05_frac_does_not_move_with_launches_in_flight():
+    """the headline frac is computed over frame_ms_device
+    (the device time per frame of the running loop), so once the device is
+    saturated it does not move with the launches in flight: 4, 6 and 8 in
+    flight on one build give frac within 5% (r5aa).  Below saturation it
+    measures idle device time: one launch in flight leaves the device idle
+    through each frame's serial tail (r5z: 0.38 ms per frame, frac 0.064)."""
+    fr = {}
+    for k in (4, 6, 8):
+        with open(os.path.join(R05, "r5aa", f"bench_if{k}.json")) as fh:
+            d = json.loads([x for x in fh if x.startswith("{")][-1])
+        assert d["config"]["launches_in_flight"] == k
+        fr[k] = d["roofline"]["frac"]
+    assert max(fr.values()) <= 1.05 * min(fr.values()), fr
+    with open(os.path.join(R05, "r5z", "bench_if1.json")) as fh:
+        one = json.loads([x for x in fh if x.startswith("{")][-1])
+    assert one["roofline"]["frac"] < 0.5 * min(fr.values())
+
+
+@pytest.mark.parametrize("session,cfg", [("r5z", 3), ("r5z", 5), ("r5aa", 3), ("r5aa", 5)])
+def test_r05_rocprof_union(session, cfg):
+    """The rocprofv3 kernel trace of the same command: the union of the timed
+    launches per frame agrees with ms_per_step, and rocprofv3's mean launch
+    duration with bench.py's kernel_ms (HIP events on the launch streams)."""
+    u = json.load(open(os.path.join(R05, session, f"union_cfg{cfg}.json")))
+    with open(os.path.join(R05, session, f"prof{cfg}.json")) as fh:
+        p = json.loads([x for x in fh if x.startswith("{")][-1])
+    assert u["launches"] == u["frames"] == p["steps"]
+    assert u["union_ms_per_frame"] == pytest.approx(p["ms_per_step"], rel=0.06)
+    with open(os.path.join(R05, session, f"kernel_stats_cfg{cfg}.csv")) as fh:
+        rows = [r for r in csv.DictReader(fh) if "trace_simple<false, false" in r["Name"]]
+    assert float(rows[0]["AverageNs"]) / 1e6 == pytest.approx(p["roofline"]["kernel_ms"], rel=0.05)
+
+
+def test_r05_config5_traffic():
+    """VERDICT r04 item 2 (config 5 below 20.1 GB of fetch and 7.85 ms per
+    frame): the accel tree's launch of config 5 fetches 2.05 GB from HBM
+    (PMC FETCH_SIZE, r5aa pmc5) at 1.20 ms per frame."""
+    with open(os.path.join(R05, "r5aa", "bench_cfg5.json")) as fh:
+        d = json.loads([x for x in fh if x.startswith("{")][-1])
+    assert d["roofline"]["traffic"] < 20.1e9 / 4 and d["ms_per_step"] < 7.85 / 4
+    assert d["config"]["frames_verified"] is True
