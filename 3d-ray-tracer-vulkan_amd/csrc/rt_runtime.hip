@@ -802,9 +802,12 @@ static size_t walk_bytes(const PerDevice& p) {
     return (size_t)(p.scene.n_layouts ? p.scene.layout_slots : p.scene.end2) * (p.scene.half ? 16 : 32);
 }
 
+// The accel walk runs 16x4 tiles on every scene: config 3 0.1205-0.1212 ms per
+// frame against 0.1226-0.1235 for 8x8, config 4 0.1482 against 0.1560-0.1569,
+// config 6 0.1233-0.1239 against 0.1216-0.1222 (profiles/r05/r5ac).
 static int wave_tile_of(const rt_ctx* ctx, const PerDevice& p) {
     if (ctx->wave_tile >= 0) return ctx->wave_tile;
-    return walk_bytes(p) > kWin32Bytes ? 1 : 0;
+    return (p.scene.n_layouts > 0 || walk_bytes(p) > kWin32Bytes) ? 1 : 0;
 }
 
 static int coop_window_of(const rt_ctx* ctx, const PerDevice& p) {

@@ -359,9 +359,11 @@ int rt_render_poll(rt_ctx* ctx, uint64_t ticket, int* done);
  *                   every frame run at once); 0 (default) = frame by frame
  *   "heavy_tiles_used" (rt_get_option only) heavy tiles of the last launch
  *   "wave_tile"     pixels per wave (8<<s) x (8>>s), s = 0..3; -1 (default) =
- *                   16x4 when the scene's walk records exceed 32 MB (config 5:
- *                   3% faster), else 8x8 (the shader's local_size; config 3:
- *                   0.8% faster than 16x4, 6% than 32x2, profiles/r02/tiles)
+ *                   16x4 on the accel tree (config 3 2% faster than 8x8,
+ *                   profiles/r05/r5ac) and when the reference tree's walk
+ *                   records exceed 32 MB (config 5: 3% faster), else 8x8 (the
+ *                   shader's local_size; config 3 on the reference tree: 0.8%
+ *                   faster than 16x4, 6% than 32x2, profiles/r02/tiles)
  *   "wave_tile_used" (rt_get_option only) the tile shape s the current scene
  *                   gets on device 0
  *   "extensions"    NON-REFERENCE features, bits (default 0 = the reference's
