@@ -168,6 +168,19 @@ struct TraceArgs {
     int      coop_win = 64;     // coop_walk's window: 64 or 32 slots (option coop_window)
     int      list_stride;       // band_list per frame: frame f's at band_list + f * list_stride
                                 //   (0 = one list for every frame of the launch)
+    // Split launch (option split_bounce, accel walk): kernel 1
+    // packs each wave's paths still alive at bounce split_bounce into the
+    // wave's 64 ray slots (3 float4 each) and writes the wave's count; a scan
+    // makes q_prefix (q_waves + 1 entries); kernel 2 finishes the paths 64 per
+    // wave in slot order.  q_slots null: one kernel.
+    int      split_bounce = 0;
+    float4*  q_slots = nullptr;
+    unsigned* q_count = nullptr;
+    unsigned* q_prefix = nullptr;
+    int      q_waves = 0;       // the slots' capacity in waves (launch_trace: kernel 1's waves)
+    int      q_grid = 0;        // kernel 2's one-wave workgroups
+    void*    q_temp = nullptr;  // the scan's temporary storage (rocPRIM), q_temp_bytes
+    size_t   q_temp_bytes = 0;
 };
 
 // Host-side compact-scene build from the reference records; validates the

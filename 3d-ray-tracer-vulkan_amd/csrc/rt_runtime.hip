@@ -4,6 +4,8 @@
 // barriers, staging image) has no counterpart: device buffers + one HIP
 // stream per device.
 #include "rt_internal.h"
+#include <rocprim/device/device_scan.hpp>
+
 #include "accel_build.h"
 
 #include <cmath>
@@ -235,6 +237,10 @@ static constexpr int kMaxSlots = 8;   // rt_render_async frame slots per device
 #ifndef RT_ACCEL_HALF
 #define RT_ACCEL_HALF 0
 #endif
+// Option split_bounce's default.
+#ifndef RT_SPLIT_BOUNCE
+#define RT_SPLIT_BOUNCE 0
+#endif
 
 struct PerDevice {
     int          device = 0;
@@ -311,6 +317,10 @@ struct PerDevice {
     std::vector<BandList> band_lists;   // rt_render_batch_device's band lists on this device
     std::vector<Graph> graphs;
     unsigned     graph_next = 0;
+    // option split_bounce: one set of ray slots per launch stream (rt_internal.h
+    // TraceArgs::q_slots), grown to the largest launch seen on that stream
+    struct Slots { hipStream_t s; char* base; int waves; size_t temp_bytes; };
+    std::vector<Slots> slots;
 };
 
 static constexpr size_t kMaxOrders = 16;
@@ -395,6 +405,8 @@ struct rt_ctx {
     int  learn_device = 1;         // heavy_first: learn the order on the device (rt_learn.hip; 0 = on the host)
     int  leaf_align = RT_LEAF_ALIGN;   // walk records: no leaf straddles a 128-B line (a pad slot before it)
     int  accel_half = RT_ACCEL_HALF;   // at the next upload: accel records in format 1 (accel_build.h)
+    int  split_bounce = RT_SPLIT_BOUNCE;   // accel walk: paths alive at this bounce finish in a second kernel
+                                   //   (0 = one kernel)
     int  accel = RT_ACCEL;         // at the next upload: 0 = the reference's tree and order; 1 / 8 = the
                                    //   SAH tree in 1 / 8 (octant) layouts (accel_build.h)
     int  order_split = 0;          // heavy_first: only tiles costing >= this percent of the costliest go first
@@ -900,7 +912,8 @@ static std::vector<uint64_t> launch_key(const TraceArgs& a, hipStream_t s) {
             (uint64_t)a.coop_lanes, (uint64_t)a.ext, (uint64_t)a.sky_enabled,
             (uint64_t)a.frame_count, P(a.accum), (uint64_t)a.walk, (uint64_t)a.block_waves, P(a.tile_order),
             (uint64_t)a.heavy_tiles, (uint64_t)(a.aux_stream != nullptr), (uint64_t)a.heavy_fused, P(a.heavy_px),
-            (uint64_t)a.n_heavy_px, P(a.tile_mask), (uint64_t)a.coop_walk, (uint64_t)a.coop_win};
+            (uint64_t)a.n_heavy_px, P(a.tile_mask), (uint64_t)a.coop_walk, (uint64_t)a.coop_win,
+            (uint64_t)a.split_bounce, P(a.q_slots), (uint64_t)a.q_waves, (uint64_t)a.q_grid};
     for (int f = 0; f < a.n_frames; ++f) {
         const CamF& c = a.cams[f];
         for (float v : {c.ox, c.oy, c.oz, c.lx, c.ly, c.lz, c.hx, c.hy, c.hz, c.vx, c.vy, c.vz}) k.push_back(F(v));
@@ -908,7 +921,57 @@ static std::vector<uint64_t> launch_key(const TraceArgs& a, hipStream_t s) {
     return k;
 }
 
-static int launch(const rt_ctx* ctx, PerDevice& p, const TraceArgs& a, hipStream_t s) {
+// Option split_bounce (accel walk, no extensions or counters): the stream's
+// ray slots for a launch of tw x th x n_frames pixels.  Slots that must grow
+// wait for the launches already on their stream, which may still use them.
+static int attach_slots(const rt_ctx* ctx, PerDevice& p, TraceArgs& a, hipStream_t s) {
+    a.q_slots = nullptr;
+    a.split_bounce = 0;
+    if (!p.scene.n_layouts || ctx->split_bounce <= 0 || ctx->split_bounce >= a.max_bounces || a.ext || a.diag ||
+        a.counters)
+        return RT_OK;
+    // kernel 1's waves, as launch_trace lays out its grid (an upper bound)
+    const int tw_w = 8 << a.wave_tile, th_w = 8 >> a.wave_tile, bw = std::max(1, a.block_waves);
+    const long long waves = (long long)((a.tw + bw * tw_w - 1) / (bw * tw_w)) * bw *
+                            ((a.th + th_w - 1) / th_w) * (long long)a.n_frames;
+    if (waves > (1 << 24)) return RT_OK;
+    PerDevice::Slots* q = nullptr;
+    for (auto& x : p.slots)
+        if (x.s == s) { q = &x; break; }
+    if (!q || q->waves < waves) {
+        if (q) {
+            RT_HIP_CHECK(hipStreamSynchronize(s));
+            (void)hipFree(q->base);
+            q->base = nullptr;
+            q->waves = 0;
+        } else {
+            p.slots.push_back(PerDevice::Slots{s, nullptr, 0, 0});
+            q = &p.slots.back();
+        }
+        size_t tb = 0;
+        RT_HIP_CHECK(rocprim::exclusive_scan(nullptr, tb, (const unsigned*)nullptr, (unsigned*)nullptr, 0u,
+                                             (size_t)waves, rocprim::plus<unsigned>()));
+        void* base = nullptr;
+        const size_t bytes = (size_t)waves * 64 * 48 + 2 * ((size_t)waves * 4 + 256) + tb + 256;
+        RT_HIP_CHECK(hipMalloc(&base, bytes));
+        q->base = static_cast<char*>(base);
+        q->waves = (int)waves;
+        q->temp_bytes = tb;
+    }
+    a.split_bounce = ctx->split_bounce;
+    a.q_slots = reinterpret_cast<float4*>(q->base);
+    a.q_count = reinterpret_cast<unsigned*>(q->base + (size_t)q->waves * 64 * 48);
+    a.q_prefix = reinterpret_cast<unsigned*>(reinterpret_cast<char*>(a.q_count) + (size_t)q->waves * 4 + 256);
+    a.q_temp = reinterpret_cast<char*>(a.q_prefix) + (size_t)q->waves * 4 + 256;
+    a.q_temp_bytes = q->temp_bytes;
+    a.q_waves = q->waves;
+    a.q_grid = std::max(1, p.n_cu * 32);        // kernel 2: a full device of one-wave workgroups
+    return RT_OK;
+}
+
+static int launch(const rt_ctx* ctx, PerDevice& p, const TraceArgs& a_in, hipStream_t s) {
+    TraceArgs a = a_in;
+    if (int rq = attach_slots(ctx, p, a, s)) return rq;
     // Only a frame of two launches (heavy tiles on an auxiliary stream,
     // heavy_stream 1) gains from a graph: its fork and join become edges.  A
     // single launch (the fused heavy tiles, or none) goes straight to the
@@ -1105,6 +1168,8 @@ int rt_destroy(rt_ctx* ctx) {
             if (p.aux_fork[k]) (void)hipEventDestroy(p.aux_fork[k]);
             if (p.aux_join[k]) (void)hipEventDestroy(p.aux_join[k]);
         }
+        for (auto& q : p.slots) (void)hipFree(q.base);
+        p.slots.clear();
         if (p.d_accum) (void)hipFree(p.d_accum);
         if (p.d_spheres) (void)hipFree(p.d_spheres);
         if (p.d_rgba) (void)hipFree(p.d_rgba);
@@ -1939,6 +2004,8 @@ int rt_set_option(rt_ctx* ctx, const char* name, int64_t value) {
         ctx->leaf_align = (int)value;                   // takes effect at the next rt_upload_scene
     } else if (std::strcmp(name, "accel") == 0 && (value == 0 || value == 1 || value == 8)) {
         ctx->accel = (int)value;                        // takes effect at the next rt_upload_scene
+    } else if (std::strcmp(name, "split_bounce") == 0 && value >= 0 && value <= 64) {
+        ctx->split_bounce = (int)value;
     } else if (std::strcmp(name, "accel_half") == 0 && (value == 0 || value == 1)) {
         ctx->accel_half = (int)value;                   // takes effect at the next rt_upload_scene
     } else if (std::strcmp(name, "heavy_stream") == 0 && value >= 0 && value <= 2) {
@@ -1980,6 +2047,7 @@ int rt_get_option(rt_ctx* ctx, const char* name, int64_t* value) {
     else if (std::strcmp(name, "leaf_align") == 0) *value = ctx->leaf_align;
     else if (std::strcmp(name, "accel") == 0) *value = ctx->accel;
     else if (std::strcmp(name, "accel_half") == 0) *value = ctx->accel_half;
+    else if (std::strcmp(name, "split_bounce") == 0) *value = ctx->split_bounce;
     else if (std::strcmp(name, "accel_half_used") == 0) *value = ctx->dev.empty() ? 0 : ctx->dev[0].scene.half;
     else if (std::strcmp(name, "walk_bytes") == 0) *value = ctx->dev.empty() ? 0 : (int64_t)walk_bytes(ctx->dev[0]);
     else if (std::strcmp(name, "accel_used") == 0) *value = ctx->dev.empty() ? 0 : ctx->dev[0].scene.n_layouts;

@@ -31,6 +31,8 @@
 #include <cstdlib>
 #include <cstring>
 
+#include <rocprim/device/device_scan.hpp>
+
 #include "rt_internal.h"
 
 namespace rtamd {
@@ -734,6 +736,10 @@ constexpr int kFeatFused = 64;    // heavy tiles in the same launch: workgroups 
 constexpr int kFeatWin32 = 128;   // cooperative windows of 32 slots (option coop_window), else 64
 constexpr int kFeatPad = 256;     // the production kernels (cooperative tail, no extensions) on records
                                   //   with pad slots (leaf_align); every other variant always reads pad bits
+constexpr int kFeatQ1 = 4096;     // split launch, kernel 1: paths alive at bounce split_bounce go to the
+                                  //   launch's ray slots (compacted per wave, no atomics)
+constexpr int kFeatQ2 = 8192;     // split launch, kernel 2: the slotted paths from bounce split_bounce,
+                                  //   64 per wave in slot order
 constexpr int kFeatHalf = 2048;   // option accel_half (with kFeatAccel): 16-B slots, half-precision internal
                                   //   boxes (accel_build.h format 1)
 constexpr int kFeatAccel = 512;   // option accel: the accel records and rules, packed records, the
@@ -833,11 +839,17 @@ void trace_simple(TraceArgs a) {
     constexpr bool ACC = (FEAT & kFeatAccel) != 0;
     constexpr bool HALF = ACC && (FEAT & kFeatHalf) != 0;
     constexpr bool PAD = !ACC && ((FEAT & kFeatPad) || (FEAT & (kFeatExt | kFeatFrontier)) || !(FEAT & kFeatCoopTail));
+    constexpr bool Q1 = (FEAT & kFeatQ1) != 0, Q2 = (FEAT & kFeatQ2) != 0;
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
     // frontier_walk's per-wave frontiers (kFCap entries per wave; dynamic LDS,
     // sized by the launch for variants with kFeatFrontier or kFeatFused)
     extern __shared__ uint4 fr[];
+    // Split kernel 2: a fixed grid of one-wave workgroups; wave k takes the
+    // slotted paths 64k .. 64k + 63 (then 64 (k + grid) ..), in slot order.
+    unsigned q_k = Q2 ? blockIdx.x : 0u;
+    const unsigned q_total = Q2 ? a.q_prefix[a.q_waves - 1] + a.q_count[a.q_waves - 1] : 0u;
+    if (Q2 && q_k * 64u >= q_total) return;
     // One wave = one tile of 64 pixels, (8 << s) x (8 >> s) with s = a.wave_tile
     // (s = 0: 8x8, the reference's local_size 8x8x1, compute_dynamic_ray.comp:157);
     // a workgroup = block_waves (4 or 1) such tiles side by side.
@@ -912,12 +924,15 @@ void trace_simple(TraceArgs a) {
     const int col = bx * a.block_waves + wave;           // wave-tile column
     const int fr_i = by / a.tiles_y;                     // the wave's frame of the batch (tile rows of frame
     by -= fr_i * a.tiles_y;                              //   f follow those of frame f - 1)
-    const int lx = col * tw_w + (tl & (tw_w - 1));
+    int lx = col * tw_w + (tl & (tw_w - 1));
     const int ly = by * th_w + (tl >> (3 + s));          // row within the frame's rows
-    const int lyo = fr_i * a.th + ly;                    // output row
+    int lyo = fr_i * a.th + ly;                          // output row
     // (a per-frame band list's -1 entries are padding rows: no pixel)
-    const bool pixel = lx < a.tw && ly < a.th && (sub < 0 || lane == 0) && !((skip_lanes >> lane) & 1ull) &&
+    const bool pixel = !Q2 && lx < a.tw && ly < a.th && (sub < 0 || lane == 0) && !((skip_lanes >> lane) & 1ull) &&
                        (a.list_stride == 0 || a.band_list[fr_i * a.list_stride + ly / a.band_h] >= 0);
+    // Split kernel 1: this wave's slot count starts at 0 (a wave whose paths
+    // all end before split_bounce never writes it again)
+    if (Q1 && lane == 0) a.q_count[k_wave] = 0u;
     const int coop_lanes = sub >= 0 ? 64 : a.coop_lanes;
     const float4* __restrict__ nodes = a.scene.nodes;
     const float4* __restrict__ leafs = a.scene.leafs;
@@ -928,8 +943,35 @@ void trace_simple(TraceArgs a) {
     unsigned long long d_iters = 0, d_windows = 0, d_coop_t = 0;   // diag builds only
     unsigned long long d_lane_windows = 0;           // diag: cooperative windows spent on this lane's walks
 
+  do {   // split kernel 2 loops over its packs of 64 slotted paths; every other kernel runs once
     uint32_t seed = 0;
     V3 o = {0.f, 0.f, 0.f}, d = {0.f, 0.f, 1.f};
+    V3 att = {1.0f, 1.0f, 1.0f};
+    bool alive = pixel;
+    int b0 = 0;
+    if (Q2) {
+        // path i of the slot order: source wave w with prefix[w] <= i < prefix[w + 1]
+        const unsigned i = q_k * 64u + (unsigned)lane;
+        alive = i < q_total;
+        b0 = a.split_bounce;
+        if (alive) {
+            int lo = 0, hi = a.q_waves;                  // prefix[lo] <= i < prefix[hi] (prefix[q_waves] = total)
+            while (hi - lo > 1) {
+                const int mid = (lo + hi) >> 1;
+                if (a.q_prefix[mid] <= i) lo = mid;
+                else hi = mid;
+            }
+            const float4* r = a.q_slots + 3 * ((size_t)lo * 64 + (i - a.q_prefix[lo]));
+            const float4 r0 = r[0], r1 = r[1], r2 = r[2];
+            o = {r0.x, r0.y, r0.z};
+            d = {r0.w, r1.x, r1.y};
+            att = {r1.z, r1.w, r2.x};
+            seed = __float_as_uint(r2.y);
+            const int pq = __float_as_int(r2.z);
+            lyo = pq / a.tw;
+            lx = pq - lyo * a.tw;
+        }
+    }
     if (pixel) {
         const int x = a.x0 + lx, y = frame_row(a, fr_i, ly);
         if ((FEAT & kFeatExt) && (a.ext & kExtAccumulate)) {
@@ -940,14 +982,26 @@ void trace_simple(TraceArgs a) {
             primary_ray(a, fr_i, x, y, seed, o, d);
         }
     }
-    V3 att = {1.0f, 1.0f, 1.0f};
-    bool alive = pixel;
 
     // The bounce loop (:179) is wave-uniform: a lane whose path has ended
     // stays in it with alive = false, so the cooperative tail below can use
     // every lane of the wave.
-    for (int b = 0; b < a.max_bounces; ++b) {
+    for (int b = b0; b < a.max_bounces; ++b) {
         if (__ballot(alive) == 0) break;
+        if (Q1 && b == a.split_bounce) {
+            // Split kernel 1: the paths still alive leave for this wave's 64
+            // ray slots, packed in lane order (no atomics); kernel 2 takes them.
+            const uint64_t m = __ballot(alive);
+            if (alive) {
+                float4* r = a.q_slots + 3 * ((size_t)k_wave * 64 + (size_t)lanes_below(m));
+                r[0] = make_float4(o.x, o.y, o.z, d.x);
+                r[1] = make_float4(d.y, d.z, att.x, att.y);
+                r[2] = make_float4(att.z, __uint_as_float(seed), __int_as_float(lyo * a.tw + lx), 0.0f);
+            }
+            if (lane == 0) a.q_count[k_wave] = (unsigned)__popcll(m);
+            alive = false;
+            break;
+        }
         float closest = kTMax;
         int hit = -1;
         const V3 inv = {1.0f / d.x, 1.0f / d.y, 1.0f / d.z};              // :89
@@ -1236,6 +1290,8 @@ void trace_simple(TraceArgs a) {
     }
     // A path still alive here ran no bounce at all (max_bounces 0): black.
     if (alive) finish_pixel<FEAT>(a, lx, lyo, V3{0.0f, 0.0f, 0.0f});
+    q_k += gridDim.x;
+  } while (Q2 && q_k * 64u < q_total);
     if (COUNT) flush_counters(a.counters, c_seg, c_node, c_tri, c_mat);
     if (DIAG) {
         diag_stamp(drec, 1);
@@ -1364,6 +1420,25 @@ hipError_t launch_trace(const TraceArgs& a, hipStream_t stream, int* kernels) {
     if (a.scene.n_layouts > 0) {
         // option accel (walk 2 records; the launcher never splits heavy tiles
         // or pixels out of an accel launch, and there is no frontier tail)
+        if (a.q_slots && a.split_bounce > 0 && a.split_bounce < a.max_bounces && feat == 0 && !a.scene.half &&
+            !a.diag && !a.counters && (int)(grid.x * grid.y) * bw <= a.q_waves) {
+            // split launch: kernel 1 to bounce split_bounce,
+            // the scan of its per-wave counts, kernel 2 for the rest
+            ao.q_waves = (int)(grid.x * grid.y) * bw;
+            hipLaunchKernelGGL((trace_simple<false, false, kFeatAccel | kFeatQ1, 2>), grid, block, 0, stream, ao);
+            size_t tb = a.q_temp_bytes;
+            const hipError_t se = rocprim::exclusive_scan(a.q_temp, tb, a.q_count, a.q_prefix, 0u,
+                                                          (size_t)ao.q_waves, rocprim::plus<unsigned>(), stream);
+            if (se != hipSuccess) return se;
+            TraceArgs a2 = ao;
+            a2.tile_order = nullptr;
+            a2.split_n = 0;
+            a2.block_waves = 1;
+            hipLaunchKernelGGL((trace_simple<false, false, kFeatAccel | kFeatQ2, 2>), dim3(a.q_grid), dim3(64), 0,
+                               stream, a2);
+            if (kernels) *kernels = 2;                          // the frame kernels (q_scan aside)
+            return hipGetLastError();
+        }
         if (a.scene.half) {
             // format 1 records: no cooperative tail (set_schedule: coop_lanes 0)
             if (feat & kFeatCoopTail) {

@@ -262,6 +262,14 @@ int rt_render_poll(rt_ctx* ctx, uint64_t ticket, int* done);
  *                   walk's own.  Heavy tiles / pixels are not
  *                   split out of accel launches (heavy_first still orders
  *                   the tiles)
+ *   "split_bounce"  accel walk, no extensions: b in 1..max_bounces-1 = a
+ *                   frame's paths still alive at bounce b leave its kernel for
+ *                   the wave's ray slots (packed per wave, no atomics), a scan
+ *                   orders them and a second kernel finishes them 64 per wave,
+ *                   so the few long late-bounce paths of a tile no longer hold
+ *                   a whole wave; 0 (default) = one kernel.
+ *                   Same frames; counting and diagnostic launches stay one
+ *                   kernel
  *   "accel_half"    at the next rt_upload_scene, accel records with the
  *                   internal nodes' boxes in IEEE half precision rounded
  *                   outward (16-B internal records instead of 32; leaves keep

@@ -233,3 +233,32 @@ def test_accel_is_the_default():
     finally:
         if old is not None:
             os.environ["RTAMD_ACCEL"] = old
+
+
+@pytest.mark.parametrize("split", [1, 2, 3])
+@pytest.mark.parametrize("k,b", [(2, 10), (3, 4), (6, 4)])
+def test_accel_split_launch(acc, k, b, split):
+    """Option split_bounce: kernel 1 to bounce split, each
+    wave's surviving paths packed into its ray slots, a scan, kernel 2 for the
+    rest, 64 paths per wave in slot order.  Same frames (RGBA8 and radiance)
+    as the oracle, in the learned order and on 4 streams."""
+    from rtamd import configs
+    from test_gpu_parity import _bands_device
+    cfg = configs.get(k)
+    built = cfg.build()
+    cam = cfg.camera()
+    _upload(acc, built, 8)
+    W, H = cfg.width, cfg.height
+    ref = _oracle(built, cam, W, H, b)
+    old = acc.get_option("split_bounce")
+    try:
+        acc.set_option("split_bounce", split)
+        acc.set_option("concurrent_launches", 4)
+        for _ in range(3):                         # the learning launch, then the learned order
+            rgba, rad, _ = _bands_device(acc, cam, W, H, b, H, 1, 0, stats=False)
+            _check(rgba, rad, None, ref, None, f"config {k} b{b} split {split}")
+        rgba, rad, _ = acc.render(cam, W, H, b, radiance=True)
+        _check(rgba, rad, None, ref, None, f"config {k} b{b} split {split} (rt_render)")
+    finally:
+        acc.set_option("split_bounce", old)
+        acc.set_option("concurrent_launches", 1)
