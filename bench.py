@@ -1196,7 +1196,7 @@ def main() -> None:
                                                                       "coop_window", "coop_window_used",
                                                                       "leaf_align", "leaf_align_used",
                                                                       "accel", "accel_used", "accel_half",
-                                                                      "accel_half_used",
+                                                                      "accel_half_used", "split_bounce",
                                                                       "wave_tile_used")},
                              "concurrent_launches": renderer.get_option("concurrent_launches"),
                              "heavy_tiles_used": heavy_used,
