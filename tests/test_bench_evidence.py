@@ -191,7 +191,9 @@ R05 = os.path.join(ROOT, "profiles", "r05")
 # (session, file) of the round-5 lines this round's evidence rests on (r5c's
 # lines predate the PMC records keyed by accel: their traffic came from the
 # reference walk's round-4 record, so they are not listed)
-R05_LINES = [("r5aa", "bench.json"), ("r5aa", "prof3.json"), ("r5aa", "prof5.json"), ("r5aa", "bench_cfg5.json"),
+R05_LINES = [("r5ah", "bench.json"), ("r5ah", "prof3.json"), ("r5ah", "prof5.json"), ("r5ah", "bench_cfg5.json"),
+             ("r5ah", "bench_cfg6.json"), ("r5ah", "bench_if4.json"), ("r5ah", "bench_if8.json"),
+             ("r5aa", "bench.json"), ("r5aa", "prof3.json"), ("r5aa", "prof5.json"), ("r5aa", "bench_cfg5.json"),
              ("r5aa", "bench_cfg6.json"), ("r5aa", "bench_if4.json"), ("r5aa", "bench_if6.json"),
              ("r5aa", "bench_if8.json")]
 
@@ -249,7 +251,7 @@ def test_r05_frac_does_not_move_with_launches_in_flight():
     assert one["roofline"]["frac"] < 0.5 * min(fr.values())
 
 
-@pytest.mark.parametrize("session,cfg", [("r5z", 3), ("r5z", 5), ("r5aa", 3), ("r5aa", 5)])
+@pytest.mark.parametrize("session,cfg", [("r5z", 3), ("r5z", 5), ("r5aa", 3), ("r5aa", 5), ("r5ah", 3), ("r5ah", 5)])
 def test_r05_rocprof_union(session, cfg):
     """The rocprofv3 kernel trace of the same command: the union of the timed
     launches per frame agrees with ms_per_step, and rocprofv3's mean launch
