@@ -181,10 +181,6 @@ struct TraceArgs {
     int      q_grid = 0;        // kernel 2's one-wave workgroups
     void*    q_temp = nullptr;  // the scan's temporary storage (rocPRIM), q_temp_bytes
     size_t   q_temp_bytes = 0;
-    // Path regeneration (option regen, accel walk): a wave
-    // traces regen tiles' pixels, a lane taking the next pixel of its pool
-    // when its path ends; 0 = one tile per wave (trace_simple).
-    int      regen = 0;
 };
 
 // Host-side compact-scene build from the reference records; validates the

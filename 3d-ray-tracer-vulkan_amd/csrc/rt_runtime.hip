@@ -237,11 +237,6 @@ static constexpr int kMaxSlots = 8;   // rt_render_async frame slots per device
 #ifndef RT_ACCEL_HALF
 #define RT_ACCEL_HALF 0
 #endif
-// Option regen's default: wave tiles per wave of the path-regenerating
-// kernel; 0 = one tile per wave (trace_simple).
-#ifndef RT_REGEN
-#define RT_REGEN 0
-#endif
 // Option split_bounce's default.
 #ifndef RT_SPLIT_BOUNCE
 #define RT_SPLIT_BOUNCE 0
@@ -410,7 +405,6 @@ struct rt_ctx {
     int  learn_device = 1;         // heavy_first: learn the order on the device (rt_learn.hip; 0 = on the host)
     int  leaf_align = RT_LEAF_ALIGN;   // walk records: no leaf straddles a 128-B line (a pad slot before it)
     int  accel_half = RT_ACCEL_HALF;   // at the next upload: accel records in format 1 (accel_build.h)
-    int  regen = RT_REGEN;         // accel walk: wave tiles per wave, lanes taking new pixels as paths end
     int  split_bounce = RT_SPLIT_BOUNCE;   // accel walk: paths alive at this bounce finish in a second kernel
                                    //   (0 = one kernel)
     int  accel = RT_ACCEL;         // at the next upload: 0 = the reference's tree and order; 1 / 8 = the
@@ -842,7 +836,6 @@ static int set_schedule(const rt_ctx* ctx, PerDevice& p, TraceArgs& a, const rt_
     a.coop_walk = p.scene.n_layouts ? 0 : ctx->coop_walk;
     a.coop_win = coop_window_of(ctx, p);
     a.block_waves = ctx->block_waves;
-    a.regen = (p.scene.n_layouts > 0 && !p.scene.half && a.block_waves == 1) ? ctx->regen : 0;
     a.ext = ctx->ext;
     a.scene.spheres = p.d_spheres;
     a.scene.n_spheres = (a.ext & kExtSpheres) ? p.n_spheres : 0;
@@ -920,7 +913,7 @@ static std::vector<uint64_t> launch_key(const TraceArgs& a, hipStream_t s) {
             (uint64_t)a.frame_count, P(a.accum), (uint64_t)a.walk, (uint64_t)a.block_waves, P(a.tile_order),
             (uint64_t)a.heavy_tiles, (uint64_t)(a.aux_stream != nullptr), (uint64_t)a.heavy_fused, P(a.heavy_px),
             (uint64_t)a.n_heavy_px, P(a.tile_mask), (uint64_t)a.coop_walk, (uint64_t)a.coop_win,
-            (uint64_t)a.split_bounce, P(a.q_slots), (uint64_t)a.q_waves, (uint64_t)a.q_grid, (uint64_t)a.regen};
+            (uint64_t)a.split_bounce, P(a.q_slots), (uint64_t)a.q_waves, (uint64_t)a.q_grid};
     for (int f = 0; f < a.n_frames; ++f) {
         const CamF& c = a.cams[f];
         for (float v : {c.ox, c.oy, c.oz, c.lx, c.ly, c.lz, c.hx, c.hy, c.hz, c.vx, c.vy, c.vz}) k.push_back(F(v));
@@ -2011,8 +2004,6 @@ int rt_set_option(rt_ctx* ctx, const char* name, int64_t value) {
         ctx->leaf_align = (int)value;                   // takes effect at the next rt_upload_scene
     } else if (std::strcmp(name, "accel") == 0 && (value == 0 || value == 1 || value == 8)) {
         ctx->accel = (int)value;                        // takes effect at the next rt_upload_scene
-    } else if (std::strcmp(name, "regen") == 0 && value >= 0 && value <= 64) {
-        ctx->regen = (int)value;
     } else if (std::strcmp(name, "split_bounce") == 0 && value >= 0 && value <= 64) {
         ctx->split_bounce = (int)value;
     } else if (std::strcmp(name, "accel_half") == 0 && (value == 0 || value == 1)) {
@@ -2057,7 +2048,6 @@ int rt_get_option(rt_ctx* ctx, const char* name, int64_t* value) {
     else if (std::strcmp(name, "accel") == 0) *value = ctx->accel;
     else if (std::strcmp(name, "accel_half") == 0) *value = ctx->accel_half;
     else if (std::strcmp(name, "split_bounce") == 0) *value = ctx->split_bounce;
-    else if (std::strcmp(name, "regen") == 0) *value = ctx->regen;
     else if (std::strcmp(name, "accel_half_used") == 0) *value = ctx->dev.empty() ? 0 : ctx->dev[0].scene.half;
     else if (std::strcmp(name, "walk_bytes") == 0) *value = ctx->dev.empty() ? 0 : (int64_t)walk_bytes(ctx->dev[0]);
     else if (std::strcmp(name, "accel_used") == 0) *value = ctx->dev.empty() ? 0 : ctx->dev[0].scene.n_layouts;

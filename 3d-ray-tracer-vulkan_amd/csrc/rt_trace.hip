@@ -1319,208 +1319,6 @@ void trace_simple(TraceArgs a) {
 }
 
 
-// Path regeneration (option regen, accel walk, format 0 records; DESIGN.md
-// §4c).  A wave owns a pool of a.regen wave tiles (positions k, k + G, k + 2G
-// ... of the launch's tile order, G = the grid: every pool mixes the order's
-// heavy and light tiles) and its lanes run their paths independently: a lane
-// whose path ends takes the pool's next pixel (a wave-uniform counter, ranks
-// by ballot: no atomics), so a wave no longer walks as long as its longest
-// path with the other lanes idle.  Each loop iteration is one walk step of the
-// walking lanes; lanes at the end of a segment wait until kRegenShade of them
-// (or every lane) are waiting, then shade together.  Per lane the arithmetic
-// is trace_simple's, in the same order: the same pixels and counters.
-constexpr int kRegenShade = 16;
-
-#ifndef RT_REGEN_WPE
-#define RT_REGEN_WPE RT_ACCEL_WPE
-#endif
-template <bool COUNT>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RT_REGEN_WPE)))
-void trace_regen(TraceArgs a) {
-    const int lane = threadIdx.x & 63;
-    const int s = a.wave_tile;
-    const int tw_w = 8 << s, th_w = 8 >> s;
-    const int n_tiles = a.tiles_x * a.tiles_y * a.n_frames;
-    const int pool = a.regen * 64;
-    const int G = (int)gridDim.x;
-    const int k = (int)blockIdx.x;
-    const float4* __restrict__ wr = a.scene.walk;
-    const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<float4*>(wr), 0, (int)((unsigned)(a.scene.end2 + 2) * 32u), 0x00020000);
-    const int end = a.scene.end;
-    unsigned long long c_seg = 0, c_node = 0, c_tri = 0, c_mat = 0;
-
-    // per-lane path state
-    uint32_t seed = 0;
-    V3 o = {0.f, 0.f, 0.f}, d = {0.f, 0.f, 1.f}, att = {1.f, 1.f, 1.f}, inv = {0.f, 0.f, 0.f};
-    float closest = kTMax;
-    int hit = -1, n = 0, lend = 0, b = 0, lx = 0, lyo = 0;
-    bool nleaf = false, incons = false;
-    bool need = true, walking = false, waiting = false;
-    float4 A = make_float4(0.f, 0.f, 0.f, 0.f), B = A, Q0 = A, Q1 = A;
-    int q_next = 0;                                       // wave-uniform: the pool's next pixel
-
-    // a segment from o along d: reset the walk at the root of d's octant layout
-    auto start_segment = [&]() {
-        closest = kTMax;
-        hit = -1;
-        incons = false;
-        inv = {1.0f / d.x, 1.0f / d.y, 1.0f / d.z};                        // :89
-        n = 0;
-        if (a.scene.n_layouts == 8)
-            n = ((__float_as_uint(d.x) >> 31) | ((__float_as_uint(d.y) >> 31) << 1) |
-                 ((__float_as_uint(d.z) >> 31) << 2)) * a.scene.layout_slots;
-        lend = n + a.scene.layout_slots;
-        nleaf = a.scene.root_leaf != 0;
-        if (COUNT) {
-            ++c_seg;
-            if (end > 0) ++c_node;                                         // the root visit
-        }
-        walking = end > 0;
-        waiting = !walking;
-        if (walking) {
-            A = wbuf(wrs, n, 0);
-            B = wbuf(wrs, n, 16);
-            if (nleaf) {
-                Q0 = wbuf(wrs, n, 32);
-                Q1 = wbuf(wrs, n, 48);
-            }
-        }
-    };
-
-    for (;;) {
-        // 1. lanes whose path ended take the pool's next pixels
-        uint64_t m = __ballot(need);
-        while (m != 0 && q_next < pool) {
-            const int q = q_next + lanes_below(m);
-            q_next += __popcll(m);
-            if (need && q < pool) {
-                const int j = k + (q >> 6) * G;                              // the tile's place in the order
-                if (j < n_tiles) {
-                    const int t = a.tile_order ? a.tile_order[j] : j;
-                    const int tl = q & 63;
-                    int by = t / a.tiles_x;
-                    const int bx = t - by * a.tiles_x;
-                    const int f = by / a.tiles_y;
-                    by -= f * a.tiles_y;
-                    const int px = bx * tw_w + (tl & (tw_w - 1));
-                    const int py = by * th_w + (tl >> (3 + s));
-                    if (px < a.tw && py < a.th &&
-                        (a.list_stride == 0 || a.band_list[f * a.list_stride + py / a.band_h] >= 0)) {
-                        lx = px;
-                        lyo = f * a.th + py;
-                        need = false;
-                        if (a.max_bounces <= 0) {
-                            finish_pixel<0>(a, lx, lyo, V3{0.0f, 0.0f, 0.0f});
-                            need = true;
-                        } else {
-                            primary_ray(a, f, a.x0 + px, frame_row(a, f, py), seed, o, d);
-                            att = {1.0f, 1.0f, 1.0f};
-                            b = 0;
-                            start_segment();
-                        }
-                    }
-                }
-            }
-            m = __ballot(need);
-        }
-        const uint64_t wm = __ballot(walking);
-        const uint64_t sm = __ballot(waiting);
-        if (wm == 0 && sm == 0) break;                     // the pool is done and every path has ended
-
-        // 2. one walk step of the walking lanes (trace_simple's accel step)
-        if (walking) {
-            float te;
-            bool ind;
-            slab(A, B, o, inv, te, ind);
-            const bool hb = ind && accel_enter(te, closest);
-            const uint32_t aw = __float_as_uint(A.w), bw = __float_as_uint(B.w);
-            const int nxt = nleaf ? n + 2 : (hb ? n + 1 : (int)(aw & kIdx));
-            const bool nl = (((hb && !nleaf) ? bw : (aw >> 31)) & 1u) != 0u;
-            const float v0x = B.w;
-            if (COUNT && hb && !nleaf) c_node += 2;
-            A = wbuf(wrs, nxt, 0);                                           // slot end is padding
-            B = wbuf(wrs, nxt, 16);
-            if (hb && nleaf) {                                               // hit_triangle (:196-200)
-                if (COUNT) ++c_tri;
-                float t;
-                if (tri_test(make_float4(v0x, Q0.x, Q0.y, 0.f), make_float4(Q0.z, Q0.w, Q1.x, 0.f),
-                             make_float4(Q1.y, Q1.z, Q1.w, 0.f), o, d, t) &&
-                    accel_take(t, (int)(aw & kTri), closest, hit)) {
-                    closest = t;
-                    hit = (int)(aw & kTri);
-                    incons = t < te;
-                }
-            }
-            if (nl && nxt < lend) {
-                Q0 = wbuf(wrs, nxt, 32);
-                Q1 = wbuf(wrs, nxt, 48);
-            }
-            n = nxt;
-            nleaf = nl;
-            if (n >= lend) {
-                walking = false;
-                waiting = true;
-            }
-        }
-
-        // 3. the waiting lanes shade together once enough of them wait
-        const uint64_t sm2 = __ballot(waiting);
-        const int nw = __popcll(sm2);
-        if (nw == 0 || (nw < kRegenShade && __ballot(walking) != 0)) continue;
-        // the reference-order fallback, whole wave per segment
-        uint64_t redo = __ballot(waiting && hit >= 0 && incons);
-        while (redo != 0) {
-            const int L = __ffsll((long long)redo) - 1;
-            redo &= redo - 1;
-            const V3 bo = {lane_f(o.x, L), lane_f(o.y, L), lane_f(o.z, L)};
-            const V3 bd = {lane_f(d.x, L), lane_f(d.y, L), lane_f(d.z, L)};
-            const V3 bi = {lane_f(inv.x, L), lane_f(inv.y, L), lane_f(inv.z, L)};
-            float bc = kTMax;
-            int bh = -1;
-            bool bx = false;
-            unsigned long long cn = 1, ct = 0;                               // the reference walk's root visit
-            coop_walk<COUNT, 64, true, false>(a.scene.walk_ref, a.scene.end2_ref, 0, bo, bd, bi, bc, bh, cn, ct, bx);
-            if (lane == L) {
-                closest = bc;
-                hit = bh;
-                if (COUNT) {
-                    c_node += cn;
-                    c_tri += ct;
-                }
-            }
-        }
-        if (waiting) {
-            waiting = false;
-            V3 fin = {0.0f, 0.0f, 0.0f};
-            bool ends = true;
-            if (hit >= 0) {                                                  // :212
-                if (COUNT) ++c_mat;
-                const V3 hp = vadd(o, vscale(d, closest));                  // ray_at :77-79
-                const V3 nrm = hit_normal(a.scene.norms, hit, d);
-                const float4 M = a.scene.mats[kShadeStride * hit];
-                V3 nd;
-                if (scatter(M, d, nrm, seed, nd)) {
-                    att = vmul(att, V3{M.x, M.y, M.z});
-                    o = hp;
-                    d = nd;
-                    ends = b == a.max_bounces - 1;                          // :229-231: black
-                }
-            } else {
-                fin = vmul(att, sky_color(d));
-            }
-            if (ends) {
-                finish_pixel<0>(a, lx, lyo, fin);
-                need = true;
-            } else {
-                ++b;
-                start_segment();
-            }
-        }
-    }
-    if (COUNT) flush_counters(a.counters, c_seg, c_node, c_tri, c_mat);
-}
-
 }  // namespace
 
 // The fused heavy-pixel launch (walk 2), in the window size and record form
@@ -1640,16 +1438,6 @@ hipError_t launch_trace(const TraceArgs& a, hipStream_t stream, int* kernels) {
             hipLaunchKernelGGL((trace_simple<false, false, kFeatAccel | kFeatQ2, 2>), dim3(a.q_grid), dim3(64), 0,
                                stream, a2);
             if (kernels) *kernels = 2;                          // the frame kernels (q_scan aside)
-            return hipGetLastError();
-        }
-        if (a.regen > 0 && feat == 0 && !a.scene.half && !a.diag && bw == 1 && !a.split_bounce) {
-            // path regeneration: a.regen tiles per wave
-            TraceArgs ar = ao;
-            ar.tiles_x = (a.tw + tw_w - 1) / tw_w;
-            const int n_tiles = ar.tiles_x * tiles_y * a.n_frames;
-            const dim3 gr((unsigned)((n_tiles + a.regen - 1) / a.regen));
-            if (a.counters) hipLaunchKernelGGL((trace_regen<true>), gr, dim3(64), 0, stream, ar);
-            else hipLaunchKernelGGL((trace_regen<false>), gr, dim3(64), 0, stream, ar);
             return hipGetLastError();
         }
         if (a.scene.half) {

@@ -262,12 +262,6 @@ int rt_render_poll(rt_ctx* ctx, uint64_t ticket, int* done);
  *                   walk's own.  Heavy tiles / pixels are not
  *                   split out of accel launches (heavy_first still orders
  *                   the tiles)
- *   "regen"         accel walk (format 0), no extensions, block_waves 1: r >
- *                   0 = each wave owns a pool of r wave tiles and a lane whose
- *                   path ends takes the pool's next pixel (path regeneration,
- *                   DESIGN.md §4c), so lanes do not idle behind the wave's
- *                   longest path; 0 = one tile per wave.  Same frames and
- *                   counters
  *   "split_bounce"  accel walk, no extensions: b in 1..max_bounces-1 = a
  *                   frame's paths still alive at bounce b leave its kernel for
  *                   the wave's ray slots (packed per wave, no atomics), a scan

@@ -263,27 +263,3 @@ def test_accel_split_launch(acc, k, b, split):
         acc.set_option("split_bounce", old)
         acc.set_option("concurrent_launches", 1)
 
-
-@pytest.mark.parametrize("regen", [1, 2, 4])
-@pytest.mark.parametrize("k,b", [(2, 10), (3, 4), (6, 4)])
-def test_accel_regen(acc, k, b, regen):
-    """Option regen: a wave owns regen tiles and its lanes
-    take new pixels as their paths end.  Same frames as the oracle and the
-    same counters as the accel model, in raster and in the learned order."""
-    from rtamd import configs
-    from test_gpu_parity import _bands_device
-    cfg = configs.get(k)
-    built = cfg.build()
-    cam = cfg.camera()
-    _upload(acc, built, 8)
-    W, H = cfg.width, cfg.height
-    ref = _oracle(built, cam, W, H, b)
-    model = _model(built, cam, W, H, b, 8)
-    old = acc.get_option("regen")
-    try:
-        acc.set_option("regen", regen)
-        for stats in (False, True, False, True):   # learning, then the learned order; counted and not
-            rgba, rad, st = _bands_device(acc, cam, W, H, b, H, 1, 0, stats=stats)
-            _check(rgba, rad, st if stats else None, ref, model, f"config {k} b{b} regen {regen}")
-    finally:
-        acc.set_option("regen", old)
