@@ -1318,7 +1318,6 @@ void trace_simple(TraceArgs a) {
     }
 }
 
-
 }  // namespace
 
 // The fused heavy-pixel launch (walk 2), in the window size and record form
