@@ -70,8 +70,7 @@ def main():
     union = union_length(iv) / 1e6
     span = (max(e for _, e in iv) - min(s for s, _ in iv)) / 1e6
     def short(k):
-        i = k.index("trace_simple") if "trace_simple" in k else k.index("trace_queue")
-        return k[i:].split(">(")[0] + ">"
+        return k[k.index("trace_simple"):].split(">(")[0] + ">"
     names = sorted({short(r["Kernel_Name"]) for r in timed})
     by_kernel = {nm: round(statistics.mean((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6
                                            for r in timed if short(r["Kernel_Name"]) == nm), 4) for nm in names}
