@@ -1031,14 +1031,13 @@ void trace_simple(TraceArgs a) {
             // Q0 and Q1, the rest of its triangle.
             float4 A, B, Q0, Q1;
             const float4* __restrict__ wr = a.scene.walk;
-#if RT_CHAIN >= 2
             // a buffer resource over the records: the next slot's address is one
-            // shift of its index (the offset field adds the 16-B halves)
+            // shift of its index (the offset field adds the 16-B halves); the
+            // half-format walk uses it whatever RT_CHAIN is
             const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc(
                 const_cast<float4*>(wr), 0,
                 HALF ? (int)((unsigned)(a.scene.end2 + 4) * 16u) : (int)((unsigned)(a.scene.end2 + 2) * 32u),
                 0x00020000);
-#endif
             if (HALF && walking) {
                 A = hbuf(wrs, n);
                 if (nleaf) {
