@@ -13,6 +13,12 @@
 // node for node: next = hit ? i+1 : skip(i).  Every schedule below visits the
 // same nodes, runs the same triangle tests in the same order and sees the same
 // closest_t at each test, so frames and work counters are identical.
+// Option accel (the default, kFeatAccel) walks the same way over
+// a SAH tree built at upload (accel_build.h), in the ray's octant layout, with
+// the rules that keep the reference's closest hit (accel_enter, accel_take) and
+// the reference-order fallback; kFeatHalf (option accel_half) reads its 16-B
+// half-precision internal records; kFeatQ1 / kFeatQ2 (option split_bounce)
+// split a frame's paths over two kernels (§4b).
 //
 // The kernel, trace_simple: one lane = one pixel for its whole path; a wave
 // is a tile of 64 pixels (the reference's 8x8 dispatch shape, or 16x4 / 32x2
