@@ -3,7 +3,15 @@
 
 Partitions of a frame over the N ranks:
 
-* weighted interleaved row bands (bench.py's N > 1 default; band_owners,
+* contiguous spans of an exchange batch (bench.py's N > 1 default since round
+  5; SpanPlan, SpanTracer, span_send / span_post_recvs / span_finish_recvs,
+  exchange_spans): a batch of G frames is one column of G x H rows cut into N
+  contiguous spans of whole bands, rank 0's root_weight times the others'; a
+  rank traces its span one frame per launch (whole frames, a band run at either
+  end) and rank 0 receives every other span straight into the batch's frames
+  (RCCL point-to-point, no assembly), the rows travelling as RGB (3/4 of the
+  bytes; the alpha byte is always 255);
+* weighted interleaved row bands (round 4's default; band_owners,
   SharePlan, gather_shares): the band_h-row bands are dealt out by a smooth
   weighted round robin, rank 0 with weight root_weight (it also receives and
   assembles every frame) and the others with weight 1, so every rank's bands
@@ -587,33 +595,88 @@ class SpanTracer:
                                        C.byref(stats) if stats is not None else None))
 
 
-def exchange_spans(column, span, plan: SpanPlan, group=None) -> None:
-    """One batch of the spans partition.  Rank 0: column is the batch's
-    [n_frames * height, W, C] frames, its own span traced in place; every
-    other span is received straight into its rows.  Rank r > 0: span is its
-    [>= rows[r], W, C] span buffer, sent to rank 0.  One batch_isend_irecv
-    (one RCCL group); on return the current stream is ordered after it."""
+def _glob(group):
+    import torch.distributed as dist
+    return (lambda r: dist.get_global_rank(group, r)) if group is not None else (lambda r: r)
+
+
+def _staged(group, t) -> bool:
+    """gloo moves host memory only: device tensors are staged through the host."""
+    import torch.distributed as dist
+    return dist.get_backend(group) == "gloo" and t is not None and t.is_cuda
+
+
+def span_send(span, plan: SpanPlan, rgb=None, rad=None, group=None) -> list:
+    """Rank r > 0's send of its span of a batch: span is its [>= rows[r], W, 4]
+    RGBA8 span buffer.  rgb (a [>= rows[r], W, 3] buffer): the rows travel as
+    RGB, packed here (the alpha byte is always 255, compute_dynamic_ray.comp:235),
+    3/4 of the bytes over the link.  rad: the span's float radiance, sent after.
+    One batch_isend_irecv (one RCCL group); returns its works (wait() orders the
+    current stream after the send)."""
     import torch.distributed as dist
     rank = dist.get_rank(group)
-    buf = column if rank == 0 else span
-    staged = dist.get_backend(group) == "gloo" and buf is not None and buf.is_cuda   # gloo moves host memory
-    glob = (lambda r: dist.get_global_rank(group, r)) if group is not None else (lambda r: r)
+    n = plan.rows[rank]
+    if n == 0:
+        return []
+    src = span[:n]
+    if rgb is not None:
+        rgb[:n].copy_(src[:, :, :3])
+        src = rgb[:n]
+    bufs = [src] + ([rad[:n]] if rad is not None else [])
+    ops = [dist.P2POp(dist.isend, b.cpu() if _staged(group, b) else b, _glob(group)(0), group) for b in bufs]
+    return dist.batch_isend_irecv(ops)
+
+
+def span_post_recvs(column, plan: SpanPlan, rgb=None, rad=None, group=None):
+    """Rank 0's receives of every other span of a batch, posted at once:
+    column is the batch's [n_frames * height, W, 4] RGBA8 frames (rank 0's
+    own span traced in place), rgb (with the RGB wire) a [n_frames * height, W,
+    3] landing the RGB rows arrive in, rad the batch's float radiance.  Returns
+    (works, landings) for span_finish_recvs."""
+    import torch
+    import torch.distributed as dist
+    glob = _glob(group)
     ops, landings = [], []
-    if rank == 0:
-        for r, y0, n in plan.recv_slices():
-            dst = column[y0:y0 + n]
-            if staged:
-                landings.append((dst, dst.cpu()))
+    for r, y0, n in plan.recv_slices():
+        for buf in ((rgb if rgb is not None else column),) + ((rad,) if rad is not None else ()):
+            dst = buf[y0:y0 + n]
+            if _staged(group, dst):
+                landings.append((dst, torch.empty(dst.shape, dtype=dst.dtype)))
                 dst = landings[-1][1]
             ops.append(dist.P2POp(dist.irecv, dst, glob(r), group))
-    elif plan.rows[rank] > 0:
-        src = span[: plan.rows[rank]]
-        ops.append(dist.P2POp(dist.isend, src.cpu() if staged else src, glob(0), group))
-    if ops:
-        for w in dist.batch_isend_irecv(ops):
-            w.wait()
+    return (dist.batch_isend_irecv(ops) if ops else []), landings
+
+
+def span_finish_recvs(works, landings, column, plan: SpanPlan, rgb=None) -> None:
+    """Completes span_post_recvs: waits for the receives (NCCL: the current
+    stream waits; gloo: the host), lands the host-staged rows, and with the RGB
+    wire writes the received RGB rows into the RGBA8 frames (their alpha bytes
+    must already be 255: set once when the frames buffer is made)."""
+    for w in works:
+        w.wait()
     for dst, host in landings:
         dst.copy_(host)
+    sl = plan.recv_slices()
+    if rgb is not None and sl:
+        y = sl[0][1]                         # the received rows follow rank 0's span, to the column's end
+        end = plan.n_frames * plan.height
+        column[y:end, :, :3].copy_(rgb[y:end])
+
+
+def exchange_spans(column, span, plan: SpanPlan, group=None, rgb=None) -> None:
+    """One batch of the spans partition, both halves at once.  Rank 0: column
+    is the batch's [n_frames * height, W, C] frames, its own span traced in
+    place; every other span is received straight into its rows.  Rank r > 0:
+    span is its [>= rows[r], W, C] span buffer, sent to rank 0.  rgb: the RGB
+    wire (C = 4; span_send / span_post_recvs).  On return the current stream is
+    ordered after the exchange."""
+    import torch.distributed as dist
+    if dist.get_rank(group) == 0:
+        works, landings = span_post_recvs(column, plan, rgb=rgb, group=group)
+        span_finish_recvs(works, landings, column, plan, rgb=rgb)
+    else:
+        for w in span_send(span, plan, rgb=rgb, group=group):
+            w.wait()
 
 
 # --- rotating row blocks (strong scaling, an option) -------------------------

@@ -347,6 +347,10 @@ def main() -> None:
     ap.add_argument("--ring", type=int, default=2,
                     help="N > 1: exchange batches of slots in the ring (>= 2); a batch's slots are retraced only "
                          "after the exchange ring - 1 batches back")
+    ap.add_argument("--wire", choices=("rgb", "rgba"), default="rgb",
+                    help="spans: the RGBA8 rows travel as RGB (the alpha byte is always 255, "
+                         "compute_dynamic_ray.comp:235), 3/4 of the bytes over each xGMI link; rank 0 writes "
+                         "them into its RGBA8 frames, whose alpha it set once")
     ap.add_argument("--gather", choices=("rgba", "radiance"), default="rgba",
                     help="N > 1: radiance = gather the float radiance beside the RGBA8 frame")
     ap.add_argument("--camera-path", choices=("static", "orbit"), default="static")
@@ -395,7 +399,7 @@ def main() -> None:
     from rtamd import configs
     from rtamd._lib import CameraUBO, Stats, check
     from rtamd.dist import (SharePlan, ShareTracer, SpanPlan, SpanTracer, TilePlan, assemble_shares, band_list,
-                            exchange_spans, gather_stack, gather_tiles)
+                            gather_stack, gather_tiles, span_finish_recvs, span_post_recvs, span_send)
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -493,6 +497,7 @@ def main() -> None:
     band_h = args.band
     plan = tplan = None
     src_index = None
+    wire_rgb = False                                  # spans: RGB rows on the wire (below)
     if mode in ("bands", "pieces"):
         rw = args.root_weight if args.root_weight >= 0 else default_root_weight(world)
         deal = args.deal
@@ -520,6 +525,14 @@ def main() -> None:
         # received into them); rank r: its span
         rows = G * H if rank == 0 else plan.per_rank
         rgba_slots = torch.empty((R, rows, W, 4), dtype=torch.uint8, device=dev)
+        wire_rgb = args.wire == "rgb" and world > 1
+        if wire_rgb:
+            # RGB on the wire: a sender packs its span, rank 0 receives into a
+            # packed landing and writes the RGB bytes into its frames, whose
+            # alpha bytes (255, as the kernel writes them) are set here once
+            rgb_slots = torch.empty((R, rows, W, 3), dtype=torch.uint8, device=dev)
+            if rank == 0:
+                rgba_slots.fill_(255)
         rad_slots = torch.empty((R, rows, W, 3), dtype=torch.float32, device=dev) if rad_on else None
         px_per_frame = plan.rows[rank] * W // G
     elif mode == "tiles":
@@ -536,7 +549,7 @@ def main() -> None:
     if emu and mode == "spans":
         # rank 0: the others' spans land in its frames (a device copy per span,
         # the bytes RCCL's receives write); rank r: its span read once (the send)
-        emu_buf = torch.zeros((plan.per_rank, W, 4), dtype=torch.uint8, device=dev)
+        emu_buf = torch.zeros((plan.per_rank, W, 3 if wire_rgb else 4), dtype=torch.uint8, device=dev)
         emu_land = torch.empty_like(emu_buf)
     elif emu:
         if mode not in ("bands", "pieces"):
@@ -693,7 +706,6 @@ def main() -> None:
     span_sent = [None] * R     # r > 0: event after the last send out of slot h
     span_recv = [None] * R     # rank 0: (works, landings, k_end, e0) of slot h's pending receive group
     send_q = []                # r > 0: (launch end events, slot, out_row, rows) of traced batches not yet sent
-    staged = backend == "gloo"  # gloo moves host memory: device rows staged through the host
 
     def span_send(timed):
         e_ends, h, orow, nr = send_q.pop(0)
@@ -703,16 +715,16 @@ def main() -> None:
         if timed:
             e0, e1 = timing_event(), timing_event()
             e0.record(main_stream)
-        src = rgba_slots[h][orow:orow + nr]
         if emu:
+            src = rgba_slots[h][orow:orow + nr]
+            if wire_rgb:
+                rgb_slots[h][orow:orow + nr].copy_(src[:, :, :3])  # pack: the alpha byte stays home
+                src = rgb_slots[h][orow:orow + nr]
             if os.environ.get("BENCH_EMULATE_NOX") != "1":
                 emu_land[:nr].copy_(src)               # the send's read of the rows
         else:
-            ops = [dist.P2POp(dist.isend, src.cpu() if staged else src, 0)]
-            if rad_on:
-                rs = rad_slots[h][orow:orow + nr]
-                ops.append(dist.P2POp(dist.isend, rs.cpu() if staged else rs, 0))
-            for w in dist.batch_isend_irecv(ops):
+            for w in span_send(rgba_slots[h], plan, rgb=rgb_slots[h] if wire_rgb else None,
+                               rad=rad_slots[h] if rad_on else None):
                 w.wait()                               # NCCL: main_stream waits for the send (host free)
         if timed:
             e1.record(main_stream)
@@ -727,34 +739,22 @@ def main() -> None:
         if timed:
             e0 = timing_event()
             e0.record(main_stream)
-        col = rgba_slots[h]
         works, landings = [], []
         if emu:
+            col = rgb_slots[h] if wire_rgb else rgba_slots[h]
             if os.environ.get("BENCH_EMULATE_NOX") != "1":
-                for r_, jl_list in recv_plan:          # the bytes the receives write
-                    for y0, nr in jl_list:
-                        col[y0:y0 + nr].copy_(emu_buf[:nr])
+                for _, y0, nr in plan.recv_slices():   # the bytes the receives write
+                    col[y0:y0 + nr].copy_(emu_buf[:nr])
         else:
-            ops = []
-            for r_, jl_list in recv_plan:
-                for y0, nr in jl_list:
-                    for buf in ((col, rad_slots[h]) if rad_on else (col,)):
-                        dst = buf[y0:y0 + nr]
-                        if staged:
-                            landings.append((dst, torch.empty(dst.shape, dtype=dst.dtype)))
-                            dst = landings[-1][1]
-                        ops.append(dist.P2POp(dist.irecv, dst, r_))
-            if ops:
-                works = dist.batch_isend_irecv(ops)
+            works, landings = span_post_recvs(rgba_slots[h], plan, rgb=rgb_slots[h] if wire_rgb else None,
+                                              rad=rad_slots[h] if rad_on else None)
         span_recv[h] = (works, landings, k0 + G, e0)
 
     def span_complete_recvs(h, timed):
         works, landings, k_end, e0 = span_recv[h]
         span_recv[h] = None
-        for w in works:
-            w.wait()                                   # NCCL: main_stream waits (gloo: the host)
-        for dst, host in landings:
-            dst.copy_(host)
+        # NCCL: main_stream waits (gloo: the host); the RGB rows into the frames
+        span_finish_recvs(works, landings, rgba_slots[h], plan, rgb=rgb_slots[h] if wire_rgb else None)
         if timed and e0 is not None:
             e1 = timing_event()
             e1.record(main_stream)
@@ -767,10 +767,6 @@ def main() -> None:
             last["rad"] = rad_slots[h][:G * H].view(G, H, W, 3) if rad_on else None
             last["frames"] = list(range(k_end - G, k_end))
 
-    # rank 0's receives per batch: for every rank r > 0, its launches' rows of
-    # the batch column in launch order (the order rank r sends them)
-    recv_plan = [(r_, [(plan.row0[r_], plan.rows[r_])]) for r_ in range(1, world) if plan.rows[r_]] \
-        if mode == "spans" else []
 
     def phase_spans(n_frames, evs=None):
         """n_frames frames in whole exchange batches: per batch this rank's
@@ -1185,7 +1181,8 @@ def main() -> None:
                 "band_h": band_h if mode in ("bands", "pieces", "spans") else None,
                 "root_weight": plan.root_weight if plan is not None else None,
                 "deal": (("rotate" if plan.lists else "fixed") if mode == "bands" else None),
-                "gather": ("rgba8 + float radiance" if rad_on else "rgba8") if dist_on else None,
+                "gather": ((("rgb8 on the wire (alpha 255 set on rank 0)" if wire_rgb else "rgba8") +
+                            (" + float radiance" if rad_on else "")) if dist_on else None),
                 "frames_verified": verified,
                 "parallelism": f"{mode}{world}",
                 "schedule": {**{k: renderer.get_option(k) for k in ("walk", "wave_tile", "coop_lanes",

@@ -275,9 +275,15 @@ def _share_worker(rank, world, port, q, kind, arg, n_frames, W, H, B):
             # bench.py --partition spans: rank 0 traces its span in place in
             # the batch's frames, the others into a span buffer; one group of
             # point-to-point receives lands every span in rank 0's frames
-            band_h, rw = arg
+            band_h, rw, wire = arg
             plan = SpanPlan(H, band_h, world, n_frames, rw)
             col = torch.zeros((n_frames * H, W, 4), dtype=torch.uint8) if rank == 0 else None
+            rgb = None
+            if wire == "rgb":
+                # the RGB wire: rank 0's frames get their alpha bytes once, the rows travel as RGB
+                rgb = torch.zeros(((n_frames * H) if rank == 0 else plan.per_rank, W, 3), dtype=torch.uint8)
+                if rank == 0:
+                    col[:, :, 3] = 255
             colr = torch.zeros((n_frames * H, W, 3), dtype=torch.float32) if rank == 0 else None
             span = torch.zeros((plan.per_rank, W, 4), dtype=torch.uint8) if rank else None
             spanr = torch.zeros((plan.per_rank, W, 3), dtype=torch.float32) if rank else None
@@ -290,7 +296,7 @@ def _share_worker(rank, world, port, q, kind, arg, n_frames, W, H, B):
                 (col if rank == 0 else span)[o:o + n] = torch.from_numpy(a)
                 (colr if rank == 0 else spanr)[o:o + n] = torch.from_numpy(r)
                 traced += W * n
-            exchange_spans(col, span, plan)
+            exchange_spans(col, span, plan, rgb=rgb)
             exchange_spans(colr, spanr, plan)
             out = col.view(n_frames, H, W, 4) if rank == 0 else None
             outr = colr.view(n_frames, H, W, 3) if rank == 0 else None
@@ -479,15 +485,19 @@ def test_share_tracer_rejects_uneven_lists():
     assert tt.rect == (960, 540, 960, 540)
 
 
-@pytest.mark.parametrize("world,n_frames,band_h,rw", [(2, 3, 4, 1.0), (4, 4, 4, 0.6), (8, 8, 2, 0.8), (3, 2, 8, 0.0)])
-def test_spans_weak_scaling(world, n_frames, band_h, rw):
+@pytest.mark.parametrize("world,n_frames,band_h,rw,wire", [(2, 3, 4, 1.0, "rgba"), (4, 4, 4, 0.6, "rgb"),
+                                                           (8, 8, 2, 0.8, "rgb"), (3, 2, 8, 0.0, "rgba"),
+                                                           (3, 2, 8, 0.5, "rgb")])
+def test_spans_weak_scaling(world, n_frames, band_h, rw, wire):
     """bench.py --partition spans: each rank traces one contiguous span of the
     batch's rows (whole frames, a run of bands at either end; rank 0's span
     rw times the others'), rank 0 in place in the batch's frames, and one
-    group of point-to-point receives lands every other span straight in them:
-    every frame and its radiance equal the oracle's, bit for bit."""
+    group of point-to-point receives lands every other span straight in them
+    (wire "rgb": the rows travel as RGB and rank 0 writes them into its RGBA8
+    frames, whose alpha bytes it set once): every frame and its radiance equal
+    the oracle's, bit for bit."""
     W, H = 48, 40
-    traced = _run_share(world, "spans", (band_h, rw), n_frames=n_frames, W=W, H=H, B=2)
+    traced = _run_share(world, "spans", (band_h, rw, wire), n_frames=n_frames, W=W, H=H, B=2)
     assert sum(traced.values()) == n_frames * W * H
     if 0 < rw < 1.0:
         assert traced[0] < min(traced[r] for r in range(1, world))
