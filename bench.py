@@ -398,8 +398,9 @@ def main() -> None:
     import rtamd
     from rtamd import configs
     from rtamd._lib import CameraUBO, Stats, check
+    from rtamd import dist as rdist
     from rtamd.dist import (SharePlan, ShareTracer, SpanPlan, SpanTracer, TilePlan, assemble_shares, band_list,
-                            gather_stack, gather_tiles, span_finish_recvs, span_post_recvs, span_send)
+                            gather_stack, gather_tiles)
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -723,7 +724,7 @@ def main() -> None:
             if os.environ.get("BENCH_EMULATE_NOX") != "1":
                 emu_land[:nr].copy_(src)               # the send's read of the rows
         else:
-            for w in span_send(rgba_slots[h], plan, rgb=rgb_slots[h] if wire_rgb else None,
+            for w in rdist.span_send(rgba_slots[h], plan, rgb=rgb_slots[h] if wire_rgb else None,
                                rad=rad_slots[h] if rad_on else None):
                 w.wait()                               # NCCL: main_stream waits for the send (host free)
         if timed:
@@ -746,7 +747,7 @@ def main() -> None:
                 for _, y0, nr in plan.recv_slices():   # the bytes the receives write
                     col[y0:y0 + nr].copy_(emu_buf[:nr])
         else:
-            works, landings = span_post_recvs(rgba_slots[h], plan, rgb=rgb_slots[h] if wire_rgb else None,
+            works, landings = rdist.span_post_recvs(rgba_slots[h], plan, rgb=rgb_slots[h] if wire_rgb else None,
                                               rad=rad_slots[h] if rad_on else None)
         span_recv[h] = (works, landings, k0 + G, e0)
 
@@ -754,7 +755,7 @@ def main() -> None:
         works, landings, k_end, e0 = span_recv[h]
         span_recv[h] = None
         # NCCL: main_stream waits (gloo: the host); the RGB rows into the frames
-        span_finish_recvs(works, landings, rgba_slots[h], plan, rgb=rgb_slots[h] if wire_rgb else None)
+        rdist.span_finish_recvs(works, landings, rgba_slots[h], plan, rgb=rgb_slots[h] if wire_rgb else None)
         if timed and e0 is not None:
             e1 = timing_event()
             e1.record(main_stream)
