@@ -231,4 +231,9 @@ hipError_t launch_trace(const TraceArgs& a, hipStream_t stream, int* kernels = n
 
 void set_error(const char* fmt, ...);
 
+// rt_wire.hip: the RGB wire format of the multi-GPU exchange (n_px pixels;
+// rgba 16-B aligned, rgb 4-B aligned).
+hipError_t wire_pack(const void* rgba, void* rgb, size_t n_px, hipStream_t s);
+hipError_t wire_unpack(const void* rgb, void* rgba, size_t n_px, hipStream_t s);
+
 }  // namespace rtamd

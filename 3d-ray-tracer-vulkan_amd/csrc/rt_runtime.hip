@@ -2086,6 +2086,34 @@ int rt_diag_copy(rt_ctx* ctx, void* dst, size_t cap_words, size_t* n_words) {
     return RT_OK;
 }
 
+static int wire_args(const void* a, const void* b, size_t n_px, const char* fn) {
+    if (n_px && (!a || !b)) {
+        set_error("%s: null buffer", fn);
+        return RT_ERR_INVALID_ARG;
+    }
+    return RT_OK;
+}
+
+int rt_pack_rgb(const void* d_rgba, void* d_rgb, size_t n_px, void* stream) {
+    if (int rc = wire_args(d_rgba, d_rgb, n_px, "rt_pack_rgb")) return rc;
+    if ((uintptr_t)d_rgba % 16 || (uintptr_t)d_rgb % 4) {
+        set_error("rt_pack_rgb: the RGBA8 buffer must be 16-B aligned and the RGB buffer 4-B aligned");
+        return RT_ERR_INVALID_ARG;
+    }
+    if (n_px) RT_HIP_CHECK(wire_pack(d_rgba, d_rgb, n_px, static_cast<hipStream_t>(stream)));
+    return RT_OK;
+}
+
+int rt_unpack_rgb(const void* d_rgb, void* d_rgba, size_t n_px, void* stream) {
+    if (int rc = wire_args(d_rgb, d_rgba, n_px, "rt_unpack_rgb")) return rc;
+    if ((uintptr_t)d_rgba % 16 || (uintptr_t)d_rgb % 4) {
+        set_error("rt_unpack_rgb: the RGBA8 buffer must be 16-B aligned and the RGB buffer 4-B aligned");
+        return RT_ERR_INVALID_ARG;
+    }
+    if (n_px) RT_HIP_CHECK(wire_unpack(d_rgb, d_rgba, n_px, static_cast<hipStream_t>(stream)));
+    return RT_OK;
+}
+
 int rt_accel_records(const void* vertices, size_t vertex_bytes, const void* materials, size_t material_bytes,
                      const void* bvh_nodes, size_t bvh_bytes, int n_layouts, uint32_t* out_words, size_t cap_words,
                      size_t* n_words, int32_t info[6]) {

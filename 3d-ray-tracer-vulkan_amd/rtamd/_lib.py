@@ -36,7 +36,7 @@ EXPORTED = (
     "rt_scene_validate", "rt_set_option", "rt_get_option", "rt_diag_copy",
     "rt_host_alloc", "rt_host_free", "rt_render_async", "rt_render_wait", "rt_upload_spheres",
     "rt_render_batch_device", "rt_band_list_rows", "rt_render_batch_lists_device", "rt_band_lists_rows",
-    "rt_render_poll", "rt_accel_records", "rt_abi_version",
+    "rt_render_poll", "rt_accel_records", "rt_abi_version", "rt_pack_rgb", "rt_unpack_rgb",
 )
 
 
@@ -136,6 +136,8 @@ def lib() -> C.CDLL:
                 "rt_accel_records": (i32, [vp, sz, vp, sz, vp, sz, i32, C.POINTER(C.c_uint32), sz, C.POINTER(sz),
                                            C.POINTER(C.c_int32)]),
                 "rt_abi_version": (i32, [C.POINTER(sz), C.POINTER(sz)]),
+                "rt_pack_rgb": (i32, [vp, vp, sz, vp]),
+                "rt_unpack_rgb": (i32, [vp, vp, sz, vp]),
             }
             for name, (res, args) in sig.items():
                 f = getattr(L, name)

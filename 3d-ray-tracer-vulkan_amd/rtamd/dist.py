@@ -606,6 +606,25 @@ def _staged(group, t) -> bool:
     return dist.get_backend(group) == "gloo" and t is not None and t.is_cuda
 
 
+def wire_copy(rgba, rgb, pack: bool) -> None:
+    """RGBA8 rows <-> RGB rows (the same [n, W, *] extent): on the device by
+    rt_pack_rgb / rt_unpack_rgb (4 pixels a thread), else (host tensors, or
+    rows not aligned for them) by a strided copy."""
+    import torch
+    n_px = rgba.shape[0] * rgba.shape[1]
+    if (rgba.is_cuda and rgba.is_contiguous() and rgb.is_contiguous() and rgba.data_ptr() % 16 == 0
+            and rgb.data_ptr() % 4 == 0):
+        s = torch.cuda.current_stream(rgba.device).cuda_stream
+        if pack:
+            check(lib().rt_pack_rgb(rgba.data_ptr(), rgb.data_ptr(), n_px, s))
+        else:
+            check(lib().rt_unpack_rgb(rgb.data_ptr(), rgba.data_ptr(), n_px, s))
+    elif pack:
+        rgb.copy_(rgba[:, :, :3])
+    else:
+        rgba[:, :, :3].copy_(rgb)
+
+
 def span_send(span, plan: SpanPlan, rgb=None, rad=None, group=None) -> list:
     """Rank r > 0's send of its span of a batch: span is its [>= rows[r], W, 4]
     RGBA8 span buffer.  rgb (a [>= rows[r], W, 3] buffer): the rows travel as
@@ -620,7 +639,7 @@ def span_send(span, plan: SpanPlan, rgb=None, rad=None, group=None) -> list:
         return []
     src = span[:n]
     if rgb is not None:
-        rgb[:n].copy_(src[:, :, :3])
+        wire_copy(src, rgb[:n], pack=True)
         src = rgb[:n]
     bufs = [src] + ([rad[:n]] if rad is not None else [])
     ops = [dist.P2POp(dist.isend, b.cpu() if _staged(group, b) else b, _glob(group)(0), group) for b in bufs]
@@ -660,7 +679,7 @@ def span_finish_recvs(works, landings, column, plan: SpanPlan, rgb=None) -> None
     if rgb is not None and sl:
         y = sl[0][1]                         # the received rows follow rank 0's span, to the column's end
         end = plan.n_frames * plan.height
-        column[y:end, :, :3].copy_(rgb[y:end])
+        wire_copy(column[y:end], rgb[y:end], pack=False)
 
 
 def exchange_spans(column, span, plan: SpanPlan, group=None, rgb=None) -> None:

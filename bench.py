@@ -719,7 +719,7 @@ def main() -> None:
         if emu:
             src = rgba_slots[h][orow:orow + nr]
             if wire_rgb:
-                rgb_slots[h][orow:orow + nr].copy_(src[:, :, :3])  # pack: the alpha byte stays home
+                rdist.wire_copy(src, rgb_slots[h][orow:orow + nr], pack=True)   # the alpha byte stays home
                 src = rgb_slots[h][orow:orow + nr]
             if os.environ.get("BENCH_EMULATE_NOX") != "1":
                 emu_land[:nr].copy_(src)               # the send's read of the rows

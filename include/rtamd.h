@@ -465,6 +465,15 @@ int rt_scene_validate(const void* vertices, size_t vertex_bytes,
  * primitives after dropping byte-identical duplicates, reference leaves, tree
  * depth}.  An analysis and test entry point (oracle/rt_accel_model.c walks
  * these records on the CPU); a host embedding the backend never needs it. */
+/* The multi-GPU wire format (rtamd/dist.py span_send / span_finish_recvs,
+ * DESIGN.md §6): a frame's alpha byte is always 255 (compute_dynamic_ray.comp:235),
+ * so rows cross the xGMI links as RGB.  rt_pack_rgb packs n_px RGBA8 pixels
+ * of d_rgba into 3-byte RGB at d_rgb; rt_unpack_rgb writes n_px RGB pixels
+ * back as RGBA8 with alpha 255.  Device pointers on the stream's device; d_rgba
+ * 16-B aligned, d_rgb 4-B aligned; enqueued on `stream`, no synchronisation. */
+int rt_pack_rgb(const void* d_rgba, void* d_rgb, size_t n_px, void* stream);
+int rt_unpack_rgb(const void* d_rgb, void* d_rgba, size_t n_px, void* stream);
+
 #define RT_ACCEL_FORMAT_HALF 0x100
 int rt_accel_records(const void* vertices, size_t vertex_bytes,
                      const void* materials, size_t material_bytes,

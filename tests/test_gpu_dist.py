@@ -248,3 +248,36 @@ def test_rccl_gather_frames_bit_exact(renderer, rccl_group, band_h, n_frames):
     one = DistRenderer(renderer, band_h=band_h).render(cam, W, H, B)
     torch.cuda.synchronize()
     assert torch.equal(one, full)
+
+
+@pytest.mark.parametrize("n_px", [1, 3, 4, 1920 * 7, 1920 * 7 + 3])
+def test_wire_rgb_round_trip(n_px):
+    """The RGB wire (rt_pack_rgb / rt_unpack_rgb, rtamd.dist.wire_copy): RGBA8
+    pixels packed to 3 bytes and written back with alpha 255 give the frame's
+    pixels back (their alpha is always 255), including the n % 4 tail; the
+    packed bytes are the RGB channels in order."""
+    import torch
+    from rtamd.dist import wire_copy
+    g = torch.Generator(device="cpu").manual_seed(n_px)
+    src = torch.randint(0, 256, (1, n_px, 4), dtype=torch.uint8, generator=g)
+    src[..., 3] = 255
+    d = src.to("cuda:0")
+    rgb = torch.full((1, n_px, 3), 7, dtype=torch.uint8, device="cuda:0")
+    wire_copy(d, rgb, pack=True)
+    back = torch.zeros((1, n_px, 4), dtype=torch.uint8, device="cuda:0")
+    wire_copy(back, rgb, pack=False)
+    torch.cuda.synchronize()
+    assert torch.equal(rgb.cpu(), src[..., :3])
+    assert torch.equal(back.cpu(), src)
+
+
+def test_wire_rgb_rejects_misaligned():
+    import ctypes as C
+    import torch
+    from rtamd import lib
+    from rtamd._lib import RtError, check
+    a = torch.zeros(64, dtype=torch.uint8, device="cuda:0")
+    with pytest.raises(RtError):
+        check(lib().rt_pack_rgb(a.data_ptr() + 4, a.data_ptr(), 4, None))
+    with pytest.raises(RtError):
+        check(lib().rt_unpack_rgb(a.data_ptr() + 1, a.data_ptr(), 4, None))
