@@ -347,10 +347,11 @@ def main() -> None:
     ap.add_argument("--ring", type=int, default=2,
                     help="N > 1: exchange batches of slots in the ring (>= 2); a batch's slots are retraced only "
                          "after the exchange ring - 1 batches back")
-    ap.add_argument("--wire", choices=("rgb", "rgba"), default="rgb",
-                    help="spans: the RGBA8 rows travel as RGB (the alpha byte is always 255, "
-                         "compute_dynamic_ray.comp:235), 3/4 of the bytes over each xGMI link; rank 0 writes "
-                         "them into its RGBA8 frames, whose alpha it set once")
+    ap.add_argument("--wire", choices=("rgb", "rgba"), default="rgba",
+                    help="spans: rgb = the RGBA8 rows travel as RGB (the alpha byte is always 255, "
+                         "compute_dynamic_ray.comp:235), 3/4 of the bytes over each xGMI link, packed and "
+                         "unpacked by rt_pack_rgb / rt_unpack_rgb (emulated 5%% slower at N = 8, profiles/r05/"
+                         "emulation/r5ap; it pays only where a link is the bound, DESIGN.md §6)")
     ap.add_argument("--gather", choices=("rgba", "radiance"), default="rgba",
                     help="N > 1: radiance = gather the float radiance beside the RGBA8 frame")
     ap.add_argument("--camera-path", choices=("static", "orbit"), default="static")
