@@ -9,8 +9,8 @@ Partitions of a frame over the N ranks:
   contiguous spans of whole bands, rank 0's root_weight times the others'; a
   rank traces its span one frame per launch (whole frames, a band run at either
   end) and rank 0 receives every other span straight into the batch's frames
-  (RCCL point-to-point, no assembly), the rows travelling as RGB (3/4 of the
-  bytes; the alpha byte is always 255);
+  (RCCL point-to-point, no assembly); optionally the rows travel as RGB (3/4
+  of the bytes; the alpha byte is always 255; wire_copy);
 * weighted interleaved row bands (round 4's default; band_owners,
   SharePlan, gather_shares): the band_h-row bands are dealt out by a smooth
   weighted round robin, rank 0 with weight root_weight (it also receives and
