@@ -139,16 +139,23 @@ def default_inflight(world: int) -> int:
     return 4
 
 
-def default_batch(world: int, weak: bool = False) -> int:
-    """Frames per launch.  N = 1: 1.  N > 1, weak scaling: N (a launch is a
-    step, this rank's share of the step's N frames: one frame of work, the
-    shape of an N = 1 launch).  N > 1, strong scaling: N / 2 (about half a
-    frame of work per launch): a rank's 1/8 share of one frame is too small
-    a launch to run past its own tail (rank emulation at N = 8, 200 steps:
-    profiles/r03/evidence_r3c/emu.jsonl, 3.9x with 1 frame per launch against
-    6.3-7.7x with 4).  At most 16."""
+def default_batch(world: int, weak: bool = False, steps: int = 0) -> int:
+    """Frames per launch.  N = 1: 2 when the timed frames are whole pairs
+    (steps even, or steps not given), else 1: a launch of two frames runs
+    past the other launches' tails with one learned order for both
+    (A/B on one box, 2 runs each: config 3 0.1190-0.1200 ms per frame
+    against 0.1214-0.1222 with 1, config 5 1.156-1.164 against 1.174,
+    config 6 0.1223-0.1239 against 0.1234-0.1239; profiles/r05/r5ar,
+    profiles/r05/r5as); an odd frame count would end on a 1-frame launch
+    of a new launch key.  N > 1, weak scaling: N (a launch is a step, this
+    rank's share of the step's N frames: one frame of work, the shape of an
+    N = 1 launch).  N > 1, strong scaling: N / 2 (about half a frame of work
+    per launch): a rank's 1/8 share of one frame is too small a launch to
+    run past its own tail (rank emulation at N = 8, 200 steps:
+    profiles/r03/evidence_r3c/emu.jsonl, 3.9x with 1 frame per launch
+    against 6.3-7.7x with 4).  At most 16."""
     if world == 1:
-        return 1
+        return 1 if steps % 2 else 2
     return max(1, min(16, world if weak else world // 2))
 
 
@@ -473,7 +480,7 @@ def main() -> None:
     weak = dist_on and args.scaling == "weak"
     step_frames = world if weak else 1                         # frames per step (weak scaling: N)
     D = args.inflight if args.inflight > 0 else default_inflight(world)
-    F = (args.batch if args.batch > 0 else default_batch(world, weak)) \
+    F = (args.batch if args.batch > 0 else default_batch(world, weak, args.steps)) \
         if mode in ("whole", "bands", "pieces", "spans") else 1
     F = min(F, 16)
     if mode in ("bands", "pieces", "spans"):
@@ -1116,8 +1123,8 @@ def main() -> None:
     n_cu = torch.cuda.get_device_properties(dev).multi_processor_count
     # PMC only from a record of this config and camera path (pmc_key)
     pmc = load_pmc(args.pmc_json, pmc_key(cfg.name, args.camera_path, renderer.get_option("accel_used"),
-                                         renderer.get_option("accel_half_used"))) \
-        if (mode == "whole" and F == 1) else None
+                                         renderer.get_option("accel_half_used"), F)) \
+        if mode == "whole" else None
     walk_mb = round(renderer.walk_bytes() / 2**20, 2)
     roof = roofline(pmc, alg_bytes, ref_layout_bytes, l_seg, launch_ms, frame_ms, n_cu, lanes, walk_mb)
 
@@ -1309,13 +1316,15 @@ def lane_utilisation(renderer, L, ctx, launch, dev):
                     "coop_windows = 64-node windows of the cooperative tail"}
 
 
-def pmc_key(config_name: str, camera_path: str, accel: int = 0, half: int = 0) -> str:
+def pmc_key(config_name: str, camera_path: str, accel: int = 0, half: int = 0, frames: int = 1) -> str:
     """The key of a PMC record in profiles/pmc_latest.json: the config, the
-    camera path unless it is the static default camera, and the accel layouts
+    camera path unless it is the static default camera, the accel layouts
     unless the scene runs the reference's own tree (accel 0; round 4's
-    records), with "h" for option accel_half's records."""
+    records), with "h" for option accel_half's records, and "@f<F>" for
+    launches of F > 1 frames (a record is per launch)."""
     k = config_name if camera_path == "static" else f"{config_name}@{camera_path}"
-    return f"{k}@accel{accel}{'h' if half else ''}" if accel else k
+    k = f"{k}@accel{accel}{'h' if half else ''}" if accel else k
+    return f"{k}@f{frames}" if frames > 1 else k
 
 
 def load_pmc(path, config_name):

@@ -99,7 +99,8 @@ def test_rocprof_union_agrees_with_ms_per_step(cfg):
 
 def test_default_schedule_helpers():
     assert bench.default_inflight(1) == 4
-    assert bench.default_batch(1) == 1
+    assert bench.default_batch(1) == 2 and bench.default_batch(1, steps=20) == 2
+    assert bench.default_batch(1, steps=5) == 1       # an odd frame count: no 1-frame launch of a new key
     for n in (2, 4, 8):
         assert bench.default_batch(n, weak=True) == n
         assert 0.5 < bench.default_root_weight(n) < 1.0
@@ -259,7 +260,8 @@ def test_r05_rocprof_union(session, cfg):
     u = json.load(open(os.path.join(R05, session, f"union_cfg{cfg}.json")))
     with open(os.path.join(R05, session, f"prof{cfg}.json")) as fh:
         p = json.loads([x for x in fh if x.startswith("{")][-1])
-    assert u["launches"] == u["frames"] == p["steps"]
+    assert u["launches"] * u.get("frames_per_launch", 1) == u["frames"] == p["steps"]
+    assert u.get("frames_per_launch", 1) == p["config"]["frames_per_launch"]
     assert u["union_ms_per_frame"] == pytest.approx(p["ms_per_step"], rel=0.06)
     with open(os.path.join(R05, session, f"kernel_stats_cfg{cfg}.csv")) as fh:
         rows = [r for r in csv.DictReader(fh) if "trace_simple<false, false" in r["Name"]]

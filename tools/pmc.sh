@@ -12,7 +12,7 @@ pass() {  # pass NAME COUNTERS...
   local name=$1; shift
   echo "$(date +%T) pass $name: $*" >> "$OUT/status.txt"
   timeout -k 10 300 rocprofv3 --pmc "$@" --kernel-include-regex "trace_(simple|persistent|coop)" --output-format csv \
-      -d "$OUT/$name" -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-pcie ${BENCH_ARGS:-} > "$OUT/$name.log" 2>&1
+      -d "$OUT/$name" -o run -- python3 bench.py --steps 4 --warmup 2 --no-cpu-baseline --no-pcie --no-lanes ${BENCH_ARGS:-} > "$OUT/$name.log" 2>&1
   local rc=$?
   echo "$(date +%T) pass $name rc=$rc" >> "$OUT/status.txt"
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi

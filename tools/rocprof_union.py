@@ -54,7 +54,15 @@ def main():
     # plain launches: trace_simple<false, false, ...>
     rows = [r for r in csv.DictReader(open(args.trace)) if "trace_simple<false, false" in r["Kernel_Name"]]
     rows.sort(key=lambda r: int(r["Dispatch_Id"]))
-    n = args.steps * args.launches_per_step
+    # launches of several frames (bench.py --batch; the N = 1 default is 2):
+    # the bench line's config.frames_per_launch
+    fpl = 1
+    if args.bench:
+        line = [x for x in open(args.bench) if x.startswith("{")][-1]
+        fpl = int(json.loads(line).get("config", {}).get("frames_per_launch") or 1)
+    if args.steps % fpl:
+        raise SystemExit(f"{args.steps} frames are not whole launches of {fpl}")
+    n = args.steps // fpl * args.launches_per_step
     if len(rows) < n:
         raise SystemExit(f"{len(rows)} plain trace launches in the trace, need {n}")
     skip = args.skip_last
@@ -80,6 +88,7 @@ def main():
         "mean_ms_by_kernel": by_kernel,
         "frames": args.steps,
         "launches": n,
+        "frames_per_launch": fpl,
         "union_ms": round(union, 4),
         "span_ms": round(span, 4),
         "union_ms_per_frame": round(union / args.steps, 4),
