@@ -97,6 +97,12 @@ def main():
         "launch_ms_min": round(min(durs), 4),
         "launch_ms_max": round(max(durs), 4),
         "launches_in_flight_mean": round(sum(durs) / union, 3),
+        # every launch of the production kernel in the trace (settle, warmup,
+        # timed, and the 1-frame verification / diagnostic launches after the
+        # timed region): what rocprofv3 --stats averages in kernel_stats.csv
+        "all_launches": len(rows),
+        "all_launch_ms_mean": round(statistics.mean((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6
+                                                    for r in rows), 4),
     }
     if args.bench:
         line = next(ln for ln in open(args.bench) if ln.lstrip().startswith("{"))
