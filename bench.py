@@ -6,8 +6,8 @@ Workload (N = 1): BASELINE config 3 — the 50k-triangle synthetic scene at
 frame traced on the GPU: every pixel's full path, RGBA8 written to HBM.  The
 render loop keeps D launches in flight (launch j on stream j mod D, each
 stream its own hardware queue), as a renderer does to hide each frame's
-serial tail; a launch traces F frames (rt_render_batch_device; F = 1 at
-N = 1).  The timed region covers exactly K frames, synchronised on both
+serial tail; a launch traces F frames (rt_render_batch_device; F = 2 at
+N = 1 when the timed frames are whole pairs, default_batch).  The timed region covers exactly K frames, synchronised on both
 sides.
 
 With N > 1 ranks (one process per GPU, torch.distributed over RCCL), every
