@@ -1,9 +1,10 @@
 """GPU: the frames a pipelined caller gets (bench.py's timed loop, HipEngine's
 frames in flight) and the runtime's synchronisation around them.
 
-* bench.py's N = 1 trace() shape: rt_render_batch_device, one whole frame and
-  no band list per launch, 4 launches at once on 4 streams (ShareTracer, the
-  class bench.py launches through), config 3: every frame equals the oracle's.
+* bench.py's N = 1 trace() shape: rt_render_batch_device, one or two whole
+  frames (the N = 1 default) and no band list per launch, 4 launches at once
+  on 4 streams (ShareTracer, the class bench.py launches through), config 3:
+  every frame equals the oracle's.
 * A scene swap between rt_render_async submits, as HipEngine.java does with
   4 frames in flight (VulkanEngine.internalSwapScene drains the device first,
   VulkanEngine.java:321): every frame equals the oracle frame of the scene it
@@ -38,13 +39,14 @@ def _orbit(cfg, k):
                           cfg.width / cfg.height)
 
 
-@pytest.mark.parametrize("accel", [0, 8])
+@pytest.mark.parametrize("accel,F", [(0, 1), (8, 1), (8, 2)])
 @pytest.mark.parametrize("camera", ["static", "orbit"])
-def test_bench_trace_shape_frames(renderer, camera, accel):
+def test_bench_trace_shape_frames(renderer, camera, accel, F):
     """Config 3 through bench.py's N = 1 launches: D = 4 launches in flight on
-    4 streams (concurrent_launches 4), each one whole frame into its slot,
-    three rounds (the learning launch, then the learned order with heavy
-    pixels).  Every frame of every round equals the oracle's."""
+    4 streams (concurrent_launches 4), each F whole frames into its slot
+    (F = 2: bench.default_batch at N = 1), three rounds (the learning launch,
+    then the learned order with heavy pixels).  Every frame of every round
+    equals the oracle's."""
     import torch
     from rtamd import configs
     from rtamd._lib import CameraUBO
@@ -57,27 +59,29 @@ def test_bench_trace_shape_frames(renderer, camera, accel):
         renderer.set_option("accel", accel)       # accel 8: the default walk
         renderer.upload_scene(built)
         renderer.set_option("concurrent_launches", D)
-        cams = [cfg.camera() if camera == "static" else _orbit(cfg, k) for k in range(D)]
+        cams = [cfg.camera() if camera == "static" else _orbit(cfg, k) for k in range(D * F)]
         refs = {}
-        for k in range(D if camera == "orbit" else 1):
+        for k in range(D * F if camera == "orbit" else 1):
             refs[k] = _oracle(built, cams[k].ubo_bytes(), W, H, B, radiance=False)[0]
         tracer = ShareTracer(renderer._ctx, W, H, B, "whole")
-        slots = torch.zeros((D, H, W, 4), dtype=torch.uint8, device="cuda:0")
+        slots = torch.zeros((D, F * H, W, 4), dtype=torch.uint8, device="cuda:0")
         streams = [torch.cuda.Stream() for _ in range(D)]
-        ubos = [(CameraUBO * 1)(c.ubo) for c in cams]
+        ubos = [(CameraUBO * F)(*[c.ubo for c in cams[j * F:(j + 1) * F]]) for j in range(D)]
         for rnd in range(3):
             torch.cuda.synchronize()
             slots.zero_()
             torch.cuda.synchronize()
             for j in range(D):
-                tracer.launch(ubos[j], j, 1, streams[j].cuda_stream, slots[j].data_ptr(), None)
+                tracer.launch(ubos[j], j * F, F, streams[j].cuda_stream, slots[j].data_ptr(), None)
             torch.cuda.synchronize()
             got = slots.cpu().numpy()
             for j in range(D):
-                ref = refs[j if camera == "orbit" else 0]
-                if not np.array_equal(got[j], ref):
-                    n = int(np.any(got[j] != ref, axis=-1).sum())
-                    raise AssertionError(f"round {rnd}, stream {j}: {n} pixels differ")
+                for f in range(F):
+                    ref = refs[j * F + f if camera == "orbit" else 0]
+                    fr = got[j][f * H:(f + 1) * H]
+                    if not np.array_equal(fr, ref):
+                        n = int(np.any(fr != ref, axis=-1).sum())
+                        raise AssertionError(f"round {rnd}, stream {j}, frame {f}: {n} pixels differ")
         assert renderer.get_option("heavy_pixels_used") > 0 or camera == "orbit" or accel
     finally:
         renderer.set_option("concurrent_launches", 1)
