@@ -401,6 +401,19 @@ __device__ __forceinline__ float4 wbuf(__amdgpu_buffer_rsrc_t r, int slot, int o
     return make_float4(__uint_as_float(v[0]), __uint_as_float(v[1]), __uint_as_float(v[2]), __uint_as_float(v[3]));
 }
 #endif
+#ifndef RT_ACC_SCALAR
+// 1 = a walk step whose walking lanes all go to one slot loads it through the
+// scalar cache (one s_load per 16 B, no vector-memory issue); A/B builds
+#define RT_ACC_SCALAR 0
+#endif
+// 16-B piece k of the walk records through the scalar cache: k must be
+// wave-uniform (readfirstlane), the records read-only for the kernel's life.
+__device__ __forceinline__ float4 sbuf(const float4* base, int k) {
+    typedef float v4f __attribute__((ext_vector_type(4)));
+    typedef __attribute__((address_space(4))) const v4f cv4f;
+    const v4f v = reinterpret_cast<cv4f*>(reinterpret_cast<uintptr_t>(base))[k];
+    return make_float4(v[0], v[1], v[2], v[3]);
+}
 // A half-format accel record's 16-B slot (accel_build.h format 1).
 __device__ __forceinline__ float4 hbuf(__amdgpu_buffer_rsrc_t r, int slot) {
     const auto v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)((unsigned)slot << 4), 0, 0);
@@ -1132,7 +1145,18 @@ void trace_simple(TraceArgs a) {
                     const bool nl = (((hb && !nleaf) ? bw : (aw >> 31)) & 1u) != 0u;
                     const float v0x = B.w;                                   // a leaf's v0.x
                     if (COUNT && hb && !nleaf) c_node += 2;
-#if RT_CHAIN >= 2
+#if RT_ACC_SCALAR
+                    // one slot for every walking lane: the scalar cache
+                    const int nf = __builtin_amdgcn_readfirstlane(nxt);
+                    const bool uni = ACC && !PAD && __ballot(nxt != nf) == 0;
+                    if (uni) {
+                        A = sbuf(wr, 2 * nf);
+                        B = sbuf(wr, 2 * nf + 1);
+                    } else {
+                        A = wbuf(wrs, nxt, 0);                               // slot end is padding
+                        B = wbuf(wrs, nxt, 16);
+                    }
+#elif RT_CHAIN >= 2
                     A = wbuf(wrs, nxt, 0);                                   // slot end is padding
                     B = wbuf(wrs, nxt, 16);
 #elif RT_CHAIN == 1
@@ -1164,7 +1188,15 @@ void trace_simple(TraceArgs a) {
                         }
                     }
                     if (nl && nxt < (ACC ? lend : wend) && !(ACC && RT_ACC_LAZY)) {
-#if RT_CHAIN >= 2
+#if RT_ACC_SCALAR
+                        if (uni) {
+                            Q0 = sbuf(wr, 2 * nf + 2);
+                            Q1 = sbuf(wr, 2 * nf + 3);
+                        } else {
+                            Q0 = wbuf(wrs, nxt, 32);
+                            Q1 = wbuf(wrs, nxt, 48);
+                        }
+#elif RT_CHAIN >= 2
                         Q0 = wbuf(wrs, nxt, 32);
                         Q1 = wbuf(wrs, nxt, 48);
 #else
