@@ -568,6 +568,16 @@ class SpanPlan:
         """(rank, row0, rows) of every span rank 0 receives."""
         return [(r, self.row0[r], self.rows[r]) for r in range(1, self.world) if self.rows[r] > 0]
 
+    def pieces(self, rank: int):
+        """(out_row, rows) of each launch of rank's span, in launch order: the
+        pieces a span travels in when it is sent launch by launch."""
+        return [(orow, (hi - lo) * self.band_h) for (_, lo, hi, orow) in self.launches[rank]]
+
+    def recv_pieces(self):
+        """(rank, row0, rows) of every launch's piece rank 0 receives, per rank
+        in launch order (the order the pieces are sent in)."""
+        return [(r, self.row0[r] + orow, n) for r in range(1, self.world) for orow, n in self.pieces(r) if n > 0]
+
 
 class SpanTracer:
     """The launches of one rank's span of a batch (bench.py's trace for
@@ -625,38 +635,42 @@ def wire_copy(rgba, rgb, pack: bool) -> None:
         rgba[:, :, :3].copy_(rgb)
 
 
-def span_send(span, plan: SpanPlan, rgb=None, rad=None, group=None) -> list:
+def span_send(span, plan: SpanPlan, rgb=None, rad=None, group=None, rows=None) -> list:
     """Rank r > 0's send of its span of a batch: span is its [>= rows[r], W, 4]
     RGBA8 span buffer.  rgb (a [>= rows[r], W, 3] buffer): the rows travel as
     RGB, packed here (the alpha byte is always 255, compute_dynamic_ray.comp:235),
     3/4 of the bytes over the link.  rad: the span's float radiance, sent after.
-    One batch_isend_irecv (one RCCL group); returns its works (wait() orders the
-    current stream after the send)."""
+    rows = (out_row, n): one launch's piece of the span only (plan.pieces; rank
+    0 then posts span_post_recvs(..., pieces=True)).  One batch_isend_irecv
+    (one RCCL group); returns its works (wait() orders the current stream after
+    the send)."""
     import torch.distributed as dist
     rank = dist.get_rank(group)
-    n = plan.rows[rank]
+    y, n = rows if rows is not None else (0, plan.rows[rank])
     if n == 0:
         return []
-    src = span[:n]
+    src = span[y:y + n]
     if rgb is not None:
-        wire_copy(src, rgb[:n], pack=True)
-        src = rgb[:n]
-    bufs = [src] + ([rad[:n]] if rad is not None else [])
+        wire_copy(src, rgb[y:y + n], pack=True)
+        src = rgb[y:y + n]
+    bufs = [src] + ([rad[y:y + n]] if rad is not None else [])
     ops = [dist.P2POp(dist.isend, b.cpu() if _staged(group, b) else b, _glob(group)(0), group) for b in bufs]
     return dist.batch_isend_irecv(ops)
 
 
-def span_post_recvs(column, plan: SpanPlan, rgb=None, rad=None, group=None):
+def span_post_recvs(column, plan: SpanPlan, rgb=None, rad=None, group=None, pieces=False):
     """Rank 0's receives of every other span of a batch, posted at once:
     column is the batch's [n_frames * height, W, 4] RGBA8 frames (rank 0's
     own span traced in place), rgb (with the RGB wire) a [n_frames * height, W,
-    3] landing the RGB rows arrive in, rad the batch's float radiance.  Returns
-    (works, landings) for span_finish_recvs."""
+    3] landing the RGB rows arrive in, rad the batch's float radiance.
+    pieces: one receive per launch of each span (the senders send launch by
+    launch: span_send(rows=...)).  Returns (works, landings) for
+    span_finish_recvs."""
     import torch
     import torch.distributed as dist
     glob = _glob(group)
     ops, landings = [], []
-    for r, y0, n in plan.recv_slices():
+    for r, y0, n in (plan.recv_pieces() if pieces else plan.recv_slices()):
         for buf in ((rgb if rgb is not None else column),) + ((rad,) if rad is not None else ()):
             dst = buf[y0:y0 + n]
             if _staged(group, dst):
@@ -682,20 +696,23 @@ def span_finish_recvs(works, landings, column, plan: SpanPlan, rgb=None) -> None
         wire_copy(column[y:end], rgb[y:end], pack=False)
 
 
-def exchange_spans(column, span, plan: SpanPlan, group=None, rgb=None) -> None:
+def exchange_spans(column, span, plan: SpanPlan, group=None, rgb=None, pieces=False) -> None:
     """One batch of the spans partition, both halves at once.  Rank 0: column
     is the batch's [n_frames * height, W, C] frames, its own span traced in
     place; every other span is received straight into its rows.  Rank r > 0:
     span is its [>= rows[r], W, C] span buffer, sent to rank 0.  rgb: the RGB
-    wire (C = 4; span_send / span_post_recvs).  On return the current stream is
-    ordered after the exchange."""
+    wire (C = 4; span_send / span_post_recvs).  pieces: the spans travel launch
+    by launch (bench.py's last batch of a phase).  On return the current
+    stream is ordered after the exchange."""
     import torch.distributed as dist
-    if dist.get_rank(group) == 0:
-        works, landings = span_post_recvs(column, plan, rgb=rgb, group=group)
+    rank = dist.get_rank(group)
+    if rank == 0:
+        works, landings = span_post_recvs(column, plan, rgb=rgb, group=group, pieces=pieces)
         span_finish_recvs(works, landings, column, plan, rgb=rgb)
     else:
-        for w in span_send(span, plan, rgb=rgb, group=group):
-            w.wait()
+        for rows in (plan.pieces(rank) if pieces else [None]):
+            for w in span_send(span, plan, rgb=rgb, group=group, rows=rows):
+                w.wait()
 
 
 # --- rotating row blocks (strong scaling, an option) -------------------------

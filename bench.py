@@ -359,6 +359,10 @@ def main() -> None:
                          "compute_dynamic_ray.comp:235), 3/4 of the bytes over each xGMI link, packed and "
                          "unpacked by rt_pack_rgb / rt_unpack_rgb (emulated 5%% slower at N = 8, profiles/r05/"
                          "emulation/r5ap; it pays only where a link is the bound, DESIGN.md §6)")
+    ap.add_argument("--last-pieces", choices=("on", "off"), default="on",
+                    help="spans: the last exchange batch of a phase travels launch by launch (each "
+                         "launch's rows sent as it ends), so only the last launch's transfer is left "
+                         "after the traces (DESIGN.md §6)")
     ap.add_argument("--gather", choices=("rgba", "radiance"), default="rgba",
                     help="N > 1: radiance = gather the float radiance beside the RGBA8 frame")
     ap.add_argument("--camera-path", choices=("static", "orbit"), default="static")
@@ -717,24 +721,30 @@ def main() -> None:
     send_q = []                # r > 0: (launch end events, slot, out_row, rows) of traced batches not yet sent
 
     def span_send(timed):
-        e_ends, h, orow, nr = send_q.pop(0)
-        for e_end in e_ends:
-            e_end.synchronize()                        # host: the batch's launches have ended
+        e_ends, h, orow, nr, pieces = send_q.pop(0)
+        if pieces is None:
+            for e_end in e_ends:
+                e_end.synchronize()                    # host: the batch's launches have ended
+            pieces = [(None, orow, nr)]
         e0 = e1 = None
         if timed:
             e0, e1 = timing_event(), timing_event()
             e0.record(main_stream)
-        if emu:
-            src = rgba_slots[h][orow:orow + nr]
-            if wire_rgb:
-                rdist.wire_copy(src, rgb_slots[h][orow:orow + nr], pack=True)   # the alpha byte stays home
-                src = rgb_slots[h][orow:orow + nr]
-            if os.environ.get("BENCH_EMULATE_NOX") != "1":
-                emu_land[:nr].copy_(src)               # the send's read of the rows
-        else:
-            for w in rdist.span_send(rgba_slots[h], plan, rgb=rgb_slots[h] if wire_rgb else None,
-                               rad=rad_slots[h] if rad_on else None):
-                w.wait()                               # NCCL: main_stream waits for the send (host free)
+        for e_end, y, n in pieces:                     # the last batch of a phase: launch by launch
+            if e_end is not None:
+                e_end.synchronize()                    # host: this launch has ended
+            if emu:
+                src = rgba_slots[h][y:y + n]
+                if wire_rgb:
+                    rdist.wire_copy(src, rgb_slots[h][y:y + n], pack=True)   # the alpha byte stays home
+                    src = rgb_slots[h][y:y + n]
+                if os.environ.get("BENCH_EMULATE_NOX") != "1":
+                    emu_land[:n].copy_(src)            # the send's read of the rows
+            else:
+                rows = (y, n) if e_end is not None else None
+                for w in rdist.span_send(rgba_slots[h], plan, rgb=rgb_slots[h] if wire_rgb else None,
+                                         rad=rad_slots[h] if rad_on else None, rows=rows):
+                    w.wait()                           # NCCL: main_stream waits for the send (host free)
         if timed:
             e1.record(main_stream)
             ex_evs.append((e0, e1))
@@ -742,8 +752,9 @@ def main() -> None:
         ev.record(main_stream)
         span_sent[h] = ev
 
-    def span_post_recvs(k0, h, timed):
-        """Rank 0: batch k0's receives of every other span, into slot h's frames."""
+    def span_post_recvs(k0, h, timed, pieces=False):
+        """Rank 0: batch k0's receives of every other span, into slot h's
+        frames (pieces: one receive per launch of each span)."""
         e0 = None
         if timed:
             e0 = timing_event()
@@ -756,7 +767,7 @@ def main() -> None:
                     col[y0:y0 + nr].copy_(emu_buf[:nr])
         else:
             works, landings = rdist.span_post_recvs(rgba_slots[h], plan, rgb=rgb_slots[h] if wire_rgb else None,
-                                              rad=rad_slots[h] if rad_on else None)
+                                                    rad=rad_slots[h] if rad_on else None, pieces=pieces)
         span_recv[h] = (works, landings, k0 + G, e0)
 
     def span_complete_recvs(h, timed):
@@ -786,18 +797,22 @@ def main() -> None:
         while st["k"] < end:
             k0 = st["k"]
             h = (k0 // G) % R
+            # the phase's last batch: its exchange is the one no later trace
+            # overlaps, so its spans travel launch by launch (--last-pieces)
+            pieces = args.last_pieces == "on" and k0 + G >= end
             if rank == 0:
                 if span_recv[h] is not None:           # the slot's last batch: its receives complete
                     span_complete_recvs(h, timed)
                 if gathered[h] is not None:
                     gathered[h].synchronize()
-                span_post_recvs(k0, h, timed)
+                span_post_recvs(k0, h, timed, pieces)
             else:
                 while any(q[1] == h for q in send_q):  # the slot's last batch: every launch sent
                     span_send(timed)
                 if span_sent[h] is not None:
                     span_sent[h].synchronize()
             used = []
+            piece_q = [] if (pieces and rank) else None
             for jl in range(len(tracer.launches)):
                 j = st["j"]
                 s = streams[j % D]
@@ -809,6 +824,12 @@ def main() -> None:
                 if timed:
                     e[1].record(s)
                     evs.append((e, 1))
+                if piece_q is not None:
+                    ev = torch.cuda.Event()
+                    ev.record(s)
+                    orow, n = plan.pieces(rank)[jl]
+                    if n:
+                        piece_q.append((ev, orow, n))
                 if s not in used:
                     used.append(s)
                 st["j"] = j + 1
@@ -819,7 +840,7 @@ def main() -> None:
                     ev = torch.cuda.Event()
                     ev.record(s)
                     ends.append(ev)
-                send_q.append((ends, h, 0, plan.rows[rank]))
+                send_q.append((ends, h, 0, plan.rows[rank], piece_q))
                 while len(send_q) > 1:                 # the batch before: sent once its launches end
                     span_send(timed)
         # the phase's exchanges complete before it ends

@@ -275,7 +275,7 @@ def _share_worker(rank, world, port, q, kind, arg, n_frames, W, H, B):
             # bench.py --partition spans: rank 0 traces its span in place in
             # the batch's frames, the others into a span buffer; one group of
             # point-to-point receives lands every span in rank 0's frames
-            band_h, rw, wire = arg
+            band_h, rw, wire, pieces = arg
             plan = SpanPlan(H, band_h, world, n_frames, rw)
             col = torch.zeros((n_frames * H, W, 4), dtype=torch.uint8) if rank == 0 else None
             rgb = None
@@ -296,8 +296,8 @@ def _share_worker(rank, world, port, q, kind, arg, n_frames, W, H, B):
                 (col if rank == 0 else span)[o:o + n] = torch.from_numpy(a)
                 (colr if rank == 0 else spanr)[o:o + n] = torch.from_numpy(r)
                 traced += W * n
-            exchange_spans(col, span, plan, rgb=rgb)
-            exchange_spans(colr, spanr, plan)
+            exchange_spans(col, span, plan, rgb=rgb, pieces=pieces)
+            exchange_spans(colr, spanr, plan, pieces=pieces)
             out = col.view(n_frames, H, W, 4) if rank == 0 else None
             outr = colr.view(n_frames, H, W, 3) if rank == 0 else None
         elif kind == "tiles":
@@ -485,19 +485,24 @@ def test_share_tracer_rejects_uneven_lists():
     assert tt.rect == (960, 540, 960, 540)
 
 
-@pytest.mark.parametrize("world,n_frames,band_h,rw,wire", [(2, 3, 4, 1.0, "rgba"), (4, 4, 4, 0.6, "rgb"),
-                                                           (8, 8, 2, 0.8, "rgb"), (3, 2, 8, 0.0, "rgba"),
-                                                           (3, 2, 8, 0.5, "rgb")])
-def test_spans_weak_scaling(world, n_frames, band_h, rw, wire):
+@pytest.mark.parametrize("world,n_frames,band_h,rw,wire,pieces", [(2, 3, 4, 1.0, "rgba", False),
+                                                                  (4, 4, 4, 0.6, "rgb", False),
+                                                                  (8, 8, 2, 0.8, "rgb", False),
+                                                                  (3, 2, 8, 0.0, "rgba", False),
+                                                                  (3, 2, 8, 0.5, "rgb", False),
+                                                                  (4, 4, 4, 0.6, "rgb", True),
+                                                                  (3, 3, 4, 0.8, "rgba", True)])
+def test_spans_weak_scaling(world, n_frames, band_h, rw, wire, pieces):
     """bench.py --partition spans: each rank traces one contiguous span of the
     batch's rows (whole frames, a run of bands at either end; rank 0's span
     rw times the others'), rank 0 in place in the batch's frames, and one
     group of point-to-point receives lands every other span straight in them
     (wire "rgb": the rows travel as RGB and rank 0 writes them into its RGBA8
-    frames, whose alpha bytes it set once): every frame and its radiance equal
-    the oracle's, bit for bit."""
+    frames, whose alpha bytes it set once; pieces: the spans travel launch by
+    launch, one receive per piece, as bench.py's last batch of a phase): every
+    frame and its radiance equal the oracle's, bit for bit."""
     W, H = 48, 40
-    traced = _run_share(world, "spans", (band_h, rw, wire), n_frames=n_frames, W=W, H=H, B=2)
+    traced = _run_share(world, "spans", (band_h, rw, wire, pieces), n_frames=n_frames, W=W, H=H, B=2)
     assert sum(traced.values()) == n_frames * W * H
     if 0 < rw < 1.0:
         assert traced[0] < min(traced[r] for r in range(1, world))
@@ -527,5 +532,11 @@ def test_span_plan_1080p():
         t = SpanTracer(None, 1920, 1080, 4, plan, r)
         assert sum(1 for b in t._lists if b is None) >= 2             # mostly whole frames
     assert plan.recv_slices() == [(r, plan.row0[r], plan.rows[r]) for r in range(1, 8)]
+    # the pieces (one per launch) tile each span in order
+    for r in range(1, 8):
+        ps = [(y, n) for rr, y, n in plan.recv_pieces() if rr == r]
+        assert ps[0][0] == plan.row0[r] and sum(n for _, n in ps) == plan.rows[r]
+        assert all(ps[i][0] + ps[i][1] == ps[i + 1][0] for i in range(len(ps) - 1))
+        assert [(plan.row0[r] + o, n) for o, n in plan.pieces(r)] == ps
     with pytest.raises(ValueError, match="divide the height"):
         SpanPlan(1080, 16, 8, 32, 0.8)
