@@ -535,18 +535,29 @@ class SpanPlan:
     frame when (band_lo, band_hi) == (0, height / band_h), written at row
     out_row of the rank's span buffer (rank 0: the batch column from row0[0])."""
 
-    def __init__(self, height: int, band_h: int, world: int, n_frames: int, root_weight: float = 1.0):
+    def __init__(self, height: int, band_h: int, world: int, n_frames: int, root_weight: float = 1.0,
+                 whole_frames: bool = False, batch: int = 0):
         if height % band_h:
             raise ValueError(f"spans: band_h ({band_h}) must divide the height ({height})")
         if not root_weight >= 0:
             raise ValueError("spans: root_weight must be >= 0")
         self.height, self.band_h, self.world, self.n_frames = height, band_h, world, n_frames
         self.root_weight = root_weight
+        self.whole_frames = whole_frames
         self.bpf = height // band_h
         total = n_frames * self.bpf
-        w = np.array([root_weight] + [1.0] * (world - 1))
-        cum = np.concatenate([[0.0], np.cumsum(w)])
-        self.cuts = [int(round(total * c / cum[-1])) for c in cum]
+        if whole_frames:
+            # cut at frame boundaries: every launch a whole frame (a band run
+            # at a span's ends is a smaller launch that runs past its tail
+            # less well); rank 0 its weighted share of frames rounded, the
+            # other ranks the rest, the remainder's extra frames rotating over
+            # them from batch to batch (batch: the batch's index)
+            c = self.frame_counts(batch)
+            self.cuts = [int(x) * self.bpf for x in np.concatenate([[0], np.cumsum(c)])]
+        else:
+            w = np.array([root_weight] + [1.0] * (world - 1))
+            cum = np.concatenate([[0.0], np.cumsum(w)])
+            self.cuts = [int(round(total * c / cum[-1])) for c in cum]
         self.cuts[-1] = total
         self.row0 = [c * band_h for c in self.cuts[:-1]]
         self.rows = [(self.cuts[r + 1] - self.cuts[r]) * band_h for r in range(world)]
@@ -563,6 +574,35 @@ class SpanPlan:
                 out_row += (hi - lo) * band_h
                 b = f * self.bpf + hi
             self.launches.append(out)
+        self._views = {}
+        if whole_frames:
+            # buffers hold the largest span of any batch
+            self.per_rank = max(max(self.frame_counts(b)) for b in range(max(1, world - 1))) * height
+
+    def frame_counts(self, batch: int):
+        """whole_frames: the frames of each rank's span in batch `batch`."""
+        if self.world == 1:
+            return [self.n_frames]
+        share = self.n_frames * self.root_weight / (self.root_weight + self.world - 1)
+        g0 = min(self.n_frames, int(np.floor(share + 0.5)))
+        q, m = divmod(self.n_frames - g0, self.world - 1)
+        out = [g0] + [q] * (self.world - 1)
+        for i in range(m):
+            out[1 + (batch * m + i) % (self.world - 1)] += 1
+        return out
+
+    def batch(self, b: int) -> "SpanPlan":
+        """The plan of batch b: this one, or with whole_frames the batch's own
+        cut (its extra frames on other ranks); one object per distinct cut."""
+        if not self.whole_frames or self.world <= 2:
+            return self
+        key = (b * ((self.n_frames - self.frame_counts(0)[0]) % (self.world - 1))) % (self.world - 1)
+        v = self._views.get(key)
+        if v is None:
+            v = SpanPlan(self.height, self.band_h, self.world, self.n_frames, self.root_weight, True, b)
+            v.per_rank = self.per_rank
+            self._views[key] = v
+        return v
 
     def recv_slices(self):
         """(rank, row0, rows) of every span rank 0 receives."""

@@ -351,6 +351,9 @@ def main() -> None:
     ap.add_argument("--exchange-every", type=int, default=0,
                     help="N > 1: frames per exchange batch (a multiple of --batch; 0 = default_span_batch for "
                          "spans, launches in flight x batch otherwise; spans fit it to divide the timed frames)")
+    ap.add_argument("--send-lag", type=int, default=1,
+                    help="spans: a sender sends each batch's span this many batches after queueing it (the host "
+                         "waits for the batch's launches to end then; the ring grows to lag + 2 slots)")
     ap.add_argument("--ring", type=int, default=2,
                     help="N > 1: exchange batches of slots in the ring (>= 2); a batch's slots are retraced only "
                          "after the exchange ring - 1 batches back")
@@ -359,6 +362,10 @@ def main() -> None:
                          "compute_dynamic_ray.comp:235), 3/4 of the bytes over each xGMI link, packed and "
                          "unpacked by rt_pack_rgb / rt_unpack_rgb (emulated 5%% slower at N = 8, profiles/r05/"
                          "emulation/r5ap; it pays only where a link is the bound, DESIGN.md §6)")
+    ap.add_argument("--span-cut", choices=("frames", "bands"), default="bands",
+                    help="spans: frames = cut each exchange batch at frame boundaries (every launch a whole "
+                         "frame; rank 0 its weighted share rounded, the others' extra frames rotating from batch "
+                         "to batch); bands = cut at band boundaries, exactly weighted (a band run at a span's ends)")
     ap.add_argument("--last-pieces", choices=("on", "off"), default="on",
                     help="spans: the last exchange batch of a phase travels launch by launch (each "
                          "launch's rows sent as it ends), so only the last launch's transfer is left "
@@ -505,7 +512,9 @@ def main() -> None:
         G = D * F                                              # N = 1: the slot ring
     # ring of exchange batches: enough for the D launches in flight plus the
     # batch being exchanged
-    R = max(3 if mode == "spans" else 2, args.ring, -(-D * F // G) + 1)
+    # spans: a sender sends a batch --send-lag batches after tracing it
+    lag = max(1, args.send_lag)
+    R = max(lag + 2 if mode == "spans" else 2, args.ring, -(-D * F // G) + 1)
     rad_on = dist_on and args.gather == "radiance"
     band_h = args.band
     plan = tplan = None
@@ -533,7 +542,8 @@ def main() -> None:
     elif mode == "spans":
         if H % band_h:
             raise SystemExit(f"--partition spans: --band ({band_h}) must divide the height ({H})")
-        plan = SpanPlan(H, band_h, world, G, args.root_weight if args.root_weight >= 0 else default_span_weight(world))
+        plan = SpanPlan(H, band_h, world, G, args.root_weight if args.root_weight >= 0 else default_span_weight(world),
+                        whole_frames=args.span_cut == "frames")
         # rank 0: the batch's frames (its own span traced in place, the others
         # received into them); rank r: its span
         rows = G * H if rank == 0 else plan.per_rank
@@ -547,7 +557,7 @@ def main() -> None:
             if rank == 0:
                 rgba_slots.fill_(255)
         rad_slots = torch.empty((R, rows, W, 3), dtype=torch.float32, device=dev) if rad_on else None
-        px_per_frame = plan.rows[rank] * W // G
+        px_per_frame = int(np.mean([plan.batch(b).rows[rank] for b in range(max(1, world - 1))])) * W // G
     elif mode == "tiles":
         tplan = TilePlan(W, H, world, G)
         src_index = torch.as_tensor(tplan.src, device=dev)
@@ -590,7 +600,24 @@ def main() -> None:
             c = cam_cache[k] = camera_path(cfg, args.camera_path, 1, k)[0]
         return c
 
-    tracer = SpanTracer(ctx, W, H, B, plan, rank) if mode == "spans" else \
+    span_tracers = {}
+
+    def view_of(k0):
+        """spans: the plan of the batch that starts at frame k0 (SpanPlan.batch)."""
+        return plan.batch(k0 // G)
+
+    def tracer_of(v):
+        """spans: the SpanTracer of batch plan v, and every launch's pointers per
+        ring slot, made once per plan (no tensor indexing on the host between
+        launches)."""
+        t = span_tracers.get(id(v))
+        if t is None:
+            tr = SpanTracer(ctx, W, H, B, v, rank)
+            t = span_tracers[id(v)] = (tr, [[span_ptrs(h, orow) for (_, _, _, orow) in tr.launches]
+                                            for h in range(R)])
+        return t
+
+    tracer = None if mode == "spans" else \
         ShareTracer(ctx, W, H, B, mode, rank, plan=plan, tplan=tplan, band_h=band_h, batch=G)
 
     def trace(k0, n, s, rgba_ptr, rad_ptr, stats=False):
@@ -608,7 +635,8 @@ def main() -> None:
         """Launch jl of this rank's span of the batch that starts at frame k0
         (rtamd.dist.SpanTracer)."""
         st_ = Stats() if stats else None
-        tracer.launch(cam_of(k0 + tracer.launches[jl][0]).ubo, jl, s.cuda_stream, rgba_ptr, rad_ptr, st_)
+        tr = tracer_of(view_of(k0))[0]
+        tr.launch(cam_of(k0 + tr.launches[jl][0]).ubo, jl, s.cuda_stream, rgba_ptr, rad_ptr, st_)
         return st_.as_dict() if stats else None
 
     def span_ptrs(h, out_row):
@@ -617,10 +645,6 @@ def main() -> None:
         y = out_row + (plan.row0[0] if rank == 0 else 0)
         return rgba_slots[h, y].data_ptr(), (rad_slots[h, y].data_ptr() if rad_on else None)
 
-    # spans: every launch's pointers per ring slot, made once (no tensor
-    # indexing on the host between launches)
-    span_tab = [[span_ptrs(h, orow) for (_, _, _, orow) in tracer.launches] for h in range(R)] \
-        if mode == "spans" else None
 
     def out_ptrs(k0, j):
         """Where launch j (frames k0 ...) writes: its slot of the ring."""
@@ -721,7 +745,7 @@ def main() -> None:
     send_q = []                # r > 0: (launch end events, slot, out_row, rows) of traced batches not yet sent
 
     def span_send(timed):
-        e_ends, h, orow, nr, pieces = send_q.pop(0)
+        e_ends, h, orow, nr, pieces, v = send_q.pop(0)
         if pieces is None:
             for e_end in e_ends:
                 e_end.synchronize()                    # host: the batch's launches have ended
@@ -742,7 +766,7 @@ def main() -> None:
                     emu_land[:n].copy_(src)            # the send's read of the rows
             else:
                 rows = (y, n) if e_end is not None else None
-                for w in rdist.span_send(rgba_slots[h], plan, rgb=rgb_slots[h] if wire_rgb else None,
+                for w in rdist.span_send(rgba_slots[h], v, rgb=rgb_slots[h] if wire_rgb else None,
                                          rad=rad_slots[h] if rad_on else None, rows=rows):
                     w.wait()                           # NCCL: main_stream waits for the send (host free)
         if timed:
@@ -760,21 +784,22 @@ def main() -> None:
             e0 = timing_event()
             e0.record(main_stream)
         works, landings = [], []
+        v = view_of(k0)
         if emu:
             col = rgb_slots[h] if wire_rgb else rgba_slots[h]
             if os.environ.get("BENCH_EMULATE_NOX") != "1":
-                for _, y0, nr in plan.recv_slices():   # the bytes the receives write
+                for _, y0, nr in v.recv_slices():      # the bytes the receives write
                     col[y0:y0 + nr].copy_(emu_buf[:nr])
         else:
-            works, landings = rdist.span_post_recvs(rgba_slots[h], plan, rgb=rgb_slots[h] if wire_rgb else None,
+            works, landings = rdist.span_post_recvs(rgba_slots[h], v, rgb=rgb_slots[h] if wire_rgb else None,
                                                     rad=rad_slots[h] if rad_on else None, pieces=pieces)
-        span_recv[h] = (works, landings, k0 + G, e0)
+        span_recv[h] = (works, landings, k0 + G, e0, v)
 
     def span_complete_recvs(h, timed):
-        works, landings, k_end, e0 = span_recv[h]
+        works, landings, k_end, e0, v = span_recv[h]
         span_recv[h] = None
         # NCCL: main_stream waits (gloo: the host); the RGB rows into the frames
-        rdist.span_finish_recvs(works, landings, rgba_slots[h], plan, rgb=rgb_slots[h] if wire_rgb else None)
+        rdist.span_finish_recvs(works, landings, rgba_slots[h], v, rgb=rgb_slots[h] if wire_rgb else None)
         if timed and e0 is not None:
             e1 = timing_event()
             e1.record(main_stream)
@@ -813,10 +838,12 @@ def main() -> None:
                     span_sent[h].synchronize()
             used = []
             piece_q = [] if (pieces and rank) else None
-            for jl in range(len(tracer.launches)):
+            v = view_of(k0)
+            tr, tab = tracer_of(v)
+            for jl in range(len(tr.launches)):
                 j = st["j"]
                 s = streams[j % D]
-                rp, dp = span_tab[h][jl]
+                rp, dp = tab[h][jl]
                 if timed:
                     e = (timing_event(), timing_event())
                     e[0].record(s)
@@ -827,21 +854,21 @@ def main() -> None:
                 if piece_q is not None:
                     ev = torch.cuda.Event()
                     ev.record(s)
-                    orow, n = plan.pieces(rank)[jl]
+                    orow, n = v.pieces(rank)[jl]
                     if n:
                         piece_q.append((ev, orow, n))
                 if s not in used:
                     used.append(s)
                 st["j"] = j + 1
             st["k"] = k0 + G
-            if rank and plan.rows[rank]:
+            if rank and v.rows[rank]:
                 ends = []
                 for s in used:
                     ev = torch.cuda.Event()
                     ev.record(s)
                     ends.append(ev)
-                send_q.append((ends, h, 0, plan.rows[rank], piece_q))
-                while len(send_q) > 1:                 # the batch before: sent once its launches end
+                send_q.append((ends, h, 0, v.rows[rank], piece_q, v))
+                while len(send_q) > lag:               # the batch before: sent once its launches end
                     span_send(timed)
         # the phase's exchanges complete before it ends
         while send_q:
@@ -907,7 +934,7 @@ def main() -> None:
         ms = []
         if mode == "spans":
             for k in ks:
-                for jl, (_, _, _, orow) in enumerate(tracer.launches):
+                for jl, (_, _, _, orow) in enumerate(tracer_of(view_of(k))[0].launches):
                     d = trace_span(k, jl, main_stream, count_rgba[orow * W].data_ptr(), None, stats=True)
                     for k2 in tot:
                         tot[k2] += d[k2]
@@ -934,7 +961,7 @@ def main() -> None:
     n_settle = int(n_settle.item()) * F
     k_t0 = after(after(0, n_settle), W_fr)
     if mode == "spans":
-        if args.camera_path == "static":
+        if args.camera_path == "static" and plan.batch(1) is plan:   # every batch the same span
             one = count_frames([k_t0])[0]
             loc = {k2: v * (K // G) for k2, v in one.items()}
         else:
@@ -1175,9 +1202,15 @@ def main() -> None:
                     f"launch (one band list per frame), {gather_kind} gather of every {G} frames + rank-0 "
                     f"assembly{shared}")
         elif mode == "spans":
-            part = (f"every batch of {G} frames cut into {world} contiguous spans of {band_h}-row bands (rank 0 "
-                    f"weight {plan.root_weight}, rows per rank {plan.rows}), one launch per frame of a span (whole "
-                    f"frames, a band run at either end), {D} launches in flight, {gather_kind} point-to-point "
+            if plan.whole_frames:
+                cut = (f"cut at frame boundaries into {world} contiguous spans of whole frames (rank 0 weight "
+                       f"{plan.root_weight}: frames per rank {plan.frame_counts(0)}, the others' extra frames "
+                       f"rotating from batch to batch), one launch per frame")
+            else:
+                cut = (f"cut into {world} contiguous spans of {band_h}-row bands (rank 0 weight {plan.root_weight}, "
+                       f"rows per rank {plan.rows}), one launch per frame of a span (whole frames, a band run at "
+                       f"either end)")
+            part = (f"every batch of {G} frames {cut}, {D} launches in flight, {gather_kind} point-to-point "
                     f"receives of every span straight into rank 0's frames (no assembly){shared}")
         elif mode == "tiles":
             part = (f"one frame per step tiled {tplan.gx} x {tplan.gy} over {world} ranks (tiles "

@@ -275,8 +275,10 @@ def _share_worker(rank, world, port, q, kind, arg, n_frames, W, H, B):
             # bench.py --partition spans: rank 0 traces its span in place in
             # the batch's frames, the others into a span buffer; one group of
             # point-to-point receives lands every span in rank 0's frames
-            band_h, rw, wire, pieces = arg
-            plan = SpanPlan(H, band_h, world, n_frames, rw)
+            band_h, rw, wire, pieces, whole_b = arg
+            # whole_b >= 0: cut at frame boundaries, batch whole_b's plan (its
+            # extra frames on its own ranks)
+            plan = SpanPlan(H, band_h, world, n_frames, rw, whole_frames=whole_b >= 0).batch(max(0, whole_b))
             col = torch.zeros((n_frames * H, W, 4), dtype=torch.uint8) if rank == 0 else None
             rgb = None
             if wire == "rgb":
@@ -473,6 +475,20 @@ def test_share_tracer_rejects_uneven_lists():
     front, as bench.py's --deal auto avoids choosing it."""
     from rtamd.dist import SharePlan, ShareTracer, TilePlan
     plan = SharePlan(1080, 16, 8, 8, 0.8, layout="dealt")
+    # cut at frame boundaries (--span-cut frames): whole-frame launches only, rank 0
+    # 3 frames, the others 4 and one extra frame rotating over them batch by batch
+    wp = SpanPlan(1080, 8, 8, 32, 0.8, whole_frames=True)
+    extra = []
+    for b in range(14):
+        v = wp.batch(b)
+        c = v.frame_counts(b)
+        assert c[0] == 3 and sum(c) == 32 and sorted(c[1:]) == [4] * 6 + [5]
+        assert v.rows == [n * 1080 for n in c] and all((lo, hi) == (0, 135) for r in range(8)
+                                                       for _, lo, hi, _ in v.launches[r])
+        assert v.per_rank == 5 * 1080 and v is wp.batch(b + 7)
+        extra.append(c.index(5))
+    assert extra[:7] == list(range(1, 8))
+    assert SpanPlan(1080, 8, 4, 16, 0.9, whole_frames=True).frame_counts(0) == [4, 4, 4, 4]
     with pytest.raises(ValueError, match="divide the height"):
         ShareTracer(None, 1920, 1080, 4, "bands", 1, plan=plan, band_h=16, batch=8)
     ok = SharePlan(1080, 8, 8, 8, 0.8, layout="dealt")
@@ -485,27 +501,31 @@ def test_share_tracer_rejects_uneven_lists():
     assert tt.rect == (960, 540, 960, 540)
 
 
-@pytest.mark.parametrize("world,n_frames,band_h,rw,wire,pieces", [(2, 3, 4, 1.0, "rgba", False),
-                                                                  (4, 4, 4, 0.6, "rgb", False),
-                                                                  (8, 8, 2, 0.8, "rgb", False),
-                                                                  (3, 2, 8, 0.0, "rgba", False),
-                                                                  (3, 2, 8, 0.5, "rgb", False),
-                                                                  (4, 4, 4, 0.6, "rgb", True),
-                                                                  (3, 3, 4, 0.8, "rgba", True)])
-def test_spans_weak_scaling(world, n_frames, band_h, rw, wire, pieces):
+@pytest.mark.parametrize("world,n_frames,band_h,rw,wire,pieces,whole_b", [(2, 3, 4, 1.0, "rgba", False, -1),
+                                                                          (4, 4, 4, 0.6, "rgb", False, -1),
+                                                                          (8, 8, 2, 0.8, "rgb", False, -1),
+                                                                          (3, 2, 8, 0.0, "rgba", False, -1),
+                                                                          (3, 2, 8, 0.5, "rgb", False, -1),
+                                                                          (4, 4, 4, 0.6, "rgb", True, -1),
+                                                                          (3, 3, 4, 0.8, "rgba", True, -1),
+                                                                          (8, 11, 4, 0.8, "rgba", True, 3),
+                                                                          (4, 6, 4, 0.6, "rgb", False, 1)])
+def test_spans_weak_scaling(world, n_frames, band_h, rw, wire, pieces, whole_b):
     """bench.py --partition spans: each rank traces one contiguous span of the
     batch's rows (whole frames, a run of bands at either end; rank 0's span
     rw times the others'), rank 0 in place in the batch's frames, and one
     group of point-to-point receives lands every other span straight in them
     (wire "rgb": the rows travel as RGB and rank 0 writes them into its RGBA8
     frames, whose alpha bytes it set once; pieces: the spans travel launch by
-    launch, one receive per piece, as bench.py's last batch of a phase): every
-    frame and its radiance equal the oracle's, bit for bit."""
+    launch, one receive per piece, as bench.py's last batch of a phase;
+    whole_b >= 0: spans cut at frame boundaries, the plan of batch whole_b):
+    every frame and its radiance equal the oracle's, bit for bit."""
     W, H = 48, 40
-    traced = _run_share(world, "spans", (band_h, rw, wire, pieces), n_frames=n_frames, W=W, H=H, B=2)
+    traced = _run_share(world, "spans", (band_h, rw, wire, pieces, whole_b), n_frames=n_frames, W=W, H=H, B=2)
     assert sum(traced.values()) == n_frames * W * H
     if 0 < rw < 1.0:
-        assert traced[0] < min(traced[r] for r in range(1, world))
+        assert traced[0] < min(traced[r] for r in range(1, world)) or \
+            (whole_b >= 0 and traced[0] <= min(traced[r] for r in range(1, world)))   # whole frames: rounded
     if rw == 0.0:
         assert traced[0] == 0
 
@@ -538,5 +558,19 @@ def test_span_plan_1080p():
         assert ps[0][0] == plan.row0[r] and sum(n for _, n in ps) == plan.rows[r]
         assert all(ps[i][0] + ps[i][1] == ps[i + 1][0] for i in range(len(ps) - 1))
         assert [(plan.row0[r] + o, n) for o, n in plan.pieces(r)] == ps
+    # cut at frame boundaries (--span-cut frames): whole-frame launches only, rank 0
+    # 3 frames, the others 4 and one extra frame rotating over them batch by batch
+    wp = SpanPlan(1080, 8, 8, 32, 0.8, whole_frames=True)
+    extra = []
+    for b in range(14):
+        v = wp.batch(b)
+        c = v.frame_counts(b)
+        assert c[0] == 3 and sum(c) == 32 and sorted(c[1:]) == [4] * 6 + [5]
+        assert v.rows == [n * 1080 for n in c] and all((lo, hi) == (0, 135) for r in range(8)
+                                                       for _, lo, hi, _ in v.launches[r])
+        assert v.per_rank == 5 * 1080 and v is wp.batch(b + 7)
+        extra.append(c.index(5))
+    assert extra[:7] == list(range(1, 8))
+    assert SpanPlan(1080, 8, 4, 16, 0.9, whole_frames=True).frame_counts(0) == [4, 4, 4, 4]
     with pytest.raises(ValueError, match="divide the height"):
         SpanPlan(1080, 16, 8, 32, 0.8)
