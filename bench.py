@@ -398,8 +398,7 @@ def main() -> None:
                     help="untimed frames before the warmup steps: this many seconds of counting-pass time "
                          "(5 to --settle-max launches; a GPU that has idled runs its first launches slower: "
                          "N = 1 at 20 steps 0.1240-0.1256 ms per frame against 0.1253-0.1292 with 0.4 s and "
-                         "100 launches, profiles/r05/r5bn; an N = 8 sender, emulated, 0.153-0.156 against "
-                         "0.163-0.166, profiles/r05/emulation/r5bl, r5bm)")
+                         "100 launches, profiles/r05/r5bn; N > 1 keeps 0.4 s and 100)")
     ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_latest.json"),
                     help="PMC per launch of each config (tools/pmc_traffic.py: SQ_INSTS_VMEM_RD, HBM bytes) for "
                          "the roofline")
@@ -954,28 +953,20 @@ def main() -> None:
     # launch's device time; a counting launch runs ~4x a plain one), so the
     # timed steps see the steady state of a running render loop (a GPU takes
     # ~0.1 s of load to settle: --settle-s), then the W warmup steps.  Agreed
-    # over the ranks, so every rank runs the same collectives.  Ranks sharing
-    # one GPU over gloo (a rehearsal, every exchange staged through the host)
-    # settle as round 4 did, 0.4 s and at most 100 launches.
+    # over the ranks, so every rank runs the same collectives.  N > 1 settles
+    # as round 4 did, 0.4 s and at most 100 launches: longer settles measured
+    # no better in the spans emulation at N = 2 and 8 (profiles/r05/emulation/
+    # r5bm, r5bp).
     settle_s, settle_max = args.settle_s, args.settle_max
-    if os.environ.get("BENCH_SHARE_GPU"):
+    if dist_on:
         settle_s, settle_max = min(settle_s, 0.4), min(settle_max, 100)
     _, ms0 = count_frames([0])
-    if mode == "spans":
-        # this rank's own launches: one per frame piece of its span, G /
-        # len(launches) of the job's frames each (a launch of F frames would
-        # count a sender's settle 8x short at N = 8: 0.165 ms per step against
-        # 0.157-0.159 settled longer, emulated, profiles/r05/emulation/r5bl)
-        est_ms = max(0.05, float(ms0[0]))
-        per_launch = G / max(1, len(tracer_of(view_of(0))[0].launches))
-    else:
-        est_ms = max(0.05, float(ms0[0]) * F)              # a launch's counting time
-        per_launch = F
-    n_settle = max(5, 2 * D, min(settle_max, int(settle_s * 1e3 / est_ms)))
-    n_settle = torch.tensor([int(np.ceil(n_settle * per_launch))], dtype=torch.int64, device=dev)
+    est_ms = max(0.05, float(ms0[0]) * F)                  # a launch's counting time
+    n_settle = torch.tensor([max(5, 2 * D, min(settle_max, int(settle_s * 1e3 / est_ms)))], dtype=torch.int64,
+                            device=dev)
     if dist_on:
-        dist.all_reduce(n_settle, op=dist.ReduceOp.MAX if mode == "spans" else dist.ReduceOp.MIN)
-    n_settle = int(n_settle.item())
+        dist.all_reduce(n_settle, op=dist.ReduceOp.MIN)
+    n_settle = int(n_settle.item()) * F
     k_t0 = after(after(0, n_settle), W_fr)
     if mode == "spans":
         if args.camera_path == "static" and plan.batch(1) is plan:   # every batch the same span
