@@ -475,20 +475,6 @@ def test_share_tracer_rejects_uneven_lists():
     front, as bench.py's --deal auto avoids choosing it."""
     from rtamd.dist import SharePlan, ShareTracer, TilePlan
     plan = SharePlan(1080, 16, 8, 8, 0.8, layout="dealt")
-    # cut at frame boundaries (--span-cut frames): whole-frame launches only, rank 0
-    # 3 frames, the others 4 and one extra frame rotating over them batch by batch
-    wp = SpanPlan(1080, 8, 8, 32, 0.8, whole_frames=True)
-    extra = []
-    for b in range(14):
-        v = wp.batch(b)
-        c = v.frame_counts(b)
-        assert c[0] == 3 and sum(c) == 32 and sorted(c[1:]) == [4] * 6 + [5]
-        assert v.rows == [n * 1080 for n in c] and all((lo, hi) == (0, 135) for r in range(8)
-                                                       for _, lo, hi, _ in v.launches[r])
-        assert v.per_rank == 5 * 1080 and v is wp.batch(b + 7)
-        extra.append(c.index(5))
-    assert extra[:7] == list(range(1, 8))
-    assert SpanPlan(1080, 8, 4, 16, 0.9, whole_frames=True).frame_counts(0) == [4, 4, 4, 4]
     with pytest.raises(ValueError, match="divide the height"):
         ShareTracer(None, 1920, 1080, 4, "bands", 1, plan=plan, band_h=16, batch=8)
     ok = SharePlan(1080, 8, 8, 8, 0.8, layout="dealt")
@@ -558,6 +544,20 @@ def test_span_plan_1080p():
         assert ps[0][0] == plan.row0[r] and sum(n for _, n in ps) == plan.rows[r]
         assert all(ps[i][0] + ps[i][1] == ps[i + 1][0] for i in range(len(ps) - 1))
         assert [(plan.row0[r] + o, n) for o, n in plan.pieces(r)] == ps
+    # cut at frame boundaries (--span-cut frames): whole-frame launches only, rank 0
+    # 3 frames, the others 4 and one extra frame rotating over them batch by batch
+    wp = SpanPlan(1080, 8, 8, 32, 0.8, whole_frames=True)
+    extra = []
+    for b in range(14):
+        v = wp.batch(b)
+        c = v.frame_counts(b)
+        assert c[0] == 3 and sum(c) == 32 and sorted(c[1:]) == [4] * 6 + [5]
+        assert v.rows == [n * 1080 for n in c] and all((lo, hi) == (0, 135) for r in range(8)
+                                                       for _, lo, hi, _ in v.launches[r])
+        assert v.per_rank == 5 * 1080 and v is wp.batch(b + 7)
+        extra.append(c.index(5))
+    assert extra[:7] == list(range(1, 8))
+    assert SpanPlan(1080, 8, 4, 16, 0.9, whole_frames=True).frame_counts(0) == [4, 4, 4, 4]
     # cut at frame boundaries (--span-cut frames): whole-frame launches only, rank 0
     # 3 frames, the others 4 and one extra frame rotating over them batch by batch
     wp = SpanPlan(1080, 8, 8, 32, 0.8, whole_frames=True)
