@@ -370,6 +370,9 @@ def main() -> None:
                     help="spans: the last exchange batch of a phase travels launch by launch (each "
                          "launch's rows sent as it ends), so only the last launch's transfer is left "
                          "after the traces (DESIGN.md §6)")
+    ap.add_argument("--piece-wait", choices=("host", "device"), default="host",
+                    help="spans, --last-pieces: each piece's send waits for its launch on the host, or on the "
+                         "device (the exchange stream waits for the launch's event; the host queues every piece)")
     ap.add_argument("--gather", choices=("rgba", "radiance"), default="rgba",
                     help="N > 1: radiance = gather the float radiance beside the RGBA8 frame")
     ap.add_argument("--camera-path", choices=("static", "orbit"), default="static")
@@ -758,7 +761,10 @@ def main() -> None:
             e0.record(main_stream)
         for e_end, y, n in pieces:                     # the last batch of a phase: launch by launch
             if e_end is not None:
-                e_end.synchronize()                    # host: this launch has ended
+                if args.piece_wait == "device":
+                    main_stream.wait_event(e_end)      # the send's stream: after this launch
+                else:
+                    e_end.synchronize()                # host: this launch has ended
             if emu:
                 src = rgba_slots[h][y:y + n]
                 if wire_rgb:
