@@ -71,9 +71,18 @@ struct Builder {
     std::vector<int> tmp;           // scratch: stable partition
     std::vector<float> rarea;       // scratch: right-side areas
 
+    // Below this depth a node splits at the median of its widest centroid
+    // axis instead of by SAH: primitives whose boxes and centroids coincide
+    // (copies of a triangle in other materials, nested boxes about one
+    // centre) make every SAH split peel one primitive off, a tree m deep
+    // built in O(m^2).  Ordinary scenes never get near it (configs 3 / 5 / 6:
+    // depth 22 / 28 / 22).
+    static constexpr int kSahDepth = 64;
+
     // Builds the subtree of the range [b, e) as node `id` (its descendants
-    // take ids id + 1 .. id + 2m - 2); returns its depth below id.
-    int build(int id, int b, int e, unsigned threads) {
+    // take ids id + 1 .. id + 2m - 2) at depth `level`; returns its depth
+    // below id.
+    int build(int id, int b, int e, unsigned threads, int level = 0) {
         BNode& nd = nodes[id];
         const int m = e - b;
         nd.m = m;
@@ -93,7 +102,21 @@ struct Builder {
         int baxis = 0, bpos = m / 2;
         float bcost = 0.0f;
         bool found = false;
-        for (int k = 0; k < 3; ++k) {
+        if (level >= kSahDepth) {                     // median of the widest centroid extent
+            float ext = -1.0f;
+            for (int k = 0; k < 3; ++k) {
+                const float x = prims[ord[k][e - 1]].c[k] - prims[ord[k][b]].c[k];
+                if (x > ext) {
+                    ext = x;
+                    baxis = k;
+                }
+            }
+            found = true;
+        }
+        // ties keep the split nearest the middle: equal costs (coincident
+        // boxes) must not peel one primitive off per level
+        const auto off_mid = [m](int pos) { return pos > m - pos ? 2 * pos - m : m - 2 * pos; };
+        for (int k = 0; k < 3 && level < kSahDepth; ++k) {
             const int* o = ord[k].data();
             float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
             for (int i = e - 1; i > b; --i) {
@@ -115,7 +138,7 @@ struct Builder {
                     hi[q] = std::max(hi[q], p.hi[q]);
                 }
                 const float cost = (float)(i - b + 1) * area(lo, hi) + (float)(e - 1 - i) * rarea[i + 1];
-                if (!found || cost < bcost) {
+                if (!found || cost < bcost || (cost == bcost && off_mid(i + 1 - b) < off_mid(bpos))) {
                     found = true;
                     baxis = k;
                     bpos = i + 1 - b;
@@ -138,12 +161,12 @@ struct Builder {
         nd.right = id + 2 * ml;   // id + 1 + (2 ml - 1)
         int dl, dr;
         if (threads > 1 && m > 16384) {
-            std::thread th([&] { dl = build(id + 1, b, mid, threads / 2); });
-            dr = build(id + 2 * ml, mid, e, threads - threads / 2);
+            std::thread th([&] { dl = build(id + 1, b, mid, threads / 2, level + 1); });
+            dr = build(id + 2 * ml, mid, e, threads - threads / 2, level + 1);
             th.join();
         } else {
-            dl = build(id + 1, b, mid, 1);
-            dr = build(id + 2 * ml, mid, e, 1);
+            dl = build(id + 1, b, mid, 1, level + 1);
+            dr = build(id + 2 * ml, mid, e, 1, level + 1);
         }
         return 1 + std::max(dl, dr);
     }
@@ -183,7 +206,7 @@ uint16_t half_bits_down(float x) {
 
 int accel_build(const void* vertices, size_t vertex_bytes, const void* materials, size_t material_bytes,
                 const void* bvh_nodes, size_t bvh_bytes, int n_layouts, int n_threads, AccelHost* out,
-                std::string* err, int format) {
+                std::string* err, int format, int64_t cap_slots) {
     *out = AccelHost{};
     if (format != 0 && format != 1) {
         *err = "accel: format must be 0 or 1";
@@ -272,10 +295,12 @@ int accel_build(const void* vertices, size_t vertex_bytes, const void* materials
     // a subtree of k triangles: k - 1 internal nodes (1 slot) and k leaves
     const auto span = [LS](int64_t k) { return (LS + 1) * k - 1; };
     const int64_t slots = span(m);
-    const int64_t cap = format ? (int64_t)(1u << 30) - 8 : (int64_t)(1u << 27) - 4;   // link bits; 4 GB
+    int64_t cap = format ? (int64_t)(1u << 30) - 8 : (int64_t)(1u << 27) - 4;   // link bits; 4 GB
+    if (cap_slots > 0 && cap_slots < cap) cap = cap_slots;
     if (slots * n_layouts + 8 > cap) {
-        *err = "accel: " + std::to_string(m) + " triangles: the layouts exceed " + std::to_string(cap) + " slots";
-        return -1;
+        *err = "accel: " + std::to_string(m) + " triangles: " + std::to_string(n_layouts) + " layouts exceed " +
+               std::to_string(cap) + " slots";
+        return kAccelTooBig;
     }
 
     // 2. the tree
@@ -386,6 +411,17 @@ int accel_build(const void* vertices, size_t vertex_bytes, const void* materials
     }
     ACCEL_T("layouts written");
     return 0;
+}
+
+int accel_build_fit(const void* vertices, size_t vertex_bytes, const void* materials, size_t material_bytes,
+                    const void* bvh_nodes, size_t bvh_bytes, int n_layouts, AccelHost* out, std::string* err,
+                    int format, int64_t cap_slots) {
+    int rc = accel_build(vertices, vertex_bytes, materials, material_bytes, bvh_nodes, bvh_bytes, n_layouts, 0, out,
+                         err, format, cap_slots);
+    if (rc == kAccelTooBig && n_layouts == 8)
+        rc = accel_build(vertices, vertex_bytes, materials, material_bytes, bvh_nodes, bvh_bytes, 1, 0, out, err,
+                         format, cap_slots);
+    return rc;
 }
 
 }  // namespace rtamd

@@ -58,14 +58,30 @@ struct AccelHost {
     double sah = 0.0;               // SAH cost of the tree (internal 1, leaf 1, relative to the root box area)
 };
 
+// The layouts do not fit the slot cap (accel_build's return value).
+constexpr int kAccelTooBig = -2;
+
 // Builds the records from the reference's buffers (the rt_upload_scene
 // inputs: 48-B vertex records, 16-B materials, 48-B preorder nodes).  The
-// buffers must already have passed build_host_scene's validation.  Returns
-// 0, or -1 with *err set.  n_threads: 0 = hardware concurrency.  format: 0 or
-// 1 (above).
+// buffers must already have passed build_host_scene's validation, and
+// bvh_bytes must cover only the nodes the root's subtree holds (HostScene::end
+// x 48): a node past the root's skip is never visited by the reference's DFS
+// (compute_dynamic_ray.comp:185-210), so its leaf is not a primitive.  Returns
+// 0, kAccelTooBig when n_layouts copies exceed the slot cap (the 32-bit buffer
+// offsets: 2^27 - 4 slots, ~5.6 M triangles at 8 layouts; cap_slots > 0 lowers
+// it, for tests), or -1 with *err set.  n_threads: 0 = hardware concurrency.
+// format: 0 or 1 (above).
 int accel_build(const void* vertices, size_t vertex_bytes, const void* materials, size_t material_bytes,
                 const void* bvh_nodes, size_t bvh_bytes, int n_layouts, int n_threads, AccelHost* out,
-                std::string* err, int format = 0);
+                std::string* err, int format = 0, int64_t cap_slots = 0);
+
+// accel_build with the capacity fallback: n_layouts 8 that do not fit become
+// 1 layout (out->n_layouts says which).  Returns 0, kAccelTooBig when one
+// layout does not fit either (the caller then walks the reference's own
+// tree, option accel 0, whose records reach ~45 M triangles), or -1.
+int accel_build_fit(const void* vertices, size_t vertex_bytes, const void* materials, size_t material_bytes,
+                    const void* bvh_nodes, size_t bvh_bytes, int n_layouts, AccelHost* out, std::string* err,
+                    int format = 0, int64_t cap_slots = 0);
 
 // Half-precision bits of the largest half <= x (-inf below -65504), and of the
 // smallest half >= x: the outward rounding of format 1's internal boxes.

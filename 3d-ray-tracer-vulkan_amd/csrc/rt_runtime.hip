@@ -41,6 +41,13 @@ void set_error(const char* fmt, ...) {
 
 // ------------------------------------------------------------ scene build --
 
+// The accel records' slot cap: 0 = the hardware's (accel_build.h).  Tests
+// lower it through RTAMD_ACCEL_CAP_SLOTS to drive the capacity fallback.
+static int64_t accel_cap_slots() {
+    const char* v = std::getenv("RTAMD_ACCEL_CAP_SLOTS");
+    return v ? std::atoll(v) : 0;
+}
+
 static inline float f32_at(const unsigned char* p, size_t off) {
     float f;
     std::memcpy(&f, p + off, 4);
@@ -1202,7 +1209,9 @@ int rt_upload_scene(rt_ctx* ctx, const void* vertices, size_t vertex_bytes,
     // line (and straddle two) starts one slot later; its predecessor's pad bit
     // (a leaf's bit 29 of word [0].w, an internal node's bit 2 of word [1].w)
     // tells the walk to step over the pad slot.
-    const size_t n2 = (size_t)hs.n_nodes;
+    // Only the root's subtree, [0, end): nodes past the root's skip are
+    // never visited by the reference's DFS (compute_dynamic_ray.comp:185-210).
+    const size_t n2 = (size_t)hs.end;
     std::vector<int> slot(n2 + 1);
     std::vector<uint8_t> padded(n2 + 1, 0);       // a pad slot precedes node i
     size_t n_leaves = 0;
@@ -1272,17 +1281,22 @@ int rt_upload_scene(rt_ctx* ctx, const void* vertices, size_t vertex_bytes,
     // every device; the reference's walk records above stay beside them for
     // the fallback, and the node-indexed arrays (walk 0, the frontier walk of
     // heavy pixels) are not needed.
+    // Past the slot cap 8 layouts become 1, and a scene too large for one
+    // walks the reference's own tree (accel_used says which: 8, 1 or 0).
     AccelHost ah;
+    bool acc = false;
     if (ctx->accel) {
         std::string msg;
-        if (accel_build(vertices, vertex_bytes, materials, material_bytes, bvh_nodes, bvh_bytes, ctx->accel, 0, &ah,
-                        &msg, ctx->accel_half ? 1 : 0)) {
+        const int rc = accel_build_fit(vertices, vertex_bytes, materials, material_bytes, bvh_nodes,
+                                       (size_t)hs.end * RT_NODE_RECORD_BYTES, ctx->accel, &ah, &msg,
+                                       ctx->accel_half ? 1 : 0, accel_cap_slots());
+        if (rc != 0 && rc != kAccelTooBig) {
             free_host_scene(&hs);
             set_error("rt_upload_scene: %s", msg.c_str());
             return RT_ERR_BAD_SCENE;
         }
+        acc = rc == 0;
     }
-    const bool acc = ctx->accel != 0;
     ctx->has_scene = false;
     for (PerDevice& p : ctx->dev) {
         RT_HIP_CHECK(hipSetDevice(p.device));
@@ -2121,14 +2135,27 @@ int rt_accel_records(const void* vertices, size_t vertex_bytes, const void* mate
     const char* err = nullptr;
     int rc = build_host_scene(vertices, vertex_bytes, materials, material_bytes, bvh_nodes, bvh_bytes, &hs, &err);
     if (rc != RT_OK) { set_error("rt_accel_records: %s", err); return rc; }
+    const size_t reach = (size_t)hs.end * RT_NODE_RECORD_BYTES;    // the root's subtree only
     free_host_scene(&hs);
     AccelHost ah;
     std::string msg;
     const int nl = n_layouts & ~RT_ACCEL_FORMAT_HALF;
-    if (accel_build(vertices, vertex_bytes, materials, material_bytes, bvh_nodes, bvh_bytes, nl, 0, &ah,
-                    &msg, (n_layouts & RT_ACCEL_FORMAT_HALF) ? 1 : 0)) {
+    if (nl != 1 && nl != 8) {
+        set_error("rt_accel_records: n_layouts must be 1 or 8");
+        return RT_ERR_INVALID_ARG;
+    }
+    rc = accel_build_fit(vertices, vertex_bytes, materials, material_bytes, bvh_nodes, reach, nl, &ah, &msg,
+                         (n_layouts & RT_ACCEL_FORMAT_HALF) ? 1 : 0, accel_cap_slots());
+    if (rc == kAccelTooBig) {                      // rt_upload_scene walks the reference's tree: no records
+        if (n_words) *n_words = 0;
+        if (info) {
+            for (int k = 0; k < 6; ++k) info[k] = 0;
+        }
+        return RT_OK;
+    }
+    if (rc != 0) {
         set_error("rt_accel_records: %s", msg.c_str());
-        return nl == 1 || nl == 8 ? RT_ERR_BAD_SCENE : RT_ERR_INVALID_ARG;
+        return RT_ERR_BAD_SCENE;
     }
     if (n_words) *n_words = ah.rec.size();
     if (info) {

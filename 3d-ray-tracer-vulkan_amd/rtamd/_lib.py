@@ -37,7 +37,41 @@ EXPORTED = (
     "rt_host_alloc", "rt_host_free", "rt_render_async", "rt_render_wait", "rt_upload_spheres",
     "rt_render_batch_device", "rt_band_list_rows", "rt_render_batch_lists_device", "rt_band_lists_rows",
     "rt_render_poll", "rt_accel_records", "rt_abi_version", "rt_pack_rgb", "rt_unpack_rgb",
+    "rt_build_id",
 )
+
+# The library's sources in the Makefile's SRC_ALL order: rt_build_id's
+# "src=" field is the first 16 hex digits of SHA-256 over them concatenated.
+BUILD_SOURCES = ("csrc/rt_trace.hip", "csrc/rt_runtime.hip", "csrc/rt_learn.hip", "csrc/rt_wire.hip",
+                 "csrc/scene_build.cpp", "csrc/accel_build.cpp", "csrc/rt_internal.h", "csrc/accel_build.h",
+                 "../include/rtamd.h")
+
+
+def source_hash() -> str:
+    """SHA-256 (16 hex digits) of the library's sources as they are in this tree."""
+    import hashlib
+    h = hashlib.sha256()
+    for f in BUILD_SOURCES:
+        with open(os.path.join(PKG_ROOT, f), "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
+def file_build_id(path: str = LIB_PATH) -> str | None:
+    """The build id embedded in a built library, read from the file (no load)."""
+    import re
+    try:
+        with open(path, "rb") as fh:
+            m = re.search(rb"RTAMD_BUILD_ID:(src=[0-9a-f]{16} git=[0-9a-z]+)", fh.read())
+    except OSError:
+        return None
+    return m.group(1).decode() if m else None
+
+
+def build_matches_tree(path: str = LIB_PATH) -> bool:
+    """True when the library at path was built from this tree's sources."""
+    bid = file_build_id(path)
+    return bid is not None and bid.startswith(f"src={source_hash()} ")
 
 
 class RtError(RuntimeError):
@@ -136,6 +170,7 @@ def lib() -> C.CDLL:
                 "rt_accel_records": (i32, [vp, sz, vp, sz, vp, sz, i32, C.POINTER(C.c_uint32), sz, C.POINTER(sz),
                                            C.POINTER(C.c_int32)]),
                 "rt_abi_version": (i32, [C.POINTER(sz), C.POINTER(sz)]),
+                "rt_build_id": (C.c_char_p, []),
                 "rt_pack_rgb": (i32, [vp, vp, sz, vp]),
                 "rt_unpack_rgb": (i32, [vp, vp, sz, vp]),
             }

@@ -259,9 +259,17 @@ int rt_render_poll(rt_ctx* ctx, uint64_t ticket, int* done);
  *                   box's t_enter is walked again in the reference's order.
  *                   Frames, segments and material reads are the reference
  *                   order's; node visits and triangle tests are the accel
- *                   walk's own.  Heavy tiles / pixels are not
- *                   split out of accel launches (heavy_first still orders
- *                   the tiles)
+ *                   walk's own.  The exactness argument holds
+ *                   when no triangle's rounded t lies more than that margin
+ *                   before its own leaf box's t_enter; no tested scene comes
+ *                   within 2^-10 of it (tests/test_accel_model.py, adversarial
+ *                   slivers, grazing rays, far-from-origin meshes), but it is
+ *                   a bound, not a proof: accel 0 is the exact mode by
+ *                   construction.  Past the records' slot cap (2^27 - 4
+ *                   slots: ~5.6 M triangles at 8 layouts) the upload falls
+ *                   back to 1 layout, then to the reference's tree
+ *                   ("accel_used").  Heavy tiles / pixels are not split out
+ *                   of accel launches (heavy_first still orders the tiles)
  *   "split_bounce"  accel walk, no extensions: b in 1..max_bounces-1 = a
  *                   frame's paths still alive at bounce b leave its kernel for
  *                   the wave's ray slots (packed per wave, no atomics), a scan
@@ -439,6 +447,14 @@ const char* rt_last_error(void);
  * as it was compiled (nullable): a host checks them once after loading. */
 int rt_abi_version(size_t* stats_bytes, size_t* camera_bytes);
 
+/* The build's provenance: "src=<16 hex> git=<12 hex>", the first 16 hex digits
+ * of SHA-256 over the library's sources and headers concatenated in the
+ * Makefile's order (SRC_ALL), and the checkout's HEAD when it was built.  The
+ * same string is embedded in the file after "RTAMD_BUILD_ID:", so a test can
+ * check a library against the tree without loading it (rtamd/_lib.py
+ * source_hash, tests/conftest.py, __graft_entry__.smoke). */
+const char* rt_build_id(void);
+
 /* Node / triangle counts and tree depth of the uploaded scene. */
 int rt_scene_info(rt_ctx* ctx, size_t* n_nodes, size_t* n_tris, int* max_depth);
 
@@ -463,8 +479,13 @@ int rt_scene_validate(const void* vertices, size_t vertex_bytes,
  * *n_words = the words of the records (n_layouts * slots, + 64 B of padding);
  * info (nullable) receives {n_layouts, slots per layout, root is a leaf,
  * primitives after dropping byte-identical duplicates, reference leaves, tree
- * depth}.  An analysis and test entry point (oracle/rt_accel_model.c walks
- * these records on the CPU); a host embedding the backend never needs it. */
+ * depth}.  Only the root's subtree counts (nodes past the root's skip are
+ * never visited by the reference).  The capacity fallback of rt_upload_scene
+ * applies: 8 layouts past the slot cap are built as 1 (info[0] = 1), and a
+ * scene too large for one layout gets no records (RT_OK, *n_words = 0, info
+ * all 0: rt_upload_scene walks the reference's own tree).  An analysis and
+ * test entry point (oracle/rt_accel_model.c walks these records on the CPU);
+ * a host embedding the backend never needs it. */
 /* The multi-GPU wire format (rtamd/dist.py span_send / span_finish_recvs,
  * DESIGN.md §6): a frame's alpha byte is always 255 (compute_dynamic_ray.comp:235),
  * so rows cross the xGMI links as RGB.  rt_pack_rgb packs n_px RGBA8 pixels

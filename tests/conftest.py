@@ -11,12 +11,12 @@ for p in (PKG_DIR, ROOT):
 
 REFERENCE = "/root/reference"
 
-# The GPU suites test_gpu_parity / test_gpu_pipeline / test_gpu_dist / test_jni_shim
-# pin the reference-order walk (option accel 0), whose work counters are the
-# oracle's own, on every Renderer that does not choose otherwise (rt_create
-# reads RTAMD_ACCEL).  The default accel walk (binned-SAH tree, DESIGN.md
-# §4a) is tested by test_gpu_accel.py and by the tests below that set option
-# accel themselves, against the same oracle frames.
+# A Renderer that does not choose otherwise walks the reference's own tree
+# (option accel 0, whose work counters are the oracle's own; rt_create reads
+# RTAMD_ACCEL).  The default accel walk (SAH tree) runs in
+# test_gpu_accel.py, in every test of test_gpu_parity.py (its module fixture
+# runs each test on accel 8 and on accel 0) and in the tests of
+# test_gpu_pipeline / test_gpu_dist / test_jni_shim parametrized over accel.
 os.environ["RTAMD_ACCEL"] = "0"
 
 
@@ -26,14 +26,21 @@ def pytest_configure(config):
 
 @pytest.fixture(scope="session", autouse=True)
 def _built():
-    """Build the native library and the oracle once (no GPU needed)."""
+    """The native library under test is this tree's: its embedded build id
+    (rt_build_id, read from the file) must carry the SHA-256 of the sources
+    as they are here.  A library that is missing or built from other sources
+    is rebuilt first (make is incremental); the oracle is built if missing."""
     import subprocess
-    lib = os.path.join(PKG_DIR, "lib", "librtamd.so")
+    from rtamd import _lib
     olib = os.path.join(ROOT, "oracle", "liboracle.so")
-    if not os.path.exists(lib):
+    if not _lib.build_matches_tree() and "RTAMD_LIB_PATH" not in os.environ:
         subprocess.run(["make", "-j8", "-C", PKG_DIR], check=True)
+    if "RTAMD_LIB_PATH" not in os.environ:
+        assert _lib.build_matches_tree(), (f"{_lib.LIB_PATH}: build id {_lib.file_build_id()} does not match "
+                                           f"the tree's sources (src={_lib.source_hash()})")
     if not os.path.exists(olib):
         subprocess.run(["make", "-C", os.path.join(ROOT, "oracle")], check=True)
+    print(f"\nlibrtamd build id: {_lib.file_build_id()} (tree src={_lib.source_hash()})")
     yield
 
 

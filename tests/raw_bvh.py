@@ -59,3 +59,27 @@ def raw_bvh_scene(n, shape, seed):
     verts[:, :, :3] = tv[order]
     return SimpleNamespace(model_vertex_data=verts.reshape(-1), model_material_data=mats[order].reshape(-1),
                            flat_bvh_data=np.frombuffer(b"".join(recs), np.uint8).copy(), triangle_count=n)
+
+
+def trailing_subtree_scene(first, second):
+    """first's buffers with second's whole tree appended after the root's
+    subtree: a valid upload (every node in preorder, every leaf's triangle in
+    the buffers) whose trailing nodes the reference's DFS never reaches
+    (compute_dynamic_ray.comp:185-210 starts at node 0 and stops when its
+    stack is empty).  second's triangles follow first's in the vertex and
+    material buffers."""
+    n0 = len(first.flat_bvh_data) // 48
+    t0 = len(first.model_vertex_data) // 12
+    nodes = np.frombuffer(bytes(second.flat_bvh_data), np.uint8).copy().view(np.int32).reshape(-1, 12)
+    leaf = nodes[:, 9] < 0
+    nodes[leaf, 8] = nodes[leaf, 8] - t0                 # -(tri + 1) -> -(tri + t0 + 1)
+    nodes[~leaf, 8] += n0
+    nodes[~leaf, 9] += n0
+    return SimpleNamespace(
+        model_vertex_data=np.concatenate([np.asarray(first.model_vertex_data, np.float32).reshape(-1),
+                                          np.asarray(second.model_vertex_data, np.float32).reshape(-1)]),
+        model_material_data=np.concatenate([np.asarray(first.model_material_data, np.float32).reshape(-1),
+                                            np.asarray(second.model_material_data, np.float32).reshape(-1)]),
+        flat_bvh_data=np.concatenate([np.frombuffer(bytes(first.flat_bvh_data), np.uint8),
+                                      nodes.view(np.uint8).reshape(-1)]),
+        triangle_count=first.triangle_count + second.triangle_count)

@@ -1,5 +1,14 @@
 """GPU parity: the HIP path through the C ABI vs the CPU oracle (oracle/rt_oracle.c).
 
+Every test runs on both walks (round 6, verdict r05 next #1): the library's
+default, option accel 8 (the SAH tree in 8 octant layouts),
+and the reference's own tree and order, accel 0.  On accel 8 the node
+visits and triangle tests are the accel walk's own and are checked against
+its CPU model (oracle/rt_accel_model.c over the same records); frames,
+segments and material reads against the reference-order oracle as on
+accel 0.  Tests that build their own contexts take the walk through
+RTAMD_ACCEL (read by rt_create).
+
 Bar: bit-exact RGBA8 and bit-exact float radiance (the sqrt'd colour before
 quantisation), and identical work counters (segments, BVH node visits,
 triangle tests, material reads), on the same buffers and camera.  That is
@@ -14,9 +23,36 @@ import numpy as np
 import pytest
 
 from conftest import has_gpu
-from raw_bvh import raw_bvh_scene
+from raw_bvh import raw_bvh_scene, trailing_subtree_scene
 
 pytestmark = pytest.mark.gpu
+
+WALKS = (8, 0)                      # accel layouts: the default walk, then the reference's
+_MODE = {"accel": 0}                # the walk the module's renderer runs (fixture below)
+
+
+@pytest.fixture(scope="module", params=WALKS, ids=lambda a: f"accel{a}")
+def renderer(request):
+    """One context per walk for the module (overrides conftest's)."""
+    if not has_gpu():
+        pytest.skip("no GPU")
+    import rtamd
+    r = rtamd.Renderer((0,))
+    r.set_option("accel", request.param)
+    _MODE["accel"] = request.param
+    for k, v in _defaults().items():
+        r.set_option(k, v)
+    yield r
+    r.close()
+
+
+def _defaults():
+    """The schedule each test restores: the library's, except the reference
+    tree's cooperative tail (coop_lanes 1) pinned as before."""
+    d = dict(DEFAULT_OPTS)
+    if _MODE["accel"]:
+        d["coop_lanes"] = -1        # the library default: no cooperative tail on the accel tree
+    return d
 
 COUNTERS = ("segments", "node_visits", "tri_tests", "mat_reads")
 DEFAULT_OPTS = {"wave_tile": -1, "coop_lanes": 1, "walk": 2, "coop_walk": 0,
@@ -26,10 +62,26 @@ DEFAULT_OPTS = {"wave_tile": -1, "coop_lanes": 1, "walk": 2, "coop_walk": 0,
                 "order_frames": 0, "learn_device": 1}
 
 
-def _oracle(built, cam_bytes, w, h, b, **kw):
+def _oracle(built, cam_bytes, w, h, b, accel=None, **kw):
+    """The reference-order oracle's frame and counts.  On the accel walk the
+    node visits and triangle tests come from its CPU model over the same
+    records (dropped where the model does not run: the extensions)."""
     from oracle import oracle_lib
-    return oracle_lib.render(built.model_vertex_data, built.model_material_data, built.flat_bvh_data,
-                             cam_bytes, w, h, b, **kw)
+    from rtamd import _lib
+    ref = oracle_lib.render(built.model_vertex_data, built.model_material_data, built.flat_bvh_data,
+                            cam_bytes, w, h, b, **kw)
+    nl = _MODE["accel"] if accel is None else accel
+    if not nl:
+        return ref
+    cnt = {k: v for k, v in ref[2].items() if k not in ("node_visits", "tri_tests")}
+    if not (kw.get("ext") or kw.get("spheres") is not None or kw.get("accum") is not None):
+        rec, info = _lib.accel_records(built, nl)
+        if not info["n_layouts"]:                   # past the slot cap: the reference's tree (its counts)
+            return ref
+        m = oracle_lib.render_accel(built.model_vertex_data, built.model_material_data, built.flat_bvh_data,
+                                    cam_bytes, w, h, b, rec, info, tile=kw.get("tile"), row_step=kw.get("row_step", 1))
+        cnt["node_visits"], cnt["tri_tests"] = m[2]["node_visits"], m[2]["tri_tests"]
+    return ref[0], ref[1], cnt
 
 
 def _assert_same(rgba, rad, st, ref_rgba, ref_rad, ref_cnt):
@@ -40,7 +92,8 @@ def _assert_same(rgba, rad, st, ref_rgba, ref_rad, ref_cnt):
         assert np.array_equal(rad.view(np.uint32), ref_rad.view(np.uint32)), "radiance bits differ"
     if st is not None:
         for k in COUNTERS:
-            assert st[k] == ref_cnt[k], (k, st[k], ref_cnt[k])
+            if k in ref_cnt:
+                assert st[k] == ref_cnt[k], (k, st[k], ref_cnt[k])
 
 
 def _full_frame(renderer, cfg, max_bounces=None):
@@ -112,8 +165,11 @@ def test_config5_1m_row_subset(renderer):
     renderer.upload_scene(built)
     info = renderer.scene_info()
     assert info["n_tris"] == built.triangle_count
-    assert renderer.get_option("coop_window_used") == 32      # ~100 MB of walk records: 32-slot windows
-    assert renderer.get_option("leaf_align_used") == 1        # and aligned leaf records
+    if _MODE["accel"]:
+        assert renderer.get_option("accel_used") == 8         # 8 layouts of ~92 MB
+    else:
+        assert renderer.get_option("coop_window_used") == 32  # ~100 MB of walk records: 32-slot windows
+        assert renderer.get_option("leaf_align_used") == 1    # and aligned leaf records
     rgba, rad, st = _bands_device(renderer, cam, cfg.width, cfg.height, cfg.max_bounces, 1, 64, 5)
     ref = _oracle(built, cam.ubo_bytes(), cfg.width, cfg.height, cfg.max_bounces,
                   tile=(0, 5, cfg.width, cfg.height - 5), row_step=64)
@@ -164,7 +220,7 @@ def test_schedules_identical(renderer, opts):
                       tile=(0, 1, cfg.width, cfg.height - 1), row_step=6)
         _assert_same(rgba, rad, st, *ref)
     finally:
-        for k, v in DEFAULT_OPTS.items():
+        for k, v in _defaults().items():
             renderer.set_option(k, v)
 
 
@@ -192,7 +248,7 @@ def test_heavy_first_order(renderer, heavy, heavy_stream):
                 rgba, rad, st = _bands_device(renderer, cam, cfg.width, cfg.height, cfg.max_bounces, 1, 9, 2)
                 _assert_same(rgba, rad, st, *ref)
     finally:
-        for k, v in DEFAULT_OPTS.items():
+        for k, v in _defaults().items():
             renderer.set_option(k, v)
 
 
@@ -226,12 +282,14 @@ def test_heavy_tiles_automatic_at_cap(renderer, concurrent, heavy_stream):
         n_cu = torch.cuda.get_device_properties(0).multi_processor_count
         cap = max(1, n_cu * 24 // 64 * renderer.get_option("heavy_cap") // 100 // concurrent)
         used = renderer.get_option("heavy_tiles_used")
-        if concurrent == 1:
+        if _MODE["accel"]:
+            assert used == 0                                # accel launches keep their heavy tiles in
+        elif concurrent == 1:
             assert used == cap
         else:   # four launches' bulk: fewer tiles outlast it, never more than the shared cap
             assert used <= cap
     finally:
-        for k, v in DEFAULT_OPTS.items():
+        for k, v in _defaults().items():
             renderer.set_option(k, v)
 
 
@@ -257,13 +315,13 @@ def test_heavy_pixels(renderer, cfg_k, factor):
         _assert_same(rgba, rad, None, *ref)
         rgba, rad, st = _bands_device(renderer, cam, cfg.width, cfg.height, cfg.max_bounces, cfg.height, 1, 0)
         _assert_same(rgba, rad, st, *ref)
-        assert renderer.get_option("heavy_pixels_used") > 0
+        assert (renderer.get_option("heavy_pixels_used") > 0) == (not _MODE["accel"])
         assert renderer.get_option("heavy_tiles_used") == 0
         rgba, rad, _ = _bands_device(renderer, cam, cfg.width, cfg.height, cfg.max_bounces, cfg.height, 1, 0,
                                      stats=False)                       # a plain launch in the learned order
         _assert_same(rgba, rad, None, *ref)
     finally:
-        for k, v in DEFAULT_OPTS.items():
+        for k, v in _defaults().items():
             renderer.set_option(k, v)
 
 
@@ -274,7 +332,11 @@ def test_bench_setting_whole_frame(renderer, cfg_k, walk):
     schedule with 4 launches in flight counted by the heavy-pixel bar
     (concurrent_launches 4).  The learning launch, then the production kernel
     (no counters) in the learned order, then a counting launch: each frame
-    equals the oracle's whole frame, and the counters its counts."""
+    equals the oracle's whole frame, and the counters its counts.  (The accel
+    walk's whole frames of configs 3-6: test_gpu_accel.py
+    test_accel_bench_setting_whole_frame.)"""
+    if _MODE["accel"]:
+        pytest.skip("accel 8: test_gpu_accel.test_accel_bench_setting_whole_frame")
     from rtamd import configs
     try:
         renderer.set_option("concurrent_launches", 4)
@@ -290,7 +352,7 @@ def test_bench_setting_whole_frame(renderer, cfg_k, walk):
             _assert_same(rgba, rad, st if stats else None, *ref)
         assert st["pixels"] == cfg.width * cfg.height
     finally:
-        for k, v in DEFAULT_OPTS.items():
+        for k, v in _defaults().items():
             renderer.set_option(k, v)
 
 
@@ -314,6 +376,9 @@ def test_moving_camera_reuses_order(renderer):
         used.append(renderer.get_option("heavy_pixels_used"))
         ref = _oracle(built, cam.ubo_bytes(), W, H, B, row_step=16)
         _assert_same(rgba[::16], rad[::16], None, *ref)
+    if _MODE["accel"]:
+        assert used == [0] * len(seq)             # accel launches trace their heavy pixels in their tiles
+        return
     assert used[0] == 0                           # the learning launch itself runs without an order
     assert used[1] > 0                            # camera 0's own order
     assert used[2] == used[1] and used[3] == used[1]   # moving: camera 0's order reused, no learning
@@ -434,16 +499,19 @@ def test_multi_device_context_interleaves(renderer):
     renderer.upload_scene(built)
     ref, ref_rad, ref_st = renderer.render(cam, cfg.width, cfg.height, cfg.max_bounces, radiance=True, stats=True)
     with rtamd.Renderer((0, 0)) as r2:
+        r2.set_option("accel", _MODE["accel"])
         r2.upload_scene(built)
+        assert r2.get_option("accel_used") == _MODE["accel"]
         rgba, rad, st = r2.render(cam, cfg.width, cfg.height, cfg.max_bounces, radiance=True, stats=True)
     assert np.array_equal(rgba, ref) and np.array_equal(rad, ref_rad)
     for k in COUNTERS:
         assert st[k] == ref_st[k]
 
 
+@pytest.mark.parametrize("accel", WALKS)
 @pytest.mark.parametrize("devices,slots", [((0,), 2), ((0, 0), 2), ((0,), 4), ((0, 0), 3), ((0,), 8)])
 @pytest.mark.parametrize("copies,depth", [(1, 1), (2, 1), (1, 2)])
-def test_render_async_matches_sync(devices, slots, copies, depth):
+def test_render_async_matches_sync(devices, slots, copies, depth, accel, monkeypatch):
     """rt_render_async (option async_slots frame slots, each tracing on its own
     stream; one copy stream, or a one-device frame's two halves on two (option
     copy_streams); strided band readback) gives rt_render's frames,
@@ -458,6 +526,7 @@ def test_render_async_matches_sync(devices, slots, copies, depth):
     cfg = configs.config2()
     built = cfg.build()
     w, h, b = 333, 201, 3            # 201 rows: a partial last 16-row band
+    monkeypatch.setenv("RTAMD_ACCEL", str(accel))
     r = rtamd.Renderer(devices)
     q = slots * depth                # host frames pending (depth 2: a slot's next trace overlaps its last readback)
     frames = [PinnedFrame(h, w) for _ in range(q)]
@@ -467,6 +536,7 @@ def test_render_async_matches_sync(devices, slots, copies, depth):
         r.set_option("copy_streams", copies)
         assert r.get_option("copy_streams") == copies
         r.upload_scene(built)
+        assert r.get_option("accel_used") == accel
         cams = [rtamd.Camera((-25.0 + 7 * k, 30.0, 140.0 - 9 * k), (0.0, 0.0, 0.0), (0.0, 1.0, 0.0), 20.0, w / h)
                 for k in range(2 * q + 3)]
         refs = [r.render(c, w, h, b)[0] for c in cams]
@@ -492,10 +562,12 @@ def test_render_async_matches_sync(devices, slots, copies, depth):
             f.close()
 
 
-def test_hip_engine_publishes_frames():
+@pytest.mark.parametrize("accel", WALKS)
+def test_hip_engine_publishes_frames(accel, monkeypatch):
     """HipEngine mirrors VulkanEngine: submit scene + camera, frames appear in the slot."""
     if not has_gpu():
         pytest.skip("no GPU")
+    monkeypatch.setenv("RTAMD_ACCEL", str(accel))
     import time
     import rtamd
     from rtamd import configs
@@ -516,7 +588,7 @@ def test_hip_engine_publishes_frames():
     assert eng.error is None, eng.error
     frame = slot.get_and_set(None)
     assert frame is not None and frame.pixel_data.shape == (180, 320, 4)
-    ref = _oracle(built, cam.ubo_bytes(), 320, 180, 3)[0]
+    ref = _oracle(built, cam.ubo_bytes(), 320, 180, 3, accel=0)[0]
     assert np.array_equal(frame.pixel_data, ref)
 
 
@@ -534,7 +606,7 @@ def test_golden_frames_on_gpu(renderer):
         rgba, rad, st = renderer.render(cam, g["width"], g["height"], g["max_bounces"], radiance=True, stats=True)
         assert hashlib.sha256(rgba.tobytes()).hexdigest() == g["rgba_sha256"], name
         assert hashlib.sha256(rad.tobytes()).hexdigest() == g["radiance_sha256"], name
-        for k in COUNTERS:
+        for k in COUNTERS if not _MODE["accel"] else ("segments", "mat_reads"):   # accel: its own walk
             assert st[k] == g["counts"][k], (name, k)
 
 
@@ -560,7 +632,7 @@ def test_unbalanced_bvh(renderer, shape, n, walk):
             _assert_same(rgba, rad, st, *_oracle(built, cam.ubo_bytes(), w, h, b))
             assert st["tri_tests"] > 0
     finally:
-        for k, v in DEFAULT_OPTS.items():
+        for k, v in _defaults().items():
             renderer.set_option(k, v)
 
 
@@ -585,10 +657,12 @@ def test_extensions_bit_exact(renderer, ext, sky):
     _assert_same(rgba, rad, st, *_oracle(built, cam.ubo_bytes(), w, h, b))
 
 
+@pytest.mark.parametrize("accel", WALKS)
 @pytest.mark.parametrize("devices", [(0,), (0, 0)])
-def test_accumulation_bit_exact(devices):
+def test_accumulation_bit_exact(devices, accel, monkeypatch):
     if not has_gpu():
         pytest.skip("no GPU")
+    monkeypatch.setenv("RTAMD_ACCEL", str(accel))
     import rtamd
     from test_oracle_kat import _ext_scene
     from rtamd import configs
@@ -635,7 +709,7 @@ def test_spheres_bit_exact(renderer, ext, sky, walk):
     finally:
         renderer.set_option("extensions", 0)
         renderer.upload_spheres(np.zeros((0, 8), np.float32))
-        for k, v in DEFAULT_OPTS.items():
+        for k, v in _defaults().items():
             renderer.set_option(k, v)
 
 
@@ -751,7 +825,7 @@ def test_batch_band_list_bit_exact(renderer, cfg_k, band_h, world, rw, rank, opt
                     assert st[k] == tot[k], (k, st[k], tot[k])
                 assert st["pixels"] == 3 * len(rows) * W
     finally:
-        for k, v in DEFAULT_OPTS.items():
+        for k, v in _defaults().items():
             renderer.set_option(k, v)
 
 
@@ -854,7 +928,7 @@ def test_batch_lists_pieces_bit_exact(renderer, cfg_k, world, rank, n):
                 if n == world:
                     assert sd["pixels"] == H * W                    # every piece once: one frame's worth
     finally:
-        for k, v in DEFAULT_OPTS.items():
+        for k, v in _defaults().items():
             renderer.set_option(k, v)
     bad = np.array([[1, 0] + [-1] * (plan.n_per - 2)], np.int32)
     with pytest.raises(RtError, match="INVALID_ARG"):
@@ -863,8 +937,9 @@ def test_batch_lists_pieces_bit_exact(renderer, cfg_k, world, rank, n):
                                              None, None, None, None))
 
 
+@pytest.mark.parametrize("accel", WALKS)
 @pytest.mark.parametrize("slots,toggle", [(4, False), (3, True)])
-def test_render_async_accumulation_and_copy_toggle(slots, toggle):
+def test_render_async_accumulation_and_copy_toggle(slots, toggle, accel, monkeypatch):
     """rt_render_async with the accumulation extension (per-device running
     sums that every frame reads and writes): with `slots` frames in flight the
     frames still reach the sums in frame_count order (the runtime serialises
@@ -884,6 +959,7 @@ def test_render_async_accumulation_and_copy_toggle(slots, toggle):
     built = _ext_scene()
     w, h, b = 150, 97, 4
     n = 2 * slots + 1
+    monkeypatch.setenv("RTAMD_ACCEL", str(accel))
     r = rtamd.Renderer((0,))
     frames = [PinnedFrame(h, w) for _ in range(n)]
     try:
@@ -909,3 +985,45 @@ def test_render_async_accumulation_and_copy_toggle(slots, toggle):
         r.close()
         for fr in frames:
             fr.close()
+
+
+def test_trailing_subtree_ignored(renderer):
+    """A valid upload with a second tree appended past the root's subtree:
+    the reference's DFS never reaches it, and neither walk may (the accel
+    records once held its triangles: advisor finding, round 5)."""
+    from rtamd import configs
+    built = trailing_subtree_scene(configs.config2().build(), raw_bvh_scene(40, "random", seed=3))
+    renderer.upload_raw(built.model_vertex_data.tobytes(), built.model_material_data.tobytes(),
+                        built.flat_bvh_data.tobytes())
+    assert renderer.get_option("accel_used") == _MODE["accel"]
+    for (w, h, b) in [(160, 90, 4), (37, 23, 10)]:
+        cam = configs.Camera.default(w, h)
+        rgba, rad, st = renderer.render(cam, w, h, b, radiance=True, stats=True)
+        _assert_same(rgba, rad, st, *_oracle(built, cam.ubo_bytes(), w, h, b))
+
+
+@pytest.mark.parametrize("extra,want", [(8, 8), (7, 1), (-1, 0)])
+def test_capacity_fallback(renderer, monkeypatch, extra, want):
+    """Past the accel records' slot cap the upload falls back from 8 layouts
+    to 1, then to the reference's tree, and says so in accel_used; the frames
+    stay the oracle's.  The cap is lowered for the test (RTAMD_ACCEL_CAP_SLOTS,
+    read at each upload); the hardware cap is 2^27 - 4 slots."""
+    if not _MODE["accel"]:
+        pytest.skip("accel 0 has no accel records")
+    from rtamd import _lib, configs
+    cfg = configs.config2()
+    built = cfg.build()
+    slots = _lib.accel_records(built, 1)[1]["slots"]
+    cap = {8: 8 * slots + 8, 7: 8 * slots + 7, -1: slots + 7}[extra]
+    monkeypatch.setenv("RTAMD_ACCEL_CAP_SLOTS", str(cap))
+    try:
+        renderer.upload_scene(built)
+        assert renderer.get_option("accel_used") == want
+        w, h, b = 320, 180, 4
+        cam = configs.Camera.default(w, h)
+        rgba, rad, st = renderer.render(cam, w, h, b, radiance=True, stats=True)
+        _assert_same(rgba, rad, st, *_oracle(built, cam.ubo_bytes(), w, h, b))
+    finally:
+        monkeypatch.delenv("RTAMD_ACCEL_CAP_SLOTS")
+        renderer.upload_scene(built)
+        assert renderer.get_option("accel_used") == 8

@@ -61,7 +61,7 @@ pmc() {  # pmc CONFIG NAME [SUFFIX EXTRA_BENCH_ARGS]
   PMC_PASSES="A C" BENCH_ARGS="--config $c $extra" bash tools/pmc.sh "${TAG}_pmc$c$sfx" || exit $?
   cp -r "gpurun_out/${TAG}_pmc$c$sfx" "$OUT/pmc$c$sfx"
   python3 tools/pmc_traffic.py "gpurun_out/${TAG}_pmc$c$sfx" "trace_simple<false, false" --config "$name" \
-      --source "profiles/r05/$TAG/pmc$c$sfx (tools/pmc.sh passes A and C, bench.py --config $c $extra)" \
+      --source "profiles/r06/$TAG/pmc$c$sfx (tools/pmc.sh passes A and C, bench.py --config $c $extra)" \
       --merge "$OUT/pmc_latest.json" > "$OUT/pmc$c$sfx.json" 2>> "$OUT/status.txt" || status "pmc_traffic cfg$c$sfx failed"
   cp "$OUT/pmc_latest.json" profiles/pmc_latest.json
 }
