@@ -47,6 +47,10 @@ def lib(envelope: bool = False, accel: bool = False) -> C.CDLL:
             _accel_lib.orc_accel_format.argtypes = [C.c_int]
             _accel_lib.orc_accel_fallbacks.restype = C.c_uint64
             _accel_lib.orc_accel_margin.argtypes = [C.c_float, C.c_float]
+            _accel_lib.orc_accel_audit.argtypes = [C.c_int]
+            _accel_lib.orc_accel_audit_get.argtypes = [C.POINTER(C.c_double)]
+            _accel_lib.orc_accel_audit_bins.argtypes = [C.POINTER(C.c_double), C.POINTER(C.c_double),
+                                                        C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
         return _accel_lib
     if envelope:
         if _env_lib is None:
@@ -160,6 +164,33 @@ def render_accel(vertices, materials, nodes, camera_ubo: bytes, width: int, heig
     if profile:
         return rgba, rad, cd, prof
     return rgba, rad, cd
+
+
+def accel_audit(on: bool = True) -> None:
+    """Starts (or stops) the accel model's margin audit (rt_accel_model.c
+    orc_accel_audit): every following render_accel segment is first walked
+    exhaustively for the reference's candidate hit i* and its box."""
+    lib(accel=True).orc_accel_audit(1 if on else 0)
+
+
+def accel_audit_result() -> dict:
+    """The audit since accel_audit(): segments with a hit, of them hits before
+    their own box's t_enter, headroom > 0.5 of the margin, unsafe (the margin
+    test fails: the exactness argument does not cover the segment), the
+    largest headroom (te* - t*) / (t* 2^-10 + 2^-10), and the hits on
+    near-degenerate triangles (|det| <= 1e-4, compute_dynamic_ray.comp:110 cuts
+    at 1e-5) with their largest headroom."""
+    out = (C.c_double * 7)()
+    lib(accel=True).orc_accel_audit_get(out)
+    sh, gr = (C.c_double * 32)(), (C.c_double * 32)()
+    shn, grn = (C.c_uint64 * 32)(), (C.c_uint64 * 32)()
+    lib(accel=True).orc_accel_audit_bins(sh, gr, shn, grn)
+
+    def bins(mx, n):      # bin k: x in (2^-(k+1), 2^-k]; only the bins with hits
+        return {str(k): [int(n[k]), float(mx[k])] for k in range(32) if n[k]}
+    return {"hits": int(out[0]), "before_box": int(out[1]), "over_half": int(out[2]), "unsafe": int(out[3]),
+            "max_headroom": float(out[4]), "sliver_hits": int(out[5]), "sliver_max_headroom": float(out[6]),
+            "by_shape": bins(sh, shn), "by_grazing": bins(gr, grn)}
 
 
 def render_profile(vertices, materials, nodes, camera_ubo: bytes, width: int, height: int, max_bounces: int,

@@ -107,9 +107,161 @@ static float half_down(float x) {           /* the largest half-precision value 
 }
 static float half_up(float x) { return -half_down(-x); }
 
+/* Audit (orc_accel_audit; tools/accel_adversarial.py, tests/test_accel_model.py).
+ * Before each segment's walk, an exhaustive walk of the same layout enters
+ * every box the ray's line crosses in front (the slab test without the
+ * closest_t compare) and tests every triangle in them: i* = the lowest
+ * (t, flattened index), te* = the t_enter of i*'s own leaf box.  The accel
+ * walk returns the reference's hit whenever te* <= t* (1 + 2^-10) + 2^-10
+ * (i*'s leaf and all its ancestors are entered; a t* before
+ * te* takes the fallback).  The audit records, per segment with a hit, the
+ * share of that margin i* consumes, headroom = (te* - t*) / (t* 2^-10 +
+ * 2^-10): <= 0 for a hit inside its box, in (0, 1] where only the margin
+ * keeps the box entered, > 1 where the argument fails (unsafe). */
+static int g_audit = 0;
+static double g_audit_max = -INFINITY;
+static uint64_t g_audit_hits = 0, g_audit_incons = 0, g_audit_half = 0, g_audit_unsafe = 0;
+static uint64_t g_audit_sliver = 0;         /* hits on i* with |det| <= 1e-4 (the 1e-5 cut's decade, :110) */
+static double g_audit_sliver_max = -INFINITY;
+/* max headroom of the hits binned by floor(-log2 x) (bin 31: x <= 2^-31):
+ * x = sin of the triangle's angle at v0, |e1 x e2| / (|e1| |e2|) (the shape
+ * Moeller-Trumbore's arithmetic is anchored at), and x = |cos| of the ray to
+ * the triangle's normal, |det| / (|e1 x e2| |d|) (grazing) */
+static double g_audit_shape[32], g_audit_graze[32];
+static uint64_t g_audit_shape_n[32], g_audit_graze_n[32];
+
+static int audit_bin(double x) {
+    if (!(x > 0.0)) return 31;
+    const int b = (int)floor(-log2(x));
+    return b < 0 ? 0 : (b > 31 ? 31 : b);
+}
+
+/* the per-bin maxima (32 doubles each; -inf: no hit in the bin) and counts */
+int orc_accel_audit_bins(double shape[32], double graze[32], uint64_t shape_n[32], uint64_t graze_n[32]) {
+    for (int k = 0; k < 32; ++k) {
+        shape[k] = g_audit_shape[k];
+        graze[k] = g_audit_graze[k];
+        shape_n[k] = g_audit_shape_n[k];
+        graze_n[k] = g_audit_graze_n[k];
+    }
+    return 0;
+}
+
+int orc_accel_audit(int on) {
+    g_audit = on;
+    g_audit_max = -INFINITY;
+    g_audit_hits = g_audit_incons = g_audit_half = g_audit_unsafe = g_audit_sliver = 0;
+    g_audit_sliver_max = -INFINITY;
+    for (int k = 0; k < 32; ++k) {
+        g_audit_shape[k] = g_audit_graze[k] = -INFINITY;
+        g_audit_shape_n[k] = g_audit_graze_n[k] = 0;
+    }
+    return 0;
+}
+
+/* {segments with a hit, of them t* < te*, headroom > 0.5, unsafe (the
+ * margin test fails), max headroom, hits with |det| <= 1e-4, their max
+ * headroom} since orc_accel_audit. */
+int orc_accel_audit_get(double out[7]) {
+    out[0] = (double)g_audit_hits;
+    out[1] = (double)g_audit_incons;
+    out[2] = (double)g_audit_half;
+    out[3] = (double)g_audit_unsafe;
+    out[4] = g_audit_max;
+    out[5] = (double)g_audit_sliver;
+    out[6] = g_audit_sliver_max;
+    return 0;
+}
+
+static void audit_segment(const scene* s, ray r) {
+    const int oct = g_layouts == 8 ? ((signbit(r.dir.x) ? 1 : 0) | (signbit(r.dir.y) ? 2 : 0) |
+                                      (signbit(r.dir.z) ? 4 : 0)) : 0;
+    size_t n = (size_t)oct * (size_t)g_slots;
+    const size_t end = n + (size_t)g_slots;
+    const size_t WS = g_fmt ? 4 : 8;
+    int leaf = g_root_leaf;
+    const vec3 inv = v3(rcp(r.dir.x), rcp(r.dir.y), rcp(r.dir.z));
+    float best_t = INFINITY, best_te = 0.0f;
+    int best = -1;
+    while (n < end) {
+        const uint32_t aw = g_rec[WS * n + 3], bw = g_fmt ? 0u : g_rec[8 * n + 7];
+        vec3 blo, bhi;
+        if (g_fmt && !leaf) {
+            const uint32_t* w = &g_rec[4 * n];
+            blo = v3(half_to_float(w[0] & 0xFFFFu), half_to_float(w[0] >> 16), half_to_float(w[1] & 0xFFFFu));
+            bhi = v3(half_to_float(w[1] >> 16), half_to_float(w[2] & 0xFFFFu), half_to_float(w[2] >> 16));
+        } else {
+            blo = v3(rec_f(n, 0), rec_f(n, 1), rec_f(n, 2));
+            bhi = v3(rec_f(n, 4), rec_f(n, 5), rec_f(n, 6));
+        }
+        const vec3 t0s = mul3(sub3(blo, r.origin), inv);
+        const vec3 t1s = mul3(sub3(bhi, r.origin), inv);
+        const float te = fmaxf(fmaxf(fminf(t0s.x, t1s.x), fminf(t0s.y, t1s.y)), fminf(t0s.z, t1s.z));
+        const float tx = fminf(fminf(fmaxf(t0s.x, t1s.x), fmaxf(t0s.y, t1s.y)), fmaxf(t0s.z, t1s.z));
+        const int hb = tx > te && tx > T_MIN;
+        if (hb && leaf) {
+            const int tri = (int)(aw & 0x1FFFFFFFu);
+            vec3 nrm;
+            float t = INFINITY;
+            if ((size_t)tri < s->n_tris &&
+                hit_triangle(r, vertex_pos(s, (size_t)tri * 3 + 0), vertex_pos(s, (size_t)tri * 3 + 1),
+                             vertex_pos(s, (size_t)tri * 3 + 2), &t, &nrm) &&
+                (t < best_t || (t == best_t && tri < best))) {
+                best_t = t;
+                best = tri;
+                best_te = te;
+            }
+        }
+        if (leaf) {
+            n += g_fmt ? 4 : 2;
+            leaf = (int)(aw >> 31);
+        } else if (hb) {
+            n += 1;
+            leaf = g_fmt ? (int)((aw >> 30) & 1u) : (int)(bw & 1u);
+        } else {
+            n = aw & (g_fmt ? 0x3FFFFFFFu : 0x7FFFFFFFu);
+            leaf = (int)(aw >> 31);
+        }
+    }
+    if (best < 0) return;
+    const double room = (double)best_t * (1.0 / 1024.0) + 1.0 / 1024.0;
+    const double head = ((double)best_te - (double)best_t) / room;
+    const int unsafe = !(best_te <= best_t * g_relax + g_relax_abs);
+    const vec3 v0 = vertex_pos(s, (size_t)best * 3 + 0);
+    const float det = dot3(sub3(vertex_pos(s, (size_t)best * 3 + 1), v0), cross3(r.dir, sub3(vertex_pos(s,
+                           (size_t)best * 3 + 2), v0)));
+    const int sliver = det >= -1e-4f && det <= 1e-4f;
+    const vec3 e1 = sub3(vertex_pos(s, (size_t)best * 3 + 1), v0), e2 = sub3(vertex_pos(s, (size_t)best * 3 + 2), v0);
+    const double cx = (double)e1.y * e2.z - (double)e1.z * e2.y, cy = (double)e1.z * e2.x - (double)e1.x * e2.z,
+                 cz = (double)e1.x * e2.y - (double)e1.y * e2.x;
+    const double cn = sqrt(cx * cx + cy * cy + cz * cz);
+    const double l1 = sqrt((double)e1.x * e1.x + (double)e1.y * e1.y + (double)e1.z * e1.z);
+    const double l2 = sqrt((double)e2.x * e2.x + (double)e2.y * e2.y + (double)e2.z * e2.z);
+    const double ld = sqrt((double)r.dir.x * r.dir.x + (double)r.dir.y * r.dir.y + (double)r.dir.z * r.dir.z);
+    const int bs = audit_bin(cn / (l1 * l2));
+    const int bg = audit_bin(fabs(((double)r.dir.x * cx + (double)r.dir.y * cy + (double)r.dir.z * cz) / (cn * ld)));
+#ifdef _OPENMP
+#pragma omp critical(orc_audit)
+#endif
+    {
+        g_audit_hits++;
+        g_audit_incons += best_t < best_te;
+        g_audit_half += head > 0.5;
+        g_audit_unsafe += (uint64_t)unsafe;
+        if (head > g_audit_max) g_audit_max = head;
+        g_audit_sliver += (uint64_t)sliver;
+        if (sliver && head > g_audit_sliver_max) g_audit_sliver_max = head;
+        g_audit_shape_n[bs]++;
+        g_audit_graze_n[bg]++;
+        if (head > g_audit_shape[bs]) g_audit_shape[bs] = head;
+        if (head > g_audit_graze[bg]) g_audit_graze[bg] = head;
+    }
+}
+
 static int accel_walk(const scene* s, ray r, float* closest_t, int* hit_index, vec3* hit_normal,
                       orc_counts* cnt) {
     if (g_slots == 0) return 0;                 /* empty scene: every ray misses */
+    if (g_audit) audit_segment(s, r);
     const int oct = g_layouts == 8 ? ((signbit(r.dir.x) ? 1 : 0) | (signbit(r.dir.y) ? 2 : 0) |
                                       (signbit(r.dir.z) ? 4 : 0)) : 0;
     size_t n = (size_t)oct * (size_t)g_slots;
