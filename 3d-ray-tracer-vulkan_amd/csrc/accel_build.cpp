@@ -42,6 +42,7 @@ struct Prim {
     float lo[3], hi[3];
     float c[3];       // box centroid
     int tri;          // flattened triangle index
+    int cls;          // shape class (accel_class)
 };
 
 struct BNode {
@@ -50,6 +51,7 @@ struct BNode {
     int prim = -1;    // >= 0: a leaf of this primitive
     int m = 0;        // primitives in the subtree
     int left = -1, right = -1;   // node ids (internal): lower-centroid side first
+    int cls = 0;      // the largest shape class in the subtree
 };
 
 float area(const float lo[3], const float hi[3]) {
@@ -97,6 +99,7 @@ struct Builder {
             }
         if (m == 1) {
             nd.prim = ord[0][b];
+            nd.cls = prims[nd.prim].cls;
             return 0;
         }
         int baxis = 0, bpos = m / 2;
@@ -168,6 +171,7 @@ struct Builder {
             dl = build(id + 1, b, mid, 1, level + 1);
             dr = build(id + 2 * ml, mid, e, 1, level + 1);
         }
+        nd.cls = std::max(nodes[id + 1].cls, nodes[id + 2 * ml].cls);
         return 1 + std::max(dl, dr);
     }
 };
@@ -180,6 +184,22 @@ uint64_t fnv(const unsigned char* p, size_t n, uint64_t h) {
 void put_f(uint32_t* w, float f) { std::memcpy(w, &f, 4); }
 
 }  // namespace
+
+int accel_class(const float e1[3], const float e2[3]) {
+    const double a[3] = {e1[0], e1[1], e1[2]}, b[3] = {e2[0], e2[1], e2[2]};
+    const double c[3] = {a[1] * b[2] - a[2] * b[1], a[2] * b[0] - a[0] * b[2], a[0] * b[1] - a[1] * b[0]};
+    const double s = std::sqrt(c[0] * c[0] + c[1] * c[1] + c[2] * c[2]) /
+                     (std::sqrt(a[0] * a[0] + a[1] * a[1] + a[2] * a[2]) * std::sqrt(b[0] * b[0] + b[1] * b[1] + b[2] * b[2]));
+    if (!(s > 0.0)) return 31;                        // a zero edge or parallel edges (never hit: det = 0)
+    const int k = (int)std::floor(-std::log2(s));
+    return k < 0 ? 0 : (k > 31 ? 31 : k);
+}
+
+float accel_relax(int cls) {
+    if (cls < kAccelClassMin) return 1.0f + 1.0f / 1024.0f;
+    // 1 + 2^(cls - 16), rounded up to a float (exact for every class in 7..31)
+    return 1.0f + std::ldexp(1.0f, cls - 16);
+}
 
 uint16_t half_bits_down(float x) {
     if (std::isnan(x)) return 0x7E00u;
@@ -287,6 +307,14 @@ int accel_build(const void* vertices, size_t vertex_bytes, const void* materials
             p.c[q] = 0.5f * (p.lo[q] + p.hi[q]);
         }
         p.tri = occ[i].tri;
+        {
+            const unsigned char* v = vb + (size_t)p.tri * 48;
+            float x[9];
+            for (int j = 0; j < 3; ++j) std::memcpy(&x[3 * j], v + 16 * j, 12);
+            const float e1[3] = {x[3] - x[0], x[4] - x[1], x[5] - x[2]};
+            const float e2[3] = {x[6] - x[0], x[7] - x[1], x[8] - x[2]};
+            p.cls = accel_class(e1, e2);
+        }
         B.prims.push_back(p);
     }
     const int m = (int)B.prims.size();
@@ -323,6 +351,9 @@ int accel_build(const void* vertices, size_t vertex_bytes, const void* materials
     B.nodes.resize(2 * (size_t)m - 1);
     const unsigned hw = n_threads > 0 ? (unsigned)n_threads : std::max(1u, std::thread::hardware_concurrency());
     out->depth = B.build(0, 0, m, std::min(hw, 64u));
+    out->max_class = B.nodes[0].cls;
+    out->relax_max = accel_relax(B.nodes[0].cls);
+    for (const Prim& p : B.prims) out->n_thin += p.cls >= kAccelClassMin ? 1 : 0;
     ACCEL_T("tree built");
     {
         const float a0 = area(B.nodes[0].lo, B.nodes[0].hi);
@@ -366,7 +397,9 @@ int accel_build(const void* vertices, size_t vertex_bytes, const void* materials
                 // e1 = v1 - v0, e2 = v2 - v0, as hit_triangle computes them (:106-107)
                 const float e1[3] = {x[3] - x[0], x[4] - x[1], x[5] - x[2]};
                 const float e2[3] = {x[6] - x[0], x[7] - x[1], x[8] - x[2]};
-                w[3] = (uint32_t)p.tri | (1u << 30);            // | L(next) << 31, below
+                // | L(next) << 31, below; bit 29: a thin triangle (class >= kAccelClassMin), entered
+                // whenever the slab test passes, whatever closest_t
+                w[3] = (uint32_t)p.tri | (1u << 30) | (p.cls >= kAccelClassMin ? 1u << 29 : 0u);
                 put_f(&w[7], x[0]);
                 put_f(&w[8], x[1]);
                 put_f(&w[9], x[2]);
@@ -382,6 +415,10 @@ int accel_build(const void* vertices, size_t vertex_bytes, const void* materials
             const int first = neg ? nd.right : nd.left, second = neg ? nd.left : nd.right;
             const size_t skip = it.pos + (size_t)span(nd.m);
             w[3] = (uint32_t)skip;                                 // | L(skip) << 31, below
+            if (format == 0) {                                     // the subtree's margin; | L(first) below
+                const float r = accel_relax(nd.cls);
+                std::memcpy(&w[7], &r, 4);
+            }
             const size_t pos2 = it.pos + 1 + (size_t)span(B.nodes[first].m);
             st.push_back({second, pos2});
             st.push_back({first, it.pos + 1});
@@ -396,7 +433,7 @@ int accel_build(const void* vertices, size_t vertex_bytes, const void* materials
                 s += (size_t)LS;
             } else if (format == 0) {
                 w[3] |= L(w[3]) << 31;
-                w[7] = L(s + 1);
+                w[7] |= L(s + 1);                         // bit 0 of the margin: it only grows by an ulp
                 s += 1;
             } else {
                 w[3] |= L(w[3]) << 31 | L(s + 1) << 30;

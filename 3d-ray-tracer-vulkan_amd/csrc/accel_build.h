@@ -21,14 +21,18 @@
 //
 // Records: the walk-2 slot format of rt_internal.h (DevScene::walk), packed
 // (no pad slots): an internal node one 32-B slot, a leaf two (box, then its
-// triangle v0 / e1 / e2).  n_layouts copies of the tree in preorder, each with
+// triangle v0 / e1 / e2).  An internal node's word 7 is its margin factor R
+// (accel_relax of its subtree's largest shape class, a float whose bit 0 is
+// L(first child)); a leaf's bit 29 of word 3 marks a thin triangle (class >=
+// kAccelClassMin), entered whenever its slab test passes.  n_layouts copies of the tree in preorder, each with
 // its own child order: layout o puts first, at a node split on axis a, the
 // child on the side a ray with sign bit ((o >> a) & 1) on axis a reaches first
 // (n_layouts 1: always the lower child).  A ray walks the layout of its
 // direction's octant (sign bits of d.x, d.y, d.z), so the stackless skip walk
 // is a near-first ordered traversal.
 //
-// Format 1 ("half", option accel_half): 16-B slots.  An internal node is one
+// Format 1 ("half", option accel_half): 16-B slots (no room for R: every
+// internal node takes the tree's largest, relax_max).  An internal node is one
 // slot: its box in IEEE half precision rounded outward (lo down, hi up; words
 // 0-2 = lo.x | lo.y << 16, lo.z | hi.x << 16, hi.y | hi.z << 16) and word 3 =
 // skip | L(first child) << 30 | L(skip) << 31.  A leaf is four slots, the same
@@ -56,7 +60,26 @@ struct AccelHost {
     int n_inputs = 0;               // leaves of the reference tree
     int depth = 0;                  // deepest leaf (root = 0)
     double sah = 0.0;               // SAH cost of the tree (internal 1, leaf 1, relative to the root box area)
+    int max_class = 0;              // the largest shape class (accel_class) of the primitives
+    int n_thin = 0;                 // primitives of class >= kAccelClassMin
+    float relax_max = 0.0f;         // accel_relax(max_class): format 1's margin for every internal node
 };
+
+// The shape class of a triangle, floor(-log2 sin(angle at v0)) in 0..31
+// (31: degenerate), sin = |e1 x e2| / (|e1| |e2|) in double from the float
+// edges hit_triangle computes (compute_dynamic_ray.comp:106-107).  Moeller-
+// Trumbore's t carries a relative error that grows as 1 / sin: the audit of
+// tools/accel_adversarial.py measured hits on needle triangles of class 16
+// whose rounded t lay 17 margins (2^-10 relative) before their own box's
+// t_enter, the case in which the accel walk could miss the reference's hit.
+constexpr int kAccelClassMin = 7;
+int accel_class(const float e1[3], const float e2[3]);
+// The margin factor R of a box whose subtree's largest class is cls: the walk
+// enters it when t_enter <= closest_t * R + 2^-10.  Class < 7: 1 + 2^-10;
+// else 1 + 2^(cls - 16) (class 16: 2, class 31: 32769), growing as the t error
+// does, 64x the error measured at class 16.  A leaf of class >= 7 (bit 29 of
+// its link word) is entered whenever its slab test passes (R = infinity).
+float accel_relax(int cls);
 
 // The layouts do not fit the slot cap (accel_build's return value).
 constexpr int kAccelTooBig = -2;

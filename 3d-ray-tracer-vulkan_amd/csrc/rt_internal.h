@@ -80,6 +80,7 @@ struct DevScene {
     int      layout_slots = 0;
     int      half = 0;          // accel format 1: 16-B slots, half-precision internal boxes (accel_build.h);
                                 //   layout_slots and end2 then count 16-B slots
+    float    relax_half = 0.0f;  // format 1: every internal node's margin factor (AccelHost::relax_max)
     float4*  walk_ref = nullptr;
     int      end2_ref = 0;
     int      ref_padded = 0;

@@ -1325,6 +1325,7 @@ int rt_upload_scene(rt_ctx* ctx, const void* vertices, size_t vertex_bytes,
             s.n_layouts = ah.n_layouts;
             s.layout_slots = ah.slots;
             s.half = ah.format;
+            s.relax_half = ah.relax_max;
             s.end = ah.slots;
             s.end2 = ah.n_layouts * ah.slots;
             s.root_leaf = ah.root_leaf;
@@ -2130,7 +2131,7 @@ int rt_unpack_rgb(const void* d_rgb, void* d_rgba, size_t n_px, void* stream) {
 
 int rt_accel_records(const void* vertices, size_t vertex_bytes, const void* materials, size_t material_bytes,
                      const void* bvh_nodes, size_t bvh_bytes, int n_layouts, uint32_t* out_words, size_t cap_words,
-                     size_t* n_words, int32_t info[6]) {
+                     size_t* n_words, int32_t info[8]) {
     HostScene hs;
     const char* err = nullptr;
     int rc = build_host_scene(vertices, vertex_bytes, materials, material_bytes, bvh_nodes, bvh_bytes, &hs, &err);
@@ -2149,7 +2150,7 @@ int rt_accel_records(const void* vertices, size_t vertex_bytes, const void* mate
     if (rc == kAccelTooBig) {                      // rt_upload_scene walks the reference's tree: no records
         if (n_words) *n_words = 0;
         if (info) {
-            for (int k = 0; k < 6; ++k) info[k] = 0;
+            for (int k = 0; k < 8; ++k) info[k] = 0;
         }
         return RT_OK;
     }
@@ -2161,6 +2162,7 @@ int rt_accel_records(const void* vertices, size_t vertex_bytes, const void* mate
     if (info) {
         info[0] = ah.n_layouts; info[1] = ah.slots; info[2] = ah.root_leaf;
         info[3] = ah.n_prims; info[4] = ah.n_inputs; info[5] = ah.depth;
+        info[6] = ah.max_class; info[7] = ah.n_thin;
     }
     if (out_words) std::memcpy(out_words, ah.rec.data(), std::min(cap_words, ah.rec.size()) * sizeof(uint32_t));
     return RT_OK;

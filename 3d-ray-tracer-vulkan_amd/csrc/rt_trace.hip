@@ -367,9 +367,25 @@ __device__ __forceinline__ float lane_f(float v, int k) {
 // t < closest_t, or on a tie with a lower flattened index (the reference
 // visits leaves in flattened-index order and keeps the first hit at a given
 // t).  oracle/rt_accel_model.c states the same arithmetic.
+//
+// Thin triangles (round 6; accel_build.h accel_class): Moeller-Trumbore's t
+// error grows as 1 / sin of the triangle's angle at v0, so a box whose
+// subtree holds a triangle of shape class c >= 7 carries its own factor R =
+// 1 + 2^(c - 16) in place of 1 + 2^-10 (an internal node's word 7, bit 0 of
+// which is L(first child)), and a thin leaf (bit 29 of its link word) is
+// entered whenever its slab test passes.  Nothing else changes: a larger
+// margin only enters more boxes.
 constexpr float kRelax = 1.0f + 1.0f / 1024.0f;
 constexpr float kRelaxAbs = 1.0f / 1024.0f;
+constexpr uint32_t kThinLeaf = 1u << 29;
 __device__ __forceinline__ bool accel_enter(float te, float closest) { return te <= closest * kRelax + kRelaxAbs; }
+// The margin factor of the record whose words 3 and 7 are aw and bw.
+__device__ __forceinline__ float accel_factor(bool leaf, uint32_t aw, uint32_t bw) {
+    return leaf ? ((aw & kThinLeaf) ? __builtin_inff() : kRelax) : __uint_as_float(bw);
+}
+__device__ __forceinline__ bool accel_enter_r(float te, float closest, float r) {
+    return te <= closest * r + kRelaxAbs;
+}
 __device__ __forceinline__ bool accel_take(float t, int tri, float closest, int hit) {
     return t < closest || (t == closest && tri < hit);
 }
@@ -474,7 +490,7 @@ __device__ __forceinline__ int coop_walk(const float4* __restrict__ walk, int en
         ++windows;
         const int j = n + lane;
         const bool ld = j < end && lane < WIN;
-        float te = 0.0f, tt = 0.0f;
+        float te = 0.0f, tt = 0.0f, rf = kRelax;
         int sk = 0, tri = -1;
         bool ind = false, tv = false, lf = false, pd = false;
         float4 A = make_float4(0.f, 0.f, 0.f, 0.f), B = A;
@@ -515,11 +531,12 @@ __device__ __forceinline__ int coop_walk(const float4* __restrict__ walk, int en
                 sk = lf ? j + 2 : (int)(aw & 0x7FFFFFFFu);
             }
             tri = (int)(aw & 0x1FFFFFFFu);
-            if (lf && ind && (ACC ? accel_enter(te, closest) : te < closest) && (!RT_COOP_DPP || lane < WIN - 1))
+            if (ACC) rf = accel_factor(lf, aw, __float_as_uint(B.w));
+            if (lf && ind && (ACC ? accel_enter_r(te, closest, rf) : te < closest) && (!RT_COOP_DPP || lane < WIN - 1))
                 tv = tri_test(make_float4(B.w, Q0.x, Q0.y, 0.f), make_float4(Q0.z, Q0.w, Q1.x, 0.f),
                               make_float4(Q1.y, Q1.z, Q1.w, 0.f), o, d, tt);
         }
-        uint64_t H = __ballot(ind && (ACC ? accel_enter(te, closest) : te < closest));
+        uint64_t H = __ballot(ind && (ACC ? accel_enter_r(te, closest, rf) : te < closest));
         uint64_t T = __ballot(tv && (ACC ? accel_take(tt, tri, closest, hit) : tt < closest));
         const uint64_t Lf = __ballot(lf);
         const uint64_t Pd = PAD ? __ballot(pd) : 0ull;              // a pad slot follows (leaf alignment)
@@ -536,7 +553,7 @@ __device__ __forceinline__ int coop_walk(const float4* __restrict__ walk, int en
                         closest = lane_f(tt, k);
                         hit = lane_i(tri, k);
                         if (ACC) incons = closest < lane_f(te, k);
-                        H = __ballot(ind && (ACC ? accel_enter(te, closest) : te < closest));
+                        H = __ballot(ind && (ACC ? accel_enter_r(te, closest, rf) : te < closest));
                         T = __ballot(tv && (ACC ? accel_take(tt, tri, closest, hit) : tt < closest));
                     }
                 }
@@ -1089,7 +1106,8 @@ void trace_simple(TraceArgs a) {
                     float te;
                     bool ind;
                     slab(lo, hi, o, inv, te, ind);
-                    const bool hb = ind && accel_enter(te, closest);
+                    const float rf = nleaf ? ((aw & kThinLeaf) ? __builtin_inff() : kRelax) : a.scene.relax_half;
+                    const bool hb = ind && accel_enter_r(te, closest, rf);
                     const int nxt = nleaf ? n + 4 : (hb ? n + 1 : (int)(aw & 0x3FFFFFFFu));
                     const bool nl = ((nleaf || !hb) ? (aw >> 31) : (aw >> 30)) & 1u;
                     const float v0x = B.w;                                   // a leaf's v0.x
@@ -1117,8 +1135,8 @@ void trace_simple(TraceArgs a) {
                     float te;
                     bool ind;
                     slab(A, B, o, inv, te, ind);
-                    const bool hb = ind && (ACC ? accel_enter(te, closest) : te < closest);
                     const uint32_t aw = __float_as_uint(A.w), bw = __float_as_uint(B.w);
+                    const bool hb = ind && (ACC ? accel_enter_r(te, closest, accel_factor(nleaf, aw, bw)) : te < closest);
                     // a leaf's next node is its successor, two slots on, whether it
                     // is hit or not (its skip); an internal node's left child is
                     // the next slot (one more past a pad slot: leaf bit 29 of word

@@ -26,7 +26,7 @@ RT_ERR = {
 }
 
 # Every symbol include/rtamd.h declares (checked by tests/test_abi.py).
-ABI_VERSION = 5           # include/rtamd.h RT_ABI_VERSION
+ABI_VERSION = 6           # include/rtamd.h RT_ABI_VERSION
 
 EXPORTED = (
     "rt_create", "rt_upload_scene", "rt_render", "rt_render_tile_device", "rt_destroy",
@@ -210,12 +210,12 @@ def accel_records(built, n_layouts: int = 8, half: bool = False):
     for b in bufs:
         args += [b.ctypes.data, b.nbytes]
     n = C.c_size_t(0)
-    info = (C.c_int32 * 6)()
+    info = (C.c_int32 * 8)()
     nl = n_layouts | (RT_ACCEL_FORMAT_HALF if half else 0)
     check(L.rt_accel_records(*args, nl, None, 0, C.byref(n), info))
     out = np.zeros(n.value, dtype=np.uint32)
     check(L.rt_accel_records(*args, nl, out.ctypes.data_as(C.POINTER(C.c_uint32)), out.size, C.byref(n), info))
-    keys = ("n_layouts", "slots", "root_leaf", "n_prims", "n_inputs", "depth")
+    keys = ("n_layouts", "slots", "root_leaf", "n_prims", "n_inputs", "depth", "max_class", "n_thin")
     d = dict(zip(keys, list(info)))
     d["format"] = 1 if half else 0
     return out, d

@@ -44,7 +44,7 @@ extern "C" {
  * calls' argument lists: bumped whenever one changes (round 4 moved
  * rt_stats.pixels to the end, SURVEY.md §8b's order).  A binding compiled
  * against another version must refuse the library (rt_abi_version). */
-#define RT_ABI_VERSION 5
+#define RT_ABI_VERSION 6
 
 typedef struct rt_ctx rt_ctx;
 
@@ -479,7 +479,8 @@ int rt_scene_validate(const void* vertices, size_t vertex_bytes,
  * *n_words = the words of the records (n_layouts * slots, + 64 B of padding);
  * info (nullable) receives {n_layouts, slots per layout, root is a leaf,
  * primitives after dropping byte-identical duplicates, reference leaves, tree
- * depth}.  Only the root's subtree counts (nodes past the root's skip are
+ * depth, the largest shape class, primitives of class >= 7 (thin: their
+ * boxes carry wider margins, "accel" above)}.  Only the root's subtree counts (nodes past the root's skip are
  * never visited by the reference).  The capacity fallback of rt_upload_scene
  * applies: 8 layouts past the slot cap are built as 1 (info[0] = 1), and a
  * scene too large for one layout gets no records (RT_OK, *n_words = 0, info
@@ -499,7 +500,7 @@ int rt_unpack_rgb(const void* d_rgb, void* d_rgba, size_t n_px, void* stream);
 int rt_accel_records(const void* vertices, size_t vertex_bytes,
                      const void* materials, size_t material_bytes,
                      const void* bvh_nodes, size_t bvh_bytes, int n_layouts,
-                     uint32_t* out_words, size_t cap_words, size_t* n_words, int32_t info[6]);
+                     uint32_t* out_words, size_t cap_words, size_t* n_words, int32_t info[8]);
 
 /* ----------------------------------------------------------- scene build -- */
 /* Host-side producers of the three buffers, replacing the Java SceneBuilder

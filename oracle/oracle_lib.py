@@ -49,6 +49,7 @@ def lib(envelope: bool = False, accel: bool = False) -> C.CDLL:
             _accel_lib.orc_accel_margin.argtypes = [C.c_float, C.c_float]
             _accel_lib.orc_accel_audit.argtypes = [C.c_int]
             _accel_lib.orc_accel_audit_get.argtypes = [C.POINTER(C.c_double)]
+            _accel_lib.orc_accel_relax_half.argtypes = [C.c_float]
             _accel_lib.orc_accel_audit_bins.argtypes = [C.POINTER(C.c_double), C.POINTER(C.c_double),
                                                         C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
         return _accel_lib
@@ -131,6 +132,12 @@ def render(vertices, materials, nodes, camera_ubo: bytes, width: int, height: in
     return rgba, rad, c.as_dict()
 
 
+def accel_relax(cls: int) -> float:
+    """accel_build.h accel_relax: the margin factor of shape class cls."""
+    one = np.float32(1.0)
+    return float(one + np.float32(2.0 ** -10)) if cls < 7 else float(one + np.float32(2.0 ** (cls - 16)))
+
+
 def render_accel(vertices, materials, nodes, camera_ubo: bytes, width: int, height: int, max_bounces: int,
                  records: np.ndarray, info: dict, tile=None, row_step: int = 1, n_threads: int = 0,
                  profile: bool = False):
@@ -152,6 +159,7 @@ def render_accel(vertices, materials, nodes, camera_ubo: bytes, width: int, heig
     L = lib(accel=True)
     if L.orc_accel_format(int(info.get("format", 0))) != 0:
         raise RuntimeError("orc_accel_format failed")
+    L.orc_accel_relax_half(accel_relax(int(info.get("max_class", 0))))
     if L.orc_accel_set(rec.ctypes.data, int(info["n_layouts"]), int(info["slots"]), int(info["root_leaf"])) != 0:
         raise RuntimeError("orc_accel_set failed")
     rc = L.orc_render_profile(vp, vn, mp, mn, bp, bn, cam.ctypes.data, width, height, max_bounces,
@@ -176,11 +184,12 @@ def accel_audit(on: bool = True) -> None:
 def accel_audit_result() -> dict:
     """The audit since accel_audit(): segments with a hit, of them hits before
     their own box's t_enter, headroom > 0.5 of the margin, unsafe (the margin
-    test fails: the exactness argument does not cover the segment), the
-    largest headroom (te* - t*) / (t* 2^-10 + 2^-10), and the hits on
+    test with i*'s class factor fails: the exactness argument does not cover
+    the segment), the largest headroom (te* - t*) / (t* 2^-10 + 2^-10) and the
+    same against i*'s class margin (max_headroom_class), and the hits on
     near-degenerate triangles (|det| <= 1e-4, compute_dynamic_ray.comp:110 cuts
     at 1e-5) with their largest headroom."""
-    out = (C.c_double * 7)()
+    out = (C.c_double * 8)()
     lib(accel=True).orc_accel_audit_get(out)
     sh, gr = (C.c_double * 32)(), (C.c_double * 32)()
     shn, grn = (C.c_uint64 * 32)(), (C.c_uint64 * 32)()
@@ -190,6 +199,7 @@ def accel_audit_result() -> dict:
         return {str(k): [int(n[k]), float(mx[k])] for k in range(32) if n[k]}
     return {"hits": int(out[0]), "before_box": int(out[1]), "over_half": int(out[2]), "unsafe": int(out[3]),
             "max_headroom": float(out[4]), "sliver_hits": int(out[5]), "sliver_max_headroom": float(out[6]),
+            "max_headroom_class": float(out[7]),
             "by_shape": bins(sh, shn), "by_grazing": bins(gr, grn)}
 
 

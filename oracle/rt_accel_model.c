@@ -25,6 +25,12 @@
  * orc_accel_format(1): the records are accel_build.h's format 1 (option
  * accel_half): 16-B slots, an internal node one slot with its box in IEEE half
  * precision (decoded exactly, as the kernel's v_cvt_f32_f16), a leaf four.
+ *
+ * Thin triangles (round 6, accel_build.h accel_class / accel_relax): a box is
+ * entered when t_enter <= closest_t * R + 2^-10 with R its record's factor
+ * (an internal node's word 7 as a float, bit 0 being L(first child); format
+ * 1: orc_accel_relax_half's one factor), and a leaf marked thin (bit 29 of
+ * word 3) whenever its slab test passes.
  */
 #define ORC_WALK_HOOK accel_walk
 #include "rt_oracle.c"
@@ -37,12 +43,45 @@ static uint64_t g_leaf_visits = 0;     /* analysis: leaf slots walked (the rest 
 /* The walk's box margin: a box is entered when t_enter <= closest_t * RELAX +
  * RELAX_ABS (accel_build.h).  orc_accel_margin changes them for studies. */
 static float g_relax = 1.0f + 1.0f / 1024.0f, g_relax_abs = 1.0f / 1024.0f;
+static int g_relax_set = 0;            /* a study changed the default margin */
+static float g_relax_half = 1.0f + 1.0f / 1024.0f;
+#define RELAX_BITS 0x3F802000u         /* 1 + 2^-10 */
 
 int orc_accel_margin(float rel, float abs_) {
     g_relax = rel;
     g_relax_abs = abs_;
+    g_relax_set = !(rel == 1.0f + 1.0f / 1024.0f && abs_ == 1.0f / 1024.0f);
     return 0;
 }
+
+/* Format 1: the margin factor of every internal node (accel_relax of the
+ * tree's largest shape class, AccelHost::relax_max). */
+int orc_accel_relax_half(float r) {
+    g_relax_half = r;
+    return 0;
+}
+
+/* The margin factor of a record (words 3 and 7: aw, bw). */
+static float rec_factor(int leaf, uint32_t aw, uint32_t bw) {
+    if (leaf) return (aw & (1u << 29)) ? INFINITY : g_relax;
+    if (g_fmt) return g_relax_half;
+    if (g_relax_set && (bw & ~1u) == RELAX_BITS) return g_relax;
+    float r;
+    memcpy(&r, &bw, 4);
+    return r;
+}
+
+/* accel_build.cpp accel_class / accel_relax, restated (the audit's margin). */
+static int shape_class(vec3 e1, vec3 e2) {
+    const double a[3] = {e1.x, e1.y, e1.z}, b[3] = {e2.x, e2.y, e2.z};
+    const double c[3] = {a[1] * b[2] - a[2] * b[1], a[2] * b[0] - a[0] * b[2], a[0] * b[1] - a[1] * b[0]};
+    const double sn = sqrt(c[0] * c[0] + c[1] * c[1] + c[2] * c[2]) /
+                      (sqrt(a[0] * a[0] + a[1] * a[1] + a[2] * a[2]) * sqrt(b[0] * b[0] + b[1] * b[1] + b[2] * b[2]));
+    if (!(sn > 0.0)) return 31;
+    const int k = (int)floor(-log2(sn));
+    return k < 0 ? 0 : (k > 31 ? 31 : k);
+}
+static float class_relax(int cls) { return cls < 7 ? 1.0f + 1.0f / 1024.0f : 1.0f + ldexpf(1.0f, cls - 16); }
 
 /* Segments re-walked in the reference's order since the last call (resets). */
 uint64_t orc_accel_fallbacks(void) {
@@ -119,7 +158,8 @@ static float half_up(float x) { return -half_down(-x); }
  * 2^-10): <= 0 for a hit inside its box, in (0, 1] where only the margin
  * keeps the box entered, > 1 where the argument fails (unsafe). */
 static int g_audit = 0;
-static double g_audit_max = -INFINITY;
+static double g_audit_max = -INFINITY;   /* against the default margin, 2^-10 */
+static double g_audit_max_c = -INFINITY; /* against i*'s class margin (what the walk applies) */
 static uint64_t g_audit_hits = 0, g_audit_incons = 0, g_audit_half = 0, g_audit_unsafe = 0;
 static uint64_t g_audit_sliver = 0;         /* hits on i* with |det| <= 1e-4 (the 1e-5 cut's decade, :110) */
 static double g_audit_sliver_max = -INFINITY;
@@ -149,7 +189,7 @@ int orc_accel_audit_bins(double shape[32], double graze[32], uint64_t shape_n[32
 
 int orc_accel_audit(int on) {
     g_audit = on;
-    g_audit_max = -INFINITY;
+    g_audit_max = g_audit_max_c = -INFINITY;
     g_audit_hits = g_audit_incons = g_audit_half = g_audit_unsafe = g_audit_sliver = 0;
     g_audit_sliver_max = -INFINITY;
     for (int k = 0; k < 32; ++k) {
@@ -160,9 +200,10 @@ int orc_accel_audit(int on) {
 }
 
 /* {segments with a hit, of them t* < te*, headroom > 0.5, unsafe (the
- * margin test fails), max headroom, hits with |det| <= 1e-4, their max
- * headroom} since orc_accel_audit. */
-int orc_accel_audit_get(double out[7]) {
+ * class margin test fails), max headroom (default margin), hits with |det| <=
+ * 1e-4, their max headroom, max headroom against the class margin} since
+ * orc_accel_audit. */
+int orc_accel_audit_get(double out[8]) {
     out[0] = (double)g_audit_hits;
     out[1] = (double)g_audit_incons;
     out[2] = (double)g_audit_half;
@@ -170,6 +211,7 @@ int orc_accel_audit_get(double out[7]) {
     out[4] = g_audit_max;
     out[5] = (double)g_audit_sliver;
     out[6] = g_audit_sliver_max;
+    out[7] = g_audit_max_c;
     return 0;
 }
 
@@ -226,8 +268,12 @@ static void audit_segment(const scene* s, ray r) {
     if (best < 0) return;
     const double room = (double)best_t * (1.0 / 1024.0) + 1.0 / 1024.0;
     const double head = ((double)best_te - (double)best_t) / room;
-    const int unsafe = !(best_te <= best_t * g_relax + g_relax_abs);
     const vec3 v0 = vertex_pos(s, (size_t)best * 3 + 0);
+    /* the walk enters i*'s leaf and ancestors with at least i*'s class factor */
+    const float rc = class_relax(shape_class(sub3(vertex_pos(s, (size_t)best * 3 + 1), v0),
+                                             sub3(vertex_pos(s, (size_t)best * 3 + 2), v0)));
+    const int unsafe = !(best_te <= best_t * rc + g_relax_abs);
+    const double head_c = ((double)best_te - (double)best_t) / ((double)best_t * ((double)rc - 1.0) + 1.0 / 1024.0);
     const float det = dot3(sub3(vertex_pos(s, (size_t)best * 3 + 1), v0), cross3(r.dir, sub3(vertex_pos(s,
                            (size_t)best * 3 + 2), v0)));
     const int sliver = det >= -1e-4f && det <= 1e-4f;
@@ -249,6 +295,7 @@ static void audit_segment(const scene* s, ray r) {
         g_audit_half += head > 0.5;
         g_audit_unsafe += (uint64_t)unsafe;
         if (head > g_audit_max) g_audit_max = head;
+        if (head_c > g_audit_max_c) g_audit_max_c = head_c;
         g_audit_sliver += (uint64_t)sliver;
         if (sliver && head > g_audit_sliver_max) g_audit_sliver_max = head;
         g_audit_shape_n[bs]++;
@@ -269,7 +316,6 @@ static int accel_walk(const scene* s, ray r, float* closest_t, int* hit_index, v
     int leaf = g_root_leaf;
     const vec3 inv = v3(rcp(r.dir.x), rcp(r.dir.y), rcp(r.dir.z));
     float c = *closest_t;
-    float thr = c * g_relax + g_relax_abs;
     float hit_te = 0.0f;                      /* t_enter of the hit triangle's own box */
     int hit = -1;
     uint64_t leaf_visits = 0;
@@ -296,7 +342,7 @@ static int accel_walk(const scene* s, ray r, float* closest_t, int* hit_index, v
         const vec3 t1s = mul3(sub3(bhi, r.origin), inv);
         const float te = fmaxf(fmaxf(fminf(t0s.x, t1s.x), fminf(t0s.y, t1s.y)), fminf(t0s.z, t1s.z));
         const float tx = fminf(fminf(fmaxf(t0s.x, t1s.x), fmaxf(t0s.y, t1s.y)), fmaxf(t0s.z, t1s.z));
-        const int hb = tx > te && tx > T_MIN && te <= thr;
+        const int hb = tx > te && tx > T_MIN && te <= c * rec_factor(leaf, aw, bw) + g_relax_abs;
         leaf_visits += (uint64_t)leaf;
         if (hb && leaf) {
             const int tri = (int)(aw & 0x1FFFFFFFu);
@@ -309,7 +355,6 @@ static int accel_walk(const scene* s, ray r, float* closest_t, int* hit_index, v
                              vertex_pos(s, (size_t)tri * 3 + 2), &t, &nrm) &&
                 (t < c || (t == c && tri < hit))) {
                 c = t;
-                thr = c * g_relax + g_relax_abs;
                 hit = tri;
                 hit_te = te;
                 *hit_normal = nrm;

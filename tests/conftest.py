@@ -40,6 +40,8 @@ def _built():
                                            f"the tree's sources (src={_lib.source_hash()})")
     if not os.path.exists(olib):
         subprocess.run(["make", "-C", os.path.join(ROOT, "oracle")], check=True)
+    # the JNI shim against the mock JNIEnv follows include/rtamd.h (incremental)
+    subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "jni"), "mock"], check=True, stdout=subprocess.DEVNULL)
     print(f"\nlibrtamd build id: {_lib.file_build_id()} (tree src={_lib.source_hash()})")
     yield
 

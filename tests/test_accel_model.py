@@ -352,31 +352,39 @@ def test_adversarial_scenes(name):
     whose hits have |det| near the shader's 1e-5 cut, grazing rays on a
     tilted ground and along the cube's faces, meshes at +-1e4, triangles
     1e-3 from the eye.  Small versions: the model's frame equals the
-    oracle's, and the audit finds no segment outside the margin (headroom
-    < 0.01 of it)."""
+    oracle's, and the audit finds no segment outside the margin the walk
+    applies (thin triangles' boxes carry wider ones: accel_build.h
+    accel_relax), with headroom to spare (< 0.25 of it)."""
     A = _adversarial()
     c = A.run_scene(name, 160, 90, 4, scale=0.1, seeds=(1,), layouts=(8,))
     e = c["seeds"]["1"]["layouts8"]
     assert e["rgba_px"] == 0 and e["radiance_px"] == 0, e
     assert e["segments_equal"] and e["mat_reads_equal"]
-    assert e["audit"]["hits"] > 0 and e["audit"]["unsafe"] == 0 and e["audit"]["max_headroom"] < 0.01, e["audit"]
+    a = e["audit"]
+    assert a["hits"] > 0 and a["unsafe"] == 0 and a["max_headroom_class"] < 0.25, a
 
 
 def test_adversarial_study_claims():
     """tests/golden/accel_adversarial.json (the full-size study): every scene,
-    seed and layout count bit-exact against the seed-1 oracle, no unsafe
-    segment, the fine mesh's near-degenerate hits present."""
+    seed and layout count bit-exact against the seed-1 oracle, no segment
+    outside the margin the walk applies (< 0.25 of it), the fine mesh's
+    near-degenerate hits present, and the needles' hits that lie more than
+    the default 2^-10 margin before their box (the case the class margins
+    exist for) found."""
     with open(os.path.join(HERE, "golden", "accel_adversarial.json")) as f:
         d = json.load(f)
     assert not d["quick"]
     names = {c["scene"] for c in d["cases"]}
     assert names == set(_adversarial().SCENES)
-    slivers = 0
+    slivers, worst = 0, 0.0
     for c in d["cases"]:
         for seed, e in c["seeds"].items():
             for k in ("layouts1", "layouts8"):
                 a = e[k]
                 assert a["rgba_px"] == 0 and a["radiance_px"] == 0, (c["scene"], seed, k)
-                assert a["audit"]["unsafe"] == 0 and a["audit"]["max_headroom"] < 0.01, (c["scene"], seed, k)
+                assert a["audit"]["unsafe"] == 0 and a["audit"]["max_headroom_class"] < 0.25, (c["scene"], seed, k)
                 slivers += a["audit"]["sliver_hits"]
+                if c["scene"] == "slivers":
+                    worst = max(worst, a["audit"]["max_headroom"])
     assert slivers > 1000
+    assert worst > 1.0
