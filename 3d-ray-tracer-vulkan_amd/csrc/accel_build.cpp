@@ -183,7 +183,152 @@ uint64_t fnv(const unsigned char* p, size_t n, uint64_t h) {
 
 void put_f(uint32_t* w, float f) { std::memcpy(w, &f, 4); }
 
+// ---- format 2: the 4-wide tree (accel_build.h) ----
+
+// The exponent of an axis: the smallest e with decode(255) >= hi (and 255 *
+// 2^e a normal float), so every child bound quantises inside [0, 255].
+int wide_exponent(float lo, float hi) {
+    const double ext = (double)hi - (double)lo;
+    int e = ext > 0.0 ? (int)std::ceil(std::log2(ext / 255.0)) : -100;
+    if (e < -100) e = -100;
+    while (wide_decode(lo, 255, e) < hi) ++e;
+    while (e > -100 && wide_decode(lo, 255, e - 1) >= hi) --e;
+    return e;
+}
+
+// The largest q with decode(q) <= x, and the smallest q with decode(q) >= x:
+// a child's box rounded outward on the node's grid (exact in the kernel's
+// float arithmetic, so the decoded box holds the child's true box).
+int wide_q_down(float origin, int e, float x) {
+    int q = (int)std::floor(((double)x - (double)origin) / std::ldexp(1.0, e));
+    q = std::max(0, std::min(255, q));
+    while (q > 0 && wide_decode(origin, q, e) > x) --q;
+    while (q < 255 && wide_decode(origin, q + 1, e) <= x) ++q;
+    return q;
+}
+int wide_q_up(float origin, int e, float x) {
+    int q = (int)std::ceil(((double)x - (double)origin) / std::ldexp(1.0, e));
+    q = std::max(0, std::min(255, q));
+    while (q < 255 && wide_decode(origin, q, e) < x) ++q;
+    while (q > 0 && wide_decode(origin, q - 1, e) >= x) --q;
+    return q;
+}
+
+struct WideEmitter {
+    const Builder& B;
+    const unsigned char* vb;
+    std::vector<uint32_t>& rec;
+    size_t next = 0;              // the next free record
+
+    uint32_t* at(size_t i) { return &rec[16 * i]; }
+
+    // The 2-4 binary nodes a wide node of binary node b holds: b's children,
+    // the largest-area internal one replaced by its two until there are 4.
+    std::vector<int> collapse(int b) const {
+        std::vector<int> c = {B.nodes[b].left, B.nodes[b].right};
+        while (c.size() < 4) {
+            int best = -1;
+            float ba = -1.0f;
+            for (size_t i = 0; i < c.size(); ++i) {
+                const BNode& n = B.nodes[c[i]];
+                if (n.prim >= 0) continue;
+                const float a = area(n.lo, n.hi);
+                if (a > ba) {
+                    ba = a;
+                    best = (int)i;
+                }
+            }
+            if (best < 0) break;
+            const int x = c[best];
+            c[best] = B.nodes[x].left;
+            c.insert(c.begin() + best + 1, B.nodes[x].right);
+        }
+        return c;
+    }
+
+    // A leaf: what the triangle test reads in the first 48 bytes, the rest of
+    // its exact box (read only for a hit that would be taken) in the last 16.
+    void leaf(int b, size_t idx) {
+        const Prim& p = B.prims[B.nodes[b].prim];
+        const BNode& nd = B.nodes[b];
+        uint32_t* w = at(idx);
+        const unsigned char* v = vb + (size_t)p.tri * 48;
+        float x[9];
+        for (int j = 0; j < 3; ++j) std::memcpy(&x[3 * j], v + 16 * j, 12);
+        const float e1[3] = {x[3] - x[0], x[4] - x[1], x[5] - x[2]};
+        const float e2[3] = {x[6] - x[0], x[7] - x[1], x[8] - x[2]};
+        w[0] = (uint32_t)p.tri | (1u << 30) | (p.cls >= kAccelClassMin ? 1u << 29 : 0u);
+        for (int j = 0; j < 3; ++j) {
+            put_f(&w[1 + j], x[j]);
+            put_f(&w[4 + j], e1[j]);
+            put_f(&w[8 + j], e2[j]);
+        }
+        put_f(&w[7], nd.lo[0]);
+        put_f(&w[11], nd.lo[1]);
+        put_f(&w[12], nd.lo[2]);
+        put_f(&w[13], nd.hi[0]);
+        put_f(&w[14], nd.hi[1]);
+        put_f(&w[15], nd.hi[2]);
+    }
+
+    // Writes binary node b (internal) as the wide node at idx, its children
+    // as one contiguous block of records, and their subtrees after it.
+    void node(int b, size_t idx) {
+        const BNode& nd = B.nodes[b];
+        const std::vector<int> c = collapse(b);
+        const size_t base = next;
+        next += c.size();
+        uint32_t* w = at(idx);
+        int e[3];
+        for (int q = 0; q < 3; ++q) {
+            put_f(&w[q], nd.lo[q]);
+            e[q] = wide_exponent(nd.lo[q], nd.hi[q]);
+        }
+        w[3] = (uint32_t)(uint8_t)(int8_t)e[0] | (uint32_t)(uint8_t)(int8_t)e[1] << 8 |
+               (uint32_t)(uint8_t)(int8_t)e[2] << 16 | (uint32_t)c.size() << 24;
+        uint32_t flags = 0;
+        for (size_t i = 0; i < c.size(); ++i) {
+            const BNode& ch = B.nodes[c[i]];
+            for (int q = 0; q < 3; ++q) {
+                w[4 + q] |= (uint32_t)wide_q_down(nd.lo[q], e[q], ch.lo[q]) << (8 * i);
+                w[7 + q] |= (uint32_t)wide_q_up(nd.lo[q], e[q], ch.hi[q]) << (8 * i);
+            }
+            uint32_t f = 0;
+            if (ch.prim >= 0) {
+                f |= 1u;                                            // a leaf
+                if (ch.cls >= kAccelClassMin) f |= 2u;              // thin: entered whenever hit
+            } else if (ch.cls >= kAccelClassMin) {
+                f |= 4u;                                            // a subtree with a wider margin
+            }
+            flags |= f << (8 * i);
+        }
+        w[10] = (uint32_t)base | (uint32_t)std::min(nd.cls, 31) << 27;
+        w[11] = flags;
+        for (size_t i = 0; i < c.size(); ++i) {
+            if (B.nodes[c[i]].prim >= 0) leaf(c[i], base + i);
+            else node(c[i], base + i);
+        }
+    }
+};
+
+void emit_wide(const Builder& B, const unsigned char* vb, AccelHost* out) {
+    const size_t m = B.prims.size();
+    out->rec.assign(16 * (2 * m + 1), 0u);             // an upper bound; trimmed below
+    WideEmitter E{B, vb, out->rec};
+    E.next = 1;
+    out->root_leaf = B.nodes[0].prim >= 0 ? 1 : 0;
+    if (out->root_leaf) E.leaf(0, 0);
+    else E.node(0, 0);
+    out->slots = (int)E.next;
+    out->rec.resize(16 * (E.next + 1));                 // + one record of zero padding
+    std::fill(out->rec.end() - 16, out->rec.end(), 0u);
+}
+
+
 }  // namespace
+
+// The float decode the kernel performs: origin + q * 2^e, rounded once.
+float wide_decode(float origin, int q, int e) { return origin + (float)q * std::ldexp(1.0f, e); }
 
 int accel_class(const float e1[3], const float e2[3]) {
     const double a[3] = {e1[0], e1[1], e1[2]}, b[3] = {e2[0], e2[1], e2[2]};
@@ -228,13 +373,13 @@ int accel_build(const void* vertices, size_t vertex_bytes, const void* materials
                 const void* bvh_nodes, size_t bvh_bytes, int n_layouts, int n_threads, AccelHost* out,
                 std::string* err, int format, int64_t cap_slots) {
     *out = AccelHost{};
-    if (format != 0 && format != 1) {
-        *err = "accel: format must be 0 or 1";
+    if (format < 0 || format > 2) {
+        *err = "accel: format must be 0, 1 or 2";
         return -1;
     }
     out->format = format;
-    const int W = format ? 4 : 8;                     // words per slot
-    const int64_t LS = format ? 4 : 2;                // slots per leaf
+    const int W = format == 1 ? 4 : 8;                // words per slot
+    const int64_t LS = format == 1 ? 4 : 2;           // slots per leaf
 #ifdef ACCEL_TIMING
     const auto t_start = std::chrono::steady_clock::now();
 #endif
@@ -242,6 +387,7 @@ int accel_build(const void* vertices, size_t vertex_bytes, const void* materials
         *err = "accel: n_layouts must be 1 or 8";
         return -1;
     }
+    if (format == 2) n_layouts = 1;                   // the wide walk orders children by t_enter
     out->n_layouts = n_layouts;
     const size_t n_nodes = bvh_bytes / 48, n_tris = vertex_bytes / 48, n_mats = material_bytes / 16;
     const unsigned char* nb = static_cast<const unsigned char*>(bvh_nodes);
@@ -251,6 +397,7 @@ int accel_build(const void* vertices, size_t vertex_bytes, const void* materials
         out->rec.assign(16, 0u);                      // 64 B of padding
         return 0;
     }
+    (void)kWideCap;
 
     // 1. the reference's leaves as primitives (triangle, leaf box), duplicates dropped
     Builder B;
@@ -322,8 +469,9 @@ int accel_build(const void* vertices, size_t vertex_bytes, const void* materials
     ACCEL_T("duplicates dropped");
     // a subtree of k triangles: k - 1 internal nodes (1 slot) and k leaves
     const auto span = [LS](int64_t k) { return (LS + 1) * k - 1; };
-    const int64_t slots = span(m);
-    int64_t cap = format ? (int64_t)(1u << 30) - 8 : (int64_t)(1u << 27) - 4;   // link bits; 4 GB
+    // format 2: m leaf records and at most m - 1 wide nodes (64 B each)
+    const int64_t slots = format == 2 ? 2 * (int64_t)m - 1 : span(m);
+    int64_t cap = format == 1 ? (int64_t)(1u << 30) - 8 : format == 2 ? kWideCap : (int64_t)(1u << 27) - 4;
     if (cap_slots > 0 && cap_slots < cap) cap = cap_slots;
     if (slots * n_layouts + 8 > cap) {
         *err = "accel: " + std::to_string(m) + " triangles: " + std::to_string(n_layouts) + " layouts exceed " +
@@ -360,6 +508,12 @@ int accel_build(const void* vertices, size_t vertex_bytes, const void* materials
         double s = 0.0;
         for (const BNode& nd : B.nodes) s += a0 > 0.0f ? (double)area(nd.lo, nd.hi) / a0 : 1.0;
         out->sah = s;
+    }
+
+    if (format == 2) {
+        emit_wide(B, vb, out);
+        ACCEL_T("wide records written");
+        return 0;
     }
 
     // 3. the layouts: preorder, near child first per the layout's sign bits

@@ -40,6 +40,25 @@
 // e2).  A subtree of m triangles takes 5m - 1 slots; a walk step of internal
 // nodes loads 16 B instead of 32.  Widened internal boxes are only entered
 // more often: every leaf box and triangle test is format 0's.
+//
+// Format 2 ("wide", option accel_wide): a 4-wide tree collapsed from the same
+// SAH tree (each wide node takes its binary node's children, the
+// largest-area internal one split until there are four), one layout, 64-B
+// records of which a step reads 48 B (3 loads); a ray orders the children it
+// enters by t_enter and keeps the rest on a short per-lane stack.  A wide
+// node: words 0-2 its box's lo (the quantisation origin), word 3 = the
+// exponents e_x, e_y, e_z (int8, bytes 0-2) | child count (2-4) << 24; words
+// 4-9 the children's boxes on the grid origin + q 2^e, 8 bits per bound, byte
+// i = child i (lo.x, lo.y, lo.z, hi.x, hi.y, hi.z), every bound rounded
+// outward in the kernel's own float arithmetic; word 10 = the children's
+// first record (they are one contiguous block) | the node's largest shape
+// class << 27 (its margin factor, accel_relax); word 11 = byte i: child i's
+// flags (1: a leaf, 2: a thin leaf, entered whenever its slab test passes, 4:
+// a subtree of class >= 7, tested with the node's factor).  A leaf: word 0 =
+// triangle index | thin << 29 | 1 << 30; words 1-3 v0, 4-6 e1, 8-10 e2 (the
+// triangle test's 48 bytes, with lo.x in word 7 and lo.y in word 11); words
+// 12-15 lo.z, hi.xyz: the rest of the exact box, read only when the triangle
+// test finds a hit the walk would take.  Record 0 is the root.
 #pragma once
 #include <cmath>
 #include <cstddef>
@@ -50,9 +69,10 @@
 namespace rtamd {
 
 struct AccelHost {
-    std::vector<uint32_t> rec;      // 8 words per slot (format 1: 4), n_layouts * slots slots, + 64 B of zero
+    std::vector<uint32_t> rec;      // 8 words per slot (format 1: 4, format 2: 16), n_layouts * slots slots, + 64 B of zero
                                     //   padding
-    int format = 0;                 // 0: 32-B slots, fp32 boxes; 1: 16-B slots, half-precision internal boxes
+    int format = 0;                 // 0: 32-B slots, fp32 boxes; 1: 16-B slots, half-precision internal boxes;
+                                    //   2: 64-B records of the 4-wide tree (slots = records)
     int n_layouts = 0;              // 1 or 8
     int slots = 0;                  // slots per layout (0: empty scene)
     int root_leaf = 0;              // the root is a leaf (a one-triangle scene)
@@ -83,6 +103,12 @@ float accel_relax(int cls);
 
 // The layouts do not fit the slot cap (accel_build's return value).
 constexpr int kAccelTooBig = -2;
+// Format 2's record cap: 64-B records addressed by 32-bit buffer offsets.
+constexpr int64_t kWideCap = (int64_t)(1u << 26) - 2;
+// The per-lane stack of the wide walk (entries), and the decode of format 2's
+// grid (accel_build.cpp; the kernel and oracle/rt_accel_model.c restate it).
+constexpr int kWideStack = 12;
+float wide_decode(float origin, int q, int e);
 
 // Builds the records from the reference's buffers (the rt_upload_scene
 // inputs: 48-B vertex records, 16-B materials, 48-B preorder nodes).  The

@@ -78,6 +78,7 @@ struct DevScene {
     // slots (pad slots as `ref_padded`).  n_layouts 0: no accel.
     int      n_layouts = 0;
     int      layout_slots = 0;
+    int      wide = 0;          // accel format 2: the 4-wide tree, 64-B records (end2 = records)
     int      half = 0;          // accel format 1: 16-B slots, half-precision internal boxes (accel_build.h);
                                 //   layout_slots and end2 then count 16-B slots
     float    relax_half = 0.0f;  // format 1: every internal node's margin factor (AccelHost::relax_max)

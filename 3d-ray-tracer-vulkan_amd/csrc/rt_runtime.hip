@@ -244,6 +244,10 @@ static constexpr int kMaxSlots = 8;   // rt_render_async frame slots per device
 #ifndef RT_ACCEL_HALF
 #define RT_ACCEL_HALF 0
 #endif
+// Option accel_wide's default: the 4-wide tree (accel_build.h format 2).
+#ifndef RT_ACCEL_WIDE
+#define RT_ACCEL_WIDE 0
+#endif
 // Option split_bounce's default.
 #ifndef RT_SPLIT_BOUNCE
 #define RT_SPLIT_BOUNCE 0
@@ -412,6 +416,7 @@ struct rt_ctx {
     int  learn_device = 1;         // heavy_first: learn the order on the device (rt_learn.hip; 0 = on the host)
     int  leaf_align = RT_LEAF_ALIGN;   // walk records: no leaf straddles a 128-B line (a pad slot before it)
     int  accel_half = RT_ACCEL_HALF;   // at the next upload: accel records in format 1 (accel_build.h)
+    int  accel_wide = RT_ACCEL_WIDE;   // at the next upload: the 4-wide tree, format 2 (overrides accel_half)
     int  split_bounce = RT_SPLIT_BOUNCE;   // accel walk: paths alive at this bounce finish in a second kernel
                                    //   (0 = one kernel)
     int  accel = RT_ACCEL;         // at the next upload: 0 = the reference's tree and order; 1 / 8 = the
@@ -818,7 +823,7 @@ static int learn_order(const rt_ctx* ctx, PerDevice& p, const TraceArgs& a, hipS
 // 0.2942-0.2954 against 0.2965-0.2987 (profiles/r04/r4aa, r4ab).
 // The records one ray walks: the reference's walk records, or one accel layout.
 static size_t walk_bytes(const PerDevice& p) {
-    return (size_t)(p.scene.n_layouts ? p.scene.layout_slots : p.scene.end2) * (p.scene.half ? 16 : 32);
+    return (size_t)(p.scene.n_layouts ? p.scene.layout_slots : p.scene.end2) * (p.scene.wide ? 64 : p.scene.half ? 16 : 32);
 }
 
 // The accel walk runs 16x4 tiles on every scene: config 3 0.1205-0.1212 ms per
@@ -838,7 +843,7 @@ static int set_schedule(const rt_ctx* ctx, PerDevice& p, TraceArgs& a, const rt_
                         const std::vector<int>* bands = nullptr) {
     a.wave_tile = wave_tile_of(ctx, p);
     // (the cooperative tail walks 32-B slots: not over half-format accel records)
-    a.coop_lanes = p.scene.half ? 0 : ctx->coop_lanes >= 0 ? ctx->coop_lanes : (p.scene.n_layouts ? 0 : 1);
+    a.coop_lanes = (p.scene.half || p.scene.wide) ? 0 : ctx->coop_lanes >= 0 ? ctx->coop_lanes : (p.scene.n_layouts ? 0 : 1);
     a.walk = p.scene.n_layouts ? 2 : ctx->walk;          // accel: the walk-2 records only
     a.coop_walk = p.scene.n_layouts ? 0 : ctx->coop_walk;
     a.coop_win = coop_window_of(ctx, p);
@@ -1072,6 +1077,7 @@ int rt_create(const int* device_ids, int n_devices, rt_ctx** out) {
         ctx->accel = k == 1 || k == 8 ? k : 0;
     }
     if (const char* v = std::getenv("RTAMD_ACCEL_HALF")) ctx->accel_half = std::atoi(v) ? 1 : 0;
+    if (const char* v = std::getenv("RTAMD_ACCEL_WIDE")) ctx->accel_wide = std::atoi(v) ? 1 : 0;
     if (const char* v = std::getenv("RTAMD_HEAVY_FIRST")) ctx->heavy_first = std::atoi(v) ? 1 : 0;
     if (const char* v = std::getenv("RTAMD_HEAVY_TILES")) ctx->heavy_tiles = std::max(-1, std::atoi(v));
     if (const char* v = std::getenv("RTAMD_LEARN_COST")) ctx->learn_cost = std::atoi(v) ? 1 : 0;
@@ -1289,7 +1295,7 @@ int rt_upload_scene(rt_ctx* ctx, const void* vertices, size_t vertex_bytes,
         std::string msg;
         const int rc = accel_build_fit(vertices, vertex_bytes, materials, material_bytes, bvh_nodes,
                                        (size_t)hs.end * RT_NODE_RECORD_BYTES, ctx->accel, &ah, &msg,
-                                       ctx->accel_half ? 1 : 0, accel_cap_slots());
+                                       ctx->accel_wide ? 2 : ctx->accel_half ? 1 : 0, accel_cap_slots());
         if (rc != 0 && rc != kAccelTooBig) {
             free_host_scene(&hs);
             set_error("rt_upload_scene: %s", msg.c_str());
@@ -1324,7 +1330,8 @@ int rt_upload_scene(rt_ctx* ctx, const void* vertices, size_t vertex_bytes,
         if (acc) {
             s.n_layouts = ah.n_layouts;
             s.layout_slots = ah.slots;
-            s.half = ah.format;
+            s.half = ah.format == 1 ? 1 : 0;
+            s.wide = ah.format == 2 ? 1 : 0;
             s.relax_half = ah.relax_max;
             s.end = ah.slots;
             s.end2 = ah.n_layouts * ah.slots;
@@ -2023,6 +2030,8 @@ int rt_set_option(rt_ctx* ctx, const char* name, int64_t value) {
         ctx->split_bounce = (int)value;
     } else if (std::strcmp(name, "accel_half") == 0 && (value == 0 || value == 1)) {
         ctx->accel_half = (int)value;                   // takes effect at the next rt_upload_scene
+    } else if (std::strcmp(name, "accel_wide") == 0 && (value == 0 || value == 1)) {
+        ctx->accel_wide = (int)value;                   // takes effect at the next rt_upload_scene
     } else if (std::strcmp(name, "heavy_stream") == 0 && value >= 0 && value <= 2) {
         ctx->heavy_stream = (int)value;
     } else if (std::strcmp(name, "graph") == 0 && (value == 0 || value == 1)) {
@@ -2064,6 +2073,8 @@ int rt_get_option(rt_ctx* ctx, const char* name, int64_t* value) {
     else if (std::strcmp(name, "accel_half") == 0) *value = ctx->accel_half;
     else if (std::strcmp(name, "split_bounce") == 0) *value = ctx->split_bounce;
     else if (std::strcmp(name, "accel_half_used") == 0) *value = ctx->dev.empty() ? 0 : ctx->dev[0].scene.half;
+    else if (std::strcmp(name, "accel_wide") == 0) *value = ctx->accel_wide;
+    else if (std::strcmp(name, "accel_wide_used") == 0) *value = ctx->dev.empty() ? 0 : ctx->dev[0].scene.wide;
     else if (std::strcmp(name, "walk_bytes") == 0) *value = ctx->dev.empty() ? 0 : (int64_t)walk_bytes(ctx->dev[0]);
     else if (std::strcmp(name, "accel_used") == 0) *value = ctx->dev.empty() ? 0 : ctx->dev[0].scene.n_layouts;
     else if (std::strcmp(name, "leaf_align_used") == 0) *value = ctx->dev.empty() ? 0 : ctx->dev[0].scene.padded;
@@ -2140,13 +2151,14 @@ int rt_accel_records(const void* vertices, size_t vertex_bytes, const void* mate
     free_host_scene(&hs);
     AccelHost ah;
     std::string msg;
-    const int nl = n_layouts & ~RT_ACCEL_FORMAT_HALF;
-    if (nl != 1 && nl != 8) {
-        set_error("rt_accel_records: n_layouts must be 1 or 8");
+    const int nl = n_layouts & ~(RT_ACCEL_FORMAT_HALF | RT_ACCEL_FORMAT_WIDE);
+    if ((nl != 1 && nl != 8) || ((n_layouts & RT_ACCEL_FORMAT_HALF) && (n_layouts & RT_ACCEL_FORMAT_WIDE))) {
+        set_error("rt_accel_records: n_layouts must be 1 or 8, with at most one format flag");
         return RT_ERR_INVALID_ARG;
     }
     rc = accel_build_fit(vertices, vertex_bytes, materials, material_bytes, bvh_nodes, reach, nl, &ah, &msg,
-                         (n_layouts & RT_ACCEL_FORMAT_HALF) ? 1 : 0, accel_cap_slots());
+                         (n_layouts & RT_ACCEL_FORMAT_HALF) ? 1 : (n_layouts & RT_ACCEL_FORMAT_WIDE) ? 2 : 0,
+                         accel_cap_slots());
     if (rc == kAccelTooBig) {                      // rt_upload_scene walks the reference's tree: no records
         if (n_words) *n_words = 0;
         if (info) {

@@ -570,6 +570,152 @@ __device__ __forceinline__ int coop_walk(const float4* __restrict__ walk, int en
     return windows;
 }
 
+// ------------------------------------------------------------ wide walk --
+//
+// Option accel_wide (accel_build.h format 2; oracle/rt_accel_model.c
+// wide_walk states the same walk on the CPU).  One step per lockstep
+// iteration: the lane reads the 48 bytes of the record its link names
+// (three 16-B buffer loads).
+//   * A leaf: hit_triangle on v0 / e1 / e2; only a hit the walk would take
+//     (accel_take) reads the last 16 bytes (the rest of the leaf's exact box)
+//     and runs the reference's slab test with the leaf's rule, which decides.
+//   * A wide node: each child's box decoded from the node's grid (origin +
+//     q 2^e, exactly the host's float arithmetic, so the decoded box holds
+//     the child's true box) and slab-tested with the child's rule; the
+//     entered children in (t_enter, slot) order: the first is next, the
+//     others go on the lane's stack, farthest first.
+// Then (a leaf, or no child entered) the lane pops: an entry whose box would
+// no longer be entered is dropped (default-margin entries; t_enter kept as
+// bfloat16 rounded down, so a drop is always right).  An empty stack ends
+// the walk; a push past kWideStackK entries marks the segment for the
+// reference-order fallback (wovf).  The stack: kWideStackK x 64 links (4 B)
+// then kWideStackK x 64 bfloat16 t_enter (2 B) per wave in LDS, entry k of
+// lane l at k x 64 + l (no bank conflicts).
+constexpr uint32_t kWLeaf = 1u << 31, kWThin = 1u << 30, kWWider = 1u << 29, kWIdx = 0x07FFFFFFu;
+constexpr int kWideStackK = 12;     // accel_build.h kWideStack: 2e-5 of config 3's segments overflow (model)
+
+__device__ __forceinline__ float4 wrec(__amdgpu_buffer_rsrc_t r, int off) {
+    const auto v = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
+    return make_float4(__uint_as_float(v[0]), __uint_as_float(v[1]), __uint_as_float(v[2]), __uint_as_float(v[3]));
+}
+
+// One step of the wide walk; returns whether the lane still walks.
+template <bool COUNT>
+__device__ __forceinline__ bool wide_step(__amdgpu_buffer_rsrc_t wrs, uint4* stk, V3 o, V3 d, V3 inv, float& closest,
+                                          int& hit, bool& incons, uint32_t& cur, int& sp, bool& ovf,
+                                          unsigned long long& c_node, unsigned long long& c_tri) {
+    const int lane = threadIdx.x & 63;
+    uint32_t* sl = reinterpret_cast<uint32_t*>(stk);                                 // links
+    unsigned short* st = reinterpret_cast<unsigned short*>(sl + kWideStackK * 64);   // bfloat16 t_enter
+    const int off = (int)((cur & kWIdx) << 6);
+    const float4 R0 = wrec(wrs, off), R1 = wrec(wrs, off + 16), R2 = wrec(wrs, off + 32);
+    bool pop = true;
+    if (cur & kWLeaf) {
+        if (COUNT) ++c_tri;
+        const uint32_t w0 = __float_as_uint(R0.x);
+        const int tri = (int)(w0 & 0x1FFFFFFFu);
+        float t;
+        if (tri_test(make_float4(R0.y, R0.z, R0.w, 0.f), make_float4(R1.x, R1.y, R1.z, 0.f),
+                     make_float4(R2.x, R2.y, R2.z, 0.f), o, d, t) &&
+            accel_take(t, tri, closest, hit)) {
+            const float4 R3 = wrec(wrs, off + 48);
+            if (COUNT) ++c_node;
+            float te;
+            bool ind;
+            slab(make_float4(R1.w, R2.w, R3.x, 0.f), make_float4(R3.y, R3.z, R3.w, 0.f), o, inv, te, ind);
+            if (ind && accel_enter_r(te, closest, (w0 & kThinLeaf) ? __builtin_inff() : kRelax)) {
+                closest = t;
+                hit = tri;
+                incons = t < te;
+            }
+        }
+    } else {
+        const uint32_t w3 = __float_as_uint(R0.w);
+        const int n = (int)((w3 >> 24) & 7u);
+        const float sx = __builtin_ldexpf(1.0f, (int)(int8_t)(w3 & 0xFFu));
+        const float sy = __builtin_ldexpf(1.0f, (int)(int8_t)((w3 >> 8) & 0xFFu));
+        const float sz = __builtin_ldexpf(1.0f, (int)(int8_t)((w3 >> 16) & 0xFFu));
+        const uint32_t qlx = __float_as_uint(R1.x), qly = __float_as_uint(R1.y), qlz = __float_as_uint(R1.z);
+        const uint32_t qhx = __float_as_uint(R1.w), qhy = __float_as_uint(R2.x), qhz = __float_as_uint(R2.y);
+        const uint32_t w10 = __float_as_uint(R2.z), fl = __float_as_uint(R2.w);
+        const int cls = (int)(w10 >> 27);
+        const float nr = cls < 7 ? kRelax : 1.0f + __builtin_ldexpf(1.0f, cls - 16);
+        const uint32_t base = w10 & kWIdx;
+        if (COUNT) c_node += (unsigned long long)n;
+        // the children's (t_enter, slot) keys; not entered: +inf.  The
+        // decode and the slab run x and y in packed FP32 (each lane of
+        // v_pk_mul_f32 / v_pk_add_f32 rounds as the scalar operation does)
+        const f2 org = {R0.x, R0.y}, sxy = {sx, sy}, oxy = {o.x, o.y}, ixy = {inv.x, inv.y};
+        float k[4];
+        int ks[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int sh = 8 * i;
+            const f2 lxy = org + f2{(float)((qlx >> sh) & 0xFFu), (float)((qly >> sh) & 0xFFu)} * sxy;
+            const f2 hxy = org + f2{(float)((qhx >> sh) & 0xFFu), (float)((qhy >> sh) & 0xFFu)} * sxy;
+            const float lz = R0.z + (float)((qlz >> sh) & 0xFFu) * sz, hz = R0.z + (float)((qhz >> sh) & 0xFFu) * sz;
+            const f2 t0 = (lxy - oxy) * ixy, t1 = (hxy - oxy) * ixy;
+            const float t0z = (lz - o.z) * inv.z, t1z = (hz - o.z) * inv.z;
+            const float te = fmaxf(fmaxf(fminf(t0.x, t1.x), fminf(t0.y, t1.y)), fminf(t0z, t1z));
+            const float tx = fminf(fminf(fmaxf(t0.x, t1.x), fmaxf(t0.y, t1.y)), fmaxf(t0z, t1z));
+            const bool ind = tx > te && tx > kTMin;
+            const uint32_t f = (fl >> sh) & 0xFFu;
+            const float rf = (f & 2u) ? __builtin_inff() : ((f & 4u) ? nr : kRelax);
+            k[i] = (i < n && ind && accel_enter_r(te, closest, rf)) ? te : __builtin_inff();
+            ks[i] = i;
+        }
+        // sort by (t_enter, slot): a five-comparator network; every key is
+        // distinct in slot, so the order is the model's insertion order
+#define RT_WCE(a, b)                                                                       \
+        {                                                                                  \
+            const bool sw = k[a] > k[b] || (k[a] == k[b] && ks[a] > ks[b]);                \
+            const float tk = sw ? k[b] : k[a];                                             \
+            k[b] = sw ? k[a] : k[b];                                                       \
+            k[a] = tk;                                                                     \
+            const int ts = sw ? ks[b] : ks[a];                                             \
+            ks[b] = sw ? ks[a] : ks[b];                                                    \
+            ks[a] = ts;                                                                    \
+        }
+        RT_WCE(0, 1) RT_WCE(2, 3) RT_WCE(0, 2) RT_WCE(1, 3) RT_WCE(1, 2)
+#undef RT_WCE
+        const int h = (k[0] != __builtin_inff()) + (k[1] != __builtin_inff()) + (k[2] != __builtin_inff()) +
+                      (k[3] != __builtin_inff());
+        if (h > 0) {
+            if (sp + h - 1 > kWideStackK) {
+                ovf = true;
+                return false;
+            }
+            const auto link = [&](int slot) -> uint32_t {
+                const uint32_t f = (fl >> (8 * slot)) & 0xFFu;
+                return (base + (uint32_t)slot) | ((f & 1u) << 31) | ((f & 2u) << 29) | ((f & 4u) << 27);
+            };
+#pragma unroll
+            for (int j = 3; j >= 1; --j) {
+                if (j < h) {
+                    sl[sp * 64 + lane] = link(ks[j]);
+                    st[sp * 64 + lane] = (unsigned short)(__float_as_uint(k[j]) >> 16);
+                    ++sp;
+                }
+            }
+            cur = link(ks[0]);
+            pop = false;
+        }
+    }
+    if (pop) {
+        const float thr = closest * kRelax + kRelaxAbs;
+        for (;;) {
+            if (sp == 0) return false;
+            --sp;
+            const uint32_t l = sl[sp * 64 + lane];
+            if ((l & (kWThin | kWWider)) || __uint_as_float((uint32_t)st[sp * 64 + lane] << 16) <= thr) {
+                cur = l;
+                break;
+            }
+        }
+    }
+    return true;
+}
+
 // ------------------------------------------------------------ frontier walk --
 //
 // The whole wave walks ONE ray (arguments wave-uniform), like coop_walk, but
@@ -778,6 +924,8 @@ constexpr int kFeatQ2 = 8192;     // split launch, kernel 2: the slotted paths f
                                   //   64 per wave in slot order
 constexpr int kFeatHalf = 2048;   // option accel_half (with kFeatAccel): 16-B slots, half-precision internal
                                   //   boxes (accel_build.h format 1)
+constexpr int kFeatWide = 1024;   // option accel_wide (with kFeatAccel): the 4-wide tree (accel_build.h format 2),
+                                  //   children ordered by t_enter, a per-lane LDS stack (wide_step)
 constexpr int kFeatAccel = 512;   // option accel: the accel records and rules, packed records, the
                                   //   reference-order fallback
 constexpr unsigned kHeavyLaneMark = kLearnHeavyMark;   // rt_internal.h
@@ -874,6 +1022,7 @@ void trace_simple(TraceArgs a) {
     // reads them always.
     constexpr bool ACC = (FEAT & kFeatAccel) != 0;
     constexpr bool HALF = ACC && (FEAT & kFeatHalf) != 0;
+    constexpr bool WIDE = ACC && (FEAT & kFeatWide) != 0;
     constexpr bool PAD = !ACC && ((FEAT & kFeatPad) || (FEAT & (kFeatExt | kFeatFrontier)) || !(FEAT & kFeatCoopTail));
     constexpr bool Q1 = (FEAT & kFeatQ1) != 0, Q2 = (FEAT & kFeatQ2) != 0;
     const int lane = threadIdx.x & 63;
@@ -1053,6 +1202,11 @@ void trace_simple(TraceArgs a) {
         }
         bool nleaf = a.scene.root_leaf != 0;
         bool walking = alive && end > 0;
+        // the wide walk (kFeatWide): the record to read next (a child link:
+        // index | flags), the lane's stack depth, and an overflowed stack
+        uint32_t wcur = a.scene.root_leaf ? kWLeaf : 0u;
+        int wsp = 0;
+        bool wovf = false;
         if (COUNT && alive) {
             ++c_seg;
             if (end > 0) ++c_node;                                       // the root visit
@@ -1072,9 +1226,12 @@ void trace_simple(TraceArgs a) {
             // half-format walk uses it whatever RT_CHAIN is
             const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc(
                 const_cast<float4*>(wr), 0,
-                HALF ? (int)((unsigned)(a.scene.end2 + 4) * 16u) : (int)((unsigned)(a.scene.end2 + 2) * 32u),
+                WIDE ? (int)((unsigned)(a.scene.end2 + 1) * 64u)
+                     : HALF ? (int)((unsigned)(a.scene.end2 + 4) * 16u) : (int)((unsigned)(a.scene.end2 + 2) * 32u),
                 0x00020000);
-            if (HALF && walking) {
+            if (WIDE) {
+                // no prefetch: a step reads its record at the top
+            } else if (HALF && walking) {
                 A = hbuf(wrs, n);
                 if (nleaf) {
                     B = hbuf(wrs, n + 1);
@@ -1091,6 +1248,11 @@ void trace_simple(TraceArgs a) {
             }
             while (walking) {
                 if (DIAG) ++d_iters;
+                if (WIDE) {
+                    walking = wide_step<COUNT>(wrs, fr + (size_t)wave * (kWideStackK * 64 * 6 / 16), o, d, inv, closest,
+                                               hit, incons, wcur, wsp, wovf, c_node, c_tri);
+                    continue;
+                }
                 if (WALK == 0) {
                     n = node_step<COUNT>(nodes, leafs, n, nleaf, o, d, inv, closest, hit, c_node, c_tri);
                 } else if (HALF) {
@@ -1282,7 +1444,7 @@ void trace_simple(TraceArgs a) {
             // is the one case where the reference's result depends on its
             // visit order; such a segment is walked again, in the reference's
             // order over the reference's records, by the whole wave.
-            uint64_t redo = __ballot(alive && hit >= 0 && incons);
+            uint64_t redo = __ballot(alive && ((hit >= 0 && incons) || (WIDE && wovf)));
             while (redo != 0) {
                 const int L = __ffsll((long long)redo) - 1;
                 redo &= redo - 1;
@@ -1468,14 +1630,17 @@ hipError_t launch_trace(const TraceArgs& a, hipStream_t stream, int* kernels) {
         }
     }
     const size_t shm_f = (size_t)bw * kFCap * sizeof(uint4);   // kFeatFrontier variants only
+    const size_t shm_w = (size_t)bw * kWideStackK * 64 * 6;       // kFeatWide: the lanes' stacks
+#define RT_SHM(F) (((F) & kFeatFrontier) ? shm_f : ((F) & kFeatWide) ? shm_w : 0)
 #define RT_SIMPLE(F, W)                                                                                         \
-    if (a.diag) hipLaunchKernelGGL((trace_simple<false, true, F, W>), grid, block, ((F) & kFeatFrontier) ? shm_f : 0, stream, ao);           \
-    else if (a.counters) hipLaunchKernelGGL((trace_simple<true, false, F, W>), grid, block, ((F) & kFeatFrontier) ? shm_f : 0, stream, ao); \
-    else hipLaunchKernelGGL((trace_simple<false, false, F, W>), grid, block, ((F) & kFeatFrontier) ? shm_f : 0, stream, ao);
+    if (a.diag) hipLaunchKernelGGL((trace_simple<false, true, F, W>), grid, block, RT_SHM(F), stream, ao);           \
+    else if (a.counters) hipLaunchKernelGGL((trace_simple<true, false, F, W>), grid, block, RT_SHM(F), stream, ao); \
+    else hipLaunchKernelGGL((trace_simple<false, false, F, W>), grid, block, RT_SHM(F), stream, ao);
     if (a.scene.n_layouts > 0) {
         // option accel (walk 2 records; the launcher never splits heavy tiles
         // or pixels out of an accel launch, and there is no frontier tail)
         if (a.q_slots && a.split_bounce > 0 && a.split_bounce < a.max_bounces && feat == 0 && !a.scene.half &&
+            !a.scene.wide &&
             !a.diag && !a.counters && (int)(grid.x * grid.y) * bw <= a.q_waves) {
             // split launch: kernel 1 to bounce split_bounce,
             // the scan of its per-wave counts, kernel 2 for the rest
@@ -1492,6 +1657,16 @@ hipError_t launch_trace(const TraceArgs& a, hipStream_t stream, int* kernels) {
             hipLaunchKernelGGL((trace_simple<false, false, kFeatAccel | kFeatQ2, 2>), dim3(a.q_grid), dim3(64), 0,
                                stream, a2);
             if (kernels) *kernels = 2;                          // the frame kernels (q_scan aside)
+            return hipGetLastError();
+        }
+        if (a.scene.wide) {
+            // format 2 records: no cooperative tail (set_schedule: coop_lanes 0)
+            if (feat & kFeatCoopTail) {
+                set_error("accel_wide launch with coop_lanes %d", a.coop_lanes);
+                return hipErrorInvalidValue;
+            }
+            if (feat & kFeatExt) RT_SIMPLE(kFeatExt | kFeatAccel | kFeatWide, 2)
+            else RT_SIMPLE(kFeatAccel | kFeatWide, 2)
             return hipGetLastError();
         }
         if (a.scene.half) {
@@ -1533,6 +1708,7 @@ hipError_t launch_trace(const TraceArgs& a, hipStream_t stream, int* kernels) {
         }
     }
 #undef RT_SIMPLE
+#undef RT_SHM
 #undef RT_FUSED_BIG
 #undef RT_FUSED
     if (join) {

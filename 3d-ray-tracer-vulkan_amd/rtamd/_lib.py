@@ -195,12 +195,14 @@ def check(rc: int) -> None:
 
 
 RT_ACCEL_FORMAT_HALF = 0x100
+RT_ACCEL_FORMAT_WIDE = 0x200
 
 
-def accel_records(built, n_layouts: int = 8, half: bool = False):
+def accel_records(built, n_layouts: int = 8, half: bool = False, wide: bool = False):
     """Option accel's records for a BuiltCpuData (rt_accel_records): returns
-    (uint32[slots_total * 8] (half: * 4, option accel_half's format), info
-    dict).  Host-only; no device needed."""
+    (uint32[slots_total * 8] (half: * 4, option accel_half's format; wide: *
+    16, option accel_wide's 64-B records), info dict).  Host-only; no device
+    needed."""
     import numpy as np
     L = lib()
     bufs = [np.ascontiguousarray(np.frombuffer(bytes(x), dtype=np.uint8)) if isinstance(x, (bytes, bytearray))
@@ -211,11 +213,11 @@ def accel_records(built, n_layouts: int = 8, half: bool = False):
         args += [b.ctypes.data, b.nbytes]
     n = C.c_size_t(0)
     info = (C.c_int32 * 8)()
-    nl = n_layouts | (RT_ACCEL_FORMAT_HALF if half else 0)
+    nl = n_layouts | (RT_ACCEL_FORMAT_HALF if half else 0) | (RT_ACCEL_FORMAT_WIDE if wide else 0)
     check(L.rt_accel_records(*args, nl, None, 0, C.byref(n), info))
     out = np.zeros(n.value, dtype=np.uint32)
     check(L.rt_accel_records(*args, nl, out.ctypes.data_as(C.POINTER(C.c_uint32)), out.size, C.byref(n), info))
     keys = ("n_layouts", "slots", "root_leaf", "n_prims", "n_inputs", "depth", "max_class", "n_thin")
     d = dict(zip(keys, list(info)))
-    d["format"] = 1 if half else 0
+    d["format"] = 1 if half else (2 if wide else 0)
     return out, d

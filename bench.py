@@ -1187,7 +1187,8 @@ def main() -> None:
     n_cu = torch.cuda.get_device_properties(dev).multi_processor_count
     # PMC only from a record of this config and camera path (pmc_key)
     pmc = load_pmc(args.pmc_json, pmc_key(cfg.name, args.camera_path, renderer.get_option("accel_used"),
-                                         renderer.get_option("accel_half_used"), F)) \
+                                         renderer.get_option("accel_half_used"), F,
+                                         renderer.get_option("accel_wide_used"))) \
         if mode == "whole" else None
     walk_mb = round(renderer.walk_bytes() / 2**20, 2)
     roof = roofline(pmc, alg_bytes, ref_layout_bytes, l_seg, launch_ms, frame_ms, n_cu, lanes, walk_mb)
@@ -1272,7 +1273,8 @@ def main() -> None:
                                                                       "coop_window", "coop_window_used",
                                                                       "leaf_align", "leaf_align_used",
                                                                       "accel", "accel_used", "accel_half",
-                                                                      "accel_half_used", "split_bounce",
+                                                                      "accel_half_used", "accel_wide",
+                                                                      "accel_wide_used", "split_bounce",
                                                                       "wave_tile_used")},
                              "concurrent_launches": renderer.get_option("concurrent_launches"),
                              "heavy_tiles_used": heavy_used,
@@ -1387,14 +1389,16 @@ def lane_utilisation(renderer, L, ctx, launch, dev):
                     "coop_windows = 64-node windows of the cooperative tail"}
 
 
-def pmc_key(config_name: str, camera_path: str, accel: int = 0, half: int = 0, frames: int = 1) -> str:
+def pmc_key(config_name: str, camera_path: str, accel: int = 0, half: int = 0, frames: int = 1,
+            wide: int = 0) -> str:
     """The key of a PMC record in profiles/pmc_latest.json: the config, the
     camera path unless it is the static default camera, the accel layouts
     unless the scene runs the reference's own tree (accel 0; round 4's
-    records), with "h" for option accel_half's records, and "@f<F>" for
-    launches of F > 1 frames (a record is per launch)."""
+    records), with "h" for option accel_half's records and "w" for option
+    accel_wide's, and "@f<F>" for launches of F > 1 frames (a record is per
+    launch)."""
     k = config_name if camera_path == "static" else f"{config_name}@{camera_path}"
-    k = f"{k}@accel{accel}{'h' if half else ''}" if accel else k
+    k = f"{k}@accel{accel}{'h' if half else ''}{'w' if wide else ''}" if accel else k
     return f"{k}@f{frames}" if frames > 1 else k
 
 

@@ -474,7 +474,9 @@ int rt_scene_validate(const void* vertices, size_t vertex_bytes,
  * pairs, n_layouts (1, or 8 = one per ray-direction octant) near-first
  * preorder layouts in the walk-record format, 8 32-bit words per 32-B slot;
  * n_layouts | RT_ACCEL_FORMAT_HALF: option accel_half's format, 4 words per
- * 16-B slot, internal boxes in half precision rounded outward.
+ * 16-B slot, internal boxes in half precision rounded outward;
+ * n_layouts | RT_ACCEL_FORMAT_WIDE: option accel_wide's 4-wide tree, one
+ * layout of 64-B records (16 words; "slots" = records).
  * Writes up to cap_words words (out_words may be NULL to size the call) and
  * *n_words = the words of the records (n_layouts * slots, + 64 B of padding);
  * info (nullable) receives {n_layouts, slots per layout, root is a leaf,
@@ -497,6 +499,7 @@ int rt_pack_rgb(const void* d_rgba, void* d_rgb, size_t n_px, void* stream);
 int rt_unpack_rgb(const void* d_rgb, void* d_rgba, size_t n_px, void* stream);
 
 #define RT_ACCEL_FORMAT_HALF 0x100
+#define RT_ACCEL_FORMAT_WIDE 0x200
 int rt_accel_records(const void* vertices, size_t vertex_bytes,
                      const void* materials, size_t material_bytes,
                      const void* bvh_nodes, size_t bvh_bytes, int n_layouts,

@@ -50,6 +50,9 @@ def lib(envelope: bool = False, accel: bool = False) -> C.CDLL:
             _accel_lib.orc_accel_audit.argtypes = [C.c_int]
             _accel_lib.orc_accel_audit_get.argtypes = [C.POINTER(C.c_double)]
             _accel_lib.orc_accel_relax_half.argtypes = [C.c_float]
+            _accel_lib.orc_accel_overflows.restype = C.c_uint64
+            _accel_lib.orc_accel_stack.argtypes = [C.c_int]
+            _accel_lib.orc_accel_count_steps.argtypes = [C.c_int]
             _accel_lib.orc_accel_audit_bins.argtypes = [C.POINTER(C.c_double), C.POINTER(C.c_double),
                                                         C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
         return _accel_lib
@@ -169,6 +172,7 @@ def render_accel(vertices, materials, nodes, camera_ubo: bytes, width: int, heig
         raise RuntimeError(f"orc_render_profile (accel) failed ({rc})")
     cd = c.as_dict()
     cd["fallbacks"] = int(L.orc_accel_fallbacks())
+    cd["overflows"] = int(L.orc_accel_overflows())
     if profile:
         return rgba, rad, cd, prof
     return rgba, rad, cd

@@ -97,10 +97,30 @@ uint64_t orc_accel_leaf_visits(void) {
     return f;
 }
 
-/* The format of the records the following renders walk: 0 or 1. */
+/* The format of the records the following renders walk: 0, 1 or 2. */
 int orc_accel_format(int fmt) {
-    if (fmt != 0 && fmt != 1) return -2;
+    if (fmt < 0 || fmt > 2) return -2;
     g_fmt = fmt;
+    return 0;
+}
+
+/* Format 2's per-lane stack (entries; accel_build.h kWideStack) and the
+ * segments whose stack overflowed (walked again in the reference's order). */
+static int g_stack_k = 12;
+static uint64_t g_overflows = 0;
+static int g_count_steps = 0;          /* analysis: node_visits counts record fetches */
+int orc_accel_stack(int k) {
+    if (k < 1 || k > 64) return -2;
+    g_stack_k = k;
+    return 0;
+}
+uint64_t orc_accel_overflows(void) {
+    const uint64_t f = g_overflows;
+    g_overflows = 0;
+    return f;
+}
+int orc_accel_count_steps(int on) {
+    g_count_steps = on;
     return 0;
 }
 
@@ -305,9 +325,164 @@ static void audit_segment(const scene* s, ray r) {
     }
 }
 
+/* Format 2 (accel_build.h): the 4-wide walk.  Each step fetches one 64-B
+ * record.  A leaf: hit_triangle on its v0 / e1 / e2; only a hit the walk would
+ * take (t < closest_t, or a tie with a lower index) reads the rest of the
+ * leaf's exact box and runs its slab test (the reference's hit_aabb
+ * arithmetic) with the leaf's rule, which decides.  A wide node: each child's
+ * box decoded from the node's grid (origin + q 2^e in float) and slab-tested
+ * with the child's rule; the entered children in (t_enter, slot) order, the
+ * first next, the rest pushed farthest first on a stack of g_stack_k entries
+ * (an overflow walks the segment again in the reference's order).  A stack
+ * entry keeps its t_enter rounded down to bfloat16 (the kernel's 2-byte LDS
+ * field); a popped default-margin entry whose rounded-down t_enter fails the
+ * rule is dropped.  node_visits = 1 (the root) + box tests (children and leaf
+ * boxes), tri_tests = leaf records read; g_count_steps: node_visits counts
+ * record fetches instead (analysis). */
+static float rec_f16(size_t idx, int w) {
+    float f;
+    memcpy(&f, &g_rec[16 * idx + (size_t)w], 4);
+    return f;
+}
+
+static void slab3(vec3 lo, vec3 hi, ray r, vec3 inv, float* te, float* tx) {
+    const vec3 t0s = mul3(sub3(lo, r.origin), inv);
+    const vec3 t1s = mul3(sub3(hi, r.origin), inv);
+    *te = fmaxf(fmaxf(fminf(t0s.x, t1s.x), fminf(t0s.y, t1s.y)), fminf(t0s.z, t1s.z));
+    *tx = fminf(fminf(fmaxf(t0s.x, t1s.x), fmaxf(t0s.y, t1s.y)), fmaxf(t0s.z, t1s.z));
+}
+
+static float bf16_down(float x) {            /* truncated to bfloat16: down for x >= 0 */
+    uint32_t u;
+    memcpy(&u, &x, 4);
+    u &= 0xFFFF0000u;
+    memcpy(&x, &u, 4);
+    return x;
+}
+
+#define WIDE_LEAF (1u << 31)
+#define WIDE_THIN (1u << 30)
+#define WIDE_WIDER (1u << 29)
+#define WIDE_IDX 0x07FFFFFFu
+
+static int wide_walk(const scene* s, ray r, float* closest_t, int* hit_index, vec3* hit_normal, orc_counts* cnt) {
+    const vec3 inv = v3(rcp(r.dir.x), rcp(r.dir.y), rcp(r.dir.z));
+    float c = *closest_t;
+    float hit_te = 0.0f;
+    int hit = -1;
+    uint32_t st_link[64];
+    float st_te[64];
+    int sp = 0, overflow = 0;
+    uint32_t cur = g_root_leaf ? WIDE_LEAF : 0u;
+    if (!g_count_steps) cnt->node_visits++;      /* the root visit (the kernel counts it at segment start) */
+    for (;;) {
+        const size_t idx = cur & WIDE_IDX;
+        if ((size_t)idx >= (size_t)g_slots) return -1;
+        const uint32_t* w = &g_rec[16 * idx];
+        if (g_count_steps) cnt->node_visits++;
+        if (cur & WIDE_LEAF) {
+            const int tri = (int)(w[0] & 0x1FFFFFFFu);
+            cnt->tri_tests++;
+            if ((size_t)tri >= s->n_tris || (size_t)tri >= s->n_mats) return -1;
+            vec3 nrm;
+            float t = INFINITY;
+            if (hit_triangle(r, vertex_pos(s, (size_t)tri * 3 + 0), vertex_pos(s, (size_t)tri * 3 + 1),
+                             vertex_pos(s, (size_t)tri * 3 + 2), &t, &nrm) &&
+                (t < c || (t == c && tri < hit))) {
+                if (!g_count_steps) cnt->node_visits++;
+                float te, tx;
+                slab3(v3(rec_f16(idx, 7), rec_f16(idx, 11), rec_f16(idx, 12)),
+                      v3(rec_f16(idx, 13), rec_f16(idx, 14), rec_f16(idx, 15)), r, inv, &te, &tx);
+                const float rf = (w[0] & (1u << 29)) ? INFINITY : g_relax;
+                if (tx > te && tx > T_MIN && te <= c * rf + g_relax_abs) {
+                    c = t;
+                    hit = tri;
+                    hit_te = te;
+                    *hit_normal = nrm;
+                }
+            }
+        } else {
+            const int n = (int)((w[3] >> 24) & 7u);
+            const vec3 org = v3(rec_f16(idx, 0), rec_f16(idx, 1), rec_f16(idx, 2));
+            const int ex = (int8_t)(w[3] & 0xFFu), ey = (int8_t)((w[3] >> 8) & 0xFFu), ez = (int8_t)((w[3] >> 16) & 0xFFu);
+            const float sx = ldexpf(1.0f, ex), sy = ldexpf(1.0f, ey), sz = ldexpf(1.0f, ez);
+            const float nr = class_relax((int)(w[10] >> 27));
+            const uint32_t base = w[10] & WIDE_IDX;
+            float ce[4];
+            uint32_t cl[4];
+            int h = 0;
+            for (int i = 0; i < n; ++i) {
+                const int sh = 8 * i;
+                const vec3 lo = v3(org.x + (float)((w[4] >> sh) & 0xFFu) * sx, org.y + (float)((w[5] >> sh) & 0xFFu) * sy,
+                                   org.z + (float)((w[6] >> sh) & 0xFFu) * sz);
+                const vec3 hi = v3(org.x + (float)((w[7] >> sh) & 0xFFu) * sx, org.y + (float)((w[8] >> sh) & 0xFFu) * sy,
+                                   org.z + (float)((w[9] >> sh) & 0xFFu) * sz);
+                if (!g_count_steps) cnt->node_visits++;
+                float te, tx;
+                slab3(lo, hi, r, inv, &te, &tx);
+                const uint32_t f = (w[11] >> sh) & 0xFFu;
+                const uint32_t link = (base + (uint32_t)i) | ((f & 1u) ? WIDE_LEAF : 0u) | ((f & 2u) ? WIDE_THIN : 0u) |
+                                      ((f & 4u) ? WIDE_WIDER : 0u);
+                const float rf = (f & 2u) ? INFINITY : ((f & 4u) ? nr : g_relax);
+                if (tx > te && tx > T_MIN && te <= c * rf + g_relax_abs) {
+                    /* insert in (t_enter, slot) order: a later slot goes after an equal te */
+                    int k = h++;
+                    while (k > 0 && ce[k - 1] > te) {
+                        ce[k] = ce[k - 1];
+                        cl[k] = cl[k - 1];
+                        --k;
+                    }
+                    ce[k] = te;
+                    cl[k] = link;
+                }
+            }
+            if (h > 0) {
+                if (sp + h - 1 > g_stack_k) {
+                    overflow = 1;
+                    break;
+                }
+                for (int k = h - 1; k >= 1; --k) {
+                    st_link[sp] = cl[k];
+                    st_te[sp] = bf16_down(ce[k]);
+                    ++sp;
+                }
+                cur = cl[0];
+                continue;
+            }
+        }
+        int found = 0;
+        while (sp > 0) {
+            --sp;
+            const uint32_t link = st_link[sp];
+            if (!(link & (WIDE_THIN | WIDE_WIDER)) && !(st_te[sp] <= c * g_relax + g_relax_abs)) continue;
+            cur = link;
+            found = 1;
+            break;
+        }
+        if (!found) break;
+    }
+    if (overflow || (hit >= 0 && c < hit_te)) {
+#ifdef _OPENMP
+#pragma omp atomic
+#endif
+        g_fallbacks++;
+        if (overflow) {
+#ifdef _OPENMP
+#pragma omp atomic
+#endif
+            g_overflows++;
+        }
+        return reference_walk(s, r, closest_t, hit_index, hit_normal, cnt);
+    }
+    *closest_t = c;
+    *hit_index = hit;
+    return 0;
+}
+
 static int accel_walk(const scene* s, ray r, float* closest_t, int* hit_index, vec3* hit_normal,
                       orc_counts* cnt) {
     if (g_slots == 0) return 0;                 /* empty scene: every ray misses */
+    if (g_fmt == 2) return wide_walk(s, r, closest_t, hit_index, hit_normal, cnt);
     if (g_audit) audit_segment(s, r);
     const int oct = g_layouts == 8 ? ((signbit(r.dir.x) ? 1 : 0) | (signbit(r.dir.y) ? 2 : 0) |
                                       (signbit(r.dir.z) ? 4 : 0)) : 0;

@@ -19,8 +19,9 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 
 
 def _records(built, n_layouts, half=False):
+    """half: True = option accel_half's format, "wide" = option accel_wide's."""
     from rtamd import _lib
-    return _lib.accel_records(built, n_layouts, half)
+    return _lib.accel_records(built, n_layouts, half is True, half == "wide")
 
 
 def _frames(built, cam, w, h, b, n_layouts, tile=None, row_step=1, half=False):
@@ -157,7 +158,7 @@ def test_duplicates_dropped():
     assert info["n_inputs"] == 65536 and info["n_prims"] == 50014
 
 
-@pytest.mark.parametrize("nl,half", [(1, False), (8, False), (8, True)])
+@pytest.mark.parametrize("nl,half", [(1, False), (8, False), (8, True), (8, "wide")])
 @pytest.mark.parametrize("k,b,tile,row_step", [(1, 1, None, 1), (2, 2, None, 2), (2, 10, (400, 200, 480, 320), 1),
                                                  (3, 4, None, 24), (6, 4, None, 40)])
 def test_model_matches_oracle(k, b, tile, row_step, nl, half):
@@ -196,7 +197,7 @@ def _tie_scenes():
     return out
 
 
-@pytest.mark.parametrize("nl,half", [(1, False), (8, False), (8, True)])
+@pytest.mark.parametrize("nl,half", [(1, False), (8, False), (8, True), (8, "wide")])
 def test_model_ties(nl, half):
     from rtamd import configs
     for name, built in _tie_scenes().items():
@@ -388,3 +389,47 @@ def test_adversarial_study_claims():
                     worst = max(worst, a["audit"]["max_headroom"])
     assert slivers > 1000
     assert worst > 1.0
+
+
+@pytest.mark.parametrize("k", [1, 2, 3, 6])
+def test_wide_records(k):
+    """Option accel_wide's records (accel_build.h format 2): every child box,
+    decoded exactly as the kernel decodes it (origin + q 2^e in float),
+    holds the child's own box (a leaf's exact box, or the union of the
+    grandchildren's decoded boxes' true extents); children are contiguous
+    blocks; every primitive is reached exactly once."""
+    from rtamd import configs
+    built = configs.get(k).build()
+    rec, info = _records(built, 8, "wide")
+    w = rec.reshape(-1, 16)
+    n_rec = info["slots"]
+    assert info["n_layouts"] == 1 and w.shape[0] == n_rec + 1
+    f32 = lambda x: np.array(x, np.uint32).view(np.float32)   # noqa: E731
+
+    seen = []
+
+    def visit(i, leaf, lo_bound, hi_bound):
+        if leaf:
+            lo, hi = f32(w[i, [7, 11, 12]]), f32(w[i, 13:16])
+            assert (lo >= lo_bound).all() and (hi <= hi_bound).all(), (i, lo, lo_bound, hi, hi_bound)
+            seen.append(int(w[i, 0]) & 0x1FFFFFFF)
+            assert (int(w[i, 0]) >> 30) & 1
+            return
+        n = int(w[i, 3]) >> 24 & 7
+        assert 2 <= n <= 4
+        org = f32(w[i, 0:3])
+        assert (org >= lo_bound).all(), (i, org, lo_bound)      # the node's true lo inside its decoded box
+        e = [np.int8(np.uint8((int(w[i, 3]) >> (8 * q)) & 0xFF)) for q in range(3)]
+        sc = np.array([np.ldexp(np.float32(1.0), int(x)) for x in e], np.float32)
+        base = int(w[i, 10]) & 0x07FFFFFF
+        for c in range(n):
+            ql = np.array([(int(w[i, 4 + q]) >> (8 * c)) & 0xFF for q in range(3)], np.float32)
+            qh = np.array([(int(w[i, 7 + q]) >> (8 * c)) & 0xFF for q in range(3)], np.float32)
+            lo = (org + ql * sc).astype(np.float32)
+            hi = (org + qh * sc).astype(np.float32)
+            f = (int(w[i, 11]) >> (8 * c)) & 0xFF
+            visit(base + c, bool(f & 1), lo, hi)
+
+    root_leaf = bool(info["root_leaf"])
+    visit(0, root_leaf, np.full(3, -np.inf, np.float32), np.full(3, np.inf, np.float32))
+    assert len(seen) == info["n_prims"] == len(set(seen))

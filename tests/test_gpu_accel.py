@@ -30,14 +30,16 @@ def _oracle(built, cam, w, h, b, **kw):
                              cam.ubo_bytes(), w, h, b, **kw)
 
 
-# A layout spec: 1 or 8 layouts; 108 = 8 layouts in option accel_half's format.
+# A layout spec: 1 or 8 layouts; 108 = 8 layouts in option accel_half's format;
+# 208 = option accel_wide's 4-wide tree (one layout).
 HALF8 = 108
+WIDE = 208
 
 
 def _model(built, cam, w, h, b, nl, **kw):
     from oracle import oracle_lib
     from rtamd import _lib
-    rec, info = _lib.accel_records(built, nl % 100, nl >= 100)
+    rec, info = _lib.accel_records(built, nl % 100, 100 <= nl < 200, nl >= 200)
     return oracle_lib.render_accel(built.model_vertex_data, built.model_material_data, built.flat_bvh_data,
                                    cam.ubo_bytes(), w, h, b, rec, info, **kw)
 
@@ -55,16 +57,19 @@ def _check(rgba, rad, st, ref, model=None, what=""):
 
 def _upload(r, built, nl):
     r.set_option("accel", nl % 100)
-    r.set_option("accel_half", 1 if nl >= 100 else 0)
+    r.set_option("accel_half", 1 if 100 <= nl < 200 else 0)
+    r.set_option("accel_wide", 1 if nl >= 200 else 0)
     try:
         r.upload_scene(built)
     finally:
         r.set_option("accel_half", 0)
-    assert r.get_option("accel_used") == nl % 100
-    assert r.get_option("accel_half_used") == (1 if nl >= 100 else 0)
+        r.set_option("accel_wide", 0)
+    assert r.get_option("accel_used") == (1 if nl >= 200 else nl % 100)
+    assert r.get_option("accel_half_used") == (1 if 100 <= nl < 200 else 0)
+    assert r.get_option("accel_wide_used") == (1 if nl >= 200 else 0)
 
 
-@pytest.mark.parametrize("nl", [1, 8, HALF8])
+@pytest.mark.parametrize("nl", [1, 8, HALF8, WIDE])
 @pytest.mark.parametrize("k,b", [(1, 1), (2, 2), (2, 10), (3, 4), (6, 4)])
 def test_accel_full_frame(acc, k, b, nl):
     """Whole frames of configs 1, 2, 3 and 6: frames equal the oracle's, the
@@ -81,7 +86,7 @@ def test_accel_full_frame(acc, k, b, nl):
         _check(rgba, rad, st, ref, model, f"config {k} b{b} layouts {nl}")
 
 
-@pytest.mark.parametrize("nl", [1, 8, HALF8])
+@pytest.mark.parametrize("nl", [1, 8, HALF8, WIDE])
 def test_accel_config5_strips(acc, nl):
     """Config 5 (1M triangles, 3840x2160, 8 bounces, all material types):
     three 64-row strips through rt_render_tile_device."""
@@ -109,7 +114,7 @@ def _tie_scenes():
     return M._tie_scenes()
 
 
-@pytest.mark.parametrize("nl", [1, 8, HALF8])
+@pytest.mark.parametrize("nl", [1, 8, HALF8, WIDE])
 def test_accel_ties_and_fallback(acc, nl):
     """Scenes built to tie: every triangle twice in two colours, an integer
     grid of coplanar and coincident faces, the cube's faces split both ways.
@@ -155,7 +160,7 @@ def test_accel_empty_and_tiny_scenes(acc):
     verts, mats = triangles_of(configs.config2().scene)
     for n in (0, 1, 2, 3):
         built = build_buffers(verts[:n], mats[:n])
-        for nl in (1, 8, HALF8):
+        for nl in (1, 8, HALF8, WIDE):
             _upload(acc, built, nl)
             for (w, h, b) in [(37, 23, 3), (1, 1, 1)]:
                 cam = configs.Camera.default(w, h)
@@ -164,7 +169,7 @@ def test_accel_empty_and_tiny_scenes(acc):
                 _check(rgba, rad, st, ref, _model(built, cam, w, h, b, nl), f"{n} triangles")
 
 
-@pytest.mark.parametrize("nl", [1, HALF8])
+@pytest.mark.parametrize("nl", [1, HALF8, WIDE])
 def test_accel_extensions(acc, nl):
     """The non-reference extensions run over the accel walk too (sky toggle,
     emissive, spheres); frames equal the oracle's extension build."""
@@ -190,7 +195,7 @@ def test_accel_extensions(acc, nl):
         acc.upload_spheres(np.zeros((0, 8), np.float32))
 
 
-@pytest.mark.parametrize("nl", [8, HALF8])
+@pytest.mark.parametrize("nl", [8, HALF8, WIDE])
 @pytest.mark.parametrize("cfg_k", [3, 4, 5, 6])
 def test_accel_bench_setting_whole_frame(acc, cfg_k, nl):
     """BASELINE configs 3, 4, 5 (1M triangles, 3840x2160, 8 bounces) and 6 as
