@@ -303,6 +303,7 @@ struct PerDevice {
     int*         h_nhpix = nullptr;           // pinned
     hipEvent_t   learn_ev = nullptr;
     bool         learn_busy = false;          // a device learning is in flight (its order pending)
+    bool         learn_oom = false;           // device learning's scratch did not fit: learn on the host
     bool         learning_device = false;     // the learning launch being planned learns on the device
     int          learning_rec_off = 0;        // its heavy-pixel waves ahead of the tile records
     // option heavy_tiles: auxiliary streams (round robin) for the concurrent heavy-tile launch
@@ -342,6 +343,8 @@ static constexpr int    kMaxHeavy = 256;
 // 28.5 GB per frame at the same frame time; config 3 (6.3 MB, L2-resident)
 // is 1.2% faster with 64 (profiles/r04/r4f).
 static constexpr size_t kWin32Bytes = 32ull << 20;
+// option split_bounce: the largest ray-slot allocation per launch stream
+static constexpr size_t kSplitSlotBytes = 256ull << 20;
 // The walk's buffer loads address the records with 32-bit byte offsets
 // (rt_trace.hip, RT_CHAIN 2): at most 2^27 - 4 slots of 32 B (~45M triangles).
 static constexpr unsigned kMaxWalkSlots = (1u << 27) - 4;
@@ -610,7 +613,7 @@ static int plan_order(const rt_ctx* ctx, PerDevice& p, TraceArgs& a, const rt_ca
     // on its stream afterwards with no synchronisation; one learning at a
     // time per device.  Other schedules learn on the host (learn_order).
     const bool device = ctx->learn_device && ctx->heavy_stream == 2 && ctx->heavy_pixels && ctx->heavy_tiles < 0 &&
-                        !ctx->order_frames;
+                        !ctx->order_frames && !p.learn_oom;
     if (p.learn_busy) return reuse ? use(*reuse) : RT_OK;   // the device learning in flight finishes first
     // a fused launch's heavy-pixel waves record first: at most one per resident
     // wave slot (the largest cap any concurrency gives)
@@ -655,11 +658,19 @@ static int learn_order_device(const rt_ctx* ctx, PerDevice& p, hipStream_t s) {
     const int conc = std::max(1, concurrency(ctx));
     const int cap = std::max(1, p.n_cu * kResidentPerCu * ctx->heavy_cap / 100 / conc);
     const size_t need = learn_scratch_bytes((int)n);
+    // Out of device memory for the learning's scratch (it sorts a 64-bit key
+    // per pixel): no order from this launch, and later launches learn on the
+    // host (advisor, round 5: a plain render must not fail on it).
+    const auto oom = [&p]() {
+        (void)hipGetLastError();
+        p.learn_oom = true;
+        return RT_OK;
+    };
     if (need > p.learn_scratch_cap) {
         if (p.d_learn_scratch) (void)hipFree(p.d_learn_scratch);
         p.d_learn_scratch = nullptr;
         p.learn_scratch_cap = 0;
-        RT_HIP_CHECK(hipMalloc(&p.d_learn_scratch, need));
+        if (hipMalloc(&p.d_learn_scratch, need) != hipSuccess) return oom();
         p.learn_scratch_cap = need;
     }
     if (!p.h_nhpix) RT_HIP_CHECK(hipHostMalloc(&p.h_nhpix, sizeof(int), hipHostMallocPortable));
@@ -673,7 +684,7 @@ static int learn_order_device(const rt_ctx* ctx, PerDevice& p, hipStream_t s) {
     const size_t b_order = up(n * sizeof(int)), b_mask = up(n * sizeof(unsigned long long));
     const size_t b_hpix = up((size_t)cap * sizeof(int));
     PerDevice::Order o{p.learning_key, nullptr, n, 0, nullptr, 0, nullptr};
-    RT_HIP_CHECK(hipMalloc(&o.d_base, b_order + b_mask + b_hpix + sizeof(int)));
+    if (hipMalloc(&o.d_base, b_order + b_mask + b_hpix + sizeof(int)) != hipSuccess) return oom();
     char* base = static_cast<char*>(o.d_base);
     o.d_order = reinterpret_cast<int*>(base);
     o.d_mask = reinterpret_cast<unsigned long long*>(base + b_order);
@@ -946,7 +957,10 @@ static int attach_slots(const rt_ctx* ctx, PerDevice& p, TraceArgs& a, hipStream
     const int tw_w = 8 << a.wave_tile, th_w = 8 >> a.wave_tile, bw = std::max(1, a.block_waves);
     const long long waves = (long long)((a.tw + bw * tw_w - 1) / (bw * tw_w)) * bw *
                             ((a.th + th_w - 1) / th_w) * (long long)a.n_frames;
-    if (waves > (1 << 24)) return RT_OK;
+    // 3 KB of ray slots per wave (64 x 48 B): a one-frame 4K launch needs
+    // ~400 MB.  Past kSplitSlotBytes the launch stays one kernel (advisor,
+    // round 5: the slots only grow, per stream).
+    if (waves > (1 << 24) || (size_t)waves * 64 * 48 > kSplitSlotBytes) return RT_OK;
     PerDevice::Slots* q = nullptr;
     for (auto& x : p.slots)
         if (x.s == s) { q = &x; break; }

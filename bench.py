@@ -423,7 +423,8 @@ def main() -> None:
     from rtamd import configs
     from rtamd._lib import CameraUBO, Stats, check
     from rtamd import dist as rdist
-    from rtamd.dist import (SharePlan, ShareTracer, SpanPlan, SpanTracer, TilePlan, assemble_shares, band_list,
+    from rtamd.dist import (SharePlan, ShareTracer, SpanPlan, SpanTracer, TilePlan, assemble_shares, assemble_tiles,
+                            band_list,
                             gather_stack, gather_tiles)
 
     rank = int(os.environ.get("RANK", "0"))
@@ -579,9 +580,14 @@ def main() -> None:
         # the bytes RCCL's receives write); rank r: its span read once (the send)
         emu_buf = torch.zeros((plan.per_rank, W, 3 if wire_rgb else 4), dtype=torch.uint8, device=dev)
         emu_land = torch.empty_like(emu_buf)
+    elif emu and mode == "tiles":
+        # rank 0: the other ranks' tiles land in a stack (the bytes RCCL's gather
+        # writes), then the assembly; rank r: its tiles read once (the send)
+        emu_t = torch.empty_like(rgba_slots[0])
+        emu_tr = torch.empty_like(rad_slots[0]) if rad_on else None
     elif emu:
         if mode not in ("bands", "pieces"):
-            raise SystemExit("BENCH_EMULATE emulates --partition bands / pieces / spans")
+            raise SystemExit("BENCH_EMULATE emulates --partition bands / pieces / spans / tiles")
         emu_buf = torch.zeros((world * plan.per_rank, W, 4) if rank == 0 else (1,), dtype=torch.uint8, device=dev)
         emu_land = torch.empty_like(emu_buf if rank == 0 else rgba_slots[0])
     streams = [torch.cuda.Stream(dev) for _ in range(D)]
@@ -711,6 +717,22 @@ def main() -> None:
                 dist.gather(rgba_slots[h], [emu_land])
                 out = None
             rad = None
+        elif emu and mode == "tiles":
+            out = rad = None
+            if os.environ.get("BENCH_EMULATE_NOX") == "1":
+                pass
+            elif rank == 0:
+                def land(local):
+                    stk = torch.empty((world,) + tuple(local.shape), dtype=local.dtype, device=local.device)
+                    for r in range(world):                 # its own tiles and the (world - 1) received ones
+                        stk[r].copy_(local)
+                    return assemble_tiles(stk, tplan, src_index)[:n]
+                out = land(rgba_slots[h])
+                rad = land(rad_slots[h]) if rad_on else None
+            else:
+                emu_t.copy_(rgba_slots[h])
+                if rad_on:
+                    emu_tr.copy_(rad_slots[h])
         elif mode == "tiles":
             out = gather_tiles(rgba_slots[h], tplan, src_index=src_index)
             rad = gather_tiles(rad_slots[h], tplan, src_index=src_index) if rad_on else None

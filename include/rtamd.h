@@ -277,7 +277,11 @@ int rt_render_poll(rt_ctx* ctx, uint64_t ticket, int* done);
  *                   so the few long late-bounce paths of a tile no longer hold
  *                   a whole wave; 0 (default) = one kernel.
  *                   Same frames; counting and diagnostic launches stay one
- *                   kernel
+ *                   kernel.  Memory: 3 KB of ray slots per wave of a launch
+ *                   (64 x 48 B), per launch stream, kept until rt_destroy; a
+ *                   launch that would need more than 256 MB (e.g. a batch of
+ *                   4K frames) stays one kernel.  Growing a stream's slots
+ *                   synchronises that stream
  *   "accel_half"    at the next rt_upload_scene, accel records with the
  *                   internal nodes' boxes in IEEE half precision rounded
  *                   outward (16-B internal records instead of 32; leaves keep

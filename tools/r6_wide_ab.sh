@@ -13,7 +13,7 @@ st() { echo "$(date +%T) $*" >> "$OUT/status.txt"; }
 chk() { local rc=$1; st "rc=$rc"; if [ "$rc" -ne 0 ] && [ "$rc" -ne 1 ]; then st "abort"; exit "$rc"; fi; }
 if [ "$TESTS" = 1 ]; then
   st "start pytest accel"
-  timeout -k 10 900 python -u -m pytest tests/test_gpu_accel.py -q -rA --timeout 300 --timeout-method thread \
+  timeout -k 10 900 python -u -m pytest tests/test_gpu_accel.py -q -rA --timeout 300 --timeout-method thread ${PYTEST_K:+-k "$PYTEST_K"} \
       > "$OUT/pytest_accel.log" 2>&1; chk $?
 fi
 for i in $(seq 1 "$REPS"); do
