@@ -1569,13 +1569,13 @@ static int device_band_list(PerDevice& p, const std::vector<int>& bands, const i
 static int render_rows_on(const rt_ctx* ctx, PerDevice& p, const rt_camera_ubo* cams, int n_frames, int width,
                           int height, int max_bounces, int band_h, int band_stride, int band_off,
                           const std::vector<int>* bands, int rows, uchar4* d_rgba, float* d_rad, hipStream_t s,
-                          bool count, int list_stride = 0) {
+                          bool count, int list_stride = 0, int x0 = 0, int y0 = 0, int tile_w = 0) {
     TraceArgs a;
     a.scene = p.scene;
     for (int f = 0; f < n_frames; ++f) a.cams[f] = cam_from_ubo(cams + f);
     a.n_frames = n_frames;
     a.width = width; a.height = height; a.max_bounces = max_bounces;
-    a.x0 = 0; a.y0 = 0; a.tw = width; a.th = rows;
+    a.x0 = x0; a.y0 = y0; a.tw = tile_w > 0 ? tile_w : width; a.th = rows;
     a.band_h = band_h; a.band_stride = band_stride; a.band_off = band_off;
     a.band_list = nullptr;
     a.list_stride = bands ? list_stride : 0;
@@ -1693,6 +1693,39 @@ int rt_render_batch_device(rt_ctx* ctx, const rt_camera_ubo* cams, int n_frames,
     if (stats) {
         RT_HIP_CHECK(hipEventSynchronize(p.ev1));
         return collect_stats(ctx, p, (uint64_t)rows * width * n_frames, stats, false);
+    }
+    return RT_OK;
+}
+
+int rt_render_batch_rect_device(rt_ctx* ctx, const rt_camera_ubo* cams, int n_frames, int width, int height,
+                                int max_bounces, int x0, int y0, int tile_w, int tile_h,
+                                void* d_out_rgba, void* d_out_radiance, void* stream, rt_stats* stats) {
+    int rc = check_render_args(ctx, cams, width, height, max_bounces, "rt_render_batch_rect_device");
+    if (rc) return rc;
+    if (n_frames < 1 || n_frames > kMaxBatch) {
+        set_error("rt_render_batch_rect_device: n_frames must be in [1, %d], got %d", kMaxBatch, n_frames);
+        return RT_ERR_INVALID_ARG;
+    }
+    if (x0 < 0 || y0 < 0 || tile_w < 0 || tile_h < 0 || x0 + tile_w > width || y0 + tile_h > height) {
+        set_error("rt_render_batch_rect_device: rectangle (%d, %d) %d x %d outside the %d x %d frame", x0, y0, tile_w,
+                  tile_h, width, height);
+        return RT_ERR_INVALID_ARG;
+    }
+    if (tile_w == 0 || tile_h == 0) {
+        if (stats) std::memset(stats, 0, sizeof *stats);
+        return RT_OK;
+    }
+    PerDevice& p = ctx->dev[0];
+    RT_HIP_CHECK(hipSetDevice(p.device));
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    // the rectangle's rows are one band of tile_h rows starting at y0
+    rc = render_rows_on(ctx, p, cams, n_frames, width, height, max_bounces, tile_h, 1, 0, nullptr, tile_h,
+                        static_cast<uchar4*>(d_out_rgba), static_cast<float*>(d_out_radiance), s, stats != nullptr, 0,
+                        x0, y0, tile_w);
+    if (rc) return rc;
+    if (stats) {
+        RT_HIP_CHECK(hipEventSynchronize(p.ev1));
+        return collect_stats(ctx, p, (uint64_t)tile_w * tile_h * n_frames, stats, false);
     }
     return RT_OK;
 }

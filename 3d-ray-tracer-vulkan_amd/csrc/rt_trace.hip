@@ -380,8 +380,18 @@ constexpr float kRelaxAbs = 1.0f / 1024.0f;
 constexpr uint32_t kThinLeaf = 1u << 29;
 __device__ __forceinline__ bool accel_enter(float te, float closest) { return te <= closest * kRelax + kRelaxAbs; }
 // The margin factor of the record whose words 3 and 7 are aw and bw.
+// (A/B builds: RT_THIN_MARGIN 0 = round 5's fixed factor, not exact for thin
+// triangles: make variant NAME=x FLAGS=-DRT_THIN_MARGIN=0)
+#ifndef RT_THIN_MARGIN
+#define RT_THIN_MARGIN 1
+#endif
 __device__ __forceinline__ float accel_factor(bool leaf, uint32_t aw, uint32_t bw) {
+#if RT_THIN_MARGIN
     return leaf ? ((aw & kThinLeaf) ? __builtin_inff() : kRelax) : __uint_as_float(bw);
+#else
+    (void)leaf; (void)aw; (void)bw;
+    return kRelax;
+#endif
 }
 __device__ __forceinline__ bool accel_enter_r(float te, float closest, float r) {
     return te <= closest * r + kRelaxAbs;
@@ -599,141 +609,118 @@ __device__ __forceinline__ float4 wrec(__amdgpu_buffer_rsrc_t r, int off) {
     return make_float4(__uint_as_float(v[0]), __uint_as_float(v[1]), __uint_as_float(v[2]), __uint_as_float(v[3]));
 }
 
-// The lane's stack: pop the next entry whose box would still be entered
-// (default-margin entries are dropped when their rounded-down t_enter fails
-// the rule); false when the stack runs dry.
-__device__ __forceinline__ bool wide_pop(const uint32_t* sl, const unsigned short* st, int lane, int& sp,
-                                         float closest, uint32_t& cur) {
-    const float thr = closest * kRelax + kRelaxAbs;
-    while (sp > 0) {
-        --sp;
-        const uint32_t l = sl[sp * 64 + lane];
-        if ((l & (kWThin | kWWider)) || __uint_as_float((uint32_t)st[sp * 64 + lane] << 16) <= thr) {
-            cur = l;
-            return true;
-        }
-    }
-    return false;
-}
-
-// One step of the wide walk over the record R0-R2 that cur names (loaded by
-// the previous step); returns whether the lane still walks.  The next
-// record's loads are issued as soon as it is known: before a leaf's triangle
-// test (the pop uses closest_t as it is before the test), and right after a
-// node's children are tested, before the pushes.
+// One step of the wide walk; returns whether the lane still walks.
 template <bool COUNT>
 __device__ __forceinline__ bool wide_step(__amdgpu_buffer_rsrc_t wrs, uint4* stk, V3 o, V3 d, V3 inv, float& closest,
-                                          int& hit, bool& incons, uint32_t& cur, int& sp, bool& ovf, float4& R0,
-                                          float4& R1, float4& R2, unsigned long long& c_node,
-                                          unsigned long long& c_tri) {
+                                          int& hit, bool& incons, uint32_t& cur, int& sp, bool& ovf,
+                                          unsigned long long& c_node, unsigned long long& c_tri) {
     const int lane = threadIdx.x & 63;
     uint32_t* sl = reinterpret_cast<uint32_t*>(stk);                                 // links
     unsigned short* st = reinterpret_cast<unsigned short*>(sl + kWideStackK * 64);   // bfloat16 t_enter
     const int off = (int)((cur & kWIdx) << 6);
+    const float4 R0 = wrec(wrs, off), R1 = wrec(wrs, off + 16), R2 = wrec(wrs, off + 32);
+    bool pop = true;
     if (cur & kWLeaf) {
-        const float4 P0 = R0, P1 = R1, P2 = R2;
-        const bool more = wide_pop(sl, st, lane, sp, closest, cur);
-        if (more) {
-            const int noff = (int)((cur & kWIdx) << 6);
-            R0 = wrec(wrs, noff);
-            R1 = wrec(wrs, noff + 16);
-            R2 = wrec(wrs, noff + 32);
-        }
         if (COUNT) ++c_tri;
-        const uint32_t w0 = __float_as_uint(P0.x);
+        const uint32_t w0 = __float_as_uint(R0.x);
         const int tri = (int)(w0 & 0x1FFFFFFFu);
         float t;
-        if (tri_test(make_float4(P0.y, P0.z, P0.w, 0.f), make_float4(P1.x, P1.y, P1.z, 0.f),
-                     make_float4(P2.x, P2.y, P2.z, 0.f), o, d, t) &&
+        if (tri_test(make_float4(R0.y, R0.z, R0.w, 0.f), make_float4(R1.x, R1.y, R1.z, 0.f),
+                     make_float4(R2.x, R2.y, R2.z, 0.f), o, d, t) &&
             accel_take(t, tri, closest, hit)) {
-            const float4 P3 = wrec(wrs, off + 48);
+            const float4 R3 = wrec(wrs, off + 48);
             if (COUNT) ++c_node;
             float te;
             bool ind;
-            slab(make_float4(P1.w, P2.w, P3.x, 0.f), make_float4(P3.y, P3.z, P3.w, 0.f), o, inv, te, ind);
+            slab(make_float4(R1.w, R2.w, R3.x, 0.f), make_float4(R3.y, R3.z, R3.w, 0.f), o, inv, te, ind);
             if (ind && accel_enter_r(te, closest, (w0 & kThinLeaf) ? __builtin_inff() : kRelax)) {
                 closest = t;
                 hit = tri;
                 incons = t < te;
             }
         }
-        return more;
-    }
-    const uint32_t w3 = __float_as_uint(R0.w);
-    const int n = (int)((w3 >> 24) & 7u);
-    const float sx = __builtin_ldexpf(1.0f, (int)(int8_t)(w3 & 0xFFu));
-    const float sy = __builtin_ldexpf(1.0f, (int)(int8_t)((w3 >> 8) & 0xFFu));
-    const float sz = __builtin_ldexpf(1.0f, (int)(int8_t)((w3 >> 16) & 0xFFu));
-    const uint32_t qlx = __float_as_uint(R1.x), qly = __float_as_uint(R1.y), qlz = __float_as_uint(R1.z);
-    const uint32_t qhx = __float_as_uint(R1.w), qhy = __float_as_uint(R2.x), qhz = __float_as_uint(R2.y);
-    const uint32_t w10 = __float_as_uint(R2.z), fl = __float_as_uint(R2.w);
-    const int cls = (int)(w10 >> 27);
-    const float nr = cls < 7 ? kRelax : 1.0f + __builtin_ldexpf(1.0f, cls - 16);
-    const uint32_t base = w10 & kWIdx;
-    if (COUNT) c_node += (unsigned long long)n;
-    // the children's (t_enter, slot) keys; not entered: +inf.  The decode
-    // and the slab run x and y in packed FP32 (each lane of v_pk_mul_f32 /
-    // v_pk_add_f32 rounds as the scalar operation does)
-    const f2 org = {R0.x, R0.y}, sxy = {sx, sy}, oxy = {o.x, o.y}, ixy = {inv.x, inv.y};
-    float k[4];
-    int ks[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const int sh = 8 * i;
-        const f2 lxy = org + f2{(float)((qlx >> sh) & 0xFFu), (float)((qly >> sh) & 0xFFu)} * sxy;
-        const f2 hxy = org + f2{(float)((qhx >> sh) & 0xFFu), (float)((qhy >> sh) & 0xFFu)} * sxy;
-        const float lz = R0.z + (float)((qlz >> sh) & 0xFFu) * sz, hz = R0.z + (float)((qhz >> sh) & 0xFFu) * sz;
-        const f2 t0 = (lxy - oxy) * ixy, t1 = (hxy - oxy) * ixy;
-        const float t0z = (lz - o.z) * inv.z, t1z = (hz - o.z) * inv.z;
-        const float te = fmaxf(fmaxf(fminf(t0.x, t1.x), fminf(t0.y, t1.y)), fminf(t0z, t1z));
-        const float tx = fminf(fminf(fmaxf(t0.x, t1.x), fmaxf(t0.y, t1.y)), fmaxf(t0z, t1z));
-        const bool ind = tx > te && tx > kTMin;
-        const uint32_t f = (fl >> sh) & 0xFFu;
-        const float rf = (f & 2u) ? __builtin_inff() : ((f & 4u) ? nr : kRelax);
-        k[i] = (i < n && ind && accel_enter_r(te, closest, rf)) ? te : __builtin_inff();
-        ks[i] = i;
-    }
-    // sort by (t_enter, slot): a five-comparator network; every key is
-    // distinct in slot, so the order is the model's insertion order
-#define RT_WCE(a, b)                                                                       \
-    {                                                                                      \
-        const bool sw = k[a] > k[b] || (k[a] == k[b] && ks[a] > ks[b]);                    \
-        const float tk = sw ? k[b] : k[a];                                                 \
-        k[b] = sw ? k[a] : k[b];                                                           \
-        k[a] = tk;                                                                         \
-        const int ts = sw ? ks[b] : ks[a];                                                 \
-        ks[b] = sw ? ks[a] : ks[b];                                                        \
-        ks[a] = ts;                                                                        \
-    }
-    RT_WCE(0, 1) RT_WCE(2, 3) RT_WCE(0, 2) RT_WCE(1, 3) RT_WCE(1, 2)
-#undef RT_WCE
-    const int h = (k[0] != __builtin_inff()) + (k[1] != __builtin_inff()) + (k[2] != __builtin_inff()) +
-                  (k[3] != __builtin_inff());
-    const auto link = [&](int slot) -> uint32_t {
-        const uint32_t f = (fl >> (8 * slot)) & 0xFFu;
-        return (base + (uint32_t)slot) | ((f & 1u) << 31) | ((f & 2u) << 29) | ((f & 4u) << 27);
-    };
-    if (h == 0) {
-        if (!wide_pop(sl, st, lane, sp, closest, cur)) return false;
     } else {
-        if (sp + h - 1 > kWideStackK) {
-            ovf = true;
-            return false;
-        }
-        cur = link(ks[0]);
-    }
-    {
-        const int noff = (int)((cur & kWIdx) << 6);
-        R0 = wrec(wrs, noff);
-        R1 = wrec(wrs, noff + 16);
-        R2 = wrec(wrs, noff + 32);
-    }
+        const uint32_t w3 = __float_as_uint(R0.w);
+        const int n = (int)((w3 >> 24) & 7u);
+        const float sx = __builtin_ldexpf(1.0f, (int)(int8_t)(w3 & 0xFFu));
+        const float sy = __builtin_ldexpf(1.0f, (int)(int8_t)((w3 >> 8) & 0xFFu));
+        const float sz = __builtin_ldexpf(1.0f, (int)(int8_t)((w3 >> 16) & 0xFFu));
+        const uint32_t qlx = __float_as_uint(R1.x), qly = __float_as_uint(R1.y), qlz = __float_as_uint(R1.z);
+        const uint32_t qhx = __float_as_uint(R1.w), qhy = __float_as_uint(R2.x), qhz = __float_as_uint(R2.y);
+        const uint32_t w10 = __float_as_uint(R2.z), fl = __float_as_uint(R2.w);
+        const int cls = (int)(w10 >> 27);
+        const float nr = cls < 7 ? kRelax : 1.0f + __builtin_ldexpf(1.0f, cls - 16);
+        const uint32_t base = w10 & kWIdx;
+        if (COUNT) c_node += (unsigned long long)n;
+        // the children's (t_enter, slot) keys; not entered: +inf.  The
+        // decode and the slab run x and y in packed FP32 (each lane of
+        // v_pk_mul_f32 / v_pk_add_f32 rounds as the scalar operation does)
+        const f2 org = {R0.x, R0.y}, sxy = {sx, sy}, oxy = {o.x, o.y}, ixy = {inv.x, inv.y};
+        float k[4];
+        int ks[4];
 #pragma unroll
-    for (int j = 3; j >= 1; --j) {
-        if (j < h) {
-            sl[sp * 64 + lane] = link(ks[j]);
-            st[sp * 64 + lane] = (unsigned short)(__float_as_uint(k[j]) >> 16);
-            ++sp;
+        for (int i = 0; i < 4; ++i) {
+            const int sh = 8 * i;
+            const f2 lxy = org + f2{(float)((qlx >> sh) & 0xFFu), (float)((qly >> sh) & 0xFFu)} * sxy;
+            const f2 hxy = org + f2{(float)((qhx >> sh) & 0xFFu), (float)((qhy >> sh) & 0xFFu)} * sxy;
+            const float lz = R0.z + (float)((qlz >> sh) & 0xFFu) * sz, hz = R0.z + (float)((qhz >> sh) & 0xFFu) * sz;
+            const f2 t0 = (lxy - oxy) * ixy, t1 = (hxy - oxy) * ixy;
+            const float t0z = (lz - o.z) * inv.z, t1z = (hz - o.z) * inv.z;
+            const float te = fmaxf(fmaxf(fminf(t0.x, t1.x), fminf(t0.y, t1.y)), fminf(t0z, t1z));
+            const float tx = fminf(fminf(fmaxf(t0.x, t1.x), fmaxf(t0.y, t1.y)), fmaxf(t0z, t1z));
+            const bool ind = tx > te && tx > kTMin;
+            const uint32_t f = (fl >> sh) & 0xFFu;
+            const float rf = (f & 2u) ? __builtin_inff() : ((f & 4u) ? nr : kRelax);
+            k[i] = (i < n && ind && accel_enter_r(te, closest, rf)) ? te : __builtin_inff();
+            ks[i] = i;
+        }
+        // sort by (t_enter, slot): a five-comparator network; every key is
+        // distinct in slot, so the order is the model's insertion order
+#define RT_WCE(a, b)                                                                       \
+        {                                                                                  \
+            const bool sw = k[a] > k[b] || (k[a] == k[b] && ks[a] > ks[b]);                \
+            const float tk = sw ? k[b] : k[a];                                             \
+            k[b] = sw ? k[a] : k[b];                                                       \
+            k[a] = tk;                                                                     \
+            const int ts = sw ? ks[b] : ks[a];                                             \
+            ks[b] = sw ? ks[a] : ks[b];                                                    \
+            ks[a] = ts;                                                                    \
+        }
+        RT_WCE(0, 1) RT_WCE(2, 3) RT_WCE(0, 2) RT_WCE(1, 3) RT_WCE(1, 2)
+#undef RT_WCE
+        const int h = (k[0] != __builtin_inff()) + (k[1] != __builtin_inff()) + (k[2] != __builtin_inff()) +
+                      (k[3] != __builtin_inff());
+        if (h > 0) {
+            if (sp + h - 1 > kWideStackK) {
+                ovf = true;
+                return false;
+            }
+            const auto link = [&](int slot) -> uint32_t {
+                const uint32_t f = (fl >> (8 * slot)) & 0xFFu;
+                return (base + (uint32_t)slot) | ((f & 1u) << 31) | ((f & 2u) << 29) | ((f & 4u) << 27);
+            };
+#pragma unroll
+            for (int j = 3; j >= 1; --j) {
+                if (j < h) {
+                    sl[sp * 64 + lane] = link(ks[j]);
+                    st[sp * 64 + lane] = (unsigned short)(__float_as_uint(k[j]) >> 16);
+                    ++sp;
+                }
+            }
+            cur = link(ks[0]);
+            pop = false;
+        }
+    }
+    if (pop) {
+        const float thr = closest * kRelax + kRelaxAbs;
+        for (;;) {
+            if (sp == 0) return false;
+            --sp;
+            const uint32_t l = sl[sp * 64 + lane];
+            if ((l & (kWThin | kWWider)) || __uint_as_float((uint32_t)st[sp * 64 + lane] << 16) <= thr) {
+                cur = l;
+                break;
+            }
         }
     }
     return true;
@@ -1253,11 +1240,7 @@ void trace_simple(TraceArgs a) {
                      : HALF ? (int)((unsigned)(a.scene.end2 + 4) * 16u) : (int)((unsigned)(a.scene.end2 + 2) * 32u),
                 0x00020000);
             if (WIDE) {
-                if (walking) {                    // the root record (a step loads the next one)
-                    A = wrec(wrs, 0);
-                    B = wrec(wrs, 16);
-                    Q0 = wrec(wrs, 32);
-                }
+                // no prefetch: a step reads its record at the top
             } else if (HALF && walking) {
                 A = hbuf(wrs, n);
                 if (nleaf) {
@@ -1277,7 +1260,7 @@ void trace_simple(TraceArgs a) {
                 if (DIAG) ++d_iters;
                 if (WIDE) {
                     walking = wide_step<COUNT>(wrs, fr + (size_t)wave * (kWideStackK * 64 * 6 / 16), o, d, inv, closest,
-                                               hit, incons, wcur, wsp, wovf, A, B, Q0, c_node, c_tri);
+                                               hit, incons, wcur, wsp, wovf, c_node, c_tri);
                     continue;
                 }
                 if (WALK == 0) {

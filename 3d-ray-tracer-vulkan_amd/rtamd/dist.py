@@ -456,8 +456,10 @@ class ShareTracer:
       frame (one list for every frame of a launch, rt_render_batch_device; or
       one list per frame when plan.lists, rt_render_batch_lists_device), packed
       at plan.off[rank][f] of the rank's exchange buffer;
-    * mode "tiles" with a TilePlan: the rank's rectangle of one frame
-      (rt_render_tile_device).
+    * mode "tiles" with a TilePlan: the rank's rectangle of n frames in one
+      launch (rt_render_batch_rect_device) when the rectangles are all the
+      plan's tile size, else one rt_render_tile_device per frame, frame f's
+      tile at f x tile_px of the buffers.
 
     Frame k of the run is frame k mod batch of the exchange batch (the plans'
     frame index).  Band lists are built once per (frame, count), so a launch
@@ -493,8 +495,17 @@ class ShareTracer:
         stp = C.byref(stats) if stats is not None else None
         if self.mode == "tiles":
             x0, y0, w, h = self.rect
-            check(L.rt_render_tile_device(self.ctx, C.byref(cams[0]), self.W, self.H, self.B, x0, y0, w, h,
-                                          rgba_ptr, rad_ptr, stream, stp))
+            if n == 1 or w * h == self.tplan.tile_px:
+                check(L.rt_render_batch_rect_device(self.ctx, cams, n, self.W, self.H, self.B, x0, y0, w, h,
+                                                    rgba_ptr, rad_ptr, stream, stp))
+            else:
+                if stats is not None:
+                    raise ValueError("stats of a multi-frame launch of unequal tiles")
+                for f in range(n):
+                    check(L.rt_render_tile_device(self.ctx, C.byref(cams[f]), self.W, self.H, self.B, x0, y0, w, h,
+                                                  rgba_ptr + f * self.tplan.tile_px * 4,
+                                                  (rad_ptr + f * self.tplan.tile_px * 12) if rad_ptr else None,
+                                                  stream, None))
         elif self.plan is not None and self.plan.lists:
             key = (k0 % self.G, n)
             pl = self._lists.get(key)

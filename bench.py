@@ -497,8 +497,7 @@ def main() -> None:
     weak = dist_on and args.scaling == "weak"
     step_frames = world if weak else 1                         # frames per step (weak scaling: N)
     D = args.inflight if args.inflight > 0 else default_inflight(world)
-    F = (args.batch if args.batch > 0 else default_batch(world, weak, args.steps)) \
-        if mode in ("whole", "bands", "pieces", "spans") else 1
+    F = args.batch if args.batch > 0 else default_batch(world, weak, args.steps)
     F = min(F, 16)
     if mode in ("bands", "pieces", "spans"):
         # one exchange per D launches: every exchange costs the host a
@@ -513,7 +512,11 @@ def main() -> None:
             while G > F and (args.steps * step_frames) % G:
                 G -= F
     elif mode == "tiles":
-        G = args.exchange_every if args.exchange_every > 0 else D
+        # F frames' tiles per launch (rt_render_batch_rect_device): a rank's
+        # launch is a frame's worth of pixels at weak scaling; one quarter-
+        # frame launch per frame ran 3-5x slower per pixel (profiles/r06/r6e)
+        G = args.exchange_every if args.exchange_every > 0 else D * F
+        G = max(F, (G + F - 1) // F * F)
     else:
         G = D * F                                              # N = 1: the slot ring
     # ring of exchange batches: enough for the D launches in flight plus the

@@ -197,6 +197,19 @@ int rt_render_batch_lists_device(rt_ctx* ctx, const rt_camera_ubo* cams, int n_f
 /* R of such lists, n_per * band_h (-1 if a list is bad).  Pure host code. */
 int rt_band_lists_rows(int height, int band_h, const int32_t* bands, int n_frames, int n_per);
 
+/* One launch over the same rectangle [x0, x0 + tile_w) x [y0, y0 + tile_h) of
+ * n_frames frames (1..16, camera cams[f] each): the tile grid of a multi-GPU
+ * frame (rtamd/dist.py TilePlan, BASELINE config 4's 2 x 2 over 4 GPUs) with
+ * several frames' tiles per launch, so a rank's launch is a frame's worth of
+ * pixels rather than a quarter frame (one quarter-frame launch per frame ran
+ * a rank's tiles 3-5x slower per pixel than whole frames: its serial tail,
+ * profiles/r06/r6e).  Outputs hold the tiles one after another (n_frames x
+ * tile_h x tile_w).  Same stream / stats semantics as rt_render_tile_device. */
+int rt_render_batch_rect_device(rt_ctx* ctx, const rt_camera_ubo* cams, int n_frames,
+                                int width, int height, int max_bounces,
+                                int x0, int y0, int tile_w, int tile_h,
+                                void* d_out_rgba, void* d_out_radiance, void* stream, rt_stats* stats);
+
 /* Pipelined frames (overlap the readback with the next
  * frame; the reference waits on a fence after every frame,
  * VulkanEngine.java:410-429).
@@ -291,6 +304,16 @@ int rt_render_poll(rt_ctx* ctx, uint64_t ticket, int* done);
  *                   §4a).  Forces coop_lanes 0.  0 / 1
  *   "accel_half_used" (rt_get_option only) 1 when device 0's accel records
  *                   are in that format
+ *   "accel_wide"    at the next rt_upload_scene, with accel on: 1 = a 4-wide
+ *                   tree collapsed from the same SAH tree, one layout of 64-B
+ *                   records, children entered in t_enter order with a per-lane
+ *                   stack of 12 entries in LDS (accel_build.h format 2; an
+ *                   overflow walks the segment in the reference's order).
+ *                   Same frames; 0.49x the wave-level loads of the default but
+ *                   1.45x its VALU instructions: measured slower (config 3
+ *                   1.35x, config 5 1.74x); default 0
+ *   "accel_wide_used" (rt_get_option only) 1 if the current scene on device 0
+ *                   has format-2 records
  *   "accel_used"    (rt_get_option only) the current scene's layouts on device
  *                   0 (0 = the reference's tree)
  *   "walk_bytes"    (rt_get_option only) bytes of the records one ray walks on

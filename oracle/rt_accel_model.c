@@ -336,8 +336,7 @@ static void audit_segment(const scene* s, ray r) {
  * (an overflow walks the segment again in the reference's order).  A stack
  * entry keeps its t_enter rounded down to bfloat16 (the kernel's 2-byte LDS
  * field); a popped default-margin entry whose rounded-down t_enter fails the
- * rule is dropped.  After a leaf the pop comes before its triangle test (with
- * closest_t as it was), as the kernel issues the next record's loads first.  node_visits = 1 (the root) + box tests (children and leaf
+ * rule is dropped.  node_visits = 1 (the root) + box tests (children and leaf
  * boxes), tri_tests = leaf records read; g_count_steps: node_visits counts
  * record fetches instead (analysis). */
 static float rec_f16(size_t idx, int w) {
@@ -382,18 +381,6 @@ static int wide_walk(const scene* s, ray r, float* closest_t, int* hit_index, ve
         const uint32_t* w = &g_rec[16 * idx];
         if (g_count_steps) cnt->node_visits++;
         if (cur & WIDE_LEAF) {
-            /* the next record first (the kernel issues its loads before this
-             * leaf's triangle test): a pop with closest_t as it is now */
-            int found = 0;
-            uint32_t nxt = 0;
-            while (sp > 0) {
-                --sp;
-                const uint32_t link = st_link[sp];
-                if (!(link & (WIDE_THIN | WIDE_WIDER)) && !(st_te[sp] <= c * g_relax + g_relax_abs)) continue;
-                nxt = link;
-                found = 1;
-                break;
-            }
             const int tri = (int)(w[0] & 0x1FFFFFFFu);
             cnt->tri_tests++;
             if ((size_t)tri >= s->n_tris || (size_t)tri >= s->n_mats) return -1;
@@ -414,9 +401,6 @@ static int wide_walk(const scene* s, ray r, float* closest_t, int* hit_index, ve
                     *hit_normal = nrm;
                 }
             }
-            if (!found) break;
-            cur = nxt;
-            continue;
         } else {
             const int n = (int)((w[3] >> 24) & 7u);
             const vec3 org = v3(rec_f16(idx, 0), rec_f16(idx, 1), rec_f16(idx, 2));

@@ -184,10 +184,13 @@ def test_span_exchange_bit_exact(renderer, world, rw, accel):
 
 @pytest.mark.parametrize("accel", [0, 8])
 @pytest.mark.parametrize("world", [1, 2, 4])
-def test_tile_exchange_bit_exact(renderer, rccl_group, world, accel):
+@pytest.mark.parametrize("size,per_launch", [((322, 181), 1), ((322, 181), 3), ((320, 180), 3)])
+def test_tile_exchange_bit_exact(renderer, rccl_group, world, accel, size, per_launch):
     """BASELINE config 4's tile grid (2 x 2 at N = 4): every rank's rectangle
     of every frame of a batch, stacked and assembled; at world size 1 the
-    gather runs over RCCL."""
+    gather runs over RCCL.  per_launch 3: the batch's tiles in one launch
+    (rt_render_batch_rect_device, bench.py's tiles mode; odd sizes: uneven
+    tiles, one launch per frame at the plan's tile pitch)."""
     import torch
     from rtamd import configs
     from rtamd._lib import CameraUBO
@@ -196,7 +199,7 @@ def test_tile_exchange_bit_exact(renderer, rccl_group, world, accel):
     renderer.set_option("accel", accel)
     renderer.upload_scene(cfg.build())
     renderer.set_option("accel", 0)
-    W, H, B, G = 322, 181, 3, 3               # odd sizes: uneven tiles, padded to the largest
+    (W, H), B, G = size, 3, 3                 # odd sizes: uneven tiles, padded to the largest
     cams = _orbit_cams(W, H, G)
     whole = _whole(renderer, cams, W, H, B)
     plan = TilePlan(W, H, world, G)
@@ -207,8 +210,13 @@ def test_tile_exchange_bit_exact(renderer, rccl_group, world, accel):
         tracer = ShareTracer(renderer._ctx, W, H, B, "tiles", rank, tplan=plan, batch=G)
         rgba = torch.zeros((G, plan.tile_px, 4), dtype=torch.uint8, device="cuda:0")
         rad = torch.zeros((G, plan.tile_px, 3), dtype=torch.float32, device="cuda:0")
-        for f in range(G):
-            tracer.launch((CameraUBO * 1)(cams[f].ubo), f, 1, s.cuda_stream, rgba[f].data_ptr(), rad[f].data_ptr())
+        if per_launch == 1:
+            for f in range(G):
+                tracer.launch((CameraUBO * 1)(cams[f].ubo), f, 1, s.cuda_stream, rgba[f].data_ptr(),
+                              rad[f].data_ptr())
+        else:
+            tracer.launch((CameraUBO * G)(*[c.ubo for c in cams[:G]]), 0, G, s.cuda_stream, rgba[0].data_ptr(),
+                          rad[0].data_ptr())
         bufs.append(rgba)
         rbufs.append(rad)
     torch.cuda.synchronize()

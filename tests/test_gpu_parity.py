@@ -1027,3 +1027,44 @@ def test_capacity_fallback(renderer, monkeypatch, extra, want):
         monkeypatch.delenv("RTAMD_ACCEL_CAP_SLOTS")
         renderer.upload_scene(built)
         assert renderer.get_option("accel_used") == 8
+
+
+def test_batch_rect_device(renderer):
+    """rt_render_batch_rect_device: one launch over the same rectangle of 3
+    frames (3 cameras): each frame's tile equals the oracle's tile, with the
+    tiles' counts; a rectangle outside the frame is rejected."""
+    import ctypes as C
+    import torch
+    from rtamd import CameraUBO, RtError, configs, lib
+    from rtamd._lib import Stats, check
+    cfg = configs.config2()
+    built = cfg.build()
+    renderer.upload_scene(built)
+    W, H, B = 640, 360, 4
+    x0, y0, tw, th = 150, 77, 333, 170
+    cams = [configs.Camera((-25.0 + 5 * f, 30.0, 140.0 - 6 * f), (0.0, 0.0, 0.0), (0.0, 1.0, 0.0), 20.0, W / H)
+            for f in range(3)]
+    ubos = (CameraUBO * 3)(*[c.ubo for c in cams])
+    for stats in (False, True, False):          # learning, counting, then the learned order
+        d_rgba = torch.empty((3, th, tw, 4), dtype=torch.uint8, device="cuda:0")
+        d_rad = torch.empty((3, th, tw, 3), dtype=torch.float32, device="cuda:0")
+        st = Stats()
+        check(lib().rt_render_batch_rect_device(renderer._ctx, ubos, 3, W, H, B, x0, y0, tw, th, d_rgba.data_ptr(),
+                                                d_rad.data_ptr(), torch.cuda.current_stream().cuda_stream,
+                                                C.byref(st) if stats else None))
+        torch.cuda.synchronize()
+        tot = {}
+        for f, c in enumerate(cams):
+            ref = _oracle(built, c.ubo_bytes(), W, H, B, tile=(x0, y0, tw, th))
+            _assert_same(d_rgba[f].cpu().numpy(), d_rad[f].cpu().numpy(), None, *ref)
+            for k in ref[2]:
+                tot[k] = tot.get(k, 0) + ref[2][k]
+        if stats:
+            sd = st.as_dict()
+            for k in COUNTERS:
+                if k in tot:
+                    assert sd[k] == tot[k], (k, sd[k], tot[k])
+            assert sd["pixels"] == 3 * tw * th
+    with pytest.raises(RtError, match="INVALID_ARG"):
+        check(lib().rt_render_batch_rect_device(renderer._ctx, ubos, 3, W, H, B, 400, 0, 300, 10, None, None, None,
+                                                None))
