@@ -25,4 +25,7 @@ st "n1 cfg4"; timeout -k 10 300 python bench.py --config 4 --steps 20 --warmup 5
 st "emu cfg4 tiles"; bash tools/emulate.sh "$OUT/emu" c4t 4 "0 1 2 3" --config 4 --partition tiles --gather radiance \
     --steps 20 --warmup 5; chk $?
 st "emu cfg4 spans"; bash tools/emulate.sh "$OUT/emu" c4s 4 "0 1 3" --config 4 --gather radiance --steps 20 --warmup 5; chk $?
+st "ab sched c3"; REPS=3 bash tools/ab_lib.sh "$OUT/absched" "--steps 200 --warmup 5" \
+    3d-ray-tracer-vulkan_amd/lib/librtamd.so 3d-ray-tracer-vulkan_amd/lib/variants/librtamd_defsched.so; chk $?
+st "knobs c3"; ARMS_FILE=tools/arms/r6_knobs.txt REPS=3 STEPS=200 bash tools/ab_args.sh "$TAG/knobs"; chk $?
 st done
