@@ -169,6 +169,7 @@ struct TraceArgs {
                                 //   1 = preorder frontier (frontier_walk)
     int      coop_win = 64;     // coop_walk's window: 64 or 32 slots (option coop_window)
     int      list_stride;       // band_list per frame: frame f's at band_list + f * list_stride
+    const int* row_off = nullptr;   // per frame: its first output row (null: f * th); device memory
                                 //   (0 = one list for every frame of the launch)
     // Split launch (option split_bounce, accel walk): kernel 1
     // packs each wave's paths still alive at bounce split_bounce into the

@@ -1569,7 +1569,8 @@ static int device_band_list(PerDevice& p, const std::vector<int>& bands, const i
 static int render_rows_on(const rt_ctx* ctx, PerDevice& p, const rt_camera_ubo* cams, int n_frames, int width,
                           int height, int max_bounces, int band_h, int band_stride, int band_off,
                           const std::vector<int>* bands, int rows, uchar4* d_rgba, float* d_rad, hipStream_t s,
-                          bool count, int list_stride = 0, int x0 = 0, int y0 = 0, int tile_w = 0) {
+                          bool count, int list_stride = 0, int x0 = 0, int y0 = 0, int tile_w = 0,
+                          bool row_offsets = false) {
     TraceArgs a;
     a.scene = p.scene;
     for (int f = 0; f < n_frames; ++f) a.cams[f] = cam_from_ubo(cams + f);
@@ -1581,6 +1582,8 @@ static int render_rows_on(const rt_ctx* ctx, PerDevice& p, const rt_camera_ubo* 
     a.list_stride = bands ? list_stride : 0;
     if (bands)
         if (int rb = device_band_list(p, *bands, &a.band_list)) return rb;
+    // row_offsets: the list ends with each frame's first output row
+    a.row_off = (bands && row_offsets) ? a.band_list + (size_t)n_frames * list_stride : nullptr;
     a.out_rgba = d_rgba;
     a.out_rad = d_rad;
     a.counters = count ? p.d_counters : nullptr;
@@ -1726,6 +1729,56 @@ int rt_render_batch_rect_device(rt_ctx* ctx, const rt_camera_ubo* cams, int n_fr
     if (stats) {
         RT_HIP_CHECK(hipEventSynchronize(p.ev1));
         return collect_stats(ctx, p, (uint64_t)tile_w * tile_h * n_frames, stats, false);
+    }
+    return RT_OK;
+}
+
+int rt_render_batch_runs_device(rt_ctx* ctx, const rt_camera_ubo* cams, int n_frames, int width, int height,
+                                int max_bounces, int band_h, const int32_t* band_lo, const int32_t* band_hi,
+                                void* d_out_rgba, void* d_out_radiance, void* stream, rt_stats* stats) {
+    int rc = check_render_args(ctx, cams, width, height, max_bounces, "rt_render_batch_runs_device");
+    if (rc) return rc;
+    if (n_frames < 1 || n_frames > kMaxBatch || !band_lo || !band_hi || band_h < 1 || height % band_h) {
+        set_error("rt_render_batch_runs_device: need 1 <= n_frames <= %d, band_h dividing the height and both run "
+                  "arrays", kMaxBatch);
+        return RT_ERR_INVALID_ARG;
+    }
+    const int n_all = (height + band_h - 1) / band_h;
+    int n_per = 0;
+    for (int f = 0; f < n_frames; ++f) {
+        if (band_lo[f] < 0 || band_hi[f] < band_lo[f] || band_hi[f] > n_all) {
+            set_error("rt_render_batch_runs_device: frame %d's run [%d, %d) is not inside [0, %d)", f, band_lo[f],
+                      band_hi[f], n_all);
+            return RT_ERR_INVALID_ARG;
+        }
+        n_per = std::max(n_per, band_hi[f] - band_lo[f]);
+    }
+    if (n_per == 0) {
+        if (stats) std::memset(stats, 0, sizeof *stats);
+        return RT_OK;
+    }
+    // one band list per frame, -1 padded to the longest run, then each
+    // frame's first output row (its rows follow the previous frame's)
+    std::vector<int> list((size_t)n_frames * n_per + n_frames, -1);
+    uint64_t pixels = 0;
+    int row = 0;
+    for (int f = 0; f < n_frames; ++f) {
+        for (int b = band_lo[f]; b < band_hi[f]; ++b) list[(size_t)f * n_per + (b - band_lo[f])] = b;
+        list[(size_t)n_frames * n_per + f] = row;
+        const int rows_f = (band_hi[f] - band_lo[f]) * band_h;
+        row += rows_f;
+        pixels += (uint64_t)rows_f * (uint64_t)width;
+    }
+    PerDevice& p = ctx->dev[0];
+    RT_HIP_CHECK(hipSetDevice(p.device));
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    rc = render_rows_on(ctx, p, cams, n_frames, width, height, max_bounces, band_h, 1, 0, &list, n_per * band_h,
+                        static_cast<uchar4*>(d_out_rgba), static_cast<float*>(d_out_radiance), s, stats != nullptr,
+                        n_per, 0, 0, 0, true);
+    if (rc) return rc;
+    if (stats) {
+        RT_HIP_CHECK(hipEventSynchronize(p.ev1));
+        return collect_stats(ctx, p, pixels, stats, false);
     }
     return RT_OK;
 }

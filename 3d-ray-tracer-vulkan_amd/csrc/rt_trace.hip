@@ -1100,7 +1100,7 @@ void trace_simple(TraceArgs a) {
     if ((FEAT & kFeatFused) && sub >= 0) {               // a heavy tile's pixel, dispatched first
         const int hf = by / a.tiles_y;                   // its frame of the batch
         const int hy = (by - hf * a.tiles_y) * th_w + (sub >> (3 + s));
-        heavy_pixel<COUNT>(a, hf, bx * tw_w + (sub & (tw_w - 1)), hy, hf * a.th + hy, fr);
+        heavy_pixel<COUNT>(a, hf, bx * tw_w + (sub & (tw_w - 1)), hy, (a.row_off ? a.row_off[hf] : hf * a.th) + hy, fr);
         if (DIAG) {
             diag_stamp(drec, 1);
             if (lane == 0) {
@@ -1121,7 +1121,9 @@ void trace_simple(TraceArgs a) {
     by -= fr_i * a.tiles_y;                              //   f follow those of frame f - 1)
     int lx = col * tw_w + (tl & (tw_w - 1));
     const int ly = by * th_w + (tl >> (3 + s));          // row within the frame's rows
-    int lyo = fr_i * a.th + ly;                          // output row
+    // output row (per-frame offsets: rt_render_batch_runs_device packs each
+    // frame's rows after the previous frame's)
+    int lyo = (a.row_off ? a.row_off[fr_i] : fr_i * a.th) + ly;
     // (a per-frame band list's -1 entries are padding rows: no pixel)
     const bool pixel = !Q2 && lx < a.tw && ly < a.th && (sub < 0 || lane == 0) && !((skip_lanes >> lane) & 1ull) &&
                        (a.list_stride == 0 || a.band_list[fr_i * a.list_stride + ly / a.band_h] >= 0);

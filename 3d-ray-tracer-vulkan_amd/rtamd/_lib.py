@@ -37,7 +37,7 @@ EXPORTED = (
     "rt_host_alloc", "rt_host_free", "rt_render_async", "rt_render_wait", "rt_upload_spheres",
     "rt_render_batch_device", "rt_band_list_rows", "rt_render_batch_lists_device", "rt_band_lists_rows",
     "rt_render_poll", "rt_accel_records", "rt_abi_version", "rt_pack_rgb", "rt_unpack_rgb",
-    "rt_build_id", "rt_render_batch_rect_device",
+    "rt_build_id", "rt_render_batch_rect_device", "rt_render_batch_runs_device",
 )
 
 # The library's sources in the Makefile's SRC_ALL order: rt_build_id's
@@ -160,6 +160,9 @@ def lib() -> C.CDLL:
                 "rt_band_lists_rows": (i32, [i32, i32, C.POINTER(C.c_int32), i32, i32]),
                 "rt_render_batch_rect_device": (i32, [vp, C.POINTER(CameraUBO), i32, i32, i32, i32, i32, i32, i32,
                                                       i32, vp, vp, vp, C.POINTER(Stats)]),
+                "rt_render_batch_runs_device": (i32, [vp, C.POINTER(CameraUBO), i32, i32, i32, i32, i32,
+                                                      C.POINTER(C.c_int32), C.POINTER(C.c_int32), vp, vp, vp,
+                                                      C.POINTER(Stats)]),
                 "rt_scene_validate": (i32, [vp, sz, vp, sz, vp, sz, C.POINTER(sz), C.POINTER(i32)]),
                 "rt_set_option": (i32, [vp, C.c_char_p, C.c_int64]),
                 "rt_get_option": (i32, [vp, C.c_char_p, C.POINTER(C.c_int64)]),

@@ -544,16 +544,23 @@ class SpanPlan:
     [row0[r], row0[r] + rows[r]) of the batch column.  launches[r] lists its
     launches: (frame, band_lo, band_hi, out_row), one frame each, the whole
     frame when (band_lo, band_hi) == (0, height / band_h), written at row
-    out_row of the rank's span buffer (rank 0: the batch column from row0[0])."""
+    out_row of the rank's span buffer (rank 0: the batch column from row0[0]).
+    groups[r] lists the GPU launches over them: (first, count) runs of up to
+    launch_frames consecutive entries of launches[r], traced in one launch
+    (rt_render_batch_runs_device; one entry: rt_render_batch_device), their
+    rows contiguous in the span buffer; pieces() follow the groups."""
 
     def __init__(self, height: int, band_h: int, world: int, n_frames: int, root_weight: float = 1.0,
-                 whole_frames: bool = False, batch: int = 0):
+                 whole_frames: bool = False, batch: int = 0, launch_frames: int = 1):
         if height % band_h:
             raise ValueError(f"spans: band_h ({band_h}) must divide the height ({height})")
         if not root_weight >= 0:
             raise ValueError("spans: root_weight must be >= 0")
         self.height, self.band_h, self.world, self.n_frames = height, band_h, world, n_frames
         self.root_weight = root_weight
+        if not 1 <= launch_frames <= 16:
+            raise ValueError("spans: launch_frames must be in 1..16")
+        self.launch_frames = launch_frames
         self.whole_frames = whole_frames
         self.bpf = height // band_h
         total = n_frames * self.bpf
@@ -585,6 +592,8 @@ class SpanPlan:
                 out_row += (hi - lo) * band_h
                 b = f * self.bpf + hi
             self.launches.append(out)
+        self.groups = [[(i, min(launch_frames, len(ls) - i)) for i in range(0, len(ls), launch_frames)]
+                       for ls in self.launches]
         self._views = {}
         if whole_frames:
             # buffers hold the largest span of any batch
@@ -610,7 +619,8 @@ class SpanPlan:
         key = (b * ((self.n_frames - self.frame_counts(0)[0]) % (self.world - 1))) % (self.world - 1)
         v = self._views.get(key)
         if v is None:
-            v = SpanPlan(self.height, self.band_h, self.world, self.n_frames, self.root_weight, True, b)
+            v = SpanPlan(self.height, self.band_h, self.world, self.n_frames, self.root_weight, True, b,
+                         self.launch_frames)
             v.per_rank = self.per_rank
             self._views[key] = v
         return v
@@ -620,9 +630,11 @@ class SpanPlan:
         return [(r, self.row0[r], self.rows[r]) for r in range(1, self.world) if self.rows[r] > 0]
 
     def pieces(self, rank: int):
-        """(out_row, rows) of each launch of rank's span, in launch order: the
-        pieces a span travels in when it is sent launch by launch."""
-        return [(orow, (hi - lo) * self.band_h) for (_, lo, hi, orow) in self.launches[rank]]
+        """(out_row, rows) of each launch (group) of rank's span, in launch
+        order: the pieces a span travels in when it is sent launch by launch."""
+        ls = self.launches[rank]
+        return [(ls[g][3], sum((ls[g + i][2] - ls[g + i][1]) * self.band_h for i in range(n)))
+                for g, n in self.groups[rank]]
 
     def recv_pieces(self):
         """(rank, row0, rows) of every launch's piece rank 0 receives, per rank
@@ -640,8 +652,33 @@ class SpanTracer:
     def __init__(self, ctx, width: int, height: int, max_bounces: int, plan: SpanPlan, rank: int = 0):
         self.ctx, self.W, self.H, self.B, self.plan, self.rank = ctx, width, height, max_bounces, plan, rank
         self.launches = plan.launches[rank]
+        self.groups = plan.groups[rank]
         self._lists = [None if (lo, hi) == (0, plan.bpf) else np.arange(lo, hi, dtype=np.int32)
                        for (_, lo, hi, _) in self.launches]
+        self._runs = [(np.ascontiguousarray([self.launches[g + i][1] for i in range(n)], dtype=np.int32),
+                       np.ascontiguousarray([self.launches[g + i][2] for i in range(n)], dtype=np.int32))
+                      for g, n in self.groups]
+
+    def group_frames(self, j: int):
+        """The frames (of the batch) of launch group j, in order."""
+        g, n = self.groups[j]
+        return [self.launches[g + i][0] for i in range(n)]
+
+    def group_row(self, j: int) -> int:
+        """The span buffer row where launch group j writes."""
+        return self.launches[self.groups[j][0]][3]
+
+    def launch_group(self, cams, j: int, stream: int, rgba_ptr, rad_ptr, stats=None) -> None:
+        """Launch group j (cams: a ctypes array of its frames' CameraUBO) on
+        `stream` into rgba_ptr / rad_ptr, the span buffer's row group_row(j)."""
+        g, n = self.groups[j]
+        if n == 1:
+            return self.launch(cams[0], g, stream, rgba_ptr, rad_ptr, stats)
+        lo, hi = self._runs[j]
+        check(lib().rt_render_batch_runs_device(self.ctx, cams, n, self.W, self.H, self.B, self.plan.band_h,
+                                                lo.ctypes.data_as(C.POINTER(C.c_int32)),
+                                                hi.ctypes.data_as(C.POINTER(C.c_int32)), rgba_ptr, rad_ptr, stream,
+                                                C.byref(stats) if stats is not None else None))
 
     def launch(self, cam, j: int, stream: int, rgba_ptr, rad_ptr, stats=None) -> None:
         """Launch j of the rank's span (cam: the CameraUBO of its frame) on

@@ -362,6 +362,9 @@ def main() -> None:
                          "compute_dynamic_ray.comp:235), 3/4 of the bytes over each xGMI link, packed and "
                          "unpacked by rt_pack_rgb / rt_unpack_rgb (emulated 5%% slower at N = 8, profiles/r05/"
                          "emulation/r5ap; it pays only where a link is the bound, DESIGN.md §6)")
+    ap.add_argument("--span-launch-frames", type=int, default=1,
+                    help="spans: consecutive frames of a rank's span per launch (1..16; 2: a span-end run goes "
+                         "with its neighbouring whole frame, rt_render_batch_runs_device)")
     ap.add_argument("--span-cut", choices=("frames", "bands"), default="bands",
                     help="spans: frames = cut each exchange batch at frame boundaries (every launch a whole "
                          "frame; rank 0 its weighted share rounded, the others' extra frames rotating from batch "
@@ -552,7 +555,7 @@ def main() -> None:
         if H % band_h:
             raise SystemExit(f"--partition spans: --band ({band_h}) must divide the height ({H})")
         plan = SpanPlan(H, band_h, world, G, args.root_weight if args.root_weight >= 0 else default_span_weight(world),
-                        whole_frames=args.span_cut == "frames")
+                        whole_frames=args.span_cut == "frames", launch_frames=args.span_launch_frames)
         # rank 0: the batch's frames (its own span traced in place, the others
         # received into them); rank r: its span
         rows = G * H if rank == 0 else plan.per_rank
@@ -627,7 +630,7 @@ def main() -> None:
         t = span_tracers.get(id(v))
         if t is None:
             tr = SpanTracer(ctx, W, H, B, v, rank)
-            t = span_tracers[id(v)] = (tr, [[span_ptrs(h, orow) for (_, _, _, orow) in tr.launches]
+            t = span_tracers[id(v)] = (tr, [[span_ptrs(h, tr.group_row(j)) for j in range(len(tr.groups))]
                                             for h in range(R)])
         return t
 
@@ -645,12 +648,21 @@ def main() -> None:
         tracer.launch(cams, k0, n, s.cuda_stream, rgba_ptr, rad_ptr, st)
         return st.as_dict() if stats else None
 
-    def trace_span(k0, jl, s, rgba_ptr, rad_ptr, stats=False):
-        """Launch jl of this rank's span of the batch that starts at frame k0
-        (rtamd.dist.SpanTracer)."""
+    def trace_span(k0, jl, s, rgba_ptr, rad_ptr, stats=False, one=False):
+        """Launch (group) jl of this rank's span of the batch that starts at
+        frame k0 (rtamd.dist.SpanTracer); one: entry jl of its frames alone
+        (the counting pass)."""
         st_ = Stats() if stats else None
         tr = tracer_of(view_of(k0))[0]
-        tr.launch(cam_of(k0 + tr.launches[jl][0]).ubo, jl, s.cuda_stream, rgba_ptr, rad_ptr, st_)
+        if one:
+            tr.launch(cam_of(k0 + tr.launches[jl][0]).ubo, jl, s.cuda_stream, rgba_ptr, rad_ptr, st_)
+            return st_.as_dict() if stats else None
+        fs = tr.group_frames(jl)
+        ck = (0, len(fs)) if args.camera_path == "static" else (k0 + fs[0], len(fs))
+        cams = cam_arrays.get(ck)
+        if cams is None:                              # the group's frames are consecutive
+            cams = cam_arrays[ck] = (CameraUBO * len(fs))(*[cam_of(k0 + f).ubo for f in fs])
+        tr.launch_group(cams, jl, s.cuda_stream, rgba_ptr, rad_ptr, st_)
         return st_.as_dict() if stats else None
 
     def span_ptrs(h, out_row):
@@ -873,7 +885,7 @@ def main() -> None:
             piece_q = [] if (pieces and rank) else None
             v = view_of(k0)
             tr, tab = tracer_of(v)
-            for jl in range(len(tr.launches)):
+            for jl in range(len(tr.groups)):
                 j = st["j"]
                 s = streams[j % D]
                 rp, dp = tab[h][jl]
@@ -968,7 +980,7 @@ def main() -> None:
         if mode == "spans":
             for k in ks:
                 for jl, (_, _, _, orow) in enumerate(tracer_of(view_of(k))[0].launches):
-                    d = trace_span(k, jl, main_stream, count_rgba[orow * W].data_ptr(), None, stats=True)
+                    d = trace_span(k, jl, main_stream, count_rgba[orow * W].data_ptr(), None, stats=True, one=True)
                     for k2 in tot:
                         tot[k2] += d[k2]
                     ms.append(d["ms"])

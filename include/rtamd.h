@@ -210,6 +210,18 @@ int rt_render_batch_rect_device(rt_ctx* ctx, const rt_camera_ubo* cams, int n_fr
                                 int x0, int y0, int tile_w, int tile_h,
                                 void* d_out_rgba, void* d_out_radiance, void* stream, rt_stats* stats);
 
+/* Batched runs of bands, packed: frame f (camera cams[f], 1 <= n_frames <= 16)
+ * traces its band_h-row bands [band_lo[f], band_hi[f]) (band_h must divide
+ * height; an empty run traces nothing), and its rows follow frame f - 1's in
+ * the DEVICE buffers (sum of the runs x band_h rows of width pixels).  The
+ * spans partition's launch of two consecutive frames of a rank's span, a run
+ * at the span's end merged with its neighbouring whole frame.
+ * Otherwise as rt_render_batch_device. */
+int rt_render_batch_runs_device(rt_ctx* ctx, const rt_camera_ubo* cams, int n_frames,
+                                int width, int height, int max_bounces, int band_h,
+                                const int32_t* band_lo, const int32_t* band_hi,
+                                void* d_out_rgba, void* d_out_radiance, void* stream, rt_stats* stats);
+
 /* Pipelined frames (overlap the readback with the next
  * frame; the reference waits on a fence after every frame,
  * VulkanEngine.java:410-429).

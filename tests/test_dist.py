@@ -275,10 +275,13 @@ def _share_worker(rank, world, port, q, kind, arg, n_frames, W, H, B):
             # bench.py --partition spans: rank 0 traces its span in place in
             # the batch's frames, the others into a span buffer; one group of
             # point-to-point receives lands every span in rank 0's frames
-            band_h, rw, wire, pieces, whole_b = arg
+            band_h, rw, wire, pieces, whole_b = arg[:5]
+            lf = arg[5] if len(arg) > 5 else 1
             # whole_b >= 0: cut at frame boundaries, batch whole_b's plan (its
-            # extra frames on its own ranks)
-            plan = SpanPlan(H, band_h, world, n_frames, rw, whole_frames=whole_b >= 0).batch(max(0, whole_b))
+            # extra frames on its own ranks); lf: frames per launch group (the
+            # pieces follow the groups)
+            plan = SpanPlan(H, band_h, world, n_frames, rw, whole_frames=whole_b >= 0,
+                            launch_frames=lf).batch(max(0, whole_b))
             col = torch.zeros((n_frames * H, W, 4), dtype=torch.uint8) if rank == 0 else None
             rgb = None
             if wire == "rgb":
@@ -487,16 +490,18 @@ def test_share_tracer_rejects_uneven_lists():
     assert tt.rect == (960, 540, 960, 540)
 
 
-@pytest.mark.parametrize("world,n_frames,band_h,rw,wire,pieces,whole_b", [(2, 3, 4, 1.0, "rgba", False, -1),
-                                                                          (4, 4, 4, 0.6, "rgb", False, -1),
-                                                                          (8, 8, 2, 0.8, "rgb", False, -1),
-                                                                          (3, 2, 8, 0.0, "rgba", False, -1),
-                                                                          (3, 2, 8, 0.5, "rgb", False, -1),
-                                                                          (4, 4, 4, 0.6, "rgb", True, -1),
-                                                                          (3, 3, 4, 0.8, "rgba", True, -1),
-                                                                          (8, 11, 4, 0.8, "rgba", True, 3),
-                                                                          (4, 6, 4, 0.6, "rgb", False, 1)])
-def test_spans_weak_scaling(world, n_frames, band_h, rw, wire, pieces, whole_b):
+@pytest.mark.parametrize("world,n_frames,band_h,rw,wire,pieces,whole_b,lf", [(2, 3, 4, 1.0, "rgba", False, -1, 1),
+                                                                          (4, 4, 4, 0.6, "rgb", False, -1, 1),
+                                                                          (8, 8, 2, 0.8, "rgb", False, -1, 1),
+                                                                          (3, 2, 8, 0.0, "rgba", False, -1, 1),
+                                                                          (3, 2, 8, 0.5, "rgb", False, -1, 1),
+                                                                          (4, 4, 4, 0.6, "rgb", True, -1, 1),
+                                                                          (3, 3, 4, 0.8, "rgba", True, -1, 1),
+                                                                          (8, 11, 4, 0.8, "rgba", True, 3, 1),
+                                                                          (4, 6, 4, 0.6, "rgb", False, 1, 1),
+                                                                          (4, 8, 4, 0.6, "rgb", True, -1, 2),
+                                                                          (3, 5, 4, 0.8, "rgba", True, -1, 3)])
+def test_spans_weak_scaling(world, n_frames, band_h, rw, wire, pieces, whole_b, lf):
     """bench.py --partition spans: each rank traces one contiguous span of the
     batch's rows (whole frames, a run of bands at either end; rank 0's span
     rw times the others'), rank 0 in place in the batch's frames, and one
@@ -507,7 +512,7 @@ def test_spans_weak_scaling(world, n_frames, band_h, rw, wire, pieces, whole_b):
     whole_b >= 0: spans cut at frame boundaries, the plan of batch whole_b):
     every frame and its radiance equal the oracle's, bit for bit."""
     W, H = 48, 40
-    traced = _run_share(world, "spans", (band_h, rw, wire, pieces, whole_b), n_frames=n_frames, W=W, H=H, B=2)
+    traced = _run_share(world, "spans", (band_h, rw, wire, pieces, whole_b, lf), n_frames=n_frames, W=W, H=H, B=2)
     assert sum(traced.values()) == n_frames * W * H
     if 0 < rw < 1.0:
         assert traced[0] < min(traced[r] for r in range(1, world)) or \
@@ -558,19 +563,23 @@ def test_span_plan_1080p():
         extra.append(c.index(5))
     assert extra[:7] == list(range(1, 8))
     assert SpanPlan(1080, 8, 4, 16, 0.9, whole_frames=True).frame_counts(0) == [4, 4, 4, 4]
-    # cut at frame boundaries (--span-cut frames): whole-frame launches only, rank 0
-    # 3 frames, the others 4 and one extra frame rotating over them batch by batch
-    wp = SpanPlan(1080, 8, 8, 32, 0.8, whole_frames=True)
-    extra = []
-    for b in range(14):
-        v = wp.batch(b)
-        c = v.frame_counts(b)
-        assert c[0] == 3 and sum(c) == 32 and sorted(c[1:]) == [4] * 6 + [5]
-        assert v.rows == [n * 1080 for n in c] and all((lo, hi) == (0, 135) for r in range(8)
-                                                       for _, lo, hi, _ in v.launches[r])
-        assert v.per_rank == 5 * 1080 and v is wp.batch(b + 7)
-        extra.append(c.index(5))
-    assert extra[:7] == list(range(1, 8))
-    assert SpanPlan(1080, 8, 4, 16, 0.9, whole_frames=True).frame_counts(0) == [4, 4, 4, 4]
     with pytest.raises(ValueError, match="divide the height"):
         SpanPlan(1080, 16, 8, 32, 0.8)
+    # launch groups (--span-launch-frames 2): runs of two consecutive entries,
+    # the span-end runs with their neighbours; the pieces follow the groups and
+    # still tile each span in order
+    gp = SpanPlan(1080, 8, 8, 32, 0.8, launch_frames=2)
+    for r in range(8):
+        ls, gs = gp.launches[r], gp.groups[r]
+        assert [i for g, n in gs for i in range(g, g + n)] == list(range(len(ls)))
+        assert all(n == 2 for _, n in gs[:-1]) and 1 <= gs[-1][1] <= 2
+        t = SpanTracer(None, 1920, 1080, 4, gp, r)
+        for j, (g, n) in enumerate(gs):
+            assert t.group_frames(j) == [ls[g + i][0] for i in range(n)]
+            assert t.group_frames(j) == list(range(ls[g][0], ls[g][0] + n))   # consecutive frames
+            assert t.group_row(j) == ls[g][3]
+        ps = gp.pieces(r)
+        assert len(ps) == len(gs) and ps[0][0] == 0 and sum(n for _, n in ps) == gp.rows[r]
+        assert all(ps[i][0] + ps[i][1] == ps[i + 1][0] for i in range(len(ps) - 1))
+    with pytest.raises(ValueError, match="launch_frames"):
+        SpanPlan(1080, 8, 8, 32, 0.8, launch_frames=0)

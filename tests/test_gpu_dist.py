@@ -132,17 +132,20 @@ def test_share_exchange_bit_exact(renderer, rccl_group, layout, world, rw, accel
         _check(assemble_shares(stk, plan, src), assemble_shares(stk_r, plan, src), whole, "RCCL gather_stack")
 
 
-@pytest.mark.parametrize("world,rw", [(1, 1.0), (2, 0.9), (4, 0.8), (8, 0.55), (8, 1.0)])
+@pytest.mark.parametrize("world,rw,lf", [(1, 1.0, 1), (2, 0.9, 1), (4, 0.8, 1), (8, 0.55, 1), (8, 1.0, 1),
+                                         (2, 0.9, 2), (4, 0.8, 2), (8, 0.55, 3)])
 @pytest.mark.parametrize("accel", [0, 8])
-def test_span_exchange_bit_exact(renderer, world, rw, accel):
+def test_span_exchange_bit_exact(renderer, world, rw, accel, lf):
     """bench.py --partition spans: every rank's span of an exchange batch
-    traced with SpanTracer's launches (one frame's band run each) on 4 streams,
+    traced with SpanTracer's launch groups (lf frames' band runs each,
+    rt_render_batch_runs_device packing them back to back) on 4 streams,
     rank 0's in place in the batch's frames, the others' into span buffers
     that land in rank 0's frames at the plan's rows (what the point-to-point
     receives write; exchange_spans itself runs over gloo in test_dist.py).
     Every frame and its radiance equal the frame traced whole."""
     import torch
     from rtamd import configs
+    from rtamd._lib import CameraUBO
     from rtamd.dist import SpanPlan, SpanTracer
     cfg = configs.config2()
     renderer.set_option("accel", accel)
@@ -152,7 +155,7 @@ def test_span_exchange_bit_exact(renderer, world, rw, accel):
     G = 4 * world if world > 1 else 4
     cams = _orbit_cams(W, H, G)
     whole = _whole(renderer, cams, W, H, B)
-    plan = SpanPlan(H, band_h, world, G, rw)
+    plan = SpanPlan(H, band_h, world, G, rw, launch_frames=lf)
     col = torch.full((G * H, W, 4), 7, dtype=torch.uint8, device="cuda:0")
     colr = torch.zeros((G * H, W, 3), dtype=torch.float32, device="cuda:0")
     streams = [torch.cuda.Stream() for _ in range(4)]
@@ -169,9 +172,11 @@ def test_span_exchange_bit_exact(renderer, world, rw, accel):
             spans.append((rank, buf, rbuf))
         for st in streams:
             st.wait_stream(torch.cuda.current_stream())
-        for jl, (f, lo, hi, orow) in enumerate(tracer.launches):
-            tracer.launch(cams[f].ubo, jl, streams[j % 4].cuda_stream, buf[base + orow].data_ptr(),
-                          rbuf[base + orow].data_ptr())
+        for jl in range(len(tracer.groups)):
+            fs = tracer.group_frames(jl)
+            orow = tracer.group_row(jl)
+            tracer.launch_group((CameraUBO * len(fs))(*[cams[f].ubo for f in fs]), jl, streams[j % 4].cuda_stream,
+                                buf[base + orow].data_ptr(), rbuf[base + orow].data_ptr())
             j += 1
     torch.cuda.synchronize()
     for rank, buf, rbuf in spans:

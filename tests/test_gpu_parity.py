@@ -1068,3 +1068,55 @@ def test_batch_rect_device(renderer):
     with pytest.raises(RtError, match="INVALID_ARG"):
         check(lib().rt_render_batch_rect_device(renderer._ctx, ubos, 3, W, H, B, 400, 0, 300, 10, None, None, None,
                                                 None))
+
+
+def test_batch_runs_device(renderer):
+    """rt_render_batch_runs_device: frame f traces its band run [lo_f, hi_f)
+    and its rows follow frame f - 1's (a span-end run, a whole frame, an empty
+    run, a run from row 0): each frame's rows equal the oracle's, with their
+    counts; the rows past the packed total stay untouched."""
+    import ctypes as C
+    import torch
+    from rtamd import CameraUBO, RtError, configs, lib
+    from rtamd._lib import Stats, check
+    cfg = configs.config2()
+    built = cfg.build()
+    renderer.upload_scene(built)
+    W, H, B, bh = 320, 184, 4, 8                       # 23 bands
+    runs = [(17, 23), (0, 23), (5, 5), (0, 9)]
+    cams = [configs.Camera((-25.0 + 5 * f, 30.0, 140.0 - 6 * f), (0.0, 0.0, 0.0), (0.0, 1.0, 0.0), 20.0, W / H)
+            for f in range(len(runs))]
+    ubos = (CameraUBO * len(runs))(*[c.ubo for c in cams])
+    lo = (C.c_int32 * len(runs))(*[r[0] for r in runs])
+    hi = (C.c_int32 * len(runs))(*[r[1] for r in runs])
+    total = sum((b - a) * bh for a, b in runs)
+    for stats in (False, True, False):
+        d_rgba = torch.full((total + 8, W, 4), 7, dtype=torch.uint8, device="cuda:0")
+        d_rad = torch.full((total + 8, W, 3), -2.0, dtype=torch.float32, device="cuda:0")
+        st = Stats()
+        check(lib().rt_render_batch_runs_device(renderer._ctx, ubos, len(runs), W, H, B, bh, lo, hi,
+                                                d_rgba.data_ptr(), d_rad.data_ptr(),
+                                                torch.cuda.current_stream().cuda_stream, C.byref(st) if stats else None))
+        torch.cuda.synchronize()
+        rgba, rad = d_rgba.cpu().numpy(), d_rad.cpu().numpy()
+        row, tot = 0, {}
+        for (a, b), c in zip(runs, cams):
+            n = (b - a) * bh
+            if n:
+                ref = _oracle(built, c.ubo_bytes(), W, H, B, tile=(0, a * bh, W, n))
+                _assert_same(rgba[row:row + n], rad[row:row + n], None, *ref)
+                for k in ref[2]:
+                    tot[k] = tot.get(k, 0) + ref[2][k]
+            row += n
+        assert (rgba[total:] == 7).all() and (rad[total:] == -2.0).all()
+        if stats:
+            sd = st.as_dict()
+            for k in COUNTERS:
+                if k in tot:
+                    assert sd[k] == tot[k], (k, sd[k], tot[k])
+            assert sd["pixels"] == total * W
+    bad = (C.c_int32 * 1)(24)
+    with pytest.raises(RtError, match="INVALID_ARG"):
+        check(lib().rt_render_batch_runs_device(renderer._ctx, ubos, 1, W, H, B, bh, lo, bad, None, None, None, None))
+    with pytest.raises(RtError, match="INVALID_ARG"):                 # band_h must divide the height
+        check(lib().rt_render_batch_runs_device(renderer._ctx, ubos, 1, W, H, B, 7, lo, hi, None, None, None, None))
