@@ -553,7 +553,7 @@ int accel_build(const void* vertices, size_t vertex_bytes, const void* materials
                 const float e2[3] = {x[6] - x[0], x[7] - x[1], x[8] - x[2]};
                 // | L(next) << 31, below; bit 29: a thin triangle (class >= kAccelClassMin), entered
                 // whenever the slab test passes, whatever closest_t
-                w[3] = (uint32_t)p.tri | (1u << 30) | (p.cls >= kAccelClassMin ? 1u << 29 : 0u);
+                w[3] = (uint32_t)p.tri | (1u << 30) | (p.cls >= kAccelClassMin ? kAccelForce : 0u);
                 put_f(&w[7], x[0]);
                 put_f(&w[8], x[1]);
                 put_f(&w[9], x[2]);
@@ -569,10 +569,8 @@ int accel_build(const void* vertices, size_t vertex_bytes, const void* materials
             const int first = neg ? nd.right : nd.left, second = neg ? nd.left : nd.right;
             const size_t skip = it.pos + (size_t)span(nd.m);
             w[3] = (uint32_t)skip;                                 // | L(skip) << 31, below
-            if (format == 0) {                                     // the subtree's margin; | L(first) below
-                const float r = accel_relax(nd.cls);
-                std::memcpy(&w[7], &r, 4);
-            }
+            if (format == 0 && nd.cls >= kAccelClassMin)           // a thin triangle below: entered whenever
+                w[3] |= kAccelForce;                               //   its slab test passes
             const size_t pos2 = it.pos + 1 + (size_t)span(B.nodes[first].m);
             st.push_back({second, pos2});
             st.push_back({first, it.pos + 1});
@@ -586,8 +584,8 @@ int accel_build(const void* vertices, size_t vertex_bytes, const void* materials
                 w[3] |= L(s + (size_t)LS) << 31;
                 s += (size_t)LS;
             } else if (format == 0) {
-                w[3] |= L(w[3]) << 31;
-                w[7] |= L(s + 1);                         // bit 0 of the margin: it only grows by an ulp
+                w[3] |= L(w[3] & ~kAccelForce) << 31;
+                w[7] |= L(s + 1);
                 s += 1;
             } else {
                 w[3] |= L(w[3]) << 31 | L(s + 1) << 30;

@@ -21,10 +21,11 @@
 //
 // Records: the walk-2 slot format of rt_internal.h (DevScene::walk), packed
 // (no pad slots): an internal node one 32-B slot, a leaf two (box, then its
-// triangle v0 / e1 / e2).  An internal node's word 7 is its margin factor R
-// (accel_relax of its subtree's largest shape class, a float whose bit 0 is
-// L(first child)); a leaf's bit 29 of word 3 marks a thin triangle (class >=
-// kAccelClassMin), entered whenever its slab test passes.  n_layouts copies of the tree in preorder, each with
+// triangle v0 / e1 / e2).  Bit 29 of word 3 (kAccelForce) marks a record whose
+// subtree holds a thin triangle (shape class >= kAccelClassMin; a leaf: its
+// own): the walk enters it whenever its slab test passes, whatever closest_t,
+// and every other record with the 2^-10 margin.  An internal node's word 7 is
+// L(first child).  n_layouts copies of the tree in preorder, each with
 // its own child order: layout o puts first, at a node split on axis a, the
 // child on the side a ray with sign bit ((o >> a) & 1) on axis a reaches first
 // (n_layouts 1: always the lower child).  A ray walks the layout of its
@@ -94,12 +95,19 @@ struct AccelHost {
 // t_enter, the case in which the accel walk could miss the reference's hit.
 constexpr int kAccelClassMin = 7;
 int accel_class(const float e1[3], const float e2[3]);
-// The margin factor R of a box whose subtree's largest class is cls: the walk
-// enters it when t_enter <= closest_t * R + 2^-10.  Class < 7: 1 + 2^-10;
-// else 1 + 2^(cls - 16) (class 16: 2, class 31: 32769), growing as the t error
-// does, 64x the error measured at class 16.  A leaf of class >= 7 (bit 29 of
-// its link word) is entered whenever its slab test passes (R = infinity).
+// The margin factor R a box whose subtree's largest class is cls needs: the
+// walk must enter it when t_enter <= closest_t * R + 2^-10.  Class < 7: 1 +
+// 2^-10; else 1 + 2^(cls - 16) (class 16: 2, class 31: 32769), growing as the
+// t error does, 64x the error measured at class 16 (the audit's bound,
+// oracle/rt_accel_model.c).  Format 0 applies 1 + 2^-10 below class 7 and
+// enters a record of class >= 7 whenever its slab test passes (kAccelForce:
+// R = infinity, one bit test in the walk instead of a per-record factor);
+// format 1 applies accel_relax(max_class) at every internal node, format 2 the
+// node's own class.
 float accel_relax(int cls);
+// Format 0: bit 29 of a record's word 3, a subtree of class >= kAccelClassMin
+// (internal skips and triangle indices stay below 2^29).
+constexpr uint32_t kAccelForce = 1u << 29;
 
 // The layouts do not fit the slot cap (accel_build's return value).
 constexpr int kAccelTooBig = -2;

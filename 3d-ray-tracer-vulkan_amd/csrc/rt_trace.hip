@@ -369,28 +369,34 @@ __device__ __forceinline__ float lane_f(float v, int k) {
 // t).  oracle/rt_accel_model.c states the same arithmetic.
 //
 // Thin triangles (round 6; accel_build.h accel_class): Moeller-Trumbore's t
-// error grows as 1 / sin of the triangle's angle at v0, so a box whose
-// subtree holds a triangle of shape class c >= 7 carries its own factor R =
-// 1 + 2^(c - 16) in place of 1 + 2^-10 (an internal node's word 7, bit 0 of
-// which is L(first child)), and a thin leaf (bit 29 of its link word) is
-// entered whenever its slab test passes.  Nothing else changes: a larger
-// margin only enters more boxes.
+// error grows as 1 / sin of the triangle's angle at v0, so a record whose
+// subtree holds a triangle of shape class >= 7 (bit 29 of its link word,
+// kAccelForce; a leaf: its own triangle) is entered whenever its slab test
+// passes, whatever closest_t.  The rest keep the 2^-10 margin.  Nothing else
+// changes: a forced record only enters more boxes.  (Per-record factors, R =
+// 1 + 2^(c - 16) in word 7, measured 5% slower on config 3 for the VALU of
+// choosing and applying them on every step: profiles/r06/r6h.)
 constexpr float kRelax = 1.0f + 1.0f / 1024.0f;
 constexpr float kRelaxAbs = 1.0f / 1024.0f;
-constexpr uint32_t kThinLeaf = 1u << 29;
+constexpr uint32_t kThinLeaf = 1u << 29;     // format 1 / 2 leaves: a thin triangle
+constexpr uint32_t kForce = 1u << 29;        // format 0: accel_build.h kAccelForce
+constexpr uint32_t kIdx = 0x1FFFFFFFu;       // node index bits of a link word (bit 29: kForce)
+constexpr uint32_t kTri = 0x1FFFFFFFu;       // triangle index bits of a leaf's link word (bit 29: pad after
+                                             //   it on the reference's tree, kForce on option accel's)
 __device__ __forceinline__ bool accel_enter(float te, float closest) { return te <= closest * kRelax + kRelaxAbs; }
-// The margin factor of the record whose words 3 and 7 are aw and bw.
-// (A/B builds: RT_THIN_MARGIN 0 = round 5's fixed factor, not exact for thin
-// triangles: make variant NAME=x FLAGS=-DRT_THIN_MARGIN=0)
+// (A/B builds: RT_THIN_MARGIN 0 = round 5's rule, the 2^-10 margin
+// everywhere, not exact for thin triangles: make variant NAME=x
+// FLAGS=-DRT_THIN_MARGIN=0)
 #ifndef RT_THIN_MARGIN
 #define RT_THIN_MARGIN 1
 #endif
-__device__ __forceinline__ float accel_factor(bool leaf, uint32_t aw, uint32_t bw) {
+// Format 0's entry rule for a record with link word aw.
+__device__ __forceinline__ bool accel_enter_w(float te, float closest, uint32_t aw) {
 #if RT_THIN_MARGIN
-    return leaf ? ((aw & kThinLeaf) ? __builtin_inff() : kRelax) : __uint_as_float(bw);
+    return accel_enter(te, closest) || (aw & kForce) != 0u;
 #else
-    (void)leaf; (void)aw; (void)bw;
-    return kRelax;
+    (void)aw;
+    return accel_enter(te, closest);
 #endif
 }
 __device__ __forceinline__ bool accel_enter_r(float te, float closest, float r) {
@@ -500,7 +506,8 @@ __device__ __forceinline__ int coop_walk(const float4* __restrict__ walk, int en
         ++windows;
         const int j = n + lane;
         const bool ld = j < end && lane < WIN;
-        float te = 0.0f, tt = 0.0f, rf = kRelax;
+        float te = 0.0f, tt = 0.0f;
+        uint32_t law = 0u;                                           // ACC: the record's link word (kForce)
         int sk = 0, tri = -1;
         bool ind = false, tv = false, lf = false, pd = false;
         float4 A = make_float4(0.f, 0.f, 0.f, 0.f), B = A;
@@ -535,18 +542,18 @@ __device__ __forceinline__ int coop_walk(const float4* __restrict__ walk, int en
             // several percent: written with masks the PAD form measured 2.7%
             // slower on config 3, profiles/r04/r4n)
             if (PAD) {
-                sk = lf ? j + 2 + (int)((aw >> 29) & 1u) : (int)(aw & 0x7FFFFFFFu);
+                sk = lf ? j + 2 + (int)((aw >> 29) & 1u) : (int)(aw & kIdx);
                 pd = lf ? ((aw >> 29) & 1u) != 0u : ((__float_as_uint(B.w) >> 2) & 1u) != 0u;
             } else {
-                sk = lf ? j + 2 : (int)(aw & 0x7FFFFFFFu);
+                sk = lf ? j + 2 : (int)(aw & kIdx);
             }
-            tri = (int)(aw & 0x1FFFFFFFu);
-            if (ACC) rf = accel_factor(lf, aw, __float_as_uint(B.w));
-            if (lf && ind && (ACC ? accel_enter_r(te, closest, rf) : te < closest) && (!RT_COOP_DPP || lane < WIN - 1))
+            tri = (int)(aw & kTri);
+            if (ACC) law = aw;
+            if (lf && ind && (ACC ? accel_enter_w(te, closest, aw) : te < closest) && (!RT_COOP_DPP || lane < WIN - 1))
                 tv = tri_test(make_float4(B.w, Q0.x, Q0.y, 0.f), make_float4(Q0.z, Q0.w, Q1.x, 0.f),
                               make_float4(Q1.y, Q1.z, Q1.w, 0.f), o, d, tt);
         }
-        uint64_t H = __ballot(ind && (ACC ? accel_enter_r(te, closest, rf) : te < closest));
+        uint64_t H = __ballot(ind && (ACC ? accel_enter_w(te, closest, law) : te < closest));
         uint64_t T = __ballot(tv && (ACC ? accel_take(tt, tri, closest, hit) : tt < closest));
         const uint64_t Lf = __ballot(lf);
         const uint64_t Pd = PAD ? __ballot(pd) : 0ull;              // a pad slot follows (leaf alignment)
@@ -563,7 +570,7 @@ __device__ __forceinline__ int coop_walk(const float4* __restrict__ walk, int en
                         closest = lane_f(tt, k);
                         hit = lane_i(tri, k);
                         if (ACC) incons = closest < lane_f(te, k);
-                        H = __ballot(ind && (ACC ? accel_enter_r(te, closest, rf) : te < closest));
+                        H = __ballot(ind && (ACC ? accel_enter_w(te, closest, law) : te < closest));
                         T = __ballot(tv && (ACC ? accel_take(tt, tri, closest, hit) : tt < closest));
                     }
                 }
@@ -758,8 +765,6 @@ __device__ __forceinline__ bool wide_step(__amdgpu_buffer_rsrc_t wrs, uint4* stk
 // If the front cannot be expanded for lack of room (never seen: the cap is
 // 4x the reference's 64-entry stack), the walk stops with pos = the
 // reference's next node, to be finished by node_step.
-constexpr uint32_t kIdx = 0x7FFFFFFFu;      // node index bits of a link word
-constexpr uint32_t kTri = 0x1FFFFFFFu;      // triangle index bits of a leaf's link word (bit 29: pad after it)
 constexpr int kFCap = 256;                   // frontier entries per wave (16 B each)
 constexpr int kFReserve = 80;                // slots speculation leaves to the front (> 64-deep descent)
 constexpr uint32_t kUnres = 0xFFFFFFFFu;
@@ -1310,7 +1315,7 @@ void trace_simple(TraceArgs a) {
                     bool ind;
                     slab(A, B, o, inv, te, ind);
                     const uint32_t aw = __float_as_uint(A.w), bw = __float_as_uint(B.w);
-                    const bool hb = ind && (ACC ? accel_enter_r(te, closest, accel_factor(nleaf, aw, bw)) : te < closest);
+                    const bool hb = ind && (ACC ? accel_enter_w(te, closest, aw) : te < closest);
                     // a leaf's next node is its successor, two slots on, whether it
                     // is hit or not (its skip); an internal node's left child is
                     // the next slot (one more past a pad slot: leaf bit 29 of word

@@ -26,11 +26,11 @@
  * accel_half): 16-B slots, an internal node one slot with its box in IEEE half
  * precision (decoded exactly, as the kernel's v_cvt_f32_f16), a leaf four.
  *
- * Thin triangles (round 6, accel_build.h accel_class / accel_relax): a box is
- * entered when t_enter <= closest_t * R + 2^-10 with R its record's factor
- * (an internal node's word 7 as a float, bit 0 being L(first child); format
- * 1: orc_accel_relax_half's one factor), and a leaf marked thin (bit 29 of
- * word 3) whenever its slab test passes.
+ * Thin triangles (round 6, accel_build.h accel_class / kAccelForce): a record
+ * whose bit 29 of word 3 is set (its subtree holds a triangle of shape class
+ * >= 7) is entered whenever its slab test passes (R = infinity); format 1's
+ * internal nodes take orc_accel_relax_half's one factor, and its thin leaves
+ * (bit 29) R = infinity too.
  */
 #define ORC_WALK_HOOK accel_walk
 #include "rt_oracle.c"
@@ -43,14 +43,11 @@ static uint64_t g_leaf_visits = 0;     /* analysis: leaf slots walked (the rest 
 /* The walk's box margin: a box is entered when t_enter <= closest_t * RELAX +
  * RELAX_ABS (accel_build.h).  orc_accel_margin changes them for studies. */
 static float g_relax = 1.0f + 1.0f / 1024.0f, g_relax_abs = 1.0f / 1024.0f;
-static int g_relax_set = 0;            /* a study changed the default margin */
 static float g_relax_half = 1.0f + 1.0f / 1024.0f;
-#define RELAX_BITS 0x3F802000u         /* 1 + 2^-10 */
 
 int orc_accel_margin(float rel, float abs_) {
     g_relax = rel;
     g_relax_abs = abs_;
-    g_relax_set = !(rel == 1.0f + 1.0f / 1024.0f && abs_ == 1.0f / 1024.0f);
     return 0;
 }
 
@@ -61,14 +58,10 @@ int orc_accel_relax_half(float r) {
     return 0;
 }
 
-/* The margin factor of a record (words 3 and 7: aw, bw). */
-static float rec_factor(int leaf, uint32_t aw, uint32_t bw) {
-    if (leaf) return (aw & (1u << 29)) ? INFINITY : g_relax;
-    if (g_fmt) return g_relax_half;
-    if (g_relax_set && (bw & ~1u) == RELAX_BITS) return g_relax;
-    float r;
-    memcpy(&r, &bw, 4);
-    return r;
+/* The margin factor of a record (word 3: aw). */
+static float rec_factor(int leaf, uint32_t aw) {
+    if (leaf || !g_fmt) return (aw & (1u << 29)) ? INFINITY : g_relax;
+    return g_relax_half;
 }
 
 /* accel_build.cpp accel_class / accel_relax, restated (the audit's margin). */
@@ -281,7 +274,7 @@ static void audit_segment(const scene* s, ray r) {
             n += 1;
             leaf = g_fmt ? (int)((aw >> 30) & 1u) : (int)(bw & 1u);
         } else {
-            n = aw & (g_fmt ? 0x3FFFFFFFu : 0x7FFFFFFFu);
+            n = aw & (g_fmt ? 0x3FFFFFFFu : 0x1FFFFFFFu);
             leaf = (int)(aw >> 31);
         }
     }
@@ -517,7 +510,7 @@ static int accel_walk(const scene* s, ray r, float* closest_t, int* hit_index, v
         const vec3 t1s = mul3(sub3(bhi, r.origin), inv);
         const float te = fmaxf(fmaxf(fminf(t0s.x, t1s.x), fminf(t0s.y, t1s.y)), fminf(t0s.z, t1s.z));
         const float tx = fminf(fminf(fmaxf(t0s.x, t1s.x), fmaxf(t0s.y, t1s.y)), fmaxf(t0s.z, t1s.z));
-        const int hb = tx > te && tx > T_MIN && te <= c * rec_factor(leaf, aw, bw) + g_relax_abs;
+        const int hb = tx > te && tx > T_MIN && te <= c * rec_factor(leaf, aw) + g_relax_abs;
         leaf_visits += (uint64_t)leaf;
         if (hb && leaf) {
             const int tri = (int)(aw & 0x1FFFFFFFu);
@@ -544,7 +537,7 @@ static int accel_walk(const scene* s, ray r, float* closest_t, int* hit_index, v
             nxt = n + 1;
             nl = g_fmt ? (int)((aw >> 30) & 1u) : (int)(bw & 1u);
         } else {
-            nxt = aw & (g_fmt ? 0x3FFFFFFFu : 0x7FFFFFFFu);
+            nxt = aw & (g_fmt ? 0x3FFFFFFFu : 0x1FFFFFFFu);
             nl = (int)(aw >> 31);
         }
         if (nxt <= n && !hb) return -1;         /* a link that does not move forward: bad records */

@@ -30,17 +30,23 @@ def _built():
     (rt_build_id, read from the file) must carry the SHA-256 of the sources
     as they are here.  A library that is missing or built from other sources
     is rebuilt first (make is incremental); the oracle is built if missing."""
+    import fcntl
     import subprocess
     from rtamd import _lib
-    if not _lib.build_matches_tree() and "RTAMD_LIB_PATH" not in os.environ:
-        subprocess.run(["make", "-j8", "-C", PKG_DIR], check=True)
-    if "RTAMD_LIB_PATH" not in os.environ:
-        assert _lib.build_matches_tree(), (f"{_lib.LIB_PATH}: build id {_lib.file_build_id()} does not match "
-                                           f"the tree's sources (src={_lib.source_hash()})")
-    # the oracle (test infrastructure) follows its sources (incremental)
-    subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle")], check=True, stdout=subprocess.DEVNULL)
-    # the JNI shim against the mock JNIEnv follows include/rtamd.h (incremental)
-    subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "jni"), "mock"], check=True, stdout=subprocess.DEVNULL)
+    # one builder at a time (pytest -n: every worker runs this fixture; a
+    # worker must not load a library another one is still writing)
+    with open(os.path.join(ROOT, ".build.lock"), "w") as lock:
+        fcntl.flock(lock, fcntl.LOCK_EX)
+        if not _lib.build_matches_tree() and "RTAMD_LIB_PATH" not in os.environ:
+            subprocess.run(["make", "-j8", "-C", PKG_DIR], check=True)
+        if "RTAMD_LIB_PATH" not in os.environ:
+            assert _lib.build_matches_tree(), (f"{_lib.LIB_PATH}: build id {_lib.file_build_id()} does not "
+                                               f"match the tree's sources (src={_lib.source_hash()})")
+        # the oracle (test infrastructure) follows its sources (incremental)
+        subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle")], check=True, stdout=subprocess.DEVNULL)
+        # the JNI shim against the mock JNIEnv follows include/rtamd.h (incremental)
+        subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "jni"), "mock"], check=True,
+                       stdout=subprocess.DEVNULL)
     print(f"\nlibrtamd build id: {_lib.file_build_id()} (tree src={_lib.source_hash()})")
     yield
 

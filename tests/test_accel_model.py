@@ -54,7 +54,7 @@ def _walk_all(rec, info, o):
             tris.append(aw & 0x1FFFFFFF)
             n, leaf = n + 2, bool(aw >> 31)
         else:
-            skip = aw & 0x7FFFFFFF
+            skip = aw & 0x1FFFFFFF
             assert n < skip <= end
             n, leaf = n + 1, bool(bw & 1)
         steps += 1
@@ -242,6 +242,57 @@ def test_study_claims():
         if c["config"].startswith(("cfg3", "cfg5", "cfg6")):
             ref = c["reference_seed1"]["visits_per_segment"]
             assert c["accel"]["layouts1"]["visits_per_segment"] < ref / 3.0
+
+
+@pytest.mark.parametrize("k", [3])
+def test_forced_records(k):
+    """Format 0's thin-triangle rule (accel_build.h kAccelForce): bit 29 of a
+    record's word 3 is set exactly when its subtree holds a triangle of shape
+    class >= 7 (a leaf: its own), in every layout; internal word 7 is L(first
+    child) only."""
+    from rtamd import configs
+    built = configs.get(k).build()
+    rec, info = _records(built, 8)
+    s = info["slots"]
+    w = rec[: 8 * 8 * s].reshape(-1, 8)
+    v = built.model_vertex_data.view(np.float32).reshape(-1, 12)
+    e1, e2 = (v[:, 4:7] - v[:, 0:3]).astype(np.float64), (v[:, 8:11] - v[:, 0:3]).astype(np.float64)
+    with np.errstate(divide="ignore", invalid="ignore"):
+        sn = np.linalg.norm(np.cross(e1, e2), axis=1) / (np.linalg.norm(e1, axis=1) * np.linalg.norm(e2, axis=1))
+        thin_tri = ~(sn > 0.0) | (np.floor(-np.log2(sn)) >= 7)
+
+    def thin(tri):
+        return bool(thin_tri[tri])
+
+    n_thin, n_forced = 0, 0
+    for o in range(8):
+        n, end, leaf = o * s, (o + 1) * s, bool(info["root_leaf"])
+        stack = []                       # (end of subtree, index of its record)
+        forced_below = {}
+        while n < end:
+            while stack and n >= stack[-1][0]:
+                stack.pop()
+            aw = int(w[n, 3])
+            if leaf:
+                t = thin(aw & 0x1FFFFFFF)
+                assert bool(aw & (1 << 29)) == t, (o, n)
+                if t:
+                    n_thin += o == 0
+                    for _, i in stack:
+                        forced_below[i] = True
+                n, leaf = n + 2, bool(aw >> 31)
+            else:
+                assert int(w[n, 7]) in (0, 1)
+                sk = aw & 0x1FFFFFFF
+                # L(skip): the record the skip lands on is a leaf (its bit 30)
+                assert bool(aw >> 31) == (sk < end and bool((int(w[sk, 3]) >> 30) & 1)), (o, n)
+                stack.append((sk, n))
+                forced_below.setdefault(n, False)
+                n, leaf = n + 1, bool(int(w[n, 7]) & 1)
+        for i, f in forced_below.items():
+            assert bool(int(w[i, 3]) & (1 << 29)) == f, (o, i)
+            n_forced += f
+    assert n_thin == info["n_thin"] > 0 and n_forced > 0
 
 
 def test_trailing_subtree_not_a_primitive():
