@@ -286,11 +286,13 @@ int rt_render_poll(rt_ctx* ctx, uint64_t ticket, int* done);
  *                   order's; node visits and triangle tests are the accel
  *                   walk's own.  The exactness argument holds
  *                   when no triangle's rounded t lies more than that margin
- *                   before its own leaf box's t_enter; no tested scene comes
- *                   within 2^-10 of it (tests/test_accel_model.py, adversarial
- *                   slivers, grazing rays, far-from-origin meshes), but it is
- *                   a bound, not a proof: accel 0 is the exact mode by
- *                   construction.  Past the records' slot cap (2^27 - 4
+ *                   before its own leaf box's t_enter.  Boxes over needle
+ *                   triangles (shape class >= 7, where Moeller-Trumbore's t
+ *                   error grows) are entered whenever their slab test passes;
+ *                   for the rest no tested scene comes within 2^-10 of the
+ *                   margin (tests/test_accel_model.py, adversarial slivers,
+ *                   grazing rays, far-from-origin meshes), but it is a bound,
+ *                   not a proof: accel 0 is the exact mode by construction.  Past the records' slot cap (2^27 - 4
  *                   slots: ~5.6 M triangles at 8 layouts) the upload falls
  *                   back to 1 layout, then to the reference's tree
  *                   ("accel_used").  Heavy tiles / pixels are not split out
@@ -521,7 +523,7 @@ int rt_scene_validate(const void* vertices, size_t vertex_bytes,
  * info (nullable) receives {n_layouts, slots per layout, root is a leaf,
  * primitives after dropping byte-identical duplicates, reference leaves, tree
  * depth, the largest shape class, primitives of class >= 7 (thin: their
- * boxes carry wider margins, "accel" above)}.  Only the root's subtree counts (nodes past the root's skip are
+ * boxes are entered whenever their slab test passes, "accel" above)}.  Only the root's subtree counts (nodes past the root's skip are
  * never visited by the reference).  The capacity fallback of rt_upload_scene
  * applies: 8 layouts past the slot cap are built as 1 (info[0] = 1), and a
  * scene too large for one layout gets no records (RT_OK, *n_words = 0, info
