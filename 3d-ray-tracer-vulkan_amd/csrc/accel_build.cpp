@@ -585,7 +585,7 @@ int accel_build(const void* vertices, size_t vertex_bytes, const void* materials
                 s += (size_t)LS;
             } else if (format == 0) {
                 w[3] |= L(w[3] & ~kAccelForce) << 31;
-                w[7] |= L(s + 1);
+                w[7] |= L(s + 1) << 31;                   // a sign test in the walk
                 s += 1;
             } else {
                 w[3] |= L(w[3]) << 31 | L(s + 1) << 30;

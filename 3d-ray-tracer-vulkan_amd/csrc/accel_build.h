@@ -25,7 +25,7 @@
 // subtree holds a thin triangle (shape class >= kAccelClassMin; a leaf: its
 // own): the walk enters it whenever its slab test passes, whatever closest_t,
 // and every other record with the 2^-10 margin.  An internal node's word 7 is
-// L(first child).  n_layouts copies of the tree in preorder, each with
+// L(first child) << 31 (the reference's walk records keep it in bit 0).  n_layouts copies of the tree in preorder, each with
 // its own child order: layout o puts first, at a node split on axis a, the
 // child on the side a ray with sign bit ((o >> a) & 1) on axis a reaches first
 // (n_layouts 1: always the lower child).  A ray walks the layout of its

@@ -444,6 +444,11 @@ __device__ __forceinline__ float4 wbuf(__amdgpu_buffer_rsrc_t r, int slot, int o
     const auto v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)((unsigned)slot << 5) + off, 0, 0);
     return make_float4(__uint_as_float(v[0]), __uint_as_float(v[1]), __uint_as_float(v[2]), __uint_as_float(v[3]));
 }
+// the same at a byte offset (slot << 5) the caller already holds
+__device__ __forceinline__ float4 wbuf_b(__amdgpu_buffer_rsrc_t r, unsigned byte, int off) {
+    const auto v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)byte + off, 0, 0);
+    return make_float4(__uint_as_float(v[0]), __uint_as_float(v[1]), __uint_as_float(v[2]), __uint_as_float(v[3]));
+}
 #endif
 #ifndef RT_ACC_SCALAR
 // 1 = a walk step whose walking lanes all go to one slot loads it through the
@@ -1276,6 +1281,16 @@ void trace_simple(TraceArgs a) {
                 }
             }
             float lim = accel_lim(closest);                          // ACC: closest_t's entry bound
+            // Option accel's format-0 walk tracks its record as a byte offset
+            // (slot << 5; the records stay below 2^27 slots, so it and the
+            // layout's end fit 32 bits): the next record's address is one
+            // select of two values known before the slab test ends, the
+            // skip's being its link word << 5 (the shift drops kForce and the
+            // L bit), and the slot index is recovered after the loop.
+            constexpr bool BYTES = ACC && !HALF && !WIDE && !PAD && WALK == 2 && RT_CHAIN == 2 &&
+                                   !RT_ACC_SCALAR && !RT_ACC_LAZY;
+            unsigned nb = (unsigned)n << 5;
+            const unsigned lend_b = (unsigned)lend << 5;
             while (walking) {
                 if (DIAG) ++d_iters;
                 if (WIDE) {
@@ -1346,13 +1361,22 @@ void trace_simple(TraceArgs a) {
                         nxt = (n_leaf & m_leaf) | (n_int & ~m_leaf);
                     } else {
 #if RT_CHAIN == 1 || RT_CHAIN == 2
-                        const int t = n + 1 + (int)nleaf;                    // known before the slab test ends
-                        nxt = (hb || nleaf) ? t : (int)(aw & kIdx);
+                        if (BYTES) {
+                            const unsigned tb = nb + (nleaf ? 64u : 32u);    // known before the slab test ends
+                            nb = (hb || nleaf) ? tb : (aw << 5);
+                            nxt = 0;                                         // (the slot: nb >> 5)
+                        } else {
+                            const int t = n + 1 + (int)nleaf;                // known before the slab test ends
+                            nxt = (hb || nleaf) ? t : (int)(aw & kIdx);
+                        }
 #else
                         nxt = nleaf ? n + 2 : (hb ? n + 1 : (int)(aw & kIdx));
 #endif
                     }
-                    const bool nl = (((hb && !nleaf) ? bw : (aw >> 31)) & 1u) != 0u;
+                    // accel records: L(first) is bit 31 of word 7, L(skip) / L(next) bit 31
+                    // of word 3 (two sign tests); the reference's: bit 0 of word 7
+                    const bool nl = ACC ? ((hb && !nleaf) ? (int)bw < 0 : (int)aw < 0)
+                                        : ((((hb && !nleaf) ? bw : (aw >> 31)) & 1u) != 0u);
                     const float v0x = B.w;                                   // a leaf's v0.x
                     if (COUNT && hb && !nleaf) c_node += 2;
 #if RT_ACC_SCALAR
@@ -1367,8 +1391,13 @@ void trace_simple(TraceArgs a) {
                         B = wbuf(wrs, nxt, 16);
                     }
 #elif RT_CHAIN >= 2
-                    A = wbuf(wrs, nxt, 0);                                   // slot end is padding
-                    B = wbuf(wrs, nxt, 16);
+                    if (BYTES) {
+                        A = wbuf_b(wrs, nb, 0);                              // slot end is padding
+                        B = wbuf_b(wrs, nb, 16);
+                    } else {
+                        A = wbuf(wrs, nxt, 0);                               // slot end is padding
+                        B = wbuf(wrs, nxt, 16);
+                    }
 #elif RT_CHAIN == 1
                     {
                         const float4* p = reinterpret_cast<const float4*>(reinterpret_cast<const char*>(wr) +
@@ -1400,7 +1429,7 @@ void trace_simple(TraceArgs a) {
                             }
                         }
                     }
-                    const bool inb = nxt < (ACC ? lend : wend);
+                    const bool inb = BYTES ? nb < lend_b : nxt < (ACC ? lend : wend);
                     if (nl && inb && !(ACC && RT_ACC_LAZY)) {
 #if RT_ACC_SCALAR
                         if (uni) {
@@ -1411,20 +1440,26 @@ void trace_simple(TraceArgs a) {
                             Q1 = wbuf(wrs, nxt, 48);
                         }
 #elif RT_CHAIN >= 2
-                        Q0 = wbuf(wrs, nxt, 32);
-                        Q1 = wbuf(wrs, nxt, 48);
+                        if (BYTES) {
+                            Q0 = wbuf_b(wrs, nb, 32);
+                            Q1 = wbuf_b(wrs, nb, 48);
+                        } else {
+                            Q0 = wbuf(wrs, nxt, 32);
+                            Q1 = wbuf(wrs, nxt, 48);
+                        }
 #else
                         Q0 = wr[2 * nxt + 2];
                         Q1 = wr[2 * nxt + 3];
 #endif
                     }
-                    n = nxt;
+                    if (!BYTES) n = nxt;
                     nleaf = nl;
                     walking = inb;
                 }
                 if (WALK == 0 || HALF) walking = n < (ACC ? lend : wend);
                 if ((FEAT & kFeatCoopTail) && __popcll(__ballot(walking)) <= coop_lanes) break;
             }
+            if (BYTES) n = (int)(nb >> 5);
         }
         if (FEAT & kFeatCoopTail) {
             // Every lane is here.  Finish the remaining walks one ray at a

@@ -272,7 +272,7 @@ static void audit_segment(const scene* s, ray r) {
             leaf = (int)(aw >> 31);
         } else if (hb) {
             n += 1;
-            leaf = g_fmt ? (int)((aw >> 30) & 1u) : (int)(bw & 1u);
+            leaf = g_fmt ? (int)((aw >> 30) & 1u) : (int)(bw >> 31);
         } else {
             n = aw & (g_fmt ? 0x3FFFFFFFu : 0x1FFFFFFFu);
             leaf = (int)(aw >> 31);
@@ -535,7 +535,7 @@ static int accel_walk(const scene* s, ray r, float* closest_t, int* hit_index, v
             nl = (int)(aw >> 31);
         } else if (hb) {
             nxt = n + 1;
-            nl = g_fmt ? (int)((aw >> 30) & 1u) : (int)(bw & 1u);
+            nl = g_fmt ? (int)((aw >> 30) & 1u) : (int)(bw >> 31);
         } else {
             nxt = aw & (g_fmt ? 0x3FFFFFFFu : 0x1FFFFFFFu);
             nl = (int)(aw >> 31);

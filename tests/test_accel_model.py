@@ -56,7 +56,7 @@ def _walk_all(rec, info, o):
         else:
             skip = aw & 0x1FFFFFFF
             assert n < skip <= end
-            n, leaf = n + 1, bool(bw & 1)
+            n, leaf = n + 1, bool(bw >> 31)
         steps += 1
         assert steps <= s
     assert n == end
@@ -122,7 +122,7 @@ def test_record_layouts_half(k):
                     lo_in = np.nextafter(lo1.astype(np.float16), np.float16(np.inf)).astype(np.float32)
                     hi_in = np.nextafter(hi1.astype(np.float16), np.float16(-np.inf)).astype(np.float32)
                     assert ((lo_in > lo0) | ~np.isfinite(lo1)).all() and ((hi_in < hi0) | ~np.isfinite(hi1)).all()
-                    leaf = bool(int(w0[7]) & 1)
+                    leaf = bool(int(w0[7]) >> 31)
                     assert leaf == bool((int(w1[3]) >> 30) & 1)
                     a, b = a + 1, b + 1
 
@@ -249,7 +249,7 @@ def test_forced_records(k):
     """Format 0's thin-triangle rule (accel_build.h kAccelForce): bit 29 of a
     record's word 3 is set exactly when its subtree holds a triangle of shape
     class >= 7 (a leaf: its own), in every layout; internal word 7 is L(first
-    child) only."""
+    child) << 31 only."""
     from rtamd import configs
     built = configs.get(k).build()
     rec, info = _records(built, 8)
@@ -282,13 +282,13 @@ def test_forced_records(k):
                         forced_below[i] = True
                 n, leaf = n + 2, bool(aw >> 31)
             else:
-                assert int(w[n, 7]) in (0, 1)
+                assert int(w[n, 7]) in (0, 1 << 31)
                 sk = aw & 0x1FFFFFFF
                 # L(skip): the record the skip lands on is a leaf (its bit 30)
                 assert bool(aw >> 31) == (sk < end and bool((int(w[sk, 3]) >> 30) & 1)), (o, n)
                 stack.append((sk, n))
                 forced_below.setdefault(n, False)
-                n, leaf = n + 1, bool(int(w[n, 7]) & 1)
+                n, leaf = n + 1, bool(int(w[n, 7]) >> 31)
         for i, f in forced_below.items():
             assert bool(int(w[i, 3]) & (1 << 29)) == f, (o, i)
             n_forced += f
