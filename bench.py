@@ -362,9 +362,12 @@ def main() -> None:
                          "compute_dynamic_ray.comp:235), 3/4 of the bytes over each xGMI link, packed and "
                          "unpacked by rt_pack_rgb / rt_unpack_rgb (emulated 5%% slower at N = 8, profiles/r05/"
                          "emulation/r5ap; it pays only where a link is the bound, DESIGN.md §6)")
-    ap.add_argument("--span-launch-frames", type=int, default=1,
-                    help="spans: consecutive frames of a rank's span per launch (1..16; 2: a span-end run goes "
-                         "with its neighbouring whole frame, rt_render_batch_runs_device)")
+    ap.add_argument("--span-launch-frames", type=int, default=2,
+                    help="spans: consecutive frames of a rank's span per launch (1..16; rt_render_batch_runs_device; "
+                         "2, the default: two frames of work per launch as at N = 1, and a span-end run goes with "
+                         "its neighbouring whole frame. Emulated on config 3 at 20 steps, slowest rank against 1 "
+                         "frame per launch: N = 2 0.158 vs 0.169 ms per step, N = 4 0.1626 vs 0.1643, N = 8 "
+                         "0.170 vs 0.169; profiles/r06/r6g, r6i)")
     ap.add_argument("--span-cut", choices=("frames", "bands"), default="bands",
                     help="spans: frames = cut each exchange batch at frame boundaries (every launch a whole "
                          "frame; rank 0 its weighted share rounded, the others' extra frames rotating from batch "
