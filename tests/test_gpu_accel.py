@@ -114,6 +114,40 @@ def _tie_scenes():
     return M._tie_scenes()
 
 
+def _adversarial():
+    import os
+    import sys
+    tools = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools")
+    if tools not in sys.path:
+        sys.path.insert(0, tools)
+    import accel_adversarial
+    return accel_adversarial
+
+
+@pytest.mark.parametrize("nl", [1, 8, HALF8, WIDE])
+@pytest.mark.parametrize("name", ["slivers", "fine_mesh", "grazing", "grazing_cube", "far_origin_near",
+                                  "far_origin_far", "far_origin_neg", "near_camera"])
+def test_accel_adversarial_scenes(acc, name, nl):
+    """The adversarial scenes of the margin audit (tools/accel_adversarial.py,
+    DESIGN.md §4a) on the GPU: needles whose rounded t lies up to 17 margins
+    before their box (the forced records of accel_build.h kAccelForce), a fine
+    shell with |det| near the shader's 1e-5 cut, grazing rays, meshes at
+    +-1e4, triangles 1e-3 from the eye.  Small versions (scale 0.3, 240 x 135,
+    4 bounces): frames equal the oracle's, counters the accel model's."""
+    from rtamd import build_buffers, configs
+    A = _adversarial()
+    verts, mats, (eye, at), vfov = A.SCENES[name](0.3)
+    w, h, b = 240, 135, 4
+    cam = configs.Camera(eye, at, (0.0, 1.0, 0.0), vfov, w / h)
+    built = build_buffers(verts, mats, 1)
+    _upload(acc, built, nl)
+    ref = _oracle(built, cam, w, h, b)
+    model = _model(built, cam, w, h, b, nl)
+    for stats in (False, True, False):
+        rgba, rad, st = acc.render(cam, w, h, b, radiance=True, stats=stats)
+        _check(rgba, rad, st, ref, model, f"{name} layouts {nl}")
+
+
 @pytest.mark.parametrize("nl", [1, 8, HALF8, WIDE])
 def test_accel_ties_and_fallback(acc, nl):
     """Scenes built to tie: every triangle twice in two colours, an integer
