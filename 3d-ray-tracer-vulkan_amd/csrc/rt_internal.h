@@ -218,6 +218,12 @@ struct LearnParams {
     int      order_split;    // percent (0 = every tile by cost)
     double   bar_scale;      // heavy-pixel bar = bar_scale x total steps
     int      cap;            // at most this many heavy pixels
+    // option xcd_order (> 0, n a multiple of 8): tile_order position k runs on
+    // XCD k % 8 (workgroups are dealt round-robin); XCD c gets the c-th eighth
+    // of the tiles in the order of (row class, row, frame, column), a row's
+    // class being (row / xcd) % 8, still most expensive first within it
+    int      xcd = 0;
+    int      tiles_x = 0, tiles_y = 0, frames = 0;
 };
 struct LearnScratch;         // device scratch (rt_learn.hip)
 size_t learn_scratch_bytes(int n);

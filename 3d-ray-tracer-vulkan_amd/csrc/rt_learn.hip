@@ -68,6 +68,10 @@ Layout layout(int n) {
                                          (const int*)nullptr, (int*)nullptr, n, 0, 32);
     (void)rocprim::radix_sort_keys_desc(nullptr, tc, (const unsigned long long*)nullptr,
                                         (unsigned long long*)nullptr, nl, 0, 64);
+    size_t tx = 0;
+    (void)rocprim::radix_sort_pairs(nullptr, tx, (const unsigned*)nullptr, (unsigned*)nullptr,
+                                    (const int*)nullptr, (int*)nullptr, n, 0, 3);
+    tb = tb > tx ? tb : tx;
     L.temp_bytes = up(tb > tc ? tb : tc);
     off += L.temp_bytes;
     L.total = off;
@@ -138,6 +142,39 @@ __global__ __launch_bounds__(256) void learn_top(const unsigned long long* __res
     if (i + 1 == cap || sorted[i + 1] == 0ull) *nhpix = i + 1;      // the last heavy pixel
 }
 
+// Option xcd_order: the eighth of the tiles (0-7) sorted position i's tile
+// belongs to, by its rank in the order (row class, row, frame, column), a
+// row's class being (row / band) % 8: XCD c's tiles are then rows of one class
+// (a band of rows every 8 bands), so its L2 serves rays from fewer parts of
+// the scene.
+__global__ __launch_bounds__(256) void xcd_keys(const int* __restrict__ order, int n, int tiles_x, int tiles_y,
+                                                int frames, int band, unsigned* __restrict__ key,
+                                                int* __restrict__ val) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int t = order[i];
+    const int col = t % tiles_x, by = t / tiles_x;
+    const int f = by / tiles_y, row = by - f * tiles_y;
+    // rows of each class: full cycles of 8 bands, then the last partial cycle
+    const int cyc = 8 * band, full = tiles_y / cyc, rem = tiles_y - full * cyc;
+    const int c = (row / band) % 8;
+    int before = 0;                                      // rows of the classes below c
+    for (int q = 0; q < c; ++q) before += full * band + min(max(rem - q * band, 0), band);
+    const int prow = before + (row / cyc) * band + row % band;   // the row's place in class order
+    const long long rank = ((long long)prow * frames + f) * tiles_x + col;
+    key[i] = (unsigned)(rank / (n / 8));
+    val[i] = t;
+}
+
+// sorted: the tiles grouped by eighth (stable: most expensive first within
+// each); position r * 8 + c takes eighth c's r-th tile.
+__global__ __launch_bounds__(256) void xcd_place(const int* __restrict__ sorted, int n, int* __restrict__ order) {
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= n) return;
+    const int m = n / 8, c = j / m, r = j - c * m;
+    order[r * 8 + c] = sorted[j];
+}
+
 }  // namespace
 
 size_t learn_scratch_bytes(int n) { return layout(n).total; }
@@ -166,6 +203,18 @@ hipError_t learn_on_device(const LearnParams& lp, const unsigned long long* rec,
     size_t tb = L.temp_bytes;
     e = rocprim::radix_sort_pairs_desc(base + L.temp, tb, key_in, key_out, val_in, d_order, lp.n, 0, 32, s);
     if (e != hipSuccess) return e;
+    if (lp.xcd > 0 && lp.n % 8 == 0 && lp.tiles_x > 0 && lp.tiles_y > 0 && lp.frames > 0 &&
+        (long long)lp.tiles_x * lp.tiles_y * lp.frames == lp.n) {
+        int* sorted = reinterpret_cast<int*>(base + L.cand);            // free until learn_cand
+        hipLaunchKernelGGL(xcd_keys, dim3(g), dim3(256), 0, s, d_order, lp.n, lp.tiles_x, lp.tiles_y, lp.frames,
+                           lp.xcd, key_in, val_in);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+        tb = L.temp_bytes;
+        e = rocprim::radix_sort_pairs(base + L.temp, tb, key_in, key_out, val_in, sorted, lp.n, 0, 3, s);
+        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL(xcd_place, dim3(g), dim3(256), 0, s, sorted, lp.n, d_order);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+    }
     const size_t nl = (size_t)lp.n * 64;
     unsigned long long* cand_out = reinterpret_cast<unsigned long long*>(base + L.cand_out);
     hipLaunchKernelGGL(learn_cand, dim3((unsigned)((nl + 255) / 256)), dim3(256), 0, s, lane, nl, hdr,

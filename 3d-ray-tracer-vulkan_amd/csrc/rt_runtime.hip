@@ -319,6 +319,7 @@ struct PerDevice {
     struct LastCam { std::vector<uint8_t> geo; std::vector<uint8_t> cam; };
     std::vector<LastCam> last_cam;
     size_t       learning_n = 0;
+    int          learning_tx = 0, learning_ty = 0, learning_frames = 0;   // its tiles (option xcd_order)
     int          last_heavy = 0;    // heavy tiles of the last launch (option "heavy_tiles_used", read only)
     int          last_heavy_px = 0; // heavy pixels of the last launch (option "heavy_pixels_used", read only)
     // option graph: plain launches captured once per launch key into a HIP
@@ -416,6 +417,8 @@ struct rt_ctx {
                                    //   (the heavy-tile bulk estimate counts this launch's work that many times)
     int  learn_cost = 1;           // heavy_first cost: 0 = lockstep steps + 2 x coop windows, 1 = wave duration
     int  learn_alone = 0;          // heavy_first: a learning launch first waits for the device to drain
+    int  xcd_order = 0;            // device-learned orders: XCD c takes one class of row bands (rt_learn.hip;
+                                   //   the band height in wave-tile rows, 0 = off)
     int  learn_device = 1;         // heavy_first: learn the order on the device (rt_learn.hip; 0 = on the host)
     int  leaf_align = RT_LEAF_ALIGN;   // walk records: no leaf straddles a 128-B line (a pad slot before it)
     int  accel_half = RT_ACCEL_HALF;   // at the next upload: accel records in format 1 (accel_build.h)
@@ -495,7 +498,8 @@ static int plan_order(const rt_ctx* ctx, PerDevice& p, TraceArgs& a, const rt_ca
                             a.band_off, a.wave_tile, a.ext, a.coop_lanes, a.walk, ctx->learn_cost, ctx->order_split,
                             ctx->heavy_factor, concurrency(ctx), ctx->heavy_cap, ctx->heavy_pixel_factor,
                             a.n_frames, bands ? (int)bands->size() : -1, a.list_stride, ctx->order_frames,
-                            ctx->heavy_stream, ctx->heavy_pixels, ctx->heavy_tiles, ctx->learn_device};
+                            ctx->heavy_stream, ctx->heavy_pixels, ctx->heavy_tiles, ctx->learn_device,
+                            ctx->xcd_order};
     if (bands) geo.insert(geo.end(), bands->begin(), bands->end());
     const size_t g = geo.size() * sizeof(int), c = (size_t)a.n_frames * sizeof(rt_camera_ubo);
     std::vector<uint8_t> key(g + c + sizeof(uint64_t));
@@ -634,6 +638,9 @@ static int plan_order(const rt_ctx* ctx, PerDevice& p, TraceArgs& a, const rt_ca
     }
     p.learning_key = key;
     p.learning_n = n;
+    p.learning_tx = (a.tw + tw_w - 1) / tw_w;
+    p.learning_ty = (a.th + th_w - 1) / th_w;
+    p.learning_frames = a.n_frames;
     p.learning_device = device;
     p.learning_rec_off = 0;
     // Option learn_alone: the learning launch waits for the device to drain,
@@ -699,6 +706,10 @@ static int learn_order_device(const rt_ctx* ctx, PerDevice& p, hipStream_t s) {
     // the host path's bar: heavy_pixel_factor% x (total steps x concurrent / resident waves)
     lp.bar_scale = ctx->heavy_pixel_factor / 100.0 * (double)conc / (double)std::max(1, p.n_cu * kResidentPerCu);
     lp.cap = cap;
+    lp.xcd = ctx->xcd_order;
+    lp.tiles_x = p.learning_tx;
+    lp.tiles_y = p.learning_ty;
+    lp.frames = p.learning_frames;
     hipError_t e = learn_on_device(lp, p.d_learn, p.d_learn_lane, p.d_learn_scratch, o.d_order, o.d_mask, o.d_hpix,
                                    o.d_nhpix, s);
     if (e == hipSuccess) e = hipMemcpyAsync(p.h_nhpix, o.d_nhpix, sizeof(int), hipMemcpyDeviceToHost, s);
@@ -1093,6 +1104,7 @@ int rt_create(const int* device_ids, int n_devices, rt_ctx** out) {
     if (const char* v = std::getenv("RTAMD_ACCEL_HALF")) ctx->accel_half = std::atoi(v) ? 1 : 0;
     if (const char* v = std::getenv("RTAMD_ACCEL_WIDE")) ctx->accel_wide = std::atoi(v) ? 1 : 0;
     if (const char* v = std::getenv("RTAMD_HEAVY_FIRST")) ctx->heavy_first = std::atoi(v) ? 1 : 0;
+    if (const char* v = std::getenv("RTAMD_XCD_ORDER")) ctx->xcd_order = std::max(0, std::min(4096, std::atoi(v)));
     if (const char* v = std::getenv("RTAMD_HEAVY_TILES")) ctx->heavy_tiles = std::max(-1, std::atoi(v));
     if (const char* v = std::getenv("RTAMD_LEARN_COST")) ctx->learn_cost = std::atoi(v) ? 1 : 0;
     if (const char* v = std::getenv("RTAMD_ORDER_SPLIT")) ctx->order_split = std::max(0, std::min(100, std::atoi(v)));
@@ -2120,6 +2132,8 @@ int rt_set_option(rt_ctx* ctx, const char* name, int64_t value) {
         ctx->order_split = (int)value;
     } else if (std::strcmp(name, "learn_alone") == 0 && (value == 0 || value == 1)) {
         ctx->learn_alone = (int)value;
+    } else if (std::strcmp(name, "xcd_order") == 0 && value >= 0 && value <= 4096) {
+        ctx->xcd_order = (int)value;
     } else if (std::strcmp(name, "learn_device") == 0 && (value == 0 || value == 1)) {
         ctx->learn_device = (int)value;
     } else if (std::strcmp(name, "leaf_align") == 0 && value >= 0 && value <= 2) {
@@ -2167,6 +2181,7 @@ int rt_get_option(rt_ctx* ctx, const char* name, int64_t* value) {
     else if (std::strcmp(name, "learn_cost") == 0) *value = ctx->learn_cost;
     else if (std::strcmp(name, "order_split") == 0) *value = ctx->order_split;
     else if (std::strcmp(name, "learn_alone") == 0) *value = ctx->learn_alone;
+    else if (std::strcmp(name, "xcd_order") == 0) *value = ctx->xcd_order;
     else if (std::strcmp(name, "learn_device") == 0) *value = ctx->learn_device;
     else if (std::strcmp(name, "leaf_align") == 0) *value = ctx->leaf_align;
     else if (std::strcmp(name, "accel") == 0) *value = ctx->accel;

@@ -405,6 +405,14 @@ int rt_render_poll(rt_ctx* ctx, uint64_t ticket, int* done);
  *   "learn_alone"   heavy_first: 1 = a learning launch first waits for the
  *                   device to drain (its wave durations then are not inflated
  *                   by other launches in flight); 0 (default) = it does not
+ *   "xcd_order"     heavy_first, orders learned on the device: 0 (default) =
+ *                   the cost order as is; r in 1..4096 = workgroup k, which
+ *                   the hardware deals to XCD k % 8, takes from one eighth of
+ *                   the tiles: rows of wave tiles in bands of r, every 8th
+ *                   band to one eighth (r >= the tile rows: 8 contiguous
+ *                   slabs), most expensive first within it, so each XCD's
+ *                   L2 serves rays from fewer parts of the scene.  Same
+ *                   results.
  *   "order_split"   heavy_first: 0 = every tile in cost order; p in 1..100 =
  *                   only the tiles costing at least p percent of the
  *                   costliest go first (in cost order), the rest keep their

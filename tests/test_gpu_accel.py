@@ -114,6 +114,29 @@ def _tie_scenes():
     return M._tie_scenes()
 
 
+@pytest.mark.parametrize("band", [2, 1000])
+def test_accel_xcd_order(acc, band):
+    """Option xcd_order (rt_learn.hip xcd_keys / xcd_place): the device-learned
+    order regrouped so that XCD c's workgroups take one class of row bands;
+    every tile still traced once, so frames and counters are unchanged
+    (config 3, 120 x 270 wave tiles, a multiple of 8)."""
+    from rtamd import configs
+    cfg = configs.config3()
+    built = cfg.build()
+    cam = cfg.camera()
+    _upload(acc, built, 8)
+    ref = _oracle(built, cam, cfg.width, cfg.height, 4)
+    model = _model(built, cam, cfg.width, cfg.height, 4, 8)
+    acc.set_option("xcd_order", band)
+    try:
+        assert acc.get_option("xcd_order") == band
+        for stats in (False, False, True, False):    # learning, then launches in the regrouped order
+            rgba, rad, st = acc.render(cam, cfg.width, cfg.height, 4, radiance=True, stats=stats)
+            _check(rgba, rad, st, ref, model, f"xcd_order {band}")
+    finally:
+        acc.set_option("xcd_order", 0)
+
+
 def _adversarial():
     import os
     import sys
