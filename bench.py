@@ -1280,7 +1280,8 @@ def main() -> None:
             "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 4),
             "higher_is_better": True,
-            "scaling": "weak" if weak else "strong",
+            # the series this run belongs to (at N = 1 weak and strong are the same work)
+            "scaling": args.scaling,
             "vs_baseline": None,
             "dtype": "f32",
             "data": f"{'reference asset' if args.config == 6 else 'synthetic'} "
