@@ -82,6 +82,8 @@ struct DevScene {
     int      half = 0;          // accel format 1: 16-B slots, half-precision internal boxes (accel_build.h);
                                 //   layout_slots and end2 then count 16-B slots
     float    relax_half = 0.0f;  // format 1: every internal node's margin factor (AccelHost::relax_max)
+    int      root_enter = 0;     // format 0: the walk starts inside the root (its slab test skipped)
+    int      root_first_leaf = 0;   // bit o: layout o's root's first child is a leaf
     float4*  walk_ref = nullptr;
     int      end2_ref = 0;
     int      ref_padded = 0;

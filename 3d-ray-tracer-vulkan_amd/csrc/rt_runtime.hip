@@ -1359,6 +1359,11 @@ int rt_upload_scene(rt_ctx* ctx, const void* vertices, size_t vertex_bytes,
             s.half = ah.format == 1 ? 1 : 0;
             s.wide = ah.format == 2 ? 1 : 0;
             s.relax_half = ah.relax_max;
+            s.root_enter = ah.format == 0 && !ah.root_leaf && ah.slots > 1 ? 1 : 0;
+            s.root_first_leaf = 0;
+            if (s.root_enter)
+                for (int o = 0; o < ah.n_layouts; ++o)
+                    s.root_first_leaf |= (int)(ah.rec[8 * (size_t)o * (size_t)ah.slots + 7] >> 31) << o;
             s.end = ah.slots;
             s.end2 = ah.n_layouts * ah.slots;
             s.root_leaf = ah.root_leaf;

@@ -1044,6 +1044,11 @@ __device__ __forceinline__ void heavy_pixel(const TraceArgs& a, int f, int lx, i
 #ifndef RT_ACC_LAZY
 #define RT_ACC_LAZY 0
 #endif
+// 1 = option accel's format-0 walk starts inside the root (DevScene::root_enter;
+// A/B builds: 0 = the root's slab test first, as the model's orc_accel_root(0))
+#ifndef RT_ROOT_ENTER
+#define RT_ROOT_ENTER 1
+#endif
 template <bool COUNT, bool DIAG = false, int FEAT = 0, int WALK = 2>
 __global__ __launch_bounds__(256)
 __attribute__((amdgpu_waves_per_eu((FEAT & kFeatFrontier) ? 1 : (FEAT & kFeatAccel) ? RT_ACCEL_WPE : RT_SIMPLE_WPE)))
@@ -1229,13 +1234,25 @@ void trace_simple(TraceArgs a) {
         int n = 0;
         int lend = wend;                  // accel: the end of this ray's layout
         bool incons = false;              // accel: the hit lies before its own box's t_enter
+        int oct = 0;                      // accel: the layout this ray walks
         if (ACC && a.scene.n_layouts == 8) {
-            n = ((__float_as_uint(d.x) >> 31) | ((__float_as_uint(d.y) >> 31) << 1) |
-                 ((__float_as_uint(d.z) >> 31) << 2)) * a.scene.layout_slots;
+            oct = (int)((__float_as_uint(d.x) >> 31) | ((__float_as_uint(d.y) >> 31) << 1) |
+                        ((__float_as_uint(d.z) >> 31) << 2));
+            n = oct * a.scene.layout_slots;
             lend = n + a.scene.layout_slots;
         }
         bool nleaf = a.scene.root_leaf != 0;
         bool walking = alive && end > 0;
+        // Format 0 (round 6): the walk starts inside the root.  Entering an
+        // internal box whose slab test would fail only tests its children,
+        // which fail it too (their boxes lie inside), so results are the
+        // same, and every segment saves the root's step; the root's two
+        // children count as visited, as when the root is entered.
+        if (ACC && !HALF && !WIDE && RT_ROOT_ENTER && a.scene.root_enter) {
+            n += 1;
+            nleaf = ((a.scene.root_first_leaf >> oct) & 1) != 0;
+            if (COUNT && alive) c_node += 2;
+        }
         // the wide walk (kFeatWide): the record to read next (a child link:
         // index | flags), the lane's stack depth, and an overflowed stack
         uint32_t wcur = a.scene.root_leaf ? kWLeaf : 0u;

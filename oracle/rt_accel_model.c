@@ -26,6 +26,9 @@
  * accel_half): 16-B slots, an internal node one slot with its box in IEEE half
  * precision (decoded exactly, as the kernel's v_cvt_f32_f16), a leaf four.
  *
+ * Format 0's walk starts inside the root (round 6; orc_accel_root): the root's
+ * box is not tested, the root counts as visited and its children are walked.
+ *
  * Thin triangles (round 6, accel_build.h accel_class / kAccelForce): a record
  * whose bit 29 of word 3 is set (its subtree holds a triangle of shape class
  * >= 7) is entered whenever its slab test passes (R = infinity); format 1's
@@ -44,6 +47,14 @@ static uint64_t g_leaf_visits = 0;     /* analysis: leaf slots walked (the rest 
  * RELAX_ABS (accel_build.h).  orc_accel_margin changes them for studies. */
 static float g_relax = 1.0f + 1.0f / 1024.0f, g_relax_abs = 1.0f / 1024.0f;
 static float g_relax_half = 1.0f + 1.0f / 1024.0f;
+static int g_root_enter = 1;           /* format 0: the walk starts inside the root */
+
+/* Format 0's root entry (1, the kernel's default: its slab test skipped; 0:
+ * tested first, as an RT_ROOT_ENTER=0 build). */
+int orc_accel_root(int on) {
+    g_root_enter = on != 0;
+    return 0;
+}
 
 int orc_accel_margin(float rel, float abs_) {
     g_relax = rel;
@@ -488,6 +499,13 @@ static int accel_walk(const scene* s, ray r, float* closest_t, int* hit_index, v
     int hit = -1;
     uint64_t leaf_visits = 0;
     const size_t WS = g_fmt ? 4 : 8;
+    if (g_root_enter && !g_fmt && !leaf && g_slots > 1) {
+        /* format 0: the walk starts inside the root (rt_trace.hip RT_ROOT_ENTER):
+         * its box is not tested; it counts as visited and entered */
+        cnt->node_visits++;
+        leaf = (int)(g_rec[8 * n + 7] >> 31);
+        n += 1;
+    }
     while (n < end) {
         const uint32_t aw = g_rec[WS * n + 3], bw = g_fmt ? 0u : g_rec[8 * n + 7];
         cnt->node_visits++;
