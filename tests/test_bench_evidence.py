@@ -316,9 +316,10 @@ R06 = os.path.join(ROOT, "profiles", "r06")
 # the final tree's lines (r6m: bench at 20 and 200 steps, the profiled runs,
 # configs 4-6, launches in flight, orbit), every one on the PMC records of the
 # same session
-R06_LINES = [("r6m", f) for f in ("bench.json", "bench200.json", "prof3.json", "prof5.json", "bench_cfg4.json",
-                                   "bench_cfg5.json", "bench_cfg6.json", "bench_if1.json", "bench_if2.json",
-                                   "bench_if4.json", "bench_orbit.json")]
+R06_LINES = [(ses, f) for ses in ("r6m", "r6t")
+             for f in ("bench.json", "bench200.json", "prof3.json", "prof5.json", "bench_cfg4.json",
+                       "bench_cfg5.json", "bench_cfg6.json", "bench_if1.json", "bench_if2.json",
+                       "bench_if4.json", "bench_orbit.json")]
 
 
 def _line6(path):
@@ -343,28 +344,31 @@ def test_r06_roofline_reproduces(session, name):
         assert src.startswith(f"profiles/r06/{session}/pmc"), src
 
 
+@pytest.mark.parametrize("session", ["r6m", "r6t"])
 @pytest.mark.parametrize("cfg", [3, 5])
-def test_r06_rocprof_union(cfg):
+def test_r06_rocprof_union(session, cfg):
     global R05
     saved = R05
     try:
         R05 = R06
-        test_r05_rocprof_union("r6m", cfg)
+        test_r05_rocprof_union(session, cfg)
     finally:
         R05 = saved
 
 
-def test_r06_final_tree():
-    """The final tree's session (r6m): every GPU test green, smoke, frames
-    verified, frac within 5% at 2 and 4 launches in flight, and config 3
-    faster per frame than round 5's final build on its box (r5au: 0.1239 ms
-    at 20 steps, 0.1198 at 200; boxes differ by a few percent)."""
-    with open(os.path.join(R06, "r6m", "pytest_gpu.log")) as fh:
+@pytest.mark.parametrize("session", ["r6m", "r6t"])
+def test_r06_final_tree(session):
+    """The final tree's sessions (r6t; r6m: the build before the walk started
+    inside the root): every GPU test green, smoke, frames verified, frac
+    within 5% at 2 and 4 launches in flight, and config 3 faster per frame
+    than round 5's final build on its box (r5au: 0.1239 ms at 20 steps,
+    0.1198 at 200; boxes differ by a few percent)."""
+    with open(os.path.join(R06, session, "pytest_gpu.log")) as fh:
         tail = fh.read().strip().splitlines()[-1]
     assert " passed" in tail and "failed" not in tail and "error" not in tail, tail
-    fr = {k: _line6(os.path.join(R06, "r6m", f"bench_if{k}.json"))["roofline"]["frac"] for k in (2, 4)}
+    fr = {k: _line6(os.path.join(R06, session, f"bench_if{k}.json"))["roofline"]["frac"] for k in (2, 4)}
     assert max(fr.values()) <= 1.05 * min(fr.values()), fr
-    b20, b200 = (_line6(os.path.join(R06, "r6m", f)) for f in ("bench.json", "bench200.json"))
+    b20, b200 = (_line6(os.path.join(R06, session, f)) for f in ("bench.json", "bench200.json"))
     assert b20["config"]["frames_verified"] and b200["config"]["frames_verified"]
     assert b20["cpu_baseline"]["gpu_rows_match"] is True
     assert b200["ms_per_step"] < 0.1198 * 1.02 and b20["ms_per_step"] < 0.1239 * 1.02
