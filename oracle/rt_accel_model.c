@@ -52,7 +52,7 @@ static int g_root_enter = 1;           /* format 0: the walk starts inside the r
 /* Format 0's root entry (1, the kernel's default: its slab test skipped; 0:
  * tested first, as an RT_ROOT_ENTER=0 build). */
 int orc_accel_root(int on) {
-    g_root_enter = on != 0;
+    g_root_enter = on < 0 ? 0 : on;
     return 0;
 }
 
@@ -499,9 +499,10 @@ static int accel_walk(const scene* s, ray r, float* closest_t, int* hit_index, v
     int hit = -1;
     uint64_t leaf_visits = 0;
     const size_t WS = g_fmt ? 4 : 8;
-    if (g_root_enter && !g_fmt && !leaf && g_slots > 1) {
+    for (int k = 0; k < g_root_enter && !g_fmt && !leaf && g_slots > 1; ++k) {
         /* format 0: the walk starts inside the root (rt_trace.hip RT_ROOT_ENTER):
-         * its box is not tested; it counts as visited and entered */
+         * its box is not tested; it counts as visited and entered (a study:
+         * g_root_enter > 1 enters the first child the same way, and so on) */
         cnt->node_visits++;
         leaf = (int)(g_rec[8 * n + 7] >> 31);
         n += 1;
