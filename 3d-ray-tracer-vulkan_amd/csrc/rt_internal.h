@@ -84,6 +84,7 @@ struct DevScene {
     float    relax_half = 0.0f;  // format 1: every internal node's margin factor (AccelHost::relax_max)
     int      root_enter = 0;     // format 0: the walk starts inside the root (its slab test skipped)
     int      root_first_leaf = 0;   // bit o: layout o's root's first child is a leaf
+    int      oct_mask = 7;       // 8 layouts: a ray walks layout (its octant & oct_mask) (option accel_octants)
     float4*  walk_ref = nullptr;
     int      end2_ref = 0;
     int      ref_padded = 0;

@@ -417,6 +417,7 @@ struct rt_ctx {
                                    //   (the heavy-tile bulk estimate counts this launch's work that many times)
     int  learn_cost = 1;           // heavy_first cost: 0 = lockstep steps + 2 x coop windows, 1 = wave duration
     int  learn_alone = 0;          // heavy_first: a learning launch first waits for the device to drain
+    int  accel_octants = 7;        // option accel (8 layouts): the octant bits a ray's layout keeps
     int  xcd_order = 0;            // device-learned orders: XCD c takes one class of row bands (rt_learn.hip;
                                    //   the band height in wave-tile rows, 0 = off)
     int  learn_device = 1;         // heavy_first: learn the order on the device (rt_learn.hip; 0 = on the host)
@@ -499,7 +500,7 @@ static int plan_order(const rt_ctx* ctx, PerDevice& p, TraceArgs& a, const rt_ca
                             ctx->heavy_factor, concurrency(ctx), ctx->heavy_cap, ctx->heavy_pixel_factor,
                             a.n_frames, bands ? (int)bands->size() : -1, a.list_stride, ctx->order_frames,
                             ctx->heavy_stream, ctx->heavy_pixels, ctx->heavy_tiles, ctx->learn_device,
-                            ctx->xcd_order};
+                            ctx->xcd_order, ctx->accel_octants};
     if (bands) geo.insert(geo.end(), bands->begin(), bands->end());
     const size_t g = geo.size() * sizeof(int), c = (size_t)a.n_frames * sizeof(rt_camera_ubo);
     std::vector<uint8_t> key(g + c + sizeof(uint64_t));
@@ -873,6 +874,7 @@ static int set_schedule(const rt_ctx* ctx, PerDevice& p, TraceArgs& a, const rt_
     a.ext = ctx->ext;
     a.scene.spheres = p.d_spheres;
     a.scene.n_spheres = (a.ext & kExtSpheres) ? p.n_spheres : 0;
+    a.scene.oct_mask = ctx->accel_octants;
     a.sky_enabled = cam->sky_enabled;
     a.frame_count = cam->frame_count;
     a.accum = nullptr;
@@ -1105,6 +1107,7 @@ int rt_create(const int* device_ids, int n_devices, rt_ctx** out) {
     if (const char* v = std::getenv("RTAMD_ACCEL_WIDE")) ctx->accel_wide = std::atoi(v) ? 1 : 0;
     if (const char* v = std::getenv("RTAMD_HEAVY_FIRST")) ctx->heavy_first = std::atoi(v) ? 1 : 0;
     if (const char* v = std::getenv("RTAMD_XCD_ORDER")) ctx->xcd_order = std::max(0, std::min(4096, std::atoi(v)));
+    if (const char* v = std::getenv("RTAMD_ACCEL_OCTANTS")) ctx->accel_octants = std::atoi(v) & 7;
     if (const char* v = std::getenv("RTAMD_HEAVY_TILES")) ctx->heavy_tiles = std::max(-1, std::atoi(v));
     if (const char* v = std::getenv("RTAMD_LEARN_COST")) ctx->learn_cost = std::atoi(v) ? 1 : 0;
     if (const char* v = std::getenv("RTAMD_ORDER_SPLIT")) ctx->order_split = std::max(0, std::min(100, std::atoi(v)));
@@ -2139,6 +2142,8 @@ int rt_set_option(rt_ctx* ctx, const char* name, int64_t value) {
         ctx->learn_alone = (int)value;
     } else if (std::strcmp(name, "xcd_order") == 0 && value >= 0 && value <= 4096) {
         ctx->xcd_order = (int)value;
+    } else if (std::strcmp(name, "accel_octants") == 0 && value >= 0 && value <= 7) {
+        ctx->accel_octants = (int)value;
     } else if (std::strcmp(name, "learn_device") == 0 && (value == 0 || value == 1)) {
         ctx->learn_device = (int)value;
     } else if (std::strcmp(name, "leaf_align") == 0 && value >= 0 && value <= 2) {
@@ -2187,6 +2192,7 @@ int rt_get_option(rt_ctx* ctx, const char* name, int64_t* value) {
     else if (std::strcmp(name, "order_split") == 0) *value = ctx->order_split;
     else if (std::strcmp(name, "learn_alone") == 0) *value = ctx->learn_alone;
     else if (std::strcmp(name, "xcd_order") == 0) *value = ctx->xcd_order;
+    else if (std::strcmp(name, "accel_octants") == 0) *value = ctx->accel_octants;
     else if (std::strcmp(name, "learn_device") == 0) *value = ctx->learn_device;
     else if (std::strcmp(name, "leaf_align") == 0) *value = ctx->leaf_align;
     else if (std::strcmp(name, "accel") == 0) *value = ctx->accel;

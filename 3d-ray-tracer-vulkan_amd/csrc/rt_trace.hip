@@ -1237,7 +1237,7 @@ void trace_simple(TraceArgs a) {
         int oct = 0;                      // accel: the layout this ray walks
         if (ACC && a.scene.n_layouts == 8) {
             oct = (int)((__float_as_uint(d.x) >> 31) | ((__float_as_uint(d.y) >> 31) << 1) |
-                        ((__float_as_uint(d.z) >> 31) << 2));
+                        ((__float_as_uint(d.z) >> 31) << 2)) & a.scene.oct_mask;
             n = oct * a.scene.layout_slots;
             lend = n + a.scene.layout_slots;
         }

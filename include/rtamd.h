@@ -405,6 +405,11 @@ int rt_render_poll(rt_ctx* ctx, uint64_t ticket, int* done);
  *   "learn_alone"   heavy_first: 1 = a learning launch first waits for the
  *                   device to drain (its wave durations then are not inflated
  *                   by other launches in flight); 0 (default) = it does not
+ *   "accel_octants" option accel with 8 layouts: the octant bits (x 1, y 2,
+ *                   z 4) that choose a ray's layout; 7 (default) = all three
+ *                   (every ray walks near child first on every axis); fewer
+ *                   bits touch fewer layouts (half the records with two bits)
+ *                   at a worse order on the dropped axes.  Same results.
  *   "xcd_order"     heavy_first, orders learned on the device: 0 (default) =
  *                   the cost order as is; r in 1..4096 = workgroup k, which
  *                   the hardware deals to XCD k % 8, takes from one eighth of

@@ -48,6 +48,12 @@ static uint64_t g_leaf_visits = 0;     /* analysis: leaf slots walked (the rest 
 static float g_relax = 1.0f + 1.0f / 1024.0f, g_relax_abs = 1.0f / 1024.0f;
 static float g_relax_half = 1.0f + 1.0f / 1024.0f;
 static int g_root_enter = 1;           /* format 0: the walk starts inside the root */
+static int g_oct_mask = 7;             /* a study: rays walk layout (octant & mask) */
+
+int orc_accel_octants(int mask) {
+    g_oct_mask = mask & 7;
+    return 0;
+}
 
 /* Format 0's root entry (1, the kernel's default: its slab test skipped; 0:
  * tested first, as an RT_ROOT_ENTER=0 build). */
@@ -489,7 +495,7 @@ static int accel_walk(const scene* s, ray r, float* closest_t, int* hit_index, v
     if (g_fmt == 2) return wide_walk(s, r, closest_t, hit_index, hit_normal, cnt);
     if (g_audit) audit_segment(s, r);
     const int oct = g_layouts == 8 ? ((signbit(r.dir.x) ? 1 : 0) | (signbit(r.dir.y) ? 2 : 0) |
-                                      (signbit(r.dir.z) ? 4 : 0)) : 0;
+                                      (signbit(r.dir.z) ? 4 : 0)) & g_oct_mask : 0;
     size_t n = (size_t)oct * (size_t)g_slots;
     const size_t end = n + (size_t)g_slots;
     int leaf = g_root_leaf;

@@ -137,6 +137,35 @@ def test_accel_xcd_order(acc, band):
         acc.set_option("xcd_order", 0)
 
 
+@pytest.mark.parametrize("mask", [5, 0])
+def test_accel_octants(acc, mask):
+    """Option accel_octants: rays walk layout (octant & mask) of the 8 (fewer
+    layouts touched, a worse child order on the dropped axes); frames equal
+    the oracle's, counters the model's with the same mask
+    (orc_accel_octants)."""
+    from oracle import oracle_lib
+    from rtamd import configs
+    cfg = configs.config3()
+    built = cfg.build()
+    cam = cfg.camera()
+    _upload(acc, built, 8)
+    ref = _oracle(built, cam, cfg.width, cfg.height, 4)
+    L = oracle_lib.lib(accel=True)
+    L.orc_accel_octants(mask)
+    try:
+        model = _model(built, cam, cfg.width, cfg.height, 4, 8)
+    finally:
+        L.orc_accel_octants(7)
+    acc.set_option("accel_octants", mask)
+    try:
+        assert acc.get_option("accel_octants") == mask
+        for stats in (False, True, False):
+            rgba, rad, st = acc.render(cam, cfg.width, cfg.height, 4, radiance=True, stats=stats)
+            _check(rgba, rad, st, ref, model, f"accel_octants {mask}")
+    finally:
+        acc.set_option("accel_octants", 7)
+
+
 def _adversarial():
     import os
     import sys
