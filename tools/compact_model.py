@@ -9,7 +9,9 @@ active wave of the group lives as long as the group's slowest wave).
 Usage: compact_model.py CONFIG [G]   
 """
 import sys, numpy as np
-sys.path[:0]=['3d-ray-tracer-vulkan_amd','.']
+import os
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(ROOT, '3d-ray-tracer-vulkan_amd'), ROOT]
 from rtamd import configs, _lib
 from oracle import oracle_lib as O
 k=int(sys.argv[1]); G=int(sys.argv[2]) if len(sys.argv)>2 else 4

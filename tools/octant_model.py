@@ -5,7 +5,9 @@ root_depth_model.py.
 Usage: octant_model.py CONFIG
 """
 import sys, numpy as np
-sys.path[:0]=['3d-ray-tracer-vulkan_amd','.']
+import os
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(ROOT, '3d-ray-tracer-vulkan_amd'), ROOT]
 from rtamd import configs, _lib
 from oracle import oracle_lib as O
 k=int(sys.argv[1])

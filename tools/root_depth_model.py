@@ -7,7 +7,9 @@ rows 1000-1539 (its top rows are sky).
 Usage: root_depth_model.py CONFIG
 """
 import sys, numpy as np, ctypes as C
-sys.path[:0]=['3d-ray-tracer-vulkan_amd','.']
+import os
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(ROOT, '3d-ray-tracer-vulkan_amd'), ROOT]
 from rtamd import configs, _lib
 from oracle import oracle_lib as O
 k=int(sys.argv[1])
