@@ -172,6 +172,44 @@ def test_model_matches_oracle(k, b, tile, row_step, nl, half):
         assert acc[2]["node_visits"] < 0.4 * ref[2]["node_visits"]
 
 
+def random_scene(seed):
+    """A random triangle soup: well-shaped triangles, needles (one edge 1e-4 -
+    1e-2 of the other) and tiny ones, in a box of random size and offset, every
+    material type."""
+    rng = np.random.default_rng(seed)
+    n = int(rng.integers(20, 600))
+    scale = float(10.0 ** rng.uniform(-1, 2))
+    off = rng.uniform(-1, 1, 3) * float(10.0 ** rng.uniform(0, 3))
+    c = rng.uniform(-1, 1, (n, 3)) * scale + off
+    e1 = rng.normal(size=(n, 3)) * scale * 0.4
+    e2 = rng.normal(size=(n, 3)) * scale * 0.4
+    kind = rng.integers(0, 3, n)
+    needle = kind == 1
+    e2[needle] = e1[needle] * (1.0 + rng.uniform(-1, 1, (int(needle.sum()), 1)) * 1e-3) + \
+        rng.normal(size=(int(needle.sum()), 3)) * scale * 10.0 ** rng.uniform(-6, -3, (int(needle.sum()), 1))
+    tiny = kind == 2
+    e1[tiny] *= 1e-3
+    e2[tiny] *= 1e-3
+    verts = np.stack([c, c + e1, c + e2], 1).astype(np.float32)
+    mats = np.concatenate([rng.uniform(0.1, 0.95, (n, 3)), rng.integers(0, 3, (n, 1))], 1).astype(np.float32)
+    eye = off + rng.uniform(-1, 1, 3) * scale * 3.0
+    return verts, mats, (tuple(eye.tolist()), tuple(off.tolist())), float(rng.uniform(20, 90))
+
+
+@pytest.mark.parametrize("nl", [1, 8])
+def test_model_random_scenes(nl):
+    """random_scene's 24 soups (tests/test_gpu_accel.py runs them on the GPU):
+    the model's frames equal the oracle's."""
+    from rtamd import build_buffers, configs
+    for seed in range(24):
+        verts, mats, (eye, at), vfov = random_scene(seed)
+        w, h, b = 64, 48, 3
+        cam = configs.Camera(eye, at, (0.0, 1.0, 0.0), vfov, w / h)
+        built = build_buffers(verts, mats, 1 + seed % 3)
+        ref, acc = _frames(built, cam, w, h, b, nl)
+        _assert_frames_equal(ref, acc, f"random scene {seed}")
+
+
 def _tie_scenes():
     from rtamd import build_buffers, configs, triangles_of
     verts, mats = triangles_of(configs.config2().scene)

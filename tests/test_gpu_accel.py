@@ -166,6 +166,24 @@ def test_accel_octants(acc, mask):
         acc.set_option("accel_octants", 7)
 
 
+@pytest.mark.parametrize("nl", [1, 8])
+def test_accel_random_scenes(acc, nl):
+    """Random triangle soups (sizes, offsets, needles, tiny triangles), 24
+    scenes: frames equal the oracle's, counters the accel model's."""
+    import test_accel_model as M
+    from rtamd import build_buffers, configs
+    for seed in range(24):
+        verts, mats, (eye, at), vfov = M.random_scene(seed)
+        w, h, b = 64, 48, 3
+        cam = configs.Camera(eye, at, (0.0, 1.0, 0.0), vfov, w / h)
+        built = build_buffers(verts, mats, 1 + seed % 3)
+        _upload(acc, built, nl)
+        ref = _oracle(built, cam, w, h, b)
+        model = _model(built, cam, w, h, b, nl)
+        rgba, rad, st = acc.render(cam, w, h, b, radiance=True, stats=True)
+        _check(rgba, rad, st, ref, model, f"random scene {seed} layouts {nl}")
+
+
 def _adversarial():
     import os
     import sys
