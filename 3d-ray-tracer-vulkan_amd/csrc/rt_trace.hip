@@ -1044,6 +1044,13 @@ __device__ __forceinline__ void heavy_pixel(const TraceArgs& a, int f, int lx, i
 #ifndef RT_ACC_LAZY
 #define RT_ACC_LAZY 0
 #endif
+// s_setprio level of a wave while it walks: the walk's dependent chain
+// (record, slab test, next address, next load) issues ahead of the waves that
+// shade, whose VALU work is not on any load's path.  1, 2 and 3 measured alike,
+// 1.0-1.5% per frame on configs 3 and 5 against 0 (profiles/r06/r6ab, r6ac).
+#ifndef RT_WALK_PRIO
+#define RT_WALK_PRIO 2
+#endif
 // 1 = option accel's format-0 walk starts inside the root (DevScene::root_enter;
 // A/B builds: 0 = the root's slab test first, as the model's orc_accel_root(0))
 #ifndef RT_ROOT_ENTER
@@ -1298,6 +1305,8 @@ void trace_simple(TraceArgs a) {
                 }
             }
             float lim = accel_lim(closest);                          // ACC: closest_t's entry bound
+            // the walk's dependent chain issues ahead of waves shading (RT_WALK_PRIO)
+            if (RT_WALK_PRIO) __builtin_amdgcn_s_setprio(RT_WALK_PRIO);
             // Option accel's format-0 walk tracks its record as a byte offset
             // (slot << 5; the records stay below 2^27 slots, so it and the
             // layout's end fit 32 bits): the next record's address is one
@@ -1477,6 +1486,7 @@ void trace_simple(TraceArgs a) {
                 if ((FEAT & kFeatCoopTail) && __popcll(__ballot(walking)) <= coop_lanes) break;
             }
             if (BYTES) n = (int)(nb >> 5);
+            if (RT_WALK_PRIO) __builtin_amdgcn_s_setprio(0);
         }
         if (FEAT & kFeatCoopTail) {
             // Every lane is here.  Finish the remaining walks one ray at a
