@@ -6,8 +6,8 @@ Workload (N = 1): BASELINE config 3 — the 50k-triangle synthetic scene at
 frame traced on the GPU: every pixel's full path, RGBA8 written to HBM.  The
 render loop keeps D launches in flight (launch j on stream j mod D, each
 stream its own hardware queue), as a renderer does to hide each frame's
-serial tail; a launch traces F frames (rt_render_batch_device; F = 2 at
-N = 1 when the timed frames are whole pairs, default_batch).  The timed region covers exactly K frames, synchronised on both
+serial tail; a launch traces F frames (rt_render_batch_device; F = 4 at
+N = 1 when the timed frames are whole quadruples, default_batch).  The timed region covers exactly K frames, synchronised on both
 sides.
 
 With N > 1 ranks (one process per GPU, torch.distributed over RCCL), every
@@ -140,14 +140,17 @@ def default_inflight(world: int) -> int:
 
 
 def default_batch(world: int, weak: bool = False, steps: int = 0) -> int:
-    """Frames per launch.  N = 1: 2 when the timed frames are whole pairs
-    (steps even, or steps not given), else 1: a launch of two frames runs
-    past the other launches' tails with one learned order for both
-    (A/B on one box, 2 runs each: config 3 0.1190-0.1200 ms per frame
-    against 0.1214-0.1222 with 1, config 5 1.156-1.164 against 1.174,
-    config 6 0.1223-0.1239 against 0.1234-0.1239; profiles/r05/r5ar,
-    profiles/r05/r5as); an odd frame count would end on a 1-frame launch
-    of a new launch key.  N > 1, weak scaling: N (a launch is a step, this
+    """Frames per launch.  N = 1: 4 when the timed frames are whole
+    quadruples (steps a multiple of 4, or steps not given), else 2 for whole
+    pairs, else 1: a launch of several frames runs past the other launches'
+    tails with one learned order for all (round 5, 2 against 1, A/B on one
+    box: config 3 0.1190-0.1200 ms per frame against 0.1214-0.1222, config 5
+    1.156-1.164 against 1.174, config 6 0.1223-0.1239 against 0.1234-0.1239;
+    profiles/r05/r5ar, r5as.  Round 6, 4 against 2 on the final walk: config
+    3 at the driver's 20 steps 0.1172 against 0.1214 ms (4 runs each), at 200
+    steps 0.1141 against 0.1148, config 5 1.127 against 1.143 and 1.127
+    against 1.140; profiles/r06/r6ag, r6af); a frame count that is not a
+    multiple would end on a smaller launch of a new launch key.  N > 1, weak scaling: N (a launch is a step, this
     rank's share of the step's N frames: one frame of work, the shape of an
     N = 1 launch).  N > 1, strong scaling: N / 2 (about half a frame of work
     per launch): a rank's 1/8 share of one frame is too small a launch to
@@ -155,7 +158,7 @@ def default_batch(world: int, weak: bool = False, steps: int = 0) -> int:
     profiles/r03/evidence_r3c/emu.jsonl, 3.9x with 1 frame per launch
     against 6.3-7.7x with 4).  At most 16."""
     if world == 1:
-        return 1 if steps % 2 else 2
+        return 4 if steps % 4 == 0 else (2 if steps % 2 == 0 else 1)
     return max(1, min(16, world if weak else world // 2))
 
 

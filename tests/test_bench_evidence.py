@@ -102,7 +102,8 @@ def test_rocprof_union_agrees_with_ms_per_step(cfg):
 
 def test_default_schedule_helpers():
     assert bench.default_inflight(1) == 4
-    assert bench.default_batch(1) == 2 and bench.default_batch(1, steps=20) == 2
+    assert bench.default_batch(1) == 4 and bench.default_batch(1, steps=20) == 4
+    assert bench.default_batch(1, steps=6) == 2       # whole pairs, not quadruples
     assert bench.default_batch(1, steps=5) == 1       # an odd frame count: no 1-frame launch of a new key
     for n in (2, 4, 8):
         assert bench.default_batch(n, weak=True) == n

@@ -79,13 +79,13 @@ for s in "$@"; do
     bench200) run bench200 600 python bench.py > "$OUT/bench200.json" 2> "$OUT/bench200.err" ;;
     prof3)    prof 3 20 ;;
     prof5)    prof 5 10 ;;
-    # record keys: bench.py pmc_key (the default accel 8 walk: "@accel8"; the N = 1 default of 2 frames per launch: "@f2")
-    pmc3)     pmc 3 cfg3_50k_1920x1080_b4@accel8@f2 ;;
-    pmc5)     pmc 5 cfg5_1M_3840x2160_b8@accel8@f2 ;;
-    pmc6)     pmc 6 cfg6_fbm_1920x1080_b4@accel8@f2 ;;
+    # record keys: bench.py pmc_key (the default accel 8 walk: "@accel8"; the N = 1 default of 4 frames per launch: "@f4")
+    pmc3)     pmc 3 cfg3_50k_1920x1080_b4@accel8@f4 ;;
+    pmc5)     pmc 5 cfg5_1M_3840x2160_b8@accel8@f4 ;;
+    pmc6)     pmc 6 cfg6_fbm_1920x1080_b4@accel8@f4 ;;
     pmc3r)    RTAMD_ACCEL=0 pmc 3 cfg3_50k_1920x1080_b4 r ;;
-    fetch5)   pmc 5 cfg5_1M_3840x2160_b8@nocoop@accel8@f2 n "--set coop_lanes=0" && \
-              pmc 5 cfg5_1M_3840x2160_b8@split40@accel8@f2 s "--set order_split=40" ;;
+    fetch5)   pmc 5 cfg5_1M_3840x2160_b8@nocoop@accel8@f4 n "--set coop_lanes=0" && \
+              pmc 5 cfg5_1M_3840x2160_b8@split40@accel8@f4 s "--set order_split=40" ;;
     pmc3o)    pmc 3 cfg3_50k_1920x1080_b4@orbit@accel8 o "--camera-path orbit --batch 1" ;;
     orbit)    run orbit 600 python bench.py --steps 20 --warmup 5 --camera-path orbit \
                   > "$OUT/bench_orbit.json" 2> "$OUT/bench_orbit.err" ;;
